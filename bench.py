@@ -1,0 +1,369 @@
+"""Hot-path benchmark: trained samples/sec (rollout + update) of the GRPO actor-learner loop.
+
+Workload (BASELINE.json configs[1] shape, the metric's [batch=64, seq=1024, group=8]):
+64 prompts x group 8 = 512 trajectories per rank, response width R = 1024, prompt width
+P = 512, Qwen2.5-1.5B vocabulary V = 151,936, bf16 logits. One step is one pass of the hot
+path over one synthetic batch:
+
+  rollout   R decode steps of skyrl_sample over [512, V] logits (T=1, top_p=1, top_k=-1)
+  pack      skyrl_pack_experience: ragged prompts/responses -> padded training tensors
+  ref/old   skyrl_logprob_fwd over all 512x1024 response positions (2 passes)
+  advantage skyrl_grpo_advantage over [512, 1024]
+  update    per micro-batch (16 seqs): logprob+entropy fwd -> fused PPO+KL loss fwd -> loss bwd
+            -> logprob bwd writing dlogits (bf16); metrics read once per step
+
+The transformer forward/backward is outside the hot path (north_star: PyTorch-ROCm owns it),
+so its logits are synthetic and resident in HBM before timing (data="synthetic"). With N > 1
+ranks every rank runs its own batch (weak scaling, no data-path collective: the advantage /
+loss / logprob rows shard by whole prompt groups); one packed fp32 metric all-reduce per step
+over RCCL keeps the reference's metric semantics.
+
+The dominant kernel (skyrl_logprob_fwd) is timed live with HIP events on its launch stream,
+and the CPU oracle (oracle/cpu_ref.py + oracle/sampler_ref.c, "port") is timed on a bounded
+sample on rank 0 at N=1.
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+P_MAX, R_MAX, PROMPTS, GROUP, VOCAB = 512, 1024, 64, 8, 151936
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy ~6.3 TB/s
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def synth_inputs(dev, N, seed=1234):
+    """SURVEY §8(d) synthetic batch (torch.Generator seed 1234)."""
+    g = torch.Generator().manual_seed(seed)
+    plens = torch.randint(16, P_MAX + 1, (PROMPTS,), generator=g).repeat_interleave(GROUP)[:N]
+    rlens = torch.randint(1, R_MAX + 1, (N,), generator=g)
+    rlens[0] = R_MAX  # the padded width is R_MAX
+    plens[0] = P_MAX
+    hit = (torch.rand(N, generator=g) < 0.3).float()
+    poff = torch.zeros(N + 1, dtype=torch.int64)
+    poff[1:] = torch.cumsum(plens, 0)
+    roff = torch.zeros(N + 1, dtype=torch.int64)
+    roff[1:] = torch.cumsum(rlens, 0)
+    ptok = torch.randint(0, VOCAB, (int(poff[-1]),), generator=g)
+    rtok = torch.randint(0, VOCAB, (int(roff[-1]),), generator=g)
+    rew = torch.zeros(int(roff[-1]))
+    rew[roff[1:] - 1] = hit
+    lmask = torch.ones(int(roff[-1]))
+    rlp = -2 + 0.1 * torch.randn(int(roff[-1]), generator=g)
+    uids = [str(i // GROUP) for i in range(N)]
+    d = dict(plens=plens, rlens=rlens, poff=poff, roff=roff, ptok=ptok, rtok=rtok, rew=rew, lmask=lmask, rlp=rlp)
+    return {k: v.to(dev) for k, v in d.items()}, uids
+
+
+def fill_logits(dev, rows, V, chunk_rows=8192):
+    """Resident bf16 logits [rows, V] ~ N(0, 3^2), generated on device in chunks."""
+    x = torch.empty((rows, V), dtype=torch.bfloat16, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(42)
+    for s in range(0, rows, chunk_rows):
+        e = min(rows, s + chunk_rows)
+        x[s:e].normal_(0.0, 3.0, generator=gen)
+    return x
+
+
+class KernelTimer:
+    """HIP events around launches of one kernel on its launch stream (timed region only)."""
+
+    def __init__(self):
+        self.pairs = []
+        self.active = False
+
+    def wrap(self, fn):
+        if not self.active:
+            return fn()
+        s = torch.cuda.current_stream()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        out = fn()
+        b.record(s)
+        self.pairs.append((a, b))
+        return out
+
+    def avg_ms(self):
+        if not self.pairs:
+            return float("nan")
+        return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
+
+
+def run(args):
+    from skyrl_amd import ops, ppo_utils
+    from skyrl_amd.config import AlgorithmConfig
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    N = PROMPTS * GROUP
+    R, V, mb = R_MAX, VOCAB, args.micro_batch
+    data, uids = synth_inputs(dev, N, seed=1234 + rank)
+
+    # resident logits: all N*R response positions if HBM allows, else a pool reused round-robin
+    free, _ = torch.cuda.mem_get_info(dev)
+    row_bytes = V * 2
+    dlogits_bytes = mb * R * row_bytes
+    budget = free - dlogits_bytes - (8 << 30)
+    rows = N * R if args.logits_rows <= 0 else args.logits_rows
+    rows = int(min(rows, max(mb * R, budget // row_bytes)))
+    rows = (rows // (mb * R)) * (mb * R)
+    log(f"rank {rank}/{world}: free HBM {free / 2**30:.1f} GiB, resident logits rows {rows} "
+        f"({rows * row_bytes / 2**30:.1f} GiB; full batch needs {N * R})")
+    logits = fill_logits(dev, rows, V)
+    dlogits = torch.empty((mb, R, V), dtype=torch.bfloat16, device=dev)
+    full = rows == N * R
+    n_pools = rows // (mb * R)
+
+    def lg_rows(seq0, nseq):  # [nseq, R, V] view of the logits of sequences seq0..
+        blk = (seq0 // mb) % n_pools
+        return logits[blk * mb * R:(blk + 1) * mb * R].view(mb, R, V)[: nseq] if not full else \
+            logits[seq0 * R:(seq0 + nseq) * R].view(nseq, R, V)
+
+    labels = torch.randint(0, V, (N, R), device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+    seq_ids = torch.arange(N, device=dev, dtype=torch.int64) + rank * N
+    tokens = torch.empty((R, N), dtype=torch.int32, device=dev)
+    samp_lp = torch.empty((R, N), dtype=torch.float32, device=dev)
+    goff, grows, ng = ops.groups_from_index(uids)
+    goff, grows = goff.to(dev), grows.to(dev)
+    cfg = AlgorithmConfig()
+    params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, has_entropy=True)
+    fwd_timer = KernelTimer()
+    metrics_acc = torch.zeros(8, dtype=torch.float32, device=dev)
+
+    def step(step_idx):
+        # ---- rollout: R decode steps over [N, V] logits (row stride R*V in the resident tensor)
+        for t in range(R):
+            if full:
+                view = logits.view(N, R, V)[:, t, :]
+            else:
+                base = (t * N) % (rows - N + 1)
+                view = logits[base:base + N]
+            ops.sample(view, temperature=1.0, seed=step_idx, seq_ids=seq_ids, step=t, tokens_out=tokens[t],
+                       logp_out=samp_lp[t])
+        # ---- pack ragged rollout output into the padded training tensors
+        seqs, att, rmask, rew, lmask, rlp = ops.pack_experience(
+            data["ptok"], data["poff"], data["rtok"], data["roff"], data["rew"], data["roff"], data["lmask"],
+            data["roff"], data["rlp"], data["roff"], N=N, P=P_MAX, R=R, pad=0, pad_token_id=0)
+        # ---- ref + old policy logprobs over all response positions (no grad)
+        ref_lp = torch.empty((N, R), dtype=torch.float32, device=dev)
+        old_lp = torch.empty((N, R), dtype=torch.float32, device=dev)
+        for s in range(0, N, mb):
+            x = lg_rows(s, mb)
+            lab = labels[s:s + mb]
+            for out in (ref_lp, old_lp):
+                ops._ffi.call("skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
+                              ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None,
+                              ops._stream(dev))
+        # ---- GRPO advantage over the whole batch
+        adv = ops.grpo_advantage(rew, rmask, goff, grows, ng)
+        # ---- update: per micro-batch logprob+entropy fwd, fused loss fwd/bwd, logprob bwd
+        metrics_acc.zero_()
+        lp = torch.empty((mb, R), dtype=torch.float32, device=dev)
+        ent = torch.empty_like(lp)
+        lse = torch.empty_like(lp)
+        for s in range(0, N, mb):
+            x = lg_rows(s, mb)
+            lab = labels[s:s + mb]
+            fwd_timer.wrap(lambda: ops._ffi.call(
+                "skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V, ops._ptr(lab),
+                lab.stride(0), lab.stride(1), 1.0, ops._ptr(lp), ops._ptr(ent), ops._ptr(lse), ops._stream(dev)))
+            lpr = lp.detach().requires_grad_(True)
+            loss, m = ops.ppo_loss(lpr, old_lp[s:s + mb], adv[s:s + mb], lmask[s:s + mb], params,
+                                   ref_log_probs=ref_lp[s:s + mb], entropy=ent)
+            (glp,) = torch.autograd.grad(loss, lpr)
+            ops._ffi.call("skyrl_logprob_bwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
+                          ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(lse), ops._ptr(ent),
+                          ops._ptr(glp), None, ops._ptr(dlogits), ops._stream(dev))
+            metrics_acc.add_(m)
+        if world > 1:
+            dist.all_reduce(metrics_acc)
+        return metrics_acc
+
+    for w in range(args.warmup):
+        t0 = time.time()
+        step(w)
+        torch.cuda.synchronize()
+        log(f"warmup {w}: {time.time() - t0:.3f}s")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    fwd_timer.active = True
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        m = step(1000 + k)
+        if k == args.steps - 1 or (k % 2 == 0):
+            log(f"step {k} enqueued ({time.perf_counter() - t0:.2f}s)")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    fwd_timer.active = False
+    mvals = m.tolist()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = N * world * args.steps / elapsed
+
+    # roofline of the dominant kernel: algorithmic bytes per launch / average launch time
+    rows_per_launch = mb * R
+    fwd_bytes = rows_per_launch * (V * 2 + 8 + 4 * 3)
+    fwd_ms = fwd_timer.avg_ms()
+    achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
+    result = {
+        "metric": "trained samples/sec (rollout+update), Qwen2.5-1.5B GRPO at 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic",
+        "config": {
+            "workload": "grpo_hot_path_qwen2.5-1.5b_vocab",
+            "prompts": PROMPTS, "group": GROUP, "global_batch": N * world, "seq_len": R, "prompt_len": P_MAX,
+            "vocab": V, "micro_batch": mb, "parallelism": f"dp{world}",
+            "logits_resident_rows": rows, "logits_full_batch_resident": full,
+            "final_loss_sum_last_step": round(mvals[0], 6),
+        },
+        "roofline": {
+            "kernel": "skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "bytes_per_launch": fwd_bytes,
+            "avg_launch_ms": round(fwd_ms, 4),
+            "launches_timed": len(fwd_timer.pairs),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args):
+    """The oracle (CPU restatement, 'port') on a bounded sample of the same workload.
+
+    Sample: 2 trajectories' per-token work (R decode steps of the C sampler oracle over V, two
+    no-grad logprob passes and one logprob fwd+bwd pass over R x V fp32 on torch-CPU) plus the
+    batch-level work (GRPO, loss fwd/bwd, pack) on the full 512 x 1024 batch divided by 512.
+    """
+    import numpy as np
+
+    from oracle import cpu_ref
+
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, args.cpu_threads) if args.cpu_threads > 0 else cores
+    torch.set_num_threads(cores)
+    R, V, N = R_MAX, VOCAB, PROMPTS * GROUP
+    n_traj = 2
+    g = torch.Generator().manual_seed(0)
+    logits = (torch.randn(n_traj, R, V, generator=g) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (n_traj, R), generator=g)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libsampler_ref.so"))
+    f = lib.sampler_ref
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                  ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p]
+    raw = logits.view(torch.int16)
+    tok = torch.empty(n_traj, dtype=torch.int32)
+    lpo = torch.empty(n_traj, dtype=torch.float32)
+    keys = torch.empty(V, dtype=torch.int32)
+    ids = torch.arange(n_traj, dtype=torch.int64)
+    steps = args.cpu_sampler_steps
+    t0 = time.perf_counter()
+    for t in range(steps):  # one decode step = n_traj rows of V
+        f(raw[:, t].contiguous().data_ptr(), 1, V, n_traj, V, 1.0, -1, 0.0, 0, ids.data_ptr(), t, tok.data_ptr(),
+          lpo.data_ptr(), keys.data_ptr())
+    t_sample = (time.perf_counter() - t0) * (R / steps)
+    tok_sample = args.cpu_logprob_tokens
+    x = logits.reshape(-1, V)[:tok_sample]
+    lab = labels.reshape(-1)[:tok_sample]
+    t0 = time.perf_counter()
+    for _ in range(2):
+        cpu_ref.logprobs_from_logits(x, lab)
+    xg = x.float().requires_grad_(True)
+    lp = cpu_ref.logprobs_from_logits(xg, lab)
+    ent = cpu_ref.entropy_from_logits(xg)
+    (lp.sum() + ent.sum()).backward()
+    t_lp = (time.perf_counter() - t0) * (n_traj * R / tok_sample)
+    # batch-level ops on the full batch
+    lens = torch.randint(1, R + 1, (N,), generator=g)
+    mask = (torch.arange(R)[None] < lens[:, None]).float()
+    rew = torch.zeros(N, R)
+    rew[torch.arange(N), lens - 1] = (torch.rand(N, generator=g) < 0.3).float()
+    uids = [str(i // GROUP) for i in range(N)]
+    lpb = -2 + 0.1 * torch.randn(N, R, generator=g)
+    t0 = time.perf_counter()
+    adv = cpu_ref.grpo_advantage(rew, mask, uids)
+    xb = lpb.clone().requires_grad_(True)
+    loss, _ = cpu_ref.policy_loss_assembly(xb, lpb + 0.01, adv, mask, lpb - 0.01, torch.rand(N, R))
+    loss.backward()
+    prompts = [list(range(int(k))) for k in torch.randint(16, P_MAX + 1, (N,), generator=g)]
+    responses = [list(range(int(k))) for k in lens]
+    cpu_ref.pack(prompts, responses, [[0.0] * len(r) for r in responses], [[1.0] * len(r) for r in responses],
+                 None, 0)
+    t_batch = time.perf_counter() - t0
+    per_traj = (t_sample + t_lp) / n_traj + t_batch / N
+    return {
+        "value": round(1.0 / per_traj, 4),
+        "unit": "samples/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"{n_traj} trajectories x R={R}: sampler_ref.c over V={V} for {steps} decode steps "
+                   f"(extrapolated to {R}), torch-CPU fp32 logprob x2 + logprob/entropy fwd+bwd on {tok_sample} "
+                   f"tokens (extrapolated to {n_traj * R}); GRPO + fused-loss fwd/bwd + pack on the full "
+                   f"{N}x{R} batch / {N}"),
+        "seconds": round(t_sample + t_lp + t_batch, 2),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--micro-batch", type=int, default=16)
+    ap.add_argument("--logits-rows", type=int, default=0, help="0 = the whole batch if HBM allows")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-sampler-steps", type=int, default=64)
+    ap.add_argument("--cpu-logprob-tokens", type=int, default=256)
+    args = ap.parse_args()
+    run(args)
+
+
+if __name__ == "__main__":
+    main()

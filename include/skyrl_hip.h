@@ -1,0 +1,221 @@
+/*
+ * skyrl_hip.h — C ABI of libskyrl_hip.so, the MI355X (gfx950) hot path of the
+ * skyrl-train GRPO/PPO actor-learner loop.
+ *
+ * Every entry point:
+ *   - takes device pointers, element counts/strides and a hipStream_t (passed as void*),
+ *   - never allocates; scratch comes from the caller (see *_workspace_bytes),
+ *   - is stream-ordered and never synchronises the host,
+ *   - returns 0 on success or a SKYRL_ERR_* code; skyrl_last_error() returns a
+ *     thread-local message describing the last failure on the calling thread.
+ *
+ * Reference interfaces each entry point replaces are cited as
+ * path:line under /root/reference/skyrl-train/skyrl_train/ (snapshot 2026-02-27).
+ * The reference has no FFI of its own (pure Python/PyTorch); the binding a
+ * maintainer would add is the ctypes stub in INTEGRATION.md.
+ */
+#ifndef SKYRL_HIP_H
+#define SKYRL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------- */
+#define SKYRL_OK 0
+#define SKYRL_ERR_INVALID 1   /* bad argument (shape, dtype, null pointer) */
+#define SKYRL_ERR_LAUNCH 2    /* hipGetLastError() after a launch was not hipSuccess */
+#define SKYRL_ERR_UNSUPPORTED 3
+
+/* ---- dtype codes (element type of a tensor argument) -------------------- */
+#define SKYRL_F32 0
+#define SKYRL_BF16 1
+#define SKYRL_I64 2
+#define SKYRL_I32 3
+#define SKYRL_U8 4   /* bool masks */
+
+/* Thread-local text of the last error on this thread ("" if none). */
+const char* skyrl_last_error(void);
+/* ABI version; bumped on any signature change. */
+int skyrl_abi_version(void);
+
+/* ---- a4: GRPO outcome advantage ----------------------------------------
+ * Replaces compute_grpo_outcome_advantage (utils/ppo_utils.py:1132-1182) as
+ * reached through compute_advantages_and_returns (ppo_utils.py:1190-1214).
+ * score[i] = sum_t rewards[i,t]; per uid group: mean, unbiased std (singleton:
+ * mean 0, std 1); adv = (score-mean)/(std+eps) (or score-mean); out = adv*mask.
+ * Groups are given in CSR form: rows of group g are group_rows[group_off[g] ..
+ * group_off[g+1]) (the host maps the reference's `index` uids to groups).
+ * rewards/out: f32 [N,R] row-major contiguous; mask: [N,R] of mask_dtype.   */
+int skyrl_grpo_advantage(const float* rewards, const void* response_mask, int mask_dtype,
+                         const int32_t* group_off, const int32_t* group_rows, int32_t num_groups,
+                         int32_t N, int32_t R, float epsilon, int32_t norm_by_std,
+                         float* advantages, float* scores_out /* [N] or NULL */, void* stream);
+
+/* ---- a5: GAE + masked whitening ----------------------------------------
+ * Replaces compute_gae_advantage_return (ppo_utils.py:1101-1129) and
+ * masked_whiten/masked_var (ppo_utils.py:148-172). Recursion over all R
+ * positions with no mask (parity trap: padded values leak into the last
+ * valid delta). adv is whitened by masked mean / unbiased masked var.
+ * workspace: skyrl_gae_workspace_bytes(N) bytes, 16-B aligned.
+ * status (int32, device): 0 ok, 1 mask sum == 0, 2 mask sum == 1 (the two
+ * ValueErrors of masked_var, ppo_utils.py:157-163).                        */
+size_t skyrl_gae_workspace_bytes(int32_t N);
+int skyrl_gae_advantage_return(const float* rewards, const float* values, const void* response_mask,
+                               int mask_dtype, int32_t N, int32_t R, float gamma, float lambd,
+                               float* advantages, float* returns, void* workspace,
+                               int32_t* status, void* stream);
+
+/* ---- a6: approximate KL -------------------------------------------------
+ * Replaces compute_approx_kl (ppo_utils.py:88-124). kl_type: 0 k1, 1 abs,
+ * 2 k2, 3 k3. loss_mask may be NULL. All f32 [n] contiguous.               */
+int skyrl_approx_kl(const float* log_probs, const float* log_probs_base, const void* loss_mask,
+                    int mask_dtype, int64_t n, int32_t kl_type, float* kl_out, void* stream);
+
+/* ---- a6 (reward side): KL penalty on rewards -----------------------------
+ * Replaces RayPPOTrainer.apply_reward_kl_penalty (trainer.py:981-1035):
+ * rewards_out = rewards - kl*max(0,coef); metrics_out[0] = avg_kl
+ * (mean over rows of masked_mean(kl,mask,-1)), metrics_out[1] = avg_kl_max
+ * (mean over rows of max_t |kl|). loss_mask f32 [N,R].                     */
+size_t skyrl_reward_kl_workspace_bytes(int32_t N);
+int skyrl_reward_kl_penalty(const float* rewards, const float* action_log_probs,
+                            const float* base_action_log_probs, const float* loss_mask,
+                            int32_t N, int32_t R, int32_t kl_type, float kl_coef,
+                            float* rewards_out, float* metrics_out /* [2] device */,
+                            void* workspace, void* stream);
+
+/* ---- a7: fused clipped policy loss + KL(ref) + entropy term --------------
+ * Replaces ppo_policy_loss (ppo_utils.py:548-586) + reduce_loss (:984-1009)
+ * + the loss assembly of PolicyWorkerBase._forward_backward_micro
+ * (workers/worker.py:810-876: entropy masked_mean, k-type KL seq-mean then
+ * batch-mean, final = pg + kl*coef - H*coef*[use_entropy_loss]).
+ * Forward writes the scalar loss, the metric vector and a per-token gradient
+ * numerator; skyrl_ppo_loss_bwd turns it into dL/dlogp (and dL/dentropy).
+ * Gradient semantics follow torch autograd of the reference: min() ties split
+ * the gradient 1/2-1/2, clamp passes gradient on the closed interval, the KL
+ * term carries NO gradient (compute_approx_kl is @torch.no_grad()).         */
+typedef struct skyrl_ppo_params {
+    float eps_clip_low;
+    float eps_clip_high;
+    float clip_ratio_c;
+    int32_t dual_clip;        /* policy_loss_type == "dual_clip" */
+    int32_t loss_reduction;   /* 0 token_mean, 1 sequence_mean, 2 seq_mean_token_sum_norm */
+    float max_seq_len;        /* used by seq_mean_token_sum_norm */
+    int32_t use_kl_loss;
+    int32_t kl_type;          /* 0 k1, 1 abs, 2 k2, 3 k3 */
+    float kl_loss_coef;
+    int32_t use_entropy_loss;
+    float entropy_loss_coef;
+    int32_t has_entropy;      /* entropy pointer given: policy_entropy metric */
+} skyrl_ppo_params;
+
+/* metric vector layout (f32, device) */
+#define SKYRL_M_FINAL_LOSS 0
+#define SKYRL_M_POLICY_LOSS 1
+#define SKYRL_M_ENTROPY 2
+#define SKYRL_M_KL 3
+#define SKYRL_M_CLIP_RATIO 4
+#define SKYRL_M_MASK_SUM 5
+#define SKYRL_M_COUNT 8
+
+size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R);
+/* workspace must be zeroed once at allocation; the kernel leaves it re-usable. */
+int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const float* advantages,
+                       const float* loss_mask /* NULL = all ones */, const float* ref_log_probs,
+                       const float* entropy, int32_t n, int32_t R, const skyrl_ppo_params* params,
+                       float* loss_out /* [1] */, float* metrics_out /* [SKYRL_M_COUNT] */,
+                       float* grad_num /* [n,R] */, float* row_scale /* [n] */, void* workspace,
+                       void* stream);
+/* grad_logp = g * grad_num * row_scale[row]; grad_entropy (optional) =
+ * -g*entropy_loss_coef*mask/max(sum mask,1) when use_entropy_loss.           */
+int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, const float* grad_num,
+                       const float* row_scale, const float* loss_mask, const float* metrics,
+                       int32_t n, int32_t R, const skyrl_ppo_params* params, float* grad_logp,
+                       float* grad_entropy /* NULL unless use_entropy_loss */, void* stream);
+
+/* ---- a8: clipped value loss ---------------------------------------------
+ * Replaces ppo_critic_loss (ppo_utils.py:175-193): 0.5*mean_rows(masked_mean(
+ * max((clip(V,old±c)-ret)^2,(V-ret)^2), mask, -1)); value_clip<0 => no clip.
+ * Forward writes loss[1], clipfrac[1] and grad_values (for g=1).            */
+int skyrl_critic_loss_fwd(const float* values, const float* old_values, const float* returns,
+                          const float* loss_mask, int32_t n, int32_t R, float value_clip,
+                          float* loss_out, float* clipfrac_out, float* grad_values, void* workspace,
+                          void* stream);
+size_t skyrl_critic_loss_workspace_bytes(int32_t n, int32_t R);
+
+/* ---- a2/a3: logprob + entropy over the vocabulary ------------------------
+ * Replaces logprobs_from_logits (utils/torch_utils.py:115-177, flash-attn CE
+ * semantics: fp32 LSE of the (temperature-divided) logits minus the label
+ * logit) and chunked_entropy_from_logits (torch_utils.py:59-111) as used by
+ * HFModelWrapper.forward (model_wrapper.py:313-363). Row r = (b,t) reads
+ * logits + b*stride_b + t*stride_t (elements), V contiguous elements.
+ * temperature: logits are divided by it in their own dtype first
+ * (model_wrapper.py:314 divides in place in bf16).
+ * Outputs (f32 [nb*nt], row-major (b,t)): logp, entropy (NULL skips), lse.  */
+int skyrl_logprob_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t,
+                      int32_t nb, int32_t nt, int32_t V, const int64_t* labels,
+                      int64_t lstride_b, int64_t lstride_t, float temperature, float* logp_out,
+                      float* entropy_out, float* lse_out, void* stream);
+/* d logits (same dtype, dense [nb,nt,V]) = (g_lp*(onehot-p) + g_ent*(-p*(logp_v+H)))/T.
+ * grad_entropy may be NULL; entropy must be given if grad_entropy is.          */
+int skyrl_logprob_bwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t,
+                      int32_t nb, int32_t nt, int32_t V, const int64_t* labels,
+                      int64_t lstride_b, int64_t lstride_t, float temperature, const float* lse,
+                      const float* entropy, const float* grad_logp, const float* grad_entropy,
+                      void* grad_logits, void* stream);
+
+/* ---- a1: rollout token sampling -----------------------------------------
+ * Replaces the vLLM sampler behind VLLMInferenceEngine.generate
+ * (inference_engines/vllm/vllm_engine.py:196-218) with sampled-token logprob
+ * extraction (vllm_engine.py:139-149) and SamplingParams defaults
+ * (config/ppo_base_config.yaml:316-324). Filter order temperature->top_k->
+ * min_p (semantics: skyrl-tx/tx/utils/generator.py:398-449); top_k<=0 off.
+ * temperature==0 => greedy (lowest index wins ties). Otherwise Gumbel-max with
+ * a counter-based hash keyed by (seed, seq_ids[i], step, vocab index), so the
+ * token is a pure function of its inputs (bit-exact vs oracle/sampler_ref.c).
+ * logp_out = log_softmax(raw logits)[token] (unscaled logits).
+ * logits row i at logits + i*ld (elements).                                  */
+int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V,
+                 float temperature, int32_t top_k, float min_p, uint64_t seed,
+                 const int64_t* seq_ids, int64_t step, int32_t* tokens_out, float* logp_out,
+                 void* workspace, void* stream);
+size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V);
+
+/* ---- a9: experience pack --------------------------------------------------
+ * Replaces convert_prompts_responses_to_batch_tensors (dataset/preprocess.py:
+ * 28-132) + pad_batch (trainer.py:872-907). Ragged inputs in CSR form
+ * (offsets int64 [N+1]); P/R = max prompt/response length; rows N..N+pad-1
+ * are clones of rows 0..pad-1 with loss_mask 0 (pad_batch).
+ * Outputs: sequences i64 [Np,P+R] (left-padded prompt | right-padded
+ * response), attention_mask i64 [Np,P+R], response_mask i64 [Np,R],
+ * rewards f32 [Np,R], loss_mask f32 [Np,R], rollout_logprobs f32 [Np,R]
+ * (NULL when logprob_vals is NULL). Np = N + pad.                            */
+typedef struct skyrl_pack_inputs {
+    const int64_t* prompt_tokens;   const int64_t* prompt_off;
+    const int64_t* response_tokens; const int64_t* response_off;
+    const float* reward_vals;       const int64_t* reward_off;
+    const float* loss_mask_vals;    const int64_t* loss_mask_off;
+    const float* logprob_vals;      const int64_t* logprob_off;   /* may be NULL */
+} skyrl_pack_inputs;
+int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int32_t pad, int32_t P, int32_t R,
+                          int64_t pad_token_id, int64_t* sequences, int64_t* attention_mask,
+                          int64_t* response_mask, float* rewards, float* loss_mask,
+                          float* rollout_logprobs, void* stream);
+
+/* ---- a12: gradient scale ------------------------------------------------
+ * grads *= scale over a flat fp32 bucket (optim_step's 1/n_micro scaling,
+ * workers/worker.py:909-914) fused with the squared-L2 partial for clipping
+ * (fsdp_utils.py:388-401): sumsq_out[0] += sum(x^2) (device, f32, atomics).  */
+int skyrl_scale_and_sumsq(float* grads, int64_t n, float scale, float* sumsq_out, void* stream);
+
+/* out[i] = g[0] * in[i] (g on device): autograd backward of a scalar loss whose
+ * per-element gradient was produced by a forward kernel for unit upstream grad. */
+int skyrl_scale_by_device_scalar(const float* g, const float* in, float* out, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKYRL_HIP_H */

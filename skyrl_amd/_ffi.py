@@ -1,0 +1,149 @@
+"""ctypes binding of ``libskyrl_hip.so`` (the C ABI declared in ``include/skyrl_hip.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C skyrl_amd/csrc``).
+There is no fallback: if the library is missing, or no GPU is visible, every op raises.
+
+torch is imported first on purpose: torch ships its own ``libamdhip64.so.7``; loading it
+before the extension makes the dynamic linker bind our NEEDED ``libamdhip64.so.7`` to the
+same HIP runtime instance, so torch's device pointers and ``hipStream_t`` handles are valid
+inside our kernels.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libskyrl_hip.so")
+
+F32, BF16, I64, I32, U8 = 0, 1, 2, 3, 4
+M_FINAL_LOSS, M_POLICY_LOSS, M_ENTROPY, M_KL, M_CLIP_RATIO, M_MASK_SUM = 0, 1, 2, 3, 4, 5
+M_COUNT = 8
+
+
+class SkyrlHipError(RuntimeError):
+    """A C-ABI entry point returned a non-zero status."""
+
+
+class PPOParams(ctypes.Structure):
+    """Mirror of ``skyrl_ppo_params`` (include/skyrl_hip.h)."""
+
+    _fields_ = [
+        ("eps_clip_low", ctypes.c_float),
+        ("eps_clip_high", ctypes.c_float),
+        ("clip_ratio_c", ctypes.c_float),
+        ("dual_clip", ctypes.c_int32),
+        ("loss_reduction", ctypes.c_int32),
+        ("max_seq_len", ctypes.c_float),
+        ("use_kl_loss", ctypes.c_int32),
+        ("kl_type", ctypes.c_int32),
+        ("kl_loss_coef", ctypes.c_float),
+        ("use_entropy_loss", ctypes.c_int32),
+        ("entropy_loss_coef", ctypes.c_float),
+        ("has_entropy", ctypes.c_int32),
+    ]
+
+
+class PackInputs(ctypes.Structure):
+    """Mirror of ``skyrl_pack_inputs`` (include/skyrl_hip.h)."""
+
+    _fields_ = [
+        ("prompt_tokens", ctypes.c_void_p),
+        ("prompt_off", ctypes.c_void_p),
+        ("response_tokens", ctypes.c_void_p),
+        ("response_off", ctypes.c_void_p),
+        ("reward_vals", ctypes.c_void_p),
+        ("reward_off", ctypes.c_void_p),
+        ("loss_mask_vals", ctypes.c_void_p),
+        ("loss_mask_off", ctypes.c_void_p),
+        ("logprob_vals", ctypes.c_void_p),
+        ("logprob_off", ctypes.c_void_p),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+_INT = ctypes.c_int
+
+# name -> (restype, argtypes); the complete exported surface of include/skyrl_hip.h
+SIGNATURES = {
+    "skyrl_last_error": (ctypes.c_char_p, []),
+    "skyrl_abi_version": (_INT, []),
+    "skyrl_grpo_advantage": (_INT, [_P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
+    "skyrl_gae_workspace_bytes": (_SZ, [_I32]),
+    "skyrl_gae_advantage_return": (_INT, [_P, _P, _P, _INT, _I32, _I32, _F, _F, _P, _P, _P, _P, _P]),
+    "skyrl_approx_kl": (_INT, [_P, _P, _P, _INT, _I64, _I32, _P, _P]),
+    "skyrl_reward_kl_workspace_bytes": (_SZ, [_I32]),
+    "skyrl_reward_kl_penalty": (_INT, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P]),
+    "skyrl_ppo_loss_workspace_bytes": (_SZ, [_I32, _I32]),
+    "skyrl_ppo_loss_fwd": (
+        _INT,
+        [_P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P, _P, _P],
+    ),
+    "skyrl_ppo_loss_bwd": (_INT, [_P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P]),
+    "skyrl_critic_loss_workspace_bytes": (_SZ, [_I32, _I32]),
+    "skyrl_critic_loss_fwd": (_INT, [_P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),
+    "skyrl_logprob_fwd": (_INT, [_P, _INT, _I64, _I64, _I32, _I32, _I32, _P, _I64, _I64, _F, _P, _P, _P, _P]),
+    "skyrl_logprob_bwd": (
+        _INT,
+        [_P, _INT, _I64, _I64, _I32, _I32, _I32, _P, _I64, _I64, _F, _P, _P, _P, _P, _P, _P],
+    ),
+    "skyrl_sample_workspace_bytes": (_SZ, [_I32, _I32]),
+    "skyrl_sample": (_INT, [_P, _INT, _I64, _I32, _I32, _F, _I32, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),
+    "skyrl_pack_experience": (
+        _INT,
+        [ctypes.POINTER(PackInputs), _I32, _I32, _I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "skyrl_scale_and_sumsq": (_INT, [_P, _I64, _F, _P, _P]),
+    "skyrl_scale_by_device_scalar": (_INT, [_P, _P, _P, _I64, _P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib_available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def load() -> ctypes.CDLL:
+    """Load the library once and bind every signature. Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"skyrl_amd HIP library not built: {LIB_PATH} is missing. "
+                "Run `python -c 'import __graft_entry__ as g; g.build()'` (make -C skyrl_amd/csrc)."
+            )
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args) -> int:
+    """Invoke a status-returning entry point; raise SkyrlHipError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.skyrl_last_error().decode(errors="replace")
+        raise SkyrlHipError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def query(name: str, *args):
+    """Invoke a non-status entry point (workspace sizes, version)."""
+    return getattr(load(), name)(*args)

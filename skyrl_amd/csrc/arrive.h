@@ -1,0 +1,59 @@
+// Last-arriver election for in-launch reductions (gfx950, 8 XCDs with private L2s).
+//
+// Producer side follows the guide's split-K recipe: every storing wave drains
+// (s_waitcnt vmcnt(0)), block barrier, lane 0 agent-scope RELEASE, asm drain
+// (ROCm 7.2 may drop the fence's own wait), relaxed agent fetch_add on the
+// ticket. The block drawing the last ticket does one agent-scope ACQUIRE
+// (invalidates this CU's L1) before a barrier, then reads every block's
+// partials with plain loads, and finally re-arms the counter to 0.
+// The counter lives in caller-owned workspace zeroed once at allocation.
+#pragma once
+#include "common.h"
+
+namespace skyrl {
+
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total, int* lds_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (prev == total - 1u);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *lds_flag = last;
+    }
+    __syncthreads();
+    return *lds_flag != 0;
+}
+
+__device__ __forceinline__ void rearm(unsigned* counter) {
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Block-wide sum of NV doubles (fixed tree, deterministic). lds: NW*NV doubles.
+template <int NW, int NV>
+__device__ __forceinline__ void block_sum_d(double (&v)[NV], double* lds) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) s += lds[j * NV + k];
+        v[k] = s;
+    }
+    __syncthreads();
+}
+
+}  // namespace skyrl

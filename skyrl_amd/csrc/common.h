@@ -1,0 +1,89 @@
+// Shared device helpers for the gfx950 hot-path kernels (wave64, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/skyrl_hip.h"
+
+namespace skyrl {
+
+constexpr int kWave = 64;
+
+// ---- error plumbing (host) -------------------------------------------------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+#define SKYRL_REQUIRE(cond, msg)                                   \
+    do {                                                           \
+        if (!(cond)) return ::skyrl::fail(SKYRL_ERR_INVALID, msg); \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- dtype helpers (device) ------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+    return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+// Round-to-nearest-even f32 -> bf16, NaN kept a NaN (quiet).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return static_cast<uint16_t>(u >> 16);
+}
+
+// Mask element as float, for every mask dtype the reference uses
+// (int64 response_mask, f32 loss_mask, bool).
+__device__ __forceinline__ float load_mask(const void* m, int dtype, int64_t i) {
+    switch (dtype) {
+        case SKYRL_F32: return reinterpret_cast<const float*>(m)[i];
+        case SKYRL_I64: return static_cast<float>(reinterpret_cast<const int64_t*>(m)[i]);
+        case SKYRL_I32: return static_cast<float>(reinterpret_cast<const int32_t*>(m)[i]);
+        case SKYRL_U8: return static_cast<float>(reinterpret_cast<const uint8_t*>(m)[i]);
+        default: return 0.f;
+    }
+}
+
+// ---- wave / block reductions ------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+
+// Sum of NV values across a block of NW waves; result valid in every thread.
+// `lds` needs NW*NV floats. Deterministic (fixed tree).
+template <int NW, int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* lds) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) s += lds[j * NV + k];
+        v[k] = s;
+    }
+    __syncthreads();
+}
+
+}  // namespace skyrl

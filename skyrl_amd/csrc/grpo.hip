@@ -1,0 +1,173 @@
+// a4: GRPO outcome advantage (reference: utils/ppo_utils.py:1132-1182).
+//
+// One launch over the whole [N,R] batch. Grid = (group, 256-column slice).
+// Every block of a group recomputes the group's row sums (the rewards of one
+// group are G*R*4 B = 32 KB at G=8, R=1024: re-read from L2/MALL, not HBM), so
+// no inter-workgroup hand-off is needed; slice s then writes its 256 columns
+// of adv*mask for all rows of the group. Row sums use a fixed reduction tree,
+// so every slice sees bit-identical scores. Group stats in fp64 (torch.std on
+// CPU accumulates in double), the normalisation itself in fp32 as the
+// reference does.
+#include "common.h"
+
+namespace skyrl {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kSlice = 256;          // columns written per block
+constexpr int kMaxCachedRows = 1024; // scores cached in LDS; larger groups recompute
+
+// Sum of one reward row by one wave (all lanes get the result).
+__device__ float row_sum_wave(const float* __restrict__ row, int R, bool vec4) {
+    const int lane = threadIdx.x & (kWave - 1);
+    float acc = 0.f;
+    if (vec4) {
+        const float4* r4 = reinterpret_cast<const float4*>(row);
+        const int n4 = R >> 2;
+        for (int i = lane; i < n4; i += kWave) {
+            float4 v = r4[i];
+            acc += (v.x + v.y) + (v.z + v.w);
+        }
+    } else {
+        for (int i = lane; i < R; i += kWave) acc += row[i];
+    }
+    return wave_sum(acc);
+}
+
+__device__ __forceinline__ void load_mask4(const void* m, int dtype, int64_t idx, float (&o)[4]) {
+    switch (dtype) {
+        case SKYRL_F32: {
+            float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(m) + idx);
+            o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+            break;
+        }
+        case SKYRL_I64: {
+            const longlong2* p = reinterpret_cast<const longlong2*>(reinterpret_cast<const int64_t*>(m) + idx);
+            longlong2 a = p[0], b = p[1];
+            o[0] = (float)a.x; o[1] = (float)a.y; o[2] = (float)b.x; o[3] = (float)b.y;
+            break;
+        }
+        case SKYRL_I32: {
+            int4 v = *reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(m) + idx);
+            o[0] = (float)v.x; o[1] = (float)v.y; o[2] = (float)v.z; o[3] = (float)v.w;
+            break;
+        }
+        default: {
+            uchar4 v = *reinterpret_cast<const uchar4*>(reinterpret_cast<const uint8_t*>(m) + idx);
+            o[0] = (float)v.x; o[1] = (float)v.y; o[2] = (float)v.z; o[3] = (float)v.w;
+            break;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void grpo_adv_kernel(
+    const float* __restrict__ rewards, const void* __restrict__ mask, int mask_dtype,
+    const int32_t* __restrict__ group_off, const int32_t* __restrict__ group_rows, int R,
+    float epsilon, int norm_by_std, bool vec4, float* __restrict__ out, float* __restrict__ scores_out) {
+    __shared__ float s_scores[kMaxCachedRows];
+    __shared__ float s_stat[2];  // mean, denom (std + eps) or 1
+
+    const int g = blockIdx.x;
+    const int slice = blockIdx.y;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    const int beg = group_off[g];
+    const int n = group_off[g + 1] - beg;
+
+    // Phase 1: row sums (score = token_level_rewards.sum(-1), ppo_utils.py:1156).
+    for (int j = w; j < n && j < kMaxCachedRows; j += kWaves) {
+        const int row = group_rows[beg + j];
+        float s = row_sum_wave(rewards + (int64_t)row * R, R, vec4);
+        if (lane == 0) {
+            s_scores[j] = s;
+            if (scores_out && slice == 0) scores_out[row] = s;
+        }
+    }
+    __syncthreads();
+
+    // Phase 2: group mean / unbiased std (ppo_utils.py:1164-1175), wave 0.
+    if (w == 0) {
+        auto score_of = [&](int j) -> float {
+            if (j < kMaxCachedRows) return s_scores[j];
+            const int row = group_rows[beg + j];
+            const float* r = rewards + (int64_t)row * R;
+            float acc = 0.f;
+            for (int i = 0; i < R; ++i) acc += r[i];
+            return acc;
+        };
+        float mean_f, denom_f;
+        if (n <= 1) {
+            mean_f = 0.f;   // singleton group: mean 0, std 1 (ppo_utils.py:1167-1169)
+            denom_f = norm_by_std ? (1.f + epsilon) : 1.f;
+        } else {
+            double sum = 0.0;
+            for (int j = lane; j < n; j += kWave) sum += (double)score_of(j);
+            sum = wave_sum(sum);
+            const double mean = sum / (double)n;
+            double m2 = 0.0;
+            for (int j = lane; j < n; j += kWave) {
+                double d = (double)score_of(j) - mean;
+                m2 += d * d;
+            }
+            m2 = wave_sum(m2);
+            mean_f = (float)mean;
+            const float std_f = (float)sqrt(m2 / (double)(n - 1));
+            denom_f = norm_by_std ? (std_f + epsilon) : 1.f;
+        }
+        if (lane == 0) {
+            s_stat[0] = mean_f;
+            s_stat[1] = denom_f;
+        }
+    }
+    __syncthreads();
+    const float mean = s_stat[0];
+    const float denom = s_stat[1];
+
+    // Phase 3: out[row, slice cols] = ((score - mean) / denom) * mask.
+    const int col0 = slice * kSlice + lane * 4;
+    for (int j = w; j < n; j += kWaves) {
+        const int row = group_rows[beg + j];
+        float score;
+        if (j < kMaxCachedRows) {
+            score = s_scores[j];
+        } else {
+            score = row_sum_wave(rewards + (int64_t)row * R, R, vec4);
+        }
+        const float a = norm_by_std ? (score - mean) / denom : (score - mean);
+        const int64_t base = (int64_t)row * R;
+        if (vec4 && col0 + 3 < R) {
+            float m[4];
+            load_mask4(mask, mask_dtype, base + col0, m);
+            float4 o = make_float4(a * m[0], a * m[1], a * m[2], a * m[3]);
+            *reinterpret_cast<float4*>(out + base + col0) = o;
+        } else {
+            for (int c = col0; c < col0 + 4 && c < R; ++c) out[base + c] = a * load_mask(mask, mask_dtype, base + c);
+        }
+    }
+}
+
+}  // namespace
+}  // namespace skyrl
+
+extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_mask, int mask_dtype,
+                                    const int32_t* group_off, const int32_t* group_rows,
+                                    int32_t num_groups, int32_t N, int32_t R, float epsilon,
+                                    int32_t norm_by_std, float* advantages, float* scores_out,
+                                    void* stream) {
+    using namespace skyrl;
+    SKYRL_REQUIRE(N >= 0 && R >= 0 && num_groups >= 0, "grpo: negative size");
+    if (N == 0 || R == 0 || num_groups == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(rewards && response_mask && group_off && group_rows && advantages, "grpo: null pointer");
+    SKYRL_REQUIRE(mask_dtype == SKYRL_F32 || mask_dtype == SKYRL_I64 || mask_dtype == SKYRL_I32 ||
+                      mask_dtype == SKYRL_U8,
+                  "grpo: unsupported mask dtype");
+    const bool vec4 = (R % 4) == 0 && (reinterpret_cast<uintptr_t>(rewards) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(advantages) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(response_mask) % 16) == 0;
+    dim3 grid(num_groups, (R + kSlice - 1) / kSlice);
+    hipLaunchKernelGGL(grpo_adv_kernel, grid, dim3(kThreads), 0, as_stream(stream), rewards,
+                       response_mask, mask_dtype, group_off, group_rows, R, epsilon, norm_by_std, vec4,
+                       advantages, scores_out);
+    return check_launch("grpo_adv_kernel");
+}

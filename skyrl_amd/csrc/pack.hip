@@ -1,0 +1,143 @@
+// a9: experience pack (ragged CSR -> padded training tensors) fused with
+// pad_batch, plus small utilities (gradient bucket scaling / sum of squares,
+// scalar-scaled copies for autograd backward).
+//
+// Reference: convert_prompts_responses_to_batch_tensors
+// (skyrl-train/skyrl_train/dataset/preprocess.py:28-132): left-padded prompt |
+// right-padded response, int64 sequences/attention/response masks, f32
+// rewards/loss masks, rollout logprobs zero-padded; pad_batch
+// (trainer.py:872-907): rows N..N+pad-1 clone rows 0..pad-1, loss_mask 0.
+//
+// Pure byte movement (HBM-bound, ~23 MB at N=512, P=512, R=1024): grid =
+// (output row, 512-column tile); each thread writes two adjacent int64 columns
+// with one 16-B store where the row allows it.
+#include "common.h"
+
+namespace skyrl {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kCols = kThreads * 2;
+
+__global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, int N, int P, int R, int64_t pad_id,
+                                                        int64_t* __restrict__ seq, int64_t* __restrict__ att,
+                                                        int64_t* __restrict__ rmask, float* __restrict__ rew,
+                                                        float* __restrict__ lmask, float* __restrict__ rlp) {
+    const int i = blockIdx.x;
+    const int src = i < N ? i : i - N;
+    const bool is_pad = i >= N;
+    const int S = P + R;
+    const int64_t p0 = in.prompt_off[src];
+    const int plen = (int)(in.prompt_off[src + 1] - p0);
+    const int lpad = P - plen;
+    const int64_t r0 = in.response_off[src];
+    const int rlen = (int)(in.response_off[src + 1] - r0);
+    const int c0 = blockIdx.y * kCols + threadIdx.x * 2;
+    const int64_t so = (int64_t)i * S;
+    const int64_t ro = (int64_t)i * R;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int c = c0 + k;
+        if (c < S) {
+            int64_t tok;
+            int64_t a;
+            if (c < P) {
+                const bool real = c >= lpad;
+                tok = real ? in.prompt_tokens[p0 + (c - lpad)] : pad_id;
+                a = real ? 1 : 0;
+            } else {
+                const int j = c - P;
+                const bool real = j < rlen;
+                tok = real ? in.response_tokens[r0 + j] : pad_id;
+                a = real ? 1 : 0;
+            }
+            seq[so + c] = tok;
+            att[so + c] = a;
+        }
+        if (c < R) {
+            rmask[ro + c] = c < rlen ? 1 : 0;
+            const int64_t w0 = in.reward_off[src];
+            const int wl = (int)(in.reward_off[src + 1] - w0);
+            rew[ro + c] = c < wl ? in.reward_vals[w0 + c] : 0.f;
+            const int64_t m0 = in.loss_mask_off[src];
+            const int ml = (int)(in.loss_mask_off[src + 1] - m0);
+            lmask[ro + c] = (!is_pad && c < ml) ? in.loss_mask_vals[m0 + c] : 0.f;
+            if (rlp) {
+                const int64_t l0 = in.logprob_off[src];
+                const int ll = (int)(in.logprob_off[src + 1] - l0);
+                rlp[ro + c] = c < ll ? in.logprob_vals[l0 + c] : 0.f;
+            }
+        }
+    }
+}
+
+__global__ void scale_sumsq_kernel(float* __restrict__ g, int64_t n, float scale, float* __restrict__ sumsq) {
+    float acc = 0.f;
+    const int64_t n4 = n / 4;
+    float4* g4 = reinterpret_cast<float4*>(g);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        float4 v = g4[i];
+        v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+        g4[i] = v;
+        acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = g[i] * scale;
+        g[i] = v;
+        acc += v * v;
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0 && sumsq) atomicAdd(sumsq, acc);
+}
+
+__global__ void scale_by_scalar_kernel(const float* __restrict__ s, const float* __restrict__ in,
+                                       float* __restrict__ out, int64_t n) {
+    const float g = s[0];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = g * in[i];
+}
+
+}  // namespace
+}  // namespace skyrl
+
+using namespace skyrl;
+
+extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int32_t pad, int32_t P, int32_t R,
+                                     int64_t pad_token_id, int64_t* sequences, int64_t* attention_mask,
+                                     int64_t* response_mask, float* rewards, float* loss_mask,
+                                     float* rollout_logprobs, void* stream) {
+    SKYRL_REQUIRE(in, "pack: inputs is null");
+    SKYRL_REQUIRE(N > 0 && pad >= 0 && pad <= N && P >= 0 && R >= 0, "pack: bad sizes");
+    SKYRL_REQUIRE(in->prompt_tokens && in->prompt_off && in->response_tokens && in->response_off && in->reward_vals &&
+                      in->reward_off && in->loss_mask_vals && in->loss_mask_off,
+                  "pack: null input pointer");
+    SKYRL_REQUIRE(!rollout_logprobs || (in->logprob_vals && in->logprob_off), "pack: logprobs requested but absent");
+    SKYRL_REQUIRE(sequences && attention_mask && response_mask && rewards && loss_mask, "pack: null output pointer");
+    const int S = P + R;
+    const int cols = S > R ? S : R;
+    if (cols == 0) return SKYRL_OK;
+    dim3 grid(N + pad, (cols + kCols - 1) / kCols);
+    hipLaunchKernelGGL(pack_kernel, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id, sequences,
+                       attention_mask, response_mask, rewards, loss_mask, rollout_logprobs);
+    return check_launch("pack_kernel");
+}
+
+extern "C" int skyrl_scale_and_sumsq(float* grads, int64_t n, float scale, float* sumsq_out, void* stream) {
+    if (n == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(grads && (reinterpret_cast<uintptr_t>(grads) % 16) == 0, "scale_and_sumsq: null/misaligned grads");
+    int64_t blocks = (n / 4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(scale_sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), grads, n, scale,
+                       sumsq_out);
+    return check_launch("scale_sumsq_kernel");
+}
+
+extern "C" int skyrl_scale_by_device_scalar(const float* g, const float* in, float* out, int64_t n, void* stream) {
+    if (n == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(g && in && out, "scale_by_device_scalar: null pointer");
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(scale_by_scalar_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), g, in, out, n);
+    return check_launch("scale_by_scalar_kernel");
+}

@@ -1,0 +1,469 @@
+// a6/a7/a8: approximate KL, fused clipped policy loss (+KL-to-ref, +entropy
+// term) forward/backward, reward KL penalty, clipped value loss.
+//
+// References (skyrl-train/skyrl_train/):
+//   compute_approx_kl            utils/ppo_utils.py:88-124
+//   ppo_policy_loss              utils/ppo_utils.py:548-586
+//   reduce_loss                  utils/ppo_utils.py:984-1009
+//   masked_mean / safe_exp_delta utils/torch_utils.py:180-192
+//   loss assembly                workers/worker.py:810-876
+//   apply_reward_kl_penalty      trainer.py:981-1035
+//   ppo_critic_loss              utils/ppo_utils.py:175-193
+//
+// Layout: all per-token tensors f32 [n,R] row-major. Grid = (row, 1024-column
+// chunk); a block reads its chunk once (20 B/token: logp, old, adv, mask, ref),
+// writes the per-token gradient numerator (4 B/token) and a 5-float partial;
+// the last-arriving block (arrive.h) folds the partials into the scalar loss,
+// the metric vector and the per-row gradient scale. The backward is then a
+// 12 B/token elementwise pass (numerator, scale, upstream grad).
+#include "arrive.h"
+
+namespace skyrl {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kChunk = kThreads * 4;  // columns per block
+constexpr int kNP = 5;                // partials: sum l*m, m, clip*m, kl*m*m, ent*m
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// compute_approx_kl on one element (before the mask multiply).
+__device__ __forceinline__ float approx_kl(float lp, float base, int kl_type) {
+    switch (kl_type) {
+        case 0: return lp - base;
+        case 1: return fabsf(lp - base);
+        case 2: { float d = lp - base; return 0.5f * (d * d); }
+        default: {
+            float kl = clampf(base - lp, -20.f, 20.f);
+            float r = expf(kl);
+            return clampf((r - kl) - 1.f, -10.f, 10.f);
+        }
+    }
+}
+
+struct TokenOut {
+    float loss;   // per-token policy loss (before mask)
+    float dldlp;  // d loss / d logp (before mask and reduction scale)
+    float clip;   // (-surr2 > -surr1)
+};
+
+// ppo_policy_loss for one token, with torch-autograd gradient semantics.
+__device__ __forceinline__ TokenOut ppo_token(float lp, float old, float A, float lo, float hi, float c,
+                                              int dual_clip) {
+    const float delta = lp - old;
+    const float ratio = expf(clampf(delta, -20.f, 20.f));
+    const float dratio = (delta >= -20.f && delta <= 20.f) ? ratio : 0.f;
+    const float surr1 = ratio * A;
+    const float rc = clampf(ratio, lo, hi);
+    const float surr2 = rc * A;
+    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+    float loss1, d1;  // loss1 = -min(surr1, surr2); d1 = d loss1 / d ratio
+    if (surr1 < surr2) {
+        loss1 = -surr1;
+        d1 = -A;
+    } else if (surr2 < surr1) {
+        loss1 = -surr2;
+        d1 = -A * inr;
+    } else {  // tie: torch.min splits the gradient in half
+        loss1 = -surr1;
+        d1 = -(0.5f * A + 0.5f * A * inr);
+    }
+    TokenOut o;
+    o.clip = (-surr2 > -surr1) ? 1.f : 0.f;
+    o.loss = loss1;
+    float d = d1;
+    if (dual_clip && A < 0.f) {
+        const float pg3 = -A * c;
+        if (pg3 < loss1) {
+            o.loss = pg3;
+            d = 0.f;
+        } else if (loss1 == pg3) {
+            d = 0.5f * d1;
+        }
+    }
+    o.dldlp = d * dratio;
+    return o;
+}
+
+__global__ __launch_bounds__(kThreads) void ppo_loss_fwd_kernel(
+    const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
+    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent, int n,
+    int R, skyrl_ppo_params p, bool vec4, float* __restrict__ loss_out, float* __restrict__ metrics,
+    float* __restrict__ gnum, float* __restrict__ row_scale, float* __restrict__ partials,
+    unsigned* __restrict__ counter) {
+    __shared__ float s_red[kWaves * kNP];
+    __shared__ double s_redd[kWaves * 6];
+    __shared__ int s_last;
+
+    const int row = blockIdx.x;
+    const int chunk = blockIdx.y;
+    const int nchunks = gridDim.y;
+    const float lo = (float)(1.0 - (double)p.eps_clip_low);
+    const float hi = (float)(1.0 + (double)p.eps_clip_high);
+    const int64_t rbase = (int64_t)row * R;
+
+    float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    auto one = [&](int64_t i, float& g) {
+        const float m = mask ? mask[i] : 1.f;
+        TokenOut t = ppo_token(lp[i], old[i], adv[i], lo, hi, p.clip_ratio_c, p.dual_clip);
+        acc[0] += t.loss * m;
+        acc[1] += m;
+        acc[2] += t.clip * m;
+        if (p.use_kl_loss) acc[3] += (approx_kl(lp[i], ref[i], p.kl_type) * m) * m;
+        if (ent) acc[4] += ent[i] * m;
+        g = t.dldlp * m;
+    };
+    const int c0 = chunk * kChunk + threadIdx.x * 4;
+    if (vec4 && c0 + 3 < R) {
+        const int64_t i = rbase + c0;
+        float4 l4 = *reinterpret_cast<const float4*>(lp + i);
+        float4 o4 = *reinterpret_cast<const float4*>(old + i);
+        float4 a4 = *reinterpret_cast<const float4*>(adv + i);
+        float4 m4 = mask ? *reinterpret_cast<const float4*>(mask + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+        float4 r4 = p.use_kl_loss ? *reinterpret_cast<const float4*>(ref + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 e4 = ent ? *reinterpret_cast<const float4*>(ent + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float L[4] = {l4.x, l4.y, l4.z, l4.w}, O[4] = {o4.x, o4.y, o4.z, o4.w};
+        const float A[4] = {a4.x, a4.y, a4.z, a4.w}, M[4] = {m4.x, m4.y, m4.z, m4.w};
+        const float RF[4] = {r4.x, r4.y, r4.z, r4.w}, E[4] = {e4.x, e4.y, e4.z, e4.w};
+        float g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            TokenOut t = ppo_token(L[k], O[k], A[k], lo, hi, p.clip_ratio_c, p.dual_clip);
+            acc[0] += t.loss * M[k];
+            acc[1] += M[k];
+            acc[2] += t.clip * M[k];
+            if (p.use_kl_loss) acc[3] += (approx_kl(L[k], RF[k], p.kl_type) * M[k]) * M[k];
+            acc[4] += E[k] * M[k];
+            g[k] = t.dldlp * M[k];
+        }
+        *reinterpret_cast<float4*>(gnum + i) = make_float4(g[0], g[1], g[2], g[3]);
+    } else if (!vec4) {
+        for (int c = chunk * kChunk + threadIdx.x; c < R && c < (chunk + 1) * kChunk; c += kThreads) {
+            float g;
+            one(rbase + c, g);
+            gnum[rbase + c] = g;
+        }
+    } else {  // vec4 layout but ragged tail (cannot happen when R % 4 == 0)
+        for (int c = c0; c < R && c < c0 + 4; ++c) {
+            float g;
+            one(rbase + c, g);
+            gnum[rbase + c] = g;
+        }
+    }
+
+    block_sum<kWaves, kNP>(acc, s_red);
+    if (threadIdx.x == 0) {
+        float* dst = partials + ((int64_t)row * nchunks + chunk) * kNP;
+#pragma unroll
+        for (int k = 0; k < kNP; ++k) dst[k] = acc[k];
+    }
+    if (!arrive_last(counter, (unsigned)(n * nchunks), &s_last)) return;
+
+    // ---- epilogue: one block folds the n*nchunks partials ---------------------
+    // tot: 0 sum l*m, 1 sum m, 2 sum clip*m, 3 sum_rows row-reduced loss (seq modes),
+    //      4 sum_rows kl_row, 5 sum ent*m
+    double tot[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = threadIdx.x; r < n; r += kThreads) {
+        double rs[kNP] = {0, 0, 0, 0, 0};
+        for (int c = 0; c < nchunks; ++c) {
+            const float* src = partials + ((int64_t)r * nchunks + c) * kNP;
+#pragma unroll
+            for (int k = 0; k < kNP; ++k) rs[k] += (double)src[k];
+        }
+        const double mrow = rs[1] > 1.0 ? rs[1] : 1.0;  // mask.sum(-1).clamp(min=1)
+        tot[0] += rs[0];
+        tot[1] += rs[1];
+        tot[2] += rs[2];
+        tot[4] += rs[3] / mrow;
+        tot[5] += rs[4];
+        if (p.loss_reduction == 1) {
+            tot[3] += rs[0] / mrow;
+            row_scale[r] = (float)(1.0 / ((double)n * mrow));
+        } else if (p.loss_reduction == 2) {
+            tot[3] += rs[0] / (double)p.max_seq_len;
+            row_scale[r] = (float)(1.0 / ((double)n * (double)p.max_seq_len));
+        }
+    }
+    block_sum_d<kWaves, 6>(tot, s_redd);
+    const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
+    if (p.loss_reduction == 0) {
+        const float sc = (float)(1.0 / msum);
+        for (int r = threadIdx.x; r < n; r += kThreads) row_scale[r] = sc;
+    }
+    if (threadIdx.x == 0) {
+        float pg;
+        if (p.loss_reduction == 0) pg = (float)(tot[0] / msum);
+        else pg = (float)(tot[3] / (double)n);
+        const float clip_ratio = (float)(tot[2] / msum);
+        const float kl = p.use_kl_loss ? (float)(tot[4] / (double)n) : 0.f;
+        const float entropy = (float)(tot[5] / msum);
+        float final_loss = pg + kl * p.kl_loss_coef;
+        if (p.use_entropy_loss) final_loss = final_loss - entropy * p.entropy_loss_coef;
+        loss_out[0] = final_loss;
+        metrics[SKYRL_M_FINAL_LOSS] = final_loss;
+        metrics[SKYRL_M_POLICY_LOSS] = pg;
+        metrics[SKYRL_M_ENTROPY] = entropy;
+        metrics[SKYRL_M_KL] = kl;
+        metrics[SKYRL_M_CLIP_RATIO] = clip_ratio;
+        metrics[SKYRL_M_MASK_SUM] = (float)tot[1];
+        metrics[6] = 0.f;
+        metrics[7] = 0.f;
+    }
+    rearm(counter);
+}
+
+__global__ __launch_bounds__(kThreads) void ppo_loss_bwd_kernel(
+    const float* __restrict__ gout, const float* __restrict__ gnum, const float* __restrict__ row_scale,
+    const float* __restrict__ mask, const float* __restrict__ metrics, int R, int use_ent, float ent_coef,
+    bool vec4, float* __restrict__ glp, float* __restrict__ gent) {
+    const int row = blockIdx.x;
+    const float g = gout[0];
+    const float s = g * row_scale[row];
+    float es = 0.f;
+    if (use_ent) {
+        const float ms = metrics[SKYRL_M_MASK_SUM];
+        es = -(g * ent_coef) / (ms > 1.f ? ms : 1.f);
+    }
+    const int64_t rbase = (int64_t)row * R;
+    const int c0 = blockIdx.y * kChunk + threadIdx.x * 4;
+    if (vec4) {
+        if (c0 + 3 < R) {
+            float4 u = *reinterpret_cast<const float4*>(gnum + rbase + c0);
+            *reinterpret_cast<float4*>(glp + rbase + c0) = make_float4(u.x * s, u.y * s, u.z * s, u.w * s);
+            if (use_ent) {
+                float4 m = mask ? *reinterpret_cast<const float4*>(mask + rbase + c0) : make_float4(1.f, 1.f, 1.f, 1.f);
+                *reinterpret_cast<float4*>(gent + rbase + c0) = make_float4(es * m.x, es * m.y, es * m.z, es * m.w);
+            }
+        }
+    } else {
+        for (int c = blockIdx.y * kChunk + threadIdx.x; c < R && c < (blockIdx.y + 1) * kChunk; c += kThreads) {
+            glp[rbase + c] = gnum[rbase + c] * s;
+            if (use_ent) gent[rbase + c] = es * (mask ? mask[rbase + c] : 1.f);
+        }
+    }
+}
+
+// ---- compute_approx_kl, elementwise ---------------------------------------------
+__global__ void approx_kl_kernel(const float* __restrict__ lp, const float* __restrict__ base,
+                                 const void* __restrict__ mask, int mask_dtype, int64_t n, int kl_type,
+                                 float* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float k = approx_kl(lp[i], base[i], kl_type);
+        if (mask) k = k * load_mask(mask, mask_dtype, i);
+        out[i] = k;
+    }
+}
+
+// ---- apply_reward_kl_penalty: one block per row + last-arriver metrics ---------
+__global__ __launch_bounds__(kThreads) void reward_kl_kernel(
+    const float* __restrict__ rewards, const float* __restrict__ lp, const float* __restrict__ base,
+    const float* __restrict__ mask, int N, int R, int kl_type, float coef, float* __restrict__ out,
+    float* __restrict__ metrics, float* __restrict__ partials, unsigned* __restrict__ counter) {
+    __shared__ float s_red[kWaves * 2];
+    __shared__ float s_max[kWaves];
+    __shared__ double s_redd[kWaves * 2];
+    __shared__ int s_last;
+    const int row = blockIdx.x;
+    const int64_t rbase = (int64_t)row * R;
+    const float c = coef > 0.f ? coef : 0.f;  // max(0, kl_loss_coef)
+    float acc[2] = {0.f, 0.f};                // sum (kl*m)*m, sum m
+    float kmax = 0.f;                         // max |kl*m|
+    for (int t = threadIdx.x; t < R; t += kThreads) {
+        const float m = mask[rbase + t];
+        const float k = approx_kl(lp[rbase + t], base[rbase + t], kl_type) * m;
+        out[rbase + t] = rewards[rbase + t] - k * c;
+        acc[0] += k * m;
+        acc[1] += m;
+        kmax = fmaxf(kmax, fabsf(k));
+    }
+    kmax = wave_max(kmax);
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x / kWave] = kmax;
+    block_sum<kWaves, 2>(acc, s_red);  // contains __syncthreads
+    if (threadIdx.x == 0) {
+        float mx = s_max[0];
+        for (int j = 1; j < kWaves; ++j) mx = fmaxf(mx, s_max[j]);
+        partials[row * 2 + 0] = acc[0] / (acc[1] > 1.f ? acc[1] : 1.f);
+        partials[row * 2 + 1] = mx;
+    }
+    if (!arrive_last(counter, (unsigned)N, &s_last)) return;
+    double tot[2] = {0.0, 0.0};
+    for (int r = threadIdx.x; r < N; r += kThreads) {
+        tot[0] += (double)partials[r * 2 + 0];
+        tot[1] += (double)partials[r * 2 + 1];
+    }
+    block_sum_d<kWaves, 2>(tot, s_redd);
+    if (threadIdx.x == 0) {
+        metrics[0] = (float)(tot[0] / (double)N);
+        metrics[1] = (float)(tot[1] / (double)N);
+    }
+    rearm(counter);
+}
+
+// ---- ppo_critic_loss -----------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void critic_loss_kernel(
+    const float* __restrict__ V, const float* __restrict__ Vold, const float* __restrict__ ret,
+    const float* __restrict__ mask, int n, int R, float vclip, float* __restrict__ loss_out,
+    float* __restrict__ clipfrac_out, float* __restrict__ gv, float* __restrict__ partials,
+    unsigned* __restrict__ counter) {
+    __shared__ float s_red[kWaves * 3];
+    __shared__ double s_redd[kWaves * 3];
+    __shared__ int s_last;
+    const int row = blockIdx.x;
+    const int64_t rbase = (int64_t)row * R;
+    const bool clip = vclip >= 0.f;
+    float acc[3] = {0.f, 0.f, 0.f};  // sum loss*m, sum m, sum (s1>s2)*m
+    for (int t = threadIdx.x; t < R; t += kThreads) {
+        const int64_t i = rbase + t;
+        const float m = mask ? mask[i] : 1.f;
+        const float v = V[i], r = ret[i];
+        float l, d, cf = 0.f;
+        const float s2 = (v - r) * (v - r);
+        const float ds2 = 2.f * (v - r);
+        if (clip) {
+            const float dv = v - Vold[i];
+            const float vc = Vold[i] + clampf(dv, -vclip, vclip);
+            const float s1 = (vc - r) * (vc - r);
+            const float ds1 = (dv >= -vclip && dv <= vclip) ? 2.f * (vc - r) : 0.f;
+            if (s1 > s2) { l = s1; d = ds1; cf = 1.f; }
+            else if (s2 > s1) { l = s2; d = ds2; }
+            else { l = s1; d = 0.5f * (ds1 + ds2); }
+        } else {
+            l = s2;
+            d = ds2;
+        }
+        acc[0] += l * m;
+        acc[1] += m;
+        acc[2] += cf * m;
+        gv[i] = d * m;  // scaled by 0.5/(n*max(row m,1)) below
+    }
+    block_sum<kWaves, 3>(acc, s_red);
+    const float mrow = acc[1] > 1.f ? acc[1] : 1.f;
+    const float sc = 0.5f / ((float)n * mrow);
+    for (int t = threadIdx.x; t < R; t += kThreads) gv[rbase + t] *= sc;
+    if (threadIdx.x == 0) {
+        partials[row * 3 + 0] = acc[0] / mrow;
+        partials[row * 3 + 1] = acc[2];
+        partials[row * 3 + 2] = acc[1];
+    }
+    if (!arrive_last(counter, (unsigned)n, &s_last)) return;
+    double tot[3] = {0.0, 0.0, 0.0};
+    for (int r = threadIdx.x; r < n; r += kThreads) {
+        tot[0] += (double)partials[r * 3 + 0];
+        tot[1] += (double)partials[r * 3 + 1];
+        tot[2] += (double)partials[r * 3 + 2];
+    }
+    block_sum_d<kWaves, 3>(tot, s_redd);
+    if (threadIdx.x == 0) {
+        loss_out[0] = 0.5f * (float)(tot[0] / (double)n);
+        clipfrac_out[0] = clip ? (float)(tot[1] / (tot[2] > 1.0 ? tot[2] : 1.0)) : 0.f;
+    }
+    rearm(counter);
+}
+
+inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16) == 0; }
+
+}  // namespace
+}  // namespace skyrl
+
+using namespace skyrl;
+
+extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
+    const size_t nchunks = (size_t)((R + kChunk - 1) / kChunk);
+    const size_t parts = (size_t)n * (nchunks ? nchunks : 1) * kNP * sizeof(float);
+    return 256 + ((parts + 255) / 256) * 256;  // [counter | pad][partials]
+}
+
+extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const float* advantages,
+                                  const float* loss_mask, const float* ref_log_probs, const float* entropy,
+                                  int32_t n, int32_t R, const skyrl_ppo_params* params, float* loss_out,
+                                  float* metrics_out, float* grad_num, float* row_scale, void* workspace,
+                                  void* stream) {
+    SKYRL_REQUIRE(params, "ppo_loss_fwd: params is null");
+    SKYRL_REQUIRE(n > 0 && R > 0, "ppo_loss_fwd: empty batch");
+    SKYRL_REQUIRE(log_probs && old_log_probs && advantages && loss_out && metrics_out && grad_num && row_scale &&
+                      workspace,
+                  "ppo_loss_fwd: null pointer");
+    SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "ppo_loss_fwd: use_kl_loss needs ref_log_probs");
+    SKYRL_REQUIRE(params->loss_reduction >= 0 && params->loss_reduction <= 2, "ppo_loss_fwd: bad loss_reduction");
+    SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
+                  "ppo_loss_fwd: seq_mean_token_sum_norm needs max_seq_len");
+    SKYRL_REQUIRE(params->kl_type >= 0 && params->kl_type <= 3, "ppo_loss_fwd: bad kl_type");
+    const bool vec4 = (R % 4) == 0 && aligned16(log_probs) && aligned16(old_log_probs) && aligned16(advantages) &&
+                      aligned16(loss_mask) && aligned16(ref_log_probs) && aligned16(entropy) && aligned16(grad_num);
+    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
+    float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
+    dim3 grid(n, (R + kChunk - 1) / kChunk);
+    hipLaunchKernelGGL(ppo_loss_fwd_kernel, grid, dim3(kThreads), 0, as_stream(stream), log_probs, old_log_probs,
+                       advantages, loss_mask, ref_log_probs, entropy, n, R, *params, vec4, loss_out, metrics_out,
+                       grad_num, row_scale, partials, counter);
+    return check_launch("ppo_loss_fwd_kernel");
+}
+
+extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, const float* grad_num, const float* row_scale,
+                                  const float* loss_mask, const float* metrics, int32_t n, int32_t R,
+                                  const skyrl_ppo_params* params, float* grad_logp, float* grad_entropy,
+                                  void* stream) {
+    SKYRL_REQUIRE(params && grad_out && grad_num && row_scale && grad_logp && metrics, "ppo_loss_bwd: null pointer");
+    SKYRL_REQUIRE(n > 0 && R > 0, "ppo_loss_bwd: empty batch");
+    const int use_ent = params->use_entropy_loss && grad_entropy != nullptr;
+    const bool vec4 = (R % 4) == 0 && aligned16(grad_num) && aligned16(grad_logp) && aligned16(loss_mask) &&
+                      aligned16(grad_entropy);
+    dim3 grid(n, (R + kChunk - 1) / kChunk);
+    hipLaunchKernelGGL(ppo_loss_bwd_kernel, grid, dim3(kThreads), 0, as_stream(stream), grad_out, grad_num, row_scale,
+                       loss_mask, metrics, R, use_ent, params->entropy_loss_coef, vec4, grad_logp, grad_entropy);
+    return check_launch("ppo_loss_bwd_kernel");
+}
+
+extern "C" int skyrl_approx_kl(const float* log_probs, const float* log_probs_base, const void* loss_mask,
+                               int mask_dtype, int64_t n, int32_t kl_type, float* kl_out, void* stream) {
+    SKYRL_REQUIRE(kl_type >= 0 && kl_type <= 3, "approx_kl: bad kl_type");
+    if (n == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(log_probs && log_probs_base && kl_out, "approx_kl: null pointer");
+    const int threads = 256;
+    int64_t blocks = (n + threads - 1) / threads;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(approx_kl_kernel, dim3((unsigned)blocks), dim3(threads), 0, as_stream(stream), log_probs,
+                       log_probs_base, loss_mask, mask_dtype, n, kl_type, kl_out);
+    return check_launch("approx_kl_kernel");
+}
+
+extern "C" size_t skyrl_reward_kl_workspace_bytes(int32_t N) {
+    return 256 + (((size_t)N * 2 * sizeof(float) + 255) / 256) * 256;
+}
+
+extern "C" int skyrl_reward_kl_penalty(const float* rewards, const float* action_log_probs,
+                                          const float* base_action_log_probs, const float* loss_mask, int32_t N,
+                                          int32_t R, int32_t kl_type, float kl_coef, float* rewards_out,
+                                          float* metrics_out, void* workspace, void* stream) {
+    SKYRL_REQUIRE(N > 0 && R > 0, "reward_kl_penalty: empty batch");
+    SKYRL_REQUIRE(rewards && action_log_probs && base_action_log_probs && loss_mask && rewards_out && metrics_out &&
+                      workspace,
+                  "reward_kl_penalty: null pointer");
+    SKYRL_REQUIRE(kl_type >= 0 && kl_type <= 3, "reward_kl_penalty: bad kl_type");
+    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
+    float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
+    hipLaunchKernelGGL(reward_kl_kernel, dim3(N), dim3(kThreads), 0, as_stream(stream), rewards, action_log_probs,
+                       base_action_log_probs, loss_mask, N, R, kl_type, kl_coef, rewards_out, metrics_out, partials,
+                       counter);
+    return check_launch("reward_kl_kernel");
+}
+
+extern "C" size_t skyrl_critic_loss_workspace_bytes(int32_t n, int32_t R) {
+    (void)R;
+    return 256 + (((size_t)n * 3 * sizeof(float) + 255) / 256) * 256;
+}
+
+extern "C" int skyrl_critic_loss_fwd(const float* values, const float* old_values, const float* returns,
+                                     const float* loss_mask, int32_t n, int32_t R, float value_clip, float* loss_out,
+                                     float* clipfrac_out, float* grad_values, void* workspace, void* stream) {
+    SKYRL_REQUIRE(n > 0 && R > 0, "critic_loss: empty batch");
+    SKYRL_REQUIRE(values && returns && loss_out && clipfrac_out && grad_values && workspace,
+                  "critic_loss: null pointer");
+    SKYRL_REQUIRE(value_clip < 0.f || old_values, "critic_loss: value_clip needs old_values");
+    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
+    float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(n), dim3(kThreads), 0, as_stream(stream), values, old_values, returns,
+                       loss_mask, n, R, value_clip, loss_out, clipfrac_out, grad_values, partials, counter);
+    return check_launch("critic_loss_kernel");
+}

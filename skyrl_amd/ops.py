@@ -1,0 +1,506 @@
+"""torch-facing wrappers of the HIP hot path (device tensors in, device tensors out).
+
+Each function validates shapes/dtypes/devices on the host, takes the current HIP stream,
+and calls one C-ABI entry point (skyrl_amd._ffi). Nothing here computes on the CPU: a
+CPU tensor, a missing GPU or a missing library is an error, never a fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Sequence, Tuple
+
+import torch
+
+from . import _ffi
+from ._ffi import BF16, F32, I32, I64, U8
+
+_MASK_DTYPES = {torch.float32: F32, torch.int64: I64, torch.int32: I32, torch.bool: U8, torch.uint8: U8}
+KL_TYPES = {"k1": 0, "abs": 1, "k2": 2, "k3": 3}
+LOSS_REDUCTIONS = {"token_mean": 0, "sequence_mean": 1, "seq_mean_token_sum_norm": 2}
+
+
+# ---------------------------------------------------------------------------- plumbing
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_gpu(*tensors: Optional[torch.Tensor]) -> torch.device:
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "skyrl_amd HIP path requires device tensors (got a tensor on "
+                f"{t.device}); there is no CPU fallback"
+            )
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} vs {t.device}")
+    if dev is None:
+        raise RuntimeError("no device tensor given")
+    return dev
+
+
+def _f32c(t: Optional[torch.Tensor], name: str) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    return t.contiguous()
+
+
+class _Workspaces:
+    """Zero-initialised scratch per (device, stream, kind); grows, never shrinks.
+
+    Kernels with an in-launch last-arriver counter (ppo loss, critic loss, reward KL,
+    sampler) rely on the counter words being zero at allocation; the kernel re-arms them.
+    """
+
+    def __init__(self):
+        self._bufs: Dict[Tuple, torch.Tensor] = {}
+
+    def get(self, device: torch.device, kind: str, nbytes: int) -> torch.Tensor:
+        stream = torch.cuda.current_stream(device).cuda_stream
+        key = (device.index, stream, kind)
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            nbytes = max(int(nbytes), 256)
+            buf = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+            self._bufs[key] = buf
+        return buf
+
+
+WORKSPACES = _Workspaces()
+
+
+# ---------------------------------------------------------------------------- a4 GRPO
+def groups_from_index(index: Sequence) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    """Map the reference's per-row uid list (`index`) to CSR groups (host, O(N)).
+
+    Mirrors the grouping of compute_grpo_outcome_advantage (ppo_utils.py:1160-1163):
+    rows sharing a uid form one group, in first-appearance order.
+    """
+    order: Dict = {}
+    members = []
+    for i, uid in enumerate(index):
+        key = uid.item() if hasattr(uid, "item") else uid
+        g = order.get(key)
+        if g is None:
+            g = order[key] = len(members)
+            members.append([])
+        members[g].append(i)
+    off = [0]
+    rows = []
+    for m in members:
+        rows.extend(m)
+        off.append(len(rows))
+    return torch.tensor(off, dtype=torch.int32), torch.tensor(rows, dtype=torch.int32), len(members)
+
+
+def grpo_advantage(
+    token_level_rewards: torch.Tensor,
+    response_mask: torch.Tensor,
+    group_off: torch.Tensor,
+    group_rows: torch.Tensor,
+    num_groups: int,
+    epsilon: float = 1e-6,
+    norm_by_std: bool = True,
+    scores_out: Optional[torch.Tensor] = None,
+) -> torch.Tensor:
+    dev = _require_gpu(token_level_rewards, response_mask)
+    rew = _f32c(token_level_rewards, "token_level_rewards")
+    if rew.dim() != 2 or response_mask.shape != rew.shape:
+        raise ValueError(f"rewards {tuple(rew.shape)} and response_mask {tuple(response_mask.shape)} must match [N,R]")
+    mask = response_mask.contiguous()
+    if mask.dtype not in _MASK_DTYPES:
+        raise TypeError(f"unsupported response_mask dtype {mask.dtype}")
+    N, R = rew.shape
+    goff = group_off.to(device=dev, dtype=torch.int32)
+    grows = group_rows.to(device=dev, dtype=torch.int32)
+    out = torch.empty((N, R), dtype=torch.float32, device=dev)
+    _ffi.call(
+        "skyrl_grpo_advantage", _ptr(rew), _ptr(mask), _MASK_DTYPES[mask.dtype], _ptr(goff), _ptr(grows),
+        int(num_groups), N, R, float(epsilon), int(bool(norm_by_std)), _ptr(out), _ptr(scores_out), _stream(dev),
+    )
+    return out
+
+
+# ---------------------------------------------------------------------------- a5 GAE
+def gae_advantage_return(
+    token_level_rewards: torch.Tensor,
+    values: torch.Tensor,
+    response_mask: torch.Tensor,
+    gamma: float,
+    lambd: float,
+    check: bool = True,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    dev = _require_gpu(token_level_rewards, values, response_mask)
+    rew = _f32c(token_level_rewards, "token_level_rewards")
+    val = _f32c(values, "values")
+    mask = response_mask.contiguous()
+    if mask.dtype not in _MASK_DTYPES:
+        raise TypeError(f"unsupported response_mask dtype {mask.dtype}")
+    if rew.dim() != 2 or val.shape != rew.shape or mask.shape != rew.shape:
+        raise ValueError("rewards, values and response_mask must all be [N,R]")
+    N, R = rew.shape
+    adv = torch.empty_like(rew)
+    ret = torch.empty_like(rew)
+    ws = WORKSPACES.get(dev, "gae", _ffi.query("skyrl_gae_workspace_bytes", N))
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    _ffi.call(
+        "skyrl_gae_advantage_return", _ptr(rew), _ptr(val), _ptr(mask), _MASK_DTYPES[mask.dtype], N, R,
+        float(gamma), float(lambd), _ptr(adv), _ptr(ret), _ptr(ws), _ptr(status), _stream(dev),
+    )
+    if check:  # the reference raises from masked_var (ppo_utils.py:157-163); one sync
+        st = int(status.item())
+        if st == 1:
+            raise ValueError("At least one element in the mask has to be 1.")
+        if st == 2:
+            raise ValueError("The sum of the mask is one, which can cause a division by zero.")
+    return adv, ret
+
+
+# ---------------------------------------------------------------------------- a6 KL
+def approx_kl(
+    log_probs: torch.Tensor,
+    log_probs_base: torch.Tensor,
+    loss_mask: Optional[torch.Tensor] = None,
+    kl_estimator_type: str = "k3",
+) -> torch.Tensor:
+    if kl_estimator_type not in KL_TYPES:
+        raise ValueError(f"Invalid KL estimator type: {kl_estimator_type}")
+    dev = _require_gpu(log_probs, log_probs_base, loss_mask)
+    lp = _f32c(log_probs, "log_probs")
+    base = _f32c(log_probs_base, "log_probs_base")
+    if base.shape != lp.shape:
+        raise ValueError("log_probs and log_probs_base must have the same shape")
+    mask = None
+    mdt = F32
+    if loss_mask is not None:
+        mask = loss_mask.contiguous()
+        if mask.shape != lp.shape:
+            mask = mask.expand_as(lp).contiguous()
+        mdt = _MASK_DTYPES[mask.dtype]
+    out = torch.empty_like(lp)
+    _ffi.call(
+        "skyrl_approx_kl", _ptr(lp), _ptr(base), _ptr(mask), mdt, lp.numel(), KL_TYPES[kl_estimator_type],
+        _ptr(out), _stream(dev),
+    )
+    return out
+
+
+def reward_kl_penalty(
+    rewards: torch.Tensor,
+    action_log_probs: torch.Tensor,
+    base_action_log_probs: torch.Tensor,
+    loss_mask: torch.Tensor,
+    kl_estimator_type: str,
+    kl_coef: float,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Returns (new rewards, device tensor [avg_kl, avg_kl_max])."""
+    dev = _require_gpu(rewards, action_log_probs, base_action_log_probs, loss_mask)
+    rew = _f32c(rewards, "rewards")
+    lp = _f32c(action_log_probs, "action_log_probs")
+    base = _f32c(base_action_log_probs, "base_action_log_probs")
+    mask = loss_mask.to(torch.float32).contiguous()
+    N, R = rew.shape
+    out = torch.empty_like(rew)
+    metrics = torch.empty(2, dtype=torch.float32, device=dev)
+    ws = WORKSPACES.get(dev, "reward_kl", _ffi.query("skyrl_reward_kl_workspace_bytes", N))
+    _ffi.call(
+        "skyrl_reward_kl_penalty", _ptr(rew), _ptr(lp), _ptr(base), _ptr(mask), N, R,
+        KL_TYPES[kl_estimator_type], float(kl_coef), _ptr(out), _ptr(metrics), _ptr(ws), _stream(dev),
+    )
+    return out, metrics
+
+
+# ---------------------------------------------------------------------------- a7 PPO loss
+def make_ppo_params(
+    *,
+    eps_clip_low: float = 0.2,
+    eps_clip_high: float = 0.2,
+    clip_ratio_c: float = 3.0,
+    policy_loss_type: str = "regular",
+    loss_reduction: str = "token_mean",
+    max_seq_len: Optional[float] = None,
+    use_kl_loss: bool = False,
+    kl_estimator_type: str = "k3",
+    kl_loss_coef: float = 0.0,
+    use_entropy_loss: bool = False,
+    entropy_loss_coef: float = 0.0,
+    has_entropy: bool = False,
+) -> _ffi.PPOParams:
+    if policy_loss_type not in ("regular", "dual_clip"):
+        raise ValueError(f"HIP PPO loss supports 'regular' and 'dual_clip', got {policy_loss_type!r}")
+    if loss_reduction not in LOSS_REDUCTIONS:
+        raise ValueError(
+            "loss_reduction must be either 'token_mean', 'sequence_mean', or 'seq_mean_token_sum_norm'"
+        )
+    if loss_reduction == "seq_mean_token_sum_norm" and max_seq_len is None:
+        raise AssertionError("max_seq_len must be provided for seq_mean_token_sum_norm loss reduction")
+    if kl_estimator_type not in KL_TYPES:
+        raise ValueError(f"Invalid KL estimator type: {kl_estimator_type}")
+    return _ffi.PPOParams(
+        float(eps_clip_low), float(eps_clip_high), float(clip_ratio_c), int(policy_loss_type == "dual_clip"),
+        LOSS_REDUCTIONS[loss_reduction], float(max_seq_len or 0.0), int(bool(use_kl_loss)),
+        KL_TYPES[kl_estimator_type], float(kl_loss_coef), int(bool(use_entropy_loss)), float(entropy_loss_coef),
+        int(bool(has_entropy)),
+    )
+
+
+class PPOLossFunction(torch.autograd.Function):
+    """Fused policy loss (+KL(ref) +entropy term) with a HIP forward and backward.
+
+    forward returns (loss 0-d, metrics f32[8] device). Gradients flow to log_probs and,
+    when params.use_entropy_loss, to entropy. The KL term has no gradient (reference:
+    compute_approx_kl is @torch.no_grad(), ppo_utils.py:87).
+    """
+
+    @staticmethod
+    def forward(ctx, log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params):
+        dev = _require_gpu(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy)
+        lp = _f32c(log_probs.detach(), "log_probs")
+        old = _f32c(old_log_probs.detach(), "old_log_probs")
+        adv = _f32c(advantages.detach(), "advantages")
+        mask = None if loss_mask is None else loss_mask.detach().to(torch.float32).contiguous()
+        ref = None if ref_log_probs is None else _f32c(ref_log_probs.detach(), "ref_log_probs")
+        ent = None if entropy is None else _f32c(entropy.detach(), "entropy")
+        if lp.dim() != 2:
+            raise ValueError(f"log_probs must be [n,R], got {tuple(lp.shape)}")
+        for name, t in (("old_log_probs", old), ("advantages", adv), ("loss_mask", mask), ("ref", ref), ("entropy", ent)):
+            if t is not None and t.shape != lp.shape:
+                raise ValueError(f"{name} shape {tuple(t.shape)} != log_probs shape {tuple(lp.shape)}")
+        n, R = lp.shape
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
+        gnum = torch.empty_like(lp)
+        row_scale = torch.empty(n, dtype=torch.float32, device=dev)
+        ws = WORKSPACES.get(dev, "ppo", _ffi.query("skyrl_ppo_loss_workspace_bytes", n, R))
+        _ffi.call(
+            "skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), _ptr(ent), n, R,
+            ctypes.byref(params), _ptr(loss), _ptr(metrics), _ptr(gnum), _ptr(row_scale), _ptr(ws), _stream(dev),
+        )
+        ctx.params = params
+        ctx.has_entropy = entropy is not None
+        ctx.save_for_backward(gnum, row_scale, mask, metrics)
+        ctx.mark_non_differentiable(metrics)
+        return loss, metrics
+
+    @staticmethod
+    def backward(ctx, grad_loss, grad_metrics):
+        gnum, row_scale, mask, metrics = ctx.saved_tensors
+        params = ctx.params
+        dev = gnum.device
+        n, R = gnum.shape
+        g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
+        glp = torch.empty_like(gnum)
+        want_ent = bool(params.use_entropy_loss) and ctx.has_entropy and ctx.needs_input_grad[5]
+        gent = torch.empty_like(gnum) if want_ent else None
+        _ffi.call(
+            "skyrl_ppo_loss_bwd", _ptr(g), _ptr(gnum), _ptr(row_scale), _ptr(mask), _ptr(metrics), n, R,
+            ctypes.byref(params), _ptr(glp), _ptr(gent), _stream(dev),
+        )
+        return glp, None, None, None, None, gent, None
+
+
+def ppo_loss(log_probs, old_log_probs, advantages, loss_mask, params, ref_log_probs=None, entropy=None):
+    """Fused loss; returns (loss 0-d tensor, metrics device tensor [8])."""
+    return PPOLossFunction.apply(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params)
+
+
+# ---------------------------------------------------------------------------- a8 critic loss
+class CriticLossFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, values, old_values, returns, loss_mask, value_clip):
+        dev = _require_gpu(values, old_values, returns, loss_mask)
+        v = _f32c(values.detach(), "values")
+        ov = None if old_values is None else _f32c(old_values.detach(), "old_values")
+        ret = _f32c(returns.detach(), "returns")
+        mask = None if loss_mask is None else loss_mask.detach().to(torch.float32).contiguous()
+        n, R = v.shape
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        clipfrac = torch.empty(1, dtype=torch.float32, device=dev)
+        gv = torch.empty_like(v)
+        ws = WORKSPACES.get(dev, "critic", _ffi.query("skyrl_critic_loss_workspace_bytes", n, R))
+        vc = -1.0 if value_clip is None else float(value_clip)
+        _ffi.call(
+            "skyrl_critic_loss_fwd", _ptr(v), _ptr(ov), _ptr(ret), _ptr(mask), n, R, vc, _ptr(loss),
+            _ptr(clipfrac), _ptr(gv), _ptr(ws), _stream(dev),
+        )
+        ctx.save_for_backward(gv)
+        ctx.mark_non_differentiable(clipfrac)
+        return loss, clipfrac
+
+    @staticmethod
+    def backward(ctx, grad_loss, grad_clip):
+        (gv,) = ctx.saved_tensors
+        out = torch.empty_like(gv)
+        g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
+        _ffi.call("skyrl_scale_by_device_scalar", _ptr(g), _ptr(gv), _ptr(out), gv.numel(), _stream(gv.device))
+        return out, None, None, None, None
+
+
+# ---------------------------------------------------------------------------- a2/a3 logprob
+def _logits_view(logits: torch.Tensor):
+    """[nb, nt, V] (or [T, V]) with unit vocab stride -> (nb, nt, V, sb, st, dtype code)."""
+    if logits.dtype == torch.bfloat16:
+        dt = BF16
+    elif logits.dtype == torch.float32:
+        dt = F32
+    else:
+        raise TypeError(f"logits must be bf16 or f32, got {logits.dtype}")
+    if logits.dim() == 2:
+        logits = logits.unsqueeze(0)
+    if logits.dim() != 3:
+        raise ValueError(f"logits must be [nb, nt, V] or [T, V], got {tuple(logits.shape)}")
+    if logits.stride(2) != 1:
+        raise ValueError("logits must be contiguous along the vocab dimension")
+    nb, nt, V = logits.shape
+    return logits, nb, nt, V, logits.stride(0), logits.stride(1), dt
+
+
+def _labels_view(labels: torch.Tensor, nb: int, nt: int):
+    if labels.dtype != torch.int64:
+        labels = labels.to(torch.int64)
+    if labels.dim() == 1:
+        labels = labels.unsqueeze(0)
+    if tuple(labels.shape) != (nb, nt):
+        raise ValueError(f"labels shape {tuple(labels.shape)} != logits leading shape {(nb, nt)}")
+    return labels, labels.stride(0), labels.stride(1)
+
+
+class LogprobEntropyFunction(torch.autograd.Function):
+    """logits [nb,nt,V] (bf16/f32, any row strides) -> (logp f32 [nb,nt], entropy f32 [nb,nt])."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, temperature, compute_entropy):
+        dev = _require_gpu(logits, labels)
+        lg, nb, nt, V, sb, st, dt = _logits_view(logits.detach())
+        lab, lsb, lst = _labels_view(labels, nb, nt)
+        logp = torch.empty((nb, nt), dtype=torch.float32, device=dev)
+        ent = torch.empty((nb, nt), dtype=torch.float32, device=dev)
+        lse = torch.empty((nb, nt), dtype=torch.float32, device=dev)
+        _ffi.call(
+            "skyrl_logprob_fwd", _ptr(lg), dt, sb, st, nb, nt, V, _ptr(lab), lsb, lst, float(temperature),
+            _ptr(logp), _ptr(ent), _ptr(lse), _stream(dev),
+        )
+        ctx.temperature = float(temperature)
+        ctx.in_shape = logits.shape
+        ctx.save_for_backward(logits, lab, lse, ent)
+        if not compute_entropy:
+            ctx.mark_non_differentiable(ent)
+        if logits.dim() == 2:
+            return logp.squeeze(0), ent.squeeze(0)
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        logits, lab, lse, ent = ctx.saved_tensors
+        lg, nb, nt, V, sb, st, dt = _logits_view(logits.detach())
+        dev = lg.device
+        glp = (torch.zeros((nb, nt), dtype=torch.float32, device=dev) if g_logp is None
+               else g_logp.to(torch.float32).reshape(nb, nt).contiguous())
+        gent = None if g_ent is None else g_ent.to(torch.float32).reshape(nb, nt).contiguous()
+        dx = torch.empty((nb, nt, V), dtype=lg.dtype, device=dev)
+        _ffi.call(
+            "skyrl_logprob_bwd", _ptr(lg), dt, sb, st, nb, nt, V, _ptr(lab), lab.stride(0), lab.stride(1),
+            ctx.temperature, _ptr(lse), _ptr(ent), _ptr(glp), _ptr(gent), _ptr(dx), _stream(dev),
+        )
+        return dx.reshape(ctx.in_shape), None, None, None
+
+
+def logprobs_and_entropy(logits, labels, temperature: float = 1.0, compute_entropy: bool = True):
+    return LogprobEntropyFunction.apply(logits, labels, temperature, compute_entropy)
+
+
+# ---------------------------------------------------------------------------- a1 sampler
+def sample(
+    logits: torch.Tensor,
+    *,
+    temperature: float = 1.0,
+    top_k: int = -1,
+    min_p: float = 0.0,
+    seed: int = 0,
+    seq_ids: Optional[torch.Tensor] = None,
+    step: int = 0,
+    want_logprobs: bool = True,
+    tokens_out: Optional[torch.Tensor] = None,
+    logp_out: Optional[torch.Tensor] = None,
+) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """One decode step over logits [nseq, V] -> (tokens int32 [nseq], logprob f32 [nseq])."""
+    dev = _require_gpu(logits, seq_ids)
+    if logits.dim() != 2 or logits.stride(1) != 1:
+        raise ValueError("logits must be [nseq, V] with unit vocab stride")
+    dt = BF16 if logits.dtype == torch.bfloat16 else (F32 if logits.dtype == torch.float32 else None)
+    if dt is None:
+        raise TypeError(f"logits must be bf16 or f32, got {logits.dtype}")
+    nseq, V = logits.shape
+    ids = None if seq_ids is None else seq_ids.to(device=dev, dtype=torch.int64).contiguous()
+    tokens = tokens_out if tokens_out is not None else torch.empty(nseq, dtype=torch.int32, device=dev)
+    if tokens.dtype != torch.int32 or tokens.numel() != nseq or not tokens.is_contiguous():
+        raise ValueError("tokens_out must be a contiguous int32 tensor of nseq elements")
+    logp = logp_out if logp_out is not None else (
+        torch.empty(nseq, dtype=torch.float32, device=dev) if want_logprobs else None)
+    if logp is not None and (logp.dtype != torch.float32 or logp.numel() != nseq or not logp.is_contiguous()):
+        raise ValueError("logp_out must be a contiguous float32 tensor of nseq elements")
+    ws = WORKSPACES.get(dev, "sample", _ffi.query("skyrl_sample_workspace_bytes", nseq, V))
+    _ffi.call(
+        "skyrl_sample", _ptr(logits), dt, logits.stride(0), nseq, V, float(temperature), int(top_k), float(min_p),
+        ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), _ptr(ids), int(step), _ptr(tokens), _ptr(logp), _ptr(ws),
+        _stream(dev),
+    )
+    return tokens, logp
+
+
+# ---------------------------------------------------------------------------- a9 pack
+def pack_experience(
+    prompt_tokens: torch.Tensor, prompt_off: torch.Tensor,
+    response_tokens: torch.Tensor, response_off: torch.Tensor,
+    reward_vals: torch.Tensor, reward_off: torch.Tensor,
+    loss_mask_vals: torch.Tensor, loss_mask_off: torch.Tensor,
+    logprob_vals: Optional[torch.Tensor], logprob_off: Optional[torch.Tensor],
+    *, N: int, P: int, R: int, pad: int = 0, pad_token_id: int = 0,
+):
+    """Device CSR inputs -> (sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs)."""
+    dev = _require_gpu(prompt_tokens, response_tokens, reward_vals, loss_mask_vals)
+
+    def i64(t):
+        return t.to(device=dev, dtype=torch.int64).contiguous()
+
+    def f32(t):
+        return t.to(device=dev, dtype=torch.float32).contiguous()
+
+    keep = [i64(prompt_tokens), i64(prompt_off), i64(response_tokens), i64(response_off), f32(reward_vals),
+            i64(reward_off), f32(loss_mask_vals), i64(loss_mask_off)]
+    has_lp = logprob_vals is not None
+    if has_lp:
+        keep += [f32(logprob_vals), i64(logprob_off)]
+    ins = _ffi.PackInputs(*[t.data_ptr() for t in keep], *([None, None] if not has_lp else []))
+    Np = N + pad
+    S = P + R
+    seq = torch.empty((Np, S), dtype=torch.int64, device=dev)
+    att = torch.empty((Np, S), dtype=torch.int64, device=dev)
+    rmask = torch.empty((Np, R), dtype=torch.int64, device=dev)
+    rew = torch.empty((Np, R), dtype=torch.float32, device=dev)
+    lmask = torch.empty((Np, R), dtype=torch.float32, device=dev)
+    rlp = torch.empty((Np, R), dtype=torch.float32, device=dev) if has_lp else None
+    _ffi.call(
+        "skyrl_pack_experience", ctypes.byref(ins), N, pad, P, R, int(pad_token_id), _ptr(seq), _ptr(att),
+        _ptr(rmask), _ptr(rew), _ptr(lmask), _ptr(rlp), _stream(dev),
+    )
+    return seq, att, rmask, rew, lmask, rlp
+
+
+# ---------------------------------------------------------------------------- a12 helpers
+def scale_and_sumsq(flat_grad: torch.Tensor, scale: float, sumsq: torch.Tensor) -> None:
+    dev = _require_gpu(flat_grad, sumsq)
+    if flat_grad.dtype != torch.float32 or not flat_grad.is_contiguous():
+        raise TypeError("flat_grad must be a contiguous float32 bucket")
+    _ffi.call("skyrl_scale_and_sumsq", _ptr(flat_grad), flat_grad.numel(), float(scale), _ptr(sumsq), _stream(dev))

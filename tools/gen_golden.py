@@ -1,0 +1,427 @@
+"""Generate golden vectors for the hot path by running the REAL reference (build container only).
+
+Imports skyrl_train from /root/reference/skyrl-train (read-only; bytecode writing disabled)
+behind a stub shim for its uninstalled infra dependencies (ray, omegaconf, loguru, jaxtyping,
+torchdata, peft, flash_attn.bert_padding — none carries hot-path arithmetic; see
+SURVEY.md §8(c) / Appendix A), calls the reference functions on seeded inputs and writes
+small .npz fixtures (inputs + expected outputs, arrays only, no pickles) to tests/golden/.
+
+The reference never travels to the GPU box: only the .npz data does.
+
+    PYTHONDONTWRITEBYTECODE=1 python -B tools/gen_golden.py
+"""
+
+from __future__ import annotations
+
+import enum
+import importlib.machinery
+import os
+import sys
+import types
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+sys.dont_write_bytecode = True
+REF = "/root/reference/skyrl-train"
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+# ----------------------------------------------------------------------------- shim
+def install_shim():
+    import torch.utils.data as tud
+
+    if not hasattr(enum, "StrEnum"):
+        class StrEnum(str, enum.Enum):
+            def __str__(self):
+                return str(self.value)
+
+        enum.StrEnum = StrEnum
+
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        m.__spec__ = importlib.machinery.ModuleSpec(name, None)
+        sys.modules[name] = m
+        return m
+
+    class _Any:
+        def __init__(self, *a, **k):
+            pass
+
+        def __getitem__(self, k):
+            return self
+
+        def __call__(self, *a, **k):
+            return self
+
+        def __getattr__(self, k):
+            return _Any()
+
+    mod("jaxtyping", Float=_Any(), Integer=_Any())
+
+    class _Log:
+        def _emit(self, *a, **k):
+            pass
+
+        debug = info = warning = error = exception = critical = success = trace = log = _emit
+
+        def opt(self, *a, **k):
+            return self
+
+        def bind(self, *a, **k):
+            return self
+
+        def remove(self, *a, **k):
+            pass
+
+        def add(self, *a, **k):
+            return 0
+
+        def level(self, *a, **k):
+            return self
+
+    mod("loguru", logger=_Log())
+
+    class DictConfig(dict):
+        pass
+
+    class ListConfig(list):
+        pass
+
+    class OmegaConf:
+        to_container = staticmethod(lambda c, resolve=True: dict(c))
+        create = staticmethod(lambda x: DictConfig(x))
+
+        @staticmethod
+        def merge(*a):
+            d = {}
+            for x in a:
+                d.update(x)
+            return DictConfig(d)
+
+    mod("omegaconf", DictConfig=DictConfig, ListConfig=ListConfig, OmegaConf=OmegaConf)
+    ray = mod("ray", is_initialized=lambda: False, init=lambda *a, **k: None, shutdown=lambda *a, **k: None,
+              remote=lambda *a, **k: (a[0] if a and callable(a[0]) else (lambda f: f)),
+              get=lambda x: x, put=lambda x: x, ObjectRef=object, get_gpu_ids=lambda: [0])
+    mod("ray.actor", ActorHandle=object)
+    ray.util = mod("ray.util")
+    mod("ray.util.placement_group", placement_group=None, PlacementGroupSchedulingStrategy=None,
+        PlacementGroup=object, placement_group_table=None)
+    mod("ray.util.scheduling_strategies", PlacementGroupSchedulingStrategy=None, NodeAffinitySchedulingStrategy=None)
+    ray._private = mod("ray._private")
+    mod("ray._private.services", get_node_ip_address=lambda: "127.0.0.1")
+    mod("torchdata")
+    mod("torchdata.stateful_dataloader", StatefulDataLoader=tud.DataLoader)
+
+    class _LoraConfig:
+        def __init__(self, *a, **k):
+            pass
+
+    mod("peft", LoraConfig=_LoraConfig, TaskType=_Any(), get_peft_model=lambda m, c: m)
+    mod("peft.tuners")
+    mod("peft.tuners.lora", LoraLayer=type("LoraLayer", (), {}))
+    mod("flash_attn")
+    mod("flash_attn.bert_padding", pad_input=None, unpad_input=None)
+    sys.path.insert(0, REF)
+    sys.path.insert(0, "/root/reference/skyrl-gym")
+
+
+def save(name, **arrays):
+    os.makedirs(OUT, exist_ok=True)
+    clean = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu()
+            if v.dtype == torch.bfloat16:
+                v = v.view(torch.int16).numpy().view(np.uint16)
+                k = k + "__bf16"
+            else:
+                v = v.numpy()
+        clean[k] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **clean)
+    print(f"wrote {name}.npz ({', '.join(clean)})")
+
+
+# ----------------------------------------------------------------------------- cases
+def gen_grpo(pu):
+    g = torch.Generator().manual_seed(1234)
+    cases = []
+    # mixed: groups of 4, 4, 3, a singleton, a zero-variance group, pad rows
+    N, R = 20, 16
+    uids = ["0"] * 4 + ["1"] * 4 + ["2"] * 3 + ["solo"] + ["zv"] * 4 + ["pad0", "pad1", "0", "1"]
+    lens = torch.randint(1, R + 1, (N,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64)
+    rew = torch.zeros(N, R)
+    for i in range(N):
+        rew[i, lens[i] - 1] = float(torch.rand((), generator=g) < 0.4)
+    rew[:11] += torch.randn(11, R, generator=g) * 0.1 * mask[:11]
+    rew[12:16] = 0.0
+    rew[12:16, 0] = 1.0
+    cases.append(("grpo_mixed", rew, mask, uids))
+    # synthetic-like: 16 prompts x group 8, Bernoulli(0.3) at last token
+    N, R = 128, 64
+    lens = torch.randint(1, R + 1, (N,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64)
+    rew = torch.zeros(N, R)
+    hit = (torch.rand(N, generator=g) < 0.3).float()
+    rew[torch.arange(N), lens - 1] = hit
+    uids = [str(i // 8) for i in range(N)]
+    cases.append(("grpo_synth", rew, mask, uids))
+    for name, rew, mask, uids in cases:
+        out = {}
+        for nbs in (True, False):
+            adv, ret = pu.compute_grpo_outcome_advantage(
+                token_level_rewards=rew.clone(), response_mask=mask, index=np.array(uids), grpo_norm_by_std=nbs)
+            assert torch.equal(adv, ret)
+            out[f"adv_norm{int(nbs)}"] = adv
+        save(name, rewards=rew, response_mask=mask, uids=np.array(uids), **out)
+
+
+def gen_gae(pu):
+    g = torch.Generator().manual_seed(7)
+    N, R = 6, 40
+    lens = torch.randint(2, R + 1, (N,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.float32)
+    rew = torch.randn(N, R, generator=g) * mask
+    vals = torch.randn(N, R, generator=g)  # padded values are NOT zero: leak trap
+    out = {}
+    for tag, gamma, lambd in (("g1_l1", 1.0, 1.0), ("g099_l095", 0.99, 0.95), ("g05_l1", 0.5, 1.0)):
+        adv, ret = pu.compute_gae_advantage_return(token_level_rewards=rew, values=vals, response_mask=mask,
+                                                   gamma=gamma, lambd=lambd)
+        out[f"adv_{tag}"] = adv
+        out[f"ret_{tag}"] = ret
+    save("gae", rewards=rew, values=vals, response_mask=mask, **out)
+    # long rows (scan across several 256-step tiles)
+    N, R = 4, 700
+    lens = torch.tensor([700, 513, 256, 3])
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64)
+    rew = torch.randn(N, R, generator=g) * 0.1 * mask
+    vals = torch.randn(N, R, generator=g) * 0.1
+    adv, ret = pu.compute_gae_advantage_return(token_level_rewards=rew, values=vals, response_mask=mask,
+                                               gamma=0.99, lambd=0.95)
+    save("gae_long", rewards=rew, values=vals, response_mask=mask, adv=adv, ret=ret)
+
+
+def gen_kl(pu):
+    g = torch.Generator().manual_seed(11)
+    lp = torch.randn(8, 33, generator=g) - 2
+    base = lp + torch.randn(8, 33, generator=g) * 0.5
+    base[0, :4] = lp[0, :4] + torch.tensor([25.0, -25.0, 5.0, -5.0])  # clamp branches
+    mask = (torch.rand(8, 33, generator=g) < 0.8).float()
+    out = {}
+    for k in ("k1", "abs", "k2", "k3"):
+        out[f"kl_{k}_masked"] = pu.compute_approx_kl(lp, base, loss_mask=mask, kl_estimator_type=k)
+        out[f"kl_{k}"] = pu.compute_approx_kl(lp, base, loss_mask=None, kl_estimator_type=k)
+    save("kl", log_probs=lp, log_probs_base=base, loss_mask=mask, **out)
+
+
+def _ppo_inputs(g, n, R):
+    lens = torch.randint(1, R + 1, (n,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).float()
+    old = torch.randn(n, R, generator=g) * 0.5 - 2
+    lp = old + torch.randn(n, R, generator=g) * 0.3
+    lp[0, :3] = old[0, :3]                      # ratio == 1 exactly (min tie)
+    lp[1, :2] = old[1, :2] + torch.tensor([30.0, -30.0])  # safe_exp_delta clamp
+    adv = torch.randn(n, R, generator=g)
+    adv[2, :2] = 0.0
+    ref = lp + torch.randn(n, R, generator=g) * 0.2
+    ent = torch.rand(n, R, generator=g) * 3
+    return lp, old, adv, mask, ref, ent
+
+
+def gen_ppo(pu, cfgmod):
+    from skyrl_train.utils.torch_utils import masked_mean
+
+    g = torch.Generator().manual_seed(99)
+    n, R = 6, 37
+    lp, old, adv, mask, ref, ent = _ppo_inputs(g, n, R)
+    out = {}
+    for lt in ("regular", "dual_clip"):
+        for red in ("token_mean", "sequence_mean", "seq_mean_token_sum_norm"):
+            cfg = cfgmod.AlgorithmConfig(policy_loss_type=lt, loss_reduction=red, max_seq_len=50,
+                                         eps_clip_low=0.2, eps_clip_high=0.28, clip_ratio_c=3.0)
+            x = lp.clone().requires_grad_(True)
+            fn = pu.PolicyLossRegistry.get(lt)
+            loss, m = fn(x, old, adv, cfg, loss_mask=mask)
+            loss.backward()
+            tag = f"{lt}_{red}"
+            out[f"loss_{tag}"] = loss.detach()
+            out[f"clip_{tag}"] = np.float32(m["clip_ratio"])
+            out[f"grad_{tag}"] = x.grad
+    # worker.py:801-876 assembly from the reference's own functions
+    for use_ent in (False, True):
+        cfg = cfgmod.AlgorithmConfig(policy_loss_type="regular", loss_reduction="token_mean")
+        x = lp.clone().requires_grad_(True)
+        e = ent.clone().requires_grad_(use_ent)
+        pg, m = pu.PolicyLossRegistry.get("regular")(x, old, adv, cfg, loss_mask=mask)
+        with torch.set_grad_enabled(use_ent):
+            entropy = masked_mean(e, mask)
+        ent_term = entropy * 0.01 if use_ent else torch.tensor(0.0)
+        kl = pu.compute_approx_kl(x, ref, loss_mask=mask, kl_estimator_type="k3")
+        kl = masked_mean(kl, mask, dim=-1).mean()
+        final = pg + kl * 0.001 - ent_term
+        final.backward()
+        tag = f"asm_ent{int(use_ent)}"
+        out[f"final_{tag}"] = final.detach()
+        out[f"pg_{tag}"] = pg.detach()
+        out[f"kl_{tag}"] = kl.detach()
+        out[f"entropy_{tag}"] = entropy.detach()
+        out[f"clip_{tag}"] = np.float32(m["clip_ratio"])
+        out[f"grad_lp_{tag}"] = x.grad
+        if use_ent:
+            out[f"grad_ent_{tag}"] = e.grad
+    save("ppo", log_probs=lp, old_log_probs=old, advantages=adv, loss_mask=mask, ref_log_probs=ref, entropy=ent,
+         **out)
+
+
+def gen_critic(pu, cfgmod):
+    g = torch.Generator().manual_seed(5)
+    n, R = 5, 29
+    lens = torch.randint(1, R + 1, (n,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).float()
+    old = torch.randn(n, R, generator=g)
+    v = old + torch.randn(n, R, generator=g) * 0.4
+    ret = torch.randn(n, R, generator=g)
+    out = {}
+    for tag, vc in (("clip", 0.2), ("noclip", None)):
+        cfg = cfgmod.AlgorithmConfig(value_clip=vc)
+        x = v.clone().requires_grad_(True)
+        loss, cf = pu.ppo_critic_loss(x, old, ret, cfg, loss_mask=mask)
+        loss.backward()
+        out[f"loss_{tag}"] = loss.detach()
+        out[f"clipfrac_{tag}"] = np.float32(cf if cf is not None else -1.0)
+        out[f"grad_{tag}"] = x.grad
+    save("critic", values=v, old_values=old, returns=ret, loss_mask=mask, **out)
+
+
+def gen_logprob(tu):
+    g = torch.Generator().manual_seed(3)
+    out = {}
+    # fp32 logits, V not a multiple of the vector width
+    B, T, V = 3, 7, 1027
+    logits = torch.randn(B, T, V, generator=g) * 3
+    labels = torch.randint(0, V, (B, T), generator=g)
+    for temp in (1.0, 0.7):
+        x = logits.clone()
+        x.div_(temp)  # model_wrapper.py:314
+        x.requires_grad_(True)
+        lp = tu.logprobs_from_logits(x, labels)
+        ent = tu.chunked_entropy_from_logits(x, requires_grad=True)
+        glp = torch.randn(B, T, generator=g)
+        gent = torch.randn(B, T, generator=g)
+        (lp * glp + ent * gent).sum().backward()
+        tag = f"f32_t{str(temp).replace('.', '')}"
+        out[f"logp_{tag}"] = lp.detach()
+        out[f"ent_{tag}"] = ent.detach()
+        out[f"glp_{tag}"] = glp
+        out[f"gent_{tag}"] = gent
+        out[f"dlogits_{tag}"] = x.grad / temp  # chain through the in-place div
+    save("logprob_f32", logits=logits, labels=labels, **out)
+    # bf16 logits (Qwen-like V slice): flash-CE semantics = fp32 math on the bf16 values
+    out = {}
+    B, T, V = 2, 5, 4096
+    lb = (torch.randn(B, T, V, generator=g) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, T), generator=g)
+    out["logp_fp32math"] = tu.logprobs_from_logits(lb.float(), labels)
+    out["ent_fp32math"] = tu.chunked_entropy_from_logits(lb.float())
+    out["ent_bf16math"] = tu.chunked_entropy_from_logits(lb).float()  # the reference's own dtype path
+    x = lb.clone()
+    x.div_(0.6)
+    out["logp_t06"] = tu.logprobs_from_logits(x.float(), labels)
+    save("logprob_bf16", logits=lb, labels=labels, **out)
+
+
+def gen_pack(pre, trainer_mod, tb):
+    g = torch.Generator().manual_seed(21)
+    N = 7
+    prompts = [torch.randint(3, 100, (int(torch.randint(1, 9, (1,), generator=g)),), generator=g).tolist()
+               for _ in range(N)]
+    responses = [torch.randint(3, 100, (int(torch.randint(1, 12, (1,), generator=g)),), generator=g).tolist()
+                 for _ in range(N)]
+    rewards = []
+    for r in responses:
+        rr = [0.0] * len(r)
+        rr[-1] = float(torch.rand((), generator=g))
+        rewards.append(rr)
+    loss_masks = [[1] * (len(r) - 1) + [0] if len(r) > 1 else [1] for r in responses]
+    logprobs = [(torch.randn(len(r), generator=g) - 1).tolist() for r in responses]
+    tok = SimpleNamespace(pad_token_id=0)
+    seq, att, am, rw, lm, lp = pre.convert_prompts_responses_to_batch_tensors(
+        tok, prompts, responses, rewards, loss_masks, logprobs)
+    # pad_batch (trainer.py:872-907) to a multiple of dp=4
+    batch = tb.TrainingInputBatch({"sequences": seq, "attention_mask": att, "response_mask": am, "rewards": rw,
+                                   "loss_mask": lm, "rollout_logprobs": lp})
+    batch.metadata = {"uids": [str(i) for i in range(N)]}
+    fake = SimpleNamespace(dispatch=SimpleNamespace(get_lcm_dp_size=lambda: 4))
+    padded = trainer_mod.RayPPOTrainer.pad_batch(fake, batch)
+
+    def ragged(lists, dtype):
+        off = np.zeros(len(lists) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(x) for x in lists])
+        vals = np.concatenate([np.asarray(x, dtype=dtype) for x in lists]) if off[-1] else np.zeros(0, dtype)
+        return vals, off
+
+    pv, po = ragged(prompts, np.int64)
+    rv, ro = ragged(responses, np.int64)
+    wv, wo = ragged(rewards, np.float32)
+    mv, mo = ragged(loss_masks, np.float32)
+    lv, lo = ragged(logprobs, np.float32)
+    save("pack", prompt_vals=pv, prompt_off=po, response_vals=rv, response_off=ro, reward_vals=wv, reward_off=wo,
+         loss_mask_vals=mv, loss_mask_off=mo, logprob_vals=lv, logprob_off=lo, pad_token_id=np.int64(0),
+         sequences=seq, attention_mask=att, response_mask=am, rewards=rw, loss_mask=lm, rollout_logprobs=lp,
+         pad_size=np.int64(padded.metadata["pad_size"]), p_sequences=padded["sequences"],
+         p_attention_mask=padded["attention_mask"], p_response_mask=padded["response_mask"],
+         p_rewards=padded["rewards"], p_loss_mask=padded["loss_mask"], p_rollout_logprobs=padded["rollout_logprobs"],
+         p_uids=np.array(padded.metadata["uids"]))
+
+
+def gen_reward_kl(trainer_mod, tb, cfgmod):
+    g = torch.Generator().manual_seed(8)
+    N, R = 9, 21
+    lens = torch.randint(1, R + 1, (N,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).float()
+    lp = torch.randn(N, R, generator=g) - 2
+    base = lp + torch.randn(N, R, generator=g) * 0.4
+    rew = torch.zeros(N, R)
+    rew[torch.arange(N), lens - 1] = 1.0
+    out = {}
+    for kind in ("k1", "k3"):
+        batch = tb.TrainingInputBatch({"loss_mask": mask, "rewards": rew.clone(), "base_action_log_probs": base,
+                                       "action_log_probs": lp})
+        batch.metadata = {}
+        cfg = SimpleNamespace(trainer=SimpleNamespace(algorithm=cfgmod.AlgorithmConfig(kl_estimator_type=kind,
+                                                                                       kl_loss_coef=0.05)))
+        fake = SimpleNamespace(cfg=cfg, reward_kl_controller=None, all_metrics={})
+        res = trainer_mod.RayPPOTrainer.apply_reward_kl_penalty(fake, batch)
+        out[f"rewards_{kind}"] = res["rewards"]
+        out[f"avg_kl_{kind}"] = np.float32(res.metadata["metrics"]["avg_kl"])
+        out[f"avg_kl_max_{kind}"] = np.float32(res.metadata["metrics"]["avg_kl_max"])
+    save("reward_kl", rewards=rew, loss_mask=mask, action_log_probs=lp, base_action_log_probs=base, kl_coef=0.05,
+         **out)
+
+
+def main():
+    install_shim()
+    torch.set_num_threads(4)
+    from skyrl_train import config as cfgmod
+    from skyrl_train import trainer as trainer_mod
+    from skyrl_train import training_batch as tb
+    from skyrl_train.dataset import preprocess as pre
+    from skyrl_train.utils import ppo_utils as pu
+    from skyrl_train.utils import torch_utils as tu
+
+    assert not tu.FLASH_ATTN_CROSS_ENTROPY_LOSS_AVAILABLE
+    gen_grpo(pu)
+    gen_gae(pu)
+    gen_kl(pu)
+    gen_ppo(pu, cfgmod)
+    gen_critic(pu, cfgmod)
+    gen_logprob(tu)
+    gen_pack(pre, trainer_mod, tb)
+    gen_reward_kl(trainer_mod, tb, cfgmod)
+
+
+if __name__ == "__main__":
+    main()
