@@ -283,7 +283,9 @@ def cpu_baseline(args):
 
     from oracle import cpu_ref
 
+    # the GPU box's CPU share is 16 threads (OMP_NUM_THREADS there); affinity shows the whole host
     cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     cores = min(cores, args.cpu_threads) if args.cpu_threads > 0 else cores
     torch.set_num_threads(cores)
     R, V, N = R_MAX, VOCAB, PROMPTS * GROUP
