@@ -140,8 +140,11 @@ def run(args):
 
     labels = torch.randint(0, V, (N, R), device=dev, generator=torch.Generator(device=dev).manual_seed(7))
     seq_ids = torch.arange(N, device=dev, dtype=torch.int64) + rank * N
-    tokens = torch.empty((R, N), dtype=torch.int32, device=dev)
-    samp_lp = torch.empty((R, N), dtype=torch.float32, device=dev)
+    from skyrl_amd.config import SamplingParams
+    from skyrl_amd.sampler import TokenSampler
+
+    sampler = TokenSampler(N, V, R, dev, SamplingParams(), seed=0, seq_ids=seq_ids)
+    base_ptr = logits.data_ptr()
     goff, grows, ng = ops.groups_from_index(uids)
     goff, grows = goff.to(dev), grows.to(dev)
     cfg = AlgorithmConfig()
@@ -151,14 +154,13 @@ def run(args):
 
     def step(step_idx):
         # ---- rollout: R decode steps over [N, V] logits (row stride R*V in the resident tensor)
+        sampler.seed = step_idx
+        sh = torch.cuda.current_stream(dev).cuda_stream
         for t in range(R):
             if full:
-                view = logits.view(N, R, V)[:, t, :]
+                sampler.step_ptr(base_ptr + 2 * V * t, R * V, t, sh)
             else:
-                base = (t * N) % (rows - N + 1)
-                view = logits[base:base + N]
-            ops.sample(view, temperature=1.0, seed=step_idx, seq_ids=seq_ids, step=t, tokens_out=tokens[t],
-                       logp_out=samp_lp[t])
+                sampler.step_ptr(base_ptr + 2 * V * ((t * N) % (rows - N + 1)), V, t, sh)
         # ---- pack ragged rollout output into the padded training tensors
         seqs, att, rmask, rew, lmask, rlp = ops.pack_experience(
             data["ptok"], data["poff"], data["rtok"], data["roff"], data["rew"], data["roff"], data["lmask"],

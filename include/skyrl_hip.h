@@ -41,6 +41,10 @@ extern "C" {
 const char* skyrl_last_error(void);
 /* ABI version; bumped on any signature change. */
 int skyrl_abi_version(void);
+/* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
+ * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
+ * {0, 1} (non-temporal streaming loads of the logits). Not thread-safe.              */
+int skyrl_tune(const char* key, int value);
 
 /* ---- a4: GRPO outcome advantage ----------------------------------------
  * Replaces compute_grpo_outcome_advantage (utils/ppo_utils.py:1132-1182) as

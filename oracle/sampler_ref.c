@@ -36,29 +36,26 @@ static uint32_t row_key(uint64_t seed, int64_t seq, int64_t step) {
     return k;
 }
 
-/* ln for positive normal floats: 2^e * m, m in [sqrt(.5), sqrt(2)), ln(1+z) = z*P7(z). */
+/* ln for positive normal floats, branch-free: ix = bits - bits(2/3), e = ix >> 23,
+ * mantissa rebased into [2/3, 4/3), ln(1+z) = z*P6(z). */
 static float det_ln(float y) {
-    uint32_t bits, mb;
-    float m, z, p, r;
+    uint32_t bits, ix, mb;
+    float m, z, p;
     int e;
     memcpy(&bits, &y, 4);
-    e = (int)(bits >> 23) - 127;
-    mb = (bits & 0x007fffffu) | 0x3f800000u;
+    ix = bits - 0x3f2aaaabu;
+    e = (int32_t)ix >> 23;
+    mb = (ix & 0x007fffffu) + 0x3f2aaaabu;
     memcpy(&m, &mb, 4);
-    if (m > 1.41421356f) {
-        m = m * 0.5f;
-        e += 1;
-    }
     z = m - 1.0f;
-    p = 0.11931054294109344f;
-    p = fmaf(p, z, -0.1868075132369995f);
-    p = fmaf(p, z, 0.20491759479045868f);
-    p = fmaf(p, z, -0.24908289313316345f);
-    p = fmaf(p, z, 0.33314675092697144f);
-    p = fmaf(p, z, -0.5000114440917969f);
-    p = fmaf(p, z, 1.0000009536743164f);
-    r = z * p;
-    return fmaf((float)e, 0.693147180559945f, r);
+    p = 0.16302786767482758f;
+    p = fmaf(p, z, -0.18978701531887054f);
+    p = fmaf(p, z, 0.19917640089988708f);
+    p = fmaf(p, z, -0.24900923669338226f);
+    p = fmaf(p, z, 0.3333371579647064f);
+    p = fmaf(p, z, -0.5000061392784119f);
+    p = fmaf(p, z, 1.0f);
+    return fmaf((float)e, 0.693147180559945f, z * p);
 }
 
 static float gumbel(uint32_t key, uint32_t v) {

@@ -75,6 +75,7 @@ _INT = ctypes.c_int
 SIGNATURES = {
     "skyrl_last_error": (ctypes.c_char_p, []),
     "skyrl_abi_version": (_INT, []),
+    "skyrl_tune": (_INT, [ctypes.c_char_p, _INT]),
     "skyrl_grpo_advantage": (_INT, [_P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
     "skyrl_gae_workspace_bytes": (_SZ, [_I32]),
     "skyrl_gae_advantage_return": (_INT, [_P, _P, _P, _INT, _I32, _I32, _F, _F, _P, _P, _P, _P, _P]),

@@ -1,22 +1,26 @@
 // Last-arriver election for in-launch reductions (gfx950, 8 XCDs with private L2s).
 //
-// Producer side follows the guide's split-K recipe: every storing wave drains
-// (s_waitcnt vmcnt(0)), block barrier, lane 0 agent-scope RELEASE, asm drain
-// (ROCm 7.2 may drop the fence's own wait), relaxed agent fetch_add on the
-// ticket. The block drawing the last ticket does one agent-scope ACQUIRE
-// (invalidates this CU's L1) before a barrier, then reads every block's
-// partials with plain loads, and finally re-arms the counter to 0.
+// Producer side (guide: split-K seam, write-through form): the block's partial record is
+// stored WRITE-THROUGH with agent-scope relaxed atomic stores (global_store ... sc1) by
+// the single storing thread, which then drains (s_waitcnt vmcnt(0)) and draws a ticket
+// with a relaxed agent-scope fetch_add. No release fence: a per-block buffer_wbl2 over
+// thousands of workgroups was the dominant cost (SQ_WAIT_ANY 82% of wave cycles in the
+// sampler). The block drawing the last ticket does one agent-scope ACQUIRE (invalidates
+// this CU's L1) before a block barrier, then reads every partial, and re-arms the counter.
 // The counter lives in caller-owned workspace zeroed once at allocation.
 #pragma once
 #include "common.h"
 
 namespace skyrl {
 
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) {  // write-through (sc1) store of a partial
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every partial of this block must have been stored with st_wt() by threadIdx.x == 0.
 __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total, int* lds_flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = (prev == total - 1u);

@@ -26,13 +26,22 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
     return __uint_as_float(static_cast<uint32_t>(h) << 16);
 }
-// Round-to-nearest-even f32 -> bf16, NaN kept a NaN (quiet).
-__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return static_cast<uint16_t>(u >> 16);
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// f32 -> bf16, round-to-nearest-even, NaN kept a NaN: one v_cvt_pk_bf16_f32 (gfx950).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+    f32x2_t f = {lo, hi};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
 }
+
+// Raw v_exp_f32 / v_log_f32 (base 2): no range-reduction wrapper. Inputs on the hot
+// paths are <= 0 (softmax numerators) or normal positives (sums), where the bare
+// instruction is accurate to ~1 ulp; exp2f()/log2f() add 4-5 VALU ops of denormal
+// handling per call.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
 
 // Mask element as float, for every mask dtype the reference uses
 // (int64 response_mask, f32 loss_mask, bool).

@@ -23,7 +23,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kRowsPerBlock = kThreads / kWave;
-constexpr int kUnroll = 4;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kDLow = -1.0e30f;  // floor for x - m so that -inf logits give e=0, e*d=0
@@ -45,11 +44,8 @@ template <> struct Elem<uint16_t> {
         }
     }
     __device__ static uint4 pack(const float (&x)[8]) {
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            w[k] = (uint32_t)f32_to_bf16(x[2 * k]) | ((uint32_t)f32_to_bf16(x[2 * k + 1]) << 16);
-        return make_uint4(w[0], w[1], w[2], w[3]);
+        return make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                          pack_bf16x2(x[6], x[7]));
     }
     __device__ static void store(uint16_t* p, float x) { *p = f32_to_bf16(x); }
 };
@@ -67,6 +63,9 @@ template <> struct Elem<float> {
     __device__ static void store(float* p, float x) { *p = x; }
 };
 
+// Online softmax state in log2 units: m = running max of x, S = sum 2^y, W = sum 2^y * y
+// with y = (x - m) * log2(e) >= -1e30 (finite even for x = -inf, so e*y = 0, never NaN).
+// lse = m + ln(S); H = ln(S) - ln(2) * W / S.
 struct SoftState {
     float m, s, w;
 };
@@ -84,24 +83,25 @@ __device__ __forceinline__ void state_add(SoftState& st, const float (&x)[K]) {
 #pragma unroll
     for (int k = 1; k < K; ++k) mx = fmaxf(mx, x[k]);
     const float mn = fmaxf(st.m, mx);
-    const float dm = st.m - mn;
-    const float a = exp2f(dm * kLog2e);
-    st.w = a * fmaf(dm, st.s, st.w);
+    const float dy = fmaxf((st.m - mn) * kLog2e, kDLow);  // first fold: -FLT_MAX*log2e would be -inf
+    const float a = fast_exp2(dy);
+    st.w = a * fmaf(dy, st.s, st.w);
     st.s = a * st.s;
     st.m = mn;
+    const float c = -mn * kLog2e;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const float d = fmaxf(x[k] - mn, kDLow);
-        const float e = exp2f(d * kLog2e);
+        const float y = fmaxf(fmaf(x[k], kLog2e, c), kDLow);
+        const float e = fast_exp2(y);
         st.s += e;
-        st.w = fmaf(e, d, st.w);
+        st.w = fmaf(e, y, st.w);
     }
 }
 
 __device__ __forceinline__ void state_merge(SoftState& a, const SoftState& b) {
     const float mn = fmaxf(a.m, b.m);
-    const float da = a.m - mn, db = b.m - mn;
-    const float ea = exp2f(da * kLog2e), eb = exp2f(db * kLog2e);
+    const float da = fmaxf((a.m - mn) * kLog2e, kDLow), db = fmaxf((b.m - mn) * kLog2e, kDLow);
+    const float ea = fast_exp2(da), eb = fast_exp2(db);
     a.w = ea * fmaf(da, a.s, a.w) + eb * fmaf(db, b.s, b.w);
     a.s = ea * a.s + eb * b.s;
     a.m = mn;
@@ -119,7 +119,14 @@ __device__ __forceinline__ SoftState wave_merge(SoftState st) {
     return st;
 }
 
-template <typename T>
+// Streaming 16-B load of data read once per pass (159 GB per pass >> L2/MALL): nontemporal.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <typename T, int kUnroll, bool kNT>
 __global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(
     const T* __restrict__ logits, int64_t sb, int64_t st_, int nt, int64_t rows, int V,
     const int64_t* __restrict__ labels, int64_t lsb, int64_t lst, float temp, bool has_t,
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(
         for (; i + (kUnroll - 1) * kWave < nvec; i += kUnroll * kWave) {
             uint4 v[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) v[u] = rv[i + u * kWave];
+            for (int u = 0; u < kUnroll; ++u) v[u] = kNT ? ld_stream(rv + i + u * kWave) : rv[i + u * kWave];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 float x[VEC];
@@ -157,7 +164,7 @@ __global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(
         }
         for (; i < nvec; i += kWave) {
             float x[VEC];
-            E::unpack(rv[i], x);
+            E::unpack(kNT ? ld_stream(rv + i) : rv[i], x);
             if (has_t) {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) x[k] = E::apply_t(x[k], temp, true);
@@ -172,19 +179,19 @@ __global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(
     }
     st = wave_merge(st);
     if (lane == 0) {
-        const float logs = log2f(st.s) * kLn2;
+        const float logs = fast_log2(st.s) * kLn2;
         const float lse = st.m + logs;
         const int64_t lab = labels[b * lsb + t * lst];
         float xl;
         if (lab >= 0 && lab < V) xl = E::apply_t(E::load(row + lab), temp, has_t);
         else xl = __builtin_nanf("");
         logp_out[r] = xl - lse;
-        if (ent_out) ent_out[r] = logs - st.w / st.s;
+        if (ent_out) ent_out[r] = logs - kLn2 * (st.w / st.s);
         if (lse_out) lse_out[r] = lse;
     }
 }
 
-template <typename T>
+template <typename T, int kUnroll, bool kNT>
 __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(
     const T* __restrict__ logits, int64_t sb, int64_t st_, int nt, int64_t rows, int V,
     const int64_t* __restrict__ labels, int64_t lsb, int64_t lst, float temp, bool has_t,
@@ -206,7 +213,7 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(
     const int64_t lab = labels[b * lsb + t * lst];
     auto grad = [&](float x, int64_t v) -> float {
         const float lp = x - L;
-        const float p = exp2f(lp * kLog2e);
+        const float p = fast_exp2(lp * kLog2e);
         float g = -glp * p - gent * p * (lp + H);
         if (v == lab) g += glp;
         return has_t ? g * inv_t : g;
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(
         for (; i + (kUnroll - 1) * kWave < nvec; i += kUnroll * kWave) {
             uint4 v[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) v[u] = rv[i + u * kWave];
+            for (int u = 0; u < kUnroll; ++u) v[u] = kNT ? ld_stream(rv + i + u * kWave) : rv[i + u * kWave];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 float x[VEC];
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(
         }
         for (; i < nvec; i += kWave) {
             float x[VEC];
-            E::unpack(rv[i], x);
+            E::unpack(kNT ? ld_stream(rv + i) : rv[i], x);
             const int64_t v0 = (int64_t)i * VEC;
 #pragma unroll
             for (int k = 0; k < VEC; ++k) x[k] = grad(E::apply_t(x[k], temp, has_t), v0 + k);
@@ -247,35 +254,78 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(
     }
 }
 
-template <typename T>
-int launch_fwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
+struct Tuning {
+    int unroll = 4;
+    int nt = 1;
+};
+Tuning g_tune;
+
+template <typename T, int U, bool NT>
+int launch_fwd_v(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
                int64_t lst, float temp, float* logp, float* ent, float* lse, hipStream_t s) {
     const int64_t rows = (int64_t)nb * nt;
     const int64_t blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
     const bool has_t = temp != 1.0f;
-    hipLaunchKernelGGL(logprob_fwd_kernel<T>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((logprob_fwd_kernel<T, U, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
                        reinterpret_cast<const T*>(logits), sb, st, nt, rows, V, labels, lsb, lst, temp, has_t, logp,
                        ent, lse);
     return check_launch("logprob_fwd_kernel");
+}
+
+template <typename T, int U, bool NT>
+int launch_bwd_v(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
+               int64_t lst, float temp, const float* lse, const float* ent, const float* glp, const float* gent,
+               void* dx, hipStream_t s) {
+    const int64_t rows = (int64_t)nb * nt;
+    const int64_t blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
+    const bool has_t = temp != 1.0f;
+    hipLaunchKernelGGL((logprob_bwd_kernel<T, U, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                       reinterpret_cast<const T*>(logits), sb, st, nt, rows, V, labels, lsb, lst, temp, has_t, lse,
+                       ent, glp, gent, reinterpret_cast<T*>(dx));
+    return check_launch("logprob_bwd_kernel");
+}
+
+template <typename T>
+int launch_fwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
+               int64_t lst, float temp, float* logp, float* ent, float* lse, hipStream_t s) {
+    const bool nt_ = g_tune.nt != 0;
+    if (g_tune.unroll == 8)
+        return nt_ ? launch_fwd_v<T, 8, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s)
+                   : launch_fwd_v<T, 8, false>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s);
+    return nt_ ? launch_fwd_v<T, 4, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s)
+               : launch_fwd_v<T, 4, false>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s);
 }
 
 template <typename T>
 int launch_bwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
                int64_t lst, float temp, const float* lse, const float* ent, const float* glp, const float* gent,
                void* dx, hipStream_t s) {
-    const int64_t rows = (int64_t)nb * nt;
-    const int64_t blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
-    const bool has_t = temp != 1.0f;
-    hipLaunchKernelGGL(logprob_bwd_kernel<T>, dim3((unsigned)blocks), dim3(kThreads), 0, s,
-                       reinterpret_cast<const T*>(logits), sb, st, nt, rows, V, labels, lsb, lst, temp, has_t, lse,
-                       ent, glp, gent, reinterpret_cast<T*>(dx));
-    return check_launch("logprob_bwd_kernel");
+    const bool nt_ = g_tune.nt != 0;
+    if (g_tune.unroll == 8)
+        return nt_ ? launch_bwd_v<T, 8, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s)
+                   : launch_bwd_v<T, 8, false>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s);
+    return nt_ ? launch_bwd_v<T, 4, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s)
+               : launch_bwd_v<T, 4, false>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s);
 }
 
 }  // namespace
 }  // namespace skyrl
 
 using namespace skyrl;
+
+extern "C" int skyrl_tune(const char* key, int value) {
+    const std::string k = key ? key : "";
+    if (k == "logprob_unroll") {
+        SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: logprob_unroll must be 4 or 8");
+        g_tune.unroll = value;
+        return SKYRL_OK;
+    }
+    if (k == "logprob_nt") {
+        g_tune.nt = value != 0;
+        return SKYRL_OK;
+    }
+    return fail(SKYRL_ERR_INVALID, "skyrl_tune: unknown key " + k);
+}
 
 extern "C" int skyrl_logprob_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t nb,
                                  int32_t nt, int32_t V, const int64_t* labels, int64_t lstride_b, int64_t lstride_t,

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_fwd_kernel(
     if (threadIdx.x == 0) {
         float* dst = partials + ((int64_t)row * nchunks + chunk) * kNP;
 #pragma unroll
-        for (int k = 0; k < kNP; ++k) dst[k] = acc[k];
+        for (int k = 0; k < kNP; ++k) st_wt(dst + k, acc[k]);
     }
     if (!arrive_last(counter, (unsigned)(n * nchunks), &s_last)) return;
 
@@ -283,8 +283,8 @@ __global__ __launch_bounds__(kThreads) void reward_kl_kernel(
     if (threadIdx.x == 0) {
         float mx = s_max[0];
         for (int j = 1; j < kWaves; ++j) mx = fmaxf(mx, s_max[j]);
-        partials[row * 2 + 0] = acc[0] / (acc[1] > 1.f ? acc[1] : 1.f);
-        partials[row * 2 + 1] = mx;
+        st_wt(partials + row * 2 + 0, acc[0] / (acc[1] > 1.f ? acc[1] : 1.f));
+        st_wt(partials + row * 2 + 1, mx);
     }
     if (!arrive_last(counter, (unsigned)N, &s_last)) return;
     double tot[2] = {0.0, 0.0};
@@ -342,9 +342,9 @@ __global__ __launch_bounds__(kThreads) void critic_loss_kernel(
     const float sc = 0.5f / ((float)n * mrow);
     for (int t = threadIdx.x; t < R; t += kThreads) gv[rbase + t] *= sc;
     if (threadIdx.x == 0) {
-        partials[row * 3 + 0] = acc[0] / mrow;
-        partials[row * 3 + 1] = acc[2];
-        partials[row * 3 + 2] = acc[1];
+        st_wt(partials + row * 3 + 0, acc[0] / mrow);
+        st_wt(partials + row * 3 + 1, acc[2]);
+        st_wt(partials + row * 3 + 2, acc[1]);
     }
     if (!arrive_last(counter, (unsigned)n, &s_last)) return;
     double tot[3] = {0.0, 0.0, 0.0};

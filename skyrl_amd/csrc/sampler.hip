@@ -51,34 +51,22 @@ __host__ __device__ __forceinline__ uint32_t row_key(uint64_t seed, int64_t seq,
     return k;
 }
 
-// Deterministic natural log for normal positive floats: exponent/mantissa split,
-// mantissa in [sqrt(.5), sqrt(2)), ln(1+z) = z*P7(z) by fmaf Horner.
+// Deterministic natural log for normal positive floats (branch-free): ix = bits - bits(2/3),
+// e = ix >> 23 (arithmetic), mantissa rebased into [2/3, 4/3), ln(1+z) = z*P6(z) by fmaf
+// Horner (|err| < 1.1e-6). Bit-identical in oracle/sampler_ref.c (same ops, contraction off).
 __host__ __device__ __forceinline__ float det_ln(float y) {
-    const uint32_t bits = __builtin_bit_cast(uint32_t, y);
-    int e = (int)(bits >> 23) - 127;
-    uint32_t mb = (bits & 0x007fffffu) | 0x3f800000u;
-    float m = __builtin_bit_cast(float, mb);
-    if (m > 1.41421356f) {
-        m = m * 0.5f;
-        e += 1;
-    }
+    const uint32_t ix = __builtin_bit_cast(uint32_t, y) - 0x3f2aaaabu;
+    const int e = (int)ix >> 23;
+    const float m = __builtin_bit_cast(float, (ix & 0x007fffffu) + 0x3f2aaaabu);
     const float z = m - 1.0f;
-    float p = 0.11931054294109344f;
-    p = fmaf(p, z, -0.1868075132369995f);
-    p = fmaf(p, z, 0.20491759479045868f);
-    p = fmaf(p, z, -0.24908289313316345f);
-    p = fmaf(p, z, 0.33314675092697144f);
-    p = fmaf(p, z, -0.5000114440917969f);
-    p = fmaf(p, z, 1.0000009536743164f);
-    const float r = z * p;
-    return fmaf((float)e, 0.693147180559945f, r);
-}
-
-__device__ __forceinline__ float gumbel(uint32_t key, uint32_t v) {
-    const uint32_t r = hash32(key ^ (v * 0x9e3779b1u));
-    const float u = (float)((r >> 8) | 1u) * 5.9604644775390625e-8f;  // odd / 2^24, exact
-    const float E = -det_ln(u);
-    return -det_ln(E);
+    float p = 0.16302786767482758f;
+    p = fmaf(p, z, -0.18978701531887054f);
+    p = fmaf(p, z, 0.19917640089988708f);
+    p = fmaf(p, z, -0.24900923669338226f);
+    p = fmaf(p, z, 0.3333371579647064f);
+    p = fmaf(p, z, -0.5000061392784119f);
+    p = fmaf(p, z, 1.0f);
+    return fmaf((float)e, 0.693147180559945f, z * p);
 }
 
 // order-preserving unsigned keys
@@ -86,6 +74,13 @@ __device__ __forceinline__ uint32_t okey_bf16(uint16_t h) {
     return (h & 0x8000u) ? (uint32_t)(uint16_t)~h : (uint32_t)(h | 0x8000u);
 }
 __device__ __forceinline__ uint32_t okey_f32(uint32_t u) { return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+// logits rows are read once per decode step: non-temporal streaming loads
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 struct Best {
     float score;
@@ -164,10 +159,11 @@ __global__ __launch_bounds__(kThreads) void sample_filter_kernel(const T* __rest
     if (threadIdx.x == 0) thr_key[blockIdx.x] = s_prefix;
 }
 
-template <typename T>
+// MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p
+template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads) void sample_kernel(
-    const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int greedy, int use_topk,
-    int use_minp, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
+    const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
+    int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     const uint32_t* __restrict__ thr_key, const float* __restrict__ row_max, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters) {
     __shared__ Part s_part[kWaves];
@@ -180,47 +176,101 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
     const int v_beg = split * chunk;
     const int v_end = min(V, v_beg + chunk);
     const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
+    constexpr bool greedy = MODE == 0;
+    const bool use_topk = MODE == 2 && use_topk_rt;
+    const bool use_minp = MODE == 2 && use_minp_rt;
     const uint32_t tk = use_topk ? thr_key[row_i] : 0u;
     const float mthr = use_minp ? row_max[row_i] * inv_t + ln_min_p : 0.f;
 
-    Best best{-INFINITY, 0x7fffffff};
-    float m = -3.402823466e38f, s = 0.f;  // raw online softmax for the logprob
-    auto visit = [&](T raw, int v) {
-        const float x = to_f<T>(raw);
-        {  // lse of the raw logits (not on the decision path)
-            const float mn = fmaxf(m, x);
-            s = s * exp2f((m - mn) * kLog2e) + exp2f(fmaxf(x - mn, -1e30f) * kLog2e);
+    // Per lane: best (score, index) over the elements it visits in ascending index order
+    // (so a strict '>' keeps the lowest index on ties) and the raw online (max, sum-exp).
+    float best_s = -INFINITY;
+    int best_i = 0x7fffffff;
+    float m = -3.402823466e38f, s = 0.f;
+    constexpr int VEC = 16 / sizeof(T);
+    auto visit_vec = [&](const T (&raw)[VEC], int v0, int cnt) {
+        float x[VEC];
+        float vmax = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            x[k] = k < cnt ? to_f<T>(raw[k]) : -INFINITY;
+            vmax = fmaxf(vmax, x[k]);
+        }
+        {  // lse of the raw logits (logprob output; not on the decision path)
+            const float mn = fmaxf(m, vmax);
+            s = s * fast_exp2((m - mn) * kLog2e);
+            const float c = -mn * kLog2e;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) s += fast_exp2(x[k] * kLog2e + c);
             m = mn;
         }
-        if (greedy) {
-            if (better(x, v, best)) best = Best{x, v};
+        if constexpr (greedy) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k)
+                if (x[k] > best_s) {
+                    best_s = x[k];
+                    best_i = v0 + k;
+                }
             return;
         }
-        const float xs = x * inv_t;
-        if (use_topk && okey<T>(raw) < tk) return;
-        if (use_minp && xs < mthr) return;
-        // Skip the noise when it cannot win: fl(xs+g) <= fl(xs+17) <= best, and a
-        // tie loses on index because a thread visits its elements in ascending v.
-        if (best.score != -INFINITY && xs + kGumbelMax <= best.score) return;
-        const float sc = xs + gumbel(key, (uint32_t)v);
-        if (better(sc, v, best)) best = Best{sc, v};
+        // Skip the vector when no element can win: fl(xs+g) <= fl(xs_max+17) <= best
+        // (inv_t > 0 keeps max(x)*inv_t == max(x*inv_t)); ties lose on index.
+        if (best_s != -INFINITY && vmax * inv_t + kGumbelMax <= best_s) return;
+        uint32_t hv = key ^ ((uint32_t)v0 * 0x9e3779b1u);
+        uint32_t hb = (uint32_t)v0 * 0x9e3779b1u;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const float xs = x[k] * inv_t;
+            bool keep = k < cnt;
+            if constexpr (MODE == 2) {
+                if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
+                if (use_minp) keep = keep && xs >= mthr;
+            }
+            hv = key ^ hb;
+            hb += 0x9e3779b1u;
+            const uint32_t r = hash32(hv);
+            const float u = (float)((r >> 8) | 1u) * 5.9604644775390625e-8f;
+            const float sc = xs + (-det_ln(-det_ln(u)));
+            if (keep && sc > best_s) {
+                best_s = sc;
+                best_i = v0 + k;
+            }
+        }
     };
-    constexpr int VEC = 16 / sizeof(T);
     const bool vec_ok = (reinterpret_cast<uintptr_t>(row + v_beg) % 16) == 0;
     int v0 = v_beg;
     if (vec_ok) {
         const int nvec = (v_end - v_beg) / VEC;
         const uint4* rv = reinterpret_cast<const uint4*>(row + v_beg);
-        for (int i = threadIdx.x; i < nvec; i += kThreads) {
-            uint4 pk = rv[i];
-            T vals[VEC];
-            memcpy(vals, &pk, 16);
+        int i = threadIdx.x;
+        for (; i + 3 * kThreads < nvec; i += 4 * kThreads) {  // 4 x 16 B in flight per lane
+            uint4 pk[4];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) visit(vals[k], v_beg + i * VEC + k);
+            for (int u = 0; u < 4; ++u) pk[u] = ld_stream(rv + i + u * kThreads);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                T vals[VEC];
+                __builtin_memcpy(vals, &pk[u], 16);
+                visit_vec(vals, v_beg + (i + u * kThreads) * VEC, VEC);
+            }
+        }
+        for (; i < nvec; i += kThreads) {
+            uint4 pk = ld_stream(rv + i);
+            T vals[VEC];
+            __builtin_memcpy(vals, &pk, 16);
+            visit_vec(vals, v_beg + i * VEC, VEC);
         }
         v0 = v_beg + nvec * VEC;
     }
-    for (int v = v0 + threadIdx.x; v < v_end; v += kThreads) visit(row[v], v);
+    // unaligned head or ragged tail: VEC-element groups, the last one partial
+    for (int g0 = v0 + threadIdx.x * VEC; g0 < v_end; g0 += kThreads * VEC) {
+        T vals[VEC];
+        const int cnt = min(VEC, v_end - g0);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) vals[k] = k < cnt ? row[g0 + k] : row[g0];
+        visit_vec(vals, g0, cnt);
+    }
+    Best best{best_s, best_i};
 
     // wave reduce: best (score desc, idx asc) and (m, s)
 #pragma unroll
@@ -231,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
         const float om = __shfl_xor(m, off, kWave);
         const float oss = __shfl_xor(s, off, kWave);
         const float mn = fmaxf(m, om);
-        s = s * exp2f((m - mn) * kLog2e) + oss * exp2f((om - mn) * kLog2e);
+        s = s * fast_exp2((m - mn) * kLog2e) + oss * fast_exp2((om - mn) * kLog2e);
         m = mn;
     }
     if (lane == 0) s_part[threadIdx.x / kWave] = Part{best.score, best.idx, m, s};
@@ -246,10 +296,14 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
                 p.idx = q.idx;
             }
             const float mn = fmaxf(p.m, q.m);
-            p.s = p.s * exp2f((p.m - mn) * kLog2e) + q.s * exp2f((q.m - mn) * kLog2e);
+            p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
             p.m = mn;
         }
-        parts[(int64_t)row_i * nsplit + split] = p;
+        float* dst = reinterpret_cast<float*>(parts + (int64_t)row_i * nsplit + split);
+        st_wt(dst + 0, p.score);
+        st_wt(reinterpret_cast<int*>(dst) + 1, p.idx);
+        st_wt(dst + 2, p.m);
+        st_wt(dst + 3, p.s);
     }
     if (nsplit > 1) {
         if (!arrive_last(counters + row_i, (unsigned)nsplit, &s_last)) return;
@@ -266,12 +320,12 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
                 p.idx = q.idx;
             }
             const float mn = fmaxf(p.m, q.m);
-            p.s = p.s * exp2f((p.m - mn) * kLog2e) + q.s * exp2f((q.m - mn) * kLog2e);
+            p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
             p.m = mn;
         }
         tokens[row_i] = p.idx;
         if (logp_out) {
-            const float lse = p.m + log2f(p.s) * kLn2;
+            const float lse = p.m + fast_log2(p.s) * kLn2;
             logp_out[row_i] = (p.idx >= 0 && p.idx < V) ? to_f<T>(row[p.idx]) - lse : __builtin_nanf("");
         }
     }
@@ -313,9 +367,16 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         int rc = check_launch("sample_filter_kernel");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(sample_kernel<T>, dim3(nseq, nsplit), dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t,
-                       greedy, use_topk, use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts,
-                       counters);
+    const dim3 grid(nseq, nsplit);
+    if (greedy)
+        hipLaunchKernelGGL((sample_kernel<T, 0>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t, 0, 0,
+                           ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+    else if (use_topk || use_minp)
+        hipLaunchKernelGGL((sample_kernel<T, 2>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
+                           use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+    else
+        hipLaunchKernelGGL((sample_kernel<T, 1>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t, 0, 0,
+                           ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
     return check_launch("sample_kernel");
 }
 
