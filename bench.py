@@ -150,6 +150,16 @@ def run(args):
     cfg = AlgorithmConfig()
     params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, has_entropy=True)
     fwd_timer = KernelTimer()
+    train_timer = KernelTimer()
+    sample_timer = KernelTimer()
+    timers = (fwd_timer, train_timer, sample_timer)
+    lp = torch.empty((mb, R), dtype=torch.float32, device=dev)
+    ent = torch.empty_like(lp)
+    lse = torch.empty_like(lp)
+    loss_buf = torch.empty((), dtype=torch.float32, device=dev)
+    met_buf = torch.empty(8, dtype=torch.float32, device=dev)
+    train_ws = torch.zeros(ops._ffi.query("skyrl_policy_train_workspace_bytes", mb, R), dtype=torch.uint8,
+                           device=dev)
     metrics_acc = torch.zeros(8, dtype=torch.float32, device=dev)
 
     def step(step_idx):
@@ -157,10 +167,11 @@ def run(args):
         sampler.seed = step_idx
         sh = torch.cuda.current_stream(dev).cuda_stream
         for t in range(R):
-            if full:
-                sampler.step_ptr(base_ptr + 2 * V * t, R * V, t, sh)
+            ptr, ld = (base_ptr + 2 * V * t, R * V) if full else (base_ptr + 2 * V * ((t * N) % (rows - N + 1)), V)
+            if t % 64 == 0:  # event-timed sample of the decode-step launches
+                sample_timer.wrap(lambda: sampler.step_ptr(ptr, ld, t, sh))
             else:
-                sampler.step_ptr(base_ptr + 2 * V * ((t * N) % (rows - N + 1)), V, t, sh)
+                sampler.step_ptr(ptr, ld, t, sh)
         # ---- pack ragged rollout output into the padded training tensors
         seqs, att, rmask, rew, lmask, rlp = ops.pack_experience(
             data["ptok"], data["poff"], data["rtok"], data["roff"], data["rew"], data["roff"], data["lmask"],
@@ -172,30 +183,37 @@ def run(args):
             x = lg_rows(s, mb)
             lab = labels[s:s + mb]
             for out in (ref_lp, old_lp):
-                ops._ffi.call("skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
-                              ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None,
-                              ops._stream(dev))
+                fwd_timer.wrap(lambda: ops._ffi.call(
+                    "skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V, ops._ptr(lab),
+                    lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None, ops._stream(dev)))
         # ---- GRPO advantage over the whole batch
         adv = ops.grpo_advantage(rew, rmask, goff, grows, ng)
-        # ---- update: per micro-batch logprob+entropy fwd, fused loss fwd/bwd, logprob bwd
+        # ---- update: per micro-batch fused policy pass (logprob/entropy fwd + PPO/KL loss +
+        #      logprob bwd -> dlogits); --unfused runs the four separate kernels instead
         metrics_acc.zero_()
-        lp = torch.empty((mb, R), dtype=torch.float32, device=dev)
-        ent = torch.empty_like(lp)
-        lse = torch.empty_like(lp)
         for s in range(0, N, mb):
             x = lg_rows(s, mb)
             lab = labels[s:s + mb]
-            fwd_timer.wrap(lambda: ops._ffi.call(
-                "skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V, ops._ptr(lab),
-                lab.stride(0), lab.stride(1), 1.0, ops._ptr(lp), ops._ptr(ent), ops._ptr(lse), ops._stream(dev)))
-            lpr = lp.detach().requires_grad_(True)
-            loss, m = ops.ppo_loss(lpr, old_lp[s:s + mb], adv[s:s + mb], lmask[s:s + mb], params,
-                                   ref_log_probs=ref_lp[s:s + mb], entropy=ent)
-            (glp,) = torch.autograd.grad(loss, lpr)
-            ops._ffi.call("skyrl_logprob_bwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
-                          ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(lse), ops._ptr(ent),
-                          ops._ptr(glp), None, ops._ptr(dlogits), ops._stream(dev))
-            metrics_acc.add_(m)
+            if args.unfused:
+                fwd_timer.wrap(lambda: ops._ffi.call(
+                    "skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V, ops._ptr(lab),
+                    lab.stride(0), lab.stride(1), 1.0, ops._ptr(lp), ops._ptr(ent), ops._ptr(lse), ops._stream(dev)))
+                lpr = lp.detach().requires_grad_(True)
+                loss, m = ops.ppo_loss(lpr, old_lp[s:s + mb], adv[s:s + mb], lmask[s:s + mb], params,
+                                       ref_log_probs=ref_lp[s:s + mb], entropy=ent)
+                (glp,) = torch.autograd.grad(loss, lpr)
+                ops._ffi.call("skyrl_logprob_bwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
+                              ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(lse), ops._ptr(ent),
+                              ops._ptr(glp), None, ops._ptr(dlogits), ops._stream(dev))
+                metrics_acc.add_(m)
+            else:
+                train_timer.wrap(lambda: ops._ffi.call(
+                    "skyrl_policy_train_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
+                    ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(old_lp[s:s + mb]),
+                    ops._ptr(adv[s:s + mb]), ops._ptr(lmask[s:s + mb]), ops._ptr(ref_lp[s:s + mb]),
+                    ctypes.byref(params), ops._ptr(loss_buf), ops._ptr(met_buf), ops._ptr(lp), ops._ptr(ent),
+                    ops._ptr(dlogits), ops._ptr(train_ws), ops._stream(dev)))
+                metrics_acc.add_(met_buf)
         if world > 1:
             dist.all_reduce(metrics_acc)
         return metrics_acc
@@ -208,7 +226,8 @@ def run(args):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    fwd_timer.active = True
+    for tm in timers:
+        tm.active = True
     t0 = time.perf_counter()
     for k in range(args.steps):
         m = step(1000 + k)
@@ -218,7 +237,8 @@ def run(args):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    fwd_timer.active = False
+    for tm in timers:
+        tm.active = False
     mvals = m.tolist()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -227,11 +247,25 @@ def run(args):
     ms_per_step = elapsed / args.steps * 1e3
     value = N * world * args.steps / elapsed
 
-    # roofline of the dominant kernel: algorithmic bytes per launch / average launch time
+    # per-kernel roofline: algorithmic bytes per launch / average event-timed launch duration
     rows_per_launch = mb * R
-    fwd_bytes = rows_per_launch * (V * 2 + 8 + 4 * 3)
-    fwd_ms = fwd_timer.avg_ms()
-    achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
+    kernels = {}
+    for name, tm, nbytes, launches_per_step in (
+        ("skyrl_sample (sample_kernel<bf16,1>)", sample_timer, N * V * 2 + N * 16, R),
+        ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
+         2 * (N // mb) + (N // mb if args.unfused else 0)),
+        ("skyrl_policy_train_fwd (policy_train_resident_kernel)", train_timer,
+         rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb),
+    ):
+        if not tm.pairs:
+            continue
+        ms = tm.avg_ms()
+        kernels[name] = {"avg_launch_ms": round(ms, 4), "bytes_per_launch": int(nbytes),
+                         "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "ms_per_step": round(ms * launches_per_step, 2), "launches_timed": len(tm.pairs)}
+    dom_name = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+    dom = kernels[dom_name]
     result = {
         "metric": "trained samples/sec (rollout+update), Qwen2.5-1.5B GRPO at 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -253,17 +287,17 @@ def run(args):
             "final_loss_sum_last_step": round(mvals[0], 6),
         },
         "roofline": {
-            "kernel": "skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)",
+            "kernel": dom_name,
             "bound": "hbm",
-            "achieved": round(achieved, 1),
+            "achieved": dom["achieved_GBps"],
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "bytes_per_launch": fwd_bytes,
-            "avg_launch_ms": round(fwd_ms, 4),
-            "launches_timed": len(fwd_timer.pairs),
+            "frac": dom["frac"],
+            "traffic": pmc_traffic(dom_name, dom["bytes_per_launch"]),
+            "bytes_per_launch": dom["bytes_per_launch"],
+            "avg_launch_ms": dom["avg_launch_ms"],
         },
+        "kernels": kernels,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -272,6 +306,20 @@ def run(args):
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel_name, algorithmic_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
+    FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, KB -> B), or None if not profiled."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        table = json.load(f)
+    for key, rec in table.get("kernels", {}).items():
+        if key in kernel_name:
+            return rec.get("hbm_bytes_per_launch")
+    return None
 
 
 def cpu_baseline(args):
@@ -362,6 +410,7 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=16)
     ap.add_argument("--logits-rows", type=int, default=0, help="0 = the whole batch if HBM allows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-sampler-steps", type=int, default=64)
     ap.add_argument("--cpu-logprob-tokens", type=int, default=256)

@@ -43,7 +43,8 @@ const char* skyrl_last_error(void);
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
- * {0, 1} (non-temporal streaming loads of the logits). Not thread-safe.              */
+ * {0, 1} (non-temporal streaming loads of the logits), "train_resident" {0, 1} (fused
+ * training pass keeps the vocab row in registers vs re-reading it). Not thread-safe.  */
 int skyrl_tune(const char* key, int value);
 
 /* ---- a4: GRPO outcome advantage ----------------------------------------
@@ -170,6 +171,25 @@ int skyrl_logprob_bwd(const void* logits, int dtype, int64_t stride_b, int64_t s
                       int64_t lstride_b, int64_t lstride_t, float temperature, const float* lse,
                       const float* entropy, const float* grad_logp, const float* grad_entropy,
                       void* grad_logits, void* stream);
+
+/* ---- a2+a3+a6+a7 fused: the policy training pass ------------------------------
+ * One call per micro-batch replaces logprob fwd + fused loss fwd + loss bwd +
+ * logprob bwd (same values and gradients as those four, see policy_train.hip):
+ * logits bf16 [n,R,V] (row (b,t) at logits + b*stride_b + t*stride_t) -> loss_out[1],
+ * metrics_out[SKYRL_M_COUNT], logp_out/entropy_out f32 [n,R], and grad_logits bf16
+ * dense [n,R,V] = dL/dlogits for a unit upstream gradient (rescale with
+ * skyrl_scale_bf16_by_device_scalar when the upstream gradient is not 1).
+ * old/adv/mask/ref: f32 [n,R] contiguous. workspace: skyrl_policy_train_workspace_bytes. */
+size_t skyrl_policy_train_workspace_bytes(int32_t n, int32_t R);
+int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t n,
+                           int32_t R, int32_t V, const int64_t* labels, int64_t lstride_b,
+                           int64_t lstride_t, float temperature, const float* old_log_probs,
+                           const float* advantages, const float* loss_mask, const float* ref_log_probs,
+                           const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                           float* logp_out, float* entropy_out, void* grad_logits, void* workspace,
+                           void* stream);
+/* x[i] *= g[0] over a bf16 buffer; a no-op kernel when g[0] == 1. */
+int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream);
 
 /* ---- a1: rollout token sampling -----------------------------------------
  * Replaces the vLLM sampler behind VLLMInferenceEngine.generate

@@ -92,6 +92,32 @@ def main():
         _ffi.call("skyrl_tune", b"logprob_unroll", 4)
         _ffi.call("skyrl_tune", b"logprob_nt", 1)
 
+    if on("fused"):
+        from skyrl_amd import ppo_utils as pu
+
+        params = pu.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=True)
+        old = torch.randn((mb, R), device=dev, generator=gen) - 12
+        adv = torch.randn((mb, R), device=dev, generator=gen)
+        msk = torch.ones((mb, R), device=dev)
+        ref = old + 0.01
+        loss = torch.empty((), device=dev)
+        met = torch.empty(8, device=dev)
+        ws = torch.zeros(_ffi.query("skyrl_policy_train_workspace_bytes", mb, R), dtype=torch.uint8, device=dev)
+        import ctypes
+
+        def fused(x):
+            _ffi.call("skyrl_policy_train_fwd", ops._ptr(x), _ffi.BF16, x.stride(0), x.stride(1), mb, R, V,
+                      ops._ptr(labels), labels.stride(0), labels.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
+                      ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met), ops._ptr(lp),
+                      ops._ptr(ent), ops._ptr(dlog), ops._ptr(ws), st)
+        for resident in (1, 0):
+            _ffi.call("skyrl_tune", b"train_resident", resident)
+            ms = statistics.median(timeit(lambda: (fused(x0), fused(x1))) / 2 for _ in range(args.rounds))
+            res[f"policy_train_fused_resident{resident}"] = {
+                "ms": ms, "GBps_hbm_algorithmic": rows * (V * 4 + 40) / ms / 1e6,
+                "vs_unfused_bytes": rows * (V * 6) / ms / 1e6}
+        _ffi.call("skyrl_tune", b"train_resident", 1)
+
     if on("sample"):
         from skyrl_amd.config import SamplingParams
         from skyrl_amd.sampler import TokenSampler

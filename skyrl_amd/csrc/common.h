@@ -72,6 +72,32 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Wave-wide max broadcast as a wave-uniform value, without LDS: DPP quad_perm xor1/xor2 and
+// row_ror 4/8 give every lane its 16-lane row max (out-of-row sources keep -inf), then the
+// four row maxima are read with v_readlane. Requires all 64 lanes active.
+__device__ __forceinline__ float wave_max_uniform(float v) {
+    auto step = [](float x, int ctrl) -> float {
+        constexpr int kNegInf = (int)0xff800000u;
+        int y;
+        switch (ctrl) {  // dpp control must be an immediate
+            case 0: y = __builtin_amdgcn_update_dpp(kNegInf, __float_as_int(x), 0xB1, 0xF, 0xF, false); break;
+            case 1: y = __builtin_amdgcn_update_dpp(kNegInf, __float_as_int(x), 0x4E, 0xF, 0xF, false); break;
+            case 2: y = __builtin_amdgcn_update_dpp(kNegInf, __float_as_int(x), 0x124, 0xF, 0xF, false); break;
+            default: y = __builtin_amdgcn_update_dpp(kNegInf, __float_as_int(x), 0x128, 0xF, 0xF, false); break;
+        }
+        return fmaxf(x, __int_as_float(y));
+    };
+    v = step(v, 0);
+    v = step(v, 1);
+    v = step(v, 2);
+    v = step(v, 3);
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
 // Sum of NV values across a block of NW waves; result valid in every thread.
 // `lds` needs NW*NV floats. Deterministic (fixed tree).
 template <int NW, int NV>

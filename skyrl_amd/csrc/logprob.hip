@@ -312,12 +312,19 @@ int launch_bwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V
 }  // namespace skyrl
 
 using namespace skyrl;
+namespace skyrl {
+extern int g_train_resident;
+}
 
 extern "C" int skyrl_tune(const char* key, int value) {
     const std::string k = key ? key : "";
     if (k == "logprob_unroll") {
         SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: logprob_unroll must be 4 or 8");
         g_tune.unroll = value;
+        return SKYRL_OK;
+    }
+    if (k == "train_resident") {
+        g_train_resident = value != 0;
         return SKYRL_OK;
     }
     if (k == "logprob_nt") {

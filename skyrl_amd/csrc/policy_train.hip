@@ -1,0 +1,558 @@
+// Fused policy training pass (a2 + a3 + a6 + a7): logprob/entropy forward, the PPO
+// clipped loss + KL(ref) + entropy term, and the logprob backward in ONE sweep pair over
+// the vocabulary per token.
+//
+// Why fusable: for regular/dual_clip PPO the gradient of the micro-batch loss w.r.t.
+// logp_t is dl/dlogp(logp_t, old_t, adv_t) * m_t * scale(row), where scale depends only
+// on the loss mask (token_mean: 1/max(sum m,1); sequence_mean: 1/(n*max(row sum,1));
+// seq_mean_token_sum_norm: 1/(n*max_seq_len)), and the entropy-loss gradient is
+// -coef * m_t / max(sum m, 1); the KL term has no gradient (compute_approx_kl is
+// @torch.no_grad(), ppo_utils.py:87). So dlogits for a unit upstream gradient are known
+// as soon as the row's logsumexp is; a non-unit upstream gradient rescales them after.
+// Reference semantics: model_wrapper.py:313-370, ppo_utils.py:88-124,548-586,984-1009,
+// workers/worker.py:810-876, torch_utils.py:59-192.
+//
+// Launches per micro-batch:
+//   1. train_scales_kernel   (1 block): mask sums -> per-row gradient scale, D
+//   2. policy_train_kernel   (1 block of 1024 threads per token): sweep 1 reads the
+//      row from HBM (online max / sum-exp / entropy, label logit), the token's loss terms
+//      and gradient coefficients, sweep 2 re-reads the row -- 300 KB, issued right after
+//      sweep 1, with <= 2 rows in flight per CU (<= 154 MB chip-wide), so it is served by
+//      the 256 MB Infinity Cache -- and writes dlogits (bf16).
+//   3. train_epilogue_kernel (1 block): folds the per-token terms into the loss scalar
+//      and the metric vector (same layout as skyrl_ppo_loss_fwd).
+// HBM traffic per token: V*2 (read) + V*2 (write) vs V*2 + V*2 + V*2 unfused.
+#include "arrive.h"
+
+namespace skyrl {
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / kWave;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kDLow = -1.0e30f;
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float (&x)[8]) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        x[2 * k] = __uint_as_float(w[k] << 16);
+        x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+}
+
+struct St {
+    float m, s, w;
+};
+__device__ __forceinline__ void st_add8(St& st, const float (&x)[8]) {
+    float mx = x[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) mx = fmaxf(mx, x[k]);
+    const float mn = fmaxf(st.m, mx);
+    const float dy = fmaxf((st.m - mn) * kLog2e, kDLow);
+    const float a = fast_exp2(dy);
+    st.w = a * fmaf(dy, st.s, st.w);
+    st.s = a * st.s;
+    st.m = mn;
+    const float c = -mn * kLog2e;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float y = fmaxf(fmaf(x[k], kLog2e, c), kDLow);
+        const float e = fast_exp2(y);
+        st.s += e;
+        st.w = fmaf(e, y, st.w);
+    }
+}
+__device__ __forceinline__ void st_merge(St& a, const St& b) {
+    const float mn = fmaxf(a.m, b.m);
+    const float da = fmaxf((a.m - mn) * kLog2e, kDLow), db = fmaxf((b.m - mn) * kLog2e, kDLow);
+    const float ea = fast_exp2(da), eb = fast_exp2(db);
+    a.w = ea * fmaf(da, a.s, a.w) + eb * fmaf(db, b.s, b.w);
+    a.s = ea * a.s + eb * b.s;
+    a.m = mn;
+}
+
+__device__ __forceinline__ float approx_kl(float lp, float base, int kl_type) {
+    switch (kl_type) {
+        case 0: return lp - base;
+        case 1: return fabsf(lp - base);
+        case 2: { float d = lp - base; return 0.5f * (d * d); }
+        default: {
+            float kl = clampf(base - lp, -20.f, 20.f);
+            float r = expf(kl);
+            return clampf((r - kl) - 1.f, -10.f, 10.f);
+        }
+    }
+}
+
+// ppo_policy_loss per token with torch-autograd gradient semantics (see ppo_loss.hip).
+__device__ __forceinline__ void ppo_token(float lp, float old, float A, float lo, float hi, float c, int dual,
+                                          float& loss, float& dldlp, float& clip) {
+    const float delta = lp - old;
+    const float ratio = expf(clampf(delta, -20.f, 20.f));
+    const float dratio = (delta >= -20.f && delta <= 20.f) ? ratio : 0.f;
+    const float surr1 = ratio * A;
+    const float surr2 = clampf(ratio, lo, hi) * A;
+    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+    float l1, d1;
+    if (surr1 < surr2) { l1 = -surr1; d1 = -A; }
+    else if (surr2 < surr1) { l1 = -surr2; d1 = -A * inr; }
+    else { l1 = -surr1; d1 = -(0.5f * A + 0.5f * A * inr); }
+    clip = (-surr2 > -surr1) ? 1.f : 0.f;
+    loss = l1;
+    float d = d1;
+    if (dual && A < 0.f) {
+        const float pg3 = -A * c;
+        if (pg3 < l1) { loss = pg3; d = 0.f; }
+        else if (l1 == pg3) { d = 0.5f * d1; }
+    }
+    dldlp = d * dratio;
+}
+
+// ---- 1. mask statistics -> gradient scales -------------------------------------------
+// One wave per row (rows strided over the 16 waves); scal[0] = sum m,
+// scal[1] = entropy-gradient scale (-coef/max(sum m,1) or 0), scal[2] = 1/max(sum m,1).
+__global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __restrict__ mask, int n, int R,
+                                                                skyrl_ppo_params p, float* __restrict__ row_scale,
+                                                                float* __restrict__ scal) {
+    __shared__ double s_tot[kWaves];
+    const int lane = threadIdx.x & 63, w = threadIdx.x / kWave;
+    double tot = 0.0;
+    for (int b = w; b < n; b += kWaves) {
+        float acc = 0.f;
+        for (int t = lane; t < R; t += kWave) acc += mask ? mask[(int64_t)b * R + t] : 1.f;
+        acc = wave_sum(acc);
+        tot += acc;
+        if (lane == 0) {
+            const double mrow = acc > 1.f ? acc : 1.0;
+            if (p.loss_reduction == 1) row_scale[b] = (float)(1.0 / ((double)n * mrow));
+            else if (p.loss_reduction == 2) row_scale[b] = (float)(1.0 / ((double)n * (double)p.max_seq_len));
+        }
+    }
+    if (lane == 0) s_tot[w] = tot;
+    __syncthreads();
+    double all = 0.0;
+    for (int j = 0; j < kWaves; ++j) all += s_tot[j];
+    const double d = all > 1.0 ? all : 1.0;
+    if (threadIdx.x == 0) {
+        scal[0] = (float)all;
+        scal[1] = p.use_entropy_loss ? (float)(-(double)p.entropy_loss_coef / d) : 0.f;
+        scal[2] = (float)(1.0 / d);
+    }
+    if (p.loss_reduction == 0) {
+        const float sc = (float)(1.0 / d);
+        for (int b = threadIdx.x; b < n; b += kThreads) row_scale[b] = sc;
+    }
+}
+
+// ---- 2. fused sweep pair per token ------------------------------------------------------
+// tok[r*4 + {0,1,2,3}] = loss*m, clip*m, kl*m*m, ent*m
+__global__ __launch_bounds__(kThreads) void policy_train_kernel(
+    const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int64_t rows, int V,
+    const int64_t* __restrict__ labels, int64_t lsb, int64_t lst, float temp, bool has_t,
+    const float* __restrict__ old, const float* __restrict__ adv, const float* __restrict__ mask,
+    const float* __restrict__ ref, const float* __restrict__ row_scale, const float* __restrict__ scal,
+    skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out, float* __restrict__ tok,
+    uint16_t* __restrict__ dx) {
+    __shared__ St s_st[kWaves];
+    __shared__ float s_g[3];  // lse, g_lp, g_ent*... (see below)
+    __shared__ float s_h;
+    const int64_t r = blockIdx.x;
+    const int64_t b = r / R, t = r % R;
+    const uint16_t* row = logits + b * sb + t * st_;
+    uint16_t* out = dx + r * (int64_t)V;
+    const int lane = threadIdx.x & 63;
+    const int nvec = V / 8;
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(row) % 16) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0;
+    auto tval = [&](float x) { return has_t ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
+
+    // ---- sweep 1: online softmax state
+    St st{-3.402823466e38f, 0.f, 0.f};
+    int done = 0;
+    if (vec_ok) {
+        const uint4* rv = reinterpret_cast<const uint4*>(row);
+        int i = threadIdx.x;
+        for (; i + 3 * kThreads < nvec; i += 4 * kThreads) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = rv[i + u * kThreads];  // default policy: keep for sweep 2
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float x[8];
+                unpack8(v[u], x);
+                if (has_t) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x[k] = tval(x[k]);
+                }
+                st_add8(st, x);
+            }
+        }
+        for (; i < nvec; i += kThreads) {
+            float x[8];
+            unpack8(rv[i], x);
+            if (has_t) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] = tval(x[k]);
+            }
+            st_add8(st, x);
+        }
+        done = nvec * 8;
+    }
+    for (int v = done + threadIdx.x; v < V; v += kThreads) {
+        float x[8];
+        const float xv = tval(bf16_to_f32(row[v]));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = k == 0 ? xv : -INFINITY;
+        st_add8(st, x);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        St o{__shfl_xor(st.m, off, kWave), __shfl_xor(st.s, off, kWave), __shfl_xor(st.w, off, kWave)};
+        st_merge(st, o);
+    }
+    if (lane == 0) s_st[threadIdx.x / kWave] = st;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        St a = s_st[0];
+        for (int j = 1; j < kWaves; ++j) st_merge(a, s_st[j]);
+        const float logs = fast_log2(a.s) * kLn2;
+        const float lse = a.m + logs;
+        const float H = logs - kLn2 * (a.w / a.s);
+        const int64_t lab = labels[b * lsb + t * lst];
+        const float xl = (lab >= 0 && lab < V) ? tval(bf16_to_f32(row[lab])) : __builtin_nanf("");
+        const float lp = xl - lse;
+        const float m = mask ? mask[r] : 1.f;
+        const float lo = (float)(1.0 - (double)p.eps_clip_low), hi = (float)(1.0 + (double)p.eps_clip_high);
+        float loss, dl, clip;
+        ppo_token(lp, old[r], adv[r], lo, hi, p.clip_ratio_c, p.dual_clip, loss, dl, clip);
+        const float kl = p.use_kl_loss ? (approx_kl(lp, ref[r], p.kl_type) * m) * m : 0.f;
+        logp_out[r] = lp;
+        if (ent_out) ent_out[r] = H;
+        *reinterpret_cast<float4*>(tok + r * 4) = make_float4(loss * m, clip * m, kl, H * m);
+        s_g[0] = lse;
+        s_g[1] = (dl * m) * row_scale[b];        // dL/dlogp for unit upstream gradient
+        s_g[2] = scal[1] * m;                    // dL/dH
+        s_h = H;
+        (void)lab;
+    }
+    __syncthreads();
+    const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_h;
+    const int64_t lab = labels[b * lsb + t * lst];
+    const float inv_t = has_t ? 1.f / temp : 1.f;
+    auto grad = [&](float x, int64_t v) -> float {
+        const float lpv = x - L;
+        const float pv = fast_exp2(lpv * kLog2e);
+        float g = -glp * pv - gent * pv * (lpv + H);
+        if (v == lab) g += glp;
+        return has_t ? g * inv_t : g;
+    };
+    // ---- sweep 2: dlogits (row re-read is MALL-resident)
+    if (vec_ok) {
+        const uint4* rv = reinterpret_cast<const uint4*>(row);
+        uint4* ov = reinterpret_cast<uint4*>(out);
+        int i = threadIdx.x;
+        for (; i + 3 * kThreads < nvec; i += 4 * kThreads) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = ld_nt(rv + i + u * kThreads);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float x[8];
+                unpack8(v[u], x);
+                const int64_t v0 = (int64_t)(i + u * kThreads) * 8;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] = grad(tval(x[k]), v0 + k);
+                ov[i + u * kThreads] = make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
+                                                  pack_bf16x2(x[4], x[5]), pack_bf16x2(x[6], x[7]));
+            }
+        }
+        for (; i < nvec; i += kThreads) {
+            float x[8];
+            unpack8(ld_nt(rv + i), x);
+            const int64_t v0 = (int64_t)i * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = grad(tval(x[k]), v0 + k);
+            ov[i] = make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                               pack_bf16x2(x[6], x[7]));
+        }
+    }
+    for (int v = done + threadIdx.x; v < V; v += kThreads) out[v] = f32_to_bf16(grad(tval(bf16_to_f32(row[v])), v));
+}
+
+// ---- 2b. register-resident variant: the row is loaded ONCE into registers (NV 16-B
+// vectors per thread, 1024 threads: NV = 19 covers V <= 155,648, Qwen2.5's 151,936), so
+// sweep 2 needs no memory reads at all: HBM traffic per token is exactly V*2 read +
+// V*2 written. One 1024-thread block per CU (<= 128 VGPRs); the per-token scalars
+// (label logit, old/adv/mask/ref, row scale) are prefetched by thread 0 up front.
+template <int NT, int NV, bool HAS_T>
+__global__ __launch_bounds__(NT) void policy_train_resident_kernel(
+    const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int V, const int64_t* __restrict__ labels,
+    int64_t lsb, int64_t lst, float temp, const float* __restrict__ old, const float* __restrict__ adv,
+    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
+    const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
+    float* __restrict__ tok, uint16_t* __restrict__ dx) {
+    __shared__ St s_st[NT / 64];
+    __shared__ float s_g[4];
+    const int64_t r = blockIdx.x;
+    const int64_t b = r / R, t = r % R;
+    const uint16_t* row = logits + b * sb + t * st_;
+    uint16_t* out = dx + r * (int64_t)V;
+    const int lane = threadIdx.x & 63;
+    const int nvec = V / 8;
+    const uint4* rv = reinterpret_cast<const uint4*>(row);
+    auto tval = [&](float x) { return HAS_T ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
+
+    int64_t lab = 0;
+    float xl = 0.f, o_old = 0.f, o_adv = 0.f, o_m = 1.f, o_ref = 0.f, o_rs = 0.f, o_ge = 0.f;
+    if (threadIdx.x == 0) {  // prefetch the token's scalars behind the row loads
+        lab = labels[b * lsb + t * lst];
+        xl = (lab >= 0 && lab < V) ? bf16_to_f32(row[lab]) : __builtin_nanf("");
+        o_old = old[r];
+        o_adv = adv[r];
+        o_m = mask ? mask[r] : 1.f;
+        o_ref = p.use_kl_loss ? ref[r] : 0.f;
+        o_rs = row_scale[b];
+        o_ge = scal[1];
+    }
+    // Host guarantees (NV-1)*NT < nvec <= NV*NT: only the last vector can be out of range.
+    uint4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV - 1; ++k) v[k] = ld_nt(rv + threadIdx.x + k * NT);
+    {
+        const int idx = threadIdx.x + (NV - 1) * NT;
+        const bool ok = idx < nvec;
+        const uint4 t4 = ld_nt(rv + (ok ? idx : nvec - 1));
+        const uint32_t ninf = 0xff80ff80u;  // bf16 -inf pair: contributes e = 0
+        v[NV - 1] = make_uint4(ok ? t4.x : ninf, ok ? t4.y : ninf, ok ? t4.z : ninf, ok ? t4.w : ninf);
+    }
+    St st{-3.402823466e38f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        float x[8];
+        unpack8(v[k], x);  // padding vectors are bf16 -inf: contribute e = 0
+        if constexpr (HAS_T) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = tval(x[j]);
+        }
+        st_add8(st, x);
+        __builtin_amdgcn_sched_barrier(0);  // one vector at a time: bounds register pressure
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        St o{__shfl_xor(st.m, off, kWave), __shfl_xor(st.s, off, kWave), __shfl_xor(st.w, off, kWave)};
+        st_merge(st, o);
+    }
+    if (lane == 0) s_st[threadIdx.x / kWave] = st;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        St a = s_st[0];
+        for (int j = 1; j < NT / 64; ++j) st_merge(a, s_st[j]);
+        const float logs = fast_log2(a.s) * kLn2;
+        const float lse = a.m + logs;
+        const float H = logs - kLn2 * (a.w / a.s);
+        const float lp = tval(xl) - lse;
+        const float lo = (float)(1.0 - (double)p.eps_clip_low), hi = (float)(1.0 + (double)p.eps_clip_high);
+        float loss, dl, clip;
+        ppo_token(lp, o_old, o_adv, lo, hi, p.clip_ratio_c, p.dual_clip, loss, dl, clip);
+        const float kl = p.use_kl_loss ? (approx_kl(lp, o_ref, p.kl_type) * o_m) * o_m : 0.f;
+        logp_out[r] = lp;
+        if (ent_out) ent_out[r] = H;
+        *reinterpret_cast<float4*>(tok + r * 4) = make_float4(loss * o_m, clip * o_m, kl, H * o_m);
+        s_g[0] = lse;
+        s_g[1] = (dl * o_m) * o_rs;
+        s_g[2] = o_ge * o_m;
+        s_g[3] = H;
+        *reinterpret_cast<int64_t*>(&s_st[0]) = lab;  // broadcast the label through LDS
+    }
+    __syncthreads();
+    const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
+    lab = *reinterpret_cast<const int64_t*>(&s_st[0]);
+    const int lab32 = (lab >= 0 && lab < V) ? (int)lab : -1;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)  // new values: no reuse of sweep-1 unpacks across the barrier
+        asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
+    const float inv_t = HAS_T ? 1.f / temp : 1.f;
+    uint4* ov = reinterpret_cast<uint4*>(out);
+
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int idx = threadIdx.x + k * NT;
+        if (k < NV - 1 || idx < nvec) {
+            float x[8];
+            unpack8(v[k], x);
+            const int v0 = idx * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float lpv = tval(x[j]) - L;
+                const float pv = fast_exp2(lpv * kLog2e);
+                float g = -glp * pv - gent * pv * (lpv + H);
+                if (v0 + j == lab32) g += glp;
+                x[j] = HAS_T ? g * inv_t : g;
+            }
+            ov[idx] = make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                 pack_bf16x2(x[6], x[7]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ---- 3. loss scalar + metrics ---------------------------------------------------------
+// One wave per row: row sums of loss*m, kl*m*m, m -> sequence-level terms in fp64;
+// token-level sums (loss*m, clip*m, ent*m) folded over the block; same metric layout as
+// skyrl_ppo_loss_fwd.
+__global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* __restrict__ tok,
+                                                                  const float* __restrict__ mask, int n, int R,
+                                                                  skyrl_ppo_params p, const float* __restrict__ scal,
+                                                                  float* __restrict__ loss_out,
+                                                                  float* __restrict__ metrics) {
+    __shared__ double s_red[kWaves * 5];
+    const int lane = threadIdx.x & 63, w = threadIdx.x / kWave;
+    // per wave (lane 0): sum l*m, rows_pg, rows_kl; per lane: clip*m, ent*m
+    double tl = 0.0, rows_pg = 0.0, rows_kl = 0.0, tc = 0.0, te = 0.0;
+    for (int b = w; b < n; b += kWaves) {
+        float a0 = 0.f, a1 = 0.f, am = 0.f;
+        for (int t = lane; t < R; t += kWave) {
+            const float4 v = *reinterpret_cast<const float4*>(tok + ((int64_t)b * R + t) * 4);
+            a0 += v.x;
+            a1 += v.z;
+            tc += v.y;
+            te += v.w;
+            am += mask ? mask[(int64_t)b * R + t] : 1.f;
+        }
+        a0 = wave_sum(a0);
+        a1 = wave_sum(a1);
+        am = wave_sum(am);
+        const double mrow = am > 1.f ? am : 1.0;
+        tl += a0;
+        if (p.loss_reduction == 1) rows_pg += a0 / mrow;
+        else if (p.loss_reduction == 2) rows_pg += a0 / (double)p.max_seq_len;
+        rows_kl += a1 / mrow;
+    }
+    tc = wave_sum(tc);
+    te = wave_sum(te);
+    if (lane == 0) {
+        s_red[w * 5 + 0] = tl;
+        s_red[w * 5 + 1] = rows_pg;
+        s_red[w * 5 + 2] = rows_kl;
+        s_red[w * 5 + 3] = tc;
+        s_red[w * 5 + 4] = te;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double v[5] = {0, 0, 0, 0, 0};
+        for (int j = 0; j < kWaves; ++j)
+            for (int k = 0; k < 5; ++k) v[k] += s_red[j * 5 + k];
+        const double msum = scal[0] > 1.f ? (double)scal[0] : 1.0;
+        const float pg = p.loss_reduction == 0 ? (float)(v[0] / msum) : (float)(v[1] / (double)n);
+        const float kl = p.use_kl_loss ? (float)(v[2] / (double)n) : 0.f;
+        const float entropy = (float)(v[4] / msum);
+        float final_loss = pg + kl * p.kl_loss_coef;
+        if (p.use_entropy_loss) final_loss = final_loss - entropy * p.entropy_loss_coef;
+        loss_out[0] = final_loss;
+        metrics[SKYRL_M_FINAL_LOSS] = final_loss;
+        metrics[SKYRL_M_POLICY_LOSS] = pg;
+        metrics[SKYRL_M_ENTROPY] = entropy;
+        metrics[SKYRL_M_KL] = kl;
+        metrics[SKYRL_M_CLIP_RATIO] = (float)(v[3] / msum);
+        metrics[SKYRL_M_MASK_SUM] = scal[0];
+        metrics[6] = 0.f;
+        metrics[7] = 0.f;
+    }
+}
+
+// dlogits *= g (skipped when g == 1: the common loss.backward() case)
+__global__ void scale_bf16_kernel(const float* __restrict__ g, uint16_t* __restrict__ x, int64_t n) {
+    const float s = g[0];
+    if (s == 1.0f) return;
+    uint4* x4 = reinterpret_cast<uint4*>(x);
+    const int64_t n8 = n / 8;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        float v[8];
+        unpack8(x4[i], v);
+        x4[i] = make_uint4(pack_bf16x2(v[0] * s, v[1] * s), pack_bf16x2(v[2] * s, v[3] * s),
+                           pack_bf16x2(v[4] * s, v[5] * s), pack_bf16x2(v[6] * s, v[7] * s));
+    }
+    for (int64_t i = n8 * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = f32_to_bf16(bf16_to_f32(x[i]) * s);
+}
+
+}  // namespace
+
+int g_train_resident = 1;  // skyrl_tune("train_resident", 0/1)
+
+}  // namespace skyrl
+
+using namespace skyrl;
+
+extern "C" size_t skyrl_policy_train_workspace_bytes(int32_t n, int32_t R) {
+    return 256 + (size_t)n * 4 + 256 + (size_t)n * R * 16 + 256;
+}
+
+extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t n,
+                                      int32_t R, int32_t V, const int64_t* labels, int64_t lstride_b,
+                                      int64_t lstride_t, float temperature, const float* old_log_probs,
+                                      const float* advantages, const float* loss_mask, const float* ref_log_probs,
+                                      const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                                      float* logp_out, float* entropy_out, void* grad_logits, void* workspace,
+                                      void* stream) {
+    SKYRL_REQUIRE(params && logits && labels && old_log_probs && advantages && loss_out && metrics_out && logp_out &&
+                      grad_logits && workspace,
+                  "policy_train_fwd: null pointer");
+    SKYRL_REQUIRE(dtype == SKYRL_BF16, "policy_train_fwd: logits must be bf16");
+    SKYRL_REQUIRE(n > 0 && R > 0 && V > 0, "policy_train_fwd: bad sizes");
+    SKYRL_REQUIRE(temperature > 0.f, "policy_train_fwd: temperature must be > 0");
+    SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "policy_train_fwd: use_kl_loss needs ref_log_probs");
+    SKYRL_REQUIRE(params->loss_reduction >= 0 && params->loss_reduction <= 2, "policy_train_fwd: bad loss_reduction");
+    SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
+                  "policy_train_fwd: seq_mean_token_sum_norm needs max_seq_len");
+    char* w = reinterpret_cast<char*>(workspace);
+    float* scal = reinterpret_cast<float*>(w);
+    float* row_scale = reinterpret_cast<float*>(w + 256);
+    float* tok = reinterpret_cast<float*>(w + 256 + (((size_t)n * 4 + 255) / 256) * 256);
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(train_scales_kernel, dim3(1), dim3(kThreads), 0, s, loss_mask, n, R, *params, row_scale, scal);
+    int rc = check_launch("train_scales_kernel");
+    if (rc) return rc;
+    const bool has_t = temperature != 1.0f;
+    const int nvec = V / 8;
+    constexpr int kRT = 768, kRV = 25;  // 768 threads x 25 x 16 B: 147,456 < V <= 153,600 (Qwen2.5)
+    const bool resident_ok = g_train_resident && (V % 8) == 0 && nvec <= kRV * kRT && nvec > (kRV - 1) * kRT &&
+                             (reinterpret_cast<uintptr_t>(logits) % 16) == 0 && (stride_b % 8) == 0 &&
+                             (stride_t % 8) == 0 && (reinterpret_cast<uintptr_t>(grad_logits) % 16) == 0;
+    if (resident_ok) {
+        auto kern = has_t ? policy_train_resident_kernel<kRT, kRV, true> : policy_train_resident_kernel<kRT, kRV, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(kRT), 0, s,
+                           reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, V, labels, lstride_b,
+                           lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs, row_scale,
+                           scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits));
+    } else
+    hipLaunchKernelGGL(policy_train_kernel, dim3((unsigned)((int64_t)n * R)), dim3(kThreads), 0, s,
+                       reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, (int64_t)n * R, V, labels,
+                       lstride_b, lstride_t, temperature, has_t, old_log_probs, advantages, loss_mask, ref_log_probs,
+                       row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits));
+    rc = check_launch("policy_train_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
+                       loss_out, metrics_out);
+    return check_launch("train_epilogue_kernel");
+}
+
+extern "C" int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream) {
+    if (n == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(g && x && (reinterpret_cast<uintptr_t>(x) % 16) == 0, "scale_bf16: null/misaligned pointer");
+    int64_t blocks = (n / 8 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(scale_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), g,
+                       reinterpret_cast<uint16_t*>(x), n);
+    return check_launch("scale_bf16_kernel");
+}

@@ -30,7 +30,6 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
-constexpr float kGumbelMax = 17.0f;  // > -ln(-ln(1-2^-24)) = 16.64: bound for the skip test
 
 __host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     x ^= x >> 16;
@@ -175,7 +174,7 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
     const T* row = logits + (int64_t)row_i * ld;
     const int v_beg = split * chunk;
     const int v_end = min(V, v_beg + chunk);
-    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
+    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);  // per (seed, seq, step)
     constexpr bool greedy = MODE == 0;
     const bool use_topk = MODE == 2 && use_topk_rt;
     const bool use_minp = MODE == 2 && use_minp_rt;
@@ -184,8 +183,9 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
 
     // Per lane: best (score, index) over the elements it visits in ascending index order
     // (so a strict '>' keeps the lowest index on ties) and the raw online (max, sum-exp).
-    float best_s = -INFINITY;
+    float best_s = -INFINITY, wbest = -INFINITY;
     int best_i = 0x7fffffff;
+    const uint32_t key2 = hash32(key ^ 0x5bd1e995u);
     float m = -3.402823466e38f, s = 0.f;
     constexpr int VEC = 16 / sizeof(T);
     auto visit_vec = [&](const T (&raw)[VEC], int v0, int cnt) {
@@ -213,61 +213,71 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
                 }
             return;
         }
-        // Skip the vector when no element can win: fl(xs+g) <= fl(xs_max+17) <= best
-        // (inv_t > 0 keeps max(x)*inv_t == max(x*inv_t)); ties lose on index.
-        if (best_s != -INFINITY && vmax * inv_t + kGumbelMax <= best_s) return;
-        uint32_t hv = key ^ ((uint32_t)v0 * 0x9e3779b1u);
-        uint32_t hb = (uint32_t)v0 * 0x9e3779b1u;
+        // Element v's uniform is u = ((t16 << 8) | lo8 | 1) * 2^-24 with t16 = half (v & 1) of
+        // hash32(key ^ (v >> 1) * phi) (one hash per 2 elements) and lo8 = the top byte of
+        // hash32(key2 ^ v * phi), evaluated only for candidates. t16 alone bounds the noise:
+        // 1 - u > (65535 - t16) / 65536 and g = -ln(-ln u) <= -ln(1 - u), so with
+        // n = 65535 - t16 > 0, g <= 16 ln 2 - ln n <= (clz(n) - 15) ln 2 (g <= 16.64 for n = 0).
+        // An element is a candidate unless xs + bound + margin < wave best (strict: an equal
+        // exact score could still win on index); the margin 0.01 >> the det_ln error (~1e-5).
+        const uint32_t g0 = (uint32_t)v0 >> 1;
+        uint32_t hh[VEC / 2];
+#pragma unroll
+        for (int q = 0; q < VEC / 2; ++q) hh[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
+            const uint32_t t16 = (hh[k >> 1] >> (16 * (k & 1))) & 0xffffu;  // v0 % 8 == 0 on every path
+            const uint32_t nn = 65535u - t16;
+            const float gub = nn ? (float)(__builtin_clz(nn) - 15) * 0.6931472f + 0.01f : 17.0f;
             const float xs = x[k] * inv_t;
             bool keep = k < cnt;
             if constexpr (MODE == 2) {
                 if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
                 if (use_minp) keep = keep && xs >= mthr;
             }
-            hv = key ^ hb;
-            hb += 0x9e3779b1u;
-            const uint32_t r = hash32(hv);
-            const float u = (float)((r >> 8) | 1u) * 5.9604644775390625e-8f;
-            const float sc = xs + (-det_ln(-det_ln(u)));
-            if (keep && sc > best_s) {
-                best_s = sc;
-                best_i = v0 + k;
+            if (keep && !(xs + gub < wbest)) {  // candidate: exact Gumbel score
+                const uint32_t lo8 = hash32(key2 ^ ((uint32_t)(v0 + k) * 0x9e3779b1u)) >> 24;
+                const float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
+                const float sc = xs + (-det_ln(-det_ln(u)));
+                if (sc > best_s) {
+                    best_s = sc;
+                    best_i = v0 + k;
+                }
             }
         }
+        wbest = wave_max_uniform(best_s);  // wave-uniform running best: lifts the bar for every lane
     };
+    // Both loops run the same trip count in every thread (out-of-range slots are -inf
+    // padding with cnt = 0), so the wave-wide max inside visit_vec never reads an inactive lane.
     const bool vec_ok = (reinterpret_cast<uintptr_t>(row + v_beg) % 16) == 0;
     int v0 = v_beg;
     if (vec_ok) {
         const int nvec = (v_end - v_beg) / VEC;
         const uint4* rv = reinterpret_cast<const uint4*>(row + v_beg);
-        int i = threadIdx.x;
-        for (; i + 3 * kThreads < nvec; i += 4 * kThreads) {  // 4 x 16 B in flight per lane
+        for (int base = 0; base < nvec; base += 4 * kThreads) {  // 4 x 16 B in flight per lane
             uint4 pk[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) pk[u] = ld_stream(rv + i + u * kThreads);
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + u * kThreads + threadIdx.x;
+                pk[u] = i < nvec ? ld_stream(rv + i) : make_uint4(0u, 0u, 0u, 0u);
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
+                const int i = base + u * kThreads + threadIdx.x;
                 T vals[VEC];
                 __builtin_memcpy(vals, &pk[u], 16);
-                visit_vec(vals, v_beg + (i + u * kThreads) * VEC, VEC);
+                visit_vec(vals, v_beg + i * VEC, i < nvec ? VEC : 0);
             }
-        }
-        for (; i < nvec; i += kThreads) {
-            uint4 pk = ld_stream(rv + i);
-            T vals[VEC];
-            __builtin_memcpy(vals, &pk, 16);
-            visit_vec(vals, v_beg + i * VEC, VEC);
         }
         v0 = v_beg + nvec * VEC;
     }
-    // unaligned head or ragged tail: VEC-element groups, the last one partial
-    for (int g0 = v0 + threadIdx.x * VEC; g0 < v_end; g0 += kThreads * VEC) {
+    // unaligned rows or the ragged tail: VEC-element groups, the last one partial
+    for (int gb = v0; gb < v_end; gb += kThreads * VEC) {
+        const int g0 = gb + threadIdx.x * VEC;
+        const int cnt = max(0, min(VEC, v_end - g0));
         T vals[VEC];
-        const int cnt = min(VEC, v_end - g0);
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) vals[k] = k < cnt ? row[g0 + k] : row[g0];
+        for (int k = 0; k < VEC; ++k) vals[k] = k < cnt ? row[g0 + k] : row[v_beg];
         visit_vec(vals, g0, cnt);
     }
     Best best{best_s, best_i};

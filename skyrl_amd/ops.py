@@ -420,6 +420,59 @@ def logprobs_and_entropy(logits, labels, temperature: float = 1.0, compute_entro
     return LogprobEntropyFunction.apply(logits, labels, temperature, compute_entropy)
 
 
+# ---------------------------------------------------------------------------- fused training pass
+class PolicyTrainFunction(torch.autograd.Function):
+    """logits -> (loss, metrics, logp, entropy) with dlogits produced in the same pass.
+
+    Equivalent to logprobs_and_entropy + ppo_loss (+ their backward) for regular/dual_clip
+    PPO; gradients flow to `logits` only (logp/entropy are returned for logging).
+    """
+
+    @staticmethod
+    def forward(ctx, logits, labels, old_log_probs, advantages, loss_mask, ref_log_probs, params, temperature):
+        dev = _require_gpu(logits, labels, old_log_probs, advantages, loss_mask, ref_log_probs)
+        lg, nb, nt, V, sb, st, dt = _logits_view(logits.detach())
+        if dt != BF16:
+            raise TypeError("the fused training pass takes bf16 logits")
+        lab, lsb, lst = _labels_view(labels, nb, nt)
+        old = _f32c(old_log_probs.detach(), "old_log_probs")
+        adv = _f32c(advantages.detach(), "advantages")
+        mask = None if loss_mask is None else loss_mask.detach().to(torch.float32).contiguous()
+        ref = None if ref_log_probs is None else _f32c(ref_log_probs.detach(), "ref_log_probs")
+        for name, t in (("old_log_probs", old), ("advantages", adv), ("loss_mask", mask), ("ref_log_probs", ref)):
+            if t is not None and tuple(t.shape) != (nb, nt):
+                raise ValueError(f"{name} shape {tuple(t.shape)} != {(nb, nt)}")
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
+        logp = torch.empty((nb, nt), dtype=torch.float32, device=dev)
+        ent = torch.empty((nb, nt), dtype=torch.float32, device=dev)
+        dx = torch.empty((nb, nt, V), dtype=torch.bfloat16, device=dev)
+        ws = WORKSPACES.get(dev, "policy_train", _ffi.query("skyrl_policy_train_workspace_bytes", nb, nt))
+        _ffi.call(
+            "skyrl_policy_train_fwd", _ptr(lg), dt, sb, st, nb, nt, V, _ptr(lab), lsb, lst, float(temperature),
+            _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), ctypes.byref(params), _ptr(loss), _ptr(metrics),
+            _ptr(logp), _ptr(ent), _ptr(dx), _ptr(ws), _stream(dev),
+        )
+        ctx.in_shape = logits.shape
+        ctx.save_for_backward(dx)
+        ctx.mark_non_differentiable(metrics, logp, ent)
+        return loss, metrics, logp, ent
+
+    @staticmethod
+    def backward(ctx, g_loss, g_metrics, g_logp, g_ent):
+        (dx,) = ctx.saved_tensors
+        g = g_loss.detach().to(torch.float32).reshape(1).contiguous()
+        _ffi.call("skyrl_scale_bf16_by_device_scalar", _ptr(g), _ptr(dx), dx.numel(), _stream(dx.device))
+        return dx.reshape(ctx.in_shape), None, None, None, None, None, None, None
+
+
+def policy_train(logits, labels, old_log_probs, advantages, loss_mask, params, ref_log_probs=None,
+                 temperature: float = 1.0):
+    """Fused policy pass; returns (loss 0-d, metrics [8], logp [n,R], entropy [n,R])."""
+    return PolicyTrainFunction.apply(logits, labels, old_log_probs, advantages, loss_mask, ref_log_probs, params,
+                                     temperature)
+
+
 # ---------------------------------------------------------------------------- a1 sampler
 def sample(
     logits: torch.Tensor,

@@ -348,3 +348,73 @@ def test_sampler_odd_vocab_and_distribution(dev):
     tok, _ = ops.sample(small.to(dev), seed=99, seq_ids=torch.arange(20000, device=dev), step=0)
     freq = torch.bincount(tok.cpu().long(), minlength=4).float() / 20000
     close(freq, torch.softmax(small[0], -1), atol=0.015)
+
+
+# ------------------------------------------------------------------------------------------ fused training pass
+@pytest.mark.parametrize("red", ["token_mean", "sequence_mean", "seq_mean_token_sum_norm"])
+@pytest.mark.parametrize("use_ent", [False, True])
+def test_policy_train_fused_matches_unfused_and_oracle(dev, red, use_ent):
+    g = torch.Generator().manual_seed(31)
+    n, R, V = 3, 40, 4096
+    logits = (torch.randn(n, R, V, generator=g) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (n, R), generator=g)
+    lens = torch.tensor([40, 17, 1])
+    mask = (torch.arange(R)[None] < lens[:, None]).float()
+    lp0 = cpu_ref.logprobs_from_logits(logits, labels)
+    old = lp0 + 0.1 * torch.randn(n, R, generator=g)
+    ref = lp0 + 0.1 * torch.randn(n, R, generator=g)
+    adv = torch.randn(n, R, generator=g)
+    cfg = AlgorithmConfig(loss_reduction=red, max_seq_len=64, use_entropy_loss=use_ent, policy_loss_type="dual_clip")
+    params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=use_ent, has_entropy=True)
+    x = logits.to(dev).requires_grad_(True)
+    loss, m, lp, ent = ops.policy_train(x, labels.to(dev), old.to(dev), adv.to(dev), mask.to(dev), params,
+                                        ref_log_probs=ref.to(dev))
+    (loss * 2.0).backward()
+    # unfused HIP path
+    x2 = logits.to(dev).requires_grad_(True)
+    lp2, ent2 = ops.logprobs_and_entropy(x2, labels.to(dev), 1.0, compute_entropy=use_ent)
+    loss2, m2 = ops.ppo_loss(lp2, old.to(dev), adv.to(dev), mask.to(dev), params, ref_log_probs=ref.to(dev),
+                             entropy=ent2)
+    (loss2 * 2.0).backward()
+    close(lp, lp2, atol=1e-6)
+    close(ent, ent2, atol=1e-6)
+    close(loss, loss2, atol=1e-6)
+    close(m[:6], m2[:6], atol=1e-6)
+    close(x.grad, x2.grad, atol=1e-6, rtol=1e-2)
+    # CPU oracle: torch autograd through the restated reference path (fp32 math on the bf16 logits)
+    xc = logits.float().requires_grad_(True)
+    lpc = cpu_ref.logprobs_from_logits(xc, labels)
+    entc = cpu_ref.entropy_from_logits(xc)
+    final, mc = cpu_ref.policy_loss_assembly(lpc, old, adv, mask, ref, entc, use_entropy_loss=use_ent,
+                                             dual_clip=True, reduction=red, max_seq_len=64)
+    (final * 2.0).backward()
+    close(loss, final, atol=2e-5, rtol=1e-4)
+    close(lp, lpc, atol=1e-4)
+    close(x.grad, xc.grad, atol=2e-6, rtol=1e-2)  # dlogits stored in bf16
+
+
+@pytest.mark.parametrize("temp", [1.0, 0.8])
+def test_policy_train_resident_qwen_vocab(dev, temp):
+    """V = 151,936 takes the register-resident fused kernel; compare with the two-sweep kernel."""
+    g = torch.Generator().manual_seed(5)
+    n, R, V = 2, 6, 151936
+    logits = (torch.randn(n, R, V, generator=g) * 3).to(torch.bfloat16).to(dev)
+    labels = torch.randint(0, V, (n, R), generator=g).to(dev)
+    mask = torch.tensor([[1.0] * 6, [1.0] * 3 + [0.0] * 3], device=dev)
+    old = torch.randn(n, R, generator=g).to(dev) - 12
+    ref = old + 0.05
+    adv = torch.randn(n, R, generator=g).to(dev)
+    params = ppo_utils.ppo_params_from_config(AlgorithmConfig(use_entropy_loss=True), use_kl_loss=True,
+                                              use_entropy_loss=True, has_entropy=True)
+    outs = []
+    for resident in (1, 0):
+        ops._ffi.call("skyrl_tune", b"train_resident", resident)
+        x = logits.clone().requires_grad_(True)
+        loss, m, lp, ent = ops.policy_train(x, labels, old, adv, mask, params, ref_log_probs=ref, temperature=temp)
+        loss.backward()
+        outs.append((loss.detach(), m.clone(), lp, ent, x.grad))
+    ops._ffi.call("skyrl_tune", b"train_resident", 1)
+    for a, b in zip(outs[0], outs[1]):
+        close(a, b, atol=1e-6, rtol=1e-5)
+    lpc = cpu_ref.logprobs_from_logits(logits.cpu(), labels.cpu(), temperature=temp)
+    close(outs[0][2], lpc, atol=1e-4)
