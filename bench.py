@@ -39,6 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 P_MAX, R_MAX, PROMPTS, GROUP, VOCAB = 512, 1024, 64, 8, 151936
+QWEN_1_5B_PARAMS = 1_543_714_304  # Qwen2.5-1.5B, tied embeddings
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy ~6.3 TB/s
 
 
@@ -118,6 +119,19 @@ def run(args):
     R, V, mb = R_MAX, VOCAB, args.micro_batch
     data, uids = synth_inputs(dev, N, seed=1234 + rank)
 
+    # a12/a14 learner state: flat fp32 gradient of the policy (written by the transformer backward,
+    # outside the path: synthetic here), FSDP2-style sharded AdamW, bf16 rollout weights
+    from skyrl_amd import comm
+
+    reducer = opt = None
+    if args.params > 0:
+        reducer = comm.GradReducer(args.params, dev, bucket_bytes=args.bucket_mb << 20)
+        init = torch.empty(args.params, dtype=torch.float32, device=dev).normal_(0.0, 0.02)
+        opt = comm.ShardedAdamW(reducer, init, comm.AdamWConfig())
+        del init
+        reducer.grad.normal_(0.0, 1e-3)
+        torch.cuda.synchronize()
+
     # resident logits: all N*R response positions if HBM allows, else a pool reused round-robin
     free, _ = torch.cuda.mem_get_info(dev)
     row_bytes = V * 2
@@ -152,7 +166,8 @@ def run(args):
     fwd_timer = KernelTimer()
     train_timer = KernelTimer()
     sample_timer = KernelTimer()
-    timers = (fwd_timer, train_timer, sample_timer)
+    adam_timer = KernelTimer()
+    timers = (fwd_timer, train_timer, sample_timer, adam_timer)
     lp = torch.empty((mb, R), dtype=torch.float32, device=dev)
     ent = torch.empty_like(lp)
     lse = torch.empty_like(lp)
@@ -172,6 +187,8 @@ def run(args):
                 sample_timer.wrap(lambda: sampler.step_ptr(ptr, ld, t, sh))
             else:
                 sampler.step_ptr(ptr, ld, t, sh)
+        if opt is not None:  # in-flight weight sync: the previous step's all-gather overlapped the rollout
+            opt.wait_weights()
         # ---- pack ragged rollout output into the padded training tensors
         seqs, att, rmask, rew, lmask, rlp = ops.pack_experience(
             data["ptok"], data["poff"], data["rtok"], data["roff"], data["rew"], data["roff"], data["lmask"],
@@ -216,6 +233,13 @@ def run(args):
                 metrics_acc.add_(met_buf)
         if world > 1:
             dist.all_reduce(metrics_acc)
+        # ---- optimizer step (one mini-batch per step at 64 prompts): DP gradient reduce-scatter on
+        #      the comm stream, sharded clip + AdamW (one HIP pass, bf16 copy written in the same
+        #      pass), then the bf16 all-gather = learner -> rollout weight sync, left in flight
+        if opt is not None:
+            reducer.launch()
+            adam_timer.wrap(lambda: opt.step(n_micro=N // mb, zero_grad=False))
+            opt.sync_weights()
         return metrics_acc
 
     for w in range(args.warmup):
@@ -256,6 +280,8 @@ def run(args):
          2 * (N // mb) + (N // mb if args.unfused else 0)),
         ("skyrl_policy_train_fwd (policy_train_resident_kernel)", train_timer,
          rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb),
+        ("skyrl_adamw_step (sumsq + plan + adamw_update_kernel<shadow>)", adam_timer,
+         (reducer.layout.shard_numel * (4 + 30)) if reducer is not None else 0, 1),
     ):
         if not tm.pairs:
             continue
@@ -285,6 +311,8 @@ def run(args):
             "vocab": V, "micro_batch": mb, "parallelism": f"dp{world}",
             "logits_resident_rows": rows, "logits_full_batch_resident": full,
             "final_loss_sum_last_step": round(mvals[0], 6),
+            "policy_params": args.params, "grad_bucket_mb": args.bucket_mb,
+            "optimizer": "sharded AdamW (fp32 master, bf16 rollout copy), reduce-scatter + all-gather over RCCL",
         },
         "roofline": {
             "kernel": dom_name,
@@ -412,6 +440,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--params", type=int, default=QWEN_1_5B_PARAMS, help="policy parameter count (0: no optimizer leg)")
+    ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--cpu-sampler-steps", type=int, default=64)
     ap.add_argument("--cpu-logprob-tokens", type=int, default=256)
     args = ap.parse_args()

@@ -239,6 +239,37 @@ int skyrl_scale_and_sumsq(float* grads, int64_t n, float scale, float* sumsq_out
  * per-element gradient was produced by a forward kernel for unit upstream grad. */
 int skyrl_scale_by_device_scalar(const float* g, const float* in, float* out, int64_t n, void* stream);
 
+/* ---- a12/a14: optimizer step ---------------------------------------------
+ * Replaces PolicyWorkerBase.optim_step (workers/worker.py:900-925) ->
+ * FSDPStrategy.optimizer_step (distributed/fsdp_strategy.py:160-190): grads *=
+ * 1/n_micro, clip_grad_norm_(max_norm) (fsdp_utils.py:388-401), skip on a
+ * non-finite norm, torch AdamW (fsdp_strategy.py:284-296), over a flat fp32
+ * parameter shard. No host sync: the step counter and the plan live on device.
+ *   skyrl_sumsq        sumsq_out[0] = sum(x^2), deterministic (workspace:
+ *                      skyrl_sumsq_workspace_bytes(n)). Under DP sharding the
+ *                      caller all-reduces it (SUM) before the plan.
+ *   skyrl_adamw_plan   grad_norm_out[0] = sqrt(sumsq)*grad_scale (the returned
+ *                      grad_norm); clip coef; ++step_count unless non-finite;
+ *                      plan: skyrl_adamw_plan_floats() floats.
+ *   skyrl_adamw_update one pass over (param, grad, exp_avg, exp_avg_sq); when
+ *                      param_bf16 != NULL also writes the bf16 copy consumed by
+ *                      the rollout engine (colocated weight sync, a14). */
+typedef struct skyrl_adamw_params {
+    float lr, beta1, beta2, eps, weight_decay;
+    float max_grad_norm; /* <= 0: no clipping (grad_norm still reported) */
+    float grad_scale;    /* 1/(n_micro) x 1/(dp world if grads are SUM-reduced) */
+} skyrl_adamw_params;
+size_t skyrl_sumsq_workspace_bytes(int64_t n);
+int skyrl_sumsq(const float* x, int64_t n, float* sumsq_out, void* workspace, void* stream);
+size_t skyrl_adamw_plan_floats(void);
+int skyrl_adamw_plan(const float* sumsq, const skyrl_adamw_params* hp, int32_t* step_count, float* plan,
+                     float* grad_norm_out, void* stream);
+int skyrl_adamw_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_bf16,
+                       int64_t n, const float* plan, float beta1, float beta2, void* stream);
+/* y = bf16(x), round-to-nearest-even: the learner -> rollout weight copy when the
+ * optimizer ran without a bf16 shadow (FSDPWeightExtractor, fsdp_worker.py:30-87). */
+int skyrl_cast_bf16(const float* x, void* y, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,6 +47,20 @@ class PPOParams(ctypes.Structure):
     ]
 
 
+class AdamWParams(ctypes.Structure):
+    """Mirror of ``skyrl_adamw_params`` (include/skyrl_hip.h)."""
+
+    _fields_ = [
+        ("lr", ctypes.c_float),
+        ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float),
+        ("eps", ctypes.c_float),
+        ("weight_decay", ctypes.c_float),
+        ("max_grad_norm", ctypes.c_float),
+        ("grad_scale", ctypes.c_float),
+    ]
+
+
 class PackInputs(ctypes.Structure):
     """Mirror of ``skyrl_pack_inputs`` (include/skyrl_hip.h)."""
 
@@ -110,6 +124,12 @@ SIGNATURES = {
     ),
     "skyrl_scale_and_sumsq": (_INT, [_P, _I64, _F, _P, _P]),
     "skyrl_scale_by_device_scalar": (_INT, [_P, _P, _P, _I64, _P]),
+    "skyrl_sumsq_workspace_bytes": (_SZ, [_I64]),
+    "skyrl_sumsq": (_INT, [_P, _I64, _P, _P, _P]),
+    "skyrl_adamw_plan_floats": (_SZ, []),
+    "skyrl_adamw_plan": (_INT, [_P, ctypes.POINTER(AdamWParams), _P, _P, _P, _P]),
+    "skyrl_adamw_update": (_INT, [_P, _P, _P, _P, _P, _I64, _P, _F, _F, _P]),
+    "skyrl_cast_bf16": (_INT, [_P, _P, _I64, _P]),
 }
 
 _lock = threading.Lock()

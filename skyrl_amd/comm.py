@@ -1,0 +1,412 @@
+"""a12–a14: the learner's data-parallel exchanges over RCCL (xGMI), one process per GPU.
+
+Reference call sites (skyrl-train/skyrl_train/):
+  a12 DP gradient reduce   FSDP2 reduce-scatter, fp32 reduce dtype (distributed/fsdp_strategy.py:216-226,
+                           253-271), 1/n_micro scaling (workers/worker.py:900-925), clip
+                           (distributed/fsdp_utils.py:388-401), AdamW (fsdp_strategy.py:284-296)
+  a13 metric all-reduce    workers/worker_utils.py:25-35 -> distributed/strategy.py:70-95 (one
+                           collective per scalar, mean = pre-divide + SUM)
+  a14 weight sync          weight_sync/broadcast_strategy.py:98-191 (per-parameter broadcast + RPC),
+                           weight_sync/base.py (WeightChunk / WeightUpdateRequest),
+                           workers/fsdp/fsdp_worker.py:201-228 (learner -> rollout)
+
+MI355X design:
+  * The flat fp32 gradient is cut into buckets (default 256 MiB: xGMI rings are per-link
+    bound, so few large collectives beat many small ones). Each bucket is reduce-scattered
+    on a dedicated comm stream as soon as the compute stream marks it ready, so the
+    exchange overlaps whatever the compute stream does next.
+  * The optimizer is sharded like FSDP2: rank r owns piece r of every bucket. Its master
+    fp32 weights, Adam moments and gradient shard are one contiguous buffer in that
+    bucket-interleaved order, so one HIP launch updates the whole shard (skyrl_adamw_*).
+  * The same update pass writes the bf16 copy of the shard; per-bucket all-gathers of it
+    ARE the colocated learner -> rollout weight sync (a14) -- no separate extraction
+    pass and no per-parameter RPC.
+  * Metrics: every mean goes into one packed SUM all-reduce, min and max share one MAX
+    all-reduce (min x = -max -x): two collectives per call instead of one per scalar.
+  * Separated placement (rollout GPUs outside the learner group): parameters are packed
+    into ~1 GiB bf16 chunks and broadcast once per chunk (BroadcastWeightSender /
+    BroadcastWeightReceiver), receivers get zero-copy views of the chunk buffer.
+
+Everything here is stream-ordered: no host synchronisation except where the reference
+itself reads a scalar (grad_norm().item() in optim_step).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import asdict, dataclass
+from typing import Callable, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_BUCKET_BYTES = 256 << 20
+_ALIGN = 64  # elements: keeps every shard piece 256-B aligned for the 16-B vector kernels
+
+
+def _world(group) -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+# ------------------------------------------------------------------------------------ a13
+def all_reduce_metrics(metrics: Dict[str, float], group=None, device=None) -> Dict[str, float]:
+    """Mirror of ``all_reduce_metrics`` (worker_utils.py:25-35): keys ending in ``_min`` are
+    min-reduced, ``_max`` max-reduced, the rest averaged over ranks. Two collectives total."""
+    world, _ = _world(group)
+    if world == 1 or not metrics:
+        return {k: float(v) for k, v in metrics.items()}
+    keys = list(metrics)
+    mean_keys = [k for k in keys if not (k.endswith("_min") or k.endswith("_max"))]
+    ext_keys = [k for k in keys if k.endswith("_min") or k.endswith("_max")]
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    out: Dict[str, float] = {}
+    if mean_keys:
+        t = torch.tensor([float(metrics[k]) for k in mean_keys], dtype=torch.float32, device=device)
+        t /= world  # strategy.py:85-87: pre-divide, then SUM
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        out.update(zip(mean_keys, t.tolist()))
+    if ext_keys:
+        sign = [-1.0 if k.endswith("_min") else 1.0 for k in ext_keys]
+        t = torch.tensor([s * float(metrics[k]) for s, k in zip(sign, ext_keys)], dtype=torch.float32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        out.update({k: s * v for s, k, v in zip(sign, ext_keys, t.tolist())})
+    return {k: out[k] for k in keys}
+
+
+# ------------------------------------------------------------------------------------ a12
+class FlatLayout:
+    """Flat parameter index space cut into buckets, each a multiple of world * _ALIGN elements.
+
+    Shard layout: rank r owns piece r of every bucket, concatenated in bucket order.
+    """
+
+    def __init__(self, numel: int, world: int, bucket_numel: int):
+        if numel <= 0:
+            raise ValueError("numel must be positive")
+        unit = world * _ALIGN
+        self.numel = numel
+        self.world = world
+        self.padded = int(math.ceil(numel / unit) * unit)
+        bucket_numel = max(unit, (bucket_numel // unit) * unit)
+        self.buckets: List[Tuple[int, int]] = []
+        s = 0
+        while s < self.padded:
+            e = min(self.padded, s + bucket_numel)
+            self.buckets.append((s, e))
+            s = e
+        self.shard_numel = self.padded // world
+        # shard offset of each bucket's piece
+        self.piece_off = []
+        off = 0
+        for s, e in self.buckets:
+            self.piece_off.append(off)
+            off += (e - s) // world
+
+    def piece(self, b: int, rank: int) -> Tuple[int, int]:
+        """Global [start, end) of bucket b's piece owned by rank."""
+        s, e = self.buckets[b]
+        n = (e - s) // self.world
+        return s + rank * n, s + (rank + 1) * n
+
+    def shard_index(self, rank: int) -> torch.Tensor:
+        """Global flat index of every element of rank's shard (int64), in shard order."""
+        parts = [torch.arange(*self.piece(b, rank), dtype=torch.int64) for b in range(len(self.buckets))]
+        return torch.cat(parts)
+
+
+class GradReducer:
+    """Bucketed DP gradient reduction on a side stream (a12).
+
+    ``grad`` is the flat fp32 gradient buffer the model's ``.grad`` tensors view. After the
+    last micro-batch, :meth:`launch` reduce-scatters every bucket (SUM) on the comm stream
+    into ``grad_shard``; :meth:`wait` makes the current stream wait for it. World size 1:
+    the shard is the gradient itself and nothing is launched.
+    """
+
+    def __init__(self, numel: int, device, group=None, bucket_bytes: int = DEFAULT_BUCKET_BYTES,
+                 dtype: torch.dtype = torch.float32):
+        self.group = group
+        self.world, self.rank = _world(group)
+        self.device = torch.device(device)
+        self.layout = FlatLayout(numel, self.world, bucket_bytes // torch.tensor([], dtype=dtype).element_size())
+        self.grad = torch.zeros(self.layout.padded, dtype=dtype, device=self.device)
+        if self.world > 1:
+            self.grad_shard = torch.zeros(self.layout.shard_numel, dtype=dtype, device=self.device)
+        else:
+            self.grad_shard = self.grad
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._done = None
+        self._works = []
+
+    def launch(self, buckets: Optional[Sequence[int]] = None) -> None:
+        """Reduce-scatter the given buckets (default: all) after the work already queued on the
+        current stream. Asynchronous with respect to the current stream."""
+        if self.world == 1:
+            return
+        lay = self.layout
+        idx = range(len(lay.buckets)) if buckets is None else buckets
+        if self.stream is not None:
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.device))
+            self.stream.wait_event(ready)
+            ctx = torch.cuda.stream(self.stream)
+        else:
+            ctx = _null_ctx()
+        with ctx:
+            for b in idx:
+                s, e = lay.buckets[b]
+                po = lay.piece_off[b]
+                out = self.grad_shard[po:po + (e - s) // self.world]
+                self._works.append(dist.reduce_scatter_tensor(out, self.grad[s:e], op=dist.ReduceOp.SUM,
+                                                              group=self.group, async_op=self.stream is None))
+            if self.stream is not None:
+                self._done = torch.cuda.Event()
+                self._done.record(self.stream)
+
+    def wait(self) -> None:
+        if self._done is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._done)
+            self._done = None
+        for w in self._works:
+            if w is not None and self.stream is None:
+                w.wait()
+        self._works = []
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+
+class _null_ctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+@dataclass
+class AdamWConfig:
+    """optimizer_config of the reference (ppo_base_config.yaml:37-44)."""
+
+    lr: float = 1e-6
+    betas: Tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 1e-2
+    max_grad_norm: float = 1.0
+
+
+class ShardedAdamW:
+    """FSDP2-style sharded AdamW whose update is one HIP pass per step (a12), writing the
+    bf16 rollout weights in the same pass and all-gathering them per bucket (a14).
+
+    ``step(n_micro)`` mirrors PolicyWorkerBase.optim_step: grads *= 1/n_micro (folded into
+    the update), DP mean (SUM reduce-scatter / world), clip at max_grad_norm, skip on a
+    non-finite norm, AdamW. Returns the pre-clip grad norm as a device scalar.
+    """
+
+    def __init__(self, reducer: GradReducer, init_params: torch.Tensor, config: AdamWConfig = AdamWConfig(),
+                 shadow_bf16: bool = True):
+        from . import _ffi
+        from .ops import _require_gpu
+
+        self._ffi = _ffi
+        dev = _require_gpu(reducer.grad)
+        self.reducer = reducer
+        self.cfg = config
+        lay = reducer.layout
+        if init_params.numel() != lay.numel:
+            raise ValueError(f"init_params has {init_params.numel()} elements, layout expects {lay.numel}")
+        flat = torch.zeros(lay.padded, dtype=torch.float32, device=dev)
+        flat[: lay.numel] = init_params.reshape(-1).to(device=dev, dtype=torch.float32)
+        if reducer.world > 1:
+            self.param = torch.cat([flat[slice(*lay.piece(b, reducer.rank))] for b in range(len(lay.buckets))])
+            del flat
+        else:
+            self.param = flat
+        self.exp_avg = torch.zeros_like(self.param)
+        self.exp_avg_sq = torch.zeros_like(self.param)
+        self.weights_bf16 = torch.empty(lay.padded, dtype=torch.bfloat16, device=dev) if shadow_bf16 else None
+        if shadow_bf16 and reducer.world == 1:
+            self.weights_bf16.copy_(flat)
+            self.shard_bf16 = self.weights_bf16
+        elif shadow_bf16:
+            self.shard_bf16 = self.param.to(torch.bfloat16)
+            self._all_gather_weights(sync=True)
+        else:
+            self.shard_bf16 = None
+        self.step_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.plan = torch.zeros(int(_ffi.query("skyrl_adamw_plan_floats")), dtype=torch.float32, device=dev)
+        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._ws = torch.zeros(int(_ffi.query("skyrl_sumsq_workspace_bytes", lay.shard_numel)), dtype=torch.uint8,
+                               device=dev)
+        self._dev = dev
+        self._gathered = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self._dev).cuda_stream)
+
+    def step(self, n_micro: int = 1, lr: Optional[float] = None, zero_grad: bool = True) -> torch.Tensor:
+        from .ops import _ptr
+
+        cfg = self.cfg
+        r = self.reducer
+        r.wait()
+        g = r.grad_shard
+        self._ffi.call("skyrl_sumsq", _ptr(g), g.numel(), _ptr(self.sumsq), _ptr(self._ws), self._stream())
+        if r.world > 1:
+            dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=r.group)
+        hp = self._ffi.AdamWParams(float(cfg.lr if lr is None else lr), float(cfg.betas[0]), float(cfg.betas[1]),
+                                   float(cfg.eps), float(cfg.weight_decay), float(cfg.max_grad_norm),
+                                   1.0 / (max(1, n_micro) * r.world))
+        self._ffi.call("skyrl_adamw_plan", _ptr(self.sumsq), ctypes.byref(hp), _ptr(self.step_count), _ptr(self.plan),
+                       _ptr(self.grad_norm), self._stream())
+        self._ffi.call("skyrl_adamw_update", _ptr(self.param), _ptr(g), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
+                       _ptr(self.shard_bf16), self.param.numel(), _ptr(self.plan), float(cfg.betas[0]),
+                       float(cfg.betas[1]), self._stream())
+        if zero_grad:  # strategy.optimizer_step ends with optimizer.zero_grad()
+            r.zero_grad()
+        return self.grad_norm
+
+    def sync_weights(self) -> None:
+        """Start the learner -> rollout weight all-gather (bf16) on the comm stream; the rollout
+        side calls :meth:`wait_weights` before it reads ``weights_bf16``."""
+        if self.weights_bf16 is None or self.reducer.world == 1:
+            return
+        self._all_gather_weights(sync=False)
+
+    def wait_weights(self) -> None:
+        if self._gathered is not None:
+            torch.cuda.current_stream(self._dev).wait_event(self._gathered)
+            self._gathered = None
+
+    def _all_gather_weights(self, sync: bool) -> None:
+        r = self.reducer
+        lay = r.layout
+        stream = r.stream
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self._dev))
+        stream.wait_event(ready)
+        with torch.cuda.stream(stream):
+            for b, (s, e) in enumerate(lay.buckets):
+                po = lay.piece_off[b]
+                n = (e - s) // r.world
+                dist.all_gather_into_tensor(self.weights_bf16[s:e], self.shard_bf16[po:po + n], group=r.group)
+            self._gathered = torch.cuda.Event()
+            self._gathered.record(stream)
+        if sync:
+            self.wait_weights()
+
+
+# ------------------------------------------------------------------------------------ a14
+@dataclass
+class WeightChunk:
+    """Mirror of weight_sync/base.py WeightChunk: one or more parameters moved together."""
+
+    names: List[str]
+    dtypes: List[str]
+    shapes: List[List[int]]
+    tensors: List[torch.Tensor]
+
+    def __post_init__(self):
+        if len({len(self.names), len(self.dtypes), len(self.shapes), len(self.tensors)}) != 1:
+            raise ValueError("names, dtypes, shapes, tensors must have the same length")
+
+    def __len__(self):
+        return len(self.names)
+
+    @property
+    def total_numel(self) -> int:
+        return sum(int(t.numel()) for t in self.tensors)
+
+
+@dataclass
+class WeightUpdateRequest:
+    """Mirror of weight_sync/base.py WeightUpdateRequest (metadata only; data moves by broadcast)."""
+
+    names: List[str]
+    dtypes: List[str]
+    shapes: List[List[int]]
+
+    def __post_init__(self):
+        if len({len(self.names), len(self.dtypes), len(self.shapes)}) != 1:
+            raise ValueError(
+                f"names, dtypes, shapes must have the same length. Got names={len(self.names)}, "
+                f"dtypes={len(self.dtypes)}, shapes={len(self.shapes)}")
+
+    def __len__(self):
+        return len(self.names)
+
+    def to_json_dict(self):
+        return asdict(self)
+
+    @classmethod
+    def from_json_dict(cls, d):
+        return cls(**d)
+
+
+_DTYPES = {"torch.bfloat16": torch.bfloat16, "bfloat16": torch.bfloat16, "torch.float16": torch.float16,
+           "torch.float32": torch.float32, "float32": torch.float32}
+
+
+def pack_chunks(named: Iterable[Tuple[str, torch.Tensor]], chunk_bytes: int = 1 << 30,
+                dtype: torch.dtype = torch.bfloat16) -> Iterator[WeightChunk]:
+    """Group parameters into chunks of about ``chunk_bytes`` (reference IPC path packs 1 GB)."""
+    names, shapes, tensors, nbytes = [], [], [], 0
+    es = torch.tensor([], dtype=dtype).element_size()
+    for name, t in named:
+        if tensors and nbytes + t.numel() * es > chunk_bytes:
+            yield WeightChunk(names, [str(dtype)] * len(names), shapes, tensors)
+            names, shapes, tensors, nbytes = [], [], [], 0
+        names.append(name)
+        shapes.append(list(t.shape))
+        tensors.append(t)
+        nbytes += t.numel() * es
+    if tensors:
+        yield WeightChunk(names, [str(dtype)] * len(names), shapes, tensors)
+
+
+class BroadcastWeightSender:
+    """Separated placement: one broadcast per packed chunk from ``src`` over ``group``
+    (reference: per-parameter broadcast + barrier, broadcast_strategy.py:98-142)."""
+
+    def __init__(self, group=None, src: int = 0, dtype: torch.dtype = torch.bfloat16,
+                 on_request: Optional[Callable[[WeightUpdateRequest], None]] = None):
+        self.group, self.src, self.dtype, self.on_request = group, src, dtype, on_request
+
+    def send_chunks(self, chunks: Iterable[WeightChunk]) -> int:
+        """Returns the number of broadcasts issued."""
+        n = 0
+        for chunk in chunks:
+            req = WeightUpdateRequest(list(chunk.names), list(chunk.dtypes), [list(s) for s in chunk.shapes])
+            if self.on_request is not None:
+                self.on_request(req)
+            flat = torch.cat([t.detach().reshape(-1).to(self.dtype) for t in chunk.tensors])
+            dist.broadcast(flat, self.src, group=self.group)
+            n += 1
+        return n
+
+
+class BroadcastWeightReceiver:
+    """Receives one packed chunk per request and yields zero-copy per-parameter views."""
+
+    def __init__(self, model_dtype: torch.dtype = torch.bfloat16, group=None, src: int = 0, device=None):
+        self.dtype, self.group, self.src = model_dtype, group, src
+        self.device = device if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+
+    def receive_weights(self, request: WeightUpdateRequest) -> Iterator[Tuple[str, torch.Tensor]]:
+        for d in request.dtypes:
+            if _DTYPES.get(d, None) != self.dtype:
+                raise AssertionError(f"dtype mismatch: request {d}, model {self.dtype}")
+        sizes = [int(math.prod(s)) for s in request.shapes]
+        flat = torch.empty(sum(sizes), dtype=self.dtype, device=self.device)
+        dist.broadcast(flat, self.src, group=self.group)
+        off = 0
+        for name, shape, n in zip(request.names, request.shapes, sizes):
+            yield name, flat[off:off + n].view(shape)
+            off += n
