@@ -58,12 +58,12 @@ static float det_ln(float y) {
     return fmaf((float)e, 0.693147180559945f, z * p);
 }
 
-/* Element v's uniform: u = ((t16 << 8) | lo8 | 1) * 2^-24, t16 = half (v & 1) of
- * hash32(key ^ (v >> 1) * phi), lo8 = top byte of hash32(key2 ^ v * phi),
+/* Element v's uniform: u = ((t16 << 8) | lo8 | 1) * 2^-24, t16 = 65535 - h16 with h16 =
+ * half (v & 1) of hash32(key ^ (v >> 1) * phi), lo8 = top byte of hash32(key2 ^ v * phi),
  * key2 = hash32(key ^ 0x5bd1e995). g = -ln(-ln u). */
 static float gumbel(uint32_t key, uint32_t v) {
     uint32_t key2 = hash32(key ^ 0x5bd1e995u);
-    uint32_t t16 = (hash32(key ^ ((v >> 1) * 0x9e3779b1u)) >> (16 * (v & 1))) & 0xffffu;
+    uint32_t t16 = ((hash32(key ^ ((v >> 1) * 0x9e3779b1u)) >> (16 * (v & 1))) & 0xffffu) ^ 0xffffu;
     uint32_t lo8 = hash32(key2 ^ (v * 0x9e3779b1u)) >> 24;
     float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
     float E = -det_ln(u);

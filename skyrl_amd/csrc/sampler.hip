@@ -21,6 +21,8 @@
 // partials in split order (lowest index wins ties).
 #include "arrive.h"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace skyrl {
@@ -28,6 +30,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
+constexpr int kRowModeMinSeqs = 256;  // enough rows to fill the chip with one workgroup each
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -158,15 +161,19 @@ __global__ __launch_bounds__(kThreads) void sample_filter_kernel(const T* __rest
     if (threadIdx.x == 0) thr_key[blockIdx.x] = s_prefix;
 }
 
-// MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p
-template <typename T, int MODE>
-__global__ __launch_bounds__(kThreads) void sample_kernel(
+// MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p.
+// NT threads per workgroup. Grid (row, split): with one split the workgroup owns the whole
+// row and finishes it alone; with several, the last-arriving split folds the partials.
+template <typename T, int MODE, int NT>
+__global__ __launch_bounds__(NT) void sample_kernel(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     const uint32_t* __restrict__ thr_key, const float* __restrict__ row_max, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters) {
-    __shared__ Part s_part[kWaves];
+    constexpr int NW = NT / kWave;
+    __shared__ Part s_part[NW];
     __shared__ int s_last;
+    __shared__ float s_bar;  // best exact score found by any wave of this workgroup
     const int row_i = blockIdx.x;
     const int split = blockIdx.y;
     const int nsplit = gridDim.y;
@@ -180,105 +187,202 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
     const bool use_minp = MODE == 2 && use_minp_rt;
     const uint32_t tk = use_topk ? thr_key[row_i] : 0u;
     const float mthr = use_minp ? row_max[row_i] * inv_t + ln_min_p : 0.f;
+    if (!greedy) {
+        if (threadIdx.x == 0) s_bar = -INFINITY;
+        __syncthreads();
+    }
 
     // Per lane: best (score, index) over the elements it visits in ascending index order
     // (so a strict '>' keeps the lowest index on ties) and the raw online (max, sum-exp).
-    float best_s = -INFINITY, wbest = -INFINITY;
+    float best_s = -INFINITY;
     int best_i = 0x7fffffff;
     const uint32_t key2 = hash32(key ^ 0x5bd1e995u);
-    float m = -3.402823466e38f, s = 0.f;
+    // raw online (max, sum-exp) for the sampled token's logprob; finite start so that an
+    // all-padding vector never forms inf - inf
+    float m = -1e30f, s = 0.f;
+    // Gumbel candidate filter. Element v's noise g is bounded by its 16-bit hash half h16
+    // alone: u = ((t16 << 8) | lo8 | 1) 2^-24 with t16 = 65535 - h16, so 1 - u > h16 / 65536
+    // and g = -ln(-ln u) <= -ln(1 - u) < ln2 (16 - log2 h16) <= ln2 (143 - bits(float(h16)) 2^-23)
+    // (a float's bit pattern is a piecewise-linear lower bound of 2^23 (log2 + 127)). With
+    // margin 0.01 (>> the det_ln error) an element can beat an exact score `bar` already found
+    // in this row only if
+    //   x/T + 143 ln2 + 0.01 - ln2 2^-23 bits >= bar  <=>  x - (T ln2 2^-23) bits >= (bar - C) T,
+    // one fma and one compare per element. Decisions are unchanged: the filter only skips
+    // elements whose exact score is provably below a score already found.
+    const float temp = greedy ? 1.f : 1.0f / inv_t;
+    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    constexpr float kC = 143.0f * 0.6931471805599453f + 0.01f;
+    float thr = -INFINITY;   // (bar - C) * T, wave-uniform
+    bool seeded = greedy;    // first vector: one exact score per lane sets the bar
     constexpr int VEC = 16 / sizeof(T);
-    auto visit_vec = [&](const T (&raw)[VEC], int v0, int cnt) {
+
+    auto exact = [&](const float xk, uint32_t h16, int v) -> float {
+        const uint32_t t16 = h16 ^ 0xffffu;
+        const uint32_t lo8 = hash32(key2 ^ ((uint32_t)v * 0x9e3779b1u)) >> 24;
+        const float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
+        return xk * inv_t + (-det_ln(-det_ln(u)));
+    };
+    auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
+        const float wb = wave_max_uniform(best_s);
+        if (lane == 0 && wb > -INFINITY)
+            __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const float sb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar)));
+        thr = (fmaxf(wb, sb) - kC) * temp;
+    };
+    // lse of the raw logits over one vector (not on the decision path)
+    auto lse_vec = [&](const float (&x)[VEC], float vmax) {
+        const float mn = fmaxf(m, vmax);
+        s *= fast_exp2((m - mn) * kLog2e);
+        const float c = -mn * kLog2e;
+        float s0 = fast_exp2(fmaf(x[0], kLog2e, c)), s1 = fast_exp2(fmaf(x[1], kLog2e, c));
+#pragma unroll
+        for (int k = 2; k < VEC; k += 2) {
+            s0 += fast_exp2(fmaf(x[k], kLog2e, c));
+            s1 += fast_exp2(fmaf(x[k + 1], kLog2e, c));
+        }
+        s += s0 + s1;
+        m = mn;
+    };
+    // One vector of VEC elements starting at v0 (v0 % 8 == 0 on every path); cnt < VEC only on
+    // the ragged tail (FULL = false).
+    auto visit_vec = [&](const T (&raw)[VEC], int v0, int cnt, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
         float x[VEC];
-        float vmax = -INFINITY;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            x[k] = k < cnt ? to_f<T>(raw[k]) : -INFINITY;
-            vmax = fmaxf(vmax, x[k]);
-        }
-        {  // lse of the raw logits (logprob output; not on the decision path)
-            const float mn = fmaxf(m, vmax);
-            s = s * fast_exp2((m - mn) * kLog2e);
-            const float c = -mn * kLog2e;
+        for (int k = 0; k < VEC; ++k) x[k] = (FULL || k < cnt) ? to_f<T>(raw[k]) : -INFINITY;
+        float vmax = x[0];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) s += fast_exp2(x[k] * kLog2e + c);
-            m = mn;
-        }
+        for (int k = 1; k < VEC; ++k) vmax = fmaxf(vmax, x[k]);
+        lse_vec(x, vmax);
         if constexpr (greedy) {
+            if (vmax > best_s) {  // first index of the new maximum (ascending visit order)
+                int kk = VEC - 1;
 #pragma unroll
-            for (int k = 0; k < VEC; ++k)
-                if (x[k] > best_s) {
-                    best_s = x[k];
-                    best_i = v0 + k;
-                }
+                for (int k = VEC - 2; k >= 0; --k) kk = (x[k] == vmax) ? k : kk;
+                best_s = vmax;
+                best_i = v0 + kk;
+            }
             return;
         }
-        // Element v's uniform is u = ((t16 << 8) | lo8 | 1) * 2^-24 with t16 = half (v & 1) of
-        // hash32(key ^ (v >> 1) * phi) (one hash per 2 elements) and lo8 = the top byte of
-        // hash32(key2 ^ v * phi), evaluated only for candidates. t16 alone bounds the noise:
-        // 1 - u > (65535 - t16) / 65536 and g = -ln(-ln u) <= -ln(1 - u), so with
-        // n = 65535 - t16 > 0, g <= 16 ln 2 - ln n <= (clz(n) - 15) ln 2 (g <= 16.64 for n = 0).
-        // An element is a candidate unless xs + bound + margin < wave best (strict: an equal
-        // exact score could still win on index); the margin 0.01 >> the det_ln error (~1e-5).
         const uint32_t g0 = (uint32_t)v0 >> 1;
-        uint32_t hh[VEC / 2];
+        uint32_t hp[VEC / 2];
 #pragma unroll
-        for (int q = 0; q < VEC / 2; ++q) hh[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
+        for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
+        auto h16 = [&](int k) -> uint32_t { return (k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu); };
+        if (!seeded) {  // wave-uniform, once: exact score of each lane's largest admissible element
+            seeded = true;
+            float xb = -INFINITY;
+            int kb = -1;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                bool keep = FULL || k < cnt;
+                if constexpr (MODE == 2) {
+                    if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
+                    if (use_minp) keep = keep && x[k] * inv_t >= mthr;
+                }
+                if (keep && x[k] > xb) {
+                    xb = x[k];
+                    kb = k;
+                }
+            }
+            if (kb >= 0) {
+                uint32_t hb = 0;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) hb = (k == kb) ? h16(k) : hb;
+                const float sc = exact(xb, hb, v0 + kb);
+                if (sc > best_s) {
+                    best_s = sc;
+                    best_i = v0 + kb;
+                }
+            }
+            raise_bar();
+        }
+        bool cand[VEC];
+        uint64_t anym = 0;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            const uint32_t t16 = (hh[k >> 1] >> (16 * (k & 1))) & 0xffffu;  // v0 % 8 == 0 on every path
-            const uint32_t nn = 65535u - t16;
-            const float gub = nn ? (float)(__builtin_clz(nn) - 15) * 0.6931472f + 0.01f : 17.0f;
-            const float xs = x[k] * inv_t;
-            bool keep = k < cnt;
+            const float bits = (float)(int)__float_as_uint((float)h16(k));
+            bool keep = FULL || k < cnt;
             if constexpr (MODE == 2) {
                 if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
-                if (use_minp) keep = keep && xs >= mthr;
+                if (use_minp) keep = keep && x[k] * inv_t >= mthr;
             }
-            if (keep && !(xs + gub < wbest)) {  // candidate: exact Gumbel score
-                const uint32_t lo8 = hash32(key2 ^ ((uint32_t)(v0 + k) * 0x9e3779b1u)) >> 24;
-                const float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
-                const float sc = xs + (-det_ln(-det_ln(u)));
+            cand[k] = keep && fmaf(bits, -kT, x[k]) >= thr;
+            anym |= __builtin_amdgcn_ballot_w64(cand[k]);
+        }
+        if (anym == 0) return;  // wave-uniform: rare once the bar is up
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            if (cand[k]) {
+                const float sc = exact(x[k], h16(k), v0 + k);
                 if (sc > best_s) {
                     best_s = sc;
                     best_i = v0 + k;
                 }
             }
         }
-        wbest = wave_max_uniform(best_s);  // wave-uniform running best: lifts the bar for every lane
+        raise_bar();
     };
-    // Both loops run the same trip count in every thread (out-of-range slots are -inf
-    // padding with cnt = 0), so the wave-wide max inside visit_vec never reads an inactive lane.
+    const std::integral_constant<bool, true> kFull{};
+    const std::integral_constant<bool, false> kPart{};
     const bool vec_ok = (reinterpret_cast<uintptr_t>(row + v_beg) % 16) == 0;
     int v0 = v_beg;
     if (vec_ok) {
         const int nvec = (v_end - v_beg) / VEC;
         const uint4* rv = reinterpret_cast<const uint4*>(row + v_beg);
-        for (int base = 0; base < nvec; base += 4 * kThreads) {  // 4 x 16 B in flight per lane
+        constexpr int kStep = 4 * NT;  // 4 x 16 B per lane per iteration
+        const int nfull = (nvec / kStep) * kStep;
+        // full iterations, software-pipelined: the next iteration's loads are issued before the
+        // current one is processed
+        uint4 cur[4], nxt[4];
+        if (nfull > 0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
+        }
+        for (int base = 0; base < nfull; base += kStep) {
+            const bool more = base + kStep < nfull;
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                T vals[VEC];
+                __builtin_memcpy(vals, &cur[u], 16);
+                visit_vec(vals, v_beg + (base + u * NT + threadIdx.x) * VEC, VEC, kFull);
+            }
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+            }
+        }
+        // the partial iteration: same trip count in every thread (out-of-range slots are -inf
+        // padding with cnt = 0), so the wave-wide max inside visit_vec never reads an inactive lane
+        if (nfull < nvec) {
             uint4 pk[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int i = base + u * kThreads + threadIdx.x;
+                const int i = nfull + u * NT + threadIdx.x;
                 pk[u] = i < nvec ? ld_stream(rv + i) : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int i = base + u * kThreads + threadIdx.x;
+                const int i = nfull + u * NT + threadIdx.x;
                 T vals[VEC];
                 __builtin_memcpy(vals, &pk[u], 16);
-                visit_vec(vals, v_beg + i * VEC, i < nvec ? VEC : 0);
+                visit_vec(vals, v_beg + i * VEC, i < nvec ? VEC : 0, kPart);
             }
         }
         v0 = v_beg + nvec * VEC;
     }
     // unaligned rows or the ragged tail: VEC-element groups, the last one partial
-    for (int gb = v0; gb < v_end; gb += kThreads * VEC) {
+    for (int gb = v0; gb < v_end; gb += NT * VEC) {
         const int g0 = gb + threadIdx.x * VEC;
         const int cnt = max(0, min(VEC, v_end - g0));
         T vals[VEC];
 #pragma unroll
         for (int k = 0; k < VEC; ++k) vals[k] = k < cnt ? row[g0 + k] : row[v_beg];
-        visit_vec(vals, g0, cnt);
+        visit_vec(vals, g0, cnt, kPart);
     }
     Best best{best_s, best_i};
 
@@ -296,9 +400,10 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
     }
     if (lane == 0) s_part[threadIdx.x / kWave] = Part{best.score, best.idx, m, s};
     __syncthreads();
+    Part p;
     if (threadIdx.x == 0) {
-        Part p = s_part[0];
-        for (int j = 1; j < kWaves; ++j) {
+        p = s_part[0];
+        for (int j = 1; j < NW; ++j) {
             const Part q = s_part[j];
             Best b{p.score, p.idx};
             if (better(q.score, q.idx, b)) {
@@ -309,30 +414,32 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
             p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
             p.m = mn;
         }
-        float* dst = reinterpret_cast<float*>(parts + (int64_t)row_i * nsplit + split);
-        st_wt(dst + 0, p.score);
-        st_wt(reinterpret_cast<int*>(dst) + 1, p.idx);
-        st_wt(dst + 2, p.m);
-        st_wt(dst + 3, p.s);
     }
     if (nsplit > 1) {
+        if (threadIdx.x == 0) {
+            float* dst = reinterpret_cast<float*>(parts + (int64_t)row_i * nsplit + split);
+            st_wt(dst + 0, p.score);
+            st_wt(reinterpret_cast<int*>(dst) + 1, p.idx);
+            st_wt(dst + 2, p.m);
+            st_wt(dst + 3, p.s);
+        }
         if (!arrive_last(counters + row_i, (unsigned)nsplit, &s_last)) return;
-    } else {
-        __syncthreads();
+        if (threadIdx.x == 0) {
+            p = parts[(int64_t)row_i * nsplit];
+            for (int j = 1; j < nsplit; ++j) {
+                const Part q = parts[(int64_t)row_i * nsplit + j];
+                Best b{p.score, p.idx};
+                if (better(q.score, q.idx, b)) {
+                    p.score = q.score;
+                    p.idx = q.idx;
+                }
+                const float mn = fmaxf(p.m, q.m);
+                p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
+                p.m = mn;
+            }
+        }
     }
     if (threadIdx.x == 0) {
-        Part p = parts[(int64_t)row_i * nsplit];
-        for (int j = 1; j < nsplit; ++j) {
-            const Part q = parts[(int64_t)row_i * nsplit + j];
-            Best b{p.score, p.idx};
-            if (better(q.score, q.idx, b)) {
-                p.score = q.score;
-                p.idx = q.idx;
-            }
-            const float mn = fmaxf(p.m, q.m);
-            p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
-            p.m = mn;
-        }
         tokens[row_i] = p.idx;
         if (logp_out) {
             const float lse = p.m + fast_log2(p.s) * kLn2;
@@ -343,11 +450,26 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(
 }
 
 int splits_for(int nseq, int V) {
+    if (nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
     int s = (2048 + nseq - 1) / nseq;
     const int max_s = (V + 4095) / 4096;  // at least 4096 elements per split
     if (s > max_s) s = max_s;
     if (s > 64) s = 64;
     return s < 1 ? 1 : s;
+}
+
+template <typename T, int MODE>
+void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int64_t ld, int V, int chunk, float inv_t,
+                 int use_topk, int use_minp, float ln_min_p, uint64_t seed, const int64_t* seq_ids, int64_t step,
+                 const uint32_t* thr, const float* rmax, int32_t* tokens, float* logp, Part* parts,
+                 unsigned* counters) {
+    if (row_mode)
+        hipLaunchKernelGGL((sample_kernel<T, MODE, 512>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
+                           use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+    else
+        hipLaunchKernelGGL((sample_kernel<T, MODE, kThreads>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t,
+                           use_topk, use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts,
+                           counters);
 }
 
 template <typename T>
@@ -378,15 +500,16 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         if (rc) return rc;
     }
     const dim3 grid(nseq, nsplit);
+    const bool row_mode = nsplit == 1 && nseq >= kRowModeMinSeqs;
     if (greedy)
-        hipLaunchKernelGGL((sample_kernel<T, 0>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t, 0, 0,
-                           ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+        launch_mode<T, 0>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
+                          rmax, tokens, logp, parts, counters);
     else if (use_topk || use_minp)
-        hipLaunchKernelGGL((sample_kernel<T, 2>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
-                           use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+        launch_mode<T, 2>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, use_topk, use_minp, ln_min_p, seed, seq_ids,
+                          step, thr, rmax, tokens, logp, parts, counters);
     else
-        hipLaunchKernelGGL((sample_kernel<T, 1>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t, 0, 0,
-                           ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+        launch_mode<T, 1>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
+                          rmax, tokens, logp, parts, counters);
     return check_launch("sample_kernel");
 }
 

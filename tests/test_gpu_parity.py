@@ -336,6 +336,38 @@ def test_sampler_bit_exact_vs_oracle(dev, dtype, cfg):
         close(lp, torch.log_softmax(logits.float(), -1)[torch.arange(n), etok.long()], atol=1e-4)
 
 
+@pytest.mark.parametrize("cfg", [(1.0, -1, 0.0), (0.0, -1, 0.0), (0.6, 40, 0.02)])
+def test_sampler_row_mode_bit_exact(dev, cfg):
+    """nseq >= 256: one workgroup per row (no split hand-off), rows strided as in the decode loop."""
+    temp, top_k, min_p = cfg
+    g = torch.Generator().manual_seed(23)
+    n, V = 300, 32003
+    full = (torch.randn(n, 2, V, generator=g) * 2.5).to(torch.bfloat16)
+    ids = torch.arange(n, dtype=torch.int64) * 7
+    x = full.to(dev)[:, 1]  # row stride 2V, odd V: unaligned rows take the ragged path
+    tok, lp = ops.sample(x, temperature=temp, top_k=top_k, min_p=min_p, seed=5, seq_ids=ids.to(dev), step=3)
+    etok, elp = _oracle_sample(full[:, 1].contiguous(), temp, top_k, min_p, 5, ids, 3)
+    assert torch.equal(tok.cpu(), etok)
+    close(lp, elp, atol=1e-4)
+
+
+def test_sampler_extreme_logit_range(dev):
+    """Logits spanning +-3e4 (bf16) with a spike: the online sum-exp must not overflow."""
+    g = torch.Generator().manual_seed(4)
+    n, V = 260, 4096
+    logits = torch.randn(n, V, generator=g) * 50
+    logits[:, 3] = 3.0e4
+    logits[:, 100] = -3.0e4
+    logits[::2, 4000] = 3.1e4
+    logits = logits.to(torch.bfloat16)
+    for temp in (1.0, 0.0):
+        tok, lp = ops.sample(logits.to(dev), temperature=temp, seed=1, step=0)
+        etok, elp = _oracle_sample(logits, temp, -1, 0.0, 1, torch.arange(n), 0)
+        assert torch.equal(tok.cpu(), etok)
+        close(lp, torch.log_softmax(logits.float(), -1)[torch.arange(n), etok.long()], atol=1e-4)
+        assert torch.isfinite(lp).all()
+
+
 def test_sampler_odd_vocab_and_distribution(dev):
     g = torch.Generator().manual_seed(2)
     V = 1027
