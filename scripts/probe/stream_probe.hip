@@ -1,0 +1,29 @@
+// Streaming-floor probe (measurement only, not part of the product): reads nrows rows of V bf16
+// with the sampler's access pattern and does minimal work, to price launch + stream time.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__global__ __launch_bounds__(NT) void stream_rows(const uint16_t* x, int64_t ld, int V, int nsplit, uint32_t* out) {
+    const int row = blockIdx.x, split = blockIdx.y;
+    const int chunk = ((V + nsplit - 1) / nsplit + 15) & ~15;
+    const int vb = split * chunk, ve = min(V, vb + chunk);
+    const u32x4* r = reinterpret_cast<const u32x4*>(x + row * ld + vb);
+    const int nvec = (ve - vb) / 8;
+    uint32_t acc = 0;
+    for (int i = threadIdx.x; i < nvec; i += 4 * NT) {
+        u32x4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = (i + u * NT < nvec) ? __builtin_nontemporal_load(r + i + u * NT) : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc ^= a[u].x ^ a[u].y ^ a[u].z ^ a[u].w;
+    }
+    if (acc == 0x12345678u) out[row] = acc;
+}
+extern "C" int probe(const void* x, int64_t ld, int nrows, int V, int mode, void* out, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == 0) hipLaunchKernelGGL(stream_rows<512>, dim3(nrows, 1), dim3(512), 0, s, (const uint16_t*)x, ld, V, 1, (uint32_t*)out);
+    else if (mode == 1) hipLaunchKernelGGL(stream_rows<256>, dim3(nrows, 4), dim3(256), 0, s, (const uint16_t*)x, ld, V, 4, (uint32_t*)out);
+    else hipLaunchKernelGGL(stream_rows<1024>, dim3(nrows, 1), dim3(1024), 0, s, (const uint16_t*)x, ld, V, 1, (uint32_t*)out);
+    return (int)hipGetLastError();
+}

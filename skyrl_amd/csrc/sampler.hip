@@ -161,11 +161,12 @@ __global__ __launch_bounds__(kThreads) void sample_filter_kernel(const T* __rest
     if (threadIdx.x == 0) thr_key[blockIdx.x] = s_prefix;
 }
 
-// MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p.
+// MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p,
+// 3 Gumbel-max without filters at T == 1 (the bound test reuses the lse exponentials).
 // NT threads per workgroup. Grid (row, split): with one split the workgroup owns the whole
 // row and finishes it alone; with several, the last-arriving split folds the partials.
 template <typename T, int MODE, int NT>
-__global__ __launch_bounds__(NT) void sample_kernel(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     const uint32_t* __restrict__ thr_key, const float* __restrict__ row_max, int32_t* __restrict__ tokens,
@@ -213,6 +214,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(
     const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
     constexpr float kC = 143.0f * 0.6931471805599453f + 0.01f;
     float thr = -INFINITY;   // (bar - C) * T, wave-uniform
+    float bar = -INFINITY;   // best exact score known to this wave (wave-uniform)
     bool seeded = greedy;    // first vector: one exact score per lane sets the bar
     constexpr int VEC = 16 / sizeof(T);
 
@@ -222,26 +224,77 @@ __global__ __launch_bounds__(NT) void sample_kernel(
         const float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
         return xk * inv_t + (-det_ln(-det_ln(u)));
     };
+    // MODE 3 (T == 1) bound in multiplicative form, reusing the lse exponentials ex = e^(x - m):
+    // nn <= 65536 e^(x - bar + 0.01) <=> nn <= ex * Q, Q = 2^16 e^(m - bar + 0.01) per lane.
+    // While some lane has m - bar > 70 (Q near overflow; an ex that underflowed, x < m - 87,
+    // could then still matter) the wave falls back to the additive bits form (qbad). Q is
+    // clamped below at FLT_MIN so that an overflowed ex (inf) stays a candidate.
+    float Q = 0.f;
+    bool qbad = true;
+    auto recompute_q = [&]() {
+        const float d = m - bar + 0.01f;
+        Q = fmaxf(fast_exp2(fmaf(fminf(d, 70.f), kLog2e, 16.0f)), 1.17549435e-38f);
+        qbad = __builtin_amdgcn_ballot_w64(!(d <= 70.f)) != 0;
+    };
     auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
         const float wb = wave_max_uniform(best_s);
         if (lane == 0 && wb > -INFINITY)
             __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const float sb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar)));
-        thr = (fmaxf(wb, sb) - kC) * temp;
+        bar = fmaxf(wb, sb);
+        thr = (bar - kC) * temp;
+        if constexpr (MODE == 3) recompute_q();
     };
-    // lse of the raw logits over one vector (not on the decision path)
-    auto lse_vec = [&](const float (&x)[VEC], float vmax) {
+    // once per wave, before any filtering: the exact score of each lane's largest admissible
+    // element of its first vector sets the bar (one exact evaluation per lane instead of VEC)
+    auto seed_vec = [&](const T (&raw)[VEC], const float (&x)[VEC], const uint32_t (&hp)[VEC / 2], int v0, int cnt) {
+        seeded = true;
+        float xb = -INFINITY;
+        int kb = -1;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            bool keep = k < cnt;
+            if constexpr (MODE == 2) {
+                if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
+                if (use_minp) keep = keep && x[k] * inv_t >= mthr;
+            }
+            if (keep && x[k] > xb) {
+                xb = x[k];
+                kb = k;
+            }
+        }
+        if (kb >= 0) {
+            uint32_t hb = 0;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) hb = (k == kb) ? ((k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu)) : hb;
+            const float sc = exact(xb, hb, v0 + kb);
+            if (sc > best_s) {
+                best_s = sc;
+                best_i = v0 + kb;
+            }
+        }
+        raise_bar();
+    };
+    // lse of the raw logits over one vector (not on the decision path); leaves exp(x - mn) in ex
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    auto lse_vec = [&](const float (&x)[VEC], float vmax, float (&ex)[VEC]) -> float {
         const float mn = fmaxf(m, vmax);
         s *= fast_exp2((m - mn) * kLog2e);
-        const float c = -mn * kLog2e;
-        float s0 = fast_exp2(fmaf(x[0], kLog2e, c)), s1 = fast_exp2(fmaf(x[1], kLog2e, c));
+        const f32x2 c2 = {-mn * kLog2e, -mn * kLog2e};
+        const f32x2 l2 = {kLog2e, kLog2e};
+        f32x2 acc = {0.f, 0.f};
 #pragma unroll
-        for (int k = 2; k < VEC; k += 2) {
-            s0 += fast_exp2(fmaf(x[k], kLog2e, c));
-            s1 += fast_exp2(fmaf(x[k + 1], kLog2e, c));
+        for (int k = 0; k < VEC; k += 2) {
+            const f32x2 xv = {x[k], x[k + 1]};
+            const f32x2 y = __builtin_elementwise_fma(xv, l2, c2);
+            ex[k] = fast_exp2(y.x);
+            ex[k + 1] = fast_exp2(y.y);
+            const f32x2 e2 = {ex[k], ex[k + 1]};
+            acc += e2;
         }
-        s += s0 + s1;
+        s += acc.x + acc.y;
         m = mn;
+        return mn;
     };
     // One vector of VEC elements starting at v0 (v0 % 8 == 0 on every path); cnt < VEC only on
     // the ragged tail (FULL = false).
@@ -253,7 +306,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(
         float vmax = x[0];
 #pragma unroll
         for (int k = 1; k < VEC; ++k) vmax = fmaxf(vmax, x[k]);
-        lse_vec(x, vmax);
+        float ex[VEC];
+        lse_vec(x, vmax, ex);
         if constexpr (greedy) {
             if (vmax > best_s) {  // first index of the new maximum (ascending visit order)
                 int kk = VEC - 1;
@@ -269,51 +323,28 @@ __global__ __launch_bounds__(NT) void sample_kernel(
 #pragma unroll
         for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
         auto h16 = [&](int k) -> uint32_t { return (k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu); };
-        if (!seeded) {  // wave-uniform, once: exact score of each lane's largest admissible element
-            seeded = true;
-            float xb = -INFINITY;
-            int kb = -1;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                bool keep = FULL || k < cnt;
-                if constexpr (MODE == 2) {
-                    if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
-                    if (use_minp) keep = keep && x[k] * inv_t >= mthr;
-                }
-                if (keep && x[k] > xb) {
-                    xb = x[k];
-                    kb = k;
-                }
-            }
-            if (kb >= 0) {
-                uint32_t hb = 0;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) hb = (k == kb) ? h16(k) : hb;
-                const float sc = exact(xb, hb, v0 + kb);
-                if (sc > best_s) {
-                    best_s = sc;
-                    best_i = v0 + kb;
-                }
-            }
-            raise_bar();
+        if constexpr (!FULL) {
+            if (!seeded) seed_vec(raw, x, hp, v0, cnt);
         }
-        bool cand[VEC];
+        // fv[k] >= 0 (or NaN) <=> element k may beat the bar; -inf for inadmissible slots
+        float fv[VEC];
         uint64_t anym = 0;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const float bits = (float)(int)__float_as_uint((float)h16(k));
+            fv[k] = fmaf(bits, -kT, x[k]) - thr;
             bool keep = FULL || k < cnt;
             if constexpr (MODE == 2) {
                 if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
                 if (use_minp) keep = keep && x[k] * inv_t >= mthr;
             }
-            cand[k] = keep && fmaf(bits, -kT, x[k]) >= thr;
-            anym |= __builtin_amdgcn_ballot_w64(cand[k]);
+            if (!FULL || MODE == 2) fv[k] = keep ? fv[k] : -INFINITY;
+            anym |= __builtin_amdgcn_ballot_w64(!(fv[k] < 0.f));
         }
         if (anym == 0) return;  // wave-uniform: rare once the bar is up
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            if (cand[k]) {
+            if (!(fv[k] < 0.f)) {
                 const float sc = exact(x[k], h16(k), v0 + k);
                 if (sc > best_s) {
                     best_s = sc;
@@ -322,6 +353,88 @@ __global__ __launch_bounds__(NT) void sample_kernel(
             }
         }
         raise_bar();
+    };
+    // MODE 3 full vector, lagged lse offset m (exps accumulate into acc2; the caller checks
+    // for overflow once per iteration)
+    auto visit3 = [&](const uint4& dw4, int v0, f32x2& acc2) {
+        T raw[VEC];
+        __builtin_memcpy(raw, &dw4, 16);
+        float x[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = to_f<T>(raw[k]);
+        const f32x2 l2 = {kLog2e, kLog2e};
+        const f32x2 c2 = {-m * kLog2e, -m * kLog2e};
+        float ex[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; k += 2) {
+            const f32x2 xv = {x[k], x[k + 1]};
+            const f32x2 y = __builtin_elementwise_fma(xv, l2, c2);
+            ex[k] = fast_exp2(y.x);
+            ex[k + 1] = fast_exp2(y.y);
+            acc2 += f32x2{ex[k], ex[k + 1]};
+        }
+        const uint32_t g0 = (uint32_t)v0 >> 1;
+        uint32_t hp[VEC / 2];
+#pragma unroll
+        for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
+        auto h16 = [&](int k) -> uint32_t { return (k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu); };
+        float fv[VEC];
+        if (!qbad) {
+            const f32x2 q2 = {Q, Q};
+            float fmx = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < VEC; k += 2) {
+                const f32x2 e2 = {ex[k], ex[k + 1]};
+                const f32x2 n2 = {-(float)h16(k), -(float)h16(k + 1)};
+                const f32x2 f = __builtin_elementwise_fma(e2, q2, n2);
+                fv[k] = f.x;
+                fv[k + 1] = f.y;
+                fmx = fmaxf(fmx, fmaxf(f.x, f.y));
+            }
+            if (__builtin_amdgcn_ballot_w64(fmx >= 0.f) == 0) return;
+        } else {
+            uint64_t anym = 0;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const float bits = (float)(int)__float_as_uint((float)h16(k));
+                fv[k] = fmaf(bits, -kT, x[k]) - thr;
+                anym |= __builtin_amdgcn_ballot_w64(!(fv[k] < 0.f));
+            }
+            if (anym == 0) return;
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            if (!(fv[k] < 0.f)) {
+                const float sc = exact(x[k], h16(k), v0 + k);
+                if (sc > best_s) {
+                    best_s = sc;
+                    best_i = v0 + k;
+                }
+            }
+        }
+        raise_bar();
+    };
+    // lse of one iteration redone with a fresh offset after an overflow of the lagged one
+    auto lse_refresh = [&](const uint4 (&dw)[4]) {
+        float mx = m;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            T raw[VEC];
+            __builtin_memcpy(raw, &dw[u], 16);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) mx = fmaxf(mx, to_f<T>(raw[k]));
+        }
+        s *= fast_exp2((m - mx) * kLog2e);
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            T raw[VEC];
+            __builtin_memcpy(raw, &dw[u], 16);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) acc += fast_exp2((to_f<T>(raw[k]) - mx) * kLog2e);
+        }
+        s += acc;
+        m = mx;
     };
     const std::integral_constant<bool, true> kFull{};
     const std::integral_constant<bool, false> kPart{};
@@ -338,6 +451,24 @@ __global__ __launch_bounds__(NT) void sample_kernel(
         if (nfull > 0) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
+            if constexpr (!greedy) {  // seed from this lane's first vector
+                T vals[VEC];
+                __builtin_memcpy(vals, &cur[0], 16);
+                float x[VEC];
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) x[k] = to_f<T>(vals[k]);
+                if constexpr (MODE == 3) {  // lagged lse offset starts at this lane's first-vector max
+                    float mx = x[0];
+#pragma unroll
+                    for (int k = 1; k < VEC; ++k) mx = fmaxf(mx, x[k]);
+                    m = mx;
+                }
+                const int v0s = v_beg + threadIdx.x * VEC;
+                uint32_t hp[VEC / 2];
+#pragma unroll
+                for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ (((uint32_t)v0s >> 1) + (uint32_t)q) * 0x9e3779b1u);
+                seed_vec(vals, x, hp, v0s, VEC);
+            }
         }
         for (int base = 0; base < nfull; base += kStep) {
             const bool more = base + kStep < nfull;
@@ -345,11 +476,22 @@ __global__ __launch_bounds__(NT) void sample_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
             }
+            if constexpr (MODE == 3) {
+                f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                T vals[VEC];
-                __builtin_memcpy(vals, &cur[u], 16);
-                visit_vec(vals, v_beg + (base + u * NT + threadIdx.x) * VEC, VEC, kFull);
+                for (int u = 0; u < 4; ++u) visit3(cur[u], v_beg + (base + u * NT + threadIdx.x) * VEC, acc2);
+                const float acc = acc2.x + acc2.y;
+                const bool ovf = !(acc < 1e30f);  // a value far above the lagged offset m
+                if (ovf) lse_refresh(cur);
+                else s += acc;
+                if (__builtin_amdgcn_ballot_w64(ovf) != 0) recompute_q();
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    T vals[VEC];
+                    __builtin_memcpy(vals, &cur[u], 16);
+                    visit_vec(vals, v_beg + (base + u * NT + threadIdx.x) * VEC, VEC, kFull);
+                }
             }
             if (more) {
 #pragma unroll
@@ -507,6 +649,9 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     else if (use_topk || use_minp)
         launch_mode<T, 2>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, use_topk, use_minp, ln_min_p, seed, seq_ids,
                           step, thr, rmax, tokens, logp, parts, counters);
+    else if (temperature == 1.0f)
+        launch_mode<T, 3>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
+                          rmax, tokens, logp, parts, counters);
     else
         launch_mode<T, 1>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
                           rmax, tokens, logp, parts, counters);
