@@ -27,3 +27,16 @@ extern "C" int probe(const void* x, int64_t ld, int nrows, int V, int mode, void
     else hipLaunchKernelGGL(stream_rows<1024>, dim3(nrows, 1), dim3(1024), 0, s, (const uint16_t*)x, ld, V, 1, (uint32_t*)out);
     return (int)hipGetLastError();
 }
+
+// read+write copy with the fused kernel's widths (16-B nt loads, 16-B nt or plain stores)
+__global__ __launch_bounds__(256) void copy_rows(const u32x4* __restrict__ x, u32x4* __restrict__ y, int64_t n, int nts) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const u32x4 v = __builtin_nontemporal_load(x + i);
+        if (nts) __builtin_nontemporal_store(v, y + i);
+        else y[i] = v;
+    }
+}
+extern "C" int probe_copy(const void* x, void* y, int64_t n16, int nts, int blocks, void* stream) {
+    hipLaunchKernelGGL(copy_rows, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)x, (u32x4*)y, n16, nts);
+    return (int)hipGetLastError();
+}

@@ -25,3 +25,17 @@ def run(mode, ld_rows):
 for mode, name in ((0, "512thr_row"), (1, "256thr_4split"), (2, "1024thr_row")):
     ms = run(mode, 64)
     print(name, f"{ms*1e3:.1f} us", f"{N*V*2/ms/1e6:.0f} GB/s")
+# read+write ceiling: 5 GB copy (the fused training pass's traffic shape)
+n = 16 * 1024 * V  # bf16 elements per micro-batch of dlogits
+src = x.view(-1)[:n]
+dst = torch.empty(n, dtype=torch.bfloat16, device=dev)
+for nts in (0, 1):
+    for blocks in (4096, 16384):
+        def g():
+            lib.probe_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), ctypes.c_int64(n // 8), nts,
+                           blocks, st)
+        g()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(); [g() for _ in range(5)]; b.record(); b.synchronize()
+        ms = a.elapsed_time(b) / 5
+        print(f"copy nts={nts} blocks={blocks}", f"{ms:.3f} ms", f"{2 * n * 2 / ms / 1e6:.0f} GB/s")

@@ -314,6 +314,7 @@ int launch_bwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V
 using namespace skyrl;
 namespace skyrl {
 extern int g_train_resident;
+extern int g_train_ntstore;
 }
 
 extern "C" int skyrl_tune(const char* key, int value) {
@@ -321,6 +322,10 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "logprob_unroll") {
         SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: logprob_unroll must be 4 or 8");
         g_tune.unroll = value;
+        return SKYRL_OK;
+    }
+    if (k == "train_ntstore") {
+        g_train_ntstore = value != 0;
         return SKYRL_OK;
     }
     if (k == "train_resident") {

@@ -41,6 +41,12 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// dlogits are written once and not re-read here: optionally non-temporal (skyrl_tune("train_ntstore"))
+__device__ __forceinline__ void st_out(uint4* p, uint4 v, bool nts) {
+    if (nts) __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(p));
+    else *p = v;
+}
+
 __device__ __forceinline__ void unpack8(const uint4& v, float (&x)[8]) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void policy_train_kernel(
     const float* __restrict__ old, const float* __restrict__ adv, const float* __restrict__ mask,
     const float* __restrict__ ref, const float* __restrict__ row_scale, const float* __restrict__ scal,
     skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out, float* __restrict__ tok,
-    uint16_t* __restrict__ dx) {
+    uint16_t* __restrict__ dx, bool nts) {
     __shared__ St s_st[kWaves];
     __shared__ float s_g[3];  // lse, g_lp, g_ent*... (see below)
     __shared__ float s_h;
@@ -271,8 +277,8 @@ __global__ __launch_bounds__(kThreads) void policy_train_kernel(
                 const int64_t v0 = (int64_t)(i + u * kThreads) * 8;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) x[k] = grad(tval(x[k]), v0 + k);
-                ov[i + u * kThreads] = make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
-                                                  pack_bf16x2(x[4], x[5]), pack_bf16x2(x[6], x[7]));
+                st_out(ov + i + u * kThreads, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
+                                                         pack_bf16x2(x[4], x[5]), pack_bf16x2(x[6], x[7])), nts);
             }
         }
         for (; i < nvec; i += kThreads) {
@@ -281,8 +287,8 @@ __global__ __launch_bounds__(kThreads) void policy_train_kernel(
             const int64_t v0 = (int64_t)i * 8;
 #pragma unroll
             for (int k = 0; k < 8; ++k) x[k] = grad(tval(x[k]), v0 + k);
-            ov[i] = make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
-                               pack_bf16x2(x[6], x[7]));
+            st_out(ov + i, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                      pack_bf16x2(x[6], x[7])), nts);
         }
     }
     for (int v = done + threadIdx.x; v < V; v += kThreads) out[v] = f32_to_bf16(grad(tval(bf16_to_f32(row[v])), v));
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     int64_t lsb, int64_t lst, float temp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
     const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
-    float* __restrict__ tok, uint16_t* __restrict__ dx) {
+    float* __restrict__ tok, uint16_t* __restrict__ dx, bool nts) {
     __shared__ St s_st[NT / 64];
     __shared__ float s_g[4];
     const int64_t r = blockIdx.x;
@@ -398,8 +404,8 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
                 if (v0 + j == lab32) g += glp;
                 x[j] = HAS_T ? g * inv_t : g;
             }
-            ov[idx] = make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
-                                 pack_bf16x2(x[6], x[7]));
+            st_out(ov + idx, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                        pack_bf16x2(x[6], x[7])), nts);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -488,6 +494,7 @@ __global__ void scale_bf16_kernel(const float* __restrict__ g, uint16_t* __restr
 }  // namespace
 
 int g_train_resident = 1;  // skyrl_tune("train_resident", 0/1)
+int g_train_ntstore = 1;   // skyrl_tune("train_ntstore", 0/1): non-temporal dlogits stores
 
 }  // namespace skyrl
 
@@ -533,12 +540,14 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
         hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(kRT), 0, s,
                            reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, V, labels, lstride_b,
                            lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs, row_scale,
-                           scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits));
+                           scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
+                           g_train_ntstore != 0);
     } else
     hipLaunchKernelGGL(policy_train_kernel, dim3((unsigned)((int64_t)n * R)), dim3(kThreads), 0, s,
                        reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, (int64_t)n * R, V, labels,
                        lstride_b, lstride_t, temperature, has_t, old_log_probs, advantages, loss_mask, ref_log_probs,
-                       row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits));
+                       row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
+                       g_train_ntstore != 0);
     rc = check_launch("policy_train_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
