@@ -371,22 +371,13 @@ def cpu_baseline(args):
     g = torch.Generator().manual_seed(0)
     logits = (torch.randn(n_traj, R, V, generator=g) * 3).to(torch.bfloat16)
     labels = torch.randint(0, V, (n_traj, R), generator=g)
-    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libsampler_ref.so"))
-    f = lib.sampler_ref
-    f.restype = None
-    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                  ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_void_p]
-    raw = logits.view(torch.int16)
-    tok = torch.empty(n_traj, dtype=torch.int32)
-    lpo = torch.empty(n_traj, dtype=torch.float32)
-    keys = torch.empty(V, dtype=torch.int32)
+    from oracle import sampler as osamp
+
     ids = torch.arange(n_traj, dtype=torch.int64)
     steps = args.cpu_sampler_steps
     t0 = time.perf_counter()
     for t in range(steps):  # one decode step = n_traj rows of V
-        f(raw[:, t].contiguous().data_ptr(), 1, V, n_traj, V, 1.0, -1, 0.0, 0, ids.data_ptr(), t, tok.data_ptr(),
-          lpo.data_ptr(), keys.data_ptr())
+        osamp.sample(logits[:, t].contiguous(), 1.0, -1, 1.0, 0.0, 0, ids, t)
     t_sample = (time.perf_counter() - t0) * (R / steps)
     tok_sample = args.cpu_logprob_tokens
     x = logits.reshape(-1, V)[:tok_sample]

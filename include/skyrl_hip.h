@@ -39,12 +39,13 @@ extern "C" {
 
 /* Thread-local text of the last error on this thread ("" if none). */
 const char* skyrl_last_error(void);
-/* ABI version; bumped on any signature change. */
+/* ABI version; bumped on any signature change (2: skyrl_sample takes top_p). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
  * {0, 1} (non-temporal streaming loads of the logits), "train_resident" {0, 1} (fused
- * training pass keeps the vocab row in registers vs re-reading it). Not thread-safe.  */
+ * training pass keeps the vocab row in registers vs re-reading it), "train_ntstore"
+ * {0, 1} (non-temporal dlogits stores). Not thread-safe.                              */
 int skyrl_tune(const char* key, int value);
 
 /* ---- a4: GRPO outcome advantage ----------------------------------------
@@ -195,15 +196,19 @@ int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* 
  * Replaces the vLLM sampler behind VLLMInferenceEngine.generate
  * (inference_engines/vllm/vllm_engine.py:196-218) with sampled-token logprob
  * extraction (vllm_engine.py:139-149) and SamplingParams defaults
- * (config/ppo_base_config.yaml:316-324). Filter order temperature->top_k->
- * min_p (semantics: skyrl-tx/tx/utils/generator.py:398-449); top_k<=0 off.
- * temperature==0 => greedy (lowest index wins ties). Otherwise Gumbel-max with
- * a counter-based hash keyed by (seed, seq_ids[i], step, vocab index), so the
- * token is a pure function of its inputs (bit-exact vs oracle/sampler_ref.c).
- * logp_out = log_softmax(raw logits)[token] (unscaled logits).
+ * (config/ppo_base_config.yaml:316-324). Filters on the temperature-scaled
+ * logits: top_k (keep >= the k-th largest, ties kept; <= 0 off), min_p
+ * (p >= min_p * p_max), then top_p (skyrl-tx/tx/utils/generator.py:424-449:
+ * in descending order keep tokens while the mass strictly before them is
+ * < top_p, the top token always, ties in index order; 1.0 off); the top_p
+ * masses are fixed-point 2^31 e^((x-max)/T) summed exactly, so decisions are
+ * reproducible. temperature==0 => greedy (lowest index wins ties). Otherwise
+ * Gumbel-max with a counter-based hash keyed by (seed, seq_ids[i], step,
+ * vocab index), so the token is a pure function of its inputs (bit-exact vs
+ * oracle/sampler_ref.c). logp_out = log_softmax(raw logits)[token].
  * logits row i at logits + i*ld (elements).                                  */
 int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V,
-                 float temperature, int32_t top_k, float min_p, uint64_t seed,
+                 float temperature, int32_t top_k, float top_p, float min_p, uint64_t seed,
                  const int64_t* seq_ids, int64_t step, int32_t* tokens_out, float* logp_out,
                  void* workspace, void* stream);
 size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V);

@@ -7,8 +7,10 @@
  * (tests/gpu/utils.py:222-236 compares text similarity only). The build therefore
  * defines its own counter-based sampler with the reference's filter semantics
  * (skyrl-tx/tx/utils/generator.py:213-227,398-449: temperature, top_k keeping values
- * >= the k-th largest, min_p relative to the max probability, greedy at T == 0,
- * logprob of the sampled token from the raw logits), and this file is its oracle:
+ * >= the k-th largest, min_p relative to the max probability, top_p keeping tokens in
+ * descending order while the mass strictly before them is < p (top token always, ties
+ * in index order), greedy at T == 0, logprob of the sampled token from the raw logits),
+ * and this file is its oracle:
  * one thread, elements in index order, every decision-path float operation an IEEE
  * basic op or fmaf, compiled with -ffp-contract=off. Tokens must match bit for bit.
  */
@@ -84,6 +86,43 @@ static uint32_t okey_f32(float x) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+
+/* deterministic 2^y for y <= 0 (0 below -126): same operations as det_exp2 in sampler.hip */
+static float det_exp2(float y) {
+    const float yc = y >= -126.0f ? y : -126.0f;
+    const float fi = floorf(yc);
+    const float f = yc - fi;
+    float p = 2.170088992e-04f, r;
+    uint32_t b;
+    p = fmaf(p, f, 1.243957202e-03f);
+    p = fmaf(p, f, 9.678921662e-03f);
+    p = fmaf(p, f, 5.548325926e-02f);
+    p = fmaf(p, f, 2.402298748e-01f);
+    p = fmaf(p, f, 6.931470037e-01f);
+    p = fmaf(p, f, 1.0f);
+    memcpy(&b, &p, 4);
+    b += (uint32_t)(int)fi << 23;
+    memcpy(&r, &b, 4);
+    return y >= -126.0f ? r : 0.0f;
+}
+/* fixed-point top_p mass 2^31 e^((x - max)/T) */
+static uint32_t mass_q(float x, float mx, float inv_t) {
+    const float y = ((x - mx) * inv_t) * 1.4426950408889634f;
+    return (uint32_t)(det_exp2(y) * 2147483648.0f);
+}
+
+typedef struct {
+    uint32_t key;
+    int idx;
+    uint32_t q;
+} kept_t;
+static int cmp_kept(const void* a, const void* b) {
+    const kept_t* x = (const kept_t*)a;
+    const kept_t* y = (const kept_t*)b;
+    if (x->key != y->key) return x->key < y->key ? 1 : -1; /* key descending */
+    return (x->idx > y->idx) - (x->idx < y->idx);          /* index ascending */
+}
+
 /* k-th largest key (1-based k): sort a copy descending. */
 static int cmp_desc(const void* a, const void* b) {
     const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
@@ -99,9 +138,10 @@ static uint32_t kth_key(uint32_t* keys, int V, int k) {
  * keys: scratch uint32[V]. tokens/logp: outputs.
  */
 void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, float temperature, int top_k,
-                 float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens, float* logp,
-                 uint32_t* keys) {
+                 float top_p, float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens,
+                 float* logp, uint32_t* keys) {
     int i, v;
+    kept_t* kept = (kept_t*)malloc(sizeof(kept_t) * (size_t)V);
     for (i = 0; i < nseq; ++i) {
         const uint16_t* rb = is_bf16 ? (const uint16_t*)logits + (int64_t)i * ld : NULL;
         const float* rf = is_bf16 ? NULL : (const float*)logits + (int64_t)i * ld;
@@ -109,6 +149,9 @@ void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, f
         const int greedy = temperature == 0.0f;
         const int use_topk = !greedy && top_k > 0 && top_k < V;
         const int use_minp = !greedy && min_p > 0.0f;
+        const int use_topp = !greedy && top_p < 1.0f;
+        uint32_t kc = 0;
+        int ic = 0x7fffffff;
         const float inv_t = greedy ? 1.0f : 1.0f / temperature;
         const uint32_t key = row_key(seed, seq_ids ? seq_ids[i] : (int64_t)i, step);
         uint32_t tk = 0;
@@ -121,6 +164,49 @@ void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, f
             tk = kth_key(keys, V, top_k);
         }
         if (use_minp) mthr = mx * inv_t + det_ln(min_p);
+        if (use_topp) {
+            /* kept set (top_k and min_p), sorted by key desc / index asc; first key group whose
+             * cumulative mass reaches p*Z is the cut; its first c tokens (index order) stay */
+            int nk = 0, g, j;
+            uint64_t Z = 0, cum = 0;
+            for (v = 0; v < V; ++v) {
+                const uint32_t kk = is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v]);
+                const float x = X(v);
+                if (use_topk && kk < tk) continue;
+                if (use_minp && x * inv_t < mthr) continue;
+                kept[nk].key = kk;
+                kept[nk].idx = v;
+                kept[nk].q = mass_q(x, mx, inv_t);
+                Z += kept[nk].q;
+                ++nk;
+            }
+            qsort(kept, (size_t)nk, sizeof(kept_t), cmp_kept);
+            {
+                const double target = (double)top_p * (double)Z;
+                for (g = 0; g < nk;) {
+                    uint64_t gm = 0;
+                    int e = g;
+                    while (e < nk && kept[e].key == kept[g].key) gm += kept[e++].q;
+                    if ((double)(cum + gm) >= target || e == nk) {
+                        const uint64_t qc = kept[g].q;
+                        long long c;
+                        kc = kept[g].key;
+                        if (qc == 0) {
+                            c = e - g;
+                        } else {
+                            c = 0;
+                            while ((double)(cum + (uint64_t)c * qc) < target) ++c;
+                        }
+                        if (g == 0 && c < 1) c = 1;
+                        if (c < e - g) ic = kept[g + c - 1].idx;
+                        break;
+                    }
+                    cum += gm;
+                    g = e;
+                }
+            }
+            (void)j;
+        }
         for (v = 0; v < V; ++v) {
             const float x = X(v);
             float sc;
@@ -131,6 +217,10 @@ void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, f
                 const float xs = x * inv_t;
                 if (use_topk && (is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v])) < tk) continue;
                 if (use_minp && xs < mthr) continue;
+                if (use_topp) {
+                    const uint32_t kk = is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v]);
+                    if (kk < kc || (kk == kc && v > ic)) continue;
+                }
                 sc = xs + gumbel(key, (uint32_t)v);
             }
             if (sc > best || (sc == best && v < best_i)) {
@@ -142,4 +232,5 @@ void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, f
         if (logp) logp[i] = (float)((double)X(best_i) - ((double)mx + log(s)));
 #undef X
     }
+    free(kept);
 }

@@ -126,7 +126,9 @@ def main():
 
         sh = torch.cuda.current_stream(dev).cuda_stream
         for name, sp in (("sample_t1", SamplingParams()), ("sample_greedy", SamplingParams(temperature=0.0)),
-                         ("sample_topk50", SamplingParams(top_k=50)), ("sample_minp", SamplingParams(min_p=0.05))):
+                         ("sample_topk50", SamplingParams(top_k=50)), ("sample_minp", SamplingParams(min_p=0.05)),
+                         ("sample_topp09", SamplingParams(top_p=0.9)),
+                         ("sample_topk50_topp09", SamplingParams(top_k=50, top_p=0.9))):
             smp = TokenSampler(N, V, R, dev, sp, seed=1)
 
             def go(t=[0]):

@@ -29,7 +29,6 @@ namespace skyrl {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
 constexpr int kRowModeMinSeqs = 256;  // enough rows to fill the chip with one workgroup each
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
@@ -108,57 +107,185 @@ __device__ __forceinline__ uint32_t okey(T v);
 template <> __device__ __forceinline__ uint32_t okey<uint16_t>(uint16_t v) { return okey_bf16(v); }
 template <> __device__ __forceinline__ uint32_t okey<float>(float v) { return okey_f32(__float_as_uint(v)); }
 
-// ---- pre-pass: per-row top_k key threshold (radix select) and raw max --------
+// inverse of okey: the logit value of a key
 template <typename T>
-__global__ __launch_bounds__(kThreads) void sample_filter_kernel(const T* __restrict__ logits, int64_t ld, int V,
-                                                                 int top_k, uint32_t* __restrict__ thr_key,
-                                                                 float* __restrict__ row_max) {
-    __shared__ unsigned hist[256];
-    __shared__ uint32_t s_prefix, s_k;
-    __shared__ float s_max[kWaves];
+__device__ __forceinline__ float from_key(uint32_t k);
+template <> __device__ __forceinline__ float from_key<uint16_t>(uint32_t k) {
+    return bf16_to_f32((uint16_t)((k & 0x8000u) ? (k & 0x7fffu) : (~k & 0xffffu)));
+}
+template <> __device__ __forceinline__ float from_key<float>(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Deterministic 2^y for y <= 0 (0 below -126): floor split, degree-6 fit of 2^f on [0, 1)
+// (max rel. err 6e-8), exponent added in the bit pattern. Bit-identical in sampler_ref.c.
+__host__ __device__ __forceinline__ float det_exp2(float y) {
+    const float yc = y >= -126.0f ? y : -126.0f;
+    const float fi = floorf(yc);
+    const float f = yc - fi;
+    float p = 2.170088992e-04f;
+    p = fmaf(p, f, 1.243957202e-03f);
+    p = fmaf(p, f, 9.678921662e-03f);
+    p = fmaf(p, f, 5.548325926e-02f);
+    p = fmaf(p, f, 2.402298748e-01f);
+    p = fmaf(p, f, 6.931470037e-01f);
+    p = fmaf(p, f, 1.0f);
+    const float r = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, p) + ((uint32_t)(int)fi << 23));
+    return y >= -126.0f ? r : 0.0f;
+}
+// top_p mass of a logit in fixed point: 2^31 * e^((x - max) / T), as an integer so that every
+// sum is exact and order-independent (the oracle makes the same decisions bit for bit)
+__host__ __device__ __forceinline__ uint32_t mass_q(float x, float mx, float inv_t) {
+    const float y = ((x - mx) * inv_t) * 1.4426950408889634f;
+    return (uint32_t)(det_exp2(y) * 2147483648.0f);
+}
+
+struct RowFilter {  // per row, written by the filter pre-pass
+    float rmax;     // raw max logit
+    uint32_t tk;    // top_k: keep keys >= tk
+    uint32_t kc;    // top_p: keep keys > kc, and key == kc at indices <= ic
+    int32_t ic;
+};
+
+// ---- filter pre-pass: one 1024-thread workgroup per row ---------------------------------
+// top_k (over all logits, ties kept: vLLM's `logits < kth` mask) and top_p (tx generator.py:
+// 424-449 on the top_k- and min_p-filtered distribution: tokens in descending order are kept
+// while the probability mass strictly before them is < p, the top token always, equal logits
+// in index order) by MSB-first radix selection over d = key(max) - key with 8-bit digits
+// (2 levels for bf16, 4 for f32): a 256-bin LDS histogram of counts (top_k) or of the
+// fixed-point masses (top_p) per level. The tie group at the top_p cut is resolved by an
+// index-ordered count.
+constexpr int kFT = 1024;
+template <typename T>
+__global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict__ logits, int64_t ld, int V, int top_k,
+                                                            int use_minp, float inv_t, float ln_min_p, float top_p,
+                                                            RowFilter* __restrict__ out) {
+    constexpr int NW = kFT / kWave;
+    constexpr int KB = sizeof(T) * 8;
+    __shared__ unsigned long long hist[256];
+    __shared__ unsigned long long s_red[NW];
+    __shared__ uint32_t s_u[NW];
+    __shared__ uint32_t s_sel[2];               // selected d, found flag
+    __shared__ unsigned long long s_below, s_at;
+    __shared__ int s_ic;
     const T* row = logits + (int64_t)blockIdx.x * ld;
-    float mx = -3.402823466e38f;
-    for (int i = threadIdx.x; i < V; i += kThreads) mx = fmaxf(mx, to_f<T>(row[i]));
-    mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x / kWave] = mx;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+
+    // pass 0: max key (an integer max, exact)
+    uint32_t km = 0u;
+    for (int i = threadIdx.x; i < V; i += kFT) km = max(km, okey<T>(row[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) km = max(km, (uint32_t)__shfl_xor((int)km, off, kWave));
+    if (lane == 0) s_u[w] = km;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float m = s_max[0];
-        for (int j = 1; j < kWaves; ++j) m = fmaxf(m, s_max[j]);
-        row_max[blockIdx.x] = m;
-    }
-    if (top_k <= 0 || top_k >= V) {
-        if (threadIdx.x == 0) thr_key[blockIdx.x] = 0u;  // keep everything
-        return;
-    }
-    constexpr int kBits = sizeof(T) * 8;
-    if (threadIdx.x == 0) {
-        s_prefix = 0u;
-        s_k = (uint32_t)top_k;
-    }
-    for (int shift = kBits - 8; shift >= 0; shift -= 8) {
-        for (int j = threadIdx.x; j < 256; j += kThreads) hist[j] = 0u;
-        __syncthreads();
-        const uint32_t prefix = s_prefix;
-        const uint32_t hi_mask = (shift + 8 >= 32) ? 0u : (0xffffffffu << (shift + 8));
-        for (int i = threadIdx.x; i < V; i += kThreads) {
-            const uint32_t k = okey<T>(row[i]);
-            if ((k & hi_mask) == (prefix & hi_mask)) atomicAdd(&hist[(k >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t need = s_k, cum = 0u;
-            int d = 255;
-            for (; d > 0; --d) {
-                if (cum + hist[d] >= need) break;
-                cum += hist[d];
+    uint32_t kmax = s_u[0];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) kmax = max(kmax, s_u[j]);
+    const float mx = from_key<T>(kmax);
+    const float mthr = mx * inv_t + ln_min_p;
+    __syncthreads();
+
+    // MSB-first radix selection: smallest d with (sum of weights over d' <= d) >= target
+    auto radix = [&](auto weight, double target) {
+        uint32_t prefix = 0u;
+        unsigned long long below = 0ull, at = 0ull;
+        for (int lvl = 0; lvl < KB / 8; ++lvl) {
+            const int shift = KB - 8 * (lvl + 1);
+            for (int j = threadIdx.x; j < 256; j += kFT) hist[j] = 0ull;
+            __syncthreads();
+            for (int i = threadIdx.x; i < V; i += kFT) {
+                const T raw = row[i];
+                const uint32_t d = kmax - okey<T>(raw);
+                if (lvl > 0 && (d >> (shift + 8)) != prefix) continue;
+                const unsigned long long wt = weight(raw, i);
+                if (wt) atomicAdd(&hist[(d >> shift) & 255u], wt);
             }
-            s_k = need - cum;
-            s_prefix = prefix | ((uint32_t)d << shift);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long cum = below;
+                int dg = 0;
+                for (; dg < 255; ++dg) {
+                    if ((double)(cum + hist[dg]) >= target) break;
+                    cum += hist[dg];
+                }
+                s_below = cum;
+                s_at = hist[dg];
+                s_sel[0] = (prefix << 8) | (uint32_t)dg;
+            }
+            __syncthreads();
+            prefix = s_sel[0];
+            below = s_below;
+            at = s_at;
+            __syncthreads();
         }
-        __syncthreads();
+        struct R { uint32_t d; unsigned long long below, at; };
+        return R{prefix, below, at};
+    };
+
+    uint32_t tk = 0u;
+    if (top_k > 0 && top_k < V) {
+        const auto r = radix([&](T, int) -> unsigned long long { return 1ull; }, (double)top_k);
+        tk = kmax - r.d;
     }
-    if (threadIdx.x == 0) thr_key[blockIdx.x] = s_prefix;
+    uint32_t kc = 0u;
+    int ic = 0x7fffffff;
+    if (top_p < 1.0f) {
+        auto kept = [&](T raw) -> bool {
+            return okey<T>(raw) >= tk && (!use_minp || to_f<T>(raw) * inv_t >= mthr);
+        };
+        // Z: exact integer sum of the kept masses
+        unsigned long long z = 0ull;
+        for (int i = threadIdx.x; i < V; i += kFT) {
+            const T raw = row[i];
+            if (kept(raw)) z += mass_q(to_f<T>(raw), mx, inv_t);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) z += (unsigned long long)__shfl_xor((long long)z, off, kWave);
+        if (lane == 0) s_red[w] = z;
+        __syncthreads();
+        unsigned long long Z = 0ull;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) Z += s_red[j];
+        const double target = (double)top_p * (double)Z;
+        const auto r = radix([&](T raw, int) -> unsigned long long {
+            return kept(raw) ? (unsigned long long)mass_q(to_f<T>(raw), mx, inv_t) : 0ull; }, target);
+        kc = kmax - r.d;
+        const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
+        const unsigned long long A = r.below;
+        if (qc != 0ull) {
+            // c = number of tie ranks j >= 0 with A + j qc < target (the first always for the top key)
+            const double jd = (target - (double)A) / (double)qc;
+            long long c = jd > 0.0 ? (long long)jd : 0;
+            while (c > 0 && (double)(A + (unsigned long long)(c - 1) * qc) >= target) --c;
+            while ((double)(A + (unsigned long long)c * qc) < target) ++c;
+            if (kc == kmax && c < 1) c = 1;
+            const long long cnt = (long long)(r.at / qc);
+            if (c < cnt) {
+                // index of the c-th tie token (1-based) in index order: rounds of kFT elements
+                if (threadIdx.x == 0) s_ic = 0x7fffffff;
+                long long seen = 0;
+                for (int base = 0; base < V; base += kFT) {
+                    const int i = base + threadIdx.x;
+                    const bool hit = i < V && okey<T>(row[i]) == kc && kept(row[i]);
+                    const uint64_t bm = __builtin_amdgcn_ballot_w64(hit);
+                    const int before_w = __builtin_popcountll(bm & ((1ull << lane) - 1ull));
+                    if (lane == 0) s_u[w] = (uint32_t)__builtin_popcountll(bm);
+                    __syncthreads();
+                    long long off_w = 0, tot = 0;
+                    for (int j = 0; j < NW; ++j) {
+                        if (j < w) off_w += s_u[j];
+                        tot += s_u[j];
+                    }
+                    if (hit && seen + off_w + before_w + 1 == c) s_ic = i;
+                    seen += tot;
+                    __syncthreads();
+                    if (seen >= c) break;
+                }
+                ic = s_ic;
+            }
+        }
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = RowFilter{mx, tk, kc, ic};
 }
 
 // MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p,
@@ -169,7 +296,7 @@ template <typename T, int MODE, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
-    const uint32_t* __restrict__ thr_key, const float* __restrict__ row_max, int32_t* __restrict__ tokens,
+    int use_topp_rt, const RowFilter* __restrict__ filt, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters) {
     constexpr int NW = NT / kWave;
     __shared__ Part s_part[NW];
@@ -186,8 +313,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     constexpr bool greedy = MODE == 0;
     const bool use_topk = MODE == 2 && use_topk_rt;
     const bool use_minp = MODE == 2 && use_minp_rt;
-    const uint32_t tk = use_topk ? thr_key[row_i] : 0u;
-    const float mthr = use_minp ? row_max[row_i] * inv_t + ln_min_p : 0.f;
+    const bool use_topp = MODE == 2 && use_topp_rt;
+    const uint32_t tk = use_topk ? filt[row_i].tk : 0u;
+    const float mthr = use_minp ? filt[row_i].rmax * inv_t + ln_min_p : 0.f;
+    const uint32_t kc = use_topp ? filt[row_i].kc : 0u;
+    const int ic = use_topp ? filt[row_i].ic : 0;
+    // the filtered distribution's support (MODE 2): top_k, min_p, top_p
+    auto admissible = [&](T rawk, float xk, int v) -> bool {
+        bool keep = true;
+        const uint32_t kk = okey<T>(rawk);
+        if (use_topk) keep = keep && kk >= tk;
+        if (use_minp) keep = keep && xk * inv_t >= mthr;
+        if (use_topp) keep = keep && (kk > kc || (kk == kc && v <= ic));
+        return keep;
+    };
     if (!greedy) {
         if (threadIdx.x == 0) s_bar = -INFINITY;
         __syncthreads();
@@ -254,10 +393,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             bool keep = k < cnt;
-            if constexpr (MODE == 2) {
-                if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
-                if (use_minp) keep = keep && x[k] * inv_t >= mthr;
-            }
+            if constexpr (MODE == 2) keep = keep && admissible(raw[k], x[k], v0 + k);
             if (keep && x[k] > xb) {
                 xb = x[k];
                 kb = k;
@@ -334,10 +470,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
             const float bits = (float)(int)__float_as_uint((float)h16(k));
             fv[k] = fmaf(bits, -kT, x[k]) - thr;
             bool keep = FULL || k < cnt;
-            if constexpr (MODE == 2) {
-                if (use_topk) keep = keep && okey<T>(raw[k]) >= tk;
-                if (use_minp) keep = keep && x[k] * inv_t >= mthr;
-            }
+            if constexpr (MODE == 2) keep = keep && admissible(raw[k], x[k], v0 + k);
             if (!FULL || MODE == 2) fv[k] = keep ? fv[k] : -INFINITY;
             anym |= __builtin_amdgcn_ballot_w64(!(fv[k] < 0.f));
         }
@@ -603,58 +736,58 @@ int splits_for(int nseq, int V) {
 template <typename T, int MODE>
 void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int64_t ld, int V, int chunk, float inv_t,
                  int use_topk, int use_minp, float ln_min_p, uint64_t seed, const int64_t* seq_ids, int64_t step,
-                 const uint32_t* thr, const float* rmax, int32_t* tokens, float* logp, Part* parts,
-                 unsigned* counters) {
+                 int use_topp, const RowFilter* filt, int32_t* tokens, float* logp, Part* parts, unsigned* counters) {
     if (row_mode)
         hipLaunchKernelGGL((sample_kernel<T, MODE, 512>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
-                           use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts, counters);
+                           use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts, counters);
     else
         hipLaunchKernelGGL((sample_kernel<T, MODE, kThreads>), grid, dim3(kThreads), 0, stream, lg, ld, V, chunk, inv_t,
-                           use_topk, use_minp, ln_min_p, seed, seq_ids, step, thr, rmax, tokens, logp, parts,
+                           use_topk, use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts,
                            counters);
 }
 
+size_t ws_align(size_t b) { return (b + 255) / 256 * 256; }
+
 template <typename T>
-int launch_sample(const void* logits, int64_t ld, int nseq, int V, float temperature, int top_k, float min_p,
-                  uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens, float* logp, void* ws,
-                  hipStream_t stream) {
+int launch_sample(const void* logits, int64_t ld, int nseq, int V, float temperature, int top_k, float top_p,
+                  float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens, float* logp,
+                  void* ws, hipStream_t stream) {
     const int nsplit = splits_for(nseq, V);
     int chunk = (V + nsplit - 1) / nsplit;
     chunk = (chunk + 15) & ~15;
     char* w = reinterpret_cast<char*>(ws);
     unsigned* counters = reinterpret_cast<unsigned*>(w);
-    size_t off = (((size_t)nseq * 4 + 255) / 256) * 256;
-    uint32_t* thr = reinterpret_cast<uint32_t*>(w + off);
-    off += (((size_t)nseq * 4 + 255) / 256) * 256;
-    float* rmax = reinterpret_cast<float*>(w + off);
-    off += (((size_t)nseq * 4 + 255) / 256) * 256;
+    size_t off = ws_align((size_t)nseq * 4);
+    RowFilter* filt = reinterpret_cast<RowFilter*>(w + off);
+    off += ws_align((size_t)nseq * sizeof(RowFilter));
     Part* parts = reinterpret_cast<Part*>(w + off);
     const int greedy = temperature == 0.f;
     const int use_topk = !greedy && top_k > 0 && top_k < V;
     const int use_minp = !greedy && min_p > 0.f;
+    const int use_topp = !greedy && top_p < 1.f;
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
     const float ln_min_p = use_minp ? det_ln(min_p) : 0.f;
     const T* lg = reinterpret_cast<const T*>(logits);
-    if (use_topk || use_minp) {
-        hipLaunchKernelGGL(sample_filter_kernel<T>, dim3(nseq), dim3(kThreads), 0, stream, lg, ld, V,
-                           use_topk ? top_k : 0, thr, rmax);
+    if (use_topk || use_minp || use_topp) {
+        hipLaunchKernelGGL(sample_filter_kernel<T>, dim3(nseq), dim3(kFT), 0, stream, lg, ld, V, use_topk ? top_k : 0,
+                           use_minp, inv_t, ln_min_p, use_topp ? top_p : 1.0f, filt);
         int rc = check_launch("sample_filter_kernel");
         if (rc) return rc;
     }
     const dim3 grid(nseq, nsplit);
     const bool row_mode = nsplit == 1 && nseq >= kRowModeMinSeqs;
     if (greedy)
-        launch_mode<T, 0>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
-                          rmax, tokens, logp, parts, counters);
-    else if (use_topk || use_minp)
+        launch_mode<T, 0>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
+                          filt, tokens, logp, parts, counters);
+    else if (use_topk || use_minp || use_topp)
         launch_mode<T, 2>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, use_topk, use_minp, ln_min_p, seed, seq_ids,
-                          step, thr, rmax, tokens, logp, parts, counters);
+                          step, use_topp, filt, tokens, logp, parts, counters);
     else if (temperature == 1.0f)
-        launch_mode<T, 3>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
-                          rmax, tokens, logp, parts, counters);
+        launch_mode<T, 3>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
+                          filt, tokens, logp, parts, counters);
     else
-        launch_mode<T, 1>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, thr,
-                          rmax, tokens, logp, parts, counters);
+        launch_mode<T, 1>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
+                          filt, tokens, logp, parts, counters);
     return check_launch("sample_kernel");
 }
 
@@ -664,23 +797,24 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
 using namespace skyrl;
 
 extern "C" size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V) {
-    const size_t a = (((size_t)nseq * 4 + 255) / 256) * 256;
-    return 3 * a + (size_t)nseq * splits_for(nseq, V) * sizeof(Part) + 256;
+    return ws_align((size_t)nseq * 4) + ws_align((size_t)nseq * sizeof(RowFilter)) +
+           (size_t)nseq * splits_for(nseq, V) * sizeof(Part) + 256;
 }
 
 extern "C" int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V, float temperature,
-                            int32_t top_k, float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step,
-                            int32_t* tokens_out, float* logp_out, void* workspace, void* stream) {
+                            int32_t top_k, float top_p, float min_p, uint64_t seed, const int64_t* seq_ids,
+                            int64_t step, int32_t* tokens_out, float* logp_out, void* workspace, void* stream) {
     SKYRL_REQUIRE(nseq >= 0 && V > 0, "sample: bad sizes");
     if (nseq == 0) return SKYRL_OK;
     SKYRL_REQUIRE(logits && tokens_out && workspace, "sample: null pointer");
     SKYRL_REQUIRE(temperature >= 0.f, "sample: temperature must be >= 0");
     SKYRL_REQUIRE(min_p >= 0.f && min_p <= 1.f, "sample: min_p must be in [0,1]");
+    SKYRL_REQUIRE(top_p > 0.f && top_p <= 1.f, "sample: top_p must be in (0,1]");
     if (dtype == SKYRL_BF16)
-        return launch_sample<uint16_t>(logits, ld, nseq, V, temperature, top_k, min_p, seed, seq_ids, step, tokens_out,
-                                       logp_out, workspace, as_stream(stream));
+        return launch_sample<uint16_t>(logits, ld, nseq, V, temperature, top_k, top_p, min_p, seed, seq_ids, step,
+                                       tokens_out, logp_out, workspace, as_stream(stream));
     if (dtype == SKYRL_F32)
-        return launch_sample<float>(logits, ld, nseq, V, temperature, top_k, min_p, seed, seq_ids, step, tokens_out,
-                                    logp_out, workspace, as_stream(stream));
+        return launch_sample<float>(logits, ld, nseq, V, temperature, top_k, top_p, min_p, seed, seq_ids, step,
+                                    tokens_out, logp_out, workspace, as_stream(stream));
     return fail(SKYRL_ERR_INVALID, "sample: logits dtype must be bf16 or f32");
 }

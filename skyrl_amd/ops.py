@@ -479,6 +479,7 @@ def sample(
     *,
     temperature: float = 1.0,
     top_k: int = -1,
+    top_p: float = 1.0,
     min_p: float = 0.0,
     seed: int = 0,
     seq_ids: Optional[torch.Tensor] = None,
@@ -505,7 +506,8 @@ def sample(
         raise ValueError("logp_out must be a contiguous float32 tensor of nseq elements")
     ws = WORKSPACES.get(dev, "sample", _ffi.query("skyrl_sample_workspace_bytes", nseq, V))
     _ffi.call(
-        "skyrl_sample", _ptr(logits), dt, logits.stride(0), nseq, V, float(temperature), int(top_k), float(min_p),
+        "skyrl_sample", _ptr(logits), dt, logits.stride(0), nseq, V, float(temperature), int(top_k), float(top_p),
+        float(min_p),
         ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), _ptr(ids), int(step), _ptr(tokens), _ptr(logp), _ptr(ws),
         _stream(dev),
     )

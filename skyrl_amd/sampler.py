@@ -28,8 +28,6 @@ class TokenSampler:
     def __init__(self, nseq: int, vocab: int, max_steps: int, device, params: Optional[SamplingParams] = None,
                  seed: int = 0, seq_ids: Optional[torch.Tensor] = None, dtype=torch.bfloat16):
         p = params or SamplingParams()
-        if p.top_p is not None and p.top_p < 1.0:
-            raise NotImplementedError("top_p < 1 is not on the HIP sampler yet (top_k / min_p are)")
         self.nseq, self.vocab, self.max_steps = nseq, vocab, max_steps
         self.device = torch.device(device)
         self.params = p
@@ -51,7 +49,7 @@ class TokenSampler:
         [nseq, V] logits, row stride in elements, and the hipStream_t handle."""
         p = self.params
         rc = self._fn(logits_ptr, self.dtype_code, row_stride, self.nseq, self.vocab, float(p.temperature),
-                      int(p.top_k if p.top_k is not None else -1), float(p.min_p or 0.0),
+                      int(p.top_k if p.top_k is not None else -1), _top_p(p), float(p.min_p or 0.0),
                       ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self._ids_ptr, int(t),
                       self._tok_ptr + 4 * self.nseq * t, self._lp_ptr + 4 * self.nseq * t, self._ws_ptr,
                       stream_handle)
@@ -65,7 +63,8 @@ class TokenSampler:
         s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         p = self.params
         rc = self._fn(logits.data_ptr(), self.dtype_code, logits.stride(0), self.nseq, self.vocab,
-                      float(p.temperature), int(p.top_k if p.top_k is not None else -1), float(p.min_p or 0.0),
+                      float(p.temperature), int(p.top_k if p.top_k is not None else -1), _top_p(p),
+                      float(p.min_p or 0.0),
                       ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self.seq_ids.data_ptr(), int(t),
                       self.tokens[t].data_ptr(), self.logprobs[t].data_ptr(), self.workspace.data_ptr(), s)
         if rc != 0:
@@ -73,11 +72,13 @@ class TokenSampler:
         return self.tokens[t], self.logprobs[t]
 
 
+def _top_p(p: SamplingParams) -> float:
+    return 1.0 if p.top_p is None else float(p.top_p)
+
+
 def sample(logits: torch.Tensor, params: Optional[SamplingParams] = None, seed: int = 0,
            seq_ids: Optional[torch.Tensor] = None, step: int = 0):
     """One-shot sampling of [nseq, V] logits with reference SamplingParams semantics."""
     p = params or SamplingParams()
-    if p.top_p is not None and p.top_p < 1.0:
-        raise NotImplementedError("top_p < 1 is not on the HIP sampler yet (top_k / min_p are)")
     return ops.sample(logits, temperature=p.temperature, top_k=p.top_k if p.top_k is not None else -1,
-                      min_p=p.min_p or 0.0, seed=seed, seq_ids=seq_ids, step=step)
+                      top_p=_top_p(p), min_p=p.min_p or 0.0, seed=seed, seq_ids=seq_ids, step=step)

@@ -294,28 +294,10 @@ def test_pack_golden(golden, dev):
 
 
 # ------------------------------------------------------------------------------------------ a1 sampler
-def _oracle_sampler():
-    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libsampler_ref.so"))
-    f = lib.sampler_ref
-    f.restype = None
-    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                  ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_void_p]
-    return f
+def _oracle_sample(logits_cpu, temperature, top_k, min_p, seed, seq_ids, step, top_p=1.0):
+    from oracle import sampler as osamp
 
-
-def _oracle_sample(logits_cpu, temperature, top_k, min_p, seed, seq_ids, step):
-    f = _oracle_sampler()
-    n, V = logits_cpu.shape
-    bf = logits_cpu.dtype == torch.bfloat16
-    raw = logits_cpu.contiguous().view(torch.int16) if bf else logits_cpu.contiguous()
-    tok = torch.empty(n, dtype=torch.int32)
-    lp = torch.empty(n, dtype=torch.float32)
-    keys = torch.empty(V, dtype=torch.int32)
-    ids = seq_ids.contiguous()
-    f(raw.data_ptr(), int(bf), V, n, V, temperature, top_k, min_p, seed, ids.data_ptr(), step, tok.data_ptr(),
-      lp.data_ptr(), keys.data_ptr())
-    return tok, lp
+    return osamp.sample(logits_cpu, temperature, top_k, top_p, min_p, seed, seq_ids, step)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -366,6 +348,55 @@ def test_sampler_extreme_logit_range(dev):
         assert torch.equal(tok.cpu(), etok)
         close(lp, torch.log_softmax(logits.float(), -1)[torch.arange(n), etok.long()], atol=1e-4)
         assert torch.isfinite(lp).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("cfg", [(1.0, -1, 0.9, 0.0), (0.8, 50, 0.9, 0.0), (1.0, -1, 0.5, 0.02), (1.3, 200, 0.97, 0.0),
+                                 (1.0, -1, 0.001, 0.0)])
+def test_sampler_top_p_bit_exact_vs_oracle(dev, dtype, cfg):
+    """top_p (skyrl-tx generator.py:424-449) after top_k/min_p; 300 rows exercise the row mode."""
+    temp, top_k, top_p, min_p = cfg
+    g = torch.Generator().manual_seed(29)
+    n, V = 300, 5003
+    logits = (torch.randn(n, V, generator=g) * 2.0).to(dtype)
+    ids = torch.arange(n, dtype=torch.int64) + 11
+    tok, lp = ops.sample(logits.to(dev), temperature=temp, top_k=top_k, top_p=top_p, min_p=min_p, seed=9,
+                         seq_ids=ids.to(dev), step=4)
+    etok, elp = _oracle_sample(logits, temp, top_k, min_p, 9, ids, 4, top_p=top_p)
+    assert torch.equal(tok.cpu(), etok)
+    close(lp, elp, atol=1e-4)
+
+
+def test_sampler_top_p_ties_and_support(dev):
+    """bf16 logits on a coarse grid: the top_p cut lands inside tie groups (index-order rule)."""
+    g = torch.Generator().manual_seed(31)
+    n, V = 64, 2048
+    logits = torch.round(torch.randn(n, V, generator=g) * 2) / 2  # ~12 distinct values, large tie groups
+    logits = logits.to(torch.bfloat16)
+    for top_p in (0.3, 0.75, 0.95):
+        for step in range(3):
+            tok, _ = ops.sample(logits.to(dev), top_p=top_p, seed=3, step=step)
+            etok, _ = _oracle_sample(logits, 1.0, -1, 0.0, 3, torch.arange(n), step, top_p=top_p)
+            assert torch.equal(tok.cpu(), etok)
+        # every sampled token is inside the nucleus computed in float64 (cut ties in index order)
+        x = logits.double()
+        p = torch.softmax(x, -1)
+        order = torch.sort(-x, dim=-1, stable=True).indices
+        ps = torch.gather(p, 1, order)
+        keep_sorted = (torch.cumsum(ps, -1) - ps) < top_p
+        keep_sorted[:, 0] = True
+        keep = torch.zeros_like(keep_sorted)
+        keep.scatter_(1, order, keep_sorted)
+        assert keep[torch.arange(n), tok.cpu().long()].all()
+
+
+def test_sampler_top_p_distribution(dev):
+    small = torch.tensor([[0.0, 1.0, 2.0, -1.0]]).repeat(20000, 1)
+    tok, _ = ops.sample(small.to(dev), top_p=0.7, seed=5, seq_ids=torch.arange(20000, device=dev), step=0)
+    freq = torch.bincount(tok.cpu().long(), minlength=4).float() / 20000
+    p = torch.softmax(small[0], -1)
+    expect = torch.tensor([0.0, p[1], p[2], 0.0]) / (p[1] + p[2])  # nucleus {2, 1}
+    close(freq, expect, atol=0.015)
 
 
 def test_sampler_odd_vocab_and_distribution(dev):
