@@ -163,17 +163,41 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
     constexpr int NW = kFT / kWave;
     constexpr int KB = sizeof(T) * 8;
     __shared__ unsigned long long hist[256];
-    __shared__ unsigned long long s_red[NW];
+    __shared__ unsigned long long s_red[NW], s_red2[NW];
+    __shared__ unsigned long long s_fine[kFT];
     __shared__ uint32_t s_u[NW];
     __shared__ uint32_t s_sel[2];               // selected d, found flag
     __shared__ unsigned long long s_below, s_at;
     __shared__ int s_ic;
     const T* row = logits + (int64_t)blockIdx.x * ld;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    constexpr int VEC = 16 / sizeof(T);
+    // every pass visits the row in 16-B vectors where aligned (VEC elements per thread per
+    // step), the unaligned head/tail element-wise; fn(raw, index)
+    const int head = (int)((16 - (reinterpret_cast<uintptr_t>(row) & 15)) & 15) / (int)sizeof(T);
+    const int h0 = head < V ? head : V;
+    const int nv = (V - h0) / VEC;
+    const int t0 = h0 + nv * VEC;
+    auto for_each = [&](auto fn) {
+        if ((reinterpret_cast<uintptr_t>(row) & (sizeof(T) - 1)) == 0) {
+            for (int i = threadIdx.x; i < h0; i += kFT) fn(row[i], i);
+            const uint4* rv = reinterpret_cast<const uint4*>(row + h0);
+            for (int j = threadIdx.x; j < nv; j += kFT) {
+                const uint4 pk = rv[j];
+                T vals[VEC];
+                __builtin_memcpy(vals, &pk, 16);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) fn(vals[k], h0 + j * VEC + k);
+            }
+            for (int i = t0 + threadIdx.x; i < V; i += kFT) fn(row[i], i);
+        } else {
+            for (int i = threadIdx.x; i < V; i += kFT) fn(row[i], i);
+        }
+    };
 
     // pass 0: max key (an integer max, exact)
     uint32_t km = 0u;
-    for (int i = threadIdx.x; i < V; i += kFT) km = max(km, okey<T>(row[i]));
+    for_each([&](T raw, int) { km = max(km, okey<T>(raw)); });
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) km = max(km, (uint32_t)__shfl_xor((int)km, off, kWave));
     if (lane == 0) s_u[w] = km;
@@ -193,13 +217,12 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
             const int shift = KB - 8 * (lvl + 1);
             for (int j = threadIdx.x; j < 256; j += kFT) hist[j] = 0ull;
             __syncthreads();
-            for (int i = threadIdx.x; i < V; i += kFT) {
-                const T raw = row[i];
+            for_each([&](T raw, int i) {
                 const uint32_t d = kmax - okey<T>(raw);
-                if (lvl > 0 && (d >> (shift + 8)) != prefix) continue;
+                if (lvl > 0 && (d >> (shift + 8)) != prefix) return;
                 const unsigned long long wt = weight(raw, i);
                 if (wt) atomicAdd(&hist[(d >> shift) & 255u], wt);
-            }
+            });
             __syncthreads();
             if (threadIdx.x == 0) {
                 unsigned long long cum = below;
@@ -222,10 +245,76 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
         return R{prefix, below, at};
     };
 
+    // bf16 fast path: one pass with a full-resolution histogram of d < kFine (every bf16 value
+    // within kFine steps of the max has its own bin; the rest is summed in registers), then a
+    // block-wide scan of the bins. Falls back to the radix passes when the target is not
+    // reached inside the window.
+    constexpr int kFine = kFT;
+    struct Sel { bool ok; uint32_t d; unsigned long long below, at, total; };
+    auto fine = [&](auto weight, double target, bool want_total) -> Sel {
+        unsigned long long* fh = reinterpret_cast<unsigned long long*>(s_fine);
+        fh[threadIdx.x] = 0ull;
+        __syncthreads();
+        unsigned long long rest = 0ull;
+        for_each([&](T raw, int i) {
+            const unsigned long long wt = weight(raw, i);
+            if (!wt) return;
+            const uint32_t d = kmax - okey<T>(raw);
+            if (d < (uint32_t)kFine) atomicAdd(&fh[d], wt);
+            else rest += wt;
+        });
+        __syncthreads();
+        // inclusive scan over the kFine bins (bin = thread), plus the out-of-window total
+        const unsigned long long mine = fh[threadIdx.x];
+        unsigned long long incl = mine;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const unsigned long long o = (unsigned long long)__shfl_up((long long)incl, off, kWave);
+            if (lane >= off) incl += o;
+        }
+        if (want_total) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) rest += (unsigned long long)__shfl_xor((long long)rest, off, kWave);
+        }
+        if (lane == kWave - 1) s_red[w] = incl;
+        if (lane == 0) s_red2[w] = rest;
+        if (threadIdx.x == 0) s_sel[1] = 0u;
+        __syncthreads();
+        unsigned long long off_w = 0ull, win = 0ull, tot_rest = 0ull;
+        for (int j = 0; j < NW; ++j) {
+            if (j < w) off_w += s_red[j];
+            win += s_red[j];
+            tot_rest += s_red2[j];
+        }
+        const unsigned long long total = win + tot_rest;
+        const double tgt = target < 0.0 ? (double)top_p * (double)total : target;  // top_p: p * Z
+        const unsigned long long cum_in = off_w + incl, cum_before = cum_in - mine;
+        if (mine && (double)cum_before < tgt && (double)cum_in >= tgt) {
+            s_sel[0] = threadIdx.x;
+            s_sel[1] = 1u;
+            s_below = cum_before;
+            s_at = mine;
+        }
+        __syncthreads();
+        Sel r{s_sel[1] != 0u, s_sel[0], s_below, s_at, total};
+        __syncthreads();
+        return r;
+    };
+
     uint32_t tk = 0u;
     if (top_k > 0 && top_k < V) {
-        const auto r = radix([&](T, int) -> unsigned long long { return 1ull; }, (double)top_k);
-        tk = kmax - r.d;
+        bool done = false;
+        if constexpr (sizeof(T) == 2) {
+            const Sel f = fine([&](T, int) -> unsigned long long { return 1ull; }, (double)top_k, false);
+            if (f.ok) {
+                tk = kmax - f.d;
+                done = true;
+            }
+        }
+        if (!done) {
+            const auto r = radix([&](T, int) -> unsigned long long { return 1ull; }, (double)top_k);
+            tk = kmax - r.d;
+        }
     }
     uint32_t kc = 0u;
     int ic = 0x7fffffff;
@@ -233,22 +322,42 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
         auto kept = [&](T raw) -> bool {
             return okey<T>(raw) >= tk && (!use_minp || to_f<T>(raw) * inv_t >= mthr);
         };
-        // Z: exact integer sum of the kept masses
-        unsigned long long z = 0ull;
-        for (int i = threadIdx.x; i < V; i += kFT) {
-            const T raw = row[i];
-            if (kept(raw)) z += mass_q(to_f<T>(raw), mx, inv_t);
+        auto wmass = [&](T raw, int) -> unsigned long long {
+            return kept(raw) ? (unsigned long long)mass_q(to_f<T>(raw), mx, inv_t) : 0ull; };
+        uint32_t dsel = 0u;
+        unsigned long long below = 0ull, at = 0ull, Z = 0ull;
+        double target = 0.0;
+        bool done = false;
+        if constexpr (sizeof(T) == 2) {  // Z and the cut in one pass (target = p * Z inside)
+            const Sel f = fine(wmass, -1.0, true);
+            Z = f.total;
+            target = (double)top_p * (double)Z;
+            if (f.ok) {
+                dsel = f.d;
+                below = f.below;
+                at = f.at;
+                done = true;
+            }
         }
+        if (!done) {
+            if (Z == 0ull) {  // Z: exact integer sum of the kept masses
+                unsigned long long z = 0ull;
+                for_each([&](T raw, int i) { z += wmass(raw, i); });
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) z += (unsigned long long)__shfl_xor((long long)z, off, kWave);
-        if (lane == 0) s_red[w] = z;
-        __syncthreads();
-        unsigned long long Z = 0ull;
+                for (int off = 32; off > 0; off >>= 1) z += (unsigned long long)__shfl_xor((long long)z, off, kWave);
+                if (lane == 0) s_red[w] = z;
+                __syncthreads();
 #pragma unroll
-        for (int j = 0; j < NW; ++j) Z += s_red[j];
-        const double target = (double)top_p * (double)Z;
-        const auto r = radix([&](T raw, int) -> unsigned long long {
-            return kept(raw) ? (unsigned long long)mass_q(to_f<T>(raw), mx, inv_t) : 0ull; }, target);
+                for (int j = 0; j < NW; ++j) Z += s_red[j];
+                __syncthreads();
+                target = (double)top_p * (double)Z;
+            }
+            const auto r = radix(wmass, target);
+            dsel = r.d;
+            below = r.below;
+            at = r.at;
+        }
+        struct { uint32_t d; unsigned long long below, at; } r{dsel, below, at};
         kc = kmax - r.d;
         const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
         const unsigned long long A = r.below;
@@ -261,22 +370,40 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
             if (kc == kmax && c < 1) c = 1;
             const long long cnt = (long long)(r.at / qc);
             if (c < cnt) {
-                // index of the c-th tie token (1-based) in index order: rounds of kFT elements
+                // index of the c-th tie token (1-based) in index order: rounds of kFT contiguous
+                // chunks of CH elements (thread t owns [base + t*CH, base + (t+1)*CH))
+                constexpr int CH = 16;
                 if (threadIdx.x == 0) s_ic = 0x7fffffff;
                 long long seen = 0;
-                for (int base = 0; base < V; base += kFT) {
-                    const int i = base + threadIdx.x;
-                    const bool hit = i < V && okey<T>(row[i]) == kc && kept(row[i]);
-                    const uint64_t bm = __builtin_amdgcn_ballot_w64(hit);
-                    const int before_w = __builtin_popcountll(bm & ((1ull << lane) - 1ull));
-                    if (lane == 0) s_u[w] = (uint32_t)__builtin_popcountll(bm);
+                for (int base = 0; base < V; base += kFT * CH) {
+                    const int i0 = base + threadIdx.x * CH;
+                    int cntt = 0;
+                    for (int k = 0; k < CH; ++k) {
+                        const int i = i0 + k;
+                        if (i < V && okey<T>(row[i]) == kc && kept(row[i])) ++cntt;
+                    }
+                    // block exclusive scan of cntt (wave scan + per-wave totals)
+                    int incl = cntt;
+#pragma unroll
+                    for (int off = 1; off < kWave; off <<= 1) {
+                        const int o = __shfl_up(incl, off, kWave);
+                        if (lane >= off) incl += o;
+                    }
+                    if (lane == kWave - 1) s_u[w] = (uint32_t)incl;
                     __syncthreads();
                     long long off_w = 0, tot = 0;
                     for (int j = 0; j < NW; ++j) {
                         if (j < w) off_w += s_u[j];
                         tot += s_u[j];
                     }
-                    if (hit && seen + off_w + before_w + 1 == c) s_ic = i;
+                    const long long before = seen + off_w + (incl - cntt);
+                    if (cntt > 0 && before < c && before + cntt >= c) {  // the c-th is in my chunk
+                        long long r2 = before;
+                        for (int k = 0; k < CH; ++k) {
+                            const int i = i0 + k;
+                            if (i < V && okey<T>(row[i]) == kc && kept(row[i]) && ++r2 == c) s_ic = i;
+                        }
+                    }
                     seen += tot;
                     __syncthreads();
                     if (seen >= c) break;
