@@ -40,7 +40,10 @@ import torch.distributed as dist  # noqa: E402
 
 P_MAX, R_MAX, PROMPTS, GROUP, VOCAB = 512, 1024, 64, 8, 151936
 QWEN_1_5B_PARAMS = 1_543_714_304  # Qwen2.5-1.5B, tied embeddings
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy ~6.3 TB/s
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# measured on the box by scripts/probe/stream_probe.py (reported beside frac, never instead of it)
+CEILING_READ_GBS = 6100.0    # read-only stream
+CEILING_RW_GBS = 4865.0      # 50/50 read+write copy (16-B nt loads/stores, 5 GB)
 
 
 def log(msg):
@@ -274,14 +277,15 @@ def run(args):
     # per-kernel roofline: algorithmic bytes per launch / average event-timed launch duration
     rows_per_launch = mb * R
     kernels = {}
-    for name, tm, nbytes, launches_per_step in (
-        ("skyrl_sample (sample_kernel<bf16,1>)", sample_timer, N * V * 2 + N * 16, R),
+    for name, tm, nbytes, launches_per_step, ceiling in (
+        ("skyrl_sample (sample_kernel<bf16,3,512>: T=1, one workgroup per row)", sample_timer, N * V * 2 + N * 16, R,
+         CEILING_READ_GBS),
         ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
-         2 * (N // mb) + (N // mb if args.unfused else 0)),
+         2 * (N // mb) + (N // mb if args.unfused else 0), CEILING_READ_GBS),
         ("skyrl_policy_train_fwd (policy_train_resident_kernel)", train_timer,
-         rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb),
+         rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb, CEILING_RW_GBS),
         ("skyrl_adamw_step (sumsq + plan + adamw_update_kernel<shadow>)", adam_timer,
-         (reducer.layout.shard_numel * (4 + 30)) if reducer is not None else 0, 1),
+         (reducer.layout.shard_numel * (4 + 30)) if reducer is not None else 0, 1, CEILING_RW_GBS),
     ):
         if not tm.pairs:
             continue
@@ -289,7 +293,8 @@ def run(args):
         kernels[name] = {"avg_launch_ms": round(ms, 4), "bytes_per_launch": int(nbytes),
                          "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                          "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "ms_per_step": round(ms * launches_per_step, 2), "launches_timed": len(tm.pairs)}
+                         "ms_per_step": round(ms * launches_per_step, 2), "launches_timed": len(tm.pairs),
+                         "ceiling_GBps": ceiling}
     dom_name = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     dom = kernels[dom_name]
     result = {
@@ -324,6 +329,8 @@ def run(args):
             "traffic": pmc_traffic(dom_name, dom["bytes_per_launch"]),
             "bytes_per_launch": dom["bytes_per_launch"],
             "avg_launch_ms": dom["avg_launch_ms"],
+            "measured_ceiling_GBps": dom["ceiling_GBps"],
+            "frac_of_measured_ceiling": round(dom["achieved_GBps"] / dom["ceiling_GBps"], 4),
         },
         "kernels": kernels,
         "cpu_baseline": None,

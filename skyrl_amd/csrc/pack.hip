@@ -9,16 +9,22 @@
 // (trainer.py:872-907): rows N..N+pad-1 clone rows 0..pad-1, loss_mask 0.
 //
 // Pure byte movement (HBM-bound, ~23 MB at N=512, P=512, R=1024): grid =
-// (output row, 512-column tile); each thread writes two adjacent int64 columns
-// with one 16-B store where the row allows it.
+// (output row, 1024-column tile); each thread writes four adjacent columns of every
+// output with 16-B stores when the row widths allow it.
 #include "common.h"
 
 namespace skyrl {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kCols = kThreads * 2;
+constexpr int kQ = 4;                  // columns per thread
+constexpr int kCols = kThreads * kQ;   // columns per workgroup
 
+// Output row i (< N: sample i; >= N: pad row cloning sample i - N with loss_mask 0). Each
+// thread produces kQ adjacent columns; with VEC (row widths multiple of kQ, 16-B aligned
+// bases) every output is written with full 16-B stores, one instruction per array and
+// thread, so each wave store covers whole cache lines.
+template <bool VEC>
 __global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, int N, int P, int R, int64_t pad_id,
                                                         int64_t* __restrict__ seq, int64_t* __restrict__ att,
                                                         int64_t* __restrict__ rmask, float* __restrict__ rew,
@@ -32,40 +38,65 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, in
     const int lpad = P - plen;
     const int64_t r0 = in.response_off[src];
     const int rlen = (int)(in.response_off[src + 1] - r0);
-    const int c0 = blockIdx.y * kCols + threadIdx.x * 2;
+    const int64_t w0 = in.reward_off[src];
+    const int wl = (int)(in.reward_off[src + 1] - w0);
+    const int64_t m0 = in.loss_mask_off[src];
+    const int ml = is_pad ? 0 : (int)(in.loss_mask_off[src + 1] - m0);
+    const int64_t l0 = rlp ? in.logprob_off[src] : 0;
+    const int ll = rlp ? (int)(in.logprob_off[src + 1] - l0) : 0;
+    const int c0 = blockIdx.y * kCols + threadIdx.x * kQ;
     const int64_t so = (int64_t)i * S;
     const int64_t ro = (int64_t)i * R;
+    int64_t tk[kQ], at[kQ], rm[kQ];
+    float rw[kQ], lm[kQ], lp[kQ];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kQ; ++k) {
         const int c = c0 + k;
-        if (c < S) {
-            int64_t tok;
-            int64_t a;
-            if (c < P) {
-                const bool real = c >= lpad;
-                tok = real ? in.prompt_tokens[p0 + (c - lpad)] : pad_id;
-                a = real ? 1 : 0;
-            } else {
-                const int j = c - P;
-                const bool real = j < rlen;
-                tok = real ? in.response_tokens[r0 + j] : pad_id;
-                a = real ? 1 : 0;
-            }
-            seq[so + c] = tok;
-            att[so + c] = a;
+        if (c < P) {
+            const bool real = c >= lpad;
+            tk[k] = real ? in.prompt_tokens[p0 + (c - lpad)] : pad_id;
+            at[k] = real;
+        } else {
+            const int j = c - P;
+            const bool real = j < rlen && c < S;
+            tk[k] = real ? in.response_tokens[r0 + j] : pad_id;
+            at[k] = real;
         }
-        if (c < R) {
-            rmask[ro + c] = c < rlen ? 1 : 0;
-            const int64_t w0 = in.reward_off[src];
-            const int wl = (int)(in.reward_off[src + 1] - w0);
-            rew[ro + c] = c < wl ? in.reward_vals[w0 + c] : 0.f;
-            const int64_t m0 = in.loss_mask_off[src];
-            const int ml = (int)(in.loss_mask_off[src + 1] - m0);
-            lmask[ro + c] = (!is_pad && c < ml) ? in.loss_mask_vals[m0 + c] : 0.f;
-            if (rlp) {
-                const int64_t l0 = in.logprob_off[src];
-                const int ll = (int)(in.logprob_off[src + 1] - l0);
-                rlp[ro + c] = c < ll ? in.logprob_vals[l0 + c] : 0.f;
+        rm[k] = c < rlen;
+        rw[k] = c < wl ? in.reward_vals[w0 + c] : 0.f;
+        lm[k] = c < ml ? in.loss_mask_vals[m0 + c] : 0.f;
+        lp[k] = c < ll ? in.logprob_vals[l0 + c] : 0.f;
+    }
+    if (VEC) {
+        if (c0 < S) {
+            longlong2* s2 = reinterpret_cast<longlong2*>(seq + so + c0);
+            longlong2* a2 = reinterpret_cast<longlong2*>(att + so + c0);
+            s2[0] = make_longlong2(tk[0], tk[1]);
+            s2[1] = make_longlong2(tk[2], tk[3]);
+            a2[0] = make_longlong2(at[0], at[1]);
+            a2[1] = make_longlong2(at[2], at[3]);
+        }
+        if (c0 < R) {
+            longlong2* m2 = reinterpret_cast<longlong2*>(rmask + ro + c0);
+            m2[0] = make_longlong2(rm[0], rm[1]);
+            m2[1] = make_longlong2(rm[2], rm[3]);
+            *reinterpret_cast<float4*>(rew + ro + c0) = make_float4(rw[0], rw[1], rw[2], rw[3]);
+            *reinterpret_cast<float4*>(lmask + ro + c0) = make_float4(lm[0], lm[1], lm[2], lm[3]);
+            if (rlp) *reinterpret_cast<float4*>(rlp + ro + c0) = make_float4(lp[0], lp[1], lp[2], lp[3]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kQ; ++k) {
+            const int c = c0 + k;
+            if (c < S) {
+                seq[so + c] = tk[k];
+                att[so + c] = at[k];
+            }
+            if (c < R) {
+                rmask[ro + c] = rm[k];
+                rew[ro + c] = rw[k];
+                lmask[ro + c] = lm[k];
+                if (rlp) rlp[ro + c] = lp[k];
             }
         }
     }
@@ -117,8 +148,15 @@ extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int
     const int cols = S > R ? S : R;
     if (cols == 0) return SKYRL_OK;
     dim3 grid(N + pad, (cols + kCols - 1) / kCols);
-    hipLaunchKernelGGL(pack_kernel, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id, sequences,
-                       attention_mask, response_mask, rewards, loss_mask, rollout_logprobs);
+    auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool vec = S % kQ == 0 && R % kQ == 0 && a16(sequences) && a16(attention_mask) && a16(response_mask) &&
+                     a16(rewards) && a16(loss_mask) && (!rollout_logprobs || a16(rollout_logprobs));
+    if (vec)
+        hipLaunchKernelGGL(pack_kernel<true>, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id,
+                           sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs);
+    else
+        hipLaunchKernelGGL(pack_kernel<false>, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id,
+                           sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs);
     return check_launch("pack_kernel");
 }
 
