@@ -27,7 +27,7 @@ import torch
 
 from . import ops
 from .config import AlgorithmConfig
-from .torch_utils import masked_mean
+from .torch_utils import masked_mean, safe_exp_delta
 
 try:  # Python >= 3.11
     from enum import StrEnum
@@ -261,11 +261,28 @@ def ppo_params_from_config(config, *, use_kl_loss=False, use_entropy_loss=False,
 
 
 def ppo_policy_loss(log_probs, old_log_probs, advantages, config, loss_mask=None, rollout_logprobs=None):
-    """regular / dual_clip PPO loss on the HIP path (ppo_utils.py:548-586)."""
+    """regular / dual_clip PPO loss on the HIP path (ppo_utils.py:548-586).
+
+    With off-policy correction enabled (off_policy_correction_utils.py:262-296) the TIS ratio
+    w > 0 (detached) folds into the advantages -- -min(r A w, clip(r) A w) = w * -min(r A, clip(r) A),
+    and dual_clip's branch on sign(A) is unchanged -- and the corrected mask drives the
+    reduction, so the same HIP kernels run; clip_ratio keeps the uncorrected mask, as in the
+    reference (it is computed before the correction).
+    """
     assert config.policy_loss_type in ["regular", "dual_clip"], "loss_type must be either 'regular' or 'dual_clip'"
-    if rollout_logprobs is not None and _off_policy_enabled(config):
-        raise NotImplementedError("off_policy_correction is not on the HIP loss path yet")
     params = ppo_params_from_config(config)
+    if rollout_logprobs is not None and _off_policy_enabled(config):
+        from .secondary import off_policy_terms
+
+        tis, extra, pg_mask = off_policy_terms(old_log_probs, rollout_logprobs, loss_mask,
+                                               config.off_policy_correction)
+        adv = advantages * tis if tis is not None else advantages
+        loss, _ = ops.ppo_loss(log_probs, old_log_probs, adv, pg_mask, params)
+        with torch.no_grad():
+            ratio = safe_exp_delta(log_probs.detach() - old_log_probs, clip=20.0, out_dtype=log_probs.dtype)
+            clipped = ratio.clamp(1 - config.eps_clip_low, 1 + config.eps_clip_high)
+            clip = masked_mean((-(clipped * advantages) > -(ratio * advantages)).float(), loss_mask).mean().item()
+        return loss, {"clip_ratio": clip, **extra}
     loss, metrics = ops.ppo_loss(log_probs, old_log_probs, advantages, loss_mask, params)
     return loss, {"clip_ratio": metrics[4].item()}
 

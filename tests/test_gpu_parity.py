@@ -208,6 +208,39 @@ def test_ppo_north_star_size_vs_oracle(dev):
     close(x.grad, xc.grad, atol=1e-9, rtol=1e-4)
 
 
+@pytest.mark.parametrize("case", ["tis_token", "tis_seq", "mask_geo", "mask_prod", "tis_outlier"])
+@pytest.mark.parametrize("lt", ["regular", "dual_clip"])
+def test_ppo_off_policy_correction_golden(golden, dev, case, lt):
+    """ppo_policy_loss + apply_off_policy_correction (off_policy_correction_utils.py:7-296) on
+    the HIP loss, against the reference's own outputs (tests/golden/ppo_offpolicy.npz)."""
+    from skyrl_amd import ppo_utils
+    from skyrl_amd.config import AlgorithmConfig, OffPolicyCorrectionConfig
+
+    d = golden("ppo_offpolicy")
+    kw = {"tis_token": dict(tis_ratio_type="token", token_tis_ratio_clip_high=2.0),
+          "tis_seq": dict(tis_ratio_type="sequence", sequence_tis_ratio_clip_high=5.0),
+          "mask_geo": dict(sequence_mask_metric="geometric", geo_mask_high=1.01, geo_mask_low=0.99),
+          "mask_prod": dict(sequence_mask_metric="product", product_mask_high=2.0, product_mask_low=0.5),
+          "tis_outlier": dict(tis_ratio_type="token", token_tis_ratio_clip_high=3.0,
+                              outlier_token_is_threshold_low=0.2, outlier_token_is_threshold_high=4.0)}[case]
+    cfg = AlgorithmConfig(policy_loss_type=lt, loss_reduction="token_mean", eps_clip_low=0.2, eps_clip_high=0.28,
+                          off_policy_correction=OffPolicyCorrectionConfig(**kw))
+    x = d["log_probs"].to(dev).requires_grad_(True)
+    loss, m = ppo_utils.PolicyLossRegistry.get(lt)(x, d["old_log_probs"].to(dev), d["advantages"].to(dev), cfg,
+                                                    loss_mask=d["loss_mask"].to(dev),
+                                                    rollout_logprobs=d["rollout_logprobs"].to(dev))
+    loss.backward()
+    t = f"{case}_{lt}"
+    ref_loss = float(d[f"loss_{t}"])
+    assert float(loss.detach()) == pytest.approx(ref_loss, rel=1e-5, abs=1e-5)
+    g = d[f"grad_{t}"]
+    torch.testing.assert_close(x.grad.cpu(), g, atol=1e-5 * max(1.0, float(g.abs().max())), rtol=1e-4)
+    keys = [str(k) for k in d[f"mkeys_{t}"]]
+    assert sorted(m) == keys
+    for k, v in zip(keys, d[f"mvals_{t}"].tolist()):
+        assert m[k] == pytest.approx(v, rel=1e-5, abs=1e-6), k
+
+
 # ------------------------------------------------------------------------------------------ a8 critic
 def test_critic_golden(golden, dev):
     d = golden("critic")

@@ -276,6 +276,43 @@ def gen_ppo(pu, cfgmod):
          **out)
 
 
+def gen_ppo_offpolicy(pu, cfgmod):
+    """ppo_policy_loss with apply_off_policy_correction enabled (off_policy_correction_utils.py:7-296)."""
+    g = torch.Generator().manual_seed(123)
+    n, R = 8, 33
+    lp, old, adv, mask, ref, ent = _ppo_inputs(g, n, R)
+    rollout = old + torch.randn(n, R, generator=g) * 0.05
+    rollout[3] = old[3] - 1.5        # large token ratios: tis caps, outlier / product masks fire
+    rollout[4] = old[4] + 0.004      # geometric mean just inside [0.99, 1.01]
+    cases = {
+        "tis_token": dict(tis_ratio_type="token", token_tis_ratio_clip_high=2.0),
+        "tis_seq": dict(tis_ratio_type="sequence", sequence_tis_ratio_clip_high=5.0),
+        "mask_geo": dict(sequence_mask_metric="geometric", geo_mask_high=1.01, geo_mask_low=0.99),
+        "mask_prod": dict(sequence_mask_metric="product", product_mask_high=2.0, product_mask_low=0.5),
+        "tis_outlier": dict(tis_ratio_type="token", token_tis_ratio_clip_high=3.0,
+                            outlier_token_is_threshold_low=0.2, outlier_token_is_threshold_high=4.0),
+    }
+    out = {}
+    names = []
+    for tag, kw in cases.items():
+        for lt in ("regular", "dual_clip"):
+            opc = cfgmod.OffPolicyCorrectionConfig(**kw)
+            cfg = cfgmod.AlgorithmConfig(policy_loss_type=lt, loss_reduction="token_mean",
+                                         eps_clip_low=0.2, eps_clip_high=0.28, off_policy_correction=opc)
+            x = lp.clone().requires_grad_(True)
+            loss, m = pu.PolicyLossRegistry.get(lt)(x, old, adv, cfg, loss_mask=mask, rollout_logprobs=rollout)
+            loss.backward()
+            t = f"{tag}_{lt}"
+            out[f"loss_{t}"] = loss.detach()
+            out[f"grad_{t}"] = x.grad
+            keys = sorted(m)
+            out[f"mkeys_{t}"] = np.array(keys)
+            out[f"mvals_{t}"] = np.array([float(m[k]) for k in keys], dtype=np.float64)
+            names.append(t)
+    save("ppo_offpolicy", log_probs=lp, old_log_probs=old, advantages=adv, loss_mask=mask, rollout_logprobs=rollout,
+         **out)
+
+
 def gen_critic(pu, cfgmod):
     g = torch.Generator().manual_seed(5)
     n, R = 5, 29
@@ -413,14 +450,19 @@ def main():
     from skyrl_train.utils import torch_utils as tu
 
     assert not tu.FLASH_ATTN_CROSS_ENTROPY_LOSS_AVAILABLE
-    gen_grpo(pu)
-    gen_gae(pu)
-    gen_kl(pu)
-    gen_ppo(pu, cfgmod)
-    gen_critic(pu, cfgmod)
-    gen_logprob(tu)
-    gen_pack(pre, trainer_mod, tb)
-    gen_reward_kl(trainer_mod, tb, cfgmod)
+    jobs = {
+        "grpo": lambda: gen_grpo(pu),
+        "gae": lambda: gen_gae(pu),
+        "kl": lambda: gen_kl(pu),
+        "ppo": lambda: gen_ppo(pu, cfgmod),
+        "ppo_offpolicy": lambda: gen_ppo_offpolicy(pu, cfgmod),
+        "critic": lambda: gen_critic(pu, cfgmod),
+        "logprob": lambda: gen_logprob(tu),
+        "pack": lambda: gen_pack(pre, trainer_mod, tb),
+        "reward_kl": lambda: gen_reward_kl(trainer_mod, tb, cfgmod),
+    }
+    for name in (sys.argv[1:] or list(jobs)):  # `python -B tools/gen_golden.py ppo_offpolicy` regenerates one
+        jobs[name]()
 
 
 if __name__ == "__main__":
