@@ -114,10 +114,15 @@ def run(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # rehearsal of the N>1 path with several ranks on one GPU (RCCL refuses duplicate GPUs)
+            dist.init_process_group(args.backend)
     N = PROMPTS * GROUP
     R, V, mb = R_MAX, VOCAB, args.micro_batch
     data, uids = synth_inputs(dev, N, seed=1234 + rank)
@@ -431,6 +436,7 @@ def cpu_baseline(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--micro-batch", type=int, default=16)

@@ -215,6 +215,8 @@ class ShardedAdamW:
 
         self._ffi = _ffi
         dev = _require_gpu(reducer.grad)
+        self._dev = dev
+        self._gathered = None
         self.reducer = reducer
         self.cfg = config
         lay = reducer.layout
@@ -244,8 +246,6 @@ class ShardedAdamW:
         self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         self._ws = torch.zeros(int(_ffi.query("skyrl_sumsq_workspace_bytes", lay.shard_numel)), dtype=torch.uint8,
                                device=dev)
-        self._dev = dev
-        self._gathered = None
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self._dev).cuda_stream)
