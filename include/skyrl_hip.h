@@ -173,6 +173,29 @@ int skyrl_logprob_bwd(const void* logits, int dtype, int64_t stride_b, int64_t s
                       const float* entropy, const float* grad_logp, const float* grad_entropy,
                       void* grad_logits, void* stream);
 
+/* ---- §8(f)1: lm_head-fused logprob + entropy (logits never materialized) ----
+ * Replaces the lm_head output -> logits.div_(T) -> logprobs_from_logits +
+ * chunked_entropy_from_logits sequence of HFModelWrapper.forward
+ * (model_wrapper.py:308-363; torch_utils.py:59-177). The caller cuts V into chunks
+ * and, per chunk c (columns [v0, v0+vc)), runs the plain GEMM z = h @ W[v0:v0+vc]^T
+ * (bf16 [T,vc], row stride ldz) into one reused buffer, then:
+ *   skyrl_lmhead_chunk_fwd  merges z into the per-token state (skyrl_lmhead_state_bytes(T);
+ *                           first=1 on chunk 0, which needs no initialized state); on the
+ *                           chunk with last=1 writes logp/entropy/lse f32 [T] (entropy,
+ *                           lse may be NULL). labels: int64, token r at labels[r*label_stride].
+ *   skyrl_lmhead_chunk_bwd  dz (bf16 [T,vc], row stride lddz) = dL/dz for the chunk, from the
+ *                           forward's lse/entropy and the upstream grad_logp/grad_entropy
+ *                           (grad_entropy may be NULL); same formula as skyrl_logprob_bwd.
+ * The caller then accumulates dh += dz @ W_chunk and dW_chunk = dz^T @ h.            */
+size_t skyrl_lmhead_state_bytes(int32_t T);
+int skyrl_lmhead_chunk_fwd(const void* z, int64_t ldz, int32_t T, int32_t vc, int64_t v0, const int64_t* labels,
+                           int64_t label_stride, float temperature, void* state, int32_t first, int32_t last,
+                           float* logp_out, float* entropy_out, float* lse_out, void* stream);
+int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int32_t vc, int64_t v0, const int64_t* labels,
+                           int64_t label_stride, float temperature, const float* lse, const float* entropy,
+                           const float* grad_logp, const float* grad_entropy, void* dz, int64_t lddz,
+                           void* stream);
+
 /* ---- a2+a3+a6+a7 fused: the policy training pass ------------------------------
  * One call per micro-batch replaces logprob fwd + fused loss fwd + loss bwd +
  * logprob bwd (same values and gradients as those four, see policy_train.hip):

@@ -852,7 +852,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
 }
 
 int splits_for(int nseq, int V) {
-    if (nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
+    if (nseq <= 0 || V <= 0 || nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
     int s = (2048 + nseq - 1) / nseq;
     const int max_s = (V + 4095) / 4096;  // at least 4096 elements per split
     if (s > max_s) s = max_s;

@@ -48,6 +48,15 @@ def test_workspace_queries():
     assert _ffi.query("skyrl_gae_workspace_bytes", 512) >= 512 * 24
 
 
+def test_workspace_queries_degenerate_sizes():
+    """Host-only size queries must not trap (e.g. divide by zero) on empty batches."""
+    for name, args in (("skyrl_sample_workspace_bytes", (0, 7)), ("skyrl_sample_workspace_bytes", (1, 1)),
+                       ("skyrl_gae_workspace_bytes", (0,)), ("skyrl_ppo_loss_workspace_bytes", (0, 0)),
+                       ("skyrl_reward_kl_workspace_bytes", (0,)), ("skyrl_critic_loss_workspace_bytes", (0, 0)),
+                       ("skyrl_policy_train_workspace_bytes", (0, 0)), ("skyrl_sumsq_workspace_bytes", (0,))):
+        assert _ffi.query(name, *args) > 0, name
+
+
 def test_oracle_sampler_builds():
     path = os.path.join(ROOT, "oracle", "_build", "libsampler_ref.so")
     assert os.path.exists(path), "oracle C restatement not built (make -C oracle)"
