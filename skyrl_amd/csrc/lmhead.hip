@@ -6,9 +6,8 @@
 // (:59-111). The backward writes bf16 dlogits [n,S,V], which the lm_head backward GEMMs read.
 //
 // Here the vocabulary is cut into chunks of vc columns. For each chunk the host runs one plain
-// library GEMM, Z_c = h @ W_c^T (hipBLASLt), into ONE reused bf16 [T,vc] buffer. The buffer is
-// sized to stay resident in the 256 MiB Infinity Cache. The kernels below consume it while
-// it is hot:
+// library GEMM, Z_c = h @ W_c^T (hipBLASLt), into ONE reused bf16 [T,vc] buffer (about the
+// size of the 256 MiB Infinity Cache). The kernels below consume it right after the GEMM:
 //   forward : merge each chunk's rows into a per-token online-softmax state (m, S, W, x_label)
 //             in log2 units, the same state as logprob.hip. The last chunk's launch finalizes
 //             logp = x_label - lse, H = ln S - ln2 * W/S and lse. One wave per token row.
@@ -46,7 +45,7 @@ __global__ __launch_bounds__(kThreads) void lmhead_fwd_kernel(
     state_init(st);
     int done = 0;
     if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
-        // default-policy loads: the chunk was just written by the GEMM and sits in L2/MALL
+        // default-policy loads: the chunk was just written by the GEMM (partly L2/MALL-resident)
         const int nvec = vc / VEC;
         const uint4* rv = reinterpret_cast<const uint4*>(row);
         int i = lane;

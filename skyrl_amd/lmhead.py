@@ -6,8 +6,8 @@ writes bf16 logits [n,S,V]. ``logits.div_(temperature)`` runs in bf16. Then
 (:59-111) read the logits. Their backward writes bf16 dlogits, which the lm_head backward GEMMs
 read.
 
-Here V is cut into chunks of ``chunk`` columns, sized so that one bf16 [T, chunk] buffer stays
-resident in the 256 MiB Infinity Cache:
+Here V is cut into chunks of ``chunk`` columns (one reused bf16 [T, chunk] buffer, about the
+size of the 256 MiB Infinity Cache):
 
   forward   per chunk: z = h @ W_c^T (hipBLASLt, into the reused buffer), then
             skyrl_lmhead_chunk_fwd merges z into the per-token softmax state; the last chunk's
@@ -31,11 +31,15 @@ import torch
 from . import _ffi
 from .ops import _ptr, _require_gpu, _stream
 
-MALL_BUDGET_BYTES = 96 << 20  # one chunk buffer (fwd) or two (bwd) well inside the 256 MiB MALL
+# Chunk buffer budget. Measured at T=8192, H=1536, V=151936 (docs: DESIGN.md §9): 16384-column
+# chunks (256 MiB) beat 4096/8192 (fewer, larger GEMMs). A two-stream pipeline that overlaps the
+# chunk kernels with the next GEMM measured 18-30 % SLOWER (the memory-bound kernel steals CU slots
+# from a GEMM that already saturates the chip), so the chunks run back to back on one stream.
+MALL_BUDGET_BYTES = 256 << 20
 
 
 def default_chunk(T: int, V: int) -> int:
-    """Largest multiple of 256 columns whose bf16 [T, chunk] buffer fits the MALL budget."""
+    """Largest multiple of 256 columns whose bf16 [T, chunk] buffer fits the budget."""
     c = MALL_BUDGET_BYTES // max(1, 2 * T)
     c = max(2048, min(65536, c // 256 * 256))
     return min(c, V)

@@ -112,5 +112,5 @@ def test_lmhead_empty_and_errors(dev):
 
 
 def test_default_chunk_fits_mall():
-    assert default_chunk(8192, 151936) * 8192 * 2 <= 96 << 20
+    assert default_chunk(8192, 151936) * 8192 * 2 <= 256 << 20
     assert default_chunk(16, 1000) == 1000
