@@ -9,8 +9,10 @@ path over one synthetic batch:
   pack      skyrl_pack_experience: ragged prompts/responses -> padded training tensors
   ref/old   skyrl_logprob_fwd over all 512x1024 response positions (2 passes)
   advantage skyrl_grpo_advantage over [512, 1024]
-  update    per micro-batch (16 seqs): logprob+entropy fwd -> fused PPO+KL loss fwd -> loss bwd
-            -> logprob bwd writing dlogits (bf16); metrics read once per step
+  update    per micro-batch (16 seqs): skyrl_policy_train_fwd, ONE pass per token computing
+            logprob + entropy + PPO/KL loss and writing dlogits (bf16); metrics read once per step
+  optimizer grad norm + clip + AdamW over Qwen2.5-1.5B's 1.54 B fp32 params, writing the bf16
+            rollout copy (reduce-scatter / all-gather over RCCL when N > 1)
 
 The transformer forward/backward is outside the hot path (north_star: PyTorch-ROCm owns it),
 so its logits are synthetic and resident in HBM before timing (data="synthetic"). With N > 1
@@ -18,9 +20,11 @@ ranks every rank runs its own batch (weak scaling, no data-path collective: the 
 loss / logprob rows shard by whole prompt groups); one packed fp32 metric all-reduce per step
 over RCCL keeps the reference's metric semantics.
 
-The dominant kernel (skyrl_logprob_fwd) is timed live with HIP events on its launch stream,
-and the CPU oracle (oracle/cpu_ref.py + oracle/sampler_ref.c, "port") is timed on a bounded
-sample on rank 0 at N=1.
+Every hot kernel is timed live with HIP events on its launch stream (the dominant one feeds
+`roofline`). After the timed steps, the advantage + loss kernels (56 B/token)
+are replayed from a HIP graph at the batch size and at 16x it (`advantage_loss`). The CPU
+oracle (oracle/cpu_ref.py + oracle/sampler_ref.c, "port") is timed on a bounded sample on
+rank 0 at N=1.
 """
 
 from __future__ import annotations
@@ -43,7 +47,7 @@ QWEN_1_5B_PARAMS = 1_543_714_304  # Qwen2.5-1.5B, tied embeddings
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # measured on the box by scripts/probe/stream_probe.py (reported beside frac, never instead of it)
 CEILING_READ_GBS = 6100.0    # read-only stream
-CEILING_RW_GBS = 4865.0      # 50/50 read+write copy (16-B nt loads/stores, 5 GB)
+CEILING_RW_GBS = 5560.0      # 50/50 read+write copy, best structure (scripts/probe/rw_probe.py, 10 GB)
 
 
 def log(msg):
@@ -338,8 +342,12 @@ def run(args):
             "frac_of_measured_ceiling": round(dom["achieved_GBps"] / dom["ceiling_GBps"], 4),
         },
         "kernels": kernels,
+        "advantage_loss": None,
         "cpu_baseline": None,
     }
+    if not args.no_adv_loss_leg:
+        result["advantage_loss"] = {"batch": advantage_loss_leg(dev, N, R),
+                                    "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
@@ -360,6 +368,79 @@ def pmc_traffic(kernel_name, algorithmic_bytes):
         if key in kernel_name:
             return rec.get("hbm_bytes_per_launch")
     return None
+
+
+def advantage_loss_leg(dev, N, R, reps=20):
+    """GRPO advantage + fused PPO/KL loss forward (+ fold) + loss backward on [N, R], the
+    SURVEY §8(d) "advantage+loss" kernels (12 + 20 + 24 = 56 algorithmic B/token). Launched
+    through the C ABI inside a captured HIP graph and replayed, so host launch cost is
+    excluded and inter-kernel gaps are included. Returns per-kernel and total microseconds."""
+    from skyrl_amd import _ffi, ppo_utils
+    from skyrl_amd.config import AlgorithmConfig
+    from skyrl_amd.ops import _ptr
+
+    g = torch.Generator(device=dev).manual_seed(7)
+    lens = torch.randint(1, R + 1, (N,), device=dev, generator=g)
+    rew = torch.zeros(N, R, device=dev)
+    rew[torch.arange(N, device=dev), lens - 1] = (torch.rand(N, device=dev, generator=g) < 0.3).float()
+    rmask = (torch.arange(R, device=dev)[None] < lens[:, None]).to(torch.int64)
+    lmask = rmask.float()
+    lp = -2 + 0.1 * torch.randn(N, R, device=dev, generator=g)
+    old = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
+    ref = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
+    adv = torch.empty(N, R, device=dev)
+    gnum = torch.empty(N, R, device=dev)
+    glp = torch.empty(N, R, device=dev)
+    rs = torch.empty(N, device=dev)
+    loss = torch.empty(1, device=dev)
+    met = torch.empty(8, device=dev)
+    gout = torch.ones(1, device=dev)
+    ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", N, R), dtype=torch.uint8, device=dev)
+    params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
+    ng = N // GROUP
+
+    def grpo(s):
+        _ffi.call("skyrl_grpo_advantage", _ptr(rew), _ptr(rmask), _ffi.I64, None, None, ng, N, R, 1e-6, 1,
+                  _ptr(adv), None, s)
+
+    def fwd(s):
+        _ffi.call("skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(lmask), _ptr(ref), None, N, R,
+                  ctypes.byref(params), _ptr(loss), _ptr(met), _ptr(gnum), _ptr(rs), _ptr(ws), s)
+
+    def bwd(s):
+        _ffi.call("skyrl_ppo_loss_bwd", _ptr(gout), _ptr(gnum), _ptr(rs), _ptr(lmask), _ptr(met), N, R,
+                  ctypes.byref(params), _ptr(glp), None, s)
+
+    out = {}
+    side = torch.cuda.Stream(dev)
+    for name, fns in (("grpo_us", (grpo,)), ("loss_fwd_us", (fwd,)), ("loss_bwd_us", (bwd,)),
+                      ("total_us", (grpo, fwd, bwd))):
+        with torch.cuda.stream(side):
+            h = torch.cuda.current_stream(dev).cuda_stream
+            for f in fns:
+                f(h)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=side):
+            h = torch.cuda.current_stream(dev).cuda_stream
+            for _ in range(reps):
+                for f in fns:
+                    f(h)
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            graph.replay()
+        b.record()
+        b.synchronize()
+        out[name] = round(a.elapsed_time(b) * 1e3 / (5 * reps), 2)
+        del graph
+    nbytes = 56 * N * R
+    gbs = nbytes / (out["total_us"] * 1e-6) / 1e9
+    out.update({"rows": N, "R": R, "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
+                "frac": round(gbs / HBM_PEAK_GBS, 4)})
+    return out
 
 
 def cpu_baseline(args):
@@ -442,6 +523,7 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=16)
     ap.add_argument("--logits-rows", type=int, default=0, help="0 = the whole batch if HBM allows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-adv-loss-leg", action="store_true", help="skip the graph-replayed advantage+loss leg")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--params", type=int, default=QWEN_1_5B_PARAMS, help="policy parameter count (0: no optimizer leg)")

@@ -45,7 +45,8 @@ int skyrl_abi_version(void);
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
  * {0, 1} (non-temporal streaming loads of the logits), "train_resident" {0, 1} (fused
  * training pass keeps the vocab row in registers vs re-reading it), "train_ntstore"
- * {0, 1} (non-temporal dlogits stores). Not thread-safe.                              */
+ * {0, 1} (non-temporal dlogits stores), "train_resident_nt" {768, 1024} (threads per
+ * register-resident row). Not thread-safe.                                             */
 int skyrl_tune(const char* key, int value);
 
 /* ---- a4: GRPO outcome advantage ----------------------------------------
@@ -55,6 +56,9 @@ int skyrl_tune(const char* key, int value);
  * mean 0, std 1); adv = (score-mean)/(std+eps) (or score-mean); out = adv*mask.
  * Groups are given in CSR form: rows of group g are group_rows[group_off[g] ..
  * group_off[g+1]) (the host maps the reference's `index` uids to groups).
+ * group_off == group_rows == NULL means contiguous groups of G = N/num_groups
+ * rows each (the trainer's layout, generators/utils.py:373-393); that form needs
+ * G <= 16, R % 4 == 0 and 16-B aligned buffers, and skips the index loads.
  * rewards/out: f32 [N,R] row-major contiguous; mask: [N,R] of mask_dtype.   */
 int skyrl_grpo_advantage(const float* rewards, const void* response_mask, int mask_dtype,
                          const int32_t* group_off, const int32_t* group_rows, int32_t num_groups,

@@ -1,0 +1,69 @@
+"""Where does the ppo_loss forward's launch time go? Builds the phase-timestamp variant
+(phase_probe.hip) and prints per-phase spans (us) for the first/last blocks and the launch."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import torch
+
+here = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(here))
+sys.path.insert(0, ROOT)
+so = "/tmp/libphase.so"
+subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC",
+                       "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "skyrl_amd", "csrc"),
+                       os.path.join(here, "phase_probe.hip"), "-o", so])
+lib = ctypes.CDLL(so, mode=ctypes.RTLD_LOCAL)
+from skyrl_amd import _ffi, ppo_utils  # noqa: E402
+from skyrl_amd.config import AlgorithmConfig  # noqa: E402
+
+dev = torch.device("cuda:0")
+N, R = 512, 1024
+g = torch.Generator(device=dev).manual_seed(0)
+lp = -2 + 0.1 * torch.randn(N, R, device=dev, generator=g)
+old = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
+ref = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
+adv = torch.randn(N, R, device=dev, generator=g)
+mask = torch.ones(N, R, device=dev)
+params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
+loss = torch.empty(1, device=dev)
+metrics = torch.empty(8, device=dev)
+gnum = torch.empty(N, R, device=dev)
+rs = torch.empty(N, device=dev)
+ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", N, R), dtype=torch.uint8, device=dev)
+st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+P = ctypes.c_void_p
+fn = lib.skyrl_ppo_loss_fwd
+fn.restype = ctypes.c_int
+fn.argtypes = [P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, P, P]
+
+
+def launch():
+    rc = fn(P(lp.data_ptr()), P(old.data_ptr()), P(adv.data_ptr()), P(mask.data_ptr()), P(ref.data_ptr()), None, N, R,
+            ctypes.byref(params), P(loss.data_ptr()), P(metrics.data_ptr()), P(gnum.data_ptr()), P(rs.data_ptr()),
+            P(ws.data_ptr()), st)
+    assert rc == 0
+
+
+for _ in range(20):
+    launch()
+torch.cuda.synchronize()
+buf = np.zeros(8192 * 8, dtype=np.uint64)
+for rep in range(3):
+    lib.probe_clear()
+    torch.cuda.synchronize()
+    launch()
+    torch.cuda.synchronize()
+    assert lib.probe_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
+    nb = int(os.environ.get("BLOCKS", N))
+    t = buf.reshape(-1, 8)[:nb].astype(np.int64)
+    d = lambda a, b: (t[:, b] - t[:, a]) / 100.0  # noqa: E731  per-block spans, us (100 MHz)
+    last = int(np.argmax(t[:, 3] > 0))
+    tp = d(0, 1)
+    print(f"rep {rep}: per block: token pass median {np.median(tp):.2f} max {tp.max():.2f}; "
+          f"wave reduce+drain+barrier median {np.median(d(1, 2)):.2f} max {d(1, 2).max():.2f}; "
+          f"last block {last}: entry->arrive {(t[last, 3] - t[last, 0]) / 100:.2f}, "
+          f"arrive {(t[last, 3] - t[last, 2]) / 100:.2f}, fold {(t[last, 4] - t[last, 3]) / 100:.2f}, "
+          f"end {(t[last, 5] - t[last, 4]) / 100:.2f}")

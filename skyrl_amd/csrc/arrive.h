@@ -50,13 +50,16 @@ __device__ __forceinline__ void block_sum_d(double (&v)[NV], double* lds) {
         for (int k = 0; k < NV; ++k) lds[w * NV + k] = v[k];
     }
     __syncthreads();
+    double s[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        double s = 0.0;
+    for (int k = 0; k < NV; ++k) s[k] = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < NW; ++j) {  // same per-quantity order; not unrolled (16 waves x 6 doubles spilled)
 #pragma unroll
-        for (int j = 0; j < NW; ++j) s += lds[j * NV + k];
-        v[k] = s;
+        for (int k = 0; k < NV; ++k) s[k] += lds[j * NV + k];
     }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = s[k];
     __syncthreads();
 }
 

@@ -211,6 +211,7 @@ int launch_bwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V
 using namespace skyrl;
 namespace skyrl {
 extern int g_train_resident;
+extern int g_train_resident_nt;
 extern int g_train_ntstore;
 }
 
@@ -227,6 +228,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
     }
     if (k == "train_resident") {
         g_train_resident = value != 0;
+        return SKYRL_OK;
+    }
+    if (k == "train_resident_nt") {
+        SKYRL_REQUIRE(value == 768 || value == 1024, "skyrl_tune: train_resident_nt must be 768 or 1024");
+        g_train_resident_nt = value;
         return SKYRL_OK;
     }
     if (k == "logprob_nt") {

@@ -297,8 +297,8 @@ __global__ __launch_bounds__(kThreads) void policy_train_kernel(
 // ---- 2b. register-resident variant: the row is loaded ONCE into registers (NV 16-B
 // vectors per thread, 1024 threads: NV = 19 covers V <= 155,648, Qwen2.5's 151,936), so
 // sweep 2 needs no memory reads at all: HBM traffic per token is exactly V*2 read +
-// V*2 written. One 1024-thread block per CU (<= 128 VGPRs); the per-token scalars
-// (label logit, old/adv/mask/ref, row scale) are prefetched by thread 0 up front.
+// V*2 written. One block per CU; the per-token scalars (old/adv/mask/ref, row scale, label)
+// are scalar loads issued up front, the label logit one broadcast load by thread 0.
 template <int NT, int NV, bool HAS_T>
 __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int V, const int64_t* __restrict__ labels,
@@ -317,18 +317,18 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     const uint4* rv = reinterpret_cast<const uint4*>(row);
     auto tval = [&](float x) { return HAS_T ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
 
-    int64_t lab = 0;
-    float xl = 0.f, o_old = 0.f, o_adv = 0.f, o_m = 1.f, o_ref = 0.f, o_rs = 0.f, o_ge = 0.f;
-    if (threadIdx.x == 0) {  // prefetch the token's scalars behind the row loads
-        lab = labels[b * lsb + t * lst];
-        xl = (lab >= 0 && lab < V) ? bf16_to_f32(row[lab]) : __builtin_nanf("");
-        o_old = old[r];
-        o_adv = adv[r];
-        o_m = mask ? mask[r] : 1.f;
-        o_ref = p.use_kl_loss ? ref[r] : 0.f;
-        o_rs = row_scale[b];
-        o_ge = scal[1];
-    }
+    // The token's scalars sit at block-uniform addresses: every thread loads them, so they
+    // become scalar loads into SGPRs, issued ahead of the row and costing no VGPRs (the row
+    // itself holds 4*NV VGPRs across the whole kernel).
+    const int64_t lab = labels[b * lsb + t * lst];
+    const float o_old = old[r];
+    const float o_adv = adv[r];
+    const float o_m = mask ? mask[r] : 1.f;
+    const float o_ref = p.use_kl_loss ? ref[r] : 0.f;
+    const float o_rs = row_scale[b];
+    const float o_ge = scal[1];
+    float xl = 0.f;
+    if (threadIdx.x == 0) xl = (lab >= 0 && lab < V) ? bf16_to_f32(row[lab]) : __builtin_nanf("");
     // Host guarantees (NV-1)*NT < nvec <= NV*NT: only the last vector can be out of range.
     uint4 v[NV];
 #pragma unroll
@@ -359,9 +359,17 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     }
     if (lane == 0) s_st[threadIdx.x / kWave] = st;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        St a = s_st[0];
-        for (int j = 1; j < NT / 64; ++j) st_merge(a, s_st[j]);
+    // wave 0 merges the NT/64 wave states as a shuffle tree (a serial lane-0 fold of 12 states
+    // sat on every row's critical path), then lane 0 evaluates the token's loss terms
+    static_assert(NT / 64 <= 16, "wave-state tree covers 16 waves");
+    if (threadIdx.x < kWave) {
+        St a = threadIdx.x < NT / 64 ? s_st[threadIdx.x] : St{-3.402823466e38f, 0.f, 0.f};
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) {
+            St o{__shfl_xor(a.m, off, kWave), __shfl_xor(a.s, off, kWave), __shfl_xor(a.w, off, kWave)};
+            st_merge(a, o);
+        }
+        if (threadIdx.x == 0) {
         const float logs = fast_log2(a.s) * kLn2;
         const float lse = a.m + logs;
         const float H = logs - kLn2 * (a.w / a.s);
@@ -377,11 +385,10 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
         s_g[1] = (dl * o_m) * o_rs;
         s_g[2] = o_ge * o_m;
         s_g[3] = H;
-        *reinterpret_cast<int64_t*>(&s_st[0]) = lab;  // broadcast the label through LDS
+        }
     }
     __syncthreads();
     const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
-    lab = *reinterpret_cast<const int64_t*>(&s_st[0]);
     const int lab32 = (lab >= 0 && lab < V) ? (int)lab : -1;
 #pragma unroll
     for (int k = 0; k < NV; ++k)  // new values: no reuse of sweep-1 unpacks across the barrier
@@ -494,6 +501,7 @@ __global__ void scale_bf16_kernel(const float* __restrict__ g, uint16_t* __restr
 }  // namespace
 
 int g_train_resident = 1;  // skyrl_tune("train_resident", 0/1)
+int g_train_resident_nt = 1024;  // skyrl_tune("train_resident_nt", 768/1024)
 int g_train_ntstore = 1;   // skyrl_tune("train_ntstore", 0/1): non-temporal dlogits stores
 
 }  // namespace skyrl
@@ -531,12 +539,18 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
     if (rc) return rc;
     const bool has_t = temperature != 1.0f;
     const int nvec = V / 8;
-    constexpr int kRT = 768, kRV = 25;  // 768 threads x 25 x 16 B: 147,456 < V <= 153,600 (Qwen2.5)
+    // Register-resident shapes for Qwen2.5's V = 151,936 (147,456 < V <= 153,600 / 155,648):
+    // 768 threads x 25 vectors (3 waves/SIMD, <= 168 VGPRs) or 1024 x 19 (4 waves/SIMD, <= 128).
+    const bool use1024 = g_train_resident_nt == 1024;
+    const int kRT = use1024 ? 1024 : 768, kRV = use1024 ? 19 : 25;
     const bool resident_ok = g_train_resident && (V % 8) == 0 && nvec <= kRV * kRT && nvec > (kRV - 1) * kRT &&
                              (reinterpret_cast<uintptr_t>(logits) % 16) == 0 && (stride_b % 8) == 0 &&
                              (stride_t % 8) == 0 && (reinterpret_cast<uintptr_t>(grad_logits) % 16) == 0;
     if (resident_ok) {
-        auto kern = has_t ? policy_train_resident_kernel<kRT, kRV, true> : policy_train_resident_kernel<kRT, kRV, false>;
+        auto kern = use1024 ? (has_t ? policy_train_resident_kernel<1024, 19, true>
+                                     : policy_train_resident_kernel<1024, 19, false>)
+                            : (has_t ? policy_train_resident_kernel<768, 25, true>
+                                     : policy_train_resident_kernel<768, 25, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(kRT), 0, s,
                            reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, V, labels, lstride_b,
                            lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs, row_scale,

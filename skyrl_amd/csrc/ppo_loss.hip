@@ -10,13 +10,27 @@
 //   apply_reward_kl_penalty      trainer.py:981-1035
 //   ppo_critic_loss              utils/ppo_utils.py:175-193
 //
-// Layout: all per-token tensors f32 [n,R] row-major. Grid = (row, 1024-column
-// chunk); a block reads its chunk once (20 B/token: logp, old, adv, mask, ref),
-// writes the per-token gradient numerator (4 B/token) and a 5-float partial;
-// the last-arriving block (arrive.h) folds the partials into the scalar loss,
+// Layout: all per-token tensors f32 [n,R] row-major. Forward: grid (row, 1024-column chunk),
+// one token per thread; it reads 20 B/token (logp, old, adv, mask, ref), writes the per-token
+// gradient numerator (4 B/token) and a 5-float record per block; a one-block fold launch
+// folds the records into the scalar loss,
 // the metric vector and the per-row gradient scale. The backward is then a
 // 12 B/token elementwise pass (numerator, scale, upstream grad).
 #include "arrive.h"
+
+// Phase timestamps for scripts/probe/phase_probe (compiled only there, never in the product).
+#ifdef SKYRL_PHASE_PROBE
+__device__ uint64_t g_phase[8192 * 8];
+#define PHASE(k)                                                                                           \
+    do {                                                                                                   \
+        if (threadIdx.x == 0)                                                                              \
+            g_phase[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PHASE(k) \
+    do {         \
+    } while (0)
+#endif
 
 namespace skyrl {
 namespace {
@@ -25,6 +39,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr int kChunk = kThreads * 4;  // columns per block
 constexpr int kNP = 5;                // partials: sum l*m, m, clip*m, kl*m*m, ent*m
+constexpr int kRec = 8;               // partial record stride (floats): two 16-B loads per record
+constexpr int kPre = 1;               // rows per thread whose records the epilogue loads at once (1024 threads)
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
@@ -86,110 +102,124 @@ __device__ __forceinline__ TokenOut ppo_token(float lp, float old, float A, floa
     return o;
 }
 
+// Grid (row, 1024-column chunk), 256 threads x 4 tokens: every thread issues its 16-B loads
+// of all inputs at once, and the 4 independent tokens give the PPO/KL arithmetic (two
+// accurate expf, clamps, selects) ILP within the wave. Measured at [512, 1024]: this 4-wave
+// shape beats one token per thread in 1024-thread blocks (16-wave fold tail per block) and a
+// wave-per-row shape (16 tokens per lane, 1 wave per SIMD).
+constexpr int kFT = kThreads * 4;  // columns per block
+constexpr int kFW = kThreads / kWave;
+
 __global__ __launch_bounds__(kThreads) void ppo_loss_fwd_kernel(
     const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent, int n,
-    int R, skyrl_ppo_params p, bool vec4, float* __restrict__ loss_out, float* __restrict__ metrics,
-    float* __restrict__ gnum, float* __restrict__ row_scale, float* __restrict__ partials,
-    unsigned* __restrict__ counter) {
-    __shared__ float s_red[kWaves * kNP];
-    __shared__ double s_redd[kWaves * 6];
-    __shared__ int s_last;
-
+    int R, skyrl_ppo_params p, bool vec4, float* __restrict__ gnum, float* __restrict__ partials) {
+    __shared__ float s_red[kFW * kNP];
+    PHASE(0);
     const int row = blockIdx.x;
     const int chunk = blockIdx.y;
     const int nchunks = gridDim.y;
     const float lo = (float)(1.0 - (double)p.eps_clip_low);
     const float hi = (float)(1.0 + (double)p.eps_clip_high);
     const int64_t rbase = (int64_t)row * R;
-
     float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    auto one = [&](int64_t i, float& g) {
-        const float m = mask ? mask[i] : 1.f;
-        TokenOut t = ppo_token(lp[i], old[i], adv[i], lo, hi, p.clip_ratio_c, p.dual_clip);
-        acc[0] += t.loss * m;
-        acc[1] += m;
-        acc[2] += t.clip * m;
-        if (p.use_kl_loss) acc[3] += (approx_kl(lp[i], ref[i], p.kl_type) * m) * m;
-        if (ent) acc[4] += ent[i] * m;
-        g = t.dldlp * m;
+    auto tok = [&](float L, float O, float A, float M, float RF, float E) -> float {
+        const TokenOut t = ppo_token(L, O, A, lo, hi, p.clip_ratio_c, p.dual_clip);
+        acc[0] += t.loss * M;
+        acc[1] += M;
+        acc[2] += t.clip * M;
+        if (p.use_kl_loss) acc[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
+        acc[4] += E * M;
+        return t.dldlp * M;
     };
-    const int c0 = chunk * kChunk + threadIdx.x * 4;
-    if (vec4 && c0 + 3 < R) {
-        const int64_t i = rbase + c0;
-        float4 l4 = *reinterpret_cast<const float4*>(lp + i);
-        float4 o4 = *reinterpret_cast<const float4*>(old + i);
-        float4 a4 = *reinterpret_cast<const float4*>(adv + i);
-        float4 m4 = mask ? *reinterpret_cast<const float4*>(mask + i) : make_float4(1.f, 1.f, 1.f, 1.f);
-        float4 r4 = p.use_kl_loss ? *reinterpret_cast<const float4*>(ref + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 e4 = ent ? *reinterpret_cast<const float4*>(ent + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float L[4] = {l4.x, l4.y, l4.z, l4.w}, O[4] = {o4.x, o4.y, o4.z, o4.w};
-        const float A[4] = {a4.x, a4.y, a4.z, a4.w}, M[4] = {m4.x, m4.y, m4.z, m4.w};
-        const float RF[4] = {r4.x, r4.y, r4.z, r4.w}, E[4] = {e4.x, e4.y, e4.z, e4.w};
-        float g[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            TokenOut t = ppo_token(L[k], O[k], A[k], lo, hi, p.clip_ratio_c, p.dual_clip);
-            acc[0] += t.loss * M[k];
-            acc[1] += M[k];
-            acc[2] += t.clip * M[k];
-            if (p.use_kl_loss) acc[3] += (approx_kl(L[k], RF[k], p.kl_type) * M[k]) * M[k];
-            acc[4] += E[k] * M[k];
-            g[k] = t.dldlp * M[k];
+    const int c0 = chunk * kFT + threadIdx.x * 4;
+    if (vec4) {
+        if (c0 + 3 < R) {  // R % 4 == 0 on this path
+            const int64_t e = rbase + c0;
+            const float4 l4 = *reinterpret_cast<const float4*>(lp + e);
+            const float4 o4 = *reinterpret_cast<const float4*>(old + e);
+            const float4 a4 = *reinterpret_cast<const float4*>(adv + e);
+            const float4 m4 = mask ? *reinterpret_cast<const float4*>(mask + e) : make_float4(1.f, 1.f, 1.f, 1.f);
+            const float4 r4 = p.use_kl_loss ? *reinterpret_cast<const float4*>(ref + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 e4 = ent ? *reinterpret_cast<const float4*>(ent + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 g;
+            g.x = tok(l4.x, o4.x, a4.x, m4.x, r4.x, e4.x);
+            g.y = tok(l4.y, o4.y, a4.y, m4.y, r4.y, e4.y);
+            g.z = tok(l4.z, o4.z, a4.z, m4.z, r4.z, e4.z);
+            g.w = tok(l4.w, o4.w, a4.w, m4.w, r4.w, e4.w);
+            *reinterpret_cast<float4*>(gnum + e) = g;
         }
-        *reinterpret_cast<float4*>(gnum + i) = make_float4(g[0], g[1], g[2], g[3]);
-    } else if (!vec4) {
-        for (int c = chunk * kChunk + threadIdx.x; c < R && c < (chunk + 1) * kChunk; c += kThreads) {
-            float g;
-            one(rbase + c, g);
-            gnum[rbase + c] = g;
-        }
-    } else {  // vec4 layout but ragged tail (cannot happen when R % 4 == 0)
-        for (int c = c0; c < R && c < c0 + 4; ++c) {
-            float g;
-            one(rbase + c, g);
-            gnum[rbase + c] = g;
+    } else {
+        for (int c = chunk * kFT + threadIdx.x; c < R && c < (chunk + 1) * kFT; c += kThreads) {
+            const int64_t e = rbase + c;
+            gnum[e] = tok(lp[e], old[e], adv[e], mask ? mask[e] : 1.f, p.use_kl_loss ? ref[e] : 0.f,
+                          ent ? ent[e] : 0.f);
         }
     }
+    PHASE(1);
+    block_sum<kFW, kNP>(acc, s_red);
+    if (threadIdx.x < kNP) partials[((int64_t)row * nchunks + chunk) * kRec + threadIdx.x] = acc[threadIdx.x];
+    PHASE(2);
+}
 
-    block_sum<kWaves, kNP>(acc, s_red);
-    if (threadIdx.x == 0) {
-        float* dst = partials + ((int64_t)row * nchunks + chunk) * kNP;
-#pragma unroll
-        for (int k = 0; k < kNP; ++k) st_wt(dst + k, acc[k]);
-    }
-    if (!arrive_last(counter, (unsigned)(n * nchunks), &s_last)) return;
-
+// The fold runs as its own one-block launch: the kernel boundary publishes every record.
+// (An in-kernel last-arriver fold measured 13-16 us at n=512: each block drained its
+// stores before ticking, and the folding block's tail sat behind all of that.)
+constexpr int kFoldT = 256;
+__global__ __launch_bounds__(kFoldT) void ppo_loss_fold_kernel(int n, int nchunks, skyrl_ppo_params p,
+                                                               const float* __restrict__ partials,
+                                                               float* __restrict__ loss_out, float* __restrict__ metrics,
+                                                               float* __restrict__ row_scale) {
+    __shared__ double s_redd[(kFoldT / kWave) * 6];
+    PHASE(3);
     // ---- epilogue: one block folds the n*nchunks partials ---------------------
     // tot: 0 sum l*m, 1 sum m, 2 sum clip*m, 3 sum_rows row-reduced loss (seq modes),
     //      4 sum_rows kl_row, 5 sum ent*m
     double tot[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = threadIdx.x; r < n; r += kThreads) {
-        double rs[kNP] = {0, 0, 0, 0, 0};
-        for (int c = 0; c < nchunks; ++c) {
-            const float* src = partials + ((int64_t)r * nchunks + c) * kNP;
+    // Each thread loads the chunk-0 records of kPre rows before the first wait (one
+    // dependent round trip for n <= kPre * kThreads rows), further chunks after.
+    for (int r0 = threadIdx.x; r0 < n; r0 += kFoldT * kPre) {
+        float4 rec[kPre][2];
 #pragma unroll
-            for (int k = 0; k < kNP; ++k) rs[k] += (double)src[k];
+        for (int u = 0; u < kPre; ++u) {
+            const int r = r0 + u * kFoldT;
+            if (r < n) {
+                const float4* src = reinterpret_cast<const float4*>(partials + (int64_t)r * nchunks * kRec);
+                rec[u][0] = src[0];
+                rec[u][1] = src[1];
+            }
         }
-        const double mrow = rs[1] > 1.0 ? rs[1] : 1.0;  // mask.sum(-1).clamp(min=1)
-        tot[0] += rs[0];
-        tot[1] += rs[1];
-        tot[2] += rs[2];
-        tot[4] += rs[3] / mrow;
-        tot[5] += rs[4];
-        if (p.loss_reduction == 1) {
-            tot[3] += rs[0] / mrow;
-            row_scale[r] = (float)(1.0 / ((double)n * mrow));
-        } else if (p.loss_reduction == 2) {
-            tot[3] += rs[0] / (double)p.max_seq_len;
-            row_scale[r] = (float)(1.0 / ((double)n * (double)p.max_seq_len));
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+            const int r = r0 + u * kFoldT;
+            if (r >= n) break;
+            double rs[kNP] = {rec[u][0].x, rec[u][0].y, rec[u][0].z, rec[u][0].w, rec[u][1].x};
+            for (int c = 1; c < nchunks; ++c) {
+                const float* src = partials + ((int64_t)r * nchunks + c) * kRec;
+#pragma unroll
+                for (int k = 0; k < kNP; ++k) rs[k] += (double)src[k];
+            }
+            const double mrow = rs[1] > 1.0 ? rs[1] : 1.0;  // mask.sum(-1).clamp(min=1)
+            tot[0] += rs[0];
+            tot[1] += rs[1];
+            tot[2] += rs[2];
+            tot[4] += rs[3] / mrow;
+            tot[5] += rs[4];
+            if (p.loss_reduction == 1) {
+                tot[3] += rs[0] / mrow;
+                row_scale[r] = (float)(1.0 / ((double)n * mrow));
+            } else if (p.loss_reduction == 2) {
+                tot[3] += rs[0] / (double)p.max_seq_len;
+                row_scale[r] = (float)(1.0 / ((double)n * (double)p.max_seq_len));
+            }
         }
     }
-    block_sum_d<kWaves, 6>(tot, s_redd);
+    PHASE(4);
+    block_sum_d<kFoldT / kWave, 6>(tot, s_redd);
     const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
     if (p.loss_reduction == 0) {
         const float sc = (float)(1.0 / msum);
-        for (int r = threadIdx.x; r < n; r += kThreads) row_scale[r] = sc;
+        for (int r = threadIdx.x; r < n; r += kFoldT) row_scale[r] = sc;
     }
     if (threadIdx.x == 0) {
         float pg;
@@ -210,7 +240,7 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_fwd_kernel(
         metrics[6] = 0.f;
         metrics[7] = 0.f;
     }
-    rearm(counter);
+    PHASE(5);
 }
 
 __global__ __launch_bounds__(kThreads) void ppo_loss_bwd_kernel(
@@ -369,8 +399,8 @@ inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<
 using namespace skyrl;
 
 extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
-    const size_t nchunks = (size_t)((R + kChunk - 1) / kChunk);
-    const size_t parts = (size_t)n * (nchunks ? nchunks : 1) * kNP * sizeof(float);
+    const size_t nchunks = (size_t)((R + kFT - 1) / kFT);
+    const size_t parts = (size_t)(n > 0 ? n : 1) * (nchunks ? nchunks : 1) * kRec * sizeof(float);
     return 256 + ((parts + 255) / 256) * 256;  // [counter | pad][partials]
 }
 
@@ -389,15 +419,17 @@ extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_p
     SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
                   "ppo_loss_fwd: seq_mean_token_sum_norm needs max_seq_len");
     SKYRL_REQUIRE(params->kl_type >= 0 && params->kl_type <= 3, "ppo_loss_fwd: bad kl_type");
+    float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
     const bool vec4 = (R % 4) == 0 && aligned16(log_probs) && aligned16(old_log_probs) && aligned16(advantages) &&
                       aligned16(loss_mask) && aligned16(ref_log_probs) && aligned16(entropy) && aligned16(grad_num);
-    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
-    float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
-    dim3 grid(n, (R + kChunk - 1) / kChunk);
+    dim3 grid(n, (R + kFT - 1) / kFT);
     hipLaunchKernelGGL(ppo_loss_fwd_kernel, grid, dim3(kThreads), 0, as_stream(stream), log_probs, old_log_probs,
-                       advantages, loss_mask, ref_log_probs, entropy, n, R, *params, vec4, loss_out, metrics_out,
-                       grad_num, row_scale, partials, counter);
-    return check_launch("ppo_loss_fwd_kernel");
+                       advantages, loss_mask, ref_log_probs, entropy, n, R, *params, vec4, grad_num, partials);
+    int rc = check_launch("ppo_loss_fwd_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(ppo_loss_fold_kernel, dim3(1), dim3(kFoldT), 0, as_stream(stream), n, (int)grid.y, *params,
+                       partials, loss_out, metrics_out, row_scale);
+    return check_launch("ppo_loss_fold_kernel");
 }
 
 extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, const float* grad_num, const float* row_scale,

@@ -104,11 +104,27 @@ def groups_from_index(index: Sequence) -> Tuple[torch.Tensor, torch.Tensor, int]
     return torch.tensor(off, dtype=torch.int32), torch.tensor(rows, dtype=torch.int32), len(members)
 
 
+def contiguous_group_size(group_off: torch.Tensor, group_rows: torch.Tensor, num_groups: int) -> int:
+    """G if the CSR groups are rows [g*G, (g+1)*G) for every g (the trainer's layout), else 0."""
+    n = int(group_rows.numel())
+    if num_groups <= 0 or n % num_groups:
+        return 0
+    G = n // num_groups
+    if G > 16:
+        return 0
+    off = group_off.cpu()
+    rows = group_rows.cpu()
+    if torch.equal(rows, torch.arange(n, dtype=rows.dtype)) and torch.equal(
+            off, torch.arange(0, n + 1, G, dtype=off.dtype)):
+        return G
+    return 0
+
+
 def grpo_advantage(
     token_level_rewards: torch.Tensor,
     response_mask: torch.Tensor,
-    group_off: torch.Tensor,
-    group_rows: torch.Tensor,
+    group_off: Optional[torch.Tensor],
+    group_rows: Optional[torch.Tensor],
     num_groups: int,
     epsilon: float = 1e-6,
     norm_by_std: bool = True,
@@ -122,8 +138,16 @@ def grpo_advantage(
     if mask.dtype not in _MASK_DTYPES:
         raise TypeError(f"unsupported response_mask dtype {mask.dtype}")
     N, R = rew.shape
-    goff = group_off.to(device=dev, dtype=torch.int32)
-    grows = group_rows.to(device=dev, dtype=torch.int32)
+    if group_off is None and group_rows is None:  # contiguous groups of N / num_groups rows
+        goff = grows = None
+        aligned = all(t.data_ptr() % 16 == 0 for t in (rew, mask))
+        if not (aligned and R % 4 == 0 and num_groups > 0 and N % num_groups == 0 and N // num_groups <= 16):
+            G = N // max(num_groups, 1)  # the CSR kernel covers what the index-free one cannot
+            goff = torch.arange(0, N + 1, max(G, 1), dtype=torch.int32, device=dev)[: num_groups + 1]
+            grows = torch.arange(N, dtype=torch.int32, device=dev)
+    else:
+        goff = group_off.to(device=dev, dtype=torch.int32)
+        grows = group_rows.to(device=dev, dtype=torch.int32)
     out = torch.empty((N, R), dtype=torch.float32, device=dev)
     _ffi.call(
         "skyrl_grpo_advantage", _ptr(rew), _ptr(mask), _MASK_DTYPES[mask.dtype], _ptr(goff), _ptr(grows),

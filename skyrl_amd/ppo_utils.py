@@ -305,6 +305,9 @@ def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, ep
                                    grpo_norm_by_std: bool = True, **kwargs):
     """HIP GRPO advantage (ppo_utils.py:1132-1182). Returns (advantages, returns) aliased."""
     off, rows, ng = ops.groups_from_index(index)
+    R = token_level_rewards.shape[-1]
+    if R % 4 == 0 and ops.contiguous_group_size(off, rows, ng):
+        off = rows = None  # contiguous equal groups: the index-free kernel
     adv = ops.grpo_advantage(token_level_rewards, response_mask, off, rows, ng, epsilon, grpo_norm_by_std)
     return adv, adv
 

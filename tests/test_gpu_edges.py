@@ -109,3 +109,27 @@ def test_reward_kl_zero_coef_is_identity(dev):
                                    0.0)
     close(out, rew, atol=0, rtol=0)
     assert float(m[0]) > 0  # the KL metric is still reported
+
+
+@pytest.mark.parametrize("G,R,mdt", [(8, 1024, torch.int64), (1, 64, torch.float32), (16, 36, torch.bool),
+                                     (5, 256, torch.int32)])
+def test_grpo_contiguous_form_matches_csr_and_oracle(dev, G, R, mdt):
+    """The index-free kernel (contiguous equal groups) is bit-identical to the CSR kernel."""
+    g = torch.Generator().manual_seed(G * 100 + R)
+    N = 6 * G
+    rew = torch.zeros(N, R)
+    lens = torch.randint(1, R + 1, (N,), generator=g)
+    rew[torch.arange(N), lens - 1] = torch.randint(0, 3, (N,), generator=g).float()
+    mask = (torch.arange(R)[None] < lens[:, None]).to(mdt)
+    uids = [str(i // G) for i in range(N)]
+    off, rows, ng = ops.groups_from_index(uids)
+    assert ops.contiguous_group_size(off, rows, ng) == G
+    a_csr = ops.grpo_advantage(rew.to(dev), mask.to(dev), off, rows, ng)
+    a_fast = ops.grpo_advantage(rew.to(dev), mask.to(dev), None, None, ng)
+    assert torch.equal(a_csr, a_fast)
+    close(a_fast, cpu_ref.grpo_advantage(rew, mask.to(torch.int64), uids), atol=1e-6)
+    # an unaligned view takes the CSR kernel through the same call
+    big = torch.zeros(N * R + 1, device=dev)
+    view = big[1:].view(N, R)
+    view.copy_(rew.to(dev))
+    assert torch.equal(ops.grpo_advantage(view, mask.to(dev), None, None, ng), a_csr)
