@@ -56,6 +56,33 @@ __device__ __forceinline__ float load_mask(const void* m, int dtype, int64_t i) 
 }
 
 // ---- wave / block reductions ------------------------------------------------
+// Four consecutive mask values from a 16-B-aligned (f32/i64/i32) or 4-B-aligned (u8) address.
+__device__ __forceinline__ void load_mask4(const void* m, int dtype, int64_t idx, float (&o)[4]) {
+    switch (dtype) {
+        case SKYRL_F32: {
+            float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(m) + idx);
+            o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+            break;
+        }
+        case SKYRL_I64: {
+            const longlong2* p = reinterpret_cast<const longlong2*>(reinterpret_cast<const int64_t*>(m) + idx);
+            longlong2 a = p[0], b = p[1];
+            o[0] = (float)a.x; o[1] = (float)a.y; o[2] = (float)b.x; o[3] = (float)b.y;
+            break;
+        }
+        case SKYRL_I32: {
+            int4 v = *reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(m) + idx);
+            o[0] = (float)v.x; o[1] = (float)v.y; o[2] = (float)v.z; o[3] = (float)v.w;
+            break;
+        }
+        default: {
+            uchar4 v = *reinterpret_cast<const uchar4*>(reinterpret_cast<const uint8_t*>(m) + idx);
+            o[0] = (float)v.x; o[1] = (float)v.y; o[2] = (float)v.z; o[3] = (float)v.w;
+            break;
+        }
+    }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);

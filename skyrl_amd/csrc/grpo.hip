@@ -37,32 +37,6 @@ __device__ float row_sum_wave(const float* __restrict__ row, int R, bool vec4) {
     return wave_sum(acc);
 }
 
-__device__ __forceinline__ void load_mask4(const void* m, int dtype, int64_t idx, float (&o)[4]) {
-    switch (dtype) {
-        case SKYRL_F32: {
-            float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(m) + idx);
-            o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-            break;
-        }
-        case SKYRL_I64: {
-            const longlong2* p = reinterpret_cast<const longlong2*>(reinterpret_cast<const int64_t*>(m) + idx);
-            longlong2 a = p[0], b = p[1];
-            o[0] = (float)a.x; o[1] = (float)a.y; o[2] = (float)b.x; o[3] = (float)b.y;
-            break;
-        }
-        case SKYRL_I32: {
-            int4 v = *reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(m) + idx);
-            o[0] = (float)v.x; o[1] = (float)v.y; o[2] = (float)v.z; o[3] = (float)v.w;
-            break;
-        }
-        default: {
-            uchar4 v = *reinterpret_cast<const uchar4*>(reinterpret_cast<const uint8_t*>(m) + idx);
-            o[0] = (float)v.x; o[1] = (float)v.y; o[2] = (float)v.z; o[3] = (float)v.w;
-            break;
-        }
-    }
-}
-
 __global__ __launch_bounds__(kThreads) void grpo_adv_kernel(
     const float* __restrict__ rewards, const void* __restrict__ mask, int mask_dtype,
     const int32_t* __restrict__ group_off, const int32_t* __restrict__ group_rows, int R,

@@ -289,11 +289,9 @@ __global__ void approx_kl_kernel(const float* __restrict__ lp, const float* __re
 __global__ __launch_bounds__(kThreads) void reward_kl_kernel(
     const float* __restrict__ rewards, const float* __restrict__ lp, const float* __restrict__ base,
     const float* __restrict__ mask, int N, int R, int kl_type, float coef, float* __restrict__ out,
-    float* __restrict__ metrics, float* __restrict__ partials, unsigned* __restrict__ counter) {
+    float* __restrict__ partials) {
     __shared__ float s_red[kWaves * 2];
     __shared__ float s_max[kWaves];
-    __shared__ double s_redd[kWaves * 2];
-    __shared__ int s_last;
     const int row = blockIdx.x;
     const int64_t rbase = (int64_t)row * R;
     const float c = coef > 0.f ? coef : 0.f;  // max(0, kl_loss_coef)
@@ -313,32 +311,44 @@ __global__ __launch_bounds__(kThreads) void reward_kl_kernel(
     if (threadIdx.x == 0) {
         float mx = s_max[0];
         for (int j = 1; j < kWaves; ++j) mx = fmaxf(mx, s_max[j]);
-        st_wt(partials + row * 2 + 0, acc[0] / (acc[1] > 1.f ? acc[1] : 1.f));
-        st_wt(partials + row * 2 + 1, mx);
+        partials[row * 2 + 0] = acc[0] / (acc[1] > 1.f ? acc[1] : 1.f);
+        partials[row * 2 + 1] = mx;
     }
-    if (!arrive_last(counter, (unsigned)N, &s_last)) return;
-    double tot[2] = {0.0, 0.0};
-    for (int r = threadIdx.x; r < N; r += kThreads) {
-        tot[0] += (double)partials[r * 2 + 0];
-        tot[1] += (double)partials[r * 2 + 1];
+}
+
+// One-block fold of the per-row records of reward_kl_kernel / critic_loss_kernel (its own
+// launch: the kernel boundary publishes the records; see ppo_loss_fold_kernel).
+// mode 0 (reward KL): metrics[0] = mean_rows rec0, metrics[1] = mean_rows rec1.
+// mode 1 (critic):    out0 = 0.5 * mean_rows rec0, out1 = clip ? sum rec1 / max(sum rec2, 1) : 0.
+template <int K>
+__global__ __launch_bounds__(kThreads) void rows_fold_kernel(const float* __restrict__ partials, int n, int mode,
+                                                            int clip, float* __restrict__ out0,
+                                                            float* __restrict__ out1) {
+    __shared__ double s_redd[kWaves * K];
+    double tot[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) tot[k] = 0.0;
+    for (int r = threadIdx.x; r < n; r += kThreads) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) tot[k] += (double)partials[r * K + k];
     }
-    block_sum_d<kWaves, 2>(tot, s_redd);
-    if (threadIdx.x == 0) {
-        metrics[0] = (float)(tot[0] / (double)N);
-        metrics[1] = (float)(tot[1] / (double)N);
+    block_sum_d<kWaves, K>(tot, s_redd);
+    if (threadIdx.x != 0) return;
+    if (mode == 0) {
+        out0[0] = (float)(tot[0] / (double)n);
+        out0[1] = (float)(tot[1] / (double)n);
+    } else {
+        out0[0] = 0.5f * (float)(tot[0] / (double)n);
+        out1[0] = clip ? (float)(tot[1] / (tot[K - 1] > 1.0 ? tot[K - 1] : 1.0)) : 0.f;
     }
-    rearm(counter);
 }
 
 // ---- ppo_critic_loss -----------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void critic_loss_kernel(
     const float* __restrict__ V, const float* __restrict__ Vold, const float* __restrict__ ret,
-    const float* __restrict__ mask, int n, int R, float vclip, float* __restrict__ loss_out,
-    float* __restrict__ clipfrac_out, float* __restrict__ gv, float* __restrict__ partials,
-    unsigned* __restrict__ counter) {
+    const float* __restrict__ mask, int n, int R, float vclip, float* __restrict__ gv,
+    float* __restrict__ partials) {
     __shared__ float s_red[kWaves * 3];
-    __shared__ double s_redd[kWaves * 3];
-    __shared__ int s_last;
     const int row = blockIdx.x;
     const int64_t rbase = (int64_t)row * R;
     const bool clip = vclip >= 0.f;
@@ -372,23 +382,10 @@ __global__ __launch_bounds__(kThreads) void critic_loss_kernel(
     const float sc = 0.5f / ((float)n * mrow);
     for (int t = threadIdx.x; t < R; t += kThreads) gv[rbase + t] *= sc;
     if (threadIdx.x == 0) {
-        st_wt(partials + row * 3 + 0, acc[0] / mrow);
-        st_wt(partials + row * 3 + 1, acc[2]);
-        st_wt(partials + row * 3 + 2, acc[1]);
+        partials[row * 3 + 0] = acc[0] / mrow;
+        partials[row * 3 + 1] = acc[2];
+        partials[row * 3 + 2] = acc[1];
     }
-    if (!arrive_last(counter, (unsigned)n, &s_last)) return;
-    double tot[3] = {0.0, 0.0, 0.0};
-    for (int r = threadIdx.x; r < n; r += kThreads) {
-        tot[0] += (double)partials[r * 3 + 0];
-        tot[1] += (double)partials[r * 3 + 1];
-        tot[2] += (double)partials[r * 3 + 2];
-    }
-    block_sum_d<kWaves, 3>(tot, s_redd);
-    if (threadIdx.x == 0) {
-        loss_out[0] = 0.5f * (float)(tot[0] / (double)n);
-        clipfrac_out[0] = clip ? (float)(tot[1] / (tot[2] > 1.0 ? tot[2] : 1.0)) : 0.f;
-    }
-    rearm(counter);
 }
 
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16) == 0; }
@@ -473,11 +470,13 @@ extern "C" int skyrl_reward_kl_penalty(const float* rewards, const float* action
                       workspace,
                   "reward_kl_penalty: null pointer");
     SKYRL_REQUIRE(kl_type >= 0 && kl_type <= 3, "reward_kl_penalty: bad kl_type");
-    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
     float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
     hipLaunchKernelGGL(reward_kl_kernel, dim3(N), dim3(kThreads), 0, as_stream(stream), rewards, action_log_probs,
-                       base_action_log_probs, loss_mask, N, R, kl_type, kl_coef, rewards_out, metrics_out, partials,
-                       counter);
+                       base_action_log_probs, loss_mask, N, R, kl_type, kl_coef, rewards_out, partials);
+    int rc = check_launch("reward_kl_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(rows_fold_kernel<2>, dim3(1), dim3(kThreads), 0, as_stream(stream), partials, N, 0, 0,
+                       metrics_out, nullptr);
     return check_launch("reward_kl_kernel");
 }
 
@@ -493,9 +492,12 @@ extern "C" int skyrl_critic_loss_fwd(const float* values, const float* old_value
     SKYRL_REQUIRE(values && returns && loss_out && clipfrac_out && grad_values && workspace,
                   "critic_loss: null pointer");
     SKYRL_REQUIRE(value_clip < 0.f || old_values, "critic_loss: value_clip needs old_values");
-    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
     float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
     hipLaunchKernelGGL(critic_loss_kernel, dim3(n), dim3(kThreads), 0, as_stream(stream), values, old_values, returns,
-                       loss_mask, n, R, value_clip, loss_out, clipfrac_out, grad_values, partials, counter);
+                       loss_mask, n, R, value_clip, grad_values, partials);
+    int rc = check_launch("critic_loss_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(rows_fold_kernel<3>, dim3(1), dim3(kThreads), 0, as_stream(stream), partials, n, 1,
+                       value_clip >= 0.f ? 1 : 0, loss_out, clipfrac_out);
     return check_launch("critic_loss_kernel");
 }
