@@ -60,15 +60,35 @@ static float det_ln(float y) {
     return fmaf((float)e, 0.693147180559945f, z * p);
 }
 
-/* Element v's uniform: u = ((t16 << 8) | lo8 | 1) * 2^-24, t16 = 65535 - h16 with h16 =
- * half (v & 1) of hash32(key ^ (v >> 1) * phi), lo8 = top byte of hash32(key2 ^ v * phi),
- * key2 = hash32(key ^ 0x5bd1e995). g = -ln(-ln u). */
+/* Pair hash from 24-bit products (restates ehash in skyrl_amd/csrc/sampler.hip). */
+static uint32_t mul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+static uint32_t ehash(uint32_t ka, uint32_t kb, uint32_t p) {
+    uint32_t h = mul24(p, 0x9e3779u) + ka;
+    h ^= h >> 16;
+    h = mul24(h, 0x85ebcau) + kb;
+    h ^= h >> 16;
+    h = mul24(h, 0xc2b2aeu);
+    h ^= h >> 16;
+    return h;
+}
+
+/* Element v's noise -ln E_v, E_v ~ Exp(1) drawn per group g = v >> 3 through the order
+ * statistics of 8 draws (restates the noise model of sample_kernel): h = ehash(key, keyb, g),
+ * the group minimum E_g = -ln(u_g) / 8 with u_g = (((h >> 16 ^ 0xffff) << 8) | (h >> 8 & 0xff)
+ * | 1) 2^-24 sits at slot p = h & 7; any other slot is E_g + (-ln U_v) with U_v = ((hash32(key2
+ * ^ v phi) >> 8) | 1) 2^-24. key2 = hash32(key ^ 0x5bd1e995), keyb = hash32(key ^ 0x27d4eb2f). */
 static float gumbel(uint32_t key, uint32_t v) {
     uint32_t key2 = hash32(key ^ 0x5bd1e995u);
-    uint32_t t16 = ((hash32(key ^ ((v >> 1) * 0x9e3779b1u)) >> (16 * (v & 1))) & 0xffffu) ^ 0xffffu;
-    uint32_t lo8 = hash32(key2 ^ (v * 0x9e3779b1u)) >> 24;
-    float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
-    float E = -det_ln(u);
+    uint32_t keyb = hash32(key ^ 0x27d4eb2fu);
+    uint32_t h = ehash(key, keyb, v >> 3);
+    uint32_t t16 = (h >> 16) ^ 0xffffu;
+    float ug = (float)(((t16 << 8) | ((h >> 8) & 0xffu)) | 1u) * 5.9604644775390625e-8f;
+    float E = -det_ln(ug) * 0.125f;
+    if ((v & 7u) != (h & 7u)) {
+        uint32_t hu = hash32(key2 ^ (v * 0x9e3779b1u));
+        float U = (float)((hu >> 8) | 1u) * 5.9604644775390625e-8f;
+        E = E + (-det_ln(U));
+    }
     return -det_ln(E);
 }
 

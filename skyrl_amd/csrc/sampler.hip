@@ -8,8 +8,9 @@
 // top_k (keep values >= k-th largest, ties kept), then min_p; T == 0 is greedy
 // over the raw logits; the returned logprob is log_softmax(raw logits)[token].
 //
-// Sampling is Gumbel-max, argmax_v (x_v/T + g_v), with g = -ln(-ln u) and u
-// from a counter-based integer hash of (seed, seq_id, step, v). Every float
+// Sampling is Gumbel-max, argmax_v (x_v/T - ln E_v) with E_v iid Exp(1), drawn per group of 8
+// elements through their order statistics (see the noise model in sample_kernel) from
+// counter-based integer hashes of (seed, seq_id, step, v). Every float
 // operation on the decision path is an IEEE basic op or an explicit fmaf and
 // contraction is off in this file, so the token is a pure function of the
 // inputs and oracle/sampler_ref.c reproduces it bit for bit.
@@ -40,6 +41,22 @@ __host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     x *= 0x846ca68bu;
     x ^= x >> 16;
     return x;
+}
+
+// Per-element noise hash of pair index p (two 16-bit halves, one per element). Built from
+// 24-bit multiplies (v_mad_u32_u24 / v_mul_u32_u24 issue at the full VALU rate, v_mul_lo_u32 at a
+// quarter of it) and 16-bit xor-shifts (one SDWA op each); the two row keys enter at two rounds, so
+// that an additive collision of the first round between rows is broken by the second.
+// Bit-identical in oracle/sampler_ref.c.
+__host__ __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+__host__ __device__ __forceinline__ uint32_t ehash(uint32_t ka, uint32_t kb, uint32_t p) {
+    uint32_t h = mul24(p, 0x9e3779u) + ka;
+    h ^= h >> 16;
+    h = mul24(h, 0x85ebcau) + kb;
+    h ^= h >> 16;
+    h = mul24(h, 0xc2b2aeu);
+    h ^= h >> 16;
+    return h;
 }
 
 __host__ __device__ __forceinline__ uint32_t row_key(uint64_t seed, int64_t seq, int64_t step) {
@@ -463,35 +480,77 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     // (so a strict '>' keeps the lowest index on ties) and the raw online (max, sum-exp).
     float best_s = -INFINITY;
     int best_i = 0x7fffffff;
-    const uint32_t key2 = hash32(key ^ 0x5bd1e995u);
+    const uint32_t key2 = hash32(key ^ 0x5bd1e995u);  // per-element uniforms (candidates only)
+    const uint32_t keyb = hash32(key ^ 0x27d4eb2fu);  // second-round key of ehash
     // raw online (max, sum-exp) for the sampled token's logprob; finite start so that an
     // all-padding vector never forms inf - inf
     float m = -1e30f, s = 0.f;
-    // Gumbel candidate filter. Element v's noise g is bounded by its 16-bit hash half h16
-    // alone: u = ((t16 << 8) | lo8 | 1) 2^-24 with t16 = 65535 - h16, so 1 - u > h16 / 65536
-    // and g = -ln(-ln u) <= -ln(1 - u) < ln2 (16 - log2 h16) <= ln2 (143 - bits(float(h16)) 2^-23)
-    // (a float's bit pattern is a piecewise-linear lower bound of 2^23 (log2 + 127)). With
-    // margin 0.01 (>> the det_ln error) an element can beat an exact score `bar` already found
-    // in this row only if
-    //   x/T + 143 ln2 + 0.01 - ln2 2^-23 bits >= bar  <=>  x - (T ln2 2^-23) bits >= (bar - C) T,
-    // one fma and one compare per element. Decisions are unchanged: the filter only skips
-    // elements whose exact score is provably below a score already found.
+    // Noise model (group-of-8 exponential race). Gumbel-max argmax_v (x_v/T - ln E_v) with E_v iid
+    // Exp(1) draws the 8 E's of group g = v >> 3 through their order statistics: the minimum
+    // E_g = -ln(u_g)/8 ~ Exp(8) sits at slot p, uniform, and the other slots are E_g + e_k with
+    // e_k = -ln U_k ~ Exp(1) (memorylessness), so every E_v is exactly Exp(1) and independent. One
+    // hash h = ehash(g) per 8 elements gives h16 = h >> 16, u_g = (((h16 ^ 0xffff) << 8) | lo8 |
+    // 1) 2^-24 with lo8 = (h >> 8) & 0xff, and p = h & 7; U_k comes from hash32(key2 ^ v phi),
+    // evaluated for candidates only.
+    // Bound: E_v >= E_g >= 1 - u_g > h16 2^-19, so -ln E_v < ln2 (19 - log2 h16) <= ln2 (146 -
+    // bits(float(h16)) 2^-23) (a float's bit pattern is a piecewise-linear lower bound of
+    // 2^23 (log2 + 127)). With margin 0.01 (>> the det_ln error) a group can hold an element that
+    // beats an exact score `bar` already found in this row only if
+    //   xmax/T + 146 ln2 + 0.01 - ln2 2^-23 bits >= bar  <=>  xmax - (T ln2 2^-23) bits >= (bar - C) T,
+    // one max over the vector, one fma and one compare per 8 elements. Decisions are unchanged:
+    // the filter only skips elements whose exact score is provably below a score already found.
     const float temp = greedy ? 1.f : 1.0f / inv_t;
     const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-    constexpr float kC = 143.0f * 0.6931471805599453f + 0.01f;
+    constexpr float kC = 146.0f * 0.6931471805599453f + 0.01f;
+    constexpr float kU24 = 5.9604644775390625e-8f;
     float thr = -INFINITY;   // (bar - C) * T, wave-uniform
     float bar = -INFINITY;   // best exact score known to this wave (wave-uniform)
     bool seeded = greedy;    // first vector: one exact score per lane sets the bar
-    constexpr int VEC = 16 / sizeof(T);
+    constexpr int VEC = 16 / sizeof(T);  // 8 bf16 (one group) or 4 f32 (half a group)
 
-    auto exact = [&](const float xk, uint32_t h16, int v) -> float {
-        const uint32_t t16 = h16 ^ 0xffffu;
-        const uint32_t lo8 = hash32(key2 ^ ((uint32_t)v * 0x9e3779b1u)) >> 24;
-        const float u = (float)(((t16 << 8) | lo8) | 1u) * 5.9604644775390625e-8f;
-        return xk * inv_t + (-det_ln(-det_ln(u)));
+    // E_g of group hash h (the group's smallest Exp(1) draw)
+    auto group_e = [&](uint32_t h) -> float {
+        const uint32_t t16 = (h >> 16) ^ 0xffffu;
+        const float ug = (float)(((t16 << 8) | ((h >> 8) & 0xffu)) | 1u) * kU24;
+        return -det_ln(ug) * 0.125f;
+    };
+    // exact score of element v of the group with hash h and minimum E_g
+    auto exact = [&](float xk, int v, uint32_t h, float Eg) -> float {
+        float E = Eg;
+        if (((uint32_t)v & 7u) != (h & 7u)) {
+            const uint32_t hu = hash32(key2 ^ ((uint32_t)v * 0x9e3779b1u));
+            const float U = (float)((hu >> 8) | 1u) * kU24;
+            E = Eg + (-det_ln(U));
+        }
+        return xk * inv_t + (-det_ln(E));
+    };
+    // Every element of a candidate vector that can still reach the bar through the group bound
+    // (the additive form per element; a tie with the bar is evaluated). Unrolled over the slots:
+    // a slot's block runs only when some lane needs it (usually one or two per candidate vector).
+    auto eval_vec = [&](const float (&x)[VEC], const bool (&ok)[VEC], int v0, uint32_t h) {
+        const float bits = (float)(int)__float_as_uint((float)(h >> 16));
+        bool need[VEC];
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            need[k] = ok[k] && !(fmaf(bits, -kT, x[k]) - thr < 0.f);
+            any = any || need[k];
+        }
+        if (!any) return;
+        const float Eg = group_e(h);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            if (need[k]) {
+                const float sc = exact(x[k], v0 + k, h, Eg);
+                if (sc > best_s) {  // ascending k within the lane's ascending visit order
+                    best_s = sc;
+                    best_i = v0 + k;
+                }
+            }
+        }
     };
     // MODE 3 (T == 1) bound in multiplicative form, reusing the lse exponentials ex = e^(x - m):
-    // nn <= 65536 e^(x - bar + 0.01) <=> nn <= ex * Q, Q = 2^16 e^(m - bar + 0.01) per lane.
+    // h16 <= 2^19 e^(xmax - bar + 0.01) <=> h16 <= exmax * Q, Q = 2^19 e^(m - bar + 0.01) per lane.
     // While some lane has m - bar > 70 (Q near overflow; an ex that underflowed, x < m - 87,
     // could then still matter) the wave falls back to the additive bits form (qbad). Q is
     // clamped below at FLT_MIN so that an overflowed ex (inf) stays a candidate.
@@ -499,7 +558,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     bool qbad = true;
     auto recompute_q = [&]() {
         const float d = m - bar + 0.01f;
-        Q = fmaxf(fast_exp2(fmaf(fminf(d, 70.f), kLog2e, 16.0f)), 1.17549435e-38f);
+        Q = fmaxf(fast_exp2(fmaf(fminf(d, 70.f), kLog2e, 19.0f)), 1.17549435e-38f);
         qbad = __builtin_amdgcn_ballot_w64(!(d <= 70.f)) != 0;
     };
     auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
@@ -511,26 +570,37 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
         thr = (bar - kC) * temp;
         if constexpr (MODE == 3) recompute_q();
     };
+    // adopt the workgroup's bar (after the seeding barrier; a per-iteration refresh measured slower:
+    // the LDS round trip stalls every wave at the same point of its iteration)
+    auto refresh_bar = [&]() {
+        const float sb = __int_as_float(__builtin_amdgcn_readfirstlane(
+            __float_as_int(__hip_atomic_load(&s_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))));
+        if (sb > bar) {
+            bar = sb;
+            thr = (bar - kC) * temp;
+            if constexpr (MODE == 3) recompute_q();
+        }
+    };
+    // additive bound test of a vector whose largest admissible logit is xm
+    auto cand_add = [&](float xm, uint32_t h) -> bool {
+        const float bits = (float)(int)__float_as_uint((float)(h >> 16));
+        return !(fmaf(bits, -kT, xm) - thr < 0.f);
+    };
     // once per wave, before any filtering: the exact score of each lane's largest admissible
     // element of its first vector sets the bar (one exact evaluation per lane instead of VEC)
-    auto seed_vec = [&](const T (&raw)[VEC], const float (&x)[VEC], const uint32_t (&hp)[VEC / 2], int v0, int cnt) {
+    auto seed_vec = [&](const float (&x)[VEC], const bool (&ok)[VEC], int v0, uint32_t h) {
         seeded = true;
         float xb = -INFINITY;
         int kb = -1;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            bool keep = k < cnt;
-            if constexpr (MODE == 2) keep = keep && admissible(raw[k], x[k], v0 + k);
-            if (keep && x[k] > xb) {
+            if (ok[k] && x[k] > xb) {
                 xb = x[k];
                 kb = k;
             }
         }
         if (kb >= 0) {
-            uint32_t hb = 0;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) hb = (k == kb) ? ((k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu)) : hb;
-            const float sc = exact(xb, hb, v0 + kb);
+            const float sc = exact(xb, v0 + kb, h, group_e(h));
             if (sc > best_s) {
                 best_s = sc;
                 best_i = v0 + kb;
@@ -559,8 +629,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
         m = mn;
         return mn;
     };
-    // One vector of VEC elements starting at v0 (v0 % 8 == 0 on every path); cnt < VEC only on
-    // the ragged tail (FULL = false).
+    // One vector of VEC elements starting at v0 (v0 % VEC == 0, so inside one group); cnt < VEC
+    // only on the ragged tail (FULL = false).
     auto visit_vec = [&](const T (&raw)[VEC], int v0, int cnt, auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
         float x[VEC];
@@ -581,37 +651,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
             }
             return;
         }
-        const uint32_t g0 = (uint32_t)v0 >> 1;
-        uint32_t hp[VEC / 2];
+        bool ok[VEC];
+        float xm = -INFINITY;
 #pragma unroll
-        for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
-        auto h16 = [&](int k) -> uint32_t { return (k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu); };
+        for (int k = 0; k < VEC; ++k) {
+            ok[k] = FULL || k < cnt;
+            if constexpr (MODE == 2) ok[k] = ok[k] && admissible(raw[k], x[k], v0 + k);
+            xm = fmaxf(xm, ok[k] ? x[k] : -INFINITY);
+        }
+        const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
         if constexpr (!FULL) {
-            if (!seeded) seed_vec(raw, x, hp, v0, cnt);
+            if (!seeded) seed_vec(x, ok, v0, h);
         }
-        // fv[k] >= 0 (or NaN) <=> element k may beat the bar; -inf for inadmissible slots
-        float fv[VEC];
-        uint64_t anym = 0;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            const float bits = (float)(int)__float_as_uint((float)h16(k));
-            fv[k] = fmaf(bits, -kT, x[k]) - thr;
-            bool keep = FULL || k < cnt;
-            if constexpr (MODE == 2) keep = keep && admissible(raw[k], x[k], v0 + k);
-            if (!FULL || MODE == 2) fv[k] = keep ? fv[k] : -INFINITY;
-            anym |= __builtin_amdgcn_ballot_w64(!(fv[k] < 0.f));
-        }
-        if (anym == 0) return;  // wave-uniform: rare once the bar is up
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            if (!(fv[k] < 0.f)) {
-                const float sc = exact(x[k], h16(k), v0 + k);
-                if (sc > best_s) {
-                    best_s = sc;
-                    best_i = v0 + k;
-                }
-            }
-        }
+        const bool cand = xm > -INFINITY && cand_add(xm, h);
+        if (__builtin_amdgcn_ballot_w64(cand) == 0) return;  // wave-uniform: rare once the bar is up
+        if (cand) eval_vec(x, ok, v0, h);
         raise_bar();
     };
     // MODE 3 full vector, lagged lse offset m (exps accumulate into acc2; the caller checks
@@ -633,44 +687,33 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
             ex[k + 1] = fast_exp2(y.y);
             acc2 += f32x2{ex[k], ex[k + 1]};
         }
-        const uint32_t g0 = (uint32_t)v0 >> 1;
-        uint32_t hp[VEC / 2];
-#pragma unroll
-        for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ ((g0 + (uint32_t)q) * 0x9e3779b1u));
-        auto h16 = [&](int k) -> uint32_t { return (k & 1) ? (hp[k >> 1] >> 16) : (hp[k >> 1] & 0xffffu); };
-        float fv[VEC];
+#ifdef SKYRL_SV_NOHASH  // scripts/probe/sampler_variants only: timing, not correct tokens
+        const uint32_t h = 0x80000000u ^ (uint32_t)v0;
+#else
+        const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+#endif
+        bool cand;
         if (!qbad) {
-            const f32x2 q2 = {Q, Q};
-            float fmx = -INFINITY;
+            float em = fmaxf(fmaxf(ex[0], ex[1]), ex[2]);
 #pragma unroll
-            for (int k = 0; k < VEC; k += 2) {
-                const f32x2 e2 = {ex[k], ex[k + 1]};
-                const f32x2 n2 = {-(float)h16(k), -(float)h16(k + 1)};
-                const f32x2 f = __builtin_elementwise_fma(e2, q2, n2);
-                fv[k] = f.x;
-                fv[k + 1] = f.y;
-                fmx = fmaxf(fmx, fmaxf(f.x, f.y));
-            }
-            if (__builtin_amdgcn_ballot_w64(fmx >= 0.f) == 0) return;
+            for (int k = 3; k + 1 < VEC; k += 2) em = fmaxf(fmaxf(em, ex[k]), ex[k + 1]);
+            if constexpr (VEC % 2 == 0) em = fmaxf(em, ex[VEC - 1]);
+            cand = fmaf(em, Q, -(float)(h >> 16)) >= 0.f;
         } else {
-            uint64_t anym = 0;
+            float xm = x[0];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const float bits = (float)(int)__float_as_uint((float)h16(k));
-                fv[k] = fmaf(bits, -kT, x[k]) - thr;
-                anym |= __builtin_amdgcn_ballot_w64(!(fv[k] < 0.f));
-            }
-            if (anym == 0) return;
+            for (int k = 1; k < VEC; ++k) xm = fmaxf(xm, x[k]);
+            cand = cand_add(xm, h);
         }
+#ifdef SKYRL_SV_NOCAND
+        cand = false;
+#endif
+        if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
+        if (cand) {
+            bool ok[VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            if (!(fv[k] < 0.f)) {
-                const float sc = exact(x[k], h16(k), v0 + k);
-                if (sc > best_s) {
-                    best_s = sc;
-                    best_i = v0 + k;
-                }
-            }
+            for (int k = 0; k < VEC; ++k) ok[k] = true;
+            eval_vec(x, ok, v0, h);
         }
         raise_bar();
     };
@@ -711,23 +754,42 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
         if (nfull > 0) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
-            if constexpr (!greedy) {  // seed from this lane's first vector
-                T vals[VEC];
-                __builtin_memcpy(vals, &cur[0], 16);
-                float x[VEC];
+            // Drain the first iteration's loads here. Otherwise the loop header merges "cur
+            // pending" (this path) with "cur in registers" (the back edge), and the waitcnt pass
+            // puts vmcnt(2)/(1)/(0) before cur[1..3] in EVERY iteration: those counts then wait for
+            // the next iteration's prefetch, and the last vector is processed with nothing in flight.
+            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+            if constexpr (!greedy) {  // seed from this lane's first two vectors
+                float x[2][VEC];
+                bool ok[2][VEC];
+                float xb[2] = {-INFINITY, -INFINITY};
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) x[k] = to_f<T>(vals[k]);
-                if constexpr (MODE == 3) {  // lagged lse offset starts at this lane's first-vector max
-                    float mx = x[0];
+                for (int u = 0; u < 2; ++u) {
+                    T vals[VEC];
+                    __builtin_memcpy(vals, &cur[u], 16);
+                    const int v0s = v_beg + (u * NT + threadIdx.x) * VEC;
 #pragma unroll
-                    for (int k = 1; k < VEC; ++k) mx = fmaxf(mx, x[k]);
-                    m = mx;
+                    for (int k = 0; k < VEC; ++k) {
+                        x[u][k] = to_f<T>(vals[k]);
+                        ok[u][k] = true;
+                        if constexpr (MODE == 2) ok[u][k] = admissible(vals[k], x[u][k], v0s + k);
+                        xb[u] = fmaxf(xb[u], ok[u][k] ? x[u][k] : -INFINITY);
+                    }
                 }
-                const int v0s = v_beg + threadIdx.x * VEC;
-                uint32_t hp[VEC / 2];
+                if constexpr (MODE == 3) m = fmaxf(xb[0], xb[1]);  // lagged lse offset: this lane's first max
+                const bool us = xb[1] > xb[0];
+                float xs[VEC];
+                bool oks[VEC];
 #pragma unroll
-                for (int q = 0; q < VEC / 2; ++q) hp[q] = hash32(key ^ (((uint32_t)v0s >> 1) + (uint32_t)q) * 0x9e3779b1u);
-                seed_vec(vals, x, hp, v0s, VEC);
+                for (int k = 0; k < VEC; ++k) {  // selects, not a dynamically indexed array (scratch)
+                    xs[k] = us ? x[1][k] : x[0][k];
+                    oks[k] = us ? ok[1][k] : ok[0][k];
+                }
+                const int v0s = v_beg + ((us ? NT : 0) + threadIdx.x) * VEC;
+                seed_vec(xs, oks, v0s, ehash(key, keyb, (uint32_t)v0s >> 3));
+                // every wave starts from the best of the workgroup's 2 x NT seeds
+                __syncthreads();
+                refresh_bar();
             }
         }
         for (int base = 0; base < nfull; base += kStep) {
