@@ -302,6 +302,32 @@ int skyrl_adamw_update(float* param, const float* grad, float* exp_avg, float* e
  * optimizer ran without a bf16 shadow (FSDPWeightExtractor, fsdp_worker.py:30-87). */
 int skyrl_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 
+/* ---- §8(f)2: rollout decode loop (paged KV cache) ------------------------
+ * Replace the attention of vLLM's decode step behind VLLMInferenceEngine.generate
+ * (inference_engines/vllm/vllm_engine.py:196-218); model semantics are HF
+ * Qwen2/Llama (rotate_half RoPE, GQA). One KV cache per layer:
+ *   K bf16 [num_blocks, nkv, 16, head_dim], V bf16 [num_blocks, nkv, head_dim, 16];
+ * slot = block * 16 + offset; head_dim in {64, 128}; nh % nkv == 0.
+ *   skyrl_rope_kv_write  qkv bf16 [T, (nh+2nkv)*head_dim] (row stride qkv_stride):
+ *                        rotates q into q_out bf16 [T,nh,head_dim], rotates k into the
+ *                        K cache (and k_out [T,nkv,head_dim] if non-NULL), copies v into
+ *                        the V cache; slot_mapping[t] < 0 skips the cache write.
+ *                        cos_sin f32 [max_pos, head_dim] = cos | sin halves.
+ *   skyrl_paged_decode   one query token per sequence: out[s] = softmax(scale q.K^T) V over
+ *                        context_lens[s] >= 1 cached tokens listed by block_tables
+ *                        i32 [nseq, bt_stride]; nh/nkv <= 16. The context is split into
+ *                        nparts partitions of part_tokens (multiple of 16; nparts *
+ *                        part_tokens >= max context); nparts > 1 needs
+ *                        skyrl_paged_decode_workspace_bytes(nseq, nh, head_dim, nparts). */
+int skyrl_rope_kv_write(const void* qkv, int64_t qkv_stride, int32_t T, int32_t nh, int32_t nkv, int32_t head_dim,
+                        const int64_t* positions, const int64_t* slot_mapping, const float* cos_sin, void* q_out,
+                        void* k_out, void* k_cache, void* v_cache, void* stream);
+size_t skyrl_paged_decode_workspace_bytes(int32_t nseq, int32_t nh, int32_t head_dim, int32_t nparts);
+int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                       const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens, int32_t nseq,
+                       int32_t nh, int32_t nkv, int32_t head_dim, float scale, int32_t part_tokens, int32_t nparts,
+                       void* out, int64_t out_stride, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

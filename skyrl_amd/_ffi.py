@@ -133,6 +133,10 @@ SIGNATURES = {
     "skyrl_adamw_plan": (_INT, [_P, ctypes.POINTER(AdamWParams), _P, _P, _P, _P]),
     "skyrl_adamw_update": (_INT, [_P, _P, _P, _P, _P, _I64, _P, _F, _F, _P]),
     "skyrl_cast_bf16": (_INT, [_P, _P, _I64, _P]),
+    "skyrl_rope_kv_write": (_INT, [_P, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "skyrl_paged_decode_workspace_bytes": (_SZ, [_I32, _I32, _I32, _I32]),
+    "skyrl_paged_decode": (_INT, [_P, _I64, _P, _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _F, _I32, _I32, _P, _I64,
+                                  _P, _P]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,316 @@
+// §8(f)2: rollout decode loop kernels — rotary embedding fused with the paged KV-cache
+// write, and single-token (decode) attention over the paged cache with MFMA.
+//
+// Replaces the attention inside vLLM's decode step that the reference drives through
+// VLLMInferenceEngine.generate (skyrl_train/inference_engines/vllm/vllm_engine.py:196-218);
+// model semantics follow HF Qwen2/Llama (apply_rotary_pos_emb with rotate_half, GQA with
+// num_key_value_heads, softmax(q.k / sqrt(D)) v).
+//
+// Cache layout (one layer; the host keeps one pair per layer):
+//   K: bf16 [num_blocks, nkv, 16, D]   — a (block, head) tile is 16 token rows of D
+//   V: bf16 [num_blocks, nkv, D, 16]   — transposed: 16 tokens contiguous per dim
+// A slot is block * 16 + offset. The V transpose makes both MFMA operands of the P.V
+// product 8-byte loads (below).
+//
+// Decode attention: one wave per (partition of <= part_tokens context tokens, kv head,
+// sequence). Per 16-token block the wave computes S^T[token x head] = K[16 x D] . Q^T[D x 16]
+// with D/32 mfma_f32_16x16x32_bf16 (the <= 16 query heads of the kv head's GQA group are the
+// 16 MFMA columns; unused columns are zero), so every lane holds 4 tokens of ONE head: the
+// online-softmax statistics are per lane, the block max is 2 xor-shuffles, and the exp'd
+// scores are already the B operand of O^T[d x head] += V^T[d x 16] . P^T[16 x head]
+// (D/16 mfma_f32_16x16x16_bf16, no lane movement, no LDS). K and V stream straight from
+// HBM into VGPRs (guide: decode attention, M <= 16 rows per kv head). Partitions are
+// merged by a small reduce kernel when a sequence spans more than one.
+#include "common.h"
+
+namespace skyrl {
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBS = 16;  // tokens per KV-cache block
+
+// ---- rotary embedding + KV-cache write ----------------------------------------------
+// grid (T, nh + 2*nkv), one wave per (token, head). Heads [0, nh) are query heads (rotated
+// into q_out), [nh, nh+nkv) key heads (rotated into the K cache at the token's slot, and
+// into k_out if given), [nh+nkv, nh+2nkv) value heads (copied into the V cache). qkv is the
+// fused projection output [T, (nh+2nkv)*D] with row stride qkv_stride (elements).
+// cos_sin: f32 [max_pos, D]: cos in [0, D/2), sin in [D/2, D) (HF's duplicated halves
+// collapse to one copy). Rotation in f32, one rounding to bf16.
+template <int D>
+__global__ __launch_bounds__(64) void rope_kv_write_kernel(
+    const uint16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ positions,
+    const int64_t* __restrict__ slots, const float* __restrict__ cos_sin, int nh, int nkv,
+    uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_out, uint16_t* __restrict__ kc,
+    uint16_t* __restrict__ vc) {
+    const int t = blockIdx.x;
+    const int hh = blockIdx.y;
+    const int lane = threadIdx.x;
+    const uint16_t* src = qkv + (int64_t)t * qkv_stride + (int64_t)hh * D;
+    constexpr int H2 = D / 2;
+    if (hh >= nh + nkv) {  // value head: copy into the transposed V tile
+        const int64_t slot = slots[t];
+        if (slot < 0) return;
+        const int kvh = hh - nh - nkv;
+        const int64_t blk = slot / kBS;
+        const int off = (int)(slot % kBS);
+        uint16_t* dst = vc + ((blk * nkv + kvh) * D) * kBS + off;
+        for (int d = lane; d < D; d += kWave) dst[(int64_t)d * kBS] = src[d];
+        return;
+    }
+    const int64_t pos = positions[t];
+    const float* cs = cos_sin + pos * D;
+    for (int i = lane; i < H2; i += kWave) {
+        const float x1 = bf16_to_f32(src[i]);
+        const float x2 = bf16_to_f32(src[i + H2]);
+        const float c = cs[i], s = cs[H2 + i];
+        const uint16_t y1 = f32_to_bf16(x1 * c - x2 * s);
+        const uint16_t y2 = f32_to_bf16(x2 * c + x1 * s);
+        if (hh < nh) {
+            uint16_t* dq = q_out + ((int64_t)t * nh + hh) * D;
+            dq[i] = y1;
+            dq[i + H2] = y2;
+        } else {
+            const int kvh = hh - nh;
+            if (k_out) {
+                uint16_t* dk = k_out + ((int64_t)t * nkv + kvh) * D;
+                dk[i] = y1;
+                dk[i + H2] = y2;
+            }
+            const int64_t slot = slots[t];
+            if (slot >= 0) {
+                const int64_t blk = slot / kBS;
+                const int off = (int)(slot % kBS);
+                uint16_t* dk = kc + ((blk * nkv + kvh) * kBS + off) * D;
+                dk[i] = y1;
+                dk[i + H2] = y2;
+            }
+        }
+    }
+}
+
+// ---- decode attention over the paged cache -------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void paged_decode_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
+    const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_tokens,
+    int nparts, uint16_t* __restrict__ out, int64_t out_stride, float* __restrict__ ws_o,
+    float* __restrict__ ws_ml) {
+    constexpr int KS = D / 32;  // k-steps of the Q.K^T MFMA
+    constexpr int NT = D / 16;  // 16-dim output tiles of the P.V MFMA
+    const int seq = blockIdx.z;
+    const int kvh = blockIdx.y;
+    const int part = blockIdx.x;
+    const int ctx = ctx_lens[seq];
+    const int t0 = part * part_tokens;
+    if (t0 >= ctx) return;
+    const int t1 = min(ctx, t0 + part_tokens);
+    const int lane = threadIdx.x;
+    const int c = lane & 15;  // MFMA column: query head within the GQA group / token row of K
+    const int g = lane >> 4;  // lane group: k-slice of the operands, 4-row slice of the result
+    const int h = kvh * qpk + c;
+    const bool hv = c < qpk;
+
+    s16x8 qf[KS];
+    const uint16_t* qrow = q + (int64_t)seq * q_stride + (int64_t)(hv ? h : 0) * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        qf[s] = *reinterpret_cast<const s16x8*>(qrow + 32 * s + 8 * g);
+        if (!hv) qf[s] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    f32x4 o[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+
+    const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
+    const int64_t head_tile = (int64_t)kBS * D;
+    const int64_t blk_stride = (int64_t)nkv * head_tile;
+    for (int tb = t0; tb < t1; tb += kBS) {
+        const int64_t blk = __builtin_amdgcn_readfirstlane(bt[tb / kBS]);
+        const uint16_t* kb = kc + blk * blk_stride + kvh * head_tile;
+        const uint16_t* vb = vc + blk * blk_stride + kvh * head_tile;
+        s16x8 kf[KS];
+        s16x4 vf[NT];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const s16x8*>(kb + c * D + 32 * s + 8 * g);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) vf[n] = *reinterpret_cast<const s16x4*>(vb + (16 * n + c) * kBS + 4 * g);
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], qf[s], sacc, 0, 0, 0);
+        // sacc[i] = S[token tb + 4g + i][head c]; tokens past the partition end are masked
+        // (their K/V slots hold stale data: select, never multiply).
+        const int nv = t1 - (tb + 4 * g);  // valid tokens among this lane's 4
+        float sv[4];
+        float bm = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            sv[i] = (i < nv) ? sacc[i] * scale_log2 : -INFINITY;
+            bm = fmaxf(bm, sv[i]);
+        }
+        bm = fmaxf(bm, __shfl_xor(bm, 16, kWave));
+        bm = fmaxf(bm, __shfl_xor(bm, 32, kWave));
+        const float mn = fmaxf(m, bm);
+        const float alpha = fast_exp2(m - mn);  // m = -inf on the first block: 0
+        float p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = fast_exp2(sv[i] - mn);
+        l = l * alpha + ((p[0] + p[1]) + (p[2] + p[3]));
+        m = mn;
+        if (nv < 4) {  // zero the V columns of masked tokens: stale V times p = 0 must not be NaN
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j >= nv) vf[n][j] = 0;
+            }
+        }
+        s16x4 pf;
+        const uint32_t p01 = pack_bf16x2(p[0], p[1]);
+        const uint32_t p23 = pack_bf16x2(p[2], p[3]);
+        pf[0] = (short)(p01 & 0xffff);
+        pf[1] = (short)(p01 >> 16);
+        pf[2] = (short)(p23 & 0xffff);
+        pf[3] = (short)(p23 >> 16);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            o[n] = o[n] * alpha;
+            o[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[n], pf, o[n], 0, 0, 0);
+        }
+    }
+    // o[n][i] = O^T[dim 16n + 4g + i][head c]; l is this lane's share of the row sum
+    l += __shfl_xor(l, 16, kWave);
+    l += __shfl_xor(l, 32, kWave);
+    if (!hv) return;
+    if (nparts == 1) {
+        const float inv = 1.f / l;
+        uint16_t* orow = out + (int64_t)seq * out_stride + (int64_t)h * D;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            uint2 w;
+            w.x = pack_bf16x2(o[n][0] * inv, o[n][1] * inv);
+            w.y = pack_bf16x2(o[n][2] * inv, o[n][3] * inv);
+            *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g) = w;
+        }
+    } else {
+        const int64_t rec = ((int64_t)seq * nh + h) * nparts + part;
+        float* wo = ws_o + rec * D;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) *reinterpret_cast<f32x4*>(wo + 16 * n + 4 * g) = o[n];
+        if (g == 0) {
+            ws_ml[rec * 2 + 0] = m;
+            ws_ml[rec * 2 + 1] = l;
+        }
+    }
+}
+
+// Merge the partitions of one (sequence, head): grid (nh, nseq), D threads.
+template <int D>
+__global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const float* __restrict__ ws_o,
+                                                                const float* __restrict__ ws_ml,
+                                                                const int32_t* __restrict__ ctx_lens, int nh,
+                                                                int part_tokens, int nparts,
+                                                                uint16_t* __restrict__ out, int64_t out_stride) {
+    const int h = blockIdx.x;
+    const int seq = blockIdx.y;
+    const int d = threadIdx.x;
+    const int ctx = ctx_lens[seq];
+    int np = (ctx + part_tokens - 1) / part_tokens;
+    np = np < nparts ? np : nparts;
+    const int64_t rec0 = ((int64_t)seq * nh + h) * nparts;
+    float M = -INFINITY;
+    for (int p = 0; p < np; ++p) M = fmaxf(M, ws_ml[(rec0 + p) * 2]);
+    float L = 0.f, acc = 0.f;
+    for (int p = 0; p < np; ++p) {
+        const float w = fast_exp2(ws_ml[(rec0 + p) * 2] - M);
+        L += w * ws_ml[(rec0 + p) * 2 + 1];
+        acc += w * ws_o[(rec0 + p) * D + d];
+    }
+    out[(int64_t)seq * out_stride + (int64_t)h * D + d] = f32_to_bf16(np > 0 ? acc / L : 0.f);
+}
+
+}  // namespace
+}  // namespace skyrl
+
+using namespace skyrl;
+
+extern "C" int skyrl_rope_kv_write(const void* qkv, int64_t qkv_stride, int32_t T, int32_t nh, int32_t nkv,
+                                   int32_t head_dim, const int64_t* positions, const int64_t* slot_mapping,
+                                   const float* cos_sin, void* q_out, void* k_out, void* k_cache, void* v_cache,
+                                   void* stream) {
+    SKYRL_REQUIRE(T >= 0 && nh > 0 && nkv > 0 && nh % nkv == 0, "rope_kv_write: bad head counts");
+    SKYRL_REQUIRE(head_dim == 64 || head_dim == 128, "rope_kv_write: head_dim must be 64 or 128");
+    if (T == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(qkv && positions && slot_mapping && cos_sin && q_out && k_cache && v_cache,
+                  "rope_kv_write: null pointer");
+    SKYRL_REQUIRE(qkv_stride >= (int64_t)(nh + 2 * nkv) * head_dim, "rope_kv_write: qkv_stride too small");
+    dim3 grid(T, nh + 2 * nkv);
+    auto* src = reinterpret_cast<const uint16_t*>(qkv);
+    auto* qo = reinterpret_cast<uint16_t*>(q_out);
+    auto* ko = reinterpret_cast<uint16_t*>(k_out);
+    auto* kcp = reinterpret_cast<uint16_t*>(k_cache);
+    auto* vcp = reinterpret_cast<uint16_t*>(v_cache);
+    if (head_dim == 128)
+        hipLaunchKernelGGL(rope_kv_write_kernel<128>, grid, dim3(64), 0, as_stream(stream), src, qkv_stride,
+                           positions, slot_mapping, cos_sin, nh, nkv, qo, ko, kcp, vcp);
+    else
+        hipLaunchKernelGGL(rope_kv_write_kernel<64>, grid, dim3(64), 0, as_stream(stream), src, qkv_stride,
+                           positions, slot_mapping, cos_sin, nh, nkv, qo, ko, kcp, vcp);
+    return check_launch("rope_kv_write_kernel");
+}
+
+extern "C" size_t skyrl_paged_decode_workspace_bytes(int32_t nseq, int32_t nh, int32_t head_dim, int32_t nparts) {
+    if (nparts <= 1) return 0;
+    const size_t recs = (size_t)(nseq > 0 ? nseq : 1) * (size_t)nh * (size_t)nparts;
+    return recs * ((size_t)head_dim + 2) * sizeof(float);
+}
+
+extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                                  const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens,
+                                  int32_t nseq, int32_t nh, int32_t nkv, int32_t head_dim, float scale,
+                                  int32_t part_tokens, int32_t nparts, void* out, int64_t out_stride, void* workspace,
+                                  void* stream) {
+    SKYRL_REQUIRE(nseq >= 0 && nh > 0 && nkv > 0 && nh % nkv == 0, "paged_decode: bad head counts");
+    SKYRL_REQUIRE(nh / nkv <= 16, "paged_decode: more than 16 query heads per kv head");
+    SKYRL_REQUIRE(head_dim == 64 || head_dim == 128, "paged_decode: head_dim must be 64 or 128");
+    SKYRL_REQUIRE(part_tokens > 0 && part_tokens % kBS == 0, "paged_decode: part_tokens must be a multiple of 16");
+    SKYRL_REQUIRE(nparts >= 1, "paged_decode: nparts must be >= 1");
+    if (nseq == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(q && k_cache && v_cache && block_tables && context_lens && out, "paged_decode: null pointer");
+    SKYRL_REQUIRE(nparts == 1 || workspace, "paged_decode: nparts > 1 needs the workspace");
+    SKYRL_REQUIRE(q_stride >= (int64_t)nh * head_dim && out_stride >= (int64_t)nh * head_dim,
+                  "paged_decode: row stride smaller than nh * head_dim");
+    SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(q) % 16) == 0 && (q_stride % 8) == 0,
+                  "paged_decode: q must be 16-B aligned with a row stride multiple of 8");
+    const float scale_log2 = scale * 1.4426950408889634f;
+    const int qpk = nh / nkv;
+    float* ws_o = reinterpret_cast<float*>(workspace);
+    float* ws_ml = ws_o ? ws_o + (size_t)nseq * nh * nparts * head_dim : nullptr;
+    dim3 grid(nparts, nkv, nseq);
+    auto* qp = reinterpret_cast<const uint16_t*>(q);
+    auto* kp = reinterpret_cast<const uint16_t*>(k_cache);
+    auto* vp = reinterpret_cast<const uint16_t*>(v_cache);
+    auto* op = reinterpret_cast<uint16_t*>(out);
+    if (head_dim == 128)
+        hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(64), 0, as_stream(stream), qp, q_stride, kp, vp,
+                           block_tables, bt_stride, context_lens, nh, nkv, qpk, scale_log2, part_tokens, nparts, op,
+                           out_stride, ws_o, ws_ml);
+    else
+        hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(64), 0, as_stream(stream), qp, q_stride, kp, vp,
+                           block_tables, bt_stride, context_lens, nh, nkv, qpk, scale_log2, part_tokens, nparts, op,
+                           out_stride, ws_o, ws_ml);
+    int rc = check_launch("paged_decode_kernel");
+    if (rc || nparts == 1) return rc;
+    dim3 rgrid(nh, nseq);
+    if (head_dim == 128)
+        hipLaunchKernelGGL(paged_decode_reduce_kernel<128>, rgrid, dim3(128), 0, as_stream(stream), ws_o, ws_ml,
+                           context_lens, nh, part_tokens, nparts, op, out_stride);
+    else
+        hipLaunchKernelGGL(paged_decode_reduce_kernel<64>, rgrid, dim3(64), 0, as_stream(stream), ws_o, ws_ml,
+                           context_lens, nh, part_tokens, nparts, op, out_stride);
+    return check_launch("paged_decode_reduce_kernel");
+}

@@ -1,0 +1,593 @@
+"""MI355X rollout engine: continuous batching over a paged KV cache, behind the reference's
+InferenceEngineInterface.
+
+Replaces vLLM inside the reference's VLLMInferenceEngine / AsyncVLLMInferenceEngine
+(skyrl_train/inference_engines/vllm/vllm_engine.py): same request/response types
+(base.py), vLLM SamplingParams keys (as built by get_vllm_sampling_params,
+inference_engines/utils.py:15-42), finish reasons "stop" / "length" / "abort", and the
+abort semantics pause_generation relies on (inference_engine_client.py:597-628: an aborted
+request returns the tokens generated so far with stop_reason "abort").
+
+Layers:
+  * EngineCore — scheduler: waiting/running queues, block allocation with recompute
+    preemption, stop conditions. Pure host logic over a runner interface (CPU-testable).
+  * ModelRunner — builds the device inputs of one scheduled batch, runs PagedDecoder
+    (prefill or decode) and the HIP sampler (skyrl_sample), returns tokens/logprobs.
+  * AMDInferenceEngine — the async InferenceEngineInterface: generate/sample, abort,
+    sleep/wake_up, weight updates (WeightUpdateRequest + receiver, or named tensors).
+
+Sampling keys: the sampler draws its noise from (seed, key, step); the engine passes
+key = (request key << 20) | response position and step 0, so a request's tokens depend
+only on its own seed/position and logits — not on which other requests share the batch.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import collections
+import itertools
+from dataclasses import dataclass, field
+from typing import Any, Callable, Deque, Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .base import InferenceEngineInput, InferenceEngineInterface, InferenceEngineOutput
+
+BLOCK_SIZE = 16
+_POS_BITS = 20
+
+WAITING, RUNNING, FINISHED = 0, 1, 2
+
+
+@dataclass
+class RequestParams:
+    """Per-request vLLM SamplingParams subset the engine honours (vllm_engine.py:118-124)."""
+
+    max_tokens: int = 16
+    min_tokens: int = 0
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = -1
+    min_p: float = 0.0
+    logprobs: Optional[int] = None
+    stop_token_ids: Tuple[int, ...] = ()
+    ignore_eos: bool = False
+    seed: Optional[int] = None
+
+    _ACCEPTED_NOOP = ("skip_special_tokens", "include_stop_str_in_output", "spaces_between_special_tokens",
+                      "detokenize", "repetition_penalty", "presence_penalty", "frequency_penalty",
+                      "max_completion_tokens")
+
+    @classmethod
+    def from_dict(cls, d: Optional[Dict[str, Any]]) -> "RequestParams":
+        d = dict(d or {})
+        p = cls()
+        if "max_completion_tokens" in d and "max_tokens" not in d:
+            d["max_tokens"] = d["max_completion_tokens"]
+        for k, v in d.items():
+            if k in ("max_tokens", "min_tokens", "top_k", "seed", "logprobs"):
+                if v is not None:
+                    setattr(p, k, int(v))
+                elif k in ("logprobs", "seed"):
+                    setattr(p, k, None)
+            elif k in ("temperature", "top_p", "min_p"):
+                setattr(p, k, float(v) if v is not None else getattr(cls, k))
+            elif k == "stop_token_ids":
+                p.stop_token_ids = tuple(int(x) for x in (v or ()))
+            elif k == "ignore_eos":
+                p.ignore_eos = bool(v)
+            elif k == "stop":
+                if v:
+                    raise ValueError("string stop sequences need a detokenizer; pass stop_token_ids instead")
+            elif k == "n":
+                if v not in (None, 1):
+                    raise ValueError("n > 1 is not supported: replicate prompts (vllm_engine.py:133-136)")
+            elif k in ("repetition_penalty", "presence_penalty", "frequency_penalty"):
+                if v not in (None, 1.0, 0.0):
+                    raise ValueError(f"{k}={v} is not supported by the MI355X sampler")
+            elif k in cls._ACCEPTED_NOOP:
+                continue
+            else:
+                raise ValueError(f"unsupported sampling parameter {k!r}")
+        if p.max_tokens < 1:
+            raise ValueError("max_tokens must be >= 1")
+        if p.temperature < 0:
+            raise ValueError("temperature must be >= 0")
+        return p
+
+    def sampler_key(self) -> Tuple[float, int, float, float]:
+        return (self.temperature, self.top_k, self.top_p, self.min_p)
+
+
+@dataclass
+class Request:
+    rid: int
+    prompt: List[int]
+    params: RequestParams
+    key: int
+    out_tokens: List[int] = field(default_factory=list)
+    out_logprobs: List[float] = field(default_factory=list)
+    blocks: List[int] = field(default_factory=list)
+    state: int = WAITING
+    finish_reason: Optional[str] = None
+    on_finish: Optional[Callable[["Request"], None]] = None
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.prompt) + len(self.out_tokens)
+
+
+class BlockAllocator:
+    """Free list of KV-cache blocks (LIFO: recently freed blocks are reused first)."""
+
+    def __init__(self, num_blocks: int):
+        self.num_blocks = num_blocks
+        self._free: List[int] = list(range(num_blocks - 1, -1, -1))
+
+    @property
+    def num_free(self) -> int:
+        return len(self._free)
+
+    def allocate(self, n: int) -> List[int]:
+        if n > len(self._free):
+            raise RuntimeError("out of KV-cache blocks")
+        out = [self._free.pop() for _ in range(n)]
+        return out
+
+    def free(self, blocks: Iterable[int]) -> None:
+        self._free.extend(reversed(list(blocks)))
+
+
+@dataclass
+class ScheduledBatch:
+    kind: str                       # "prefill" | "decode"
+    requests: List[Request]
+    # per request: (temperature, top_k, top_p, min_p), sampler key, mask-stop flag
+    keys: np.ndarray                # int64 [n]: (key << 20) | response position
+    suppress: List[Tuple[int, ...]]  # stop ids to mask (min_tokens not reached), per request
+
+
+def _blocks_needed(num_tokens: int) -> int:
+    return (num_tokens + BLOCK_SIZE - 1) // BLOCK_SIZE
+
+
+class EngineCore:
+    """Scheduler over a runner with `execute(batch) -> (tokens int64 [n], logprobs f32 [n])`."""
+
+    def __init__(self, runner, num_blocks: int, max_num_seqs: int = 512, max_model_len: int = 4096,
+                 max_prefill_tokens: int = 32768, eos_token_id: Optional[int] = None, seed: int = 0):
+        self.runner = runner
+        self.allocator = BlockAllocator(num_blocks)
+        self.max_num_seqs = max_num_seqs
+        self.max_model_len = max_model_len
+        self.max_prefill_tokens = max_prefill_tokens
+        self.eos_token_id = eos_token_id
+        self.seed = seed
+        self.waiting: Deque[Request] = collections.deque()
+        self.running: List[Request] = []
+        self._rid = itertools.count()
+        self.num_preemptions = 0
+        self.num_steps = 0
+
+    # ---------------------------------------------------------------- requests
+    def add_request(self, prompt: Sequence[int], params: RequestParams,
+                    on_finish: Optional[Callable[[Request], None]] = None) -> Request:
+        prompt = [int(t) for t in prompt]
+        if len(prompt) == 0:
+            raise ValueError("empty prompt")
+        if len(prompt) + 1 > self.max_model_len:
+            raise ValueError(f"prompt of {len(prompt)} tokens exceeds max_model_len={self.max_model_len}")
+        if _blocks_needed(len(prompt) + 1) > self.allocator.num_blocks:
+            raise ValueError("prompt does not fit in the KV cache")
+        rid = next(self._rid)
+        key = (int(params.seed) & ((1 << 42) - 1)) | (1 << 42) if params.seed is not None else rid
+        req = Request(rid=rid, prompt=prompt, params=params, key=key, on_finish=on_finish)
+        self.waiting.append(req)
+        return req
+
+    def has_unfinished(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def abort_all(self) -> List[Request]:
+        """Finish every waiting and running request with stop_reason "abort"."""
+        done = []
+        for r in list(self.running) + list(self.waiting):
+            self._finish(r, "abort")
+            done.append(r)
+        self.running.clear()
+        self.waiting.clear()
+        return done
+
+    def abort(self, rids: Iterable[int]) -> List[Request]:
+        rids = set(rids)
+        done = [r for r in list(self.running) + list(self.waiting) if r.rid in rids]
+        for r in done:
+            self._finish(r, "abort")
+        self.running = [r for r in self.running if r.rid not in rids]
+        self.waiting = collections.deque(r for r in self.waiting if r.rid not in rids)
+        return done
+
+    def _finish(self, r: Request, reason: str) -> None:
+        if r.blocks:
+            self.allocator.free(r.blocks)
+            r.blocks = []
+        r.state = FINISHED
+        r.finish_reason = reason
+        if r.on_finish is not None:
+            r.on_finish(r)
+
+    # ---------------------------------------------------------------- scheduling
+    def _schedule_prefill(self) -> List[Request]:
+        batch: List[Request] = []
+        padded_max = 0
+        while self.waiting and len(self.running) + len(batch) < self.max_num_seqs:
+            r = self.waiting[0]
+            n = r.num_tokens
+            need = _blocks_needed(n + 1)
+            lmax = max(padded_max, n)
+            if batch and lmax * (len(batch) + 1) > self.max_prefill_tokens:
+                break
+            if need > self.allocator.num_free:
+                break
+            self.waiting.popleft()
+            r.blocks = self.allocator.allocate(need)
+            r.state = RUNNING
+            batch.append(r)
+            padded_max = lmax
+        return batch
+
+    def _ensure_decode_blocks(self) -> None:
+        """Every running request needs the block holding position num_tokens-1; preempt the most
+        recently admitted requests (recompute later) while blocks run out."""
+        i = 0
+        while i < len(self.running):
+            r = self.running[i]
+            need = _blocks_needed(r.num_tokens)
+            if need <= len(r.blocks):
+                i += 1
+                continue
+            if self.allocator.num_free > 0:
+                r.blocks.extend(self.allocator.allocate(need - len(r.blocks)))
+                i += 1
+                continue
+            victim = self.running.pop()
+            self.allocator.free(victim.blocks)
+            victim.blocks = []
+            victim.state = WAITING
+            self.waiting.appendleft(victim)
+            self.num_preemptions += 1
+            if victim is r:
+                continue  # r itself was preempted; index i now points past the end or at the next
+        if not self.running and self.waiting and not self.allocator.num_free:
+            raise RuntimeError("KV cache too small for a single request")
+
+    def _keys_and_masks(self, reqs: List[Request]) -> Tuple[np.ndarray, List[Tuple[int, ...]]]:
+        keys = np.fromiter(((r.key << _POS_BITS) | len(r.out_tokens) for r in reqs), dtype=np.int64,
+                           count=len(reqs))
+        sup = []
+        for r in reqs:
+            p = r.params
+            if len(r.out_tokens) < p.min_tokens:
+                ids = set(p.stop_token_ids)
+                if self.eos_token_id is not None and not p.ignore_eos:
+                    ids.add(self.eos_token_id)
+                sup.append(tuple(sorted(ids)))
+            else:
+                sup.append(())
+        return keys, sup
+
+    def step(self) -> List[Request]:
+        """Run one prefill or decode step; returns the requests that finished in it."""
+        self.num_steps += 1
+        batch = self._schedule_prefill()
+        kind = "prefill"
+        if not batch:
+            self._ensure_decode_blocks()
+            batch = list(self.running)
+            kind = "decode"
+            if not batch:
+                return []
+        keys, sup = self._keys_and_masks(batch)
+        tokens, logprobs = self.runner.execute(ScheduledBatch(kind, batch, keys, sup))
+        if kind == "prefill":
+            self.running.extend(batch)
+        finished: List[Request] = []
+        for r, t, lp in zip(batch, tokens.tolist(), logprobs.tolist()):
+            r.out_tokens.append(t)
+            r.out_logprobs.append(lp)
+            reason = self._stop_reason(r, t)
+            if reason is not None:
+                finished.append(r)
+                self._finish(r, reason)
+        if finished:
+            done = {id(r) for r in finished}
+            self.running = [r for r in self.running if id(r) not in done]
+        return finished
+
+    def _stop_reason(self, r: Request, tok: int) -> Optional[str]:
+        p = r.params
+        n = len(r.out_tokens)
+        if n >= p.min_tokens:
+            if tok in p.stop_token_ids:
+                return "stop"
+            if not p.ignore_eos and self.eos_token_id is not None and tok == self.eos_token_id:
+                return "stop"
+        if n >= p.max_tokens or r.num_tokens >= self.max_model_len:
+            return "length"
+        return None
+
+
+class ModelRunner:
+    """Device side of one scheduled batch: PagedDecoder forward + lm_head + HIP sampler."""
+
+    def __init__(self, model, num_blocks: int, max_num_seqs: int, seed: int = 0):
+        import torch
+
+        from . import model as model_mod
+
+        self.torch = torch
+        self.model = model
+        self.device = model.device
+        self.seed = int(seed)
+        s = model.spec
+        self.cache = model_mod.PagedKVCache(s.num_layers, num_blocks, s.num_kv_heads, s.head_dim, self.device)
+        self.max_blocks = _blocks_needed(model.max_model_len)
+        self.max_num_seqs = max_num_seqs
+        self._sampler_ws = None
+
+    def release_cache(self):
+        self.cache = None
+
+    def ensure_cache(self, num_blocks: int):
+        if self.cache is None:
+            from .model import PagedKVCache
+
+            s = self.model.spec
+            self.cache = PagedKVCache(s.num_layers, num_blocks, s.num_kv_heads, s.head_dim, self.device)
+
+    def _h2d(self, arr: np.ndarray):
+        t = self.torch.from_numpy(arr)
+        return t.pin_memory().to(self.device, non_blocking=True)
+
+    def execute(self, batch: ScheduledBatch):
+        torch = self.torch
+        from .model import StepInputs
+
+        reqs = batch.requests
+        n = len(reqs)
+        if batch.kind == "prefill":
+            seqs = [r.prompt + r.out_tokens for r in reqs]
+            lens = [len(s) for s in seqs]
+            tok = np.fromiter(itertools.chain.from_iterable(seqs), dtype=np.int64, count=sum(lens))
+            pos = np.concatenate([np.arange(L, dtype=np.int64) for L in lens])
+            slots = np.concatenate([_slots(r.blocks, 0, L) for r, L in zip(reqs, lens)])
+            packed = self._h2d(np.concatenate([tok, pos, slots]))
+            T = tok.shape[0]
+            inp = StepInputs(tokens=packed[:T], positions=packed[T:2 * T], slots=packed[2 * T:], seq_lens=lens)
+            hidden = self.model.forward_prefill(inp, self.cache)
+        else:
+            L = np.fromiter((r.num_tokens for r in reqs), dtype=np.int64, count=n)
+            tok = np.fromiter((r.out_tokens[-1] for r in reqs), dtype=np.int64, count=n)
+            pos = L - 1
+            slots = np.fromiter((r.blocks[(p // BLOCK_SIZE)] * BLOCK_SIZE + p % BLOCK_SIZE
+                                 for r, p in zip(reqs, pos.tolist())), dtype=np.int64, count=n)
+            max_ctx = int(L.max())
+            nbt = _blocks_needed(max_ctx)
+            bt = np.zeros((n, nbt + 1), dtype=np.int32)  # column 0: context length, then the table
+            bt[:, 0] = L
+            for i, r in enumerate(reqs):
+                b = r.blocks[:nbt]
+                bt[i, 1:1 + len(b)] = b
+            packed = self._h2d(np.concatenate([tok, pos, slots]))
+            bt_d = self._h2d(bt)
+            inp = StepInputs(tokens=packed[:n], positions=packed[n:2 * n], slots=packed[2 * n:],
+                             block_tables=bt_d[:, 1:], context_lens=bt_d[:, 0].contiguous(), max_ctx=max_ctx)
+            hidden = self.model.forward_decode(inp, self.cache)
+        logits = self.model.logits(hidden)
+        return self._sample(logits, batch)
+
+    def _sample(self, logits, batch: ScheduledBatch):
+        torch = self.torch
+        from .. import _ffi
+        from ..ops import _ptr, _stream
+
+        n, V = logits.shape
+        for i, ids in enumerate(batch.suppress):
+            if ids:
+                logits[i, list(ids)] = float("-inf")
+        keys = self._h2d(batch.keys)
+        tokens = torch.empty(n, dtype=torch.int32, device=self.device)
+        lps = torch.empty(n, dtype=torch.float32, device=self.device)
+        groups: Dict[Tuple, List[int]] = {}
+        for i, r in enumerate(batch.requests):
+            groups.setdefault(r.params.sampler_key(), []).append(i)
+        ws_bytes = _ffi.query("skyrl_sample_workspace_bytes", max(n, self.max_num_seqs), V)
+        if self._sampler_ws is None or self._sampler_ws.numel() < ws_bytes:
+            self._sampler_ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
+        st = _stream(self.device)
+        for (temp, top_k, top_p, min_p), rows in groups.items():
+            if len(rows) == n:
+                lg, ky, to, lo = logits, keys, tokens, lps
+            else:
+                idx = torch.tensor(rows, dtype=torch.int64, device=self.device)
+                lg, ky = logits.index_select(0, idx), keys.index_select(0, idx)
+                to = torch.empty(len(rows), dtype=torch.int32, device=self.device)
+                lo = torch.empty(len(rows), dtype=torch.float32, device=self.device)
+            _ffi.call("skyrl_sample", _ptr(lg), _ffi.BF16, lg.stride(0), lg.shape[0], V, float(temp), int(top_k),
+                      float(top_p), float(min_p), self.seed & 0xFFFFFFFFFFFFFFFF, _ptr(ky), 0, _ptr(to), _ptr(lo),
+                      _ptr(self._sampler_ws), st)
+            if len(rows) != n:
+                tokens.index_copy_(0, idx, to)
+                lps.index_copy_(0, idx, lo)
+        out = torch.stack([tokens.to(torch.float64), lps.to(torch.float64)]).cpu().numpy()
+        return out[0].astype(np.int64), out[1].astype(np.float32)
+
+
+def _slots(blocks: List[int], start: int, end: int) -> np.ndarray:
+    p = np.arange(start, end, dtype=np.int64)
+    b = np.asarray(blocks, dtype=np.int64)
+    return b[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
+
+
+class AMDInferenceEngine(InferenceEngineInterface):
+    """One rollout engine on one GPU (tp = pp = dp = 1), asyncio-driven.
+
+    `model` is a PagedDecoder; `num_blocks` sizes the KV cache (default: ``kv_cache_fraction``
+    of the free HBM after weights). Decoding runs in a background task while any request is
+    unfinished; each step is one prefill or decode batch of every running request."""
+
+    def __init__(self, model, num_blocks: Optional[int] = None, max_num_seqs: int = 512,
+                 max_prefill_tokens: int = 32768, seed: int = 0, kv_cache_fraction: float = 0.5,
+                 tokenizer=None, runner=None):
+        self.model = model
+        self.tokenizer = tokenizer
+        if num_blocks is None:
+            import torch
+
+            from .model import PagedKVCache
+
+            free, _ = torch.cuda.mem_get_info(model.device)
+            s = model.spec
+            num_blocks = int(free * kv_cache_fraction) // PagedKVCache.bytes_per_block(
+                s.num_layers, s.num_kv_heads, s.head_dim)
+        self.num_blocks = num_blocks
+        self.runner = runner if runner is not None else ModelRunner(model, num_blocks, max_num_seqs, seed)
+        self.core = EngineCore(self.runner, num_blocks, max_num_seqs=max_num_seqs,
+                               max_model_len=model.max_model_len, max_prefill_tokens=max_prefill_tokens,
+                               eos_token_id=model.spec.eos_token_id, seed=seed)
+        self._task: Optional[asyncio.Task] = None
+        self._futures: Dict[int, asyncio.Future] = {}
+        self._receiver = None
+        self._offloaded = None
+
+    # ---------------------------------------------------------------- generation
+    def _decode_text(self, ids: List[int]) -> str:
+        if self.tokenizer is None:
+            return ""
+        return self.tokenizer.decode(ids, skip_special_tokens=True)
+
+    def _submit(self, prompt: List[int], params: RequestParams) -> asyncio.Future:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+
+        def done(r: Request, fut=fut):
+            self._futures.pop(r.rid, None)
+            if not fut.done():
+                fut.set_result(r)
+
+        req = self.core.add_request(prompt, params, on_finish=done)
+        self._futures[req.rid] = fut
+        if self._task is None or self._task.done():
+            self._task = loop.create_task(self._run())
+        return fut
+
+    async def _run(self):
+        try:
+            while self.core.has_unfinished():
+                self.core.step()
+                await asyncio.sleep(0)
+        except BaseException as e:  # fail every pending request instead of hanging it
+            for fut in list(self._futures.values()):
+                if not fut.done():
+                    fut.set_exception(e)
+            self._futures.clear()
+            self.core.abort_all()
+            raise
+
+    def _output(self, reqs: List[Request], want_logprobs: bool) -> InferenceEngineOutput:
+        return InferenceEngineOutput(
+            responses=[self._decode_text(r.out_tokens) for r in reqs],
+            stop_reasons=[r.finish_reason for r in reqs],
+            response_ids=[list(r.out_tokens) for r in reqs],
+            response_logprobs=[list(r.out_logprobs) for r in reqs] if want_logprobs else None,
+        )
+
+    async def generate(self, input_batch: InferenceEngineInput) -> InferenceEngineOutput:
+        prompts = input_batch.get("prompts")
+        ids = input_batch.get("prompt_token_ids")
+        if prompts is not None or ids is None:
+            raise ValueError("AMDInferenceEngine only accepts `prompt_token_ids`, not `prompts` "
+                             "(vllm_engine.py:112-114)")
+        params = RequestParams.from_dict(input_batch.get("sampling_params"))
+        futs = [self._submit(p, params) for p in ids]
+        reqs = await asyncio.gather(*futs)
+        return self._output(list(reqs), params.logprobs is not None)
+
+    async def sample(self, prompt_token_ids: List[int], num_samples: int,
+                     sampling_params: Dict[str, Any]) -> InferenceEngineOutput:
+        """All num_samples requests go into the batch at once (independent keys per request)."""
+        return await self.generate({"prompt_token_ids": [list(prompt_token_ids)] * num_samples,
+                                    "sampling_params": sampling_params})
+
+    async def abort_generation(self) -> None:
+        self.core.abort_all()
+
+    async def chat_completion(self, request_payload: Dict[str, Any]) -> Dict[str, Any]:
+        raise NotImplementedError("OpenAI HTTP endpoints are out of scope for the MI355X engine")
+
+    async def completion(self, request_payload: Dict[str, Any]) -> Dict[str, Any]:
+        raise NotImplementedError("OpenAI HTTP endpoints are out of scope for the MI355X engine")
+
+    # ---------------------------------------------------------------- memory
+    async def sleep(self, *args: Any, **kwargs: Any):
+        """level 1: offload weights to host and free the KV cache; level 2: discard weights too
+        (they come back through update_named_weights) — vllm_engine.py sleep()."""
+        if self.core.has_unfinished():
+            self.core.abort_all()
+        level = kwargs.get("level", 2)
+        self.runner.release_cache()
+        if level == 1:
+            self._offloaded = [(n, t.detach().to("cpu")) for n, t in self.model.hf_named_tensors()]
+        self.model.release()
+
+    async def wake_up(self, *args: Any, **kwargs: Any):
+        tags = kwargs.get("tags") or ["weights", "kv_cache"]
+        if "weights" in tags and not self.model.layers:
+            self.model._alloc(seed=None)
+            if self._offloaded is not None:
+                self.model.load_weights(self._offloaded)
+                self._offloaded = None
+        if "kv_cache" in tags:
+            self.runner.ensure_cache(self.num_blocks)
+
+    # ---------------------------------------------------------------- weights
+    async def init_weight_update_communicator(self, init_info):
+        """init_info: a ready receiver (has `receive_weights(request)`), or a dict with
+        {"group", "src"} for a broadcast receiver (broadcast_strategy.py:173-191)."""
+        if hasattr(init_info, "receive_weights"):
+            self._receiver = init_info
+        else:
+            from ..comm import BroadcastWeightReceiver
+
+            info = dict(init_info or {})
+            self._receiver = BroadcastWeightReceiver(self.model.dtype, group=info.get("group"),
+                                                     src=info.get("src", 0), device=self.model.device)
+
+    async def update_named_weights(self, request):
+        """request: a WeightUpdateRequest (data through the receiver), or a dict / object with
+        `names` and `tensors` (colocated path: CUDA-IPC handles resolved by the caller)."""
+        tensors = request.get("tensors") if isinstance(request, dict) else getattr(request, "tensors", None)
+        names = request["names"] if isinstance(request, dict) else request.names
+        if tensors is not None:
+            n = self.model.load_weights(zip(names, tensors))
+        else:
+            if self._receiver is None:
+                raise RuntimeError("init_weight_update_communicator was not called")
+            n = self.model.load_weights(self._receiver.receive_weights(request))
+        return n
+
+    async def reset_prefix_cache(self):
+        return None  # no prefix cache: every prompt is prefilled
+
+    async def teardown(self):
+        self.core.abort_all()
+        self.runner.release_cache()
+
+    def tp_size(self) -> int:
+        return 1
+
+    def pp_size(self) -> int:
+        return 1
+
+    def dp_size(self) -> int:
+        return 1

@@ -1,0 +1,105 @@
+"""Host launchers of the decode-loop kernels (csrc/attention.hip) through the C ABI.
+
+The rollout engine calls these once per layer per step; they check shapes on the host
+before any launch (a wrong stride would otherwise read out of bounds on the device) and
+raise if the HIP library is missing — there is no CPU fallback on the product path.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import _ffi
+from ..ops import _ptr, _require_gpu, _stream
+
+BLOCK_SIZE = 16  # tokens per KV-cache block (the kernels' fixed tile)
+
+
+def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, slot_mapping: torch.Tensor, cos_sin: torch.Tensor,
+                  nh: int, nkv: int, head_dim: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                  q_out: Optional[torch.Tensor] = None, k_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rotate q/k of the fused projection ``qkv`` [T, (nh+2nkv)*D] (bf16, unit last stride),
+    write k/v into one layer's paged cache at ``slot_mapping`` and return rotated q [T, nh, D]."""
+    dev = _require_gpu(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache)
+    T = qkv.shape[0]
+    width = (nh + 2 * nkv) * head_dim
+    if qkv.dtype != torch.bfloat16 or qkv.dim() != 2 or qkv.shape[1] != width or qkv.stride(1) != 1:
+        raise ValueError(f"qkv must be bf16 [T, {width}] with unit column stride, got {tuple(qkv.shape)}")
+    if positions.dtype != torch.int64 or slot_mapping.dtype != torch.int64 or positions.numel() != T \
+            or slot_mapping.numel() != T:
+        raise ValueError("positions and slot_mapping must be int64 [T]")
+    if cos_sin.dtype != torch.float32 or cos_sin.dim() != 2 or cos_sin.shape[1] != head_dim:
+        raise ValueError(f"cos_sin must be f32 [max_pos, {head_dim}]")
+    nb = k_cache.shape[0]
+    if k_cache.shape != (nb, nkv, BLOCK_SIZE, head_dim) or v_cache.shape != (nb, nkv, head_dim, BLOCK_SIZE) \
+            or not (k_cache.is_contiguous() and v_cache.is_contiguous()):
+        raise ValueError("k_cache must be [blocks, nkv, 16, D] and v_cache [blocks, nkv, D, 16], contiguous")
+    if q_out is None:
+        q_out = torch.empty((T, nh, head_dim), dtype=torch.bfloat16, device=dev)
+    if k_out is not None and (k_out.shape != (T, nkv, head_dim) or not k_out.is_contiguous()):
+        raise ValueError("k_out must be contiguous [T, nkv, D]")
+    _ffi.call("skyrl_rope_kv_write", _ptr(qkv), qkv.stride(0), T, nh, nkv, head_dim, _ptr(positions),
+              _ptr(slot_mapping), _ptr(cos_sin), _ptr(q_out), _ptr(k_out), _ptr(k_cache), _ptr(v_cache), _stream(dev))
+    return q_out
+
+
+def choose_partition(nseq: int, nkv: int, max_ctx: int, target_waves: int = 2048) -> int:
+    """Context tokens per decode wave: the largest of 512/256/128/64 that still gives about
+    ``target_waves`` waves (256 CUs x 8), so small batches split long contexts."""
+    for part in (512, 256, 128):
+        if nseq * nkv * math.ceil(max(max_ctx, 1) / part) >= target_waves:
+            return part
+    return 64
+
+
+class DecodeWorkspace:
+    """Grows-only fp32 scratch for the partition merge (reused every layer and step)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = torch.empty(0, dtype=torch.uint8, device=self.device)
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(nbytes, 2 * self.buf.numel()), dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                 context_lens: torch.Tensor, max_ctx: int, scale: float, out: Optional[torch.Tensor] = None,
+                 workspace: Optional[DecodeWorkspace] = None, part_tokens: Optional[int] = None) -> torch.Tensor:
+    """softmax(scale * q K^T) V for one query token per sequence over its paged context.
+
+    q: bf16 [n, nh, D]; block_tables: int32 [n, max_blocks]; context_lens: int32 [n] (>= 1,
+    <= max_ctx, and max_blocks * 16 >= max_ctx). Returns bf16 [n, nh, D]."""
+    dev = _require_gpu(q, k_cache, v_cache, block_tables, context_lens)
+    n, nh, D = q.shape
+    nb, nkv = k_cache.shape[0], k_cache.shape[1]
+    if q.dtype != torch.bfloat16 or q.stride(2) != 1 or q.stride(1) != D:
+        raise ValueError("q must be bf16 [n, nh, D] with contiguous heads")
+    if k_cache.shape != (nb, nkv, BLOCK_SIZE, D) or v_cache.shape != (nb, nkv, D, BLOCK_SIZE):
+        raise ValueError("cache shapes do not match q")
+    if block_tables.dtype != torch.int32 or block_tables.dim() != 2 or block_tables.shape[0] != n \
+            or block_tables.stride(1) != 1:
+        raise ValueError("block_tables must be int32 [n, max_blocks] with unit column stride")
+    if context_lens.dtype != torch.int32 or context_lens.numel() != n or not context_lens.is_contiguous():
+        raise ValueError("context_lens must be contiguous int32 [n]")
+    if block_tables.shape[1] * BLOCK_SIZE < max_ctx:
+        raise ValueError("block_tables too narrow for max_ctx")
+    if out is None:
+        out = torch.empty((n, nh, D), dtype=torch.bfloat16, device=dev)
+    if n == 0:
+        return out
+    part = part_tokens or choose_partition(n, nkv, max_ctx)
+    nparts = max(1, math.ceil(max_ctx / part))
+    ws = None
+    if nparts > 1:
+        nbytes = _ffi.query("skyrl_paged_decode_workspace_bytes", n, nh, D, nparts)
+        ws = (workspace or DecodeWorkspace(dev)).get(nbytes)
+    _ffi.call("skyrl_paged_decode", _ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
+              block_tables.stride(0), _ptr(context_lens), n, nh, nkv, D, float(scale), part, nparts, _ptr(out),
+              out.stride(0), _ptr(ws), _stream(dev))
+    return out

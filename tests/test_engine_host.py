@@ -1,0 +1,237 @@
+"""Rollout engine host logic on CPU: scheduler, block allocation and recompute preemption,
+stop conditions, abort, the async InferenceEngineInterface and the client's pause/resume retry
+(inference_engines/inference_engine_client.py:223-330,597-628). The device runner is replaced
+by a deterministic fake whose next token is a function of the whole token history, so any
+scheduling error (lost tokens, wrong positions after preemption) changes the outputs."""
+
+import asyncio
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from skyrl_amd.inference_engines.client import InferenceEngineClient, route_prompts_to_engines
+from skyrl_amd.inference_engines.engine import BLOCK_SIZE, AMDInferenceEngine, EngineCore, RequestParams
+
+V = 97
+
+
+def next_token(history, suppress=()):
+    t = (sum((i + 1) * x for i, x in enumerate(history)) * 31 + 7) % V
+    while t in suppress:
+        t = (t + 1) % V
+    return t
+
+
+class FakeRunner:
+    def __init__(self, num_blocks):
+        self.owner = {}  # block -> rid, to catch double allocation
+        self.batches = []
+        self.num_blocks = num_blocks
+
+    def execute(self, batch):
+        self.batches.append((batch.kind, len(batch.requests)))
+        seen = {}
+        for r in batch.requests:
+            need = (r.num_tokens + (1 if batch.kind == "prefill" else 0) + BLOCK_SIZE - 1) // BLOCK_SIZE
+            assert len(r.blocks) >= min(need, (r.num_tokens + BLOCK_SIZE - 1) // BLOCK_SIZE)
+            for b in r.blocks:
+                assert 0 <= b < self.num_blocks
+                assert seen.setdefault(b, r.rid) == r.rid, "block shared by two running requests"
+        toks = np.array([next_token(r.prompt + r.out_tokens, sup) for r, sup in zip(batch.requests, batch.suppress)],
+                        dtype=np.int64)
+        lps = -np.arange(len(toks), dtype=np.float32) / 10
+        return toks, lps
+
+    def release_cache(self):
+        pass
+
+    def ensure_cache(self, n):
+        pass
+
+
+def run_all(core):
+    while core.has_unfinished():
+        core.step()
+
+
+def reference_output(prompt, params, eos=None):
+    out = []
+    while True:
+        sup = ()
+        if len(out) < params.min_tokens:
+            sup = tuple(sorted(set(params.stop_token_ids) | ({eos} if eos is not None else set())))
+        t = next_token(prompt + out, sup)
+        out.append(t)
+        if len(out) >= params.min_tokens and (t in params.stop_token_ids or t == eos):
+            return out, "stop"
+        if len(out) >= params.max_tokens:
+            return out, "length"
+
+
+def test_request_params_parse():
+    p = RequestParams.from_dict({"max_tokens": 8, "min_tokens": 1, "temperature": 0.7, "top_p": 0.9, "top_k": 50,
+                                 "min_p": 0.0, "logprobs": 0, "stop": None, "skip_special_tokens": True,
+                                 "include_stop_str_in_output": True})
+    assert (p.max_tokens, p.min_tokens, p.top_k, p.logprobs) == (8, 1, 50, 0)
+    with pytest.raises(ValueError):
+        RequestParams.from_dict({"n": 2})
+    with pytest.raises(ValueError):
+        RequestParams.from_dict({"stop": ["\n"]})
+    with pytest.raises(ValueError):
+        RequestParams.from_dict({"bogus": 1})
+
+
+@pytest.mark.parametrize("num_blocks", [400, 12])
+def test_scheduler_outputs_independent_of_cache_pressure(num_blocks):
+    """With 12 blocks the running set must be preempted and recomputed repeatedly; outputs must
+    equal the unconstrained sequential answer."""
+    rng = np.random.default_rng(0)
+    runner = FakeRunner(num_blocks)
+    core = EngineCore(runner, num_blocks, max_num_seqs=6, max_model_len=200, max_prefill_tokens=64,
+                      eos_token_id=3)
+    reqs, expect = [], []
+    for i in range(10):
+        prompt = rng.integers(0, V, size=int(rng.integers(1, 30))).tolist()
+        params = RequestParams(max_tokens=int(rng.integers(1, 40)), min_tokens=int(rng.integers(0, 3)),
+                               stop_token_ids=(5,))
+        reqs.append(core.add_request(prompt, params))
+        expect.append(reference_output(prompt, params, eos=3))
+    run_all(core)
+    for r, (toks, reason) in zip(reqs, expect):
+        assert r.out_tokens == toks and r.finish_reason == reason
+    assert core.allocator.num_free == num_blocks
+    if num_blocks == 12:
+        assert core.num_preemptions > 0
+    kinds = {k for k, _ in runner.batches}
+    assert kinds == {"prefill", "decode"}
+    assert max(n for _, n in runner.batches) <= 6
+
+
+def test_max_model_len_and_validation():
+    core = EngineCore(FakeRunner(100), 100, max_model_len=20)
+    with pytest.raises(ValueError):
+        core.add_request(list(range(20)), RequestParams(max_tokens=5))
+    with pytest.raises(ValueError):
+        core.add_request([], RequestParams())
+    r = core.add_request(list(range(15)), RequestParams(max_tokens=50, ignore_eos=True))
+    run_all(core)
+    assert r.finish_reason == "length" and r.num_tokens == 20
+
+
+def test_abort_returns_partial_tokens():
+    core = EngineCore(FakeRunner(100), 100, max_num_seqs=1)
+    a = core.add_request([1, 2, 3], RequestParams(max_tokens=50, ignore_eos=True))
+    b = core.add_request([4, 5], RequestParams(max_tokens=50, ignore_eos=True))
+    for _ in range(4):
+        core.step()
+    core.abort_all()
+    assert a.finish_reason == "abort" and len(a.out_tokens) == 4
+    assert b.finish_reason == "abort" and b.out_tokens == []  # was waiting (max_num_seqs=1)
+    assert core.allocator.num_free == 100 and not core.has_unfinished()
+
+
+def fake_engine(num_blocks=200, max_num_seqs=8, eos=None, max_model_len=256):
+    model = SimpleNamespace(max_model_len=max_model_len, spec=SimpleNamespace(eos_token_id=eos))
+    return AMDInferenceEngine(model, num_blocks=num_blocks, max_num_seqs=max_num_seqs,
+                              runner=FakeRunner(num_blocks))
+
+
+def test_async_generate_and_sample():
+    eng = fake_engine(eos=3)
+    prompts = [[1, 2], [3, 4, 5], [6]]
+    sp = {"max_tokens": 10, "min_tokens": 1, "logprobs": 0}
+    out = asyncio.run(eng.generate({"prompt_token_ids": prompts, "sampling_params": sp}))
+    for p, ids, reason in zip(prompts, out["response_ids"], out["stop_reasons"]):
+        exp, er = reference_output(p, RequestParams.from_dict(sp), eos=3)
+        assert ids == exp and reason == er
+    assert len(out["response_logprobs"]) == 3 and len(out["response_logprobs"][0]) == len(out["response_ids"][0])
+    out2 = asyncio.run(eng.generate({"prompt_token_ids": prompts, "sampling_params": {"max_tokens": 2}}))
+    assert out2["response_logprobs"] is None
+    s = asyncio.run(eng.sample([1, 2], 3, {"max_tokens": 4}))
+    assert len(s["response_ids"]) == 3
+    with pytest.raises(ValueError):
+        asyncio.run(eng.generate({"prompts": [[{"role": "user", "content": "x"}]], "prompt_token_ids": None}))
+
+
+def test_concurrent_generate_calls_share_the_engine():
+    eng = fake_engine(max_num_seqs=4)
+
+    async def main():
+        calls = [eng.generate({"prompt_token_ids": [[i, i + 1]], "sampling_params": {"max_tokens": 6 + i}})
+                 for i in range(7)]
+        return await asyncio.gather(*calls)
+
+    outs = asyncio.run(main())
+    for i, o in enumerate(outs):
+        exp, _ = reference_output([i, i + 1], RequestParams(max_tokens=6 + i))
+        assert o["response_ids"][0] == exp
+
+
+def test_route_prompts_to_engines():
+    assert route_prompts_to_engines(5, 2, None) == {0: [0, 1, 2], 1: [3, 4]}
+    r = route_prompts_to_engines(4, 3, ["a", "b", "a", 7])
+    assert sorted(i for v in r.values() for i in v) == [0, 1, 2, 3]
+    assert [k for k, v in r.items() if 0 in v] == [k for k, v in r.items() if 2 in v]
+    assert len(route_prompts_to_engines(1, 4, None)) == 1
+
+
+def test_client_pause_abort_resume_retry():
+    """A single-prompt generate() interrupted by pause_generation returns the same tokens as
+    an uninterrupted one: the aborted partial is resent as prompt + accumulated tokens."""
+    eng = fake_engine()
+    client = InferenceEngineClient([eng], abort_grace_seconds=0.0)
+    sp = {"max_tokens": 40, "logprobs": 0, "ignore_eos": True}
+    exp, _ = reference_output([9, 8, 7], RequestParams.from_dict(sp))
+
+    async def main():
+        task = asyncio.create_task(client.generate({"prompt_token_ids": [[9, 8, 7]], "sampling_params": sp}))
+        for _ in range(10):
+            await asyncio.sleep(0)
+        await client.pause_generation()
+        assert eng.core.num_steps > 0
+        await asyncio.sleep(0.01)
+        await client.resume_generation()
+        return await task
+
+    out = asyncio.run(main())
+    assert out["response_ids"][0] == exp and out["stop_reasons"] == ["length"]
+    assert len(out["response_logprobs"][0]) == 40
+    with pytest.raises(RuntimeError):
+        asyncio.run(client.resume_generation())
+
+
+def test_client_batched_generate_over_two_engines():
+    engines = [fake_engine(), fake_engine()]
+    client = InferenceEngineClient(engines)
+    prompts = [[i, 2 * i + 1] for i in range(5)]
+    out = asyncio.run(client.generate({"prompt_token_ids": prompts, "sampling_params": {"max_tokens": 5}}))
+    for p, ids in zip(prompts, out["response_ids"]):
+        assert ids == reference_output(p, RequestParams(max_tokens=5))[0]
+    assert client.dp_size() == 2
+
+
+def test_decoder_hf_weight_names_round_trip():
+    """PagedDecoder stores q/k/v and gate/up fused; HF state-dict names load into the right
+    slices and come back out unchanged (host-side mapping only, CPU tensors)."""
+    import torch
+    from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from skyrl_amd.inference_engines.model import PagedDecoder
+
+    cfg = Qwen2Config(vocab_size=101, hidden_size=256, intermediate_size=384, num_hidden_layers=2,
+                      num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=64,
+                      tie_word_embeddings=True)
+    torch.manual_seed(0)
+    hf = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    sd = {k: v + 0.01 * torch.randn_like(v) for k, v in hf.state_dict().items()}
+    m = PagedDecoder(cfg, "cpu", seed=None)
+    assert m.load_weights(sd.items()) == len(sd) - 1  # tied lm_head is skipped, as vLLM does
+    ours = dict(m.hf_named_tensors())
+    for k, v in sd.items():
+        if k != "lm_head.weight":
+            assert torch.equal(ours[k], v), k
+    with pytest.raises(KeyError):
+        m.load_weights([("model.layers.9.mlp.up_proj.weight", sd["model.layers.0.mlp.up_proj.weight"])])
+    with pytest.raises(ValueError):
+        m.load_weights([("model.norm.weight", torch.zeros(3))])
