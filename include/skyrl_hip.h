@@ -315,9 +315,11 @@ int skyrl_cast_bf16(const float* x, void* y, int64_t n, void* stream);
  *                        cos_sin f32 [max_pos, head_dim] = cos | sin halves.
  *   skyrl_paged_decode   one query token per sequence: out[s] = softmax(scale q.K^T) V over
  *                        context_lens[s] >= 1 cached tokens listed by block_tables
- *                        i32 [nseq, bt_stride]; nh/nkv <= 16. The context is split into
- *                        nparts partitions of part_tokens (multiple of 16; nparts *
- *                        part_tokens >= max context); nparts > 1 needs
+ *                        i32 [nseq, bt_stride]; nh/nkv <= 16. Each sequence's context is
+ *                        split over at most nparts waves per kv head, each partition at
+ *                        least part_tokens (a multiple of 16) tokens, decided on device
+ *                        from context_lens (so a fixed launch fits any context);
+ *                        nparts > 1 needs
  *                        skyrl_paged_decode_workspace_bytes(nseq, nh, head_dim, nparts). */
 int skyrl_rope_kv_write(const void* qkv, int64_t qkv_stride, int32_t T, int32_t nh, int32_t nkv, int32_t head_dim,
                         const int64_t* positions, const int64_t* slot_mapping, const float* cos_sin, void* q_out,
@@ -327,6 +329,14 @@ int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, con
                        const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens, int32_t nseq,
                        int32_t nh, int32_t nkv, int32_t head_dim, float scale, int32_t part_tokens, int32_t nparts,
                        void* out, int64_t out_stride, void* workspace, void* stream);
+/* Decoder-layer glue (HF Qwen2DecoderLayer/LlamaDecoderLayer), bf16 [n, H] rows:
+ *   skyrl_add_rmsnorm  hidden = bf16(hidden + delta) (delta may be NULL), then
+ *                      out = bf16(weight * bf16(hidden * rsqrt(mean(hidden^2) + eps)));
+ *                      H % 4 == 0, H <= 8192.
+ *   skyrl_silu_mul     out [n, I] = bf16(bf16(silu(gate)) * up) of gate_up [n, 2I]. */
+int skyrl_add_rmsnorm(const void* delta, void* hidden, const void* weight, int32_t n, int32_t H, float eps, void* out,
+                      void* stream);
+int skyrl_silu_mul(const void* gate_up, int64_t n, int32_t I, void* out, void* stream);
 
 #ifdef __cplusplus
 }

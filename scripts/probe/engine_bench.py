@@ -48,9 +48,10 @@ def attn_bench(nseq, ctx, nh, nkv, D=128, reps=20):
     out = torch.empty_like(q)
     ws = kernels.DecodeWorkspace(DEV)
     res = {}
-    for part in (None, 256, 512):
+    auto = kernels.choose_nparts(nseq, nkv, ctx)
+    for nparts in sorted({auto, max(1, auto // 2), 2 * auto}):
         f = lambda: kernels.paged_decode(q, kc, vc, bt, cl, ctx, 1 / math.sqrt(D), out=out, workspace=ws,  # noqa
-                                         part_tokens=part)
+                                         nparts=nparts)
         f()
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -61,7 +62,7 @@ def attn_bench(nseq, ctx, nh, nkv, D=128, reps=20):
         b.synchronize()
         us = a.elapsed_time(b) * 1e3 / reps
         nbytes = nseq * ctx * nkv * D * 2 * 2 + 2 * nseq * nh * D * 2
-        res[str(part or kernels.choose_partition(nseq, nkv, ctx))] = {
+        res[f"nparts={nparts}" + (" (auto)" if nparts == auto else "")] = {
             "us": round(us, 2), "GBps": round(nbytes / (us * 1e-6) / 1e9, 1), "bytes": nbytes}
     return res
 
@@ -106,7 +107,7 @@ def decode_step_bench(nseq, ctx, layers, reps=10):
     return {"nseq": nseq, "ctx": ctx, "layers": layers, "eager_ms": round(eager_ms, 3), "graph_ms": round(graph_ms, 3)}
 
 
-def engine_bench(nprompts, max_tokens, layers):
+def engine_bench(nprompts, max_tokens, layers, use_graphs=True):
     from skyrl_amd.inference_engines.engine import AMDInferenceEngine
     from skyrl_amd.inference_engines.model import PagedDecoder
 
@@ -118,10 +119,12 @@ def engine_bench(nprompts, max_tokens, layers):
     g = torch.Generator().manual_seed(1234)
     lens = torch.randint(16, 513, (nprompts,), generator=g).tolist()
     prompts = [torch.randint(0, cfg.vocab_size, (L,), generator=g).tolist() for L in lens]
-    eng = AMDInferenceEngine(model, num_blocks=None, max_num_seqs=nprompts, kv_cache_fraction=0.3)
+    eng = AMDInferenceEngine(model, num_blocks=None, max_num_seqs=nprompts, kv_cache_fraction=0.3,
+                             use_graphs=use_graphs)
     sp = {"temperature": 1.0, "max_tokens": max_tokens, "ignore_eos": True, "logprobs": 0}
-    # warm-up (one short generate)
-    asyncio.run(eng.generate({"prompt_token_ids": prompts[:8], "sampling_params": {"max_tokens": 4}}))
+    # warm-up: the full batch for a few tokens captures the decode graph of its bucket
+    asyncio.run(eng.generate({"prompt_token_ids": prompts, "sampling_params": {"max_tokens": 3}}))
+    eng.core.stats.clear()
     torch.cuda.synchronize()
     steps0 = eng.core.num_steps
     t0 = time.time()
@@ -134,7 +137,8 @@ def engine_bench(nprompts, max_tokens, layers):
             "kv_blocks": eng.num_blocks, "seconds": round(dt, 3), "generated_tokens": ntok,
             "tokens_per_s": round(ntok / dt, 1), "engine_steps": steps,
             "ms_per_step": round(dt / steps * 1e3, 3), "preemptions": eng.core.num_preemptions,
-            "init_s": round(init_s, 2)}
+            "init_s": round(init_s, 2), "graphs": use_graphs,
+            "stats": {k: round(v, 4) for k, v in eng.core.stats.items()}}
 
 
 def main():
@@ -155,6 +159,8 @@ def main():
             print(json.dumps({name: res["attention"][f"{name} nseq={nseq} ctx={ctx}"]}), file=sys.stderr, flush=True)
     if not args.skip_engine:
         res["engine"] = engine_bench(args.prompts, args.max_tokens, args.layers)
+        print(json.dumps(res["engine"]), file=sys.stderr, flush=True)
+        res["engine_eager"] = engine_bench(args.prompts, args.max_tokens, args.layers, use_graphs=False)
     print(json.dumps(res), flush=True)
 
 

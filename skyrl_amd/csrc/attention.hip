@@ -32,6 +32,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBS = 16;  // tokens per KV-cache block
 
+// Per-sequence split of a context of ctx tokens over at most nparts waves, each partition at
+// least part_min tokens (a multiple of 16): part = max(part_min, ceil16(ceil(ctx / nparts))).
+// Both the attention and the merge kernel derive it from the device-resident context length,
+// so one launch shape (fixed nparts, e.g. a captured graph) adapts to every context.
+__device__ __forceinline__ void seq_split(int ctx, int part_min, int nparts, int& part, int& np) {
+    int p = (ctx + nparts - 1) / nparts;
+    p = (p + kBS - 1) / kBS * kBS;
+    part = p > part_min ? p : part_min;
+    np = (ctx + part - 1) / part;
+}
+
 // ---- rotary embedding + KV-cache write ----------------------------------------------
 // grid (T, nh + 2*nkv), one wave per (token, head). Heads [0, nh) are query heads (rotated
 // into q_out), [nh, nh+nkv) key heads (rotated into the K cache at the token's slot, and
@@ -96,7 +107,7 @@ template <int D>
 __global__ __launch_bounds__(64) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
-    const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_tokens,
+    const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_min,
     int nparts, uint16_t* __restrict__ out, int64_t out_stride, float* __restrict__ ws_o,
     float* __restrict__ ws_ml) {
     constexpr int KS = D / 32;  // k-steps of the Q.K^T MFMA
@@ -105,8 +116,10 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     const int kvh = blockIdx.y;
     const int part = blockIdx.x;
     const int ctx = ctx_lens[seq];
+    int part_tokens, np;
+    seq_split(ctx, part_min, nparts, part_tokens, np);
+    if (part >= np) return;
     const int t0 = part * part_tokens;
-    if (t0 >= ctx) return;
     const int t1 = min(ctx, t0 + part_tokens);
     const int lane = threadIdx.x;
     const int c = lane & 15;  // MFMA column: query head within the GQA group / token row of K
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
     if (!hv) return;
-    if (nparts == 1) {
+    if (np == 1) {  // the whole context in this wave: final output, the merge skips this sequence
         const float inv = 1.f / l;
         uint16_t* orow = out + (int64_t)seq * out_stride + (int64_t)h * D;
 #pragma unroll
@@ -213,14 +226,15 @@ template <int D>
 __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const float* __restrict__ ws_o,
                                                                 const float* __restrict__ ws_ml,
                                                                 const int32_t* __restrict__ ctx_lens, int nh,
-                                                                int part_tokens, int nparts,
+                                                                int part_min, int nparts,
                                                                 uint16_t* __restrict__ out, int64_t out_stride) {
     const int h = blockIdx.x;
     const int seq = blockIdx.y;
     const int d = threadIdx.x;
     const int ctx = ctx_lens[seq];
-    int np = (ctx + part_tokens - 1) / part_tokens;
-    np = np < nparts ? np : nparts;
+    int part_tokens, np;
+    seq_split(ctx, part_min, nparts, part_tokens, np);
+    if (np == 1) return;  // written directly by the attention kernel
     const int64_t rec0 = ((int64_t)seq * nh + h) * nparts;
     float M = -INFINITY;
     for (int p = 0; p < np; ++p) M = fmaxf(M, ws_ml[(rec0 + p) * 2]);
@@ -277,7 +291,8 @@ extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k
     SKYRL_REQUIRE(nseq >= 0 && nh > 0 && nkv > 0 && nh % nkv == 0, "paged_decode: bad head counts");
     SKYRL_REQUIRE(nh / nkv <= 16, "paged_decode: more than 16 query heads per kv head");
     SKYRL_REQUIRE(head_dim == 64 || head_dim == 128, "paged_decode: head_dim must be 64 or 128");
-    SKYRL_REQUIRE(part_tokens > 0 && part_tokens % kBS == 0, "paged_decode: part_tokens must be a multiple of 16");
+    SKYRL_REQUIRE(part_tokens > 0 && part_tokens % kBS == 0,
+                  "paged_decode: part_tokens (minimum partition) must be a multiple of 16");
     SKYRL_REQUIRE(nparts >= 1, "paged_decode: nparts must be >= 1");
     if (nseq == 0) return SKYRL_OK;
     SKYRL_REQUIRE(q && k_cache && v_cache && block_tables && context_lens && out, "paged_decode: null pointer");

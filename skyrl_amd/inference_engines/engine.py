@@ -25,7 +25,9 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import heapq
 import itertools
+import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Deque, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -109,6 +111,7 @@ class Request:
     out_logprobs: List[float] = field(default_factory=list)
     blocks: List[int] = field(default_factory=list)
     state: int = WAITING
+    row: int = -1  # persistent batch row while running (the runner's per-row device state)
     finish_reason: Optional[str] = None
     on_finish: Optional[Callable[["Request"], None]] = None
 
@@ -166,8 +169,10 @@ class EngineCore:
         self.waiting: Deque[Request] = collections.deque()
         self.running: List[Request] = []
         self._rid = itertools.count()
+        self._free_rows = list(range(max_num_seqs))  # lowest row first: keeps the batch compact
         self.num_preemptions = 0
         self.num_steps = 0
+        self.stats: Dict[str, float] = collections.defaultdict(float)  # per-kind step counts and seconds
 
     # ---------------------------------------------------------------- requests
     def add_request(self, prompt: Sequence[int], params: RequestParams,
@@ -211,10 +216,16 @@ class EngineCore:
         if r.blocks:
             self.allocator.free(r.blocks)
             r.blocks = []
+        self._release_row(r)
         r.state = FINISHED
         r.finish_reason = reason
         if r.on_finish is not None:
             r.on_finish(r)
+
+    def _release_row(self, r: Request) -> None:
+        if r.row >= 0:
+            heapq.heappush(self._free_rows, r.row)
+            r.row = -1
 
     # ---------------------------------------------------------------- scheduling
     def _schedule_prefill(self) -> List[Request]:
@@ -231,6 +242,7 @@ class EngineCore:
                 break
             self.waiting.popleft()
             r.blocks = self.allocator.allocate(need)
+            r.row = heapq.heappop(self._free_rows)
             r.state = RUNNING
             batch.append(r)
             padded_max = lmax
@@ -253,6 +265,7 @@ class EngineCore:
             victim = self.running.pop()
             self.allocator.free(victim.blocks)
             victim.blocks = []
+            self._release_row(victim)
             victim.state = WAITING
             self.waiting.appendleft(victim)
             self.num_preemptions += 1
@@ -287,8 +300,11 @@ class EngineCore:
             kind = "decode"
             if not batch:
                 return []
+        t0 = time.perf_counter()
         keys, sup = self._keys_and_masks(batch)
+        t1 = time.perf_counter()
         tokens, logprobs = self.runner.execute(ScheduledBatch(kind, batch, keys, sup))
+        t2 = time.perf_counter()
         if kind == "prefill":
             self.running.extend(batch)
         finished: List[Request] = []
@@ -302,6 +318,10 @@ class EngineCore:
         if finished:
             done = {id(r) for r in finished}
             self.running = [r for r in self.running if id(r) not in done]
+        st = self.stats
+        st[kind + "_steps"] += 1
+        st[kind + "_exec_s"] += t2 - t1
+        st[kind + "_host_s"] += (t1 - t0) + (time.perf_counter() - t2)
         return finished
 
     def _stop_reason(self, r: Request, tok: int) -> Optional[str]:
@@ -318,24 +338,55 @@ class EngineCore:
 
 
 class ModelRunner:
-    """Device side of one scheduled batch: PagedDecoder forward + lm_head + HIP sampler."""
+    """Device side of one scheduled batch: PagedDecoder forward + lm_head + HIP sampler.
 
-    def __init__(self, model, num_blocks: int, max_num_seqs: int, seed: int = 0):
+    Decode runs over the persistent batch rows [0, nb) (nb = the smallest bucket >= 1 + the
+    highest running row): per-row inputs (token, position, slot, context length, block-table
+    row) are staged in pinned host buffers and copied with two H2D copies into static device
+    buffers, and the forward + lm_head of bucket nb is a captured HIP graph replayed per step
+    (one launch instead of ~10 per layer from Python). Idle rows feed token 0 at position 0
+    with slot -1 (no cache write) and context 1. Prefill runs eagerly (ragged shapes)."""
+
+    BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 192, 256, 384, 512, 768, 1024)
+
+    def __init__(self, model, num_blocks: int, max_num_seqs: int, seed: int = 0, use_graphs: bool = True):
         import torch
-
-        from . import model as model_mod
 
         self.torch = torch
         self.model = model
         self.device = model.device
         self.seed = int(seed)
-        s = model.spec
-        self.cache = model_mod.PagedKVCache(s.num_layers, num_blocks, s.num_kv_heads, s.head_dim, self.device)
-        self.max_blocks = _blocks_needed(model.max_model_len)
+        self.num_blocks = num_blocks
         self.max_num_seqs = max_num_seqs
+        self.max_blocks = _blocks_needed(model.max_model_len)
+        self.use_graphs = use_graphs
+        self.buckets = [b for b in self.BUCKETS if b < max_num_seqs] + [max_num_seqs]
+        self.cache = None
+        R = max_num_seqs
+        pin = torch.cuda.is_available()
+        self.h_i64 = torch.zeros((3, R), dtype=torch.int64, pin_memory=pin)       # token | position | slot
+        self.h_i32 = torch.zeros((R, self.max_blocks), dtype=torch.int32, pin_memory=pin)  # block tables
+        self.h_ctx = torch.zeros(R, dtype=torch.int32, pin_memory=pin)
+        self.h_keys = torch.zeros(R, dtype=torch.int64, pin_memory=pin)
+        self.n_i64, self.n_i32, self.n_keys = self.h_i64.numpy(), self.h_i32.numpy(), self.h_keys.numpy()
+        self.n_ctx = self.h_ctx.numpy()
+        self.d_i64 = torch.zeros((3, R), dtype=torch.int64, device=self.device)
+        self.d_i32 = torch.zeros((R, self.max_blocks), dtype=torch.int32, device=self.device)
+        self.d_ctx = torch.ones(R, dtype=torch.int32, device=self.device)
+        self.d_keys = torch.zeros(R, dtype=torch.int64, device=self.device)
+        self.tokens = torch.empty(R, dtype=torch.int32, device=self.device)
+        self.lps = torch.empty(R, dtype=torch.float32, device=self.device)
+        self.h_out = torch.zeros((2, R), dtype=torch.float64, pin_memory=pin)
+        self._nblk = np.zeros(R, dtype=np.int64)  # table entries already staged per row
+        self._graphs: Dict[int, Tuple[Any, Any]] = {}
+        self._pool = None
         self._sampler_ws = None
+        self.ensure_cache(num_blocks)
 
+    # ---------------------------------------------------------------- memory
     def release_cache(self):
+        self._graphs.clear()
+        self._pool = None
         self.cache = None
 
     def ensure_cache(self, num_blocks: int):
@@ -344,11 +395,84 @@ class ModelRunner:
 
             s = self.model.spec
             self.cache = PagedKVCache(s.num_layers, num_blocks, s.num_kv_heads, s.head_dim, self.device)
+            self._graphs.clear()
+
+    def drop_graphs(self):
+        """Weights were re-allocated (sleep level 2 / wake_up): captured graphs point at the old storage."""
+        self._graphs.clear()
+        self._pool = None
 
     def _h2d(self, arr: np.ndarray):
-        t = self.torch.from_numpy(arr)
-        return t.pin_memory().to(self.device, non_blocking=True)
+        return self.torch.from_numpy(arr).pin_memory().to(self.device, non_blocking=True)
 
+    # ---------------------------------------------------------------- decode inputs
+    def _decode_inputs(self, nb: int, fixed: bool):
+        from .model import StepInputs
+
+        nparts = max_ctx = None
+        if fixed:  # graph: the wave count is baked into the launch (the split adapts on device)
+            from . import kernels
+
+            max_ctx = self.model.max_model_len
+            nparts = kernels.choose_nparts(nb, self.model.spec.num_kv_heads, max_ctx)
+        return StepInputs(tokens=self.d_i64[0, :nb], positions=self.d_i64[1, :nb], slots=self.d_i64[2, :nb],
+                          block_tables=self.d_i32[:nb], context_lens=self.d_ctx[:nb], max_ctx=max_ctx or 0,
+                          nparts=nparts)
+
+    def _forward_logits(self, inp):
+        return self.model.logits(self.model.forward_decode(inp, self.cache))
+
+    def _graph(self, nb: int):
+        g = self._graphs.get(nb)
+        if g is not None:
+            return g
+        torch = self.torch
+        from . import kernels
+
+        s = self.model.spec
+        need = 0  # pre-size the merge workspace for every bucket: a graph must never see it move
+        for b in self.buckets:
+            nparts = kernels.choose_nparts(b, s.num_kv_heads, self.model.max_model_len)
+            need = max(need, _decode_ws_bytes(b, s.num_heads, s.head_dim, nparts))
+        self.model.workspace.get(need)
+        inp = self._decode_inputs(nb, fixed=True)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self._forward_logits(inp)  # warm-up outside capture (library handles, workspaces)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, pool=self._pool):
+            logits = self._forward_logits(inp)
+        self._graphs[nb] = (graph, logits)
+        return self._graphs[nb]
+
+    def _stage_decode(self, reqs: List["Request"], nb: int) -> None:
+        n_i64, n_i32, n_ctx = self.n_i64, self.n_i32, self.n_ctx
+        n_i64[:, :nb] = 0
+        n_i64[2, :nb] = -1
+        n_ctx[:nb] = 1
+        rows = np.fromiter((r.row for r in reqs), dtype=np.int64, count=len(reqs))
+        L = np.fromiter((r.num_tokens for r in reqs), dtype=np.int64, count=len(reqs))
+        for r in reqs:  # table rows: only newly allocated blocks are staged
+            k = self._nblk[r.row]
+            if len(r.blocks) != k:
+                if len(r.blocks) < k:
+                    k = 0
+                n_i32[r.row, k:len(r.blocks)] = r.blocks[k:]
+                self._nblk[r.row] = len(r.blocks)
+        n_i64[0, rows] = np.fromiter((r.out_tokens[-1] for r in reqs), dtype=np.int64, count=len(reqs))
+        pos = L - 1
+        n_i64[1, rows] = pos
+        n_i64[2, rows] = n_i32[rows, pos // BLOCK_SIZE].astype(np.int64) * BLOCK_SIZE + pos % BLOCK_SIZE
+        n_ctx[rows] = L
+        self.d_i64[:, :nb].copy_(self.h_i64[:, :nb], non_blocking=True)
+        self.d_i32[:nb].copy_(self.h_i32[:nb], non_blocking=True)
+        self.d_ctx[:nb].copy_(self.h_ctx[:nb], non_blocking=True)
+
+    # ---------------------------------------------------------------- execute
     def execute(self, batch: ScheduledBatch):
         torch = self.torch
         from .model import StepInputs
@@ -364,63 +488,70 @@ class ModelRunner:
             packed = self._h2d(np.concatenate([tok, pos, slots]))
             T = tok.shape[0]
             inp = StepInputs(tokens=packed[:T], positions=packed[T:2 * T], slots=packed[2 * T:], seq_lens=lens)
-            hidden = self.model.forward_prefill(inp, self.cache)
+            logits = self.model.logits(self.model.forward_prefill(inp, self.cache))
+            for r in reqs:
+                self._nblk[r.row] = 0  # (re)admitted row: restage its whole table
+            rows = np.arange(n)
         else:
-            L = np.fromiter((r.num_tokens for r in reqs), dtype=np.int64, count=n)
-            tok = np.fromiter((r.out_tokens[-1] for r in reqs), dtype=np.int64, count=n)
-            pos = L - 1
-            slots = np.fromiter((r.blocks[(p // BLOCK_SIZE)] * BLOCK_SIZE + p % BLOCK_SIZE
-                                 for r, p in zip(reqs, pos.tolist())), dtype=np.int64, count=n)
-            max_ctx = int(L.max())
-            nbt = _blocks_needed(max_ctx)
-            bt = np.zeros((n, nbt + 1), dtype=np.int32)  # column 0: context length, then the table
-            bt[:, 0] = L
-            for i, r in enumerate(reqs):
-                b = r.blocks[:nbt]
-                bt[i, 1:1 + len(b)] = b
-            packed = self._h2d(np.concatenate([tok, pos, slots]))
-            bt_d = self._h2d(bt)
-            inp = StepInputs(tokens=packed[:n], positions=packed[n:2 * n], slots=packed[2 * n:],
-                             block_tables=bt_d[:, 1:], context_lens=bt_d[:, 0].contiguous(), max_ctx=max_ctx)
-            hidden = self.model.forward_decode(inp, self.cache)
-        logits = self.model.logits(hidden)
-        return self._sample(logits, batch)
+            hi = 1 + max(r.row for r in reqs)
+            nb = next(b for b in self.buckets if b >= hi)
+            self._stage_decode(reqs, nb)
+            if self.use_graphs:
+                graph, logits = self._graph(nb)
+                graph.replay()
+            else:
+                inp = self._decode_inputs(nb, fixed=False)
+                inp.max_ctx = int(max(r.num_tokens for r in reqs))
+                logits = self._forward_logits(inp)
+            rows = np.fromiter((r.row for r in reqs), dtype=np.int64, count=n)
+        return self._sample(logits, batch, rows)
 
-    def _sample(self, logits, batch: ScheduledBatch):
+    def _sample(self, logits, batch: ScheduledBatch, rows: np.ndarray):
         torch = self.torch
         from .. import _ffi
         from ..ops import _ptr, _stream
 
-        n, V = logits.shape
-        for i, ids in enumerate(batch.suppress):
+        nb, V = logits.shape
+        for r_i, ids in zip(rows.tolist(), batch.suppress):
             if ids:
-                logits[i, list(ids)] = float("-inf")
-        keys = self._h2d(batch.keys)
-        tokens = torch.empty(n, dtype=torch.int32, device=self.device)
-        lps = torch.empty(n, dtype=torch.float32, device=self.device)
+                logits[r_i, list(ids)] = float("-inf")
+        self.n_keys[:nb] = 0
+        self.n_keys[rows] = batch.keys
+        self.d_keys[:nb].copy_(self.h_keys[:nb], non_blocking=True)
         groups: Dict[Tuple, List[int]] = {}
-        for i, r in enumerate(batch.requests):
-            groups.setdefault(r.params.sampler_key(), []).append(i)
-        ws_bytes = _ffi.query("skyrl_sample_workspace_bytes", max(n, self.max_num_seqs), V)
+        for r_i, r in zip(rows.tolist(), batch.requests):
+            groups.setdefault(r.params.sampler_key(), []).append(r_i)
+        ws_bytes = _ffi.query("skyrl_sample_workspace_bytes", max(nb, self.max_num_seqs), V)
         if self._sampler_ws is None or self._sampler_ws.numel() < ws_bytes:
             self._sampler_ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
         st = _stream(self.device)
-        for (temp, top_k, top_p, min_p), rows in groups.items():
-            if len(rows) == n:
-                lg, ky, to, lo = logits, keys, tokens, lps
+        for (temp, top_k, top_p, min_p), grows in groups.items():
+            if len(groups) == 1:  # every row of the bucket (idle rows are sampled and dropped)
+                lg, ky, to, lo = logits, self.d_keys[:nb], self.tokens[:nb], self.lps[:nb]
             else:
-                idx = torch.tensor(rows, dtype=torch.int64, device=self.device)
-                lg, ky = logits.index_select(0, idx), keys.index_select(0, idx)
-                to = torch.empty(len(rows), dtype=torch.int32, device=self.device)
-                lo = torch.empty(len(rows), dtype=torch.float32, device=self.device)
+                idx = torch.tensor(grows, dtype=torch.int64).to(self.device, non_blocking=True)
+                lg, ky = logits.index_select(0, idx), self.d_keys.index_select(0, idx)
+                to = torch.empty(len(grows), dtype=torch.int32, device=self.device)
+                lo = torch.empty(len(grows), dtype=torch.float32, device=self.device)
             _ffi.call("skyrl_sample", _ptr(lg), _ffi.BF16, lg.stride(0), lg.shape[0], V, float(temp), int(top_k),
                       float(top_p), float(min_p), self.seed & 0xFFFFFFFFFFFFFFFF, _ptr(ky), 0, _ptr(to), _ptr(lo),
                       _ptr(self._sampler_ws), st)
-            if len(rows) != n:
-                tokens.index_copy_(0, idx, to)
-                lps.index_copy_(0, idx, lo)
-        out = torch.stack([tokens.to(torch.float64), lps.to(torch.float64)]).cpu().numpy()
-        return out[0].astype(np.int64), out[1].astype(np.float32)
+            if len(groups) != 1:
+                self.tokens.index_copy_(0, idx, to)
+                self.lps.index_copy_(0, idx, lo)
+        m = max(nb, int(rows.max()) + 1)
+        out = self.h_out[:, :m]
+        out[0].copy_(self.tokens[:m], non_blocking=True)
+        out[1].copy_(self.lps[:m], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        o = out.numpy()
+        return o[0, rows].astype(np.int64), o[1, rows].astype(np.float32)
+
+
+def _decode_ws_bytes(nseq: int, nh: int, head_dim: int, nparts: int) -> int:
+    from .. import _ffi
+
+    return int(_ffi.query("skyrl_paged_decode_workspace_bytes", nseq, nh, head_dim, nparts))
 
 
 def _slots(blocks: List[int], start: int, end: int) -> np.ndarray:
@@ -438,7 +569,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
 
     def __init__(self, model, num_blocks: Optional[int] = None, max_num_seqs: int = 512,
                  max_prefill_tokens: int = 32768, seed: int = 0, kv_cache_fraction: float = 0.5,
-                 tokenizer=None, runner=None):
+                 tokenizer=None, runner=None, use_graphs: bool = True):
         self.model = model
         self.tokenizer = tokenizer
         if num_blocks is None:
@@ -451,7 +582,8 @@ class AMDInferenceEngine(InferenceEngineInterface):
             num_blocks = int(free * kv_cache_fraction) // PagedKVCache.bytes_per_block(
                 s.num_layers, s.num_kv_heads, s.head_dim)
         self.num_blocks = num_blocks
-        self.runner = runner if runner is not None else ModelRunner(model, num_blocks, max_num_seqs, seed)
+        self.runner = runner if runner is not None else ModelRunner(model, num_blocks, max_num_seqs, seed,
+                                                                         use_graphs=use_graphs)
         self.core = EngineCore(self.runner, num_blocks, max_num_seqs=max_num_seqs,
                                max_model_len=model.max_model_len, max_prefill_tokens=max_prefill_tokens,
                                eos_token_id=model.spec.eos_token_id, seed=seed)
@@ -544,6 +676,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
         tags = kwargs.get("tags") or ["weights", "kv_cache"]
         if "weights" in tags and not self.model.layers:
             self.model._alloc(seed=None)
+            self.runner.drop_graphs()
             if self._offloaded is not None:
                 self.model.load_weights(self._offloaded)
                 self._offloaded = None

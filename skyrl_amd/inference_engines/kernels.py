@@ -46,13 +46,43 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, slot_mapping: torc
     return q_out
 
 
-def choose_partition(nseq: int, nkv: int, max_ctx: int, target_waves: int = 2048) -> int:
-    """Context tokens per decode wave: the largest of 512/256/128/64 that still gives about
-    ``target_waves`` waves (256 CUs x 8), so small batches split long contexts."""
-    for part in (512, 256, 128):
-        if nseq * nkv * math.ceil(max(max_ctx, 1) / part) >= target_waves:
-            return part
-    return 64
+def add_rmsnorm(delta: Optional[torch.Tensor], hidden: torch.Tensor, weight: torch.Tensor, eps: float,
+                out: torch.Tensor) -> torch.Tensor:
+    """hidden += delta (bf16, in place; delta may be None), out = RMSNorm(hidden) * weight."""
+    dev = _require_gpu(hidden, weight, out, delta)
+    n, H = hidden.shape
+    for t in (hidden, out) + ((delta,) if delta is not None else ()):
+        if t.dtype != torch.bfloat16 or t.shape != (n, H) or not t.is_contiguous():
+            raise ValueError(f"add_rmsnorm: expected contiguous bf16 [{n}, {H}]")
+    if weight.dtype != torch.bfloat16 or weight.shape != (H,):
+        raise ValueError("add_rmsnorm: weight must be bf16 [H]")
+    _ffi.call("skyrl_add_rmsnorm", _ptr(delta), _ptr(hidden), _ptr(weight), n, H, float(eps), _ptr(out), _stream(dev))
+    return out
+
+
+def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up of the fused [n, 2I] gate|up projection -> bf16 [n, I]."""
+    dev = _require_gpu(gate_up)
+    n, I2 = gate_up.shape
+    if gate_up.dtype != torch.bfloat16 or not gate_up.is_contiguous() or I2 % 8:
+        raise ValueError("silu_mul: gate_up must be contiguous bf16 [n, 2I] with I % 4 == 0")
+    if out is None:
+        out = torch.empty((n, I2 // 2), dtype=torch.bfloat16, device=dev)
+    _ffi.call("skyrl_silu_mul", _ptr(gate_up), n, I2 // 2, _ptr(out), _stream(dev))
+    return out
+
+
+MIN_PARTITION = 64  # context tokens: below this a wave's fixed cost outweighs its KV stream
+
+
+def choose_nparts(nseq: int, nkv: int, max_ctx: int, target_waves: int = 1024) -> int:
+    """Waves per (sequence, kv head) for about ``target_waves`` waves in flight (256 CUs x 4;
+    measured: fewer, longer waves beat finer splits down to that count),
+    never more than max_ctx / MIN_PARTITION. The kernel splits each sequence's own context
+    over that many waves (at least MIN_PARTITION tokens each), so the choice only sizes the
+    grid: two calls whose nparts differ only by this cap compute identical splits."""
+    want = math.ceil(target_waves / max(1, nseq * nkv))
+    return max(1, min(want, math.ceil(max(max_ctx, 1) / MIN_PARTITION)))
 
 
 class DecodeWorkspace:
@@ -70,11 +100,13 @@ class DecodeWorkspace:
 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                  context_lens: torch.Tensor, max_ctx: int, scale: float, out: Optional[torch.Tensor] = None,
-                 workspace: Optional[DecodeWorkspace] = None, part_tokens: Optional[int] = None) -> torch.Tensor:
+                 workspace: Optional[DecodeWorkspace] = None, nparts: Optional[int] = None,
+                 part_min: int = MIN_PARTITION) -> torch.Tensor:
     """softmax(scale * q K^T) V for one query token per sequence over its paged context.
 
     q: bf16 [n, nh, D]; block_tables: int32 [n, max_blocks]; context_lens: int32 [n] (>= 1,
-    <= max_ctx, and max_blocks * 16 >= max_ctx). Returns bf16 [n, nh, D]."""
+    <= max_ctx, and max_blocks * 16 >= max_ctx). Each context is split on device over at most
+    ``nparts`` waves per kv head of at least ``part_min`` tokens. Returns bf16 [n, nh, D]."""
     dev = _require_gpu(q, k_cache, v_cache, block_tables, context_lens)
     n, nh, D = q.shape
     nb, nkv = k_cache.shape[0], k_cache.shape[1]
@@ -93,13 +125,12 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
         out = torch.empty((n, nh, D), dtype=torch.bfloat16, device=dev)
     if n == 0:
         return out
-    part = part_tokens or choose_partition(n, nkv, max_ctx)
-    nparts = max(1, math.ceil(max_ctx / part))
+    nparts = nparts or choose_nparts(n, nkv, max_ctx)
     ws = None
     if nparts > 1:
         nbytes = _ffi.query("skyrl_paged_decode_workspace_bytes", n, nh, D, nparts)
         ws = (workspace or DecodeWorkspace(dev)).get(nbytes)
     _ffi.call("skyrl_paged_decode", _ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
-              block_tables.stride(0), _ptr(context_lens), n, nh, nkv, D, float(scale), part, nparts, _ptr(out),
+              block_tables.stride(0), _ptr(context_lens), n, nh, nkv, D, float(scale), part_min, nparts, _ptr(out),
               out.stride(0), _ptr(ws), _stream(dev))
     return out

@@ -107,6 +107,7 @@ class StepInputs:
     block_tables: Optional[torch.Tensor] = None  # int32 [n, max_blocks]
     context_lens: Optional[torch.Tensor] = None  # int32 [n]
     max_ctx: int = 0
+    nparts: Optional[int] = None  # decode waves per (sequence, kv head); None: chosen per call
     # prefill only: sequence lengths (host) of the ragged token batch
     seq_lens: Optional[List[int]] = None
 
@@ -210,19 +211,23 @@ class PagedDecoder:
         self.layers = []
 
     # ---------------------------------------------------------------- forward
-    def _rmsnorm(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        # HF Qwen2RMSNorm: f32 variance, normalise in f32, cast, then scale in the model dtype
-        xf = x.float()
-        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.spec.rms_norm_eps)
-        return w * xf.to(x.dtype)
-
-    def _mlp(self, x: torch.Tensor, L) -> torch.Tensor:
-        gu = F.linear(x, L["wgu"])
-        I = self.spec.intermediate_size
-        return F.linear(F.silu(gu[:, :I]) * gu[:, I:], L["wd"])
-
-    def _qkv(self, x, L):
-        return F.linear(x, L["wqkv"], L["bqkv"])
+    def _run_layers(self, h: torch.Tensor, attention) -> torch.Tensor:
+        """Residual stream h [T, H] (bf16, updated in place) through every layer; `attention(li, L,
+        qkv)` returns the attention output [T, nh*D]. Norms and the SiLU gate are the fused HIP
+        kernels (csrc/decoder_ops.hip); GEMMs are hipBLASLt through torch. Returns the final-norm
+        output [T, H]."""
+        s = self.spec
+        eps = s.rms_norm_eps
+        x = torch.empty_like(h)
+        kernels.add_rmsnorm(None, h, self.layers[0]["ln1"], eps, x)
+        for li, L in enumerate(self.layers):
+            qkv = F.linear(x, L["wqkv"], L["bqkv"])
+            a = attention(li, L, qkv)
+            kernels.add_rmsnorm(F.linear(a, L["wo"]), h, L["ln2"], eps, x)
+            act = kernels.silu_mul(F.linear(x, L["wgu"]))
+            nxt = self.layers[li + 1]["ln1"] if li + 1 < len(self.layers) else self.norm
+            kernels.add_rmsnorm(F.linear(act, L["wd"]), h, nxt, eps, x)
+        return x
 
     def forward_decode(self, inp: StepInputs, cache: PagedKVCache) -> torch.Tensor:
         """One token per sequence: returns the final hidden states [n, H]."""
@@ -231,16 +236,15 @@ class PagedDecoder:
         n = h.shape[0]
         q_buf = torch.empty((n, s.num_heads, s.head_dim), dtype=self.dtype, device=self.device)
         a_buf = torch.empty_like(q_buf)
-        for li, L in enumerate(self.layers):
-            x = self._rmsnorm(h, L["ln1"])
-            qkv = self._qkv(x, L)
+
+        def attention(li, L, qkv):
             q = kernels.rope_kv_write(qkv, inp.positions, inp.slots, self.cos_sin, s.num_heads, s.num_kv_heads,
                                       s.head_dim, cache.k[li], cache.v[li], q_out=q_buf)
             a = kernels.paged_decode(q, cache.k[li], cache.v[li], inp.block_tables, inp.context_lens, inp.max_ctx,
-                                     self.scale, out=a_buf, workspace=self.workspace)
-            h = h + F.linear(a.view(n, -1), L["wo"])
-            h = h + self._mlp(self._rmsnorm(h, L["ln2"]), L)
-        return self._rmsnorm(h, self.norm)
+                                     self.scale, out=a_buf, workspace=self.workspace, nparts=inp.nparts)
+            return a.view(n, -1)
+
+        return self._run_layers(h, attention)
 
     def forward_prefill(self, inp: StepInputs, cache: PagedKVCache) -> torch.Tensor:
         """Ragged prompts (total T tokens, lengths inp.seq_lens): writes their K/V into the cache
@@ -259,30 +263,23 @@ class PagedDecoder:
         pad_idx = pad_idx.to(dev, non_blocking=True)
         valid = (j[None] < lens_t[:, None]).reshape(-1).nonzero().squeeze(1).to(dev, non_blocking=True)
         last = (starts + lens_t - 1).to(dev, non_blocking=True)
-
-        h = F.embedding(inp.tokens, self.embed)
         k_out = torch.empty((T, s.num_kv_heads, s.head_dim), dtype=self.dtype, device=dev)
         rep = s.num_heads // s.num_kv_heads
-        for li, L in enumerate(self.layers):
-            x = self._rmsnorm(h, L["ln1"])
-            qkv = self._qkv(x, L)
+
+        def padded(t):
+            z = torch.cat([t, t.new_zeros((1,) + tuple(t.shape[1:]))], 0)
+            return z[pad_idx].transpose(1, 2)  # [B, heads, Lmax, D]
+
+        def attention(li, L, qkv):
             q = kernels.rope_kv_write(qkv, inp.positions, inp.slots, self.cos_sin, s.num_heads, s.num_kv_heads,
                                       s.head_dim, cache.k[li], cache.v[li], k_out=k_out)
             v = qkv[:, (s.num_heads + s.num_kv_heads) * s.head_dim:].reshape(T, s.num_kv_heads, s.head_dim)
-
-            def padded(t):
-                z = torch.cat([t, t.new_zeros((1,) + tuple(t.shape[1:]))], 0)
-                return z[pad_idx].transpose(1, 2)  # [B, heads, Lmax, D]
-
             qp, kp, vp = padded(q), padded(k_out), padded(v)
-            if rep > 1:
-                kp = kp.repeat_interleave(rep, dim=1)
-                vp = vp.repeat_interleave(rep, dim=1)
-            o = F.scaled_dot_product_attention(qp, kp, vp, is_causal=True, scale=self.scale)
-            o = o.transpose(1, 2).reshape(B * Lmax, s.num_heads * s.head_dim)[valid]
-            h = h + F.linear(o, L["wo"])
-            h = h + self._mlp(self._rmsnorm(h, L["ln2"]), L)
-        return self._rmsnorm(h[last], self.norm)
+            o = F.scaled_dot_product_attention(qp, kp, vp, is_causal=True, scale=self.scale, enable_gqa=rep > 1)
+            return o.transpose(1, 2).reshape(B * Lmax, s.num_heads * s.head_dim)[valid]
+
+        h = F.embedding(inp.tokens, self.embed)
+        return self._run_layers(h, attention)[last]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """lm_head: bf16 [n, V] (the sampler's input)."""

@@ -32,6 +32,8 @@ class FakeRunner:
     def execute(self, batch):
         self.batches.append((batch.kind, len(batch.requests)))
         seen = {}
+        rows = [r.row for r in batch.requests]
+        assert len(set(rows)) == len(rows) and min(rows) >= 0, "persistent rows must be unique"
         for r in batch.requests:
             need = (r.num_tokens + (1 if batch.kind == "prefill" else 0) + BLOCK_SIZE - 1) // BLOCK_SIZE
             assert len(r.blocks) >= min(need, (r.num_tokens + BLOCK_SIZE - 1) // BLOCK_SIZE)
@@ -47,6 +49,9 @@ class FakeRunner:
         pass
 
     def ensure_cache(self, n):
+        pass
+
+    def drop_graphs(self):
         pass
 
 
@@ -235,3 +240,33 @@ def test_decoder_hf_weight_names_round_trip():
         m.load_weights([("model.layers.9.mlp.up_proj.weight", sd["model.layers.0.mlp.up_proj.weight"])])
     with pytest.raises(ValueError):
         m.load_weights([("model.norm.weight", torch.zeros(3))])
+
+
+def test_model_runner_stages_decode_rows():
+    """ModelRunner's host staging (CPU tensors, no kernel call): idle rows get slot -1 and
+    context 1; running rows get their last token, position, slot and block-table row."""
+    import torch
+    from transformers import Qwen2Config
+
+    from skyrl_amd.inference_engines.engine import ModelRunner, Request
+    from skyrl_amd.inference_engines.model import PagedDecoder
+
+    cfg = Qwen2Config(vocab_size=64, hidden_size=256, intermediate_size=256, num_hidden_layers=1,
+                      num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=128)
+    m = PagedDecoder(cfg, "cpu", seed=None)
+    runner = ModelRunner(m, num_blocks=40, max_num_seqs=6)
+    a = Request(rid=0, prompt=list(range(20)), params=RequestParams(), key=0, out_tokens=[7], blocks=[5, 9],
+                row=0)
+    b = Request(rid=1, prompt=[1, 2], params=RequestParams(), key=1, out_tokens=[3, 4], blocks=[11], row=3)
+    runner._stage_decode([a, b], 4)
+    tok, pos, slot = runner.d_i64[:, :4].tolist()
+    assert tok == [7, 0, 0, 4] and pos == [20, 0, 0, 3]
+    assert slot == [9 * 16 + 4, -1, -1, 11 * 16 + 3]
+    t = runner.d_i32[:4].tolist()
+    assert runner.d_ctx[:4].tolist() == [21, 1, 1, 4]
+    assert t[0][0:2] == [5, 9] and t[3][0] == 11
+    a.blocks.append(17)  # a new block is staged incrementally
+    a.out_tokens += [1] * 12
+    runner._stage_decode([a], 1)
+    assert runner.d_i32[0, 0:3].tolist() == [5, 9, 17] and runner.d_i64[2, 0].item() == 17 * 16 + 0
+    assert torch.equal(runner.d_ctx[:1], torch.tensor([33], dtype=torch.int32))
