@@ -1,0 +1,176 @@
+"""Ray-free GRPO/PPO driver: one training step = rollout on the MI355X engine -> experience pack
+-> ref/old logprobs -> advantages -> clipped policy-gradient update -> weight sync back into
+the engine.
+
+Follows the step of RayPPOTrainer.train (skyrl_train/trainer.py:236-352): generate
+(`generate`, :427-470), postprocess_generator_output + convert_to_training_input (:592-757),
+fwd_logprobs_values_reward (:1037-1066), compute_advantages_and_returns (:759-862),
+train_critic_and_policy -> _execute_training_step (:1067-1120) with the mini-/micro-batch
+structure of PolicyWorkerBase (workers/worker.py:664-925), then the weight sync
+(broadcast_to_inference_engines, fsdp_worker.py:201-228). Ray actors, FSDP sharding and
+the dispatch layer collapse into this process: the learner is a HF transformers model under
+torch.autocast(bf16) (the north star keeps the transformer in PyTorch), and everything on the
+§8 path runs through the HIP kernels — the engine's sampler and decode loop, the pack kernel,
+GRPO, the lm_head-fused logprob/entropy and the fused PPO/KL loss.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import math
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+import torch
+
+from . import ppo_utils, trainer_utils
+from .config import AlgorithmConfig
+from .lmhead import lmhead_logprobs_and_entropy
+
+
+@dataclass
+class TrainerConfig:
+    n_samples_per_prompt: int = 8
+    policy_mini_batch_size: int = 256          # prompts per optimizer step (ppo_base_config.yaml)
+    micro_train_batch_size_per_gpu: int = 1    # sequences per forward/backward
+    micro_forward_batch_size_per_gpu: int = 1  # sequences per no-grad forward
+    update_epochs_per_batch: int = 1
+    lr: float = 1e-6
+    betas: Sequence[float] = (0.9, 0.999)
+    weight_decay: float = 0.01
+    max_grad_norm: float = 1.0
+    temperature: float = 1.0
+    sampling_params: Dict[str, Any] = field(default_factory=lambda: {"max_tokens": 1024, "min_tokens": 1})
+    algorithm: AlgorithmConfig = field(default_factory=AlgorithmConfig)
+
+
+def _positions(attention_mask: torch.Tensor) -> torch.Tensor:
+    """model_wrapper.py:272-273: left-padded position ids."""
+    pos = attention_mask.long().cumsum(-1) - 1
+    return pos.masked_fill_(attention_mask == 0, 1)
+
+
+class GRPOTrainer:
+    """policy: HF CausalLM (fp32 master weights) on the GPU; ref: frozen HF CausalLM (or None when
+    the KL loss is off); client: an InferenceEngineClient (or one engine) whose weights mirror the
+    policy; reward_fn(prompt_ids, response_ids, extra) -> float."""
+
+    def __init__(self, cfg: TrainerConfig, policy, client, reward_fn: Callable[..., float], pad_token_id: int,
+                 ref=None):
+        self.cfg = cfg
+        self.policy = policy
+        self.ref = ref
+        self.client = client
+        self.reward_fn = reward_fn
+        self.pad_token_id = pad_token_id
+        alg = cfg.algorithm
+        if alg.use_kl_loss and ref is None:
+            raise ValueError("use_kl_loss needs a reference model")
+        self.loss_params = ppo_utils.ppo_params_from_config(
+            alg, use_kl_loss=alg.use_kl_loss, use_entropy_loss=alg.use_entropy_loss, has_entropy=True)
+        self.optimizer = torch.optim.AdamW(policy.parameters(), lr=cfg.lr, betas=tuple(cfg.betas),
+                                           weight_decay=cfg.weight_decay, eps=1e-8)
+        self.global_step = 0
+
+    # ---------------------------------------------------------------- rollout
+    async def _generate(self, prompts: List[List[int]]) -> Dict[str, Any]:
+        G = self.cfg.n_samples_per_prompt
+        ids = [p for p in prompts for _ in range(G)]
+        sp = dict(self.cfg.sampling_params)
+        sp.setdefault("logprobs", 0)
+        sp.setdefault("temperature", self.cfg.temperature)
+        out = await self.client.generate({"prompt_token_ids": ids, "sampling_params": sp})
+        return {"prompt_token_ids": ids, "response_ids": out["response_ids"], "stop_reasons": out["stop_reasons"],
+                "rollout_logprobs": out["response_logprobs"],
+                "loss_masks": [[1] * len(r) for r in out["response_ids"]]}
+
+    # ---------------------------------------------------------------- model passes
+    def _logprobs(self, model, seq, att, R, grad: bool):
+        """action log-probs (and entropy) of the last R positions: HFModelWrapper.forward
+        (model_wrapper.py:261-375) with the lm_head-fused HIP logprob/entropy."""
+        with torch.autocast("cuda", dtype=torch.bfloat16), torch.set_grad_enabled(grad):
+            hidden = model.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
+            h = hidden[:, -R - 1:-1].to(torch.bfloat16)
+            w = model.lm_head.weight.to(torch.bfloat16)
+            return lmhead_logprobs_and_entropy(h, w, seq[:, -R:], temperature=self.cfg.temperature,
+                                               compute_entropy=grad)
+
+    @torch.no_grad()
+    def _fwd_logprobs(self, model, data) -> torch.Tensor:
+        seq, att = data["sequences"], data["attention_mask"]
+        R = data["response_mask"].shape[1]
+        mb = self.cfg.micro_forward_batch_size_per_gpu
+        return torch.cat([self._logprobs(model, seq[i:i + mb], att[i:i + mb], R, grad=False)[0]
+                          for i in range(0, len(seq), mb)])
+
+    # ---------------------------------------------------------------- step
+    def step(self, prompts: List[List[int]], extras: Optional[List[Any]] = None) -> Dict[str, float]:
+        cfg, alg = self.cfg, self.cfg.algorithm
+        G = cfg.n_samples_per_prompt
+        gen = asyncio.run(self._generate(prompts))
+        uids = [str(i // G) for i in range(len(gen["response_ids"]))]
+        ext = extras or [None] * len(prompts)
+        gen["rewards"] = [float(self.reward_fn(p, r, ext[i // G]))
+                          for i, (p, r) in enumerate(zip(gen["prompt_token_ids"], gen["response_ids"]))]
+        gen, metrics = trainer_utils.postprocess_generator_output(gen, uids, G)
+        data = trainer_utils.convert_to_training_input(gen, uids, self.pad_token_id, dp_size=1,
+                                                       device=next(self.policy.parameters()).device)
+        # fwd_logprobs_values_reward: old (policy) and ref log-probs, no grad
+        data["action_log_probs"] = self._fwd_logprobs(self.policy, data)
+        if self.ref is not None:
+            data["base_action_log_probs"] = self._fwd_logprobs(self.ref, data)
+        data = trainer_utils.compute_advantages_and_returns(data, alg)
+        metrics.update(data.metadata.get("metrics", {}))
+        m = data["loss_mask"]
+        rl = data["rollout_logprobs"]
+        if rl is not None:  # rollout (engine) vs learner log-probs of the same tokens
+            metrics["logprobs_diff_mean"] = float(((rl - data["action_log_probs"]).abs() * m).sum() / m.sum().clamp(min=1))
+        metrics.update(self._train_policy(data))
+        self._sync_weights()
+        self.global_step += 1
+        return metrics
+
+    def _train_policy(self, data) -> Dict[str, float]:
+        """_execute_training_step: mini-batches of policy_mini_batch_size prompts (no shuffle,
+        trainer.py:1067-1081), micro-batches inside, loss scaled by 1/n_micro, grad clip, AdamW."""
+        cfg = self.cfg
+        n = len(data["sequences"])
+        mini = cfg.policy_mini_batch_size * cfg.n_samples_per_prompt
+        mb = cfg.micro_train_batch_size_per_gpu
+        R = data["response_mask"].shape[1]
+        acc: Dict[str, List[float]] = {}
+        for _ in range(cfg.update_epochs_per_batch):
+            for s0, s1 in trainer_utils.mini_batch_slices(n, mini):
+                n_micro = math.ceil((s1 - s0) / mb)
+                mets = []
+                for i in range(s0, s1, mb):
+                    j = min(i + mb, s1)
+                    lp, ent = self._logprobs(self.policy, data["sequences"][i:j], data["attention_mask"][i:j], R,
+                                             grad=True)
+                    ref = data["base_action_log_probs"][i:j] if self.ref is not None else None
+                    loss, met = self._loss(lp, data, i, j, ref, ent)
+                    (loss / n_micro).backward()
+                    mets.append(met)
+                grad_norm = torch.nn.utils.clip_grad_norm_(self.policy.parameters(), cfg.max_grad_norm)
+                self.optimizer.step()
+                self.optimizer.zero_grad(set_to_none=True)
+                mt = torch.stack(mets).mean(0).tolist()
+                for k, v in (("final_loss", mt[0]), ("policy_loss", mt[1]), ("policy_entropy", mt[2]),
+                             ("policy_kl", mt[3]), ("ppo_clip_ratio", mt[4]), ("grad_norm", float(grad_norm))):
+                    acc.setdefault(k, []).append(v)
+        return trainer_utils.reduce_metrics(acc)
+
+    def _loss(self, lp, data, i, j, ref, ent):
+        from . import ops
+
+        return ops.ppo_loss(lp, data["action_log_probs"][i:j], data["advantages"][i:j], data["loss_mask"][i:j],
+                            self.loss_params, ref_log_probs=ref, entropy=ent)
+
+    @torch.no_grad()
+    def _sync_weights(self):
+        """broadcast_to_inference_engines: bf16 copies of every parameter under its HF name."""
+        names, tensors = [], []
+        for name, p in self.policy.named_parameters():
+            names.append(name)
+            tensors.append(p.detach().to(torch.bfloat16))
+        asyncio.run(self.client.update_named_weights({"names": names, "tensors": tensors}))
