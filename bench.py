@@ -350,10 +350,33 @@ def run(args):
                                     "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0 and world == 1 and not args.no_e2e:
+        del logits, dlogits, reducer, opt  # the real-model leg needs the HBM the resident logits hold
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        result["end_to_end"] = end_to_end_leg()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def end_to_end_leg(timeout_s=900):
+    """The same configuration with the transformer in the loop (scripts/e2e_bench.py, a child
+    process): random-init Qwen2.5-1.5B policy + ref, AMDInferenceEngine rollout of 512
+    trajectories (responses U[1,1024]), HF learner fwd/bwd with the HIP logprob/loss path, AdamW,
+    weight sync. Informational: the headline value above is the hot path (north star)."""
+    import subprocess
+
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "scripts", "e2e_bench.py"), "--steps", "1", "--warmup", "1"]
+    try:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, timeout=timeout_s, text=True)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode != 0 or not lines:
+            return {"error": f"exit {p.returncode}"}
+        return json.loads(lines[-1])
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout after {timeout_s}s"}
 
 
 def pmc_traffic(kernel_name, algorithmic_bytes):
@@ -523,6 +546,7 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=16)
     ap.add_argument("--logits-rows", type=int, default=0, help="0 = the whole batch if HBM allows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the real-model end-to-end leg (N=1 only)")
     ap.add_argument("--no-adv-loss-leg", action="store_true", help="skip the graph-replayed advantage+loss leg")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import asyncio
 import math
+import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
@@ -71,6 +72,14 @@ class GRPOTrainer:
         self.optimizer = torch.optim.AdamW(policy.parameters(), lr=cfg.lr, betas=tuple(cfg.betas),
                                            weight_decay=cfg.weight_decay, eps=1e-8)
         self.global_step = 0
+        self.timings: Dict[str, float] = {}  # seconds per phase of the last step (device-synchronised)
+        self._t = 0.0
+
+    def _mark(self, phase: str) -> None:
+        torch.cuda.synchronize()
+        now = time.perf_counter()
+        self.timings[phase] = now - self._t
+        self._t = now
 
     # ---------------------------------------------------------------- rollout
     async def _generate(self, prompts: List[List[int]]) -> Dict[str, Any]:
@@ -107,7 +116,11 @@ class GRPOTrainer:
     def step(self, prompts: List[List[int]], extras: Optional[List[Any]] = None) -> Dict[str, float]:
         cfg, alg = self.cfg, self.cfg.algorithm
         G = cfg.n_samples_per_prompt
+        self.timings = {}
+        torch.cuda.synchronize()
+        self._t = time.perf_counter()
         gen = asyncio.run(self._generate(prompts))
+        self._mark("generate")
         uids = [str(i // G) for i in range(len(gen["response_ids"]))]
         ext = extras or [None] * len(prompts)
         gen["rewards"] = [float(self.reward_fn(p, r, ext[i // G]))
@@ -115,18 +128,23 @@ class GRPOTrainer:
         gen, metrics = trainer_utils.postprocess_generator_output(gen, uids, G)
         data = trainer_utils.convert_to_training_input(gen, uids, self.pad_token_id, dp_size=1,
                                                        device=next(self.policy.parameters()).device)
+        self._mark("reward_and_pack")
         # fwd_logprobs_values_reward: old (policy) and ref log-probs, no grad
         data["action_log_probs"] = self._fwd_logprobs(self.policy, data)
         if self.ref is not None:
             data["base_action_log_probs"] = self._fwd_logprobs(self.ref, data)
+        self._mark("fwd_logprobs")
         data = trainer_utils.compute_advantages_and_returns(data, alg)
+        self._mark("advantages")
         metrics.update(data.metadata.get("metrics", {}))
         m = data["loss_mask"]
         rl = data["rollout_logprobs"]
         if rl is not None:  # rollout (engine) vs learner log-probs of the same tokens
             metrics["logprobs_diff_mean"] = float(((rl - data["action_log_probs"]).abs() * m).sum() / m.sum().clamp(min=1))
         metrics.update(self._train_policy(data))
+        self._mark("train")
         self._sync_weights()
+        self._mark("weight_sync")
         self.global_step += 1
         return metrics
 
