@@ -53,6 +53,7 @@ class RequestParams:
     min_p: float = 0.0
     logprobs: Optional[int] = None
     stop_token_ids: Tuple[int, ...] = ()
+    stop: Tuple[str, ...] = ()  # stop strings (need the engine's tokenizer), kept in the output text
     ignore_eos: bool = False
     seed: Optional[int] = None
 
@@ -79,8 +80,7 @@ class RequestParams:
             elif k == "ignore_eos":
                 p.ignore_eos = bool(v)
             elif k == "stop":
-                if v:
-                    raise ValueError("string stop sequences need a detokenizer; pass stop_token_ids instead")
+                p.stop = tuple([v] if isinstance(v, str) else (v or ()))
             elif k == "n":
                 if v not in (None, 1):
                     raise ValueError("n > 1 is not supported: replicate prompts (vllm_engine.py:133-136)")
@@ -158,8 +158,10 @@ class EngineCore:
     """Scheduler over a runner with `execute(batch) -> (tokens int64 [n], logprobs f32 [n])`."""
 
     def __init__(self, runner, num_blocks: int, max_num_seqs: int = 512, max_model_len: int = 4096,
-                 max_prefill_tokens: int = 32768, eos_token_id: Optional[int] = None, seed: int = 0):
+                 max_prefill_tokens: int = 32768, eos_token_id: Optional[int] = None, seed: int = 0,
+                 detokenize: Optional[Callable[[List[int]], str]] = None):
         self.runner = runner
+        self.detokenize = detokenize  # stop strings are matched on the decoded tail of the output
         self.allocator = BlockAllocator(num_blocks)
         self.max_num_seqs = max_num_seqs
         self.max_model_len = max_model_len
@@ -184,6 +186,8 @@ class EngineCore:
             raise ValueError(f"prompt of {len(prompt)} tokens exceeds max_model_len={self.max_model_len}")
         if _blocks_needed(len(prompt) + 1) > self.allocator.num_blocks:
             raise ValueError("prompt does not fit in the KV cache")
+        if params.stop and self.detokenize is None:
+            raise ValueError("string stop sequences need the engine's tokenizer; pass stop_token_ids instead")
         rid = next(self._rid)
         key = (int(params.seed) & ((1 << 42) - 1)) | (1 << 42) if params.seed is not None else rid
         req = Request(rid=rid, prompt=prompt, params=params, key=key, on_finish=on_finish)
@@ -332,6 +336,10 @@ class EngineCore:
                 return "stop"
             if not p.ignore_eos and self.eos_token_id is not None and tok == self.eos_token_id:
                 return "stop"
+            if p.stop:  # a token covers >= 1 character: the last max-len tokens hold any new match
+                tail = self.detokenize(r.out_tokens[-(max(len(s) for s in p.stop) + 1):])
+                if any(s in tail for s in p.stop):
+                    return "stop"
         if n >= p.max_tokens or r.num_tokens >= self.max_model_len:
             return "length"
         return None
@@ -586,17 +594,28 @@ class AMDInferenceEngine(InferenceEngineInterface):
                                                                          use_graphs=use_graphs)
         self.core = EngineCore(self.runner, num_blocks, max_num_seqs=max_num_seqs,
                                max_model_len=model.max_model_len, max_prefill_tokens=max_prefill_tokens,
-                               eos_token_id=model.spec.eos_token_id, seed=seed)
+                               eos_token_id=model.spec.eos_token_id, seed=seed,
+                               detokenize=(lambda ids: tokenizer.decode(ids, skip_special_tokens=True))
+                               if tokenizer is not None else None)
         self._task: Optional[asyncio.Task] = None
         self._futures: Dict[int, asyncio.Future] = {}
         self._receiver = None
         self._offloaded = None
 
     # ---------------------------------------------------------------- generation
-    def _decode_text(self, ids: List[int]) -> str:
+    def _decode_text(self, r: Request) -> str:
         if self.tokenizer is None:
             return ""
-        return self.tokenizer.decode(ids, skip_special_tokens=True)
+        text = self.tokenizer.decode(r.out_tokens, skip_special_tokens=True)
+        if r.finish_reason == "stop" and r.params.stop and r.out_tokens:
+            # include_stop_str_in_output: cut after the stop string the last token completed
+            # (vLLM searches only the newly added characters plus one stop length back)
+            new = len(self.tokenizer.decode(r.out_tokens[-1:], skip_special_tokens=True))
+            for s in r.params.stop:
+                i = text.find(s, max(0, len(text) - new - len(s)))
+                if i >= 0:
+                    return text[:i + len(s)]
+        return text
 
     def _submit(self, prompt: List[int], params: RequestParams) -> asyncio.Future:
         loop = asyncio.get_running_loop()
@@ -628,7 +647,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
 
     def _output(self, reqs: List[Request], want_logprobs: bool) -> InferenceEngineOutput:
         return InferenceEngineOutput(
-            responses=[self._decode_text(r.out_tokens) for r in reqs],
+            responses=[self._decode_text(r) for r in reqs],
             stop_reasons=[r.finish_reason for r in reqs],
             response_ids=[list(r.out_tokens) for r in reqs],
             response_logprobs=[list(r.out_logprobs) for r in reqs] if want_logprobs else None,

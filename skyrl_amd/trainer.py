@@ -56,8 +56,12 @@ class GRPOTrainer:
     the KL loss is off); client: an InferenceEngineClient (or one engine) whose weights mirror the
     policy; reward_fn(prompt_ids, response_ids, extra) -> float."""
 
-    def __init__(self, cfg: TrainerConfig, policy, client, reward_fn: Callable[..., float], pad_token_id: int,
-                 ref=None):
+    def __init__(self, cfg: TrainerConfig, policy, client, reward_fn: Optional[Callable[..., float]], pad_token_id: int,
+                 ref=None, generator=None, env_class: Optional[str] = None):
+        """With `generator` (a SkyRLGymGenerator over the same client) `step` takes chat prompts and
+        env extras and runs the multi-turn agent loop: rewards and loss masks come from it."""
+        self.generator = generator
+        self.env_class = env_class
         self.cfg = cfg
         self.policy = policy
         self.ref = ref
@@ -119,12 +123,25 @@ class GRPOTrainer:
         self.timings = {}
         torch.cuda.synchronize()
         self._t = time.perf_counter()
-        gen = asyncio.run(self._generate(prompts))
+        ext = extras or [None] * len(prompts)
+        if self.generator is not None:  # multi-turn agent loop: per-token rewards + observation masks
+            from .generators import TrajectoryID
+            from .generators.skyrl_gym_generator import get_vllm_sampling_params
+
+            gen = asyncio.run(self.generator.generate({
+                "sampling_params": get_vllm_sampling_params(self.generator.cfg.sampling_params),
+                "prompts": [p for p in prompts for _ in range(G)],
+                "env_classes": [self.env_class] * (G * len(prompts)),
+                "env_extras": [dict(e or {}) for e in ext for _ in range(G)],
+                "trajectory_ids": [TrajectoryID(f"{self.global_step}_{i}", j) for i in range(len(prompts))
+                                   for j in range(G)]}))
+        else:
+            gen = asyncio.run(self._generate(prompts))
         self._mark("generate")
         uids = [str(i // G) for i in range(len(gen["response_ids"]))]
-        ext = extras or [None] * len(prompts)
-        gen["rewards"] = [float(self.reward_fn(p, r, ext[i // G]))
-                          for i, (p, r) in enumerate(zip(gen["prompt_token_ids"], gen["response_ids"]))]
+        if self.generator is None:
+            gen["rewards"] = [float(self.reward_fn(p, r, ext[i // G]))
+                              for i, (p, r) in enumerate(zip(gen["prompt_token_ids"], gen["response_ids"]))]
         gen, metrics = trainer_utils.postprocess_generator_output(gen, uids, G)
         data = trainer_utils.convert_to_training_input(gen, uids, self.pad_token_id, dp_size=1,
                                                        device=next(self.policy.parameters()).device)

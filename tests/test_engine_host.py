@@ -81,10 +81,37 @@ def test_request_params_parse():
     assert (p.max_tokens, p.min_tokens, p.top_k, p.logprobs) == (8, 1, 50, 0)
     with pytest.raises(ValueError):
         RequestParams.from_dict({"n": 2})
-    with pytest.raises(ValueError):
-        RequestParams.from_dict({"stop": ["\n"]})
+    assert RequestParams.from_dict({"stop": ["</sql>", "x"]}).stop == ("</sql>", "x")
+    assert RequestParams.from_dict({"stop": "\n"}).stop == ("\n",)
+    with pytest.raises(ValueError):  # stop strings need a tokenizer in the engine
+        EngineCore(FakeRunner(10), 10).add_request([1], RequestParams(stop=("\n",)))
     with pytest.raises(ValueError):
         RequestParams.from_dict({"bogus": 1})
+
+
+def test_stop_strings_end_a_request_and_cut_the_text():
+    """vLLM semantics: a stop string in the decoded output finishes the request with "stop" (not
+    before min_tokens); the response text ends with it (include_stop_str_in_output)."""
+    chars = "abcdefghijklmnopqrstuvwxyz</>"
+
+    class CharTok:
+        def decode(self, ids, skip_special_tokens=True):
+            return "".join(chars[i % len(chars)] for i in ids)
+
+    class ScriptRunner(FakeRunner):
+        def execute(self, batch):
+            toks = [chars.index("</sql>"[len(r.out_tokens) % 6]) if r.prompt[0] == 0 else 0 for r in batch.requests]
+            return np.array(toks, dtype=np.int64), np.zeros(len(toks), dtype=np.float32)
+
+    model = SimpleNamespace(max_model_len=256, spec=SimpleNamespace(eos_token_id=None))
+    eng = AMDInferenceEngine(model, num_blocks=50, max_num_seqs=4, runner=ScriptRunner(50), tokenizer=CharTok())
+    out = asyncio.run(eng.generate({"prompt_token_ids": [[0, 1], [1, 2]],
+                                    "sampling_params": {"max_tokens": 20, "stop": ["sql>"], "min_tokens": 1}}))
+    assert out["stop_reasons"] == ["stop", "length"]
+    assert out["responses"][0] == "</sql>" and len(out["response_ids"][0]) == 6
+    out = asyncio.run(eng.generate({"prompt_token_ids": [[0, 1]],
+                                    "sampling_params": {"max_tokens": 20, "stop": ["sql>"], "min_tokens": 9}}))
+    assert out["stop_reasons"] == ["stop"] and out["responses"][0] == "</sql></sql>" and len(out["response_ids"][0]) == 12
 
 
 @pytest.mark.parametrize("num_blocks", [400, 12])
