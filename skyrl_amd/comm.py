@@ -410,3 +410,94 @@ class BroadcastWeightReceiver:
         for name, shape, n in zip(request.names, request.shapes, sizes):
             yield name, flat[off:off + n].view(shape)
             off += n
+
+
+# ------------------------------------------------------------- a14 sharded-source broadcast
+class ShardedBroadcastWeightSender:
+    """Separated placement with every learner rank as a source: the packed bf16
+    parameter stream is cut into `len(src_ranks)` contiguous shards and learner rank i
+    broadcasts shard i, all shards in flight at once (async collectives), so the traffic
+    leaves from every learner GPU's links instead of one rank's. The reference broadcasts
+    each parameter from rank 0 (broadcast_strategy.py:98-142)."""
+
+    def __init__(self, src_ranks: Sequence[int], group=None, dtype: torch.dtype = torch.bfloat16):
+        self.src_ranks, self.group, self.dtype = list(src_ranks), group, dtype
+
+    @staticmethod
+    def shard_bounds(total: int, nshards: int) -> List[Tuple[int, int]]:
+        per = -(-total // nshards)
+        per = -(-per // _ALIGN) * _ALIGN
+        return [(min(i * per, total), min((i + 1) * per, total)) for i in range(nshards)]
+
+    def send(self, named: Sequence[Tuple[str, torch.Tensor]]) -> "WeightUpdateRequest":
+        """Every learner rank calls this with the same (name, tensor) list; returns the metadata
+        the receivers need (the reference sends it by RPC)."""
+        req = WeightUpdateRequest([n for n, _ in named], [str(self.dtype)] * len(named),
+                                  [list(t.shape) for _, t in named])
+        flat = torch.cat([t.detach().reshape(-1).to(self.dtype) for _, t in named])
+        _sharded_broadcast(flat, self.src_ranks, self.group)
+        return req
+
+
+class ShardedBroadcastWeightReceiver:
+    """Receiving side of ShardedBroadcastWeightSender: one buffer, per-shard async broadcasts
+    into slices of it, then zero-copy per-parameter views."""
+
+    def __init__(self, src_ranks: Sequence[int], model_dtype: torch.dtype = torch.bfloat16, group=None, device=None):
+        self.src_ranks, self.dtype, self.group = list(src_ranks), model_dtype, group
+        self.device = device if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+
+    def receive_weights(self, request: "WeightUpdateRequest") -> Iterator[Tuple[str, torch.Tensor]]:
+        sizes = [int(math.prod(s)) for s in request.shapes]
+        flat = torch.empty(sum(sizes), dtype=self.dtype, device=self.device)
+        _sharded_broadcast(flat, self.src_ranks, self.group)
+        off = 0
+        for name, shape, n in zip(request.names, request.shapes, sizes):
+            yield name, flat[off:off + n].view(shape)
+            off += n
+
+
+def _sharded_broadcast(flat: torch.Tensor, src_ranks: Sequence[int], group) -> None:
+    works = []
+    for (a, b), src in zip(ShardedBroadcastWeightSender.shard_bounds(flat.numel(), len(src_ranks)), src_ranks):
+        if b > a:
+            works.append(dist.broadcast(flat[a:b], src, group=group, async_op=True))
+    for w in works:
+        w.wait()
+
+
+# ------------------------------------------------------------- a12 for module parameters
+def allreduce_grads(params: Iterable[torch.Tensor], group=None, bucket_bytes: int = 64 << 20) -> int:
+    """Mean of `.grad` over the DP group for parameters that are not views of a flat buffer
+    (a HF module under the GRPOTrainer): grads are packed into ~bucket_bytes fp32 buckets, one
+    SUM all-reduce per bucket, scaled by 1/world and copied back (FSDP's mean reduce,
+    fsdp_strategy.py:216-226). Returns the number of collectives issued."""
+    world, _ = _world(group)
+    grads = [p.grad for p in params if p.grad is not None]
+    if world == 1 or not grads:
+        return 0
+    n = 0
+    bucket: List[torch.Tensor] = []
+    size = 0
+
+    def flush():
+        nonlocal n
+        flat = torch.cat([g.reshape(-1).to(torch.float32) for g in bucket])
+        dist.all_reduce(flat, group=group)
+        flat.mul_(1.0 / world)
+        off = 0
+        for g in bucket:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+        n += 1
+
+    for g in grads:
+        bucket.append(g)
+        size += g.numel() * 4
+        if size >= bucket_bytes:
+            flush()
+            bucket, size = [], 0
+    if bucket:
+        flush()
+    return n

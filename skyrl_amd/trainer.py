@@ -24,7 +24,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import torch
 
-from . import ppo_utils, trainer_utils
+from . import comm, ppo_utils, trainer_utils
 from .config import AlgorithmConfig
 from .lmhead import lmhead_logprobs_and_entropy
 
@@ -57,9 +57,13 @@ class GRPOTrainer:
     policy; reward_fn(prompt_ids, response_ids, extra) -> float."""
 
     def __init__(self, cfg: TrainerConfig, policy, client, reward_fn: Optional[Callable[..., float]], pad_token_id: int,
-                 ref=None, generator=None, env_class: Optional[str] = None):
+                 ref=None, generator=None, env_class: Optional[str] = None, dp_group=None):
         """With `generator` (a SkyRLGymGenerator over the same client) `step` takes chat prompts and
-        env extras and runs the multi-turn agent loop: rewards and loss masks come from it."""
+        env extras and runs the multi-turn agent loop: rewards and loss masks come from it.
+        Under data parallelism (one process per GPU, `dp_group` initialised) every rank steps on
+        its own prompts with its own colocated engine; gradients are mean-reduced in buckets
+        before clipping (comm.allreduce_grads) and metrics are all-reduced."""
+        self.dp_group = dp_group
         self.generator = generator
         self.env_class = env_class
         self.cfg = cfg
@@ -186,6 +190,7 @@ class GRPOTrainer:
                     loss, met = self._loss(lp, data, i, j, ref, ent)
                     (loss / n_micro).backward()
                     mets.append(met)
+                comm.allreduce_grads(self.policy.parameters(), self.dp_group)
                 grad_norm = torch.nn.utils.clip_grad_norm_(self.policy.parameters(), cfg.max_grad_norm)
                 self.optimizer.step()
                 self.optimizer.zero_grad(set_to_none=True)
@@ -193,7 +198,8 @@ class GRPOTrainer:
                 for k, v in (("final_loss", mt[0]), ("policy_loss", mt[1]), ("policy_entropy", mt[2]),
                              ("policy_kl", mt[3]), ("ppo_clip_ratio", mt[4]), ("grad_norm", float(grad_norm))):
                     acc.setdefault(k, []).append(v)
-        return trainer_utils.reduce_metrics(acc)
+        return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
+                                       device=next(self.policy.parameters()).device)
 
     def _loss(self, lp, data, i, j, ref, ent):
         from . import ops

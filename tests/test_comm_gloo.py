@@ -170,3 +170,48 @@ def test_weight_update_request_validation():
         comm.WeightUpdateRequest(["a"], [], [[1]])
     r = comm.WeightUpdateRequest(["a"], ["torch.bfloat16"], [[2, 3]])
     assert comm.WeightUpdateRequest.from_json_dict(r.to_json_dict()) == r
+
+
+# --------------------------------------------------------------------------- a14 sharded sources
+def _sharded_bcast_case(rank, world):
+    learners = [0, 1]  # ranks 0, 1 learn; rank 2 is a rollout engine
+    g = torch.Generator().manual_seed(0)
+    named = [("model.embed_tokens.weight", torch.randn(37, 16, generator=g)),
+             ("model.norm.weight", torch.randn(16, generator=g)),
+             ("model.layers.0.mlp.up_proj.weight", torch.randn(48, 16, generator=g))]
+    if rank in learners:
+        req = comm.ShardedBroadcastWeightSender(learners).send(named)
+        assert req.names == [n for n, _ in named]
+    else:
+        req = comm.WeightUpdateRequest([n for n, _ in named], ["torch.bfloat16"] * 3, [list(t.shape) for _, t in named])
+        got = dict(comm.ShardedBroadcastWeightReceiver(learners, device="cpu").receive_weights(req))
+        for n, t in named:
+            assert torch.equal(got[n], t.to(torch.bfloat16)), n  # bit-exact bf16 copy
+
+
+def test_sharded_source_weight_broadcast_gloo():
+    _run(_sharded_bcast_case, world=3)
+
+
+def _grad_allreduce_case(rank, world):
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4))
+    x = torch.randn(6, 8, generator=torch.Generator().manual_seed(rank))
+    m(x).pow(2).sum().backward()
+    mine = [p.grad.clone() for p in m.parameters()]
+    n = comm.allreduce_grads(m.parameters(), bucket_bytes=256)
+    assert n >= 2  # several buckets
+    # reference: the mean of every rank's gradient (recomputed locally for both ranks)
+    ref = []
+    for r in range(world):
+        mm = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4))
+        mm.load_state_dict(m.state_dict())
+        mm(torch.randn(6, 8, generator=torch.Generator().manual_seed(r))).pow(2).sum().backward()
+        ref.append([p.grad for p in mm.parameters()])
+    for p, *gs in zip(m.parameters(), *ref):
+        torch.testing.assert_close(p.grad, sum(gs) / world, rtol=1e-6, atol=1e-6)
+    assert any(not torch.equal(a, p.grad) for a, p in zip(mine, m.parameters()))
+
+
+def test_allreduce_grads_gloo():
+    _run(_grad_allreduce_case)
