@@ -112,6 +112,8 @@ class Request:
     blocks: List[int] = field(default_factory=list)
     state: int = WAITING
     row: int = -1  # persistent batch row while running (the runner's per-row device state)
+    num_cached: int = 0  # leading tokens whose K/V came from the prefix cache at admission
+    block_hashes: List[int] = field(default_factory=list)
     finish_reason: Optional[str] = None
     on_finish: Optional[Callable[["Request"], None]] = None
 
@@ -121,24 +123,84 @@ class Request:
 
 
 class BlockAllocator:
-    """Free list of KV-cache blocks (LIFO: recently freed blocks are reused first)."""
+    """Reference-counted KV-cache blocks with an optional prefix cache.
 
-    def __init__(self, num_blocks: int):
+    Plain blocks return to a LIFO free list when their last user releases them. With prefix
+    caching, a full block of a prefill input is registered under the chain hash of its tokens
+    (hash of the previous block's hash and its 16 ids); when released it stays resident and
+    evictable (LRU) so a later request with the same prefix can share it read-only — vLLM's
+    automatic prefix caching (enable_prefix_caching, ppo_base_config.yaml generator section),
+    which GRPO's n_samples_per_prompt identical prompts hit."""
+
+    def __init__(self, num_blocks: int, enable_caching: bool = False):
         self.num_blocks = num_blocks
+        self.enable_caching = enable_caching
         self._free: List[int] = list(range(num_blocks - 1, -1, -1))
+        self._ref = [0] * num_blocks
+        self._hash_of: Dict[int, int] = {}
+        self._by_hash: Dict[int, int] = {}
+        self._evictable: "collections.OrderedDict[int, None]" = collections.OrderedDict()
+        self.hits = 0
 
     @property
     def num_free(self) -> int:
-        return len(self._free)
+        return len(self._free) + len(self._evictable)
 
     def allocate(self, n: int) -> List[int]:
-        if n > len(self._free):
+        if n > self.num_free:
             raise RuntimeError("out of KV-cache blocks")
-        out = [self._free.pop() for _ in range(n)]
+        out = []
+        for _ in range(n):
+            if self._free:
+                b = self._free.pop()
+            else:  # evict the least recently released cached block
+                b, _ = self._evictable.popitem(last=False)
+                del self._by_hash[self._hash_of.pop(b)]
+            self._ref[b] = 1
+            out.append(b)
         return out
 
     def free(self, blocks: Iterable[int]) -> None:
-        self._free.extend(reversed(list(blocks)))
+        for b in reversed(list(blocks)):
+            self._ref[b] -= 1
+            if self._ref[b] == 0:
+                if b in self._hash_of:
+                    self._evictable[b] = None
+                else:
+                    self._free.append(b)
+
+    # ---- prefix cache
+    def lookup(self, h: int) -> Optional[int]:
+        return self._by_hash.get(h)
+
+    def acquire(self, b: int) -> None:
+        """Take a reference on a cached block (found by lookup)."""
+        if self._ref[b] == 0:
+            del self._evictable[b]
+        self._ref[b] += 1
+        self.hits += 1
+
+    def register(self, b: int, h: int) -> None:
+        if self.enable_caching and h not in self._by_hash and b not in self._hash_of:
+            self._by_hash[h] = b
+            self._hash_of[b] = h
+
+    def reset(self) -> None:
+        """Forget every cached prefix (after a weight update the cached K/V are stale)."""
+        for b in self._evictable:
+            self._free.append(b)
+        self._evictable.clear()
+        self._hash_of.clear()
+        self._by_hash.clear()
+
+
+def block_hashes(tokens: Sequence[int], nblocks: int) -> List[int]:
+    """Chain hashes of the first `nblocks` full 16-token blocks."""
+    out, h = [], 0
+    for i in range(nblocks):
+        h = hash((h, tuple(tokens[i * BLOCK_SIZE:(i + 1) * BLOCK_SIZE])))
+        out.append(h)
+    return out
 
 
 @dataclass
@@ -159,10 +221,10 @@ class EngineCore:
 
     def __init__(self, runner, num_blocks: int, max_num_seqs: int = 512, max_model_len: int = 4096,
                  max_prefill_tokens: int = 32768, eos_token_id: Optional[int] = None, seed: int = 0,
-                 detokenize: Optional[Callable[[List[int]], str]] = None):
+                 detokenize: Optional[Callable[[List[int]], str]] = None, enable_prefix_caching: bool = False):
         self.runner = runner
         self.detokenize = detokenize  # stop strings are matched on the decoded tail of the output
-        self.allocator = BlockAllocator(num_blocks)
+        self.allocator = BlockAllocator(num_blocks, enable_caching=enable_prefix_caching)
         self.max_num_seqs = max_num_seqs
         self.max_model_len = max_model_len
         self.max_prefill_tokens = max_prefill_tokens
@@ -233,24 +295,53 @@ class EngineCore:
 
     # ---------------------------------------------------------------- scheduling
     def _schedule_prefill(self) -> List[Request]:
+        """Admit waiting requests (FIFO) while rows, blocks and the padded-token budget last.
+        With prefix caching a request takes the cached blocks of its longest cached prefix
+        (never the block of its last token, which must be computed for its logits); a request
+        whose next uncached block is being computed by an earlier request of this same batch
+        waits one step, so the GRPO siblings of a prompt share its prefill."""
+        alloc = self.allocator
         batch: List[Request] = []
+        deferred: List[Request] = []
+        pending = set()
         padded_max = 0
         while self.waiting and len(self.running) + len(batch) < self.max_num_seqs:
             r = self.waiting[0]
-            n = r.num_tokens
-            need = _blocks_needed(n + 1)
-            lmax = max(padded_max, n)
+            toks = r.prompt + r.out_tokens
+            n = len(toks)
+            hashes = block_hashes(toks, (n - 1) // BLOCK_SIZE) if alloc.enable_caching else []
+            cached = []
+            for h in hashes:
+                b = alloc.lookup(h)
+                if b is None:
+                    break
+                cached.append(b)
+            k = len(cached)
+            if k < len(hashes) and hashes[k] in pending:
+                deferred.append(self.waiting.popleft())
+                continue
+            lmax = max(padded_max, n - k * BLOCK_SIZE)
             if batch and lmax * (len(batch) + 1) > self.max_prefill_tokens:
                 break
-            if need > self.allocator.num_free:
+            need = _blocks_needed(n + 1) - k
+            if need > alloc.num_free - sum(1 for b in cached if b in alloc._evictable):
                 break
             self.waiting.popleft()
-            r.blocks = self.allocator.allocate(need)
+            for b in cached:
+                alloc.acquire(b)
+            r.blocks = cached + alloc.allocate(need)
+            r.num_cached = k * BLOCK_SIZE
+            r.block_hashes = hashes
+            pending.update(hashes[k:])
             r.row = heapq.heappop(self._free_rows)
             r.state = RUNNING
             batch.append(r)
             padded_max = lmax
+        self.waiting.extendleft(reversed(deferred))
         return batch
+
+    def reset_prefix_cache(self) -> None:
+        self.allocator.reset()
 
     def _ensure_decode_blocks(self) -> None:
         """Every running request needs the block holding position num_tokens-1; preempt the most
@@ -311,6 +402,9 @@ class EngineCore:
         t2 = time.perf_counter()
         if kind == "prefill":
             self.running.extend(batch)
+            for r in batch:  # the full blocks this prefill computed are now shareable
+                for i in range(r.num_cached // BLOCK_SIZE, len(r.block_hashes)):
+                    self.allocator.register(r.blocks[i], r.block_hashes[i])
         finished: List[Request] = []
         for r, t, lp in zip(batch, tokens.tolist(), logprobs.tolist()):
             r.out_tokens.append(t)
@@ -488,14 +582,23 @@ class ModelRunner:
         reqs = batch.requests
         n = len(reqs)
         if batch.kind == "prefill":
-            seqs = [r.prompt + r.out_tokens for r in reqs]
+            cached = [r.num_cached for r in reqs]  # prefix-cache hits: only the suffix is computed
+            seqs = [(r.prompt + r.out_tokens)[c:] for r, c in zip(reqs, cached)]
             lens = [len(s) for s in seqs]
             tok = np.fromiter(itertools.chain.from_iterable(seqs), dtype=np.int64, count=sum(lens))
-            pos = np.concatenate([np.arange(L, dtype=np.int64) for L in lens])
-            slots = np.concatenate([_slots(r.blocks, 0, L) for r, L in zip(reqs, lens)])
+            pos = np.concatenate([np.arange(c, c + L, dtype=np.int64) for c, L in zip(cached, lens)])
+            slots = np.concatenate([_slots(r.blocks, c, c + L) for r, c, L in zip(reqs, cached, lens)])
             packed = self._h2d(np.concatenate([tok, pos, slots]))
             T = tok.shape[0]
-            inp = StepInputs(tokens=packed[:T], positions=packed[T:2 * T], slots=packed[2 * T:], seq_lens=lens)
+            bt = None
+            if any(cached):
+                width = max(len(r.blocks) for r in reqs)
+                bt_np = np.zeros((n, width), dtype=np.int32)
+                for i, r in enumerate(reqs):
+                    bt_np[i, :len(r.blocks)] = r.blocks
+                bt = self._h2d(bt_np)
+            inp = StepInputs(tokens=packed[:T], positions=packed[T:2 * T], slots=packed[2 * T:], seq_lens=lens,
+                             cached_lens=cached, block_tables=bt)
             logits = self.model.logits(self.model.forward_prefill(inp, self.cache))
             for r in reqs:
                 self._nblk[r.row] = 0  # (re)admitted row: restage its whole table
@@ -577,7 +680,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
 
     def __init__(self, model, num_blocks: Optional[int] = None, max_num_seqs: int = 512,
                  max_prefill_tokens: int = 32768, seed: int = 0, kv_cache_fraction: float = 0.5,
-                 tokenizer=None, runner=None, use_graphs: bool = True):
+                 tokenizer=None, runner=None, use_graphs: bool = True, enable_prefix_caching: bool = True):
         self.model = model
         self.tokenizer = tokenizer
         if num_blocks is None:
@@ -596,7 +699,8 @@ class AMDInferenceEngine(InferenceEngineInterface):
                                max_model_len=model.max_model_len, max_prefill_tokens=max_prefill_tokens,
                                eos_token_id=model.spec.eos_token_id, seed=seed,
                                detokenize=(lambda ids: tokenizer.decode(ids, skip_special_tokens=True))
-                               if tokenizer is not None else None)
+                               if tokenizer is not None else None,
+                               enable_prefix_caching=enable_prefix_caching)
         self._task: Optional[asyncio.Task] = None
         self._futures: Dict[int, asyncio.Future] = {}
         self._receiver = None
@@ -687,6 +791,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
             self.core.abort_all()
         level = kwargs.get("level", 2)
         self.runner.release_cache()
+        self.core.reset_prefix_cache()
         if level == 1:
             self._offloaded = [(n, t.detach().to("cpu")) for n, t in self.model.hf_named_tensors()]
         self.model.release()
@@ -726,10 +831,11 @@ class AMDInferenceEngine(InferenceEngineInterface):
             if self._receiver is None:
                 raise RuntimeError("init_weight_update_communicator was not called")
             n = self.model.load_weights(self._receiver.receive_weights(request))
+        self.core.reset_prefix_cache()  # cached K/V were computed by the old weights
         return n
 
     async def reset_prefix_cache(self):
-        return None  # no prefix cache: every prompt is prefilled
+        self.core.reset_prefix_cache()
 
     async def teardown(self):
         self.core.abort_all()

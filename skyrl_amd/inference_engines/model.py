@@ -108,8 +108,9 @@ class StepInputs:
     context_lens: Optional[torch.Tensor] = None  # int32 [n]
     max_ctx: int = 0
     nparts: Optional[int] = None  # decode waves per (sequence, kv head); None: chosen per call
-    # prefill only: sequence lengths (host) of the ragged token batch
+    # prefill only: tokens computed per sequence (host) and the cached prefix each starts after
     seq_lens: Optional[List[int]] = None
+    cached_lens: Optional[List[int]] = None
 
 
 class PagedDecoder:
@@ -247,39 +248,72 @@ class PagedDecoder:
         return self._run_layers(h, attention)
 
     def forward_prefill(self, inp: StepInputs, cache: PagedKVCache) -> torch.Tensor:
-        """Ragged prompts (total T tokens, lengths inp.seq_lens): writes their K/V into the cache
-        and returns the final hidden state of each sequence's last token [B, H].
-        Attention over each prompt is causal SDPA on a right-padded batch (no prefix cache)."""
+        """Ragged prefill (total T tokens; per sequence inp.seq_lens tokens starting at position
+        inp.cached_lens[i]): writes their K/V into the cache and returns the final hidden state of
+        each sequence's last token [B, H].
+
+        Sequences without a cached prefix attend with causal SDPA on a right-padded batch of
+        their own tokens. Sequences whose leading blocks came from the prefix cache compute
+        only their suffix: each suffix token is one query row of the paged decode kernel over
+        its sequence's block table with context = position + 1 (its K/V, and those of the
+        suffix tokens before it, are written by rope_kv_write first)."""
         s = self.spec
-        lens = inp.seq_lens
-        B, Lmax = len(lens), max(lens)
+        lens = list(inp.seq_lens)
+        cached = list(inp.cached_lens) if inp.cached_lens is not None else [0] * len(lens)
         T = int(sum(lens))
         dev = self.device
-        # flat index of (b, j) in the ragged batch, T for padding (points at a zero row)
-        starts = torch.tensor([0] + list(lens[:-1]), dtype=torch.int64).cumsum(0)
-        j = torch.arange(Lmax, dtype=torch.int64)
+        starts = torch.tensor([0] + lens[:-1], dtype=torch.int64).cumsum(0)
         lens_t = torch.tensor(lens, dtype=torch.int64)
-        pad_idx = torch.where(j[None] < lens_t[:, None], starts[:, None] + j[None], torch.full((1, 1), T))
-        pad_idx = pad_idx.to(dev, non_blocking=True)
-        valid = (j[None] < lens_t[:, None]).reshape(-1).nonzero().squeeze(1).to(dev, non_blocking=True)
         last = (starts + lens_t - 1).to(dev, non_blocking=True)
-        k_out = torch.empty((T, s.num_kv_heads, s.head_dim), dtype=self.dtype, device=dev)
+        full = [i for i, c in enumerate(cached) if c == 0]
+        part = [i for i, c in enumerate(cached) if c > 0]
+        nhd = s.num_heads * s.head_dim
+        k_out = torch.empty((T, s.num_kv_heads, s.head_dim), dtype=self.dtype, device=dev) if full else None
         rep = s.num_heads // s.num_kv_heads
+        if full:  # padded layout of the uncached sequences (T indexes a zero row)
+            fl = lens_t[full]
+            Lmax = int(fl.max())
+            j = torch.arange(Lmax, dtype=torch.int64)
+            inside = j[None] < fl[:, None]
+            pad_idx = torch.where(inside, starts[full][:, None] + j[None], torch.full((1, 1), T)).to(dev)
+            valid = inside.reshape(-1).nonzero().squeeze(1).to(dev)
+            tok_full = (starts[full][:, None] + j[None])[inside].to(dev)
+        if part:  # one decode-kernel row per suffix token
+            tok_part = torch.cat([torch.arange(int(starts[i]), int(starts[i]) + lens[i]) for i in part])
+            seq_of = torch.cat([torch.full((lens[i],), i, dtype=torch.int64) for i in part])
+            ctx = torch.cat([torch.arange(cached[i] + 1, cached[i] + lens[i] + 1, dtype=torch.int32) for i in part])
+            max_ctx = int(ctx.max())
+            bt = inp.block_tables.index_select(0, seq_of.to(dev))[:, :-(-max_ctx // BLOCK_SIZE)].contiguous()
+            tok_part, ctx = tok_part.to(dev), ctx.to(dev)
+
+        def attention(li, L, qkv):
+            q = kernels.rope_kv_write(qkv, inp.positions, inp.slots, self.cos_sin, s.num_heads, s.num_kv_heads,
+                                      s.head_dim, cache.k[li], cache.v[li], k_out=k_out)
+            if not part:
+                o = self._sdpa(q, k_out, qkv, T, pad_idx, rep)
+                return o.transpose(1, 2).reshape(-1, nhd)[valid]
+            o = torch.empty((T, nhd), dtype=self.dtype, device=dev)
+            if full:
+                of = self._sdpa(q, k_out, qkv, T, pad_idx, rep)
+                o.index_copy_(0, tok_full, of.transpose(1, 2).reshape(-1, nhd)[valid])
+            op = kernels.paged_decode(q.index_select(0, tok_part), cache.k[li], cache.v[li], bt, ctx, max_ctx,
+                                      self.scale, workspace=self.workspace)
+            o.index_copy_(0, tok_part, op.view(-1, nhd))
+            return o
+
+        h = F.embedding(inp.tokens, self.embed)
+        return self._run_layers(h, attention)[last]
+
+    def _sdpa(self, q, k, qkv, T, pad_idx, rep):
+        s = self.spec
+        v = qkv[:, (s.num_heads + s.num_kv_heads) * s.head_dim:].reshape(T, s.num_kv_heads, s.head_dim)
 
         def padded(t):
             z = torch.cat([t, t.new_zeros((1,) + tuple(t.shape[1:]))], 0)
             return z[pad_idx].transpose(1, 2)  # [B, heads, Lmax, D]
 
-        def attention(li, L, qkv):
-            q = kernels.rope_kv_write(qkv, inp.positions, inp.slots, self.cos_sin, s.num_heads, s.num_kv_heads,
-                                      s.head_dim, cache.k[li], cache.v[li], k_out=k_out)
-            v = qkv[:, (s.num_heads + s.num_kv_heads) * s.head_dim:].reshape(T, s.num_kv_heads, s.head_dim)
-            qp, kp, vp = padded(q), padded(k_out), padded(v)
-            o = F.scaled_dot_product_attention(qp, kp, vp, is_causal=True, scale=self.scale, enable_gqa=rep > 1)
-            return o.transpose(1, 2).reshape(B * Lmax, s.num_heads * s.head_dim)[valid]
-
-        h = F.embedding(inp.tokens, self.embed)
-        return self._run_layers(h, attention)[last]
+        return F.scaled_dot_product_attention(padded(q), padded(k), padded(v), is_causal=True, scale=self.scale,
+                                              enable_gqa=rep > 1)
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """lm_head: bf16 [n, V] (the sampler's input)."""

@@ -34,12 +34,18 @@ class FakeRunner:
         seen = {}
         rows = [r.row for r in batch.requests]
         assert len(set(rows)) == len(rows) and min(rows) >= 0, "persistent rows must be unique"
+        written = {}
         for r in batch.requests:
             need = (r.num_tokens + (1 if batch.kind == "prefill" else 0) + BLOCK_SIZE - 1) // BLOCK_SIZE
             assert len(r.blocks) >= min(need, (r.num_tokens + BLOCK_SIZE - 1) // BLOCK_SIZE)
-            for b in r.blocks:
+            first = r.num_cached if batch.kind == "prefill" else r.num_tokens - 1  # first position written
+            for i, b in enumerate(r.blocks):
                 assert 0 <= b < self.num_blocks
-                assert seen.setdefault(b, r.rid) == r.rid, "block shared by two running requests"
+                seen.setdefault(b, set()).add(r.rid)
+                if (i + 1) * BLOCK_SIZE > first and i * BLOCK_SIZE < r.num_tokens:
+                    assert written.setdefault(b, r.rid) == r.rid, "a block written this step is written twice"
+        for b, rid in written.items():  # shared (prefix-cached) blocks are read-only
+            assert seen[b] == {rid}, "a block written this step is also read by another request"
         toks = np.array([next_token(r.prompt + r.out_tokens, sup) for r, sup in zip(batch.requests, batch.suppress)],
                         dtype=np.int64)
         lps = -np.arange(len(toks), dtype=np.float32) / 10
@@ -297,3 +303,61 @@ def test_model_runner_stages_decode_rows():
     runner._stage_decode([a], 1)
     assert runner.d_i32[0, 0:3].tolist() == [5, 9, 17] and runner.d_i64[2, 0].item() == 17 * 16 + 0
     assert torch.equal(runner.d_ctx[:1], torch.tensor([33], dtype=torch.int32))
+
+
+def test_block_allocator_prefix_cache():
+    from skyrl_amd.inference_engines.engine import BlockAllocator, block_hashes
+
+    a = BlockAllocator(4, enable_caching=True)
+    b = a.allocate(2)
+    h = block_hashes(list(range(40)), 2)
+    assert h == block_hashes(list(range(32)) + [9] * 8, 2) and h != block_hashes(list(range(1, 41)), 2)
+    a.register(b[0], h[0])
+    a.register(b[1], h[1])
+    a.free(b)
+    assert a.num_free == 4 and a.lookup(h[0]) == b[0]  # released but still cached (evictable)
+    a.acquire(b[0])
+    assert a.num_free == 3
+    c = a.allocate(3)  # 2 plain free blocks, then evicts the LRU cached block (b[1])
+    assert b[1] in c and a.lookup(h[1]) is None and a.lookup(h[0]) == b[0]
+    a.free(c + [b[0]])
+    a.reset()
+    assert a.lookup(h[0]) is None and a.num_free == 4
+
+
+def test_prefix_caching_shares_prompt_blocks_and_keeps_outputs():
+    """GRPO shape: 3 prompts x 4 samples. With the prefix cache the siblings of a prompt reuse
+    its full prompt blocks (read-only) and compute only the tail; the tokens are unchanged."""
+    rng = np.random.default_rng(3)
+    prompts = [rng.integers(0, V, size=int(n)).tolist() for n in (40, 17, 70)]
+    results = {}
+    for caching in (False, True):
+        runner = FakeRunner(200)
+        seen_cached = []
+        orig = runner.execute
+
+        def execute(batch, orig=orig, seen=seen_cached, caching=caching):
+            if batch.kind == "prefill":
+                for r in batch.requests:
+                    seen.append(r.num_cached)
+                    k = r.num_cached // BLOCK_SIZE
+                    assert r.num_cached % BLOCK_SIZE == 0 and r.num_cached < r.num_tokens
+                    if caching:
+                        assert len(r.block_hashes) == (r.num_tokens - 1) // BLOCK_SIZE and k <= len(r.block_hashes)
+            return orig(batch)
+
+        runner.execute = execute
+        core = EngineCore(runner, 200, max_num_seqs=16, max_model_len=200, enable_prefix_caching=caching)
+        reqs = [core.add_request(p, RequestParams(max_tokens=12, ignore_eos=True)) for p in prompts for _ in range(4)]
+        first_blocks = {}
+        while core.has_unfinished():
+            core.step()
+            for r in core.running:
+                first_blocks.setdefault(tuple(r.prompt[:16]), set()).add(r.blocks[0])
+        results[caching] = [r.out_tokens for r in reqs]
+        assert core.allocator.num_free == 200
+        if caching:
+            assert seen_cached.count(0) == 3 and sum(c > 0 for c in seen_cached) == 9
+            assert all(len(v) == 1 for v in first_blocks.values())  # siblings share block 0
+            assert core.allocator.hits >= 9
+    assert results[True] == results[False]
