@@ -37,6 +37,7 @@ class TrainerConfig:
     micro_forward_batch_size_per_gpu: int = 1  # sequences per no-grad forward
     update_epochs_per_batch: int = 1
     lr: float = 1e-6
+    critic_lr: float = 5e-6                     # trainer.critic.optimizer_config.lr
     betas: Sequence[float] = (0.9, 0.999)
     weight_decay: float = 0.01
     max_grad_norm: float = 1.0
@@ -51,13 +52,37 @@ def _positions(attention_mask: torch.Tensor) -> torch.Tensor:
     return pos.masked_fill_(attention_mask == 0, 1)
 
 
+class CriticModel(torch.nn.Module):
+    """get_llm_for_sequence_regression's critic (model_wrapper.py:402-500): the HF base model plus
+    `value_head = Linear(H, 1, bias=False)`; values of the last R action positions, i.e. the
+    hidden states at [-R-1:-1] like the action log-probs."""
+
+    def __init__(self, hf_config, value_head_prefix: str = "value_head"):
+        super().__init__()
+        from transformers import AutoModel
+
+        self.model = AutoModel.from_config(hf_config)
+        self.value_head_prefix = value_head_prefix
+        setattr(self, value_head_prefix, torch.nn.Linear(hf_config.hidden_size, 1, bias=False))
+
+    def forward(self, seq: torch.Tensor, att: torch.Tensor, R: int) -> torch.Tensor:
+        h = self.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
+        return getattr(self, self.value_head_prefix)(h).squeeze(-1)[:, :-1][:, -R:]
+
+
 class GRPOTrainer:
     """policy: HF CausalLM (fp32 master weights) on the GPU; ref: frozen HF CausalLM (or None when
     the KL loss is off); client: an InferenceEngineClient (or one engine) whose weights mirror the
-    policy; reward_fn(prompt_ids, response_ids, extra) -> float."""
+    policy; reward_fn(prompt_ids, response_ids, extra) -> float. With `critic` (a CriticModel) the
+    step is PPO with a value function: values in the no-grad pass, advantages by the configured
+    estimator (GAE on the HIP kernel for advantage_estimator="gae"), critic update before the
+    policy update."""
 
     def __init__(self, cfg: TrainerConfig, policy, client, reward_fn: Optional[Callable[..., float]], pad_token_id: int,
-                 ref=None, generator=None, env_class: Optional[str] = None, dp_group=None):
+                 ref=None, generator=None, env_class: Optional[str] = None, dp_group=None, critic=None):
+        self.critic = critic
+        self.critic_optimizer = torch.optim.AdamW(critic.parameters(), lr=cfg.critic_lr, betas=tuple(cfg.betas),
+                                                  weight_decay=cfg.weight_decay, eps=1e-8) if critic else None
         """With `generator` (a SkyRLGymGenerator over the same client) `step` takes chat prompts and
         env extras and runs the multi-turn agent loop: rewards and loss masks come from it.
         Under data parallelism (one process per GPU, `dp_group` initialised) every rank steps on
@@ -120,6 +145,14 @@ class GRPOTrainer:
         return torch.cat([self._logprobs(model, seq[i:i + mb], att[i:i + mb], R, grad=False)[0]
                           for i in range(0, len(seq), mb)])
 
+    @torch.no_grad()
+    def _fwd_values(self, data) -> torch.Tensor:
+        seq, att = data["sequences"], data["attention_mask"]
+        R = data["response_mask"].shape[1]
+        mb = self.cfg.micro_forward_batch_size_per_gpu
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return torch.cat([self.critic(seq[i:i + mb], att[i:i + mb], R).float() for i in range(0, len(seq), mb)])
+
     # ---------------------------------------------------------------- step
     def step(self, prompts: List[List[int]], extras: Optional[List[Any]] = None) -> Dict[str, float]:
         cfg, alg = self.cfg, self.cfg.algorithm
@@ -154,6 +187,8 @@ class GRPOTrainer:
         data["action_log_probs"] = self._fwd_logprobs(self.policy, data)
         if self.ref is not None:
             data["base_action_log_probs"] = self._fwd_logprobs(self.ref, data)
+        if self.critic is not None:
+            data["values"] = self._fwd_values(data)
         self._mark("fwd_logprobs")
         data = trainer_utils.compute_advantages_and_returns(data, alg)
         self._mark("advantages")
@@ -162,12 +197,43 @@ class GRPOTrainer:
         rl = data["rollout_logprobs"]
         if rl is not None:  # rollout (engine) vs learner log-probs of the same tokens
             metrics["logprobs_diff_mean"] = float(((rl - data["action_log_probs"]).abs() * m).sum() / m.sum().clamp(min=1))
+        if self.critic is not None:  # train_critic_and_policy: the critic steps first (trainer.py:1085-1120)
+            metrics.update(self._train_critic(data))
         metrics.update(self._train_policy(data))
         self._mark("train")
         self._sync_weights()
         self._mark("weight_sync")
         self.global_step += 1
         return metrics
+
+    def _train_critic(self, data) -> Dict[str, float]:
+        """CriticWorkerBase._forward_backward_micro (worker.py:1062-1114) + optim_step: HIP clipped
+        value loss against the GAE returns, loss / n_micro, clip, AdamW."""
+        cfg = self.cfg
+        n = len(data["sequences"])
+        mini = cfg.policy_mini_batch_size * cfg.n_samples_per_prompt
+        mb = cfg.micro_train_batch_size_per_gpu
+        R = data["response_mask"].shape[1]
+        acc: Dict[str, List[float]] = {}
+        for s0, s1 in trainer_utils.mini_batch_slices(n, mini):
+            n_micro = math.ceil((s1 - s0) / mb)
+            for i in range(s0, s1, mb):
+                j = min(i + mb, s1)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    v = self.critic(data["sequences"][i:j], data["attention_mask"][i:j], R).float()
+                loss, clipfrac = ppo_utils.ppo_critic_loss(v, data["values"][i:j], data["returns"][i:j],
+                                                           cfg.algorithm, loss_mask=data["loss_mask"][i:j])
+                (loss / n_micro).backward()
+                acc.setdefault("critic_loss", []).append(float(loss.detach()))
+                if clipfrac is not None:
+                    acc.setdefault("values_clipfrac", []).append(clipfrac)
+            comm.allreduce_grads(self.critic.parameters(), self.dp_group)
+            gn = torch.nn.utils.clip_grad_norm_(self.critic.parameters(), cfg.max_grad_norm)
+            self.critic_optimizer.step()
+            self.critic_optimizer.zero_grad(set_to_none=True)
+            acc.setdefault("critic_grad_norm", []).append(float(gn))
+        return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
+                                       device=next(self.critic.parameters()).device)
 
     def _train_policy(self, data) -> Dict[str, float]:
         """_execute_training_step: mini-batches of policy_mini_batch_size prompts (no shuffle,
