@@ -732,7 +732,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
 
         req = self.core.add_request(prompt, params, on_finish=done)
         self._futures[req.rid] = fut
-        if self._task is None or self._task.done():
+        if self._task is None or self._task.done() or self._task.get_loop() is not loop:  # (a previous asyncio.run's loop)
             self._task = loop.create_task(self._run())
         return fut
 

@@ -175,10 +175,21 @@ class GRPOTrainer:
         else:
             gen = asyncio.run(self._generate(prompts))
         self._mark("generate")
-        uids = [str(i // G) for i in range(len(gen["response_ids"]))]
         if self.generator is None:
             gen["rewards"] = [float(self.reward_fn(p, r, ext[i // G]))
                               for i, (p, r) in enumerate(zip(gen["prompt_token_ids"], gen["response_ids"]))]
+        metrics = self.train_on(gen)
+        self._sync_weights()
+        self._mark("weight_sync")
+        return metrics
+
+    def train_on(self, gen: Dict[str, Any]) -> Dict[str, float]:
+        """Everything after generation for one batch of groups (G consecutive trajectories per
+        prompt, rewards filled in): pack, old/ref logprobs (+ values), advantages, critic and
+        policy updates. Advances global_step; the caller syncs the engine's weights."""
+        cfg, alg = self.cfg, self.cfg.algorithm
+        G = cfg.n_samples_per_prompt
+        uids = [str(i // G) for i in range(len(gen["response_ids"]))]
         gen, metrics = trainer_utils.postprocess_generator_output(gen, uids, G)
         data = trainer_utils.convert_to_training_input(gen, uids, self.pad_token_id, dp_size=1,
                                                        device=next(self.policy.parameters()).device)
@@ -201,8 +212,6 @@ class GRPOTrainer:
             metrics.update(self._train_critic(data))
         metrics.update(self._train_policy(data))
         self._mark("train")
-        self._sync_weights()
-        self._mark("weight_sync")
         self.global_step += 1
         return metrics
 
@@ -274,10 +283,13 @@ class GRPOTrainer:
                             self.loss_params, ref_log_probs=ref, entropy=ent)
 
     @torch.no_grad()
-    def _sync_weights(self):
+    def weight_update_request(self) -> Dict[str, Any]:
         """broadcast_to_inference_engines: bf16 copies of every parameter under its HF name."""
         names, tensors = [], []
         for name, p in self.policy.named_parameters():
             names.append(name)
             tensors.append(p.detach().to(torch.bfloat16))
-        asyncio.run(self.client.update_named_weights({"names": names, "tensors": tensors}))
+        return {"names": names, "tensors": tensors}
+
+    def _sync_weights(self):
+        asyncio.run(self.client.update_named_weights(self.weight_update_request()))
