@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}"
+ARGS="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-e2e}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 if [ "${PMC:-1}" = 1 ]; then
