@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--micro", type=int, default=16)
+    ap.add_argument("--tunable", action="store_true", help="TunableOp GEMM search in the rollout engine")
     args = ap.parse_args()
     from transformers import AutoModelForCausalLM, Qwen2Config
 
@@ -57,7 +58,9 @@ def main():
     engine_model = PagedDecoder(cfg, DEV, seed=None, max_model_len=512 + args.max_response + 16)
     engine_model.load_weights((n, p.detach().to(torch.bfloat16)) for n, p in policy.named_parameters())
     engine = AMDInferenceEngine(engine_model, num_blocks=None, max_num_seqs=args.prompts * args.group,
-                                kv_cache_fraction=0.15, seed=0)
+                                kv_cache_fraction=0.15, seed=0,
+                                tunable_gemm=os.path.join(os.environ.get("TMPDIR", "/tmp"), "skyrl_tunableop.csv")
+                                if args.tunable else None)
     log(f"models ready in {time.time() - t0:.1f}s; kv blocks {engine.num_blocks}")
     tcfg = TrainerConfig(n_samples_per_prompt=args.group, policy_mini_batch_size=args.prompts,
                          micro_train_batch_size_per_gpu=args.micro, micro_forward_batch_size_per_gpu=args.micro,
