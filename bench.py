@@ -348,6 +348,8 @@ def run(args):
     if not args.no_adv_loss_leg:
         result["advantage_loss"] = {"batch": advantage_loss_leg(dev, N, R),
                                     "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
+    if not args.no_attention_leg:
+        result["rollout_attention"] = rollout_attention_leg(dev, N)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -466,6 +468,57 @@ def advantage_loss_leg(dev, N, R, reps=20):
     return out
 
 
+def rollout_attention_leg(dev, nseq, reps=20):
+    """Rollout decode attention (csrc/attention.hip paged_decode_kernel) at the
+    headline shape: Qwen2.5-1.5B heads (12 q / 2 kv, D=128), one decode step of all nseq
+    trajectories with ragged contexts U[17, 1536] (prompt U[16,512] + responses up to 1024).
+    Algorithmic bytes = K+V of every live context token (nkv*D*2 B each, x2) + q + out, i.e.
+    1024 B/token; timed per launch with HIP events on the stream the kernel runs on."""
+    import math
+
+    from skyrl_amd.inference_engines import kernels
+
+    nh, nkv, D, BS = 12, 2, 128, 16
+    g = torch.Generator(device=dev).manual_seed(11)
+    ctx = torch.randint(17, 1537, (nseq,), device=dev, generator=g, dtype=torch.int32)
+    nb = (ctx + BS - 1) // BS
+    max_ctx = int(ctx.max())
+    width = (max_ctx + BS - 1) // BS
+    nblk = int(nb.sum())
+    kc = torch.randn(nblk, nkv, BS, D, device=dev, generator=g).to(torch.bfloat16)
+    vc = torch.randn(nblk, nkv, D, BS, device=dev, generator=g).to(torch.bfloat16)
+    perm = torch.randperm(nblk, device=dev, generator=g).int()  # scattered blocks, as after churn
+    bt = torch.zeros(nseq, width, dtype=torch.int32, device=dev)
+    starts = torch.cumsum(nb, 0) - nb
+    col = torch.arange(width, device=dev)
+    live = col[None] < nb[:, None]
+    bt[live] = perm[(starts[:, None] + col[None])[live]]
+    q = torch.randn(nseq, nh, D, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.empty_like(q)
+    ws = kernels.DecodeWorkspace(dev)
+    nparts = kernels.choose_nparts(nseq, nkv, max_ctx)
+    run = lambda: kernels.paged_decode(q, kc, vc, bt, ctx, max_ctx, 1 / math.sqrt(D), out=out,  # noqa: E731
+                                       workspace=ws, nparts=nparts)
+    run()
+    torch.cuda.synchronize(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        run()
+    b.record()
+    b.synchronize()
+    us = a.elapsed_time(b) * 1e3 / reps
+    tokens = int(ctx.sum())
+    nbytes = tokens * nkv * D * 2 * 2 + 2 * nseq * nh * D * 2
+    gbs = nbytes / (us * 1e-6) / 1e9
+    return {"kernel": "paged_decode_kernel<128> (+ reduce)", "seqs": nseq, "context_tokens": tokens,
+            "context_len": "U[17,1536]", "heads": f"{nh}q/{nkv}kv x {D}", "nparts": nparts,
+            "avg_launch_us": round(us, 2), "bytes_per_launch": nbytes, "achieved_GBps": round(gbs, 1),
+            "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "frac_of_measured_read_ceiling": round(gbs / CEILING_READ_GBS, 4),
+            "traffic": pmc_traffic("paged_decode_kernel", nbytes)}
+
+
 def cpu_baseline(args):
     """The oracle (CPU restatement, 'port') on a bounded sample of the same workload.
 
@@ -548,6 +601,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the real-model end-to-end leg (N=1 only)")
     ap.add_argument("--no-adv-loss-leg", action="store_true", help="skip the graph-replayed advantage+loss leg")
+    ap.add_argument("--no-attention-leg", action="store_true", help="skip the rollout paged-attention leg")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--params", type=int, default=QWEN_1_5B_PARAMS, help="policy parameter count (0: no optimizer leg)")

@@ -139,19 +139,40 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     for (int n = 0; n < NT; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, l = 0.f;
 
-    const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
+    // Block ids of this partition: one vector load of up to 64 table entries (one per lane),
+    // read back with readlane, so the per-block address chain has no dependent table load.
+    // K/V of block j+1 are issued before block j is computed (two blocks in flight per wave).
+    const int32_t* bt = block_tables + (int64_t)seq * bt_stride + t0 / kBS;
+    const int nb = (t1 - t0 + kBS - 1) / kBS;
+    int tbl = lane < nb ? bt[lane] : 0;
     const int64_t head_tile = (int64_t)kBS * D;
     const int64_t blk_stride = (int64_t)nkv * head_tile;
-    for (int tb = t0; tb < t1; tb += kBS) {
-        const int64_t blk = __builtin_amdgcn_readfirstlane(bt[tb / kBS]);
-        const uint16_t* kb = kc + blk * blk_stride + kvh * head_tile;
-        const uint16_t* vb = vc + blk * blk_stride + kvh * head_tile;
-        s16x8 kf[KS];
-        s16x4 vf[NT];
+    const uint16_t* kbase = kc + kvh * head_tile + c * D + 8 * g;
+    const uint16_t* vbase = vc + kvh * head_tile + c * kBS + 4 * g;
+    s16x8 kf[KS];
+    s16x4 vf[NT];
+    {
+        const int64_t blk = __builtin_amdgcn_readlane(tbl, 0);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const s16x8*>(kb + c * D + 32 * s + 8 * g);
+        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const s16x8*>(kbase + blk * blk_stride + 32 * s);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) vf[n] = *reinterpret_cast<const s16x4*>(vb + (16 * n + c) * kBS + 4 * g);
+        for (int n = 0; n < NT; ++n) vf[n] = *reinterpret_cast<const s16x4*>(vbase + blk * blk_stride + 16 * n * kBS);
+    }
+    for (int j = 0; j < nb; ++j) {
+        const int tb = t0 + j * kBS;
+        const bool more = j + 1 < nb;
+        s16x8 kn[KS];
+        s16x4 vn[NT];
+        if (more) {
+            if (((j + 1) & 63) == 0) tbl = (j + 1 + lane < nb) ? bt[j + 1 + lane] : 0;
+            const int64_t blk = __builtin_amdgcn_readlane(tbl, (j + 1) & 63);
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                kn[s] = *reinterpret_cast<const s16x8*>(kbase + blk * blk_stride + 32 * s);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                vn[n] = *reinterpret_cast<const s16x4*>(vbase + blk * blk_stride + 16 * n * kBS);
+        }
         f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], qf[s], sacc, 0, 0, 0);
@@ -193,6 +214,12 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
         for (int n = 0; n < NT; ++n) {
             o[n] = o[n] * alpha;
             o[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[n], pf, o[n], 0, 0, 0);
+        }
+        if (more) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) kf[s] = kn[s];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) vf[n] = vn[n];
         }
     }
     // o[n][i] = O^T[dim 16n + 4g + i][head c]; l is this lane's share of the row sum

@@ -75,13 +75,17 @@ def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
 MIN_PARTITION = 64  # context tokens: below this a wave's fixed cost outweighs its KV stream
 
 
-def choose_nparts(nseq: int, nkv: int, max_ctx: int, target_waves: int = 1024) -> int:
+def choose_nparts(nseq: int, nkv: int, max_ctx: int, target_waves: int = 1024, min_split: int = 1) -> int:
     """Waves per (sequence, kv head) for about ``target_waves`` waves in flight (256 CUs x 4;
-    measured: fewer, longer waves beat finer splits down to that count),
-    never more than max_ctx / MIN_PARTITION. The kernel splits each sequence's own context
-    over that many waves (at least MIN_PARTITION tokens each), so the choice only sizes the
-    grid: two calls whose nparts differ only by this cap compute identical splits."""
-    want = math.ceil(target_waves / max(1, nseq * nkv))
+    measured: fewer, longer waves beat finer splits down to that count), never more than
+    max_ctx / MIN_PARTITION. ``min_split`` > 1 forces a split even when the batch alone fills
+    the chip: at 512 ragged rollout contexts U[17,1536] 2-4 splits measured 4.0-4.3 TB/s vs
+    3.8 unsplit, but at 512 uniform contexts of 1280 2 splits lose 10% (5.05 vs 5.65 TB/s),
+    so the default stays 1 (scripts/probe/attn_ragged_sweep.py). The kernel splits each
+    sequence's own context over that many waves (at least MIN_PARTITION tokens each), so the
+    choice only sizes the grid: two calls whose nparts differ only by this cap compute
+    identical splits."""
+    want = max(min_split, math.ceil(target_waves / max(1, nseq * nkv)))
     return max(1, min(want, math.ceil(max(max_ctx, 1) / MIN_PARTITION)))
 
 
