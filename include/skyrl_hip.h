@@ -195,6 +195,14 @@ size_t skyrl_lmhead_state_bytes(int32_t T);
 int skyrl_lmhead_chunk_fwd(const void* z, int64_t ldz, int32_t T, int32_t vc, int64_t v0, const int64_t* labels,
                            int64_t label_stride, float temperature, void* state, int32_t first, int32_t last,
                            float* logp_out, float* entropy_out, float* lse_out, void* stream);
+/* Vocab-parallel (tensor-parallel lm_head) variant, replacing DistributedLogprob +
+ * _VocabParallelEntropy (distributed/megatron/model_utils.py:64-136, 548-578): each rank runs
+ * skyrl_lmhead_chunk_fwd over its shard with v0 = global column and last=0 on every chunk, the
+ * ranks all-gather their [T] states (skyrl_lmhead_state_bytes(T) each, rank order), and
+ * skyrl_lmhead_state_merge folds the nstates states into logp/entropy/lse f32 [T]. The
+ * backward is skyrl_lmhead_chunk_bwd on the local shard with the merged lse/entropy.      */
+int skyrl_lmhead_state_merge(const void* states, int32_t nstates, int32_t T, float* logp_out, float* entropy_out,
+                             float* lse_out, void* stream);
 int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int32_t vc, int64_t v0, const int64_t* labels,
                            int64_t label_stride, float temperature, const float* lse, const float* entropy,
                            const float* grad_logp, const float* grad_entropy, void* dz, int64_t lddz,

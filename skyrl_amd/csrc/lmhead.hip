@@ -30,6 +30,15 @@ struct __align__(16) ChunkState {
     float m, s, w, xl;
 };
 
+__device__ __forceinline__ void finalize_row(const SoftState& st, float xl, int64_t r, float* __restrict__ logp_out,
+                                             float* __restrict__ ent_out, float* __restrict__ lse_out) {
+    const float logs = fast_log2(st.s) * kLn2;
+    const float lse = st.m + logs;
+    logp_out[r] = xl - lse;  // NaN for a label outside [0, V), as logprob.hip
+    if (ent_out) ent_out[r] = logs - kLn2 * (st.w / st.s);
+    if (lse_out) lse_out[r] = lse;
+}
+
 __global__ __launch_bounds__(kThreads) void lmhead_fwd_kernel(
     const uint16_t* __restrict__ z, int64_t ldz, int T, int vc, int64_t v0, const int64_t* __restrict__ labels,
     int64_t lstride, float temp, bool has_t, ChunkState* __restrict__ state, int first, int last,
@@ -94,11 +103,7 @@ __global__ __launch_bounds__(kThreads) void lmhead_fwd_kernel(
         state[r] = ChunkState{st.m, st.s, st.w, xl};
         return;
     }
-    const float logs = fast_log2(st.s) * kLn2;
-    const float lse = st.m + logs;
-    logp_out[r] = xl - lse;  // NaN for a label outside [0, V), as logprob.hip
-    if (ent_out) ent_out[r] = logs - kLn2 * (st.w / st.s);
-    if (lse_out) lse_out[r] = lse;
+    finalize_row(st, xl, r, logp_out, ent_out, lse_out);
 }
 
 __global__ __launch_bounds__(kThreads) void lmhead_bwd_kernel(
@@ -158,6 +163,27 @@ __global__ __launch_bounds__(kThreads) void lmhead_bwd_kernel(
     for (int i = done + lane; i < vc; i += kWave) E::store(out + i, grad(E::apply_t(E::load(row + i), temp, has_t), i));
 }
 
+// Vocab-parallel merge (DistributedLogprob, megatron/model_utils.py:26-136 + _VocabParallelEntropy
+// :548-578): each tensor-parallel rank ran the chunk kernel over its vocab shard with last=0 and
+// the ranks all-gathered the [T] states. One thread per token merges the nstates states (the
+// label logit comes from the one shard holding the label) and finalizes like the last chunk.
+__global__ __launch_bounds__(kThreads) void lmhead_state_merge_kernel(const ChunkState* __restrict__ states,
+                                                                      int nstates, int T, float* __restrict__ logp_out,
+                                                                      float* __restrict__ ent_out,
+                                                                      float* __restrict__ lse_out) {
+    const int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (r >= T) return;
+    const ChunkState c0 = states[r];
+    SoftState st{c0.m, c0.s, c0.w};
+    float xl = c0.xl;
+    for (int k = 1; k < nstates; ++k) {
+        const ChunkState c = states[(int64_t)k * T + r];
+        state_merge(st, SoftState{c.m, c.s, c.w});
+        if (__builtin_isnan(xl)) xl = c.xl;
+    }
+    finalize_row(st, xl, r, logp_out, ent_out, lse_out);
+}
+
 inline unsigned blocks_for(int T) { return (unsigned)((T + kRowsPerBlock - 1) / kRowsPerBlock); }
 
 }  // namespace
@@ -198,4 +224,15 @@ extern "C" int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int
                        temperature != 1.0f, lse, entropy, grad_logp, grad_entropy, reinterpret_cast<uint16_t*>(dz),
                        lddz);
     return check_launch("lmhead_bwd_kernel");
+}
+
+extern "C" int skyrl_lmhead_state_merge(const void* states, int32_t nstates, int32_t T, float* logp_out,
+                                        float* entropy_out, float* lse_out, void* stream) {
+    SKYRL_REQUIRE(T >= 0 && nstates >= 1, "lmhead_state_merge: bad sizes");
+    if (T == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(states && logp_out, "lmhead_state_merge: null pointer");
+    hipLaunchKernelGGL(lmhead_state_merge_kernel, dim3((unsigned)((T + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       as_stream(stream), reinterpret_cast<const ChunkState*>(states), nstates, T, logp_out,
+                       entropy_out, lse_out);
+    return check_launch("lmhead_state_merge_kernel");
 }
