@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--micro", type=int, default=16)
     ap.add_argument("--tunable", action="store_true", help="TunableOp GEMM search in the rollout engine")
+    ap.add_argument("--no-packing", action="store_true", help="padded learner batches (no sample packing)")
     args = ap.parse_args()
     from transformers import AutoModelForCausalLM, Qwen2Config
 
@@ -65,6 +66,7 @@ def main():
     tcfg = TrainerConfig(n_samples_per_prompt=args.group, policy_mini_batch_size=args.prompts,
                          micro_train_batch_size_per_gpu=args.micro, micro_forward_batch_size_per_gpu=args.micro,
                          lr=1e-6, sampling_params={"min_tokens": 1, "ignore_eos": True},
+                         use_sample_packing=not args.no_packing,
                          algorithm=AlgorithmConfig(use_kl_loss=True))
     g = torch.Generator().manual_seed(1234)
     N = args.prompts * args.group
@@ -111,7 +113,8 @@ def main():
                       "config": {"model": "Qwen2.5-1.5B (random init)", "layers": args.layers, "prompts": args.prompts,
                                  "group": args.group, "prompt_len": "U[16,512]",
                                  "response_len": f"U[1,{args.max_response}]", "micro_batch": args.micro,
-                                 "gradient_checkpointing": True, "learner": "HF transformers fp32 master, autocast bf16"},
+                                 "gradient_checkpointing": True, "sample_packing": tcfg.use_sample_packing,
+                                 "learner": "HF transformers fp32 master, autocast bf16"},
                       "generated_tokens": sum(resp_len), "steps": steps}), flush=True)
 
 

@@ -27,6 +27,7 @@ import torch
 from . import comm, ppo_utils, trainer_utils
 from .config import AlgorithmConfig
 from .lmhead import lmhead_logprobs_and_entropy
+from .packing import enable_sample_packing, packed_hidden_states
 
 
 @dataclass
@@ -42,6 +43,7 @@ class TrainerConfig:
     weight_decay: float = 0.01
     max_grad_norm: float = 1.0
     temperature: float = 1.0
+    use_sample_packing: bool = True             # trainer.use_sample_packing (config.py:457): padding-free learner
     sampling_params: Dict[str, Any] = field(default_factory=lambda: {"max_tokens": 1024, "min_tokens": 1})
     algorithm: AlgorithmConfig = field(default_factory=AlgorithmConfig)
 
@@ -65,7 +67,10 @@ class CriticModel(torch.nn.Module):
         self.value_head_prefix = value_head_prefix
         setattr(self, value_head_prefix, torch.nn.Linear(hf_config.hidden_size, 1, bias=False))
 
-    def forward(self, seq: torch.Tensor, att: torch.Tensor, R: int) -> torch.Tensor:
+    def forward(self, seq: torch.Tensor, att: torch.Tensor, R: int, packed: bool = False) -> torch.Tensor:
+        if packed:  # padding-free (skyrl_amd.packing); the model must be switched by enable_sample_packing
+            h = packed_hidden_states(self.model, seq, att, R)
+            return getattr(self, self.value_head_prefix)(h).squeeze(-1)
         h = self.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
         return getattr(self, self.value_head_prefix)(h).squeeze(-1)[:, :-1][:, -R:]
 
@@ -104,6 +109,10 @@ class GRPOTrainer:
             alg, use_kl_loss=alg.use_kl_loss, use_entropy_loss=alg.use_entropy_loss, has_entropy=True)
         self.optimizer = torch.optim.AdamW(policy.parameters(), lr=cfg.lr, betas=tuple(cfg.betas),
                                            weight_decay=cfg.weight_decay, eps=1e-8)
+        if cfg.use_sample_packing:
+            for m in (policy, ref, critic.model if critic is not None else None):
+                if m is not None:
+                    enable_sample_packing(m)
         self.global_step = 0
         self.timings: Dict[str, float] = {}  # seconds per phase of the last step (device-synchronised)
         self._t = 0.0
@@ -131,8 +140,11 @@ class GRPOTrainer:
         """action log-probs (and entropy) of the last R positions: HFModelWrapper.forward
         (model_wrapper.py:261-375) with the lm_head-fused HIP logprob/entropy."""
         with torch.autocast("cuda", dtype=torch.bfloat16), torch.set_grad_enabled(grad):
-            hidden = model.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
-            h = hidden[:, -R - 1:-1].to(torch.bfloat16)
+            if self.cfg.use_sample_packing:
+                h = packed_hidden_states(model.model, seq, att, R).to(torch.bfloat16)
+            else:
+                hidden = model.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
+                h = hidden[:, -R - 1:-1].to(torch.bfloat16)
             w = model.lm_head.weight.to(torch.bfloat16)
             return lmhead_logprobs_and_entropy(h, w, seq[:, -R:], temperature=self.cfg.temperature,
                                                compute_entropy=grad)
@@ -151,7 +163,8 @@ class GRPOTrainer:
         R = data["response_mask"].shape[1]
         mb = self.cfg.micro_forward_batch_size_per_gpu
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            return torch.cat([self.critic(seq[i:i + mb], att[i:i + mb], R).float() for i in range(0, len(seq), mb)])
+            return torch.cat([self.critic(seq[i:i + mb], att[i:i + mb], R, self.cfg.use_sample_packing).float()
+                              for i in range(0, len(seq), mb)])
 
     # ---------------------------------------------------------------- step
     def step(self, prompts: List[List[int]], extras: Optional[List[Any]] = None) -> Dict[str, float]:
@@ -229,7 +242,8 @@ class GRPOTrainer:
             for i in range(s0, s1, mb):
                 j = min(i + mb, s1)
                 with torch.autocast("cuda", dtype=torch.bfloat16):
-                    v = self.critic(data["sequences"][i:j], data["attention_mask"][i:j], R).float()
+                    v = self.critic(data["sequences"][i:j], data["attention_mask"][i:j], R,
+                                    self.cfg.use_sample_packing).float()
                 loss, clipfrac = ppo_utils.ppo_critic_loss(v, data["values"][i:j], data["returns"][i:j],
                                                            cfg.algorithm, loss_mask=data["loss_mask"][i:j])
                 (loss / n_micro).backward()
