@@ -146,8 +146,18 @@ class GRPOTrainer:
                 hidden = model.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
                 h = hidden[:, -R - 1:-1].to(torch.bfloat16)
             w = model.lm_head.weight.to(torch.bfloat16)
-            return lmhead_logprobs_and_entropy(h, w, seq[:, -R:], temperature=self.cfg.temperature,
-                                               compute_entropy=grad)
+            labels = seq[:, -R:]
+            live = att[:, -R:].bool()  # positions whose label is a real response token
+            if bool(live.all()):
+                return lmhead_logprobs_and_entropy(h, w, labels, temperature=self.cfg.temperature,
+                                                   compute_entropy=grad)
+            # the lm_head GEMMs only over live rows (padding is about half of [n, R] at U[1, R]
+            # responses); padded positions read 0, as the reference's pad_input leaves them
+            lp_v, ent_v = lmhead_logprobs_and_entropy(h[live], w, labels[live], temperature=self.cfg.temperature,
+                                                      compute_entropy=grad)
+            zeros = torch.zeros(live.shape, dtype=torch.float32, device=h.device)
+            return (zeros.masked_scatter(live, lp_v),
+                    zeros.masked_scatter(live, ent_v) if ent_v is not None else None)
 
     @torch.no_grad()
     def _fwd_logprobs(self, model, data) -> torch.Tensor:
