@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64) void rope_kv_write_kernel(
 
 // ---- decode attention over the paged cache -------------------------------------------
 template <int D>
-__global__ __launch_bounds__(64) void paged_decode_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
     const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_min,
@@ -141,7 +141,6 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
 
     // Block ids of this partition: one vector load of up to 64 table entries (one per lane),
     // read back with readlane, so the per-block address chain has no dependent table load.
-    // K/V of block j+1 are issued before block j is computed (two blocks in flight per wave).
     const int32_t* bt = block_tables + (int64_t)seq * bt_stride + t0 / kBS;
     const int nb = (t1 - t0 + kBS - 1) / kBS;
     int tbl = lane < nb ? bt[lane] : 0;
@@ -149,29 +148,27 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
     const int64_t blk_stride = (int64_t)nkv * head_tile;
     const uint16_t* kbase = kc + kvh * head_tile + c * D + 8 * g;
     const uint16_t* vbase = vc + kvh * head_tile + c * kBS + 4 * g;
-    s16x8 kf[KS];
-    s16x4 vf[NT];
-    {
-        const int64_t blk = __builtin_amdgcn_readlane(tbl, 0);
+    auto load_blk = [&](int jb, s16x8 (&kd)[KS], s16x4 (&vd)[NT]) {
+        const int64_t blk = __builtin_amdgcn_readlane(tbl, jb & 63);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const s16x8*>(kbase + blk * blk_stride + 32 * s);
+        for (int s = 0; s < KS; ++s) kd[s] = *reinterpret_cast<const s16x8*>(kbase + blk * blk_stride + 32 * s);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) vf[n] = *reinterpret_cast<const s16x4*>(vbase + blk * blk_stride + 16 * n * kBS);
-    }
+        for (int n = 0; n < NT; ++n) vd[n] = *reinterpret_cast<const s16x4*>(vbase + blk * blk_stride + 16 * n * kBS);
+    };
+    // three blocks in flight per wave (current + two ahead): the loop is bound by the load
+    // latency, and the extra 32 VGPRs keep the occupancy tier (3 waves / SIMD) unchanged
+    s16x8 kf[KS], k1[KS];
+    s16x4 vf[NT], v1[NT];
+    load_blk(0, kf, vf);
+    if (nb > 1) load_blk(1, k1, v1);
     for (int j = 0; j < nb; ++j) {
         const int tb = t0 + j * kBS;
-        const bool more = j + 1 < nb;
-        s16x8 kn[KS];
-        s16x4 vn[NT];
-        if (more) {
-            if (((j + 1) & 63) == 0) tbl = (j + 1 + lane < nb) ? bt[j + 1 + lane] : 0;
-            const int64_t blk = __builtin_amdgcn_readlane(tbl, (j + 1) & 63);
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-                kn[s] = *reinterpret_cast<const s16x8*>(kbase + blk * blk_stride + 32 * s);
-#pragma unroll
-            for (int n = 0; n < NT; ++n)
-                vn[n] = *reinterpret_cast<const s16x4*>(vbase + blk * blk_stride + 16 * n * kBS);
+        const bool more2 = j + 2 < nb;
+        s16x8 k2[KS];
+        s16x4 v2[NT];
+        if (more2) {
+            if (((j + 2) & 63) == 0) tbl = (j + 2 + lane < nb) ? bt[j + 2 + lane] : 0;
+            load_blk(j + 2, k2, v2);
         }
         f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -215,11 +212,15 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(
             o[n] = o[n] * alpha;
             o[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[n], pf, o[n], 0, 0, 0);
         }
-        if (more) {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) kf[s] = kn[s];
+        for (int s = 0; s < KS; ++s) {
+            kf[s] = k1[s];
+            if (more2) k1[s] = k2[s];
+        }
 #pragma unroll
-            for (int n = 0; n < NT; ++n) vf[n] = vn[n];
+        for (int n = 0; n < NT; ++n) {
+            vf[n] = v1[n];
+            if (more2) v1[n] = v2[n];
         }
     }
     // o[n][i] = O^T[dim 16n + 4g + i][head c]; l is this lane's share of the row sum
