@@ -1,5 +1,7 @@
 """T=1 sampler at 512 rows x V=151936 (bf16, resident): time per launch for a forced split
-count (env SKYRL_SAMPLER_SPLITS, read once per process). Prints one JSON line."""
+count (env SKYRL_SAMPLER_SPLITS, read once per process). The product build has no such
+override: for the sweep, splits_for() in csrc/sampler.hip was temporarily patched to return
+atoi(getenv("SKYRL_SAMPLER_SPLITS")) when set. Prints one JSON line."""
 import json
 import os
 import sys
