@@ -164,8 +164,12 @@ class GRPOTrainer:
         seq, att = data["sequences"], data["attention_mask"]
         R = data["response_mask"].shape[1]
         mb = self.cfg.micro_forward_batch_size_per_gpu
-        return torch.cat([self._logprobs(model, seq[i:i + mb], att[i:i + mb], R, grad=False)[0]
-                          for i in range(0, len(seq), mb)])
+        # one autocast region over all micro-batches: each fp32 weight is cast to bf16 once per
+        # pass (autocast's cast cache lives until the outermost region exits), not once per
+        # micro-batch
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return torch.cat([self._logprobs(model, seq[i:i + mb], att[i:i + mb], R, grad=False)[0]
+                              for i in range(0, len(seq), mb)])
 
     @torch.no_grad()
     def _fwd_values(self, data) -> torch.Tensor:
