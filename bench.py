@@ -346,7 +346,7 @@ def run(args):
         "cpu_baseline": None,
     }
     if not args.no_adv_loss_leg:
-        result["advantage_loss"] = {"batch": advantage_loss_leg(dev, N, R),
+        result["advantage_loss"] = {"batch": advantage_loss_leg(dev, N, R, variants=args.adv_loss_variants),
                                     "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
     if not args.no_attention_leg:
         result["rollout_attention"] = rollout_attention_leg(dev, N)
@@ -395,11 +395,14 @@ def pmc_traffic(kernel_name, algorithmic_bytes):
     return None
 
 
-def advantage_loss_leg(dev, N, R, reps=20):
-    """GRPO advantage + fused PPO/KL loss forward (+ fold) + loss backward on [N, R], the
-    SURVEY §8(d) "advantage+loss" kernels (12 + 20 + 24 = 56 algorithmic B/token). Launched
-    through the C ABI inside a captured HIP graph and replayed, so host launch cost is
-    excluded and inter-kernel gaps are included. Returns per-kernel and total microseconds."""
+def advantage_loss_leg(dev, N, R, reps=20, variants=False):
+    """GRPO advantage + fused PPO/KL loss (forward, gradient and loss fold in ONE launch) +
+    the loss backward (an in-place rescale that touches nothing at unit upstream gradient)
+    on [N, R]: the SURVEY §8(d) "advantage+loss" kernels (12 + 20 + 24 = 56 algorithmic
+    B/token). Launched through the C ABI inside a captured HIP graph and replayed, so host
+    launch cost is excluded and inter-kernel gaps are included. The loss-mask row sums are
+    the pack kernel's (skyrl_pack_experience emits them with the batch). Returns per-kernel
+    and total microseconds."""
     from skyrl_amd import _ffi, ppo_utils
     from skyrl_amd.config import AlgorithmConfig
     from skyrl_amd.ops import _ptr
@@ -410,13 +413,12 @@ def advantage_loss_leg(dev, N, R, reps=20):
     rew[torch.arange(N, device=dev), lens - 1] = (torch.rand(N, device=dev, generator=g) < 0.3).float()
     rmask = (torch.arange(R, device=dev)[None] < lens[:, None]).to(torch.int64)
     lmask = rmask.float()
+    rows = lens.float()  # = pack's loss_mask_row_sum for this batch
     lp = -2 + 0.1 * torch.randn(N, R, device=dev, generator=g)
     old = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
     ref = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
     adv = torch.empty(N, R, device=dev)
-    gnum = torch.empty(N, R, device=dev)
     glp = torch.empty(N, R, device=dev)
-    rs = torch.empty(N, device=dev)
     loss = torch.empty(1, device=dev)
     met = torch.empty(8, device=dev)
     gout = torch.ones(1, device=dev)
@@ -428,18 +430,16 @@ def advantage_loss_leg(dev, N, R, reps=20):
         _ffi.call("skyrl_grpo_advantage", _ptr(rew), _ptr(rmask), _ffi.I64, None, None, ng, N, R, 1e-6, 1,
                   _ptr(adv), None, s)
 
-    def fwd(s):
-        _ffi.call("skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(lmask), _ptr(ref), None, N, R,
-                  ctypes.byref(params), _ptr(loss), _ptr(met), _ptr(gnum), _ptr(rs), _ptr(ws), s)
+    def fwd(s, with_rows=True):
+        _ffi.call("skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(lmask), _ptr(ref), None,
+                  _ptr(rows) if with_rows else None, N, R, ctypes.byref(params), _ptr(loss), _ptr(met), _ptr(glp),
+                  None, _ptr(ws), s)
 
     def bwd(s):
-        _ffi.call("skyrl_ppo_loss_bwd", _ptr(gout), _ptr(gnum), _ptr(rs), _ptr(lmask), _ptr(met), N, R,
-                  ctypes.byref(params), _ptr(glp), None, s)
+        _ffi.call("skyrl_ppo_loss_bwd", _ptr(gout), N * R, _ptr(glp), None, s)
 
-    out = {}
-    side = torch.cuda.Stream(dev)
-    for name, fns in (("grpo_us", (grpo,)), ("loss_fwd_us", (fwd,)), ("loss_bwd_us", (bwd,)),
-                      ("total_us", (grpo, fwd, bwd))):
+    def timed(fns):
+        side = torch.cuda.Stream(dev)
         with torch.cuda.stream(side):
             h = torch.cuda.current_stream(dev).cuda_stream
             for f in fns:
@@ -459,8 +459,24 @@ def advantage_loss_leg(dev, N, R, reps=20):
             graph.replay()
         b.record()
         b.synchronize()
-        out[name] = round(a.elapsed_time(b) * 1e3 / (5 * reps), 2)
         del graph
+        return round(a.elapsed_time(b) * 1e3 / (5 * reps), 2)
+
+    out = {}
+    for name, fns in (("grpo_us", (grpo,)), ("loss_fwd_us", (fwd,)), ("loss_bwd_us", (bwd,)),
+                      ("total_us", (grpo, fwd, bwd))):
+        out[name] = timed(fns)
+    if variants:
+        out["variants"] = {"total_without_row_sums_us": timed((grpo, lambda s: fwd(s, False), bwd)),
+                           "grpo_adv_loss_no_bwd_us": timed((grpo, fwd))}
+        for sl in (1, 2, 4):
+            _ffi.call("skyrl_tune", b"grpo_slices", sl)
+            out["variants"][f"grpo_slices{sl}_us"] = timed((grpo,))
+        _ffi.call("skyrl_tune", b"grpo_slices", 4)
+        for u in (1, 2, 4):
+            _ffi.call("skyrl_tune", b"loss_units", u)
+            out["variants"][f"loss_units{u}_us"] = timed((fwd,))
+        _ffi.call("skyrl_tune", b"loss_units", 0)
     nbytes = 56 * N * R
     gbs = nbytes / (out["total_us"] * 1e-6) / 1e9
     out.update({"rows": N, "R": R, "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
@@ -601,6 +617,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the real-model end-to-end leg (N=1 only)")
     ap.add_argument("--no-adv-loss-leg", action="store_true", help="skip the graph-replayed advantage+loss leg")
+    ap.add_argument("--adv-loss-variants", action="store_true", help="also time the A/B variants of that leg")
     ap.add_argument("--no-attention-leg", action="store_true", help="skip the rollout paged-attention leg")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)

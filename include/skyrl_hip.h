@@ -39,7 +39,9 @@ extern "C" {
 
 /* Thread-local text of the last error on this thread ("" if none). */
 const char* skyrl_last_error(void);
-/* ABI version; bumped on any signature change (2: skyrl_sample takes top_p). */
+/* ABI version; bumped on any signature change (2: skyrl_sample takes top_p; 3: one-launch
+ * skyrl_ppo_loss_fwd writing final gradients, in-place skyrl_ppo_loss_bwd, pack emits
+ * loss-mask row sums). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -102,8 +104,8 @@ int skyrl_reward_kl_penalty(const float* rewards, const float* action_log_probs,
  * + the loss assembly of PolicyWorkerBase._forward_backward_micro
  * (workers/worker.py:810-876: entropy masked_mean, k-type KL seq-mean then
  * batch-mean, final = pg + kl*coef - H*coef*[use_entropy_loss]).
- * Forward writes the scalar loss, the metric vector and a per-token gradient
- * numerator; skyrl_ppo_loss_bwd turns it into dL/dlogp (and dL/dentropy).
+ * Forward writes the scalar loss, the metric vector and dL/dlogp (and dL/dentropy)
+ * for a unit upstream gradient; skyrl_ppo_loss_bwd rescales them for any other.
  * Gradient semantics follow torch autograd of the reference: min() ties split
  * the gradient 1/2-1/2, clamp passes gradient on the closed interval, the KL
  * term carries NO gradient (compute_approx_kl is @torch.no_grad()).         */
@@ -132,19 +134,27 @@ typedef struct skyrl_ppo_params {
 #define SKYRL_M_COUNT 8
 
 size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R);
-/* workspace must be zeroed once at allocation; the kernel leaves it re-usable. */
+/* ONE launch (two when row_mask_sum is NULL, plus one when a token_mean total over
+ * n > 1024 rows is needed): writes the scalar loss, the metric vector and the FINAL
+ * gradients for a unit upstream gradient:
+ *   grad_logp[i,t]    = dL/dlogp[i,t]
+ *   grad_entropy[i,t] = -entropy_loss_coef*mask/max(sum mask,1) (only when use_entropy_loss;
+ *                       pass NULL otherwise).
+ * row_mask_sum: f32 [n] per-row sums of loss_mask (skyrl_pack_experience emits them), or
+ * NULL to have them computed here. The reduction scales depend on the mask only, so the
+ * gradient is final when written. workspace (skyrl_ppo_loss_workspace_bytes) must be zeroed
+ * once at allocation; the kernel leaves it re-usable.                                      */
 int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const float* advantages,
                        const float* loss_mask /* NULL = all ones */, const float* ref_log_probs,
-                       const float* entropy, int32_t n, int32_t R, const skyrl_ppo_params* params,
+                       const float* entropy, const float* row_mask_sum /* [n] or NULL */,
+                       int32_t n, int32_t R, const skyrl_ppo_params* params,
                        float* loss_out /* [1] */, float* metrics_out /* [SKYRL_M_COUNT] */,
-                       float* grad_num /* [n,R] */, float* row_scale /* [n] */, void* workspace,
-                       void* stream);
-/* grad_logp = g * grad_num * row_scale[row]; grad_entropy (optional) =
- * -g*entropy_loss_coef*mask/max(sum mask,1) when use_entropy_loss.           */
-int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, const float* grad_num,
-                       const float* row_scale, const float* loss_mask, const float* metrics,
-                       int32_t n, int32_t R, const skyrl_ppo_params* params, float* grad_logp,
-                       float* grad_entropy /* NULL unless use_entropy_loss */, void* stream);
+                       float* grad_logp /* [n,R] */, float* grad_entropy /* [n,R] or NULL */,
+                       void* workspace, void* stream);
+/* Autograd backward of the loss: grad_logp (and grad_entropy, if given) *= grad_out[0] in
+ * place; no memory is touched when grad_out[0] == 1 (loss.backward()).                    */
+int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, int64_t numel, float* grad_logp,
+                       float* grad_entropy /* or NULL */, void* stream);
 
 /* ---- a8: clipped value loss ---------------------------------------------
  * Replaces ppo_critic_loss (ppo_utils.py:175-193): 0.5*mean_rows(masked_mean(
@@ -256,7 +266,9 @@ size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V);
  * Outputs: sequences i64 [Np,P+R] (left-padded prompt | right-padded
  * response), attention_mask i64 [Np,P+R], response_mask i64 [Np,R],
  * rewards f32 [Np,R], loss_mask f32 [Np,R], rollout_logprobs f32 [Np,R]
- * (NULL when logprob_vals is NULL). Np = N + pad.                            */
+ * (NULL when logprob_vals is NULL), loss_mask_row_sum f32 [Np] (per-row sum of
+ * loss_mask, the input of skyrl_ppo_loss_fwd's reduction scales; may be NULL).
+ * Np = N + pad.                                                               */
 typedef struct skyrl_pack_inputs {
     const int64_t* prompt_tokens;   const int64_t* prompt_off;
     const int64_t* response_tokens; const int64_t* response_off;
@@ -267,7 +279,7 @@ typedef struct skyrl_pack_inputs {
 int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int32_t pad, int32_t P, int32_t R,
                           int64_t pad_token_id, int64_t* sequences, int64_t* attention_mask,
                           int64_t* response_mask, float* rewards, float* loss_mask,
-                          float* rollout_logprobs, void* stream);
+                          float* rollout_logprobs, float* loss_mask_row_sum, void* stream);
 
 /* ---- a12: gradient scale ------------------------------------------------
  * grads *= scale over a flat fp32 bucket (optim_step's 1/n_micro scaling,

@@ -30,20 +30,20 @@ mask = torch.ones(N, R, device=dev)
 params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
 loss = torch.empty(1, device=dev)
 metrics = torch.empty(8, device=dev)
-gnum = torch.empty(N, R, device=dev)
-rs = torch.empty(N, device=dev)
+glp = torch.empty(N, R, device=dev)
+rows = mask.sum(-1)
 ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", N, R), dtype=torch.uint8, device=dev)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 P = ctypes.c_void_p
 fn = lib.skyrl_ppo_loss_fwd
 fn.restype = ctypes.c_int
-fn.argtypes = [P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, P, P]
+fn.argtypes = [P, P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, P, P]
 
 
 def launch():
-    rc = fn(P(lp.data_ptr()), P(old.data_ptr()), P(adv.data_ptr()), P(mask.data_ptr()), P(ref.data_ptr()), None, N, R,
-            ctypes.byref(params), P(loss.data_ptr()), P(metrics.data_ptr()), P(gnum.data_ptr()), P(rs.data_ptr()),
-            P(ws.data_ptr()), st)
+    rc = fn(P(lp.data_ptr()), P(old.data_ptr()), P(adv.data_ptr()), P(mask.data_ptr()), P(ref.data_ptr()), None,
+            P(rows.data_ptr()), N, R, ctypes.byref(params), P(loss.data_ptr()), P(metrics.data_ptr()),
+            P(glp.data_ptr()), None, P(ws.data_ptr()), st)
     assert rc == 0
 
 
@@ -57,13 +57,12 @@ for rep in range(3):
     launch()
     torch.cuda.synchronize()
     assert lib.probe_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
-    nb = int(os.environ.get("BLOCKS", N))
-    t = buf.reshape(-1, 8)[:nb].astype(np.int64)
-    d = lambda a, b: (t[:, b] - t[:, a]) / 100.0  # noqa: E731  per-block spans, us (100 MHz)
-    last = int(np.argmax(t[:, 3] > 0))
-    tp = d(0, 1)
-    print(f"rep {rep}: per block: token pass median {np.median(tp):.2f} max {tp.max():.2f}; "
-          f"wave reduce+drain+barrier median {np.median(d(1, 2)):.2f} max {d(1, 2).max():.2f}; "
-          f"last block {last}: entry->arrive {(t[last, 3] - t[last, 0]) / 100:.2f}, "
-          f"arrive {(t[last, 3] - t[last, 2]) / 100:.2f}, fold {(t[last, 4] - t[last, 3]) / 100:.2f}, "
-          f"end {(t[last, 5] - t[last, 4]) / 100:.2f}")
+    t = buf.reshape(-1, 8).astype(np.int64)
+    t = t[: int(np.nonzero(t[:, 0])[0].max()) + 1]
+    t0 = t[:, 0].min()
+    us = lambda x: (x - t0) / 100.0  # noqa: E731  (s_memrealtime: 100 MHz)
+    f = len(t) - 1  # the folding block (the last of the grid)
+    print(f"rep {rep}: {len(t)} blocks: entries {us(t[:, 0]).min():.2f}..{us(t[:, 0]).max():.2f} us; "
+          f"total ready (median span) {np.median((t[1:, 4] - t[1:, 0]) / 100):.2f}; "
+          f"token pass done (median span) {np.median((t[1:, 1] - t[1:, 0]) / 100):.2f}, last at {us(t[1:, 1]).max():.2f}; "
+          f"folder: entry {us(t[f, 0]):.2f}, fold start {us(t[f, 2]):.2f}, end {us(t[f, 3]):.2f}")

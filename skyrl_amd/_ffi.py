@@ -99,9 +99,9 @@ SIGNATURES = {
     "skyrl_ppo_loss_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_ppo_loss_fwd": (
         _INT,
-        [_P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P, _P, _P],
+        [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P, _P, _P],
     ),
-    "skyrl_ppo_loss_bwd": (_INT, [_P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P]),
+    "skyrl_ppo_loss_bwd": (_INT, [_P, _I64, _P, _P, _P]),
     "skyrl_critic_loss_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_critic_loss_fwd": (_INT, [_P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),
     "skyrl_logprob_fwd": (_INT, [_P, _INT, _I64, _I64, _I32, _I32, _I32, _P, _I64, _I64, _F, _P, _P, _P, _P]),
@@ -124,7 +124,7 @@ SIGNATURES = {
     "skyrl_sample": (_INT, [_P, _INT, _I64, _I32, _I32, _F, _I32, _F, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),
     "skyrl_pack_experience": (
         _INT,
-        [ctypes.POINTER(PackInputs), _I32, _I32, _I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _P],
+        [ctypes.POINTER(PackInputs), _I32, _I32, _I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "skyrl_scale_and_sumsq": (_INT, [_P, _I64, _F, _P, _P]),
     "skyrl_scale_by_device_scalar": (_INT, [_P, _P, _P, _I64, _P]),

@@ -468,6 +468,115 @@ def _sharded_broadcast(flat: torch.Tensor, src_ranks: Sequence[int], group) -> N
 
 
 # ------------------------------------------------------------- a12 for module parameters
+class BucketedGradAllReduce:
+    """DP gradient mean for a module's parameters (the HF learner), overlapped with the backward.
+
+    Every trainable fp32 parameter's ``.grad`` is a view into one of a few flat fp32 buckets
+    (~``bucket_bytes``, filled in reverse parameter order, the order the backward produces
+    them). :meth:`arm` before the LAST micro-batch's backward; from then on a
+    post-accumulate-grad hook counts each bucket's parameters, and when a bucket is complete
+    its SUM all-reduce (x 1/world) is launched on a dedicated comm stream while the backward
+    continues with the earlier layers -- the reference's FSDP2 reduce-scatter per wrapped
+    layer during the backward (fsdp_strategy.py:216-226,253-271). Buckets are launched
+    strictly in index order, so every rank issues the same collective sequence. :meth:`wait`
+    (before clipping) launches any bucket whose parameters got no gradient and makes the
+    compute stream wait for the comm stream. World size 1: the buckets are still the grads'
+    storage and nothing is launched.
+    """
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], group=None, bucket_bytes: int = 64 << 20):
+        self.group = group
+        self.world, _ = _world(group)
+        ps = [p for p in params if p.requires_grad]
+        if not ps:
+            raise ValueError("no trainable parameters")
+        for p in ps:
+            if p.dtype != torch.float32:
+                raise TypeError(f"BucketedGradAllReduce keeps fp32 grads; got a {p.dtype} parameter")
+        self.device = ps[0].device
+        groups: List[List[torch.nn.Parameter]] = []
+        cur: List[torch.nn.Parameter] = []
+        size = 0
+        for p in reversed(ps):
+            cur.append(p)
+            size += p.numel() * 4
+            if size >= bucket_bytes:
+                groups.append(cur)
+                cur, size = [], 0
+        if cur:
+            groups.append(cur)
+        self.buckets: List[Tuple[torch.Tensor, List[torch.nn.Parameter]]] = []
+        self._bucket_of: Dict[int, int] = {}
+        for b, plist in enumerate(groups):
+            flat = torch.zeros(sum(p.numel() for p in plist), dtype=torch.float32, device=self.device)
+            off = 0
+            for p in plist:
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                self._bucket_of[id(p)] = b
+                off += p.numel()
+            self.buckets.append((flat, plist))
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in ps]
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._armed = False
+        self._pending: List[int] = []
+        self._ready: List[bool] = []
+        self._next = 0
+        self.launched_during_backward = 0
+
+    def arm(self) -> None:
+        """Call before the backward of the mini-batch's last micro-batch."""
+        if self.world == 1:
+            return
+        self._armed = True
+        self._pending = [len(pl) for _, pl in self.buckets]
+        self._ready = [False] * len(self.buckets)
+        self._next = 0
+        self.launched_during_backward = 0
+
+    def _on_grad(self, p) -> None:
+        if not self._armed:
+            return
+        b = self._bucket_of[id(p)]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._ready[b] = True
+            while self._next < len(self.buckets) and self._ready[self._next]:
+                self._launch(self._next)
+                self._next += 1
+                self.launched_during_backward += 1
+
+    def _launch(self, b: int) -> None:
+        flat = self.buckets[b][0]
+        if self.stream is None:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            flat.mul_(1.0 / self.world)
+            return
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        self.stream.wait_event(ready)
+        with torch.cuda.stream(self.stream):
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            flat.mul_(1.0 / self.world)
+
+    def wait(self) -> int:
+        """Finish the exchange (launching buckets that got no gradient); returns the number of
+        buckets launched from inside the backward."""
+        if not self._armed:
+            return 0
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        self._armed = False
+        return self.launched_during_backward
+
+    def zero_grad(self) -> None:
+        for flat, _ in self.buckets:
+            flat.zero_()
+
+
+
 def allreduce_grads(params: Iterable[torch.Tensor], group=None, bucket_bytes: int = 64 << 20) -> int:
     """Mean of `.grad` over the DP group for parameters that are not views of a flat buffer
     (a HF module under the GRPOTrainer): grads are packed into ~bucket_bytes fp32 buckets, one

@@ -200,7 +200,89 @@ __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_contig_kernel(
     }
 }
 
+
+// Contiguous uniform groups spread over S column slices per group (S in {2, 4}): a block per
+// (group, slice), one wave per row. Every block of a group sums the group's whole reward rows
+// (same per-lane order and tree as above, so all slices see bit-identical scores) but reads
+// the mask and writes the advantages of its own R/S columns only. The slices of a group are
+// placed on the same XCD (blocks are dispatched round-robin over the 8 XCDs, so block b runs
+// on XCD b % 8): their repeated reward reads hit that XCD's L2, and 4x as many CUs stream the
+// mask/advantage bytes as in the one-block-per-group form.
+template <int MDT, int S>
+__global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_sliced_kernel(
+    const float* __restrict__ rewards, const void* __restrict__ mask, int num_groups, int G, int R, float epsilon,
+    int norm_by_std, float* __restrict__ out, float* __restrict__ scores_out) {
+    __shared__ float s_scores[kMaxFastG];
+    const int b = blockIdx.x;
+    const int xcd = b & 7;
+    const int k = b >> 3;
+    const int slice = k % S;
+    const int group = (k / S) * 8 + xcd;
+    if (group >= num_groups) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    const int64_t row = (int64_t)group * G + w;
+    const float* rrow = rewards + row * R;
+    const int n4 = R >> 2;
+    const int sw = (n4 + S - 1) / S;  // 16-B vectors per slice
+    const int s0 = slice * sw, s1 = (s0 + sw < n4) ? s0 + sw : n4;
+    // this lane's slice vector (the common R = 1024, S = 4 case: exactly one) and its reward
+    // vectors, all issued before the first wait
+    const int vi = s0 + lane;
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+    if (vi < s1) load_mask4(mask, MDT, row * R + 4 * vi, m);
+    float acc = 0.f;
+    {
+        float4 v[kFastUnroll];
+#pragma unroll
+        for (int u = 0; u < kFastUnroll; ++u) {
+            const int i = lane + u * kWave;
+            v[u] = i < n4 ? reinterpret_cast<const float4*>(rrow)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < kFastUnroll; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+    }
+    for (int i = lane + kFastUnroll * kWave; i < n4; i += kWave) {
+        const float4 v = reinterpret_cast<const float4*>(rrow)[i];
+        acc += (v.x + v.y) + (v.z + v.w);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+        s_scores[w] = acc;
+        if (scores_out && slice == 0) scores_out[row] = acc;
+    }
+    __syncthreads();
+    float mean_f, denom_f;
+    if (G <= 1) {
+        mean_f = 0.f;
+        denom_f = norm_by_std ? (1.f + epsilon) : 1.f;
+    } else {
+        double sum = 0.0;
+        for (int j = 0; j < G; ++j) sum += (double)s_scores[j];
+        const double mean = sum / (double)G;
+        double m2 = 0.0;
+        for (int j = 0; j < G; ++j) {
+            const double d = (double)s_scores[j] - mean;
+            m2 += d * d;
+        }
+        mean_f = (float)mean;
+        const float std_f = (float)sqrt(m2 / (double)(G - 1));
+        denom_f = norm_by_std ? (std_f + epsilon) : 1.f;
+    }
+    const float sc = s_scores[w];
+    const float a = norm_by_std ? (sc - mean_f) / denom_f : (sc - mean_f);
+    float4* orow = reinterpret_cast<float4*>(out + row * R);
+    if (vi < s1) orow[vi] = make_float4(a * m[0], a * m[1], a * m[2], a * m[3]);
+    for (int i = vi + kWave; i < s1; i += kWave) {
+        float mm[4];
+        load_mask4(mask, MDT, row * R + 4 * i, mm);
+        orow[i] = make_float4(a * mm[0], a * mm[1], a * mm[2], a * mm[3]);
+    }
+}
+
 }  // namespace
+int g_grpo_slices = 4;  // skyrl_tune("grpo_slices", 1/2/4): column slices per group (contiguous form)
+
 }  // namespace skyrl
 
 extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_mask, int mask_dtype,
@@ -222,6 +304,18 @@ extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_m
     if (!group_off && !group_rows) {  // contiguous uniform groups of N / num_groups rows
         SKYRL_REQUIRE(N % num_groups == 0, "grpo: contiguous groups need N % num_groups == 0");
         const int G = N / num_groups;
+        if (vec4 && G <= kMaxFastG && g_grpo_slices > 1) {
+            const int S = g_grpo_slices;
+            auto pick = [&](auto k2, auto k4) { return S == 2 ? k2 : k4; };
+            auto k = mask_dtype == SKYRL_I64   ? pick(grpo_adv_sliced_kernel<SKYRL_I64, 2>, grpo_adv_sliced_kernel<SKYRL_I64, 4>)
+                     : mask_dtype == SKYRL_F32 ? pick(grpo_adv_sliced_kernel<SKYRL_F32, 2>, grpo_adv_sliced_kernel<SKYRL_F32, 4>)
+                     : mask_dtype == SKYRL_I32 ? pick(grpo_adv_sliced_kernel<SKYRL_I32, 2>, grpo_adv_sliced_kernel<SKYRL_I32, 4>)
+                                               : pick(grpo_adv_sliced_kernel<SKYRL_U8, 2>, grpo_adv_sliced_kernel<SKYRL_U8, 4>);
+            const int ngp = (num_groups + 7) / 8 * 8;
+            hipLaunchKernelGGL(k, dim3(ngp * S), dim3(G * kWave), 0, as_stream(stream), rewards, response_mask,
+                               num_groups, G, R, epsilon, norm_by_std, advantages, scores_out);
+            return check_launch("grpo_adv_sliced_kernel");
+        }
         if (vec4 && G <= kMaxFastG) {
             auto k = mask_dtype == SKYRL_I64   ? grpo_adv_contig_kernel<SKYRL_I64>
                      : mask_dtype == SKYRL_F32 ? grpo_adv_contig_kernel<SKYRL_F32>

@@ -213,6 +213,8 @@ namespace skyrl {
 extern int g_train_resident;
 extern int g_train_resident_nt;
 extern int g_train_ntstore;
+extern int g_grpo_slices;
+extern int g_loss_units;
 }
 
 extern "C" int skyrl_tune(const char* key, int value) {
@@ -233,6 +235,16 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "train_resident_nt") {
         SKYRL_REQUIRE(value == 768 || value == 1024, "skyrl_tune: train_resident_nt must be 768 or 1024");
         g_train_resident_nt = value;
+        return SKYRL_OK;
+    }
+    if (k == "grpo_slices") {
+        SKYRL_REQUIRE(value == 1 || value == 2 || value == 4, "skyrl_tune: grpo_slices must be 1, 2 or 4");
+        g_grpo_slices = value;
+        return SKYRL_OK;
+    }
+    if (k == "loss_units") {
+        SKYRL_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "skyrl_tune: loss_units must be 0, 1, 2 or 4");
+        g_loss_units = value;
         return SKYRL_OK;
     }
     if (k == "logprob_nt") {

@@ -28,7 +28,8 @@ template <bool VEC>
 __global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, int N, int P, int R, int64_t pad_id,
                                                         int64_t* __restrict__ seq, int64_t* __restrict__ att,
                                                         int64_t* __restrict__ rmask, float* __restrict__ rew,
-                                                        float* __restrict__ lmask, float* __restrict__ rlp) {
+                                                        float* __restrict__ lmask, float* __restrict__ rlp,
+                                                        float* __restrict__ lm_rowsum) {
     const int i = blockIdx.x;
     const int src = i < N ? i : i - N;
     const bool is_pad = i >= N;
@@ -66,6 +67,13 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, in
         rw[k] = c < wl ? in.reward_vals[w0 + c] : 0.f;
         lm[k] = c < ml ? in.loss_mask_vals[m0 + c] : 0.f;
         lp[k] = c < ll ? in.logprob_vals[l0 + c] : 0.f;
+    }
+    if (lm_rowsum && blockIdx.y == 0) {  // per-row loss-mask sum for the loss's reduction scales
+        __shared__ float s_red[kThreads / kWave];
+        float acc[1] = {0.f};
+        for (int c = threadIdx.x; c < ml && c < R; c += kThreads) acc[0] += in.loss_mask_vals[m0 + c];
+        block_sum<kThreads / kWave, 1>(acc, s_red);
+        if (threadIdx.x == 0) lm_rowsum[i] = acc[0];
     }
     if (VEC) {
         if (c0 < S) {
@@ -136,7 +144,7 @@ using namespace skyrl;
 extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int32_t pad, int32_t P, int32_t R,
                                      int64_t pad_token_id, int64_t* sequences, int64_t* attention_mask,
                                      int64_t* response_mask, float* rewards, float* loss_mask,
-                                     float* rollout_logprobs, void* stream) {
+                                     float* rollout_logprobs, float* loss_mask_row_sum, void* stream) {
     SKYRL_REQUIRE(in, "pack: inputs is null");
     SKYRL_REQUIRE(N > 0 && pad >= 0 && pad <= N && P >= 0 && R >= 0, "pack: bad sizes");
     SKYRL_REQUIRE(in->prompt_tokens && in->prompt_off && in->response_tokens && in->response_off && in->reward_vals &&
@@ -145,18 +153,21 @@ extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int
     SKYRL_REQUIRE(!rollout_logprobs || (in->logprob_vals && in->logprob_off), "pack: logprobs requested but absent");
     SKYRL_REQUIRE(sequences && attention_mask && response_mask && rewards && loss_mask, "pack: null output pointer");
     const int S = P + R;
-    const int cols = S > R ? S : R;
-    if (cols == 0) return SKYRL_OK;
+    int cols = S > R ? S : R;
+    if (cols == 0 && !loss_mask_row_sum) return SKYRL_OK;
+    if (cols == 0) cols = 1;
     dim3 grid(N + pad, (cols + kCols - 1) / kCols);
     auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool vec = S % kQ == 0 && R % kQ == 0 && a16(sequences) && a16(attention_mask) && a16(response_mask) &&
                      a16(rewards) && a16(loss_mask) && (!rollout_logprobs || a16(rollout_logprobs));
     if (vec)
         hipLaunchKernelGGL(pack_kernel<true>, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id,
-                           sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs);
+                           sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs,
+                           loss_mask_row_sum);
     else
         hipLaunchKernelGGL(pack_kernel<false>, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id,
-                           sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs);
+                           sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs,
+                           loss_mask_row_sum);
     return check_launch("pack_kernel");
 }
 

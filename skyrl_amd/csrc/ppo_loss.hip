@@ -10,12 +10,11 @@
 //   apply_reward_kl_penalty      trainer.py:981-1035
 //   ppo_critic_loss              utils/ppo_utils.py:175-193
 //
-// Layout: all per-token tensors f32 [n,R] row-major. Forward: grid (row, 1024-column chunk),
-// one token per thread; it reads 20 B/token (logp, old, adv, mask, ref), writes the per-token
-// gradient numerator (4 B/token) and a 5-float record per block; a one-block fold launch
-// folds the records into the scalar loss,
-// the metric vector and the per-row gradient scale. The backward is then a
-// 12 B/token elementwise pass (numerator, scale, upstream grad).
+// Layout: all per-token tensors f32 [n,R] row-major. The policy loss is ONE launch: grid
+// (row, 1024-column chunk), 4 tokens per thread; it reads 20 B/token (logp, old, adv, mask,
+// ref), writes the final dL/dlogp for a unit upstream gradient (4 B/token) and a 5-float
+// record per block, and the last-arriving block folds the records into the scalar loss and
+// the metric vector. The backward rescales in place only when the upstream gradient != 1.
 #include "arrive.h"
 
 // Phase timestamps for scripts/probe/phase_probe (compiled only there, never in the product).
@@ -37,10 +36,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kChunk = kThreads * 4;  // columns per block
 constexpr int kNP = 5;                // partials: sum l*m, m, clip*m, kl*m*m, ent*m
-constexpr int kRec = 8;               // partial record stride (floats): two 16-B loads per record
-constexpr int kPre = 1;               // rows per thread whose records the epilogue loads at once (1024 threads)
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
@@ -102,175 +98,258 @@ __device__ __forceinline__ TokenOut ppo_token(float lp, float old, float A, floa
     return o;
 }
 
+// ---- fused loss: ONE launch writes dL/dlogp (unit upstream gradient) + loss/metrics ----
 // Grid (row, 1024-column chunk), 256 threads x 4 tokens: every thread issues its 16-B loads
 // of all inputs at once, and the 4 independent tokens give the PPO/KL arithmetic (two
-// accurate expf, clamps, selects) ILP within the wave. Measured at [512, 1024]: this 4-wave
-// shape beats one token per thread in 1024-thread blocks (16-wave fold tail per block) and a
-// wave-per-row shape (16 tokens per lane, 1 wave per SIMD).
-constexpr int kFT = kThreads * 4;  // columns per block
+// accurate expf, clamps, selects) ILP within the wave. The reduction scale of every token is
+// known before the loss is: it depends on the loss mask only (token_mean 1/max(sum m, 1),
+// sequence_mean 1/(n*max(row m, 1)), seq_mean_token_sum_norm 1/(n*max_seq_len)), and the
+// per-row mask sums come in with the batch (pack emits them). So the gradient is final when
+// written: 4 B/token out for 20 B/token in.
+//
+// The scalar loss and the metrics come out of the same launch, and they need no per-row
+// state at fold time: with the row sums known up front, every reported quantity is a LINEAR
+// sum of per-token terms -- sum l*m*w_row (w = 1, 1/max(row m, 1) or 1/max_seq_len by
+// reduction), sum clip*m, sum kl*m*m/max(row m, 1), sum ent*m, sum m -- so each block
+// reduces its tokens to 5 numbers. Those are folded without any atomic read-modify-write
+// (one ticket counter hit by every block serialises at the L2, about 10 ns per block
+// measured: +5 us at 512 blocks, +80 us at 8192): each block publishes its 5 partials as
+// 8-byte {epoch, value} granules (one write-through 64-bit store each, untorn: guide G16
+// R2), laid out value-major so the folder's loads coalesce, and ONE designated block (the last
+// of the grid, after its own tokens) waits in a fixed order until every tag carries this
+// launch's epoch, then sums them in fp64. (A dedicated folder block polling from the start
+// measured slower: its sc1 polls slowed the workers' streams, 11.6 vs 8.4 us at 512 rows.) The epoch lives in the workspace and the folder advances it
+// at the end, so a replayed graph never mistakes the previous launch's granules for this
+// launch's. Every spin is bounded: on timeout the loss and the metrics are NaN and
+// metrics[6] = 1.
+constexpr int kFT = kThreads * 4;  // columns per work unit (one row chunk)
 constexpr int kFW = kThreads / kWave;
+constexpr int kInlineTotalRows = 1024;  // token_mean total summed by every block up to this n
+constexpr int kMaxGranPerThread = 8;    // folder: granule loads per thread per poll (x kNP)
+constexpr unsigned kMaxPolls = 1u << 22;
 
-__global__ __launch_bounds__(kThreads) void ppo_loss_fwd_kernel(
-    const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
-    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent, int n,
-    int R, skyrl_ppo_params p, bool vec4, float* __restrict__ gnum, float* __restrict__ partials) {
-    __shared__ float s_red[kFW * kNP];
-    PHASE(0);
-    const int row = blockIdx.x;
-    const int chunk = blockIdx.y;
-    const int nchunks = gridDim.y;
-    const float lo = (float)(1.0 - (double)p.eps_clip_low);
-    const float hi = (float)(1.0 + (double)p.eps_clip_high);
-    const int64_t rbase = (int64_t)row * R;
-    float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    auto tok = [&](float L, float O, float A, float M, float RF, float E) -> float {
-        const TokenOut t = ppo_token(L, O, A, lo, hi, p.clip_ratio_c, p.dual_clip);
-        acc[0] += t.loss * M;
-        acc[1] += M;
-        acc[2] += t.clip * M;
-        if (p.use_kl_loss) acc[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
-        acc[4] += E * M;
-        return t.dldlp * M;
-    };
-    const int c0 = chunk * kFT + threadIdx.x * 4;
-    if (vec4) {
-        if (c0 + 3 < R) {  // R % 4 == 0 on this path
-            const int64_t e = rbase + c0;
-            const float4 l4 = *reinterpret_cast<const float4*>(lp + e);
-            const float4 o4 = *reinterpret_cast<const float4*>(old + e);
-            const float4 a4 = *reinterpret_cast<const float4*>(adv + e);
-            const float4 m4 = mask ? *reinterpret_cast<const float4*>(mask + e) : make_float4(1.f, 1.f, 1.f, 1.f);
-            const float4 r4 = p.use_kl_loss ? *reinterpret_cast<const float4*>(ref + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 e4 = ent ? *reinterpret_cast<const float4*>(ent + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 g;
-            g.x = tok(l4.x, o4.x, a4.x, m4.x, r4.x, e4.x);
-            g.y = tok(l4.y, o4.y, a4.y, m4.y, r4.y, e4.y);
-            g.z = tok(l4.z, o4.z, a4.z, m4.z, r4.z, e4.z);
-            g.w = tok(l4.w, o4.w, a4.w, m4.w, r4.w, e4.w);
-            *reinterpret_cast<float4*>(gnum + e) = g;
-        }
-    } else {
-        for (int c = chunk * kFT + threadIdx.x; c < R && c < (chunk + 1) * kFT; c += kThreads) {
-            const int64_t e = rbase + c;
-            gnum[e] = tok(lp[e], old[e], adv[e], mask ? mask[e] : 1.f, p.use_kl_loss ? ref[e] : 0.f,
-                          ent ? ent[e] : 0.f);
-        }
-    }
-    PHASE(1);
-    block_sum<kFW, kNP>(acc, s_red);
-    if (threadIdx.x < kNP) partials[((int64_t)row * nchunks + chunk) * kRec + threadIdx.x] = acc[threadIdx.x];
-    PHASE(2);
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void store_granule(unsigned long long* g, unsigned epoch, float v) {
+    __hip_atomic_store((gu64*)g, ((unsigned long long)epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long load_granule(const unsigned long long* g) {
+    return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The fold runs as its own one-block launch: the kernel boundary publishes every record.
-// (An in-kernel last-arriver fold measured 13-16 us at n=512: each block drained its
-// stores before ticking, and the folding block's tail sat behind all of that.)
-constexpr int kFoldT = 256;
-__global__ __launch_bounds__(kFoldT) void ppo_loss_fold_kernel(int n, int nchunks, skyrl_ppo_params p,
-                                                               const float* __restrict__ partials,
-                                                               float* __restrict__ loss_out, float* __restrict__ metrics,
-                                                               float* __restrict__ row_scale) {
-    __shared__ double s_redd[(kFoldT / kWave) * 6];
-    PHASE(3);
-    // ---- epilogue: one block folds the n*nchunks partials ---------------------
-    // tot: 0 sum l*m, 1 sum m, 2 sum clip*m, 3 sum_rows row-reduced loss (seq modes),
-    //      4 sum_rows kl_row, 5 sum ent*m
-    double tot[6] = {0, 0, 0, 0, 0, 0};
-    // Each thread loads the chunk-0 records of kPre rows before the first wait (one
-    // dependent round trip for n <= kPre * kThreads rows), further chunks after.
-    for (int r0 = threadIdx.x; r0 < n; r0 += kFoldT * kPre) {
-        float4 rec[kPre][2];
+// Sum the nb blocks' granules (value-major [kNP][nb]) into the loss and the metric vector;
+// run by the whole folding block. Thread t owns blocks t, t + kThreads, ... (fixed order).
+__device__ void fold_granules(const unsigned long long* gran, unsigned epoch, int nb, int n,
+                              const skyrl_ppo_params& p, double* s_redd, float* __restrict__ loss_out,
+                              float* __restrict__ metrics) {
+    double tot[kNP] = {0, 0, 0, 0, 0};  // sum l*m*w, sum m, sum clip*m, sum kl*m*m/mrow, sum ent*m
+    bool timed_out = false;
+    for (int b0 = threadIdx.x; b0 < nb && !timed_out; b0 += kThreads * kMaxGranPerThread) {
+        float v[kMaxGranPerThread][kNP];
+        for (unsigned polls = 0;; ++polls) {
+            bool ok = true;
 #pragma unroll
-        for (int u = 0; u < kPre; ++u) {
-            const int r = r0 + u * kFoldT;
-            if (r < n) {
-                const float4* src = reinterpret_cast<const float4*>(partials + (int64_t)r * nchunks * kRec);
-                rec[u][0] = src[0];
-                rec[u][1] = src[1];
+            for (int u = 0; u < kMaxGranPerThread; ++u) {
+                const int b = b0 + u * kThreads;
+                if (b < nb) {
+#pragma unroll
+                    for (int k = 0; k < kNP; ++k) {
+                        const unsigned long long x = load_granule(gran + (int64_t)k * nb + b);
+                        v[u][k] = __uint_as_float((unsigned)x);
+                        ok = ok && (unsigned)(x >> 32) == epoch;
+                    }
+                }
             }
+            if (ok) break;
+            if (polls >= kMaxPolls) {
+                timed_out = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
         }
 #pragma unroll
-        for (int u = 0; u < kPre; ++u) {
-            const int r = r0 + u * kFoldT;
-            if (r >= n) break;
-            double rs[kNP] = {rec[u][0].x, rec[u][0].y, rec[u][0].z, rec[u][0].w, rec[u][1].x};
-            for (int c = 1; c < nchunks; ++c) {
-                const float* src = partials + ((int64_t)r * nchunks + c) * kRec;
+        for (int u = 0; u < kMaxGranPerThread; ++u)
+            if (b0 + u * kThreads < nb)
 #pragma unroll
-                for (int k = 0; k < kNP; ++k) rs[k] += (double)src[k];
-            }
-            const double mrow = rs[1] > 1.0 ? rs[1] : 1.0;  // mask.sum(-1).clamp(min=1)
-            tot[0] += rs[0];
-            tot[1] += rs[1];
-            tot[2] += rs[2];
-            tot[4] += rs[3] / mrow;
-            tot[5] += rs[4];
-            if (p.loss_reduction == 1) {
-                tot[3] += rs[0] / mrow;
-                row_scale[r] = (float)(1.0 / ((double)n * mrow));
-            } else if (p.loss_reduction == 2) {
-                tot[3] += rs[0] / (double)p.max_seq_len;
-                row_scale[r] = (float)(1.0 / ((double)n * (double)p.max_seq_len));
-            }
-        }
+                for (int k = 0; k < kNP; ++k) tot[k] += (double)v[u][k];
     }
-    PHASE(4);
-    block_sum_d<kFoldT / kWave, 6>(tot, s_redd);
-    const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
-    if (p.loss_reduction == 0) {
-        const float sc = (float)(1.0 / msum);
-        for (int r = threadIdx.x; r < n; r += kFoldT) row_scale[r] = sc;
-    }
+    const int any_timeout = __syncthreads_or(timed_out ? 1 : 0);
+    block_sum_d<kFW, kNP>(tot, s_redd);
     if (threadIdx.x == 0) {
-        float pg;
-        if (p.loss_reduction == 0) pg = (float)(tot[0] / msum);
-        else pg = (float)(tot[3] / (double)n);
-        const float clip_ratio = (float)(tot[2] / msum);
-        const float kl = p.use_kl_loss ? (float)(tot[4] / (double)n) : 0.f;
-        const float entropy = (float)(tot[5] / msum);
+        const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
+        float pg = p.loss_reduction == 0 ? (float)(tot[0] / msum) : (float)(tot[0] / (double)n);
+        float clip_ratio = (float)(tot[2] / msum);
+        float kl = p.use_kl_loss ? (float)(tot[3] / (double)n) : 0.f;
+        float entropy = (float)(tot[4] / msum);
         float final_loss = pg + kl * p.kl_loss_coef;
         if (p.use_entropy_loss) final_loss = final_loss - entropy * p.entropy_loss_coef;
+        float mask_sum = (float)tot[1];
+        if (any_timeout) pg = clip_ratio = kl = entropy = final_loss = mask_sum = __int_as_float(0x7fc00000);
         loss_out[0] = final_loss;
         metrics[SKYRL_M_FINAL_LOSS] = final_loss;
         metrics[SKYRL_M_POLICY_LOSS] = pg;
         metrics[SKYRL_M_ENTROPY] = entropy;
         metrics[SKYRL_M_KL] = kl;
         metrics[SKYRL_M_CLIP_RATIO] = clip_ratio;
-        metrics[SKYRL_M_MASK_SUM] = (float)tot[1];
-        metrics[6] = 0.f;
+        metrics[SKYRL_M_MASK_SUM] = mask_sum;
+        metrics[6] = any_timeout ? 1.f : 0.f;  // fold timed out
         metrics[7] = 0.f;
     }
-    PHASE(5);
 }
 
-__global__ __launch_bounds__(kThreads) void ppo_loss_bwd_kernel(
-    const float* __restrict__ gout, const float* __restrict__ gnum, const float* __restrict__ row_scale,
-    const float* __restrict__ mask, const float* __restrict__ metrics, int R, int use_ent, float ent_coef,
-    bool vec4, float* __restrict__ glp, float* __restrict__ gent) {
-    const int row = blockIdx.x;
-    const float g = gout[0];
-    const float s = g * row_scale[row];
-    float es = 0.f;
-    if (use_ent) {
-        const float ms = metrics[SKYRL_M_MASK_SUM];
-        es = -(g * ent_coef) / (ms > 1.f ? ms : 1.f);
+// Per-row sums of the loss mask (one wave per row), for callers that do not carry them.
+__global__ __launch_bounds__(kThreads) void mask_row_sum_kernel(const float* __restrict__ mask, int n, int R,
+                                                                float* __restrict__ out) {
+    const int row = blockIdx.x * kFW + threadIdx.x / kWave;
+    if (row >= n) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const float* m = mask + (int64_t)row * R;
+    float acc = 0.f;
+    for (int t = lane; t < R; t += kWave) acc += m[t];
+    acc = wave_sum(acc);
+    if (lane == 0) out[row] = acc;
+}
+
+// token_mean total: sum of n row sums in fp64 in a fixed order (bit-identical in every block).
+__global__ __launch_bounds__(kThreads) void mask_total_kernel(const float* __restrict__ row_msum, int n,
+                                                              float* __restrict__ total) {
+    __shared__ double s[kFW];
+    double t[1] = {0.0};
+    for (int r = threadIdx.x; r < n; r += kThreads) t[0] += (double)row_msum[r];
+    block_sum_d<kFW, 1>(t, s);
+    if (threadIdx.x == 0) total[0] = (float)t[0];
+}
+
+// Work unit = one 1024-column chunk of one row; block b takes units [b*U, b*U + U). U = 1 up
+// to 2048 units (512 rows: 8.4 us vs 10.1 at U = 2 and 13.6 at U = 4, measured), U = 4 above
+// (8192 rows: 63 us vs 80 at U = 1: a quarter of the granules to fold).
+template <bool VEC4, int U>
+__global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
+    const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
+    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent,
+    const float* __restrict__ row_msum, const float* __restrict__ msum_total, int n, int R, int nchunks,
+    skyrl_ppo_params p, float* __restrict__ glp, float* __restrict__ gent, unsigned long long* __restrict__ gran,
+    unsigned* __restrict__ epoch_word, float* __restrict__ loss_out, float* __restrict__ metrics) {
+    __shared__ float s_red[kFW * kNP];
+    __shared__ double s_redd[kFW * kNP];
+    __shared__ unsigned s_epoch;
+    PHASE(0);
+    if (threadIdx.x == 0) s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const int units = n * nchunks;
+    const int nb = gridDim.x;
+    const int wb = blockIdx.x;
+    const float lo = (float)(1.0 - (double)p.eps_clip_low);
+    const float hi = (float)(1.0 + (double)p.eps_clip_high);
+    // issue every 16-B load of all U units first (R % 4 == 0 on the VEC4 path)
+    float4 l4[U], o4[U], a4[U], m4[U], r4[U], e4[U];
+    int row_u[U];
+    bool live[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int unit = wb * U + u;
+        row_u[u] = unit < units ? unit / nchunks : 0;
+        const int c0 = (unit - row_u[u] * nchunks) * kFT + threadIdx.x * 4;
+        live[u] = VEC4 && unit < units && c0 + 3 < R;
+        l4[u] = o4[u] = a4[u] = r4[u] = e4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        m4[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (live[u]) {
+            const int64_t e = (int64_t)row_u[u] * R + c0;
+            l4[u] = *reinterpret_cast<const float4*>(lp + e);
+            o4[u] = *reinterpret_cast<const float4*>(old + e);
+            a4[u] = *reinterpret_cast<const float4*>(adv + e);
+            if (mask) m4[u] = *reinterpret_cast<const float4*>(mask + e);
+            if (p.use_kl_loss) r4[u] = *reinterpret_cast<const float4*>(ref + e);
+            if (ent) e4[u] = *reinterpret_cast<const float4*>(ent + e);
+        }
     }
-    const int64_t rbase = (int64_t)row * R;
-    const int c0 = blockIdx.y * kChunk + threadIdx.x * 4;
-    if (vec4) {
-        if (c0 + 3 < R) {
-            float4 u = *reinterpret_cast<const float4*>(gnum + rbase + c0);
-            *reinterpret_cast<float4*>(glp + rbase + c0) = make_float4(u.x * s, u.y * s, u.z * s, u.w * s);
-            if (use_ent) {
-                float4 m = mask ? *reinterpret_cast<const float4*>(mask + rbase + c0) : make_float4(1.f, 1.f, 1.f, 1.f);
-                *reinterpret_cast<float4*>(gent + rbase + c0) = make_float4(es * m.x, es * m.y, es * m.z, es * m.w);
+    // the mask-only scales while the loads are in flight
+    const bool need_total = p.loss_reduction == 0 || (p.use_entropy_loss && gent);
+    // every wave sums the n row sums itself (same lanes, same order, xor tree: the same value
+    // in every wave of every block), so no barrier stands between the loads and the math
+    float total = 0.f;
+    if (need_total) {
+        if (msum_total) {
+            total = msum_total[0];
+        } else {
+            const int lane = threadIdx.x & (kWave - 1);
+            for (int r = lane; r < n; r += kWave) total += row_msum[r];
+            total = wave_sum(total);
+        }
+    }
+    const float tok_scale = 1.f / (total > 1.f ? total : 1.f);  // token_mean
+    const float escale = need_total ? -(p.entropy_loss_coef / (total > 1.f ? total : 1.f)) : 0.f;
+    PHASE(4);
+
+    float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};  // sum l*m*w, m, clip*m, kl*m*m/mrow, ent*m
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int unit = wb * U + u;
+        if (unit >= units) break;
+        const int row = row_u[u];
+        const double mr = (double)row_msum[row];
+        const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
+        float scale, w;  // gradient scale; weight of the row's l*m in the pg sum
+        if (p.loss_reduction == 0) { scale = tok_scale; w = 1.f; }
+        else if (p.loss_reduction == 1) { scale = (float)(1.0 / ((double)n * (mr > 1.0 ? mr : 1.0))); w = inv_mrow; }
+        else { scale = (float)(1.0 / ((double)n * (double)p.max_seq_len)); w = (float)(1.0 / (double)p.max_seq_len); }
+        float a[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        auto tok = [&](float L, float O, float A, float M, float RF, float E) -> float {
+            const TokenOut t = ppo_token(L, O, A, lo, hi, p.clip_ratio_c, p.dual_clip);
+            a[0] += t.loss * M;
+            a[1] += M;
+            a[2] += t.clip * M;
+            if (p.use_kl_loss) a[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
+            a[4] += E * M;
+            return (t.dldlp * M) * scale;
+        };
+        const int64_t rbase = (int64_t)row * R;
+        const int chunk = unit - row * nchunks;
+        if (VEC4) {
+            if (live[u]) {
+                const int64_t e = rbase + chunk * kFT + threadIdx.x * 4;
+                float4 g;
+                g.x = tok(l4[u].x, o4[u].x, a4[u].x, m4[u].x, r4[u].x, e4[u].x);
+                g.y = tok(l4[u].y, o4[u].y, a4[u].y, m4[u].y, r4[u].y, e4[u].y);
+                g.z = tok(l4[u].z, o4[u].z, a4[u].z, m4[u].z, r4[u].z, e4[u].z);
+                g.w = tok(l4[u].w, o4[u].w, a4[u].w, m4[u].w, r4[u].w, e4[u].w);
+                *reinterpret_cast<float4*>(glp + e) = g;
+                if (gent) *reinterpret_cast<float4*>(gent + e) =
+                    make_float4(escale * m4[u].x, escale * m4[u].y, escale * m4[u].z, escale * m4[u].w);
+            }
+        } else {
+            for (int c = chunk * kFT + threadIdx.x; c < R && c < (chunk + 1) * kFT; c += kThreads) {
+                const int64_t e = rbase + c;
+                const float M = mask ? mask[e] : 1.f;
+                glp[e] = tok(lp[e], old[e], adv[e], M, p.use_kl_loss ? ref[e] : 0.f, ent ? ent[e] : 0.f);
+                if (gent) gent[e] = escale * M;
             }
         }
-    } else {
-        for (int c = blockIdx.y * kChunk + threadIdx.x; c < R && c < (blockIdx.y + 1) * kChunk; c += kThreads) {
-            glp[rbase + c] = gnum[rbase + c] * s;
-            if (use_ent) gent[rbase + c] = es * (mask ? mask[rbase + c] : 1.f);
-        }
+        acc[0] += a[0] * w;
+        acc[1] += a[1];
+        acc[2] += a[2];
+        acc[3] += a[3] * inv_mrow;
+        acc[4] += a[4];
+    }
+    PHASE(1);
+    block_sum<kFW, kNP>(acc, s_red);  // (its barrier also publishes s_epoch)
+    const unsigned epoch = s_epoch;
+    if (threadIdx.x < kNP) store_granule(gran + (int64_t)threadIdx.x * nb + wb, epoch, acc[threadIdx.x]);
+    if (wb != nb - 1) return;
+    PHASE(2);
+    fold_granules(gran, epoch, nb, n, p, s_redd, loss_out, metrics);
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)epoch_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PHASE(3);
+}
+
+// In-place x *= g[0] (the autograd backward of the fused loss); nothing is touched when g == 1.
+__global__ void rescale_kernel(const float* __restrict__ g, float* __restrict__ x, float* __restrict__ y, int64_t n) {
+    const float s = g[0];
+    if (s == 1.0f) return;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        x[i] *= s;
+        if (y) y[i] *= s;
     }
 }
 
@@ -388,6 +467,11 @@ __global__ __launch_bounds__(kThreads) void critic_loss_kernel(
     }
 }
 
+__global__ void fill_kernel(float* __restrict__ x, int n, float v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = v;
+}
+
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16) == 0; }
 
 }  // namespace
@@ -395,53 +479,92 @@ inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<
 
 using namespace skyrl;
 
+namespace skyrl {
+int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
+}
+
 extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
     const size_t nchunks = (size_t)((R + kFT - 1) / kFT);
-    const size_t parts = (size_t)(n > 0 ? n : 1) * (nchunks ? nchunks : 1) * kRec * sizeof(float);
-    return 256 + ((parts + 255) / 256) * 256;  // [counter | pad][partials]
+    const size_t nn = (size_t)(n > 0 ? n : 1);
+    const size_t parts = nn * (nchunks ? nchunks : 1) * kNP * sizeof(unsigned long long);
+    const size_t rows = ((nn * sizeof(float) + 255) / 256) * 256;
+    // [epoch | total | pad][granules][row mask sums]
+    return 256 + ((parts + 255) / 256) * 256 + rows;
 }
 
 extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const float* advantages,
                                   const float* loss_mask, const float* ref_log_probs, const float* entropy,
-                                  int32_t n, int32_t R, const skyrl_ppo_params* params, float* loss_out,
-                                  float* metrics_out, float* grad_num, float* row_scale, void* workspace,
-                                  void* stream) {
+                                  const float* row_mask_sum, int32_t n, int32_t R, const skyrl_ppo_params* params,
+                                  float* loss_out, float* metrics_out, float* grad_logp, float* grad_entropy,
+                                  void* workspace, void* stream) {
     SKYRL_REQUIRE(params, "ppo_loss_fwd: params is null");
     SKYRL_REQUIRE(n > 0 && R > 0, "ppo_loss_fwd: empty batch");
-    SKYRL_REQUIRE(log_probs && old_log_probs && advantages && loss_out && metrics_out && grad_num && row_scale &&
-                      workspace,
+    SKYRL_REQUIRE(log_probs && old_log_probs && advantages && loss_out && metrics_out && grad_logp && workspace,
                   "ppo_loss_fwd: null pointer");
     SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "ppo_loss_fwd: use_kl_loss needs ref_log_probs");
     SKYRL_REQUIRE(params->loss_reduction >= 0 && params->loss_reduction <= 2, "ppo_loss_fwd: bad loss_reduction");
     SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
                   "ppo_loss_fwd: seq_mean_token_sum_norm needs max_seq_len");
     SKYRL_REQUIRE(params->kl_type >= 0 && params->kl_type <= 3, "ppo_loss_fwd: bad kl_type");
-    float* partials = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256);
+    SKYRL_REQUIRE(!grad_entropy || params->use_entropy_loss, "ppo_loss_fwd: grad_entropy needs use_entropy_loss");
+    const int nchunks = (R + kFT - 1) / kFT;
+    char* w = reinterpret_cast<char*>(workspace);
+    unsigned* epoch_word = reinterpret_cast<unsigned*>(w);
+    float* total = reinterpret_cast<float*>(w + 64);
+    unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + 256);
+    const size_t parts = (size_t)n * nchunks * kNP * sizeof(unsigned long long);
+    float* rows_ws = reinterpret_cast<float*>(w + 256 + ((parts + 255) / 256) * 256);
+    hipStream_t s = as_stream(stream);
+    const float* rows = row_mask_sum;
+    if (!rows) {  // the caller does not carry the loss-mask row sums: one extra launch
+        if (loss_mask) {
+            hipLaunchKernelGGL(mask_row_sum_kernel, dim3((n + kFW - 1) / kFW), dim3(kThreads), 0, s, loss_mask, n, R,
+                               rows_ws);
+            int rc = check_launch("mask_row_sum_kernel");
+            if (rc) return rc;
+        } else {
+            hipLaunchKernelGGL(fill_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, rows_ws, n,
+                               (float)R);
+            int rc = check_launch("fill_kernel");
+            if (rc) return rc;
+        }
+        rows = rows_ws;
+    }
+    const bool need_total = params->loss_reduction == 0 || (params->use_entropy_loss && grad_entropy);
+    const float* tot = nullptr;
+    if (need_total && n > kInlineTotalRows) {
+        hipLaunchKernelGGL(mask_total_kernel, dim3(1), dim3(kThreads), 0, s, rows, n, total);
+        int rc = check_launch("mask_total_kernel");
+        if (rc) return rc;
+        tot = total;
+    }
     const bool vec4 = (R % 4) == 0 && aligned16(log_probs) && aligned16(old_log_probs) && aligned16(advantages) &&
-                      aligned16(loss_mask) && aligned16(ref_log_probs) && aligned16(entropy) && aligned16(grad_num);
-    dim3 grid(n, (R + kFT - 1) / kFT);
-    hipLaunchKernelGGL(ppo_loss_fwd_kernel, grid, dim3(kThreads), 0, as_stream(stream), log_probs, old_log_probs,
-                       advantages, loss_mask, ref_log_probs, entropy, n, R, *params, vec4, grad_num, partials);
-    int rc = check_launch("ppo_loss_fwd_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(ppo_loss_fold_kernel, dim3(1), dim3(kFoldT), 0, as_stream(stream), n, (int)grid.y, *params,
-                       partials, loss_out, metrics_out, row_scale);
-    return check_launch("ppo_loss_fold_kernel");
+                      aligned16(loss_mask) && aligned16(ref_log_probs) && aligned16(entropy) && aligned16(grad_logp) &&
+                      aligned16(grad_entropy);
+    const int units = n * nchunks;
+    int U = g_loss_units > 0 ? g_loss_units : (units > 2048 ? 4 : 1);
+    if (!vec4) U = 1;
+    const int nb = (units + U - 1) / U;
+    auto k = !vec4 ? ppo_loss_grad_kernel<false, 1>
+             : U == 1 ? ppo_loss_grad_kernel<true, 1> : U == 2 ? ppo_loss_grad_kernel<true, 2>
+                                                            : ppo_loss_grad_kernel<true, 4>;
+    hipLaunchKernelGGL(k, dim3(nb), dim3(kThreads), 0, s, log_probs, old_log_probs, advantages, loss_mask, ref_log_probs,
+                       entropy, rows, tot, n, R, nchunks, *params, grad_logp, grad_entropy, gran, epoch_word, loss_out,
+                       metrics_out);
+    return check_launch("ppo_loss_grad_kernel");
 }
 
-extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, const float* grad_num, const float* row_scale,
-                                  const float* loss_mask, const float* metrics, int32_t n, int32_t R,
-                                  const skyrl_ppo_params* params, float* grad_logp, float* grad_entropy,
+extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, int64_t numel, float* grad_logp, float* grad_entropy,
                                   void* stream) {
-    SKYRL_REQUIRE(params && grad_out && grad_num && row_scale && grad_logp && metrics, "ppo_loss_bwd: null pointer");
-    SKYRL_REQUIRE(n > 0 && R > 0, "ppo_loss_bwd: empty batch");
-    const int use_ent = params->use_entropy_loss && grad_entropy != nullptr;
-    const bool vec4 = (R % 4) == 0 && aligned16(grad_num) && aligned16(grad_logp) && aligned16(loss_mask) &&
-                      aligned16(grad_entropy);
-    dim3 grid(n, (R + kChunk - 1) / kChunk);
-    hipLaunchKernelGGL(ppo_loss_bwd_kernel, grid, dim3(kThreads), 0, as_stream(stream), grad_out, grad_num, row_scale,
-                       loss_mask, metrics, R, use_ent, params->entropy_loss_coef, vec4, grad_logp, grad_entropy);
-    return check_launch("ppo_loss_bwd_kernel");
+    SKYRL_REQUIRE(grad_out && grad_logp, "ppo_loss_bwd: null pointer");
+    SKYRL_REQUIRE(numel >= 0, "ppo_loss_bwd: negative size");
+    if (numel == 0) return SKYRL_OK;
+    // a small grid: at unit upstream gradient (the common case) the launch only dispatches
+    int64_t blocks = (numel + kThreads - 1) / kThreads;
+    if (blocks > 256) blocks = 256;
+    hipLaunchKernelGGL(rescale_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, as_stream(stream), grad_out,
+                       grad_logp, grad_entropy, numel);
+    return check_launch("rescale_kernel");
 }
 
 extern "C" int skyrl_approx_kl(const float* log_probs, const float* log_probs_base, const void* loss_mask,

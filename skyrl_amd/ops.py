@@ -280,7 +280,9 @@ def make_ppo_params(
 
 
 class PPOLossFunction(torch.autograd.Function):
-    """Fused policy loss (+KL(ref) +entropy term) with a HIP forward and backward.
+    """Fused policy loss (+KL(ref) +entropy term): ONE HIP launch computes the loss, the
+    metrics and the final dL/dlogp (and dL/dentropy) for a unit upstream gradient; the
+    backward rescales them in place only when the upstream gradient is not 1.
 
     forward returns (loss 0-d, metrics f32[8] device). Gradients flow to log_probs and,
     when params.use_entropy_loss, to entropy. The KL term has no gradient (reference:
@@ -288,7 +290,8 @@ class PPOLossFunction(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params):
+    def forward(ctx, log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params,
+                loss_mask_row_sum):
         dev = _require_gpu(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy)
         lp = _f32c(log_probs.detach(), "log_probs")
         old = _f32c(old_log_probs.detach(), "old_log_probs")
@@ -302,41 +305,43 @@ class PPOLossFunction(torch.autograd.Function):
             if t is not None and t.shape != lp.shape:
                 raise ValueError(f"{name} shape {tuple(t.shape)} != log_probs shape {tuple(lp.shape)}")
         n, R = lp.shape
+        rows = None
+        if loss_mask_row_sum is not None:
+            rows = _f32c(loss_mask_row_sum.detach(), "loss_mask_row_sum")
+            if tuple(rows.shape) != (n,):
+                raise ValueError(f"loss_mask_row_sum shape {tuple(rows.shape)} != {(n,)}")
         loss = torch.empty((), dtype=torch.float32, device=dev)
         metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
-        gnum = torch.empty_like(lp)
-        row_scale = torch.empty(n, dtype=torch.float32, device=dev)
+        glp = torch.empty_like(lp)
+        want_ent = bool(params.use_entropy_loss) and entropy is not None and ctx.needs_input_grad[5]
+        gent = torch.empty_like(lp) if want_ent else None
         ws = WORKSPACES.get(dev, "ppo", _ffi.query("skyrl_ppo_loss_workspace_bytes", n, R))
         _ffi.call(
-            "skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), _ptr(ent), n, R,
-            ctypes.byref(params), _ptr(loss), _ptr(metrics), _ptr(gnum), _ptr(row_scale), _ptr(ws), _stream(dev),
+            "skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), _ptr(ent), _ptr(rows), n, R,
+            ctypes.byref(params), _ptr(loss), _ptr(metrics), _ptr(glp), _ptr(gent), _ptr(ws), _stream(dev),
         )
-        ctx.params = params
-        ctx.has_entropy = entropy is not None
-        ctx.save_for_backward(gnum, row_scale, mask, metrics)
+        ctx.save_for_backward(glp, gent)
         ctx.mark_non_differentiable(metrics)
+        ctx.used = False
         return loss, metrics
 
     @staticmethod
     def backward(ctx, grad_loss, grad_metrics):
-        gnum, row_scale, mask, metrics = ctx.saved_tensors
-        params = ctx.params
-        dev = gnum.device
-        n, R = gnum.shape
+        if ctx.used:  # the gradients are rescaled in place
+            raise RuntimeError("the fused PPO loss supports a single backward pass")
+        ctx.used = True
+        glp, gent = ctx.saved_tensors
         g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
-        glp = torch.empty_like(gnum)
-        want_ent = bool(params.use_entropy_loss) and ctx.has_entropy and ctx.needs_input_grad[5]
-        gent = torch.empty_like(gnum) if want_ent else None
-        _ffi.call(
-            "skyrl_ppo_loss_bwd", _ptr(g), _ptr(gnum), _ptr(row_scale), _ptr(mask), _ptr(metrics), n, R,
-            ctypes.byref(params), _ptr(glp), _ptr(gent), _stream(dev),
-        )
-        return glp, None, None, None, None, gent, None
+        _ffi.call("skyrl_ppo_loss_bwd", _ptr(g), glp.numel(), _ptr(glp), _ptr(gent), _stream(glp.device))
+        return glp, None, None, None, None, gent, None, None
 
 
-def ppo_loss(log_probs, old_log_probs, advantages, loss_mask, params, ref_log_probs=None, entropy=None):
-    """Fused loss; returns (loss 0-d tensor, metrics device tensor [8])."""
-    return PPOLossFunction.apply(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params)
+def ppo_loss(log_probs, old_log_probs, advantages, loss_mask, params, ref_log_probs=None, entropy=None,
+             loss_mask_row_sum=None):
+    """Fused loss; returns (loss 0-d tensor, metrics device tensor [8]). ``loss_mask_row_sum``
+    (f32 [n], per-row sums of ``loss_mask``, as pack_experience emits them) saves one launch."""
+    return PPOLossFunction.apply(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params,
+                                 loss_mask_row_sum)
 
 
 # ---------------------------------------------------------------------------- a8 critic loss
@@ -545,9 +550,10 @@ def pack_experience(
     reward_vals: torch.Tensor, reward_off: torch.Tensor,
     loss_mask_vals: torch.Tensor, loss_mask_off: torch.Tensor,
     logprob_vals: Optional[torch.Tensor], logprob_off: Optional[torch.Tensor],
-    *, N: int, P: int, R: int, pad: int = 0, pad_token_id: int = 0,
+    *, N: int, P: int, R: int, pad: int = 0, pad_token_id: int = 0, return_row_sums: bool = False,
 ):
-    """Device CSR inputs -> (sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs)."""
+    """Device CSR inputs -> (sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs)
+    [+ loss_mask_row_sum f32 [N+pad] when ``return_row_sums``]."""
     dev = _require_gpu(prompt_tokens, response_tokens, reward_vals, loss_mask_vals)
 
     def i64(t):
@@ -570,10 +576,13 @@ def pack_experience(
     rew = torch.empty((Np, R), dtype=torch.float32, device=dev)
     lmask = torch.empty((Np, R), dtype=torch.float32, device=dev)
     rlp = torch.empty((Np, R), dtype=torch.float32, device=dev) if has_lp else None
+    rows = torch.empty(Np, dtype=torch.float32, device=dev) if return_row_sums else None
     _ffi.call(
         "skyrl_pack_experience", ctypes.byref(ins), N, pad, P, R, int(pad_token_id), _ptr(seq), _ptr(att),
-        _ptr(rmask), _ptr(rew), _ptr(lmask), _ptr(rlp), _stream(dev),
+        _ptr(rmask), _ptr(rew), _ptr(lmask), _ptr(rlp), _ptr(rows), _stream(dev),
     )
+    if return_row_sums:
+        return seq, att, rmask, rew, lmask, rlp, rows
     return seq, att, rmask, rew, lmask, rlp
 
 

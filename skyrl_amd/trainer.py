@@ -92,7 +92,9 @@ class GRPOTrainer:
         env extras and runs the multi-turn agent loop: rewards and loss masks come from it.
         Under data parallelism (one process per GPU, `dp_group` initialised) every rank steps on
         its own prompts with its own colocated engine; gradients are mean-reduced in buckets
-        before clipping (comm.allreduce_grads) and metrics are all-reduced."""
+        whose all-reduces are launched from the last micro-batch's backward as each bucket
+        completes (comm.BucketedGradAllReduce, overlapped with the rest of the backward), and
+        metrics are all-reduced."""
         self.dp_group = dp_group
         self.generator = generator
         self.env_class = env_class
@@ -113,6 +115,11 @@ class GRPOTrainer:
             for m in (policy, ref, critic.model if critic is not None else None):
                 if m is not None:
                     enable_sample_packing(m)
+        world = torch.distributed.get_world_size(dp_group) if (
+            torch.distributed.is_available() and torch.distributed.is_initialized()) else 1
+        self.grad_sync = comm.BucketedGradAllReduce(policy.parameters(), dp_group) if world > 1 else None
+        self.critic_grad_sync = (comm.BucketedGradAllReduce(critic.parameters(), dp_group)
+                                 if world > 1 and critic is not None else None)
         self.global_step = 0
         self.timings: Dict[str, float] = {}  # seconds per phase of the last step (device-synchronised)
         self._t = 0.0
@@ -260,14 +267,20 @@ class GRPOTrainer:
                                     self.cfg.use_sample_packing).float()
                 loss, clipfrac = ppo_utils.ppo_critic_loss(v, data["values"][i:j], data["returns"][i:j],
                                                            cfg.algorithm, loss_mask=data["loss_mask"][i:j])
+                if self.critic_grad_sync is not None and j == s1:
+                    self.critic_grad_sync.arm()
                 (loss / n_micro).backward()
                 acc.setdefault("critic_loss", []).append(float(loss.detach()))
                 if clipfrac is not None:
                     acc.setdefault("values_clipfrac", []).append(clipfrac)
-            comm.allreduce_grads(self.critic.parameters(), self.dp_group)
+            if self.critic_grad_sync is not None:
+                self.critic_grad_sync.wait()
             gn = torch.nn.utils.clip_grad_norm_(self.critic.parameters(), cfg.max_grad_norm)
             self.critic_optimizer.step()
-            self.critic_optimizer.zero_grad(set_to_none=True)
+            if self.critic_grad_sync is not None:
+                self.critic_grad_sync.zero_grad()
+            else:
+                self.critic_optimizer.zero_grad(set_to_none=True)
             acc.setdefault("critic_grad_norm", []).append(float(gn))
         return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
                                        device=next(self.critic.parameters()).device)
@@ -291,12 +304,18 @@ class GRPOTrainer:
                                              grad=True)
                     ref = data["base_action_log_probs"][i:j] if self.ref is not None else None
                     loss, met = self._loss(lp, data, i, j, ref, ent)
+                    if self.grad_sync is not None and j == s1:
+                        self.grad_sync.arm()  # the last micro-batch: buckets all-reduce during its backward
                     (loss / n_micro).backward()
                     mets.append(met)
-                comm.allreduce_grads(self.policy.parameters(), self.dp_group)
+                if self.grad_sync is not None:
+                    self.grad_sync.wait()
                 grad_norm = torch.nn.utils.clip_grad_norm_(self.policy.parameters(), cfg.max_grad_norm)
                 self.optimizer.step()
-                self.optimizer.zero_grad(set_to_none=True)
+                if self.grad_sync is not None:
+                    self.grad_sync.zero_grad()
+                else:
+                    self.optimizer.zero_grad(set_to_none=True)
                 mt = torch.stack(mets).mean(0).tolist()
                 for k, v in (("final_loss", mt[0]), ("policy_loss", mt[1]), ("policy_entropy", mt[2]),
                              ("policy_kl", mt[3]), ("ppo_clip_ratio", mt[4]), ("grad_norm", float(grad_norm))):

@@ -215,3 +215,41 @@ def _grad_allreduce_case(rank, world):
 
 def test_allreduce_grads_gloo():
     _run(_grad_allreduce_case)
+
+
+# --------------------------------------------------------------------------- a12, overlapped
+def _mlp(seed):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(12, 32), torch.nn.Tanh(), torch.nn.Linear(32, 32), torch.nn.Tanh(),
+                               torch.nn.Linear(32, 5))
+
+
+def _bucketed_case(rank, world):
+    """BucketedGradAllReduce: buckets launched from the last micro-batch's backward hooks give
+    the DP mean of the accumulated micro-batch gradients (FSDP2's reduce during backward)."""
+    model = _mlp(0)
+    ref = _mlp(0)
+    sync = comm.BucketedGradAllReduce(model.parameters(), bucket_bytes=100 * 4)
+    assert len(sync.buckets) >= 3
+    g = torch.Generator().manual_seed(100 + rank)
+    xs = [torch.randn(7, 12, generator=g) for _ in range(2)]
+    for step in range(2):
+        for k, x in enumerate(xs):
+            if k == len(xs) - 1:
+                sync.arm()
+            (model(x * (step + 1)).square().mean() / len(xs)).backward()
+            (ref(x * (step + 1)).square().mean() / len(xs)).backward()
+        launched = sync.wait()
+        assert launched == len(sync.buckets)  # every bucket went out from inside the backward
+        for p, q in zip(model.parameters(), ref.parameters()):
+            local = q.grad.clone()
+            allg = [torch.empty_like(local) for _ in range(world)]
+            dist.all_gather(allg, local)
+            torch.testing.assert_close(p.grad, sum(allg) / world, atol=1e-6, rtol=1e-6)
+        sync.zero_grad()
+        for q in ref.parameters():
+            q.grad = None
+
+
+def test_bucketed_grad_allreduce_during_backward_gloo():
+    _run(_bucketed_case)

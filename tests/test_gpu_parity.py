@@ -208,6 +208,62 @@ def test_ppo_north_star_size_vs_oracle(dev):
     close(x.grad, xc.grad, atol=1e-9, rtol=1e-4)
 
 
+@pytest.mark.parametrize("red", ["token_mean", "sequence_mean", "seq_mean_token_sum_norm"])
+@pytest.mark.parametrize("n", [37, 1500])
+def test_ppo_one_launch_paths_agree(dev, red, n):
+    """The one-launch loss with the pack's row sums, with in-kernel row sums, and (n > 1024)
+    with the separate token_mean total all give the oracle's loss/metrics/gradients; the
+    backward rescales by a non-unit upstream gradient (and leaves unit ones untouched)."""
+    g = torch.Generator().manual_seed(n)
+    for R in (300, 1024, 2500):
+        lens = torch.randint(0, R + 1, (n,), generator=g)
+        mask = (torch.arange(R)[None] < lens[:, None]).float()
+        lp = -2 + 0.1 * torch.randn(n, R, generator=g)
+        old = lp + 0.05 * torch.randn(n, R, generator=g)
+        ref = lp + 0.05 * torch.randn(n, R, generator=g)
+        adv = torch.randn(n, R, generator=g) * mask
+        ent = torch.rand(n, R, generator=g)
+        cfg = AlgorithmConfig(loss_reduction=red, max_seq_len=R, use_entropy_loss=True, entropy_loss_coef=0.01,
+                              policy_loss_type="dual_clip")
+        params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=True, has_entropy=True)
+        xc = lp.clone().requires_grad_(True)
+        ec = ent.clone().requires_grad_(True)
+        e, em = cpu_ref.policy_loss_assembly(xc, old, adv, mask, ref, ec, use_entropy_loss=True, ent_coef=0.01,
+                                             reduction=red, max_seq_len=R, dual_clip=True)
+        (e * 2.5).backward()
+        outs = []
+        for rows in (mask.sum(-1).to(dev), None):
+            x = lp.to(dev).requires_grad_(True)
+            en = ent.to(dev).requires_grad_(True)
+            loss, m = ops.ppo_loss(x, old.to(dev), adv.to(dev), mask.to(dev), params, ref.to(dev), en,
+                                   loss_mask_row_sum=rows)
+            (loss * 2.5).backward()
+            close(loss, e, atol=1e-6, rtol=1e-5)
+            close(m[4], em["clip_ratio"], atol=1e-6)
+            close(m[3], em["policy_kl"], atol=1e-6, rtol=1e-5)
+            close(m[5], mask.sum(), atol=0)
+            close(x.grad, xc.grad, atol=1e-9, rtol=1e-4)
+            close(en.grad, ec.grad, atol=1e-12, rtol=1e-5)
+            outs.append((loss.detach().cpu(), x.grad.cpu(), m.cpu()))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        assert torch.equal(outs[0][2], outs[1][2])
+
+
+def test_pack_emits_loss_mask_row_sums(golden, dev):
+    d = golden("pack")
+    N = len(d["prompt_off"]) - 1
+    P = int((d["prompt_off"][1:] - d["prompt_off"][:-1]).max())
+    R = int((d["response_off"][1:] - d["response_off"][:-1]).max())
+    pad = int(d["pad_size"])
+    out = ops.pack_experience(d["prompt_vals"].to(dev), d["prompt_off"], d["response_vals"].to(dev),
+                              d["response_off"], d["reward_vals"].to(dev), d["reward_off"],
+                              d["loss_mask_vals"].to(dev), d["loss_mask_off"], d["logprob_vals"].to(dev),
+                              d["logprob_off"], N=N, P=P, R=R, pad=pad, pad_token_id=0, return_row_sums=True)
+    assert len(out) == 7
+    assert torch.equal(out[4].cpu(), d["p_loss_mask"])
+    assert torch.equal(out[6].cpu(), d["p_loss_mask"].sum(-1))
+
+
 @pytest.mark.parametrize("case", ["tis_token", "tis_seq", "mask_geo", "mask_prod", "tis_outlier"])
 @pytest.mark.parametrize("lt", ["regular", "dual_clip"])
 def test_ppo_off_policy_correction_golden(golden, dev, case, lt):
