@@ -241,7 +241,7 @@ def run(args):
                     ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(old_lp[s:s + mb]),
                     ops._ptr(adv[s:s + mb]), ops._ptr(lmask[s:s + mb]), ops._ptr(ref_lp[s:s + mb]),
                     ctypes.byref(params), ops._ptr(loss_buf), ops._ptr(met_buf), ops._ptr(lp), ops._ptr(ent),
-                    ops._ptr(dlogits), ops._ptr(train_ws), ops._stream(dev)))
+                    ops._ptr(dlogits), R * V, V, ops._ptr(train_ws), ops._stream(dev)))
                 metrics_acc.add_(met_buf)
         if world > 1:
             dist.all_reduce(metrics_acc)
@@ -350,6 +350,8 @@ def run(args):
                                     "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
     if not args.no_attention_leg:
         result["rollout_attention"] = rollout_attention_leg(dev, N)
+    if not args.no_vocab_legs:
+        result["policy_train_vocabs"] = policy_train_vocab_legs(dev, mb, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -481,6 +483,47 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
     gbs = nbytes / (out["total_us"] * 1e-6) / 1e9
     out.update({"rows": N, "R": R, "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
                 "frac": round(gbs / HBM_PEAK_GBS, 4)})
+    return out
+
+
+def policy_train_vocab_legs(dev, mb, R, reps=10):
+    """The fused training pass (skyrl_policy_train_fwd) at every BASELINE.json vocabulary, one
+    micro-batch of mb x R tokens each: GPT-2 (50,257: odd V, so the rows of a [n, S, V] model
+    output are not 16-B aligned; timed on the model-wrapper slice [:, -R-1:-1] of such a
+    tensor), Llama-3 (128,256), Qwen2.5-1.5B (151,936), Qwen2.5-7B (152,064). Algorithmic bytes
+    per token: V*2 read + V*2 written + 36 (label, old, adv, mask, ref, logp, entropy, record)."""
+    from skyrl_amd import ops, ppo_utils
+    from skyrl_amd.config import AlgorithmConfig
+
+    params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=True)
+    out = {}
+    for name, V in (("gpt2", 50257), ("llama3_8b", 128256), ("qwen2.5_1.5b", 151936), ("qwen2.5_7b", 152064)):
+        S = R + 2 if V % 8 else R
+        full = torch.empty((mb, S, V), dtype=torch.bfloat16, device=dev).normal_(0.0, 3.0)
+        x = full[:, S - R - 1:S - 1] if V % 8 else full
+        g = torch.Generator(device=dev).manual_seed(3)
+        labels = torch.randint(0, V, (mb, R), device=dev, generator=g)
+        old = -12 + torch.randn(mb, R, device=dev, generator=g)
+        adv = torch.randn(mb, R, device=dev, generator=g)
+        mask = torch.ones(mb, R, device=dev)
+        ref = old + 0.01
+        torch.cuda.synchronize(dev)
+        run = lambda: ops.policy_train(x, labels, old, adv, mask, params, ref_log_probs=ref)  # noqa: E731
+        run()
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            run()
+        b.record()
+        b.synchronize()
+        ms = a.elapsed_time(b) / reps
+        nbytes = mb * R * (4 * V + 36)
+        out[name] = {"V": V, "rows_16B_aligned": V % 8 == 0, "ms_per_microbatch": round(ms, 4),
+                     "bytes": nbytes, "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                     "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        del full, x
+        torch.cuda.empty_cache()
     return out
 
 
@@ -619,6 +662,7 @@ def main():
     ap.add_argument("--no-adv-loss-leg", action="store_true", help="skip the graph-replayed advantage+loss leg")
     ap.add_argument("--adv-loss-variants", action="store_true", help="also time the A/B variants of that leg")
     ap.add_argument("--no-attention-leg", action="store_true", help="skip the rollout paged-attention leg")
+    ap.add_argument("--no-vocab-legs", action="store_true", help="skip the per-vocabulary fused training pass legs")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--params", type=int, default=QWEN_1_5B_PARAMS, help="policy parameter count (0: no optimizer leg)")

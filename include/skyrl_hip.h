@@ -41,14 +41,16 @@ extern "C" {
 const char* skyrl_last_error(void);
 /* ABI version; bumped on any signature change (2: skyrl_sample takes top_p; 3: one-launch
  * skyrl_ppo_loss_fwd writing final gradients, in-place skyrl_ppo_loss_bwd, pack emits
- * loss-mask row sums). */
+ * loss-mask row sums; 4: skyrl_policy_train_fwd takes grad_logits strides). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
  * {0, 1} (non-temporal streaming loads of the logits), "train_resident" {0, 1} (fused
  * training pass keeps the vocab row in registers vs re-reading it), "train_ntstore"
  * {0, 1} (non-temporal dlogits stores), "train_resident_nt" {768, 1024} (threads per
- * register-resident row). Not thread-safe.                                             */
+ * register-resident row at Qwen2.5's vocabulary), "grpo_slices" {1, 2, 4} (column slices
+ * per group of the contiguous-group GRPO kernel), "loss_units" {0 auto, 1, 2, 4} (row chunks
+ * per block of the fused PPO loss). Not thread-safe.                                    */
 int skyrl_tune(const char* key, int value);
 
 /* ---- a4: GRPO outcome advantage ----------------------------------------
@@ -223,8 +225,12 @@ int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int32_t vc, in
  * logprob bwd (same values and gradients as those four, see policy_train.hip):
  * logits bf16 [n,R,V] (row (b,t) at logits + b*stride_b + t*stride_t) -> loss_out[1],
  * metrics_out[SKYRL_M_COUNT], logp_out/entropy_out f32 [n,R], and grad_logits bf16
- * dense [n,R,V] = dL/dlogits for a unit upstream gradient (rescale with
- * skyrl_scale_bf16_by_device_scalar when the upstream gradient is not 1).
+ * [n,R,V] (row (b,t) at grad_logits + b*gstride_b + t*gstride_t) = dL/dlogits for a unit
+ * upstream gradient (rescale with skyrl_scale_bf16_by_device_scalar when the upstream
+ * gradient is not 1). Any V and row alignment (GPT-2's odd 50,257 included); the
+ * register-resident kernel (V <= 155,648) needs every grad_logits row to sit at the same
+ * position within 16 B as its logits row (equal strides mod 8 elements and 16-B-congruent
+ * bases), which the dense [n,R,V] layout gives whenever V % 8 == 0.
  * old/adv/mask/ref: f32 [n,R] contiguous. workspace: skyrl_policy_train_workspace_bytes. */
 size_t skyrl_policy_train_workspace_bytes(int32_t n, int32_t R);
 int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t n,
@@ -232,7 +238,8 @@ int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int6
                            int64_t lstride_t, float temperature, const float* old_log_probs,
                            const float* advantages, const float* loss_mask, const float* ref_log_probs,
                            const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
-                           float* logp_out, float* entropy_out, void* grad_logits, void* workspace,
+                           float* logp_out, float* entropy_out, void* grad_logits, int64_t gstride_b,
+                           int64_t gstride_t, void* workspace,
                            void* stream);
 /* x[i] *= g[0] over a bf16 buffer; a no-op kernel when g[0] == 1. */
 int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream);

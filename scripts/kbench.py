@@ -109,7 +109,7 @@ def main():
             _ffi.call("skyrl_policy_train_fwd", ops._ptr(x), _ffi.BF16, x.stride(0), x.stride(1), mb, R, V,
                       ops._ptr(labels), labels.stride(0), labels.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
                       ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met), ops._ptr(lp),
-                      ops._ptr(ent), ops._ptr(dlog), ops._ptr(ws), st)
+                      ops._ptr(ent), ops._ptr(dlog), R * V, V, ops._ptr(ws), st)
         for resident, nts, nt in ((1, 1, 768), (1, 1, 1024), (1, 0, 1024), (0, 1, 1024)):
             _ffi.call("skyrl_tune", b"train_resident", resident)
             _ffi.call("skyrl_tune", b"train_ntstore", nts)

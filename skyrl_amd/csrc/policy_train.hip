@@ -168,14 +168,14 @@ __global__ __launch_bounds__(kThreads) void policy_train_kernel(
     const float* __restrict__ old, const float* __restrict__ adv, const float* __restrict__ mask,
     const float* __restrict__ ref, const float* __restrict__ row_scale, const float* __restrict__ scal,
     skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out, float* __restrict__ tok,
-    uint16_t* __restrict__ dx, bool nts) {
+    uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts) {
     __shared__ St s_st[kWaves];
     __shared__ float s_g[3];  // lse, g_lp, g_ent*... (see below)
     __shared__ float s_h;
     const int64_t r = blockIdx.x;
     const int64_t b = r / R, t = r % R;
     const uint16_t* row = logits + b * sb + t * st_;
-    uint16_t* out = dx + r * (int64_t)V;
+    uint16_t* out = dx + b * gsb + t * gst;
     const int lane = threadIdx.x & 63;
     const int nvec = V / 8;
     const bool vec_ok = (reinterpret_cast<uintptr_t>(row) % 16) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0;
@@ -295,26 +295,35 @@ __global__ __launch_bounds__(kThreads) void policy_train_kernel(
 }
 
 // ---- 2b. register-resident variant: the row is loaded ONCE into registers (NV 16-B
-// vectors per thread, 1024 threads: NV = 19 covers V <= 155,648, Qwen2.5's 151,936), so
-// sweep 2 needs no memory reads at all: HBM traffic per token is exactly V*2 read +
-// V*2 written. One block per CU; the per-token scalars (old/adv/mask/ref, row scale, label)
-// are scalar loads issued up front, the label logit one broadcast load by thread 0.
-template <int NT, int NV, bool HAS_T>
+// vectors per thread, NT threads: 1024 x 19 covers V <= 155,648, Qwen2.5's 151,936 and
+// 152,064; 1024 x 16 Llama-3's 128,256; 1024 x 7 GPT-2's 50,257), so sweep 2 needs no
+// memory reads at all: HBM traffic per token is exactly V*2 read + V*2 written. One block
+// per CU; the per-token scalars (old/adv/mask/ref, row scale, label) are scalar loads issued
+// up front, the label logit one broadcast load by thread 0.
+// Any row alignment: the row is read as the 16-B vectors of its aligned-down span (h = the
+// row start's element offset within 16 B, 0 for Qwen/Llama rows; GPT-2's odd V makes it vary
+// per row), slots outside [0, V) read as bf16 -inf (e = 0 in the softmax). dlogits rows share
+// the logits rows' alignment (host check), so full vectors are stored whole and only a row's
+// first and last vectors go element by element.
+template <int NT, int NV, bool HAS_T, bool EDGE>
 __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int V, const int64_t* __restrict__ labels,
     int64_t lsb, int64_t lst, float temp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
     const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
-    float* __restrict__ tok, uint16_t* __restrict__ dx, bool nts) {
+    float* __restrict__ tok, uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts) {
     __shared__ St s_st[NT / 64];
     __shared__ float s_g[4];
     const int64_t r = blockIdx.x;
     const int64_t b = r / R, t = r % R;
     const uint16_t* row = logits + b * sb + t * st_;
-    uint16_t* out = dx + r * (int64_t)V;
+    uint16_t* out = dx + b * gsb + t * gst;
     const int lane = threadIdx.x & 63;
-    const int nvec = V / 8;
-    const uint4* rv = reinterpret_cast<const uint4*>(row);
+    // EDGE = false: 16-B-aligned rows and V % 8 == 0 (Qwen, Llama): no partial vectors, and the
+    // edge logic below compiles away (it costs ~20 VGPRs and spills at NV >= 16)
+    const int h = EDGE ? (int)((reinterpret_cast<uintptr_t>(row) >> 1) & 7) : 0;  // uniform per block
+    const int nvec = EDGE ? (h + V + 7) >> 3 : V >> 3;                           // vectors of the span
+    const uint4* rv = reinterpret_cast<const uint4*>(row - h);
     auto tval = [&](float x) { return HAS_T ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
 
     // The token's scalars sit at block-uniform addresses: every thread loads them, so they
@@ -329,22 +338,50 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     const float o_ge = scal[1];
     float xl = 0.f;
     if (threadIdx.x == 0) xl = (lab >= 0 && lab < V) ? bf16_to_f32(row[lab]) : __builtin_nanf("");
-    // Host guarantees (NV-1)*NT < nvec <= NV*NT: only the last vector can be out of range.
+    constexpr uint32_t kNinf2 = 0xff80ff80u;  // two bf16 -inf: contribute e = 0
     uint4 v[NV];
+    // !EDGE: the host guarantees (NV-1)*NT < nvec <= NV*NT, so only the last vector can be out of
+    // range and the others load unconditionally (one address live at a time, as few VGPRs as the
+    // row itself needs)
+    if constexpr (!EDGE) {
 #pragma unroll
-    for (int k = 0; k < NV - 1; ++k) v[k] = ld_nt(rv + threadIdx.x + k * NT);
-    {
+        for (int k = 0; k < NV - 1; ++k) v[k] = ld_nt(rv + threadIdx.x + k * NT);
         const int idx = threadIdx.x + (NV - 1) * NT;
         const bool ok = idx < nvec;
         const uint4 t4 = ld_nt(rv + (ok ? idx : nvec - 1));
-        const uint32_t ninf = 0xff80ff80u;  // bf16 -inf pair: contributes e = 0
-        v[NV - 1] = make_uint4(ok ? t4.x : ninf, ok ? t4.y : ninf, ok ? t4.z : ninf, ok ? t4.w : ninf);
+        v[NV - 1] = make_uint4(ok ? t4.x : kNinf2, ok ? t4.y : kNinf2, ok ? t4.z : kNinf2, ok ? t4.w : kNinf2);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int idx = threadIdx.x + k * NT;
+            const bool ok = idx < nvec;
+            const uint4 t4 = ld_nt(rv + (ok ? idx : 0));
+            v[k] = make_uint4(ok ? t4.x : kNinf2, ok ? t4.y : kNinf2, ok ? t4.z : kNinf2, ok ? t4.w : kNinf2);
+        }
+    }
+    // the span's first and last vectors may hold slots outside the row: -inf them (only the
+    // lanes holding those two vectors take the branch)
+#pragma unroll
+    for (int k = 0; k < (EDGE ? NV : 0); ++k) {
+        const int idx = threadIdx.x + k * NT;
+        const int lo = h - 8 * idx, hi = V + h - 8 * idx;  // valid slots: lo <= j < hi
+        if (idx < nvec && (lo > 0 || hi < 8)) {
+            uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < lo || j >= hi) {
+                    const uint32_t keep = (j & 1) ? 0x0000ffffu : 0xffff0000u;
+                    w[j >> 1] = (w[j >> 1] & keep) | (kNinf2 & ~keep);
+                }
+            }
+            v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
     }
     St st{-3.402823466e38f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         float x[8];
-        unpack8(v[k], x);  // padding vectors are bf16 -inf: contribute e = 0
+        unpack8(v[k], x);  // padding slots are bf16 -inf: contribute e = 0
         if constexpr (HAS_T) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = tval(x[j]);
@@ -389,17 +426,17 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     }
     __syncthreads();
     const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
-    const int lab32 = (lab >= 0 && lab < V) ? (int)lab : -1;
+    const int lab_s = (lab >= 0 && lab < V) ? (int)lab + h : -1;  // label's slot in the aligned-down span
 #pragma unroll
     for (int k = 0; k < NV; ++k)  // new values: no reuse of sweep-1 unpacks across the barrier
         asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
     const float inv_t = HAS_T ? 1.f / temp : 1.f;
-    uint4* ov = reinterpret_cast<uint4*>(out);
+    uint4* ov = reinterpret_cast<uint4*>(out - h);
 
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int idx = threadIdx.x + k * NT;
-        if (k < NV - 1 || idx < nvec) {
+        if ((!EDGE && k < NV - 1) || idx < nvec) {
             float x[8];
             unpack8(v[k], x);
             const int v0 = idx * 8;
@@ -408,11 +445,19 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
                 const float lpv = tval(x[j]) - L;
                 const float pv = fast_exp2(lpv * kLog2e);
                 float g = -glp * pv - gent * pv * (lpv + H);
-                if (v0 + j == lab32) g += glp;
+                if (v0 + j == lab_s) g += glp;
                 x[j] = HAS_T ? g * inv_t : g;
             }
-            st_out(ov + idx, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
-                                        pack_bf16x2(x[6], x[7])), nts);
+            const int lo = h - v0, hi = V + h - v0;
+            if (!EDGE || (lo <= 0 && hi >= 8)) {
+                st_out(ov + idx, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
+                                            pack_bf16x2(x[4], x[5]), pack_bf16x2(x[6], x[7])), nts);
+            } else {  // the row's first / last vector: only its own slots
+                uint16_t* o16 = reinterpret_cast<uint16_t*>(ov + idx);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j >= lo && j < hi) o16[j] = f32_to_bf16(x[j]);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -512,18 +557,71 @@ extern "C" size_t skyrl_policy_train_workspace_bytes(int32_t n, int32_t R) {
     return 256 + (size_t)n * 4 + 256 + (size_t)n * R * 16 + 256;
 }
 
+namespace {
+// Register-resident instantiations (1024 threads): NV vectors per thread cover spans up to
+// NV * 8192 elements. The host takes the smallest NV that covers the row's aligned-down span.
+using TrainKernel = void (*)(const uint16_t*, int64_t, int64_t, int, int, const int64_t*, int64_t, int64_t, float,
+                             const float*, const float*, const float*, const float*, const float*, const float*,
+                             skyrl_ppo_params, float*, float*, float*, uint16_t*, int64_t, int64_t, bool);
+template <int NV, bool EDGE>
+TrainKernel pick_resident(bool has_t) {
+    return has_t ? policy_train_resident_kernel<1024, NV, true, EDGE> : policy_train_resident_kernel<1024, NV, false, EDGE>;
+}
+// rows with partial vectors (EDGE): the smallest listed NV covering the span; NV <= 14 fits
+// the edge logic without spills
+constexpr int kEdgeNV[] = {2, 4, 6, 7, 8, 10, 12, 14};
+TrainKernel resident_edge_for(int nv, bool has_t) {
+    switch (nv) {
+        case 2: return pick_resident<2, true>(has_t);
+        case 4: return pick_resident<4, true>(has_t);
+        case 6: return pick_resident<6, true>(has_t);
+        case 7: return pick_resident<7, true>(has_t);
+        case 8: return pick_resident<8, true>(has_t);
+        case 10: return pick_resident<10, true>(has_t);
+        case 12: return pick_resident<12, true>(has_t);
+        default: return pick_resident<14, true>(has_t);
+    }
+}
+// aligned rows: NV = ceil(nvec / 1024) exactly, 1..19 (V <= 155,648)
+TrainKernel resident_aligned_for(int nv, bool has_t) {
+    switch (nv) {
+        case 1: return pick_resident<1, false>(has_t);
+        case 2: return pick_resident<2, false>(has_t);
+        case 3: return pick_resident<3, false>(has_t);
+        case 4: return pick_resident<4, false>(has_t);
+        case 5: return pick_resident<5, false>(has_t);
+        case 6: return pick_resident<6, false>(has_t);
+        case 7: return pick_resident<7, false>(has_t);
+        case 8: return pick_resident<8, false>(has_t);
+        case 9: return pick_resident<9, false>(has_t);
+        case 10: return pick_resident<10, false>(has_t);
+        case 11: return pick_resident<11, false>(has_t);
+        case 12: return pick_resident<12, false>(has_t);
+        case 13: return pick_resident<13, false>(has_t);
+        case 14: return pick_resident<14, false>(has_t);
+        case 15: return pick_resident<15, false>(has_t);
+        case 16: return pick_resident<16, false>(has_t);
+        case 17: return pick_resident<17, false>(has_t);
+        case 18: return pick_resident<18, false>(has_t);
+        default: return pick_resident<19, false>(has_t);
+    }
+}
+}  // namespace
+
 extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t n,
                                       int32_t R, int32_t V, const int64_t* labels, int64_t lstride_b,
                                       int64_t lstride_t, float temperature, const float* old_log_probs,
                                       const float* advantages, const float* loss_mask, const float* ref_log_probs,
                                       const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
-                                      float* logp_out, float* entropy_out, void* grad_logits, void* workspace,
-                                      void* stream) {
+                                      float* logp_out, float* entropy_out, void* grad_logits, int64_t gstride_b,
+                                      int64_t gstride_t, void* workspace, void* stream) {
     SKYRL_REQUIRE(params && logits && labels && old_log_probs && advantages && loss_out && metrics_out && logp_out &&
                       grad_logits && workspace,
                   "policy_train_fwd: null pointer");
     SKYRL_REQUIRE(dtype == SKYRL_BF16, "policy_train_fwd: logits must be bf16");
     SKYRL_REQUIRE(n > 0 && R > 0 && V > 0, "policy_train_fwd: bad sizes");
+    SKYRL_REQUIRE(gstride_t >= V && (n == 1 || gstride_b >= (int64_t)(R - 1) * gstride_t + V),
+                  "policy_train_fwd: grad_logits rows overlap");
     SKYRL_REQUIRE(temperature > 0.f, "policy_train_fwd: temperature must be > 0");
     SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "policy_train_fwd: use_kl_loss needs ref_log_probs");
     SKYRL_REQUIRE(params->loss_reduction >= 0 && params->loss_reduction <= 2, "policy_train_fwd: bad loss_reduction");
@@ -539,29 +637,47 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
     if (rc) return rc;
     const bool has_t = temperature != 1.0f;
     const int nvec = V / 8;
-    // Register-resident shapes for Qwen2.5's V = 151,936 (147,456 < V <= 153,600 / 155,648):
-    // 768 threads x 25 vectors (3 waves/SIMD, <= 168 VGPRs) or 1024 x 19 (4 waves/SIMD, <= 128).
-    const bool use1024 = g_train_resident_nt == 1024;
-    const int kRT = use1024 ? 1024 : 768, kRV = use1024 ? 19 : 25;
-    const bool resident_ok = g_train_resident && (V % 8) == 0 && nvec <= kRV * kRT && nvec > (kRV - 1) * kRT &&
-                             (reinterpret_cast<uintptr_t>(logits) % 16) == 0 && (stride_b % 8) == 0 &&
-                             (stride_t % 8) == 0 && (reinterpret_cast<uintptr_t>(grad_logits) % 16) == 0;
-    if (resident_ok) {
-        auto kern = use1024 ? (has_t ? policy_train_resident_kernel<1024, 19, true>
-                                     : policy_train_resident_kernel<1024, 19, false>)
-                            : (has_t ? policy_train_resident_kernel<768, 25, true>
-                                     : policy_train_resident_kernel<768, 25, false>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(kRT), 0, s,
-                           reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, V, labels, lstride_b,
-                           lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs, row_scale,
-                           scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
+    auto* out = reinterpret_cast<uint16_t*>(grad_logits);
+    const auto* in = reinterpret_cast<const uint16_t*>(logits);
+    // dlogits rows must share the logits rows' position within 16 B (then every row's
+    // aligned-down span maps slot for slot); both 2-byte aligned.
+    const bool same_align = ((reinterpret_cast<uintptr_t>(out) - reinterpret_cast<uintptr_t>(in)) % 16) == 0 &&
+                            ((gstride_b - stride_b) % 8) == 0 && ((gstride_t - stride_t) % 8) == 0 &&
+                            (reinterpret_cast<uintptr_t>(in) % 2) == 0;
+    // Qwen2.5's V = 151,936 at 768 threads x 25 vectors (skyrl_tune("train_resident_nt", 768))
+    const bool use768 = g_train_resident_nt == 768 && nvec <= 25 * 768 && nvec > 24 * 768;
+    // rows without partial vectors: 16-B-aligned logits and dlogits rows, V % 8 == 0
+    const bool aligned = (V % 8) == 0 && (reinterpret_cast<uintptr_t>(in) % 16) == 0 && (stride_b % 8) == 0 &&
+                         (stride_t % 8) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0 &&
+                         (gstride_b % 8) == 0 && (gstride_t % 8) == 0;
+    int nv = 0;
+    if (aligned) {
+        nv = (nvec + 1023) / 1024;
+        if (nv > 19) nv = 0;
+    } else {
+        const int span = (V + 7 + 7) / 8;  // aligned-down span in vectors, worst-case row offset
+        for (int cand : kEdgeNV)
+            if (span <= cand * 1024) { nv = cand; break; }
+    }
+    const bool resident_ok = g_train_resident && same_align && nv > 0;
+    if (g_train_resident && use768 && aligned) {
+        auto kern = has_t ? policy_train_resident_kernel<768, 25, true, false>
+                          : policy_train_resident_kernel<768, 25, false, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(768), 0, s, in, stride_b, stride_t, R, V, labels,
+                           lstride_b, lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
+                           row_scale, scal, *params, logp_out, entropy_out, tok, out, gstride_b, gstride_t,
+                           g_train_ntstore != 0);
+    } else if (resident_ok) {
+        hipLaunchKernelGGL(aligned ? resident_aligned_for(nv, has_t) : resident_edge_for(nv, has_t),
+                           dim3((unsigned)((int64_t)n * R)), dim3(1024), 0, s, in, stride_b, stride_t, R, V, labels,
+                           lstride_b, lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
+                           row_scale, scal, *params, logp_out, entropy_out, tok, out, gstride_b, gstride_t,
                            g_train_ntstore != 0);
     } else
-    hipLaunchKernelGGL(policy_train_kernel, dim3((unsigned)((int64_t)n * R)), dim3(kThreads), 0, s,
-                       reinterpret_cast<const uint16_t*>(logits), stride_b, stride_t, R, (int64_t)n * R, V, labels,
-                       lstride_b, lstride_t, temperature, has_t, old_log_probs, advantages, loss_mask, ref_log_probs,
-                       row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
-                       g_train_ntstore != 0);
+    hipLaunchKernelGGL(policy_train_kernel, dim3((unsigned)((int64_t)n * R)), dim3(kThreads), 0, s, in, stride_b,
+                       stride_t, R, (int64_t)n * R, V, labels, lstride_b, lstride_t, temperature, has_t, old_log_probs,
+                       advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok, out,
+                       gstride_b, gstride_t, g_train_ntstore != 0);
     rc = check_launch("policy_train_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,

@@ -475,23 +475,31 @@ class PolicyTrainFunction(torch.autograd.Function):
         metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
         logp = torch.empty((nb, nt), dtype=torch.float32, device=dev)
         ent = torch.empty((nb, nt), dtype=torch.float32, device=dev)
-        dx = torch.empty((nb, nt, V), dtype=torch.bfloat16, device=dev)
+        if V % 8 == 0 and lg.data_ptr() % 16 == 0 and sb % 8 == 0 and st % 8 == 0:
+            flat = torch.empty(nb * nt * V, dtype=torch.bfloat16, device=dev)
+            dx = flat.view(nb, nt, V)
+        else:
+            # rows not 16-B aligned (GPT-2's odd V): dlogits rows mirror the logits rows' strides
+            # and position within 16 B, which the register-resident kernel needs
+            off = (lg.data_ptr() // 2) % 8
+            flat = torch.empty(off + (nb - 1) * sb + (nt - 1) * st + V, dtype=torch.bfloat16, device=dev)
+            dx = flat.as_strided((nb, nt, V), (sb, st, 1), storage_offset=off)
         ws = WORKSPACES.get(dev, "policy_train", _ffi.query("skyrl_policy_train_workspace_bytes", nb, nt))
         _ffi.call(
             "skyrl_policy_train_fwd", _ptr(lg), dt, sb, st, nb, nt, V, _ptr(lab), lsb, lst, float(temperature),
             _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), ctypes.byref(params), _ptr(loss), _ptr(metrics),
-            _ptr(logp), _ptr(ent), _ptr(dx), _ptr(ws), _stream(dev),
+            _ptr(logp), _ptr(ent), _ptr(dx), dx.stride(0), dx.stride(1), _ptr(ws), _stream(dev),
         )
         ctx.in_shape = logits.shape
-        ctx.save_for_backward(dx)
+        ctx.save_for_backward(dx, flat)
         ctx.mark_non_differentiable(metrics, logp, ent)
         return loss, metrics, logp, ent
 
     @staticmethod
     def backward(ctx, g_loss, g_metrics, g_logp, g_ent):
-        (dx,) = ctx.saved_tensors
+        dx, flat = ctx.saved_tensors
         g = g_loss.detach().to(torch.float32).reshape(1).contiguous()
-        _ffi.call("skyrl_scale_bf16_by_device_scalar", _ptr(g), _ptr(dx), dx.numel(), _stream(dx.device))
+        _ffi.call("skyrl_scale_bf16_by_device_scalar", _ptr(g), _ptr(flat), flat.numel(), _stream(dx.device))
         return dx.reshape(ctx.in_shape), None, None, None, None, None, None, None
 
 
