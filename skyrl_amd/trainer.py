@@ -147,12 +147,13 @@ class GRPOTrainer:
         """action log-probs (and entropy) of the last R positions: HFModelWrapper.forward
         (model_wrapper.py:261-375) with the lm_head-fused HIP logprob/entropy."""
         with torch.autocast("cuda", dtype=torch.bfloat16), torch.set_grad_enabled(grad):
+            base = model.base_model  # model.model (Qwen2/Llama), model.transformer (GPT-2)
             if self.cfg.use_sample_packing:
-                h = packed_hidden_states(model.model, seq, att, R).to(torch.bfloat16)
+                h = packed_hidden_states(base, seq, att, R).to(torch.bfloat16)
             else:
-                hidden = model.model(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
+                hidden = base(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
                 h = hidden[:, -R - 1:-1].to(torch.bfloat16)
-            w = model.lm_head.weight.to(torch.bfloat16)
+            w = model.get_output_embeddings().weight.to(torch.bfloat16)
             labels = seq[:, -R:]
             live = att[:, -R:].bool()  # positions whose label is a real response token
             if bool(live.all()):
@@ -168,6 +169,7 @@ class GRPOTrainer:
 
     @torch.no_grad()
     def _fwd_logprobs(self, model, data) -> torch.Tensor:
+        model.eval()  # forward passes run without dropout (worker.py:982); training in train mode (:750)
         seq, att = data["sequences"], data["attention_mask"]
         R = data["response_mask"].shape[1]
         mb = self.cfg.micro_forward_batch_size_per_gpu
@@ -180,6 +182,7 @@ class GRPOTrainer:
 
     @torch.no_grad()
     def _fwd_values(self, data) -> torch.Tensor:
+        self.critic.eval()  # worker.py:1172-1179
         seq, att = data["sequences"], data["attention_mask"]
         R = data["response_mask"].shape[1]
         mb = self.cfg.micro_forward_batch_size_per_gpu
@@ -252,6 +255,7 @@ class GRPOTrainer:
     def _train_critic(self, data) -> Dict[str, float]:
         """CriticWorkerBase._forward_backward_micro (worker.py:1062-1114) + optim_step: HIP clipped
         value loss against the GAE returns, loss / n_micro, clip, AdamW."""
+        self.critic.train()  # worker.py:1074
         cfg = self.cfg
         n = len(data["sequences"])
         mini = cfg.policy_mini_batch_size * cfg.n_samples_per_prompt
@@ -288,6 +292,7 @@ class GRPOTrainer:
     def _train_policy(self, data) -> Dict[str, float]:
         """_execute_training_step: mini-batches of policy_mini_batch_size prompts (no shuffle,
         trainer.py:1067-1081), micro-batches inside, loss scaled by 1/n_micro, grad clip, AdamW."""
+        self.policy.train()  # worker.py:750
         cfg = self.cfg
         n = len(data["sequences"])
         mini = cfg.policy_mini_batch_size * cfg.n_samples_per_prompt
