@@ -24,6 +24,22 @@
 // HBM traffic per token: V*2 (read) + V*2 (write) vs V*2 + V*2 + V*2 unfused.
 #include "arrive.h"
 
+// Phase timestamps for scripts/probe/train_phase_probe (compiled only there, never in the product).
+#ifdef SKYRL_TRAIN_PHASE_PROBE
+__device__ uint64_t g_tphase[16384 * 8];
+#define TPHASE(k)                                                                                       \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 16384) {                                                   \
+            g_tphase[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                          \
+            if ((k) == 0) g_tphase[blockIdx.x * 8 + 7] = (uint64_t)__smid();                            \
+        }                                                                                               \
+    } while (0)
+#else
+#define TPHASE(k) \
+    do {          \
+    } while (0)
+#endif
+
 namespace skyrl {
 namespace {
 
@@ -314,6 +330,7 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     float* __restrict__ tok, uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts) {
     __shared__ St s_st[NT / 64];
     __shared__ float s_g[4];
+    TPHASE(0);
     const int64_t r = blockIdx.x;
     const int64_t b = r / R, t = r % R;
     const uint16_t* row = logits + b * sb + t * st_;
@@ -394,8 +411,10 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
         St o{__shfl_xor(st.m, off, kWave), __shfl_xor(st.s, off, kWave), __shfl_xor(st.w, off, kWave)};
         st_merge(st, o);
     }
+    TPHASE(1);
     if (lane == 0) s_st[threadIdx.x / kWave] = st;
     __syncthreads();
+    TPHASE(2);
     // wave 0 merges the NT/64 wave states as a shuffle tree (a serial lane-0 fold of 12 states
     // sat on every row's critical path), then lane 0 evaluates the token's loss terms
     static_assert(NT / 64 <= 16, "wave-state tree covers 16 waves");
@@ -425,6 +444,7 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
         }
     }
     __syncthreads();
+    TPHASE(3);
     const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
     const int lab_s = (lab >= 0 && lab < V) ? (int)lab + h : -1;  // label's slot in the aligned-down span
 #pragma unroll
@@ -461,6 +481,7 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+    TPHASE(4);
 }
 
 // ---- 3. loss scalar + metrics ---------------------------------------------------------

@@ -115,3 +115,4 @@ def test_policy_train_per_vocab(dev, V, temp):
     close(ent, entc, atol=1e-4)
     close(m[4], mc["clip_ratio"], atol=1e-6)
     close(grad[:, -R - 1:-1], xs.grad / temp, atol=2e-6, rtol=1e-2)  # d(x/T)/dx = 1/T; dlogits in bf16
+
