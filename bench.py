@@ -164,7 +164,11 @@ def run(args):
         return logits[blk * mb * R:(blk + 1) * mb * R].view(mb, R, V)[: nseq] if not full else \
             logits[seq0 * R:(seq0 + nseq) * R].view(nseq, R, V)
 
-    labels = torch.randint(0, V, (N, R), device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+    # the rollout's sampled tokens / logprobs ([R, N] per decode step) become the ragged response
+    # CSR that pack consumes: token j of sequence n was sampled at decode step j - roff[n]
+    roff = data["roff"]
+    tok_n = torch.repeat_interleave(torch.arange(N, device=dev), data["rlens"])
+    tok_t = torch.arange(int(roff[-1]), device=dev) - roff[:-1][tok_n]
     seq_ids = torch.arange(N, device=dev, dtype=torch.int64) + rank * N
     from skyrl_amd.config import SamplingParams
     from skyrl_amd.sampler import TokenSampler
@@ -202,16 +206,20 @@ def run(args):
         if opt is not None:  # in-flight weight sync: the previous step's all-gather overlapped the rollout
             opt.wait_weights()
         # ---- pack ragged rollout output into the padded training tensors
+        rtok = sampler.tokens[tok_t, tok_n]
+        rlp_sampled = sampler.logprobs[tok_t, tok_n]
         seqs, att, rmask, rew, lmask, rlp = ops.pack_experience(
-            data["ptok"], data["poff"], data["rtok"], data["roff"], data["rew"], data["roff"], data["lmask"],
-            data["roff"], data["rlp"], data["roff"], N=N, P=P_MAX, R=R, pad=0, pad_token_id=0)
-        # ---- ref + old policy logprobs over all response positions (no grad)
+            data["ptok"], data["poff"], rtok, roff, data["rew"], roff, data["lmask"],
+            roff, rlp_sampled, roff, N=N, P=P_MAX, R=R, pad=0, pad_token_id=0)
+        labels = seqs[:, P_MAX:]  # the sampled response tokens (int64 view, row stride P+R)
+        # ---- ref + old policy logprobs over all response positions (no grad). The old policy is the
+        #      rollout policy (on-policy, one mini-batch per step: ratio 1 as in the reference); the ref
+        #      policy's logits stand in as another sequence block's, so KL-to-ref is nonzero
         ref_lp = torch.empty((N, R), dtype=torch.float32, device=dev)
         old_lp = torch.empty((N, R), dtype=torch.float32, device=dev)
         for s in range(0, N, mb):
-            x = lg_rows(s, mb)
             lab = labels[s:s + mb]
-            for out in (ref_lp, old_lp):
+            for out, x in ((ref_lp, lg_rows((s + mb) % N, mb)), (old_lp, lg_rows(s, mb))):
                 fwd_timer.wrap(lambda: ops._ffi.call(
                     "skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V, ops._ptr(lab),
                     lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None, ops._stream(dev)))

@@ -220,6 +220,28 @@ int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int32_t vc, in
                            const float* grad_logp, const float* grad_entropy, void* dz, int64_t lddz,
                            void* stream);
 
+/* ---- §8(f)1 decode side: lm_head GEMM with the sampler in its epilogue ----------------
+ * Replaces the rollout step's logits = lm_head(hidden) + sampler sequence (vLLM
+ * LogitsProcessor + Sampler behind vllm_engine.py:139-149,196-218; params
+ * inference_engines/utils.py:15-42) with one MFMA GEMM whose epilogue runs skyrl_sample's
+ * decision on the bf16 logits tile in LDS, so [M,V] logits never reach HBM.
+ * hidden bf16 [M,K] (row stride ld_hidden), weight bf16 [V,K] (HF lm_head.weight, row stride
+ * ld_weight); K % 64 == 0, strides multiples of 8 elements, operands 16-B aligned.
+ *   skyrl_lmhead_gemm    out bf16 [M,N] (row stride ld_out) = hidden @ weight^T (fp32 accumulate,
+ *                        round to bf16): the plain GEMM of the same kernel.
+ *   skyrl_lmhead_sample  tokens_out int32 [M], logp_out f32 [M] (may be NULL) exactly as
+ *                        skyrl_sample(logits = skyrl_lmhead_gemm(...), temperature, top_k=-1,
+ *                        top_p=1, min_p=0, seed, seq_ids, step) decides them (tokens bit-exact;
+ *                        logp = log_softmax(raw logits)[token]). No top_k/top_p/min_p here:
+ *                        callers with filters use the unfused pair. Workspace:
+ *                        skyrl_lmhead_sample_workspace_bytes(M, V), 16-B aligned.            */
+int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
+                      int32_t N, int32_t K, void* out, int64_t ld_out, void* stream);
+size_t skyrl_lmhead_sample_workspace_bytes(int32_t M, int32_t V);
+int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
+                        int32_t V, int32_t K, float temperature, uint64_t seed, const int64_t* seq_ids, int64_t step,
+                        int32_t* tokens_out, float* logp_out, void* workspace, void* stream);
+
 /* ---- a2+a3+a6+a7 fused: the policy training pass ------------------------------
  * One call per micro-batch replaces logprob fwd + fused loss fwd + loss bwd +
  * logprob bwd (same values and gradients as those four, see policy_train.hip):

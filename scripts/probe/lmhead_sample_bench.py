@@ -1,0 +1,74 @@
+"""Decode-step lm_head + sampler (§8(f)1 decode side) at the config-2 shape (H=1536, V=151,936):
+
+  unfused : torch F.linear (hipBLASLt) -> bf16 logits [M,V] -> skyrl_sample
+  gemm    : skyrl_lmhead_gemm alone (the fused kernel's GEMM with a bf16 store epilogue)
+  linear  : torch F.linear alone
+  fused   : skyrl_lmhead_sample (sampler in the GEMM epilogue + one merge launch)
+
+One JSON line per (M, T). Random operands (bf16 GEMMs clock lower on random data than on zeros).
+"""
+
+import argparse
+import json
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, ".")
+from skyrl_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, nargs="+", default=[512, 256, 64, 8])
+    ap.add_argument("--H", type=int, default=1536)
+    ap.add_argument("--V", type=int, default=151936)
+    ap.add_argument("--T", type=float, nargs="+", default=[1.0])
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    H, V = args.H, args.V
+    w = (torch.randn(V, H, device=dev) * (3.0 / H ** 0.5)).to(torch.bfloat16)
+    for M in args.M:
+        h = torch.randn(M, H, device=dev).to(torch.bfloat16)
+        ids = torch.arange(M, device=dev)
+        z = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
+        tok = torch.empty(M, dtype=torch.int32, device=dev)
+        lp = torch.empty(M, dtype=torch.float32, device=dev)
+        flops = 2.0 * M * H * V
+        for T in args.T:
+            def unfused():
+                torch.matmul(h, w.T, out=z)
+                ops.sample(z, temperature=T, seed=1, seq_ids=ids, step=3, tokens_out=tok, logp_out=lp)
+
+            def fused():
+                ops.lmhead_sample(h, w, temperature=T, seed=1, seq_ids=ids, step=3, tokens_out=tok, logp_out=lp)
+
+            res = {"M": M, "H": H, "V": V, "T": T,
+                   "linear_us": timeit(lambda: torch.matmul(h, w.T, out=z), args.iters),
+                   "gemm_us": timeit(lambda: ops.lmhead_gemm(h, w, out=z), args.iters),
+                   "unfused_us": timeit(unfused, args.iters),
+                   "fused_us": timeit(fused, args.iters)}
+            res["sampler_us"] = res["unfused_us"] - res["linear_us"]
+            for k in ("linear", "gemm", "fused"):
+                res[f"{k}_TFs"] = round(flops / (res[f"{k}_us"] * 1e-6) / 1e12, 1)
+            res["fused_speedup"] = round(res["unfused_us"] / res["fused_us"], 3)
+            print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in res.items()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

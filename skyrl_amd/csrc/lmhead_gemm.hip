@@ -1,0 +1,372 @@
+// SURVEY §8(f)1, decode side: the lm_head GEMM with the sampler fused into its epilogue, so the
+// [n, V] decode logits never reach HBM.
+//
+// Reference: the rollout step's logits + sampler (vLLM's LogitsProcessor + Sampler behind
+// VLLMInferenceEngine.generate, skyrl-train/skyrl_train/inference_engines/vllm/vllm_engine.py:
+// 139-149,196-218; sampling params inference_engines/utils.py:15-42). The unfused path here is
+// a library GEMM writing bf16 logits [n, V] followed by skyrl_sample (sampler.hip), which reads
+// them back: 2 x 2 V bytes per row of HBM traffic on top of the GEMM.
+//
+// GEMM: Z = H W^T with H [M, K] (final-norm hidden states) and W [V, K] (the HF lm_head weight,
+// both K-contiguous), bf16 in, fp32 accumulate on MFMA (v_mfma_f32_16x16x32_bf16).
+//   * Tile 256 x 256 x 64 per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 outputs
+//     per wave: 8 x 4 accumulators of 16 x 16). One workgroup per CU (128 KB of LDS).
+//   * Operands stream HBM -> LDS with global_load_lds (16 B per lane, no VGPR round trip) into
+//     two 64 KB stages; tile t+1 is in flight while tile t feeds the MFMAs. One barrier per K
+//     step. LDS rows are 128 B, with the 16-B chunk index XOR-swizzled by (row >> 1) & 7 (the
+//     swizzle is applied to the per-lane global source address, the LDS image stays
+//     lane-linear) so the fragment reads (ds_read_b128, 16 rows x 4 chunks) are conflict-free.
+//   * XCD-aware order: workgroup ids are remapped (bijectively) so that each XCD walks a
+//     contiguous range of tiles with M fastest: the M tiles that share a W tile run together on
+//     one XCD and read it once from HBM into that XCD's L2.
+// Epilogue: the 256 x 256 accumulator tile is rounded to bf16 (the logits the unfused path
+// would have written) into a swizzled LDS image, then
+//   * STORE: written out as bf16 Z (the plain GEMM; also the parity handle for the fused path);
+//   * SAMPLE / GREEDY: two threads per row run the sampler's decision (noise.h: group-of-8
+//     exponential race, group bound, exact det_ln scores; greedy = first maximum) and the raw
+//     online (max, sum-exp) over the tile's 256 columns. One 20-B partial per (row, tile).
+// A one-wave-per-row merge folds a row's tile partials (argmax, lowest index on ties; LSE) into
+// the token and its logprob log_softmax(raw logits)[token]. Decisions equal skyrl_sample's /
+// oracle/sampler_ref.c's on the bf16 logits this GEMM produces (STORE), bit for bit.
+#include "noise.h"
+
+namespace skyrl {
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int kOpBytes = 256 * BK * 2;        // one operand tile [256 rows][64 k] bf16
+constexpr int kStageBytes = 2 * kOpBytes;     // H tile + W tile
+constexpr int kLdsBytes = 2 * kStageBytes;    // two stages = the [256][256] bf16 epilogue image
+constexpr float kLog2eG = 1.4426950408889634f;
+constexpr float kLn2G = 0.6931471805599453f;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2 };
+
+// byte offset of 16-B chunk c (8 bf16) of row r in the [256][256] bf16 epilogue image
+__device__ __forceinline__ int img_off(int r, int c) { return r * 512 + ((c ^ ((r & 7) << 1)) << 4); }
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
+    const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
+    int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
+    int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt) {
+    __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int mtile = wg % mt, ntile = wg / mt;
+    const int m0 = mtile * BM, n0 = ntile * BN;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = w >> 2, wn = w & 3;
+
+    // staging: waves 0-3 copy the H tile, waves 4-7 the W tile, 8 pieces of 8 rows x 128 B each
+    const int opnd = w >> 2, grp0 = (w & 3) * 8, lrow = lane >> 3, pc = lane & 7;
+    const uint16_t* gsrc[8];
+    {
+        const uint16_t* base = opnd ? W : H;
+        const int64_t ld = opnd ? ldw : ldh;
+        const int r0 = opnd ? n0 : m0, lim = (opnd ? N : M) - 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int row = (grp0 + j) * 8 + lrow;
+            const int c = pc ^ ((row >> 1) & 7);  // the logical chunk that lands in physical chunk pc
+            gsrc[j] = base + (int64_t)min(r0 + row, lim) * ld + c * 8;
+        }
+    }
+    char* const sdst = smem + opnd * kOpBytes + grp0 * 1024;
+    auto stage = [&](int buf, int k0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + k0), (lds_void*)(sdst + buf * kStageBytes + j * 1024),
+                                             16, 0, 0);
+    };
+    // fragment offsets: rows wm*128 + mb*16 + (lane & 15) of H, wn*64 + nb*16 + (lane & 15) of W;
+    // k chunk ks*4 + (lane >> 4) (16x16x32 operand map); the swizzle term is ((lane & 15) >> 1)
+    int aoff[2], boff[2];
+    {
+        const int sw = (lane & 15) >> 1;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = (ks * 4 + (lane >> 4)) ^ sw;
+            aoff[ks] = (wm * 128 + (lane & 15)) * 128 + c * 16;
+            boff[ks] = kOpBytes + (wn * 64 + (lane & 15)) * 128 + c * 16;
+        }
+    }
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nk; ++t) {
+        const char* sb = smem + (t & 1) * kStageBytes;
+        if (t + 1 < nk) stage((t + 1) & 1, (t + 1) * BK);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 b[4];
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 2048);
+#pragma unroll
+            for (int mb = 0; mb < 8; ++mb) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 2048);
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[nb], acc[mb][nb], 0, 0, 0);
+            }
+        }
+        // this wave's fragment reads are done (the next stage overwrites this buffer) and its
+        // staging of tile t+1 has landed; the barrier makes both hold for every wave
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+
+    // ---- epilogue: bf16 tile into the LDS image (C map: row (lane >> 4) * 4 + i, col lane & 15)
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = wm * 128 + mb * 16 + (lane >> 4) * 4 + i;
+                const int c = wn * 64 + nb * 16 + (lane & 15);
+                *reinterpret_cast<uint16_t*>(smem + img_off(r, c >> 3) + (c & 7) * 2) = f32_to_bf16(acc[mb][nb][i]);
+            }
+    __syncthreads();
+
+    if constexpr (EPI == EPI_STORE) {
+        const bool vec = (ldz & 7) == 0 && (reinterpret_cast<uintptr_t>(Z) & 15) == 0;
+#pragma unroll 4
+        for (int it = 0; it < 16; ++it) {
+            const int lin = it * NT + threadIdx.x;
+            const int r = lin >> 5, c = lin & 31;
+            const int grow = m0 + r, col = n0 + c * 8;
+            if (grow >= M || col >= N) continue;
+            const uint4 v = *reinterpret_cast<const uint4*>(smem + img_off(r, c));
+            uint16_t* dst = Z + (int64_t)grow * ldz + col;
+            if (vec && col + 8 <= N) {
+                *reinterpret_cast<uint4*>(dst) = v;
+            } else {
+                uint16_t e[8];
+                __builtin_memcpy(e, &v, 16);
+                for (int k = 0; k < 8 && col + k < N; ++k) dst[k] = e[k];
+            }
+        }
+        return;
+    } else {
+        constexpr bool greedy = EPI == EPI_GREEDY;
+        const int r = threadIdx.x >> 1, hh = threadIdx.x & 1;
+        const int grow = m0 + r;
+        const bool row_ok = grow < M;
+        uint32_t key = 0u, key2 = 0u, keyb = 0u;
+        if (!greedy && row_ok) {
+            key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
+            key2 = noise_key2(key);
+            keyb = noise_keyb(key);
+        }
+        const float temp = greedy ? 1.f : 1.0f / inv_t;
+        const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+        float best_s = -INFINITY, best_x = __builtin_nanf("");
+        int best_i = 0x7fffffff;
+        float m = -1e30f, s = 0.f;
+        float thr = -INFINITY;  // (best exact score so far - kNoiseC) * T
+        bool seeded = false;
+        // thread hh visits chunks 2i + hh (ascending): the image swizzle makes a 16-lane read group
+        // (8 rows x 2 parities) hit 16 distinct bank slots
+#pragma unroll 2
+        for (int i = 0; i < 16; ++i) {
+            const int c = 2 * i + hh;
+            const int v0 = n0 + c * 8;
+            const int cnt = min(8, N - v0);
+            if (cnt <= 0) break;
+            const uint4 pk = *reinterpret_cast<const uint4*>(smem + img_off(r, c));
+            const uint32_t wds[4] = {pk.x, pk.y, pk.z, pk.w};
+            float x[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x[2 * k] = __uint_as_float(wds[k] << 16);
+                x[2 * k + 1] = __uint_as_float(wds[k] & 0xffff0000u);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = k < cnt ? x[k] : -INFINITY;
+            float vmax = x[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) vmax = fmaxf(vmax, x[k]);
+            {  // raw online (max, sum-exp)
+                const float mn = fmaxf(m, vmax);
+                float acc_e = 0.f;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc_e += fast_exp2((x[k] - mn) * kLog2eG);
+                s = s * fast_exp2((m - mn) * kLog2eG) + acc_e;
+                m = mn;
+            }
+            if constexpr (greedy) {
+                if (vmax > best_s) {
+                    int kk = 7;
+#pragma unroll
+                    for (int k = 6; k >= 0; --k) kk = (x[k] == vmax) ? k : kk;
+                    best_s = vmax;
+                    best_i = v0 + kk;
+                    best_x = vmax;
+                }
+                continue;
+            } else {
+                const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+                if (!seeded) {  // the exact score of this thread's first largest element sets its bar
+                    seeded = true;
+                    int kb = 0;
+#pragma unroll
+                    for (int k = 7; k >= 0; --k) kb = (x[k] == vmax) ? k : kb;
+                    best_s = noise_score(x[kb], inv_t, v0 + kb, h, group_min_e(h), key2);
+                    best_i = v0 + kb;
+                    best_x = x[kb];
+                    thr = (best_s - kNoiseC) * temp;
+                }
+                const float bits = noise_bits(h);
+                if (fmaf(bits, -kT, vmax) - thr < 0.f) continue;  // no element of the group can reach the bar
+                const float Eg = group_min_e(h);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (k < cnt && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
+                        const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
+                        if (sc > best_s) {  // ascending visit order: strict keeps the lowest index
+                            best_s = sc;
+                            best_i = v0 + k;
+                            best_x = x[k];
+                        }
+                    }
+                }
+                thr = (best_s - kNoiseC) * temp;
+            }
+        }
+        // the row's two threads are lanes 2j, 2j + 1
+        {
+            const float os = __shfl_xor(best_s, 1, kWave);
+            const int oi = __shfl_xor(best_i, 1, kWave);
+            const float ox = __shfl_xor(best_x, 1, kWave);
+            if (better(os, oi, Best{best_s, best_i})) {
+                best_s = os;
+                best_i = oi;
+                best_x = ox;
+            }
+            const float om = __shfl_xor(m, 1, kWave), oss = __shfl_xor(s, 1, kWave);
+            const float mn = fmaxf(m, om);
+            s = s * fast_exp2((m - mn) * kLog2eG) + oss * fast_exp2((om - mn) * kLog2eG);
+            m = mn;
+        }
+        if (hh == 0 && row_ok) {
+            const int64_t pi = (int64_t)grow * nt + ntile;
+            parts[pi] = make_float4(best_s, __int_as_float(best_i), m, s);
+            part_x[pi] = best_x;
+        }
+    }
+}
+
+// One wave per row: fold the row's nt tile partials (ascending tile order per lane, then a
+// xor tree with the (score desc, index asc) order) and finalize token + logprob.
+__global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* __restrict__ parts,
+                                                                 const float* __restrict__ part_x, int nt,
+                                                                 int32_t* __restrict__ tokens,
+                                                                 float* __restrict__ logp_out) {
+    const int row = blockIdx.x, lane = threadIdx.x;
+    Best b{-INFINITY, 0x7fffffff};
+    float bx = __builtin_nanf(""), m = -1e30f, s = 0.f;
+    for (int j = lane; j < nt; j += 64) {
+        const float4 p = parts[(int64_t)row * nt + j];
+        const int idx = __float_as_int(p.y);
+        if (better(p.x, idx, b)) {
+            b = Best{p.x, idx};
+            bx = part_x[(int64_t)row * nt + j];
+        }
+        const float mn = fmaxf(m, p.z);
+        s = s * fast_exp2((m - mn) * kLog2eG) + p.w * fast_exp2((p.z - mn) * kLog2eG);
+        m = mn;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(b.score, off, kWave);
+        const int oi = __shfl_xor(b.idx, off, kWave);
+        const float ox = __shfl_xor(bx, off, kWave);
+        if (better(os, oi, b)) {
+            b = Best{os, oi};
+            bx = ox;
+        }
+        const float om = __shfl_xor(m, off, kWave), oss = __shfl_xor(s, off, kWave);
+        const float mn = fmaxf(m, om);
+        s = s * fast_exp2((m - mn) * kLog2eG) + oss * fast_exp2((om - mn) * kLog2eG);
+        m = mn;
+    }
+    if (lane == 0) {
+        tokens[row] = b.idx;
+        if (logp_out) logp_out[row] = bx - (m + fast_log2(s) * kLn2G);
+    }
+}
+
+inline int tiles(int n, int b) { return (n + b - 1) / b; }
+
+int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M, int N, int K) {
+    SKYRL_REQUIRE(M >= 0 && N > 0 && K > 0, "lmhead_gemm: bad sizes");
+    SKYRL_REQUIRE(K % BK == 0, "lmhead_gemm: K must be a multiple of 64");
+    SKYRL_REQUIRE(ldh >= K && ldw >= K && ldh % 8 == 0 && ldw % 8 == 0, "lmhead_gemm: row strides must be >= K and 16-B multiples");
+    SKYRL_REQUIRE(h && w, "lmhead_gemm: null operand");
+    SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(h) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
+                  "lmhead_gemm: operands must be 16-B aligned");
+    return SKYRL_OK;
+}
+
+}  // namespace
+}  // namespace skyrl
+
+using namespace skyrl;
+
+extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
+                                 int32_t N, int32_t K, void* out, int64_t ld_out, void* stream) {
+    int rc = check_operands(hidden, ld_hidden, weight, ld_weight, M, N, K);
+    if (rc) return rc;
+    if (M == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(out && ld_out >= N, "lmhead_gemm: bad output");
+    const int mt = tiles(M, BM), nt = tiles(N, BN);
+    hipLaunchKernelGGL(lmhead_gemm_kernel<EPI_STORE>, dim3(mt * nt), dim3(NT), 0, as_stream(stream),
+                       reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
+                       ld_weight, M, N, K, mt, reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
+                       nullptr, nullptr, nt);
+    return check_launch("lmhead_gemm_kernel<store>");
+}
+
+extern "C" size_t skyrl_lmhead_sample_workspace_bytes(int32_t M, int32_t V) {
+    const size_t n = (size_t)(M > 0 ? M : 1) * tiles(V > 0 ? V : 1, BN);
+    return n * sizeof(float4) + n * sizeof(float) + 256;
+}
+
+extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight,
+                                   int32_t M, int32_t V, int32_t K, float temperature, uint64_t seed,
+                                   const int64_t* seq_ids, int64_t step, int32_t* tokens_out, float* logp_out,
+                                   void* workspace, void* stream) {
+    int rc = check_operands(hidden, ld_hidden, weight, ld_weight, M, V, K);
+    if (rc) return rc;
+    if (M == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(tokens_out && workspace, "lmhead_sample: null pointer");
+    SKYRL_REQUIRE(temperature >= 0.f, "lmhead_sample: temperature must be >= 0");
+    SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_sample: workspace must be 16-B aligned");
+    const int mt = tiles(M, BM), nt = tiles(V, BN);
+    float4* parts = reinterpret_cast<float4*>(workspace);
+    float* part_x = reinterpret_cast<float*>(parts + (size_t)M * nt);
+    const bool greedy = temperature == 0.f;
+    const float inv_t = greedy ? 1.f : 1.0f / temperature;
+    auto kern = greedy ? lmhead_gemm_kernel<EPI_GREEDY> : lmhead_gemm_kernel<EPI_SAMPLE>;
+    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(NT), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
+                       ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt, nullptr, 0ll, inv_t,
+                       seed, seq_ids, step, parts, part_x, nt);
+    rc = check_launch("lmhead_gemm_kernel<sample>");
+    if (rc) return rc;
+    hipLaunchKernelGGL(lmhead_sample_merge_kernel, dim3(M), dim3(64), 0, as_stream(stream), parts, part_x, nt, tokens_out,
+                       logp_out);
+    return check_launch("lmhead_sample_merge_kernel");
+}

@@ -21,6 +21,7 @@
 // workgroup, and the last-arriving split of the row (arrive.h) folds the
 // partials in split order (lowest index wins ties).
 #include "arrive.h"
+#include "noise.h"
 
 #include <type_traits>
 
@@ -34,59 +35,6 @@ constexpr int kRowModeMinSeqs = 256;  // enough rows to fill the chip with one w
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
-    x ^= x >> 16;
-    x *= 0x7feb352du;
-    x ^= x >> 15;
-    x *= 0x846ca68bu;
-    x ^= x >> 16;
-    return x;
-}
-
-// Per-element noise hash of pair index p (two 16-bit halves, one per element). Built from
-// 24-bit multiplies (v_mad_u32_u24 / v_mul_u32_u24 issue at the full VALU rate, v_mul_lo_u32 at a
-// quarter of it) and 16-bit xor-shifts (one SDWA op each); the two row keys enter at two rounds, so
-// that an additive collision of the first round between rows is broken by the second.
-// Bit-identical in oracle/sampler_ref.c.
-__host__ __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
-__host__ __device__ __forceinline__ uint32_t ehash(uint32_t ka, uint32_t kb, uint32_t p) {
-    uint32_t h = mul24(p, 0x9e3779u) + ka;
-    h ^= h >> 16;
-    h = mul24(h, 0x85ebcau) + kb;
-    h ^= h >> 16;
-    h = mul24(h, 0xc2b2aeu);
-    h ^= h >> 16;
-    return h;
-}
-
-__host__ __device__ __forceinline__ uint32_t row_key(uint64_t seed, int64_t seq, int64_t step) {
-    uint32_t k = hash32((uint32_t)seed ^ 0x9e3779b9u);
-    k = hash32(k ^ (uint32_t)(seed >> 32));
-    k = hash32(k ^ (uint32_t)((uint64_t)seq));
-    k = hash32(k ^ (uint32_t)((uint64_t)seq >> 32));
-    k = hash32(k ^ (uint32_t)((uint64_t)step));
-    k = hash32(k ^ (uint32_t)((uint64_t)step >> 32));
-    return k;
-}
-
-// Deterministic natural log for normal positive floats (branch-free): ix = bits - bits(2/3),
-// e = ix >> 23 (arithmetic), mantissa rebased into [2/3, 4/3), ln(1+z) = z*P6(z) by fmaf
-// Horner (|err| < 1.1e-6). Bit-identical in oracle/sampler_ref.c (same ops, contraction off).
-__host__ __device__ __forceinline__ float det_ln(float y) {
-    const uint32_t ix = __builtin_bit_cast(uint32_t, y) - 0x3f2aaaabu;
-    const int e = (int)ix >> 23;
-    const float m = __builtin_bit_cast(float, (ix & 0x007fffffu) + 0x3f2aaaabu);
-    const float z = m - 1.0f;
-    float p = 0.16302786767482758f;
-    p = fmaf(p, z, -0.18978701531887054f);
-    p = fmaf(p, z, 0.19917640089988708f);
-    p = fmaf(p, z, -0.24900923669338226f);
-    p = fmaf(p, z, 0.3333371579647064f);
-    p = fmaf(p, z, -0.5000061392784119f);
-    p = fmaf(p, z, 1.0f);
-    return fmaf((float)e, 0.693147180559945f, z * p);
-}
-
 // order-preserving unsigned keys
 __device__ __forceinline__ uint32_t okey_bf16(uint16_t h) {
     return (h & 0x8000u) ? (uint32_t)(uint16_t)~h : (uint32_t)(h | 0x8000u);
@@ -98,14 +46,6 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_stream(const uint4* p) {
     const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-struct Best {
-    float score;
-    int idx;
-};
-__device__ __forceinline__ bool better(float s, int i, const Best& b) {
-    return s > b.score || (s == b.score && i < b.idx);
 }
 
 struct Part {  // per (row, split) partial
@@ -480,8 +420,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     // (so a strict '>' keeps the lowest index on ties) and the raw online (max, sum-exp).
     float best_s = -INFINITY;
     int best_i = 0x7fffffff;
-    const uint32_t key2 = hash32(key ^ 0x5bd1e995u);  // per-element uniforms (candidates only)
-    const uint32_t keyb = hash32(key ^ 0x27d4eb2fu);  // second-round key of ehash
+    const uint32_t key2 = noise_key2(key);  // per-element uniforms (candidates only)
+    const uint32_t keyb = noise_keyb(key);  // second-round key of ehash
     // raw online (max, sum-exp) for the sampled token's logprob; finite start so that an
     // all-padding vector never forms inf - inf
     float m = -1e30f, s = 0.f;
@@ -501,29 +441,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     // the filter only skips elements whose exact score is provably below a score already found.
     const float temp = greedy ? 1.f : 1.0f / inv_t;
     const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-    constexpr float kC = 146.0f * 0.6931471805599453f + 0.01f;
-    constexpr float kU24 = 5.9604644775390625e-8f;
+    constexpr float kC = kNoiseC;
     float thr = -INFINITY;   // (bar - C) * T, wave-uniform
     float bar = -INFINITY;   // best exact score known to this wave (wave-uniform)
     bool seeded = greedy;    // first vector: one exact score per lane sets the bar
     constexpr int VEC = 16 / sizeof(T);  // 8 bf16 (one group) or 4 f32 (half a group)
 
     // E_g of group hash h (the group's smallest Exp(1) draw)
-    auto group_e = [&](uint32_t h) -> float {
-        const uint32_t t16 = (h >> 16) ^ 0xffffu;
-        const float ug = (float)(((t16 << 8) | ((h >> 8) & 0xffu)) | 1u) * kU24;
-        return -det_ln(ug) * 0.125f;
-    };
+    auto group_e = [&](uint32_t h) -> float { return group_min_e(h); };
     // exact score of element v of the group with hash h and minimum E_g
-    auto exact = [&](float xk, int v, uint32_t h, float Eg) -> float {
-        float E = Eg;
-        if (((uint32_t)v & 7u) != (h & 7u)) {
-            const uint32_t hu = hash32(key2 ^ ((uint32_t)v * 0x9e3779b1u));
-            const float U = (float)((hu >> 8) | 1u) * kU24;
-            E = Eg + (-det_ln(U));
-        }
-        return xk * inv_t + (-det_ln(E));
-    };
+    auto exact = [&](float xk, int v, uint32_t h, float Eg) -> float { return noise_score(xk, inv_t, v, h, Eg, key2); };
     // Every element of a candidate vector that can still reach the bar through the group bound
     // (the additive form per element; a tie with the bar is evaluated). Unrolled over the slots:
     // a slot's block runs only when some lane needs it (usually one or two per candidate vector).

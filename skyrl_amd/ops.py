@@ -551,6 +551,57 @@ def sample(
     return tokens, logp
 
 
+# ------------------------------------------------- §8(f)1 decode: lm_head GEMM + fused sampler
+def _lmhead_operands(hidden: torch.Tensor, weight: torch.Tensor):
+    dev = _require_gpu(hidden, weight)
+    if hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+        raise TypeError("lm_head operands must be bf16")
+    if hidden.dim() != 2 or weight.dim() != 2 or hidden.shape[1] != weight.shape[1]:
+        raise ValueError(f"hidden [M,K] and weight [V,K] expected, got {tuple(hidden.shape)} and {tuple(weight.shape)}")
+    if hidden.stride(1) != 1 or weight.stride(1) != 1:
+        raise ValueError("lm_head operands need a unit K stride")
+    return dev
+
+
+def lmhead_gemm(hidden: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 logits [M,V] = hidden [M,K] @ weight[V,K]^T on the MFMA kernel of the fused sampler."""
+    dev = _lmhead_operands(hidden, weight)
+    M, K = hidden.shape
+    V = weight.shape[0]
+    z = out if out is not None else torch.empty((M, V), dtype=torch.bfloat16, device=dev)
+    _ffi.call("skyrl_lmhead_gemm", _ptr(hidden), hidden.stride(0), _ptr(weight), weight.stride(0), M, V, K, _ptr(z),
+              z.stride(0), _stream(dev))
+    return z
+
+
+def lmhead_sample(
+    hidden: torch.Tensor,
+    weight: torch.Tensor,
+    *,
+    temperature: float = 1.0,
+    seed: int = 0,
+    seq_ids: Optional[torch.Tensor] = None,
+    step: int = 0,
+    want_logprobs: bool = True,
+    tokens_out: Optional[torch.Tensor] = None,
+    logp_out: Optional[torch.Tensor] = None,
+) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """sample(hidden @ weight^T, temperature, seed, seq_ids, step) without materializing the logits:
+    the same tokens as ops.sample on ops.lmhead_gemm's logits (no top_k / top_p / min_p)."""
+    dev = _lmhead_operands(hidden, weight)
+    M, K = hidden.shape
+    V = weight.shape[0]
+    ids = None if seq_ids is None else seq_ids.to(device=dev, dtype=torch.int64).contiguous()
+    tokens = tokens_out if tokens_out is not None else torch.empty(M, dtype=torch.int32, device=dev)
+    logp = logp_out if logp_out is not None else (
+        torch.empty(M, dtype=torch.float32, device=dev) if want_logprobs else None)
+    ws = WORKSPACES.get(dev, "lmhead_sample", _ffi.query("skyrl_lmhead_sample_workspace_bytes", M, V))
+    _ffi.call("skyrl_lmhead_sample", _ptr(hidden), hidden.stride(0), _ptr(weight), weight.stride(0), M, V, K,
+              float(temperature), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), _ptr(ids), int(step),
+              _ptr(tokens), _ptr(logp), _ptr(ws), _stream(dev))
+    return tokens, logp
+
+
 # ---------------------------------------------------------------------------- a9 pack
 def pack_experience(
     prompt_tokens: torch.Tensor, prompt_off: torch.Tensor,

@@ -1,0 +1,138 @@
+"""§8(f)1 decode side: the MFMA lm_head GEMM (csrc/lmhead_gemm.hip) and the sampler fused into
+its epilogue, against
+
+  * torch (exact small-integer operands: every product and sum is exact, so the bf16 logits must
+    match bit for bit, which pins the MFMA operand/accumulator maps and the tile edges);
+  * torch fp32 on random operands (bf16 output resolution);
+  * the unfused path: skyrl_sample over the logits skyrl_lmhead_gemm writes -- tokens bit-exact,
+    logprobs 1e-4 -- and oracle/sampler_ref.c on those same logits (tokens bit-exact);
+
+at every BASELINE.json vocabulary (GPT-2 50,257: odd V, misaligned output rows), hidden sizes
+768 / 1536 / 3584 / 4096, ragged M and V tile edges, T = 1, 0.7 and greedy.
+"""
+
+import pytest
+import torch
+
+from skyrl_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _ints(shape, g, lo=-3, hi=4):
+    return torch.randint(lo, hi, shape, generator=g).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,V,K", [(300, 1037, 192), (256, 256, 64), (1, 300, 128), (513, 2100, 256)])
+def test_gemm_exact_small_integers(dev, M, V, K):
+    g = torch.Generator().manual_seed(M + V + K)
+    h, w = _ints((M, K), g), _ints((V, K), g)
+    w[:, 0] += torch.arange(V).remainder(5).to(torch.bfloat16)  # asymmetric: a row/col swap cannot pass
+    z = ops.lmhead_gemm(h.to(dev), w.to(dev))
+    ref = (h.float() @ w.float().T).to(torch.bfloat16)
+    assert torch.equal(z.cpu(), ref)
+
+
+def test_gemm_strided_operands(dev):
+    """Row strides larger than K (a [n, S, H] hidden slice) and an output with ld > V."""
+    g = torch.Generator().manual_seed(5)
+    M, V, K = 70, 777, 128
+    hb = _ints((M, K + 64), g)
+    w = _ints((V, K), g)
+    out = torch.full((M, V + 9), 7.0, dtype=torch.bfloat16, device=dev)
+    ops.lmhead_gemm(hb.to(dev)[:, :K], w.to(dev), out=out[:, :V])
+    assert torch.equal(out[:, :V].cpu(), (hb[:, :K].float() @ w.float().T).to(torch.bfloat16))
+    assert bool((out[:, V:] == 7.0).all())  # nothing written past N
+
+
+def test_gemm_random_vs_fp32(dev):
+    g = torch.Generator().manual_seed(11)
+    M, V, K = 512, 4136, 1536
+    h = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(V, K, generator=g) * 0.05).to(torch.bfloat16)
+    z = ops.lmhead_gemm(h.to(dev), w.to(dev)).float().cpu()
+    ref = h.float() @ w.float().T
+    torch.testing.assert_close(z, ref, rtol=8e-3, atol=2e-3)  # bf16 output rounding
+
+
+def _case(M, V, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(V, K, generator=g) * (3.0 / K ** 0.5)).to(torch.bfloat16)  # logits ~ N(0, 9)
+    ids = torch.randint(0, 1 << 40, (M,), generator=g)
+    return h, w, ids
+
+
+@pytest.mark.parametrize("V,K", [(50257, 768), (128256, 4096), (151936, 1536), (152064, 3584)])
+@pytest.mark.parametrize("temp", [1.0, 0.7, 0.0])
+def test_fused_sample_equals_unfused_per_vocab(dev, V, K, temp):
+    for M, seed in ((37, 1), (300, 2)):
+        h, w, ids = _case(M, V, K, seed + V)
+        hd, wd, idd = h.to(dev), w.to(dev), ids.to(dev)
+        z = ops.lmhead_gemm(hd, wd)
+        tu, lu = ops.sample(z, temperature=temp, seed=77, seq_ids=idd, step=5)
+        tf, lf = ops.lmhead_sample(hd, wd, temperature=temp, seed=77, seq_ids=idd, step=5)
+        assert torch.equal(tf.cpu(), tu.cpu()), f"M={M}: {(tf != tu).sum().item()} tokens differ"
+        torch.testing.assert_close(lf.cpu(), lu.cpu(), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("temp", [1.0, 0.7, 0.0])
+def test_fused_sample_vs_oracle(dev, temp):
+    from oracle import sampler as osamp
+
+    M, V, K = 24, 151936, 1536
+    h, w, ids = _case(M, V, K, 99)
+    hd, wd = h.to(dev), w.to(dev)
+    z = ops.lmhead_gemm(hd, wd).cpu()
+    for step in (0, 13):
+        tf, lf = ops.lmhead_sample(hd, wd, temperature=temp, seed=2024, seq_ids=ids.to(dev), step=step)
+        et, el = osamp.sample(z, temp, -1, 1.0, 0.0, 2024, ids, step)
+        assert torch.equal(tf.cpu(), et)
+        torch.testing.assert_close(lf.cpu(), el, atol=1e-4, rtol=1e-5)
+
+
+def test_fused_sample_row_independence_and_edges(dev):
+    """A row's token depends only on its own hidden state, key and step (not on M or on which
+    tile row it lands in), and M = 1 / M = 257 / a ragged last vocab tile work."""
+    V, K = 1000, 256
+    h, w, ids = _case(257, V, K, 3)
+    hd, wd, idd = h.to(dev), w.to(dev), ids.to(dev)
+    t_all, l_all = ops.lmhead_sample(hd, wd, seed=1, seq_ids=idd, step=2)
+    for lo, hi in ((0, 1), (256, 257), (100, 220)):
+        t, lp = ops.lmhead_sample(hd[lo:hi].contiguous(), wd, seed=1, seq_ids=idd[lo:hi], step=2)
+        assert torch.equal(t.cpu(), t_all[lo:hi].cpu())
+        torch.testing.assert_close(lp.cpu(), l_all[lo:hi].cpu(), atol=1e-5, rtol=1e-6)
+
+
+def test_fused_sample_distribution_small_vocab(dev):
+    """Empirical frequencies over 40k independent rows follow softmax(logits / T) (chi-square)."""
+    import numpy as np
+    from scipy import stats
+
+    V, K, M = 24, 64, 40000
+    g = torch.Generator().manual_seed(8)
+    w = (torch.randn(V, K, generator=g) * 0.3).to(torch.bfloat16)
+    h1 = torch.randn(1, K, generator=g).to(torch.bfloat16)
+    hd = h1.to(dev).expand(M, K).contiguous()
+    wd = w.to(dev)
+    logits = ops.lmhead_gemm(hd[:1], wd).float().cpu()[0]
+    for temp in (1.0, 0.7):
+        tok, _ = ops.lmhead_sample(hd, wd, temperature=temp, seed=5, seq_ids=torch.arange(M, device=dev), step=0)
+        counts = np.bincount(tok.cpu().numpy(), minlength=V)
+        p = torch.softmax(logits / temp, 0).double().numpy()
+        keep = p * M >= 5
+        obs = np.append(counts[keep], counts[~keep].sum())
+        exp = np.append(p[keep], p[~keep].sum()) * M
+        pval = stats.chisquare(obs, exp).pvalue
+        assert pval > 1e-3, (temp, pval)
+
+
+def test_lmhead_rejects_bad_operands(dev):
+    h = torch.zeros(4, 100, dtype=torch.bfloat16, device=dev)  # K not a multiple of 64
+    w = torch.zeros(10, 100, dtype=torch.bfloat16, device=dev)
+    from skyrl_amd._ffi import SkyrlHipError
+
+    with pytest.raises(SkyrlHipError):
+        ops.lmhead_gemm(h, w)
+    with pytest.raises(TypeError):
+        ops.lmhead_gemm(h.float(), w)
