@@ -1,3 +1,6 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_vocabs.py -q --timeout 200 --timeout-method thread -k "persistent or policy_train" > gpurun_out/r02_t11.log 2>&1; echo "tests rc=$?" >> gpurun_out/r02_t11.log
-timeout -k 10 300 python scripts/kbench.py --only fused --rounds 5 > gpurun_out/r02_kb11.json 2> gpurun_out/r02_kb11.err
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_lmhead_sample.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r02_lms_test.log 2>&1; rc=$?; echo "tests rc=$rc" >> gpurun_out/r02_lms_test.log
+[ $rc -ge 124 ] && exit $rc
+timeout -k 10 300 python scripts/probe/lmhead_sample_bench.py --T 1.0 0.0 > gpurun_out/r02_lms_bench.json 2> gpurun_out/r02_lms_bench.err || exit $?
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 --no-e2e --no-cpu-baseline --no-vocab-legs > gpurun_out/r02_bench_coherent.json 2> gpurun_out/r02_bench_coherent.err

@@ -39,11 +39,14 @@ def main():
     ap.add_argument("--V", type=int, default=151936)
     ap.add_argument("--T", type=float, nargs="+", default=[1.0])
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--pipes", type=int, nargs="+", default=[0], help="skyrl_tune lmhead_pipe variants")
     args = ap.parse_args()
     dev = torch.device("cuda")
     H, V = args.H, args.V
     w = (torch.randn(V, H, device=dev) * (3.0 / H ** 0.5)).to(torch.bfloat16)
-    for M in args.M:
+    from skyrl_amd import _ffi
+    for M, pipe in [(m, p) for m in args.M for p in args.pipes]:
+        _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
         h = torch.randn(M, H, device=dev).to(torch.bfloat16)
         ids = torch.arange(M, device=dev)
         z = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
@@ -58,7 +61,7 @@ def main():
             def fused():
                 ops.lmhead_sample(h, w, temperature=T, seed=1, seq_ids=ids, step=3, tokens_out=tok, logp_out=lp)
 
-            res = {"M": M, "H": H, "V": V, "T": T,
+            res = {"M": M, "H": H, "V": V, "T": T, "pipe": pipe,
                    "linear_us": timeit(lambda: torch.matmul(h, w.T, out=z), args.iters),
                    "gemm_us": timeit(lambda: ops.lmhead_gemm(h, w, out=z), args.iters),
                    "unfused_us": timeit(unfused, args.iters),

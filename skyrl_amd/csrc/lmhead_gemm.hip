@@ -33,10 +33,8 @@
 namespace skyrl {
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
-constexpr int kOpBytes = 256 * BK * 2;        // one operand tile [256 rows][64 k] bf16
-constexpr int kStageBytes = 2 * kOpBytes;     // H tile + W tile
-constexpr int kLdsBytes = 2 * kStageBytes;    // two stages = the [256][256] bf16 epilogue image
+constexpr int BM = 256, BN = 256, NT = 512;
+constexpr int kLdsBytes = 131072;  // the pipeline stages, then the [256][256] bf16 epilogue image
 constexpr float kLog2eG = 1.4426950408889634f;
 constexpr float kLn2G = 0.6931471805599453f;
 
@@ -47,14 +45,36 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2 };
 
+// K pipeline: BKT-deep K tiles in S LDS stages (S - 1 tiles in flight while one feeds the MFMAs)
+template <int BKT, int S>
+struct Pipe {
+    static constexpr int kRowBytes = BKT * 2;                 // one operand row of a K tile
+    static constexpr int kChunks = kRowBytes / 16;            // 16-B chunks per row
+    static constexpr int kRowsPerWin = 256 / kRowBytes;       // rows per 256-B LDS bank window
+    static constexpr int kOpBytes = 256 * kRowBytes;          // one operand tile
+    static constexpr int kStageBytes = 2 * kOpBytes;          // H tile + W tile
+    static constexpr int kRowsPerPiece = 1024 / kRowBytes;    // rows per 1-KB wave copy (64 x 16 B)
+    static constexpr int kPieces = 256 / kRowsPerPiece / 4;   // copies per wave per operand tile
+    static constexpr int KS = BKT / 32;                       // 16x16x32 k-steps per K tile
+    static_assert(S >= 2 && S * kStageBytes <= kLdsBytes, "LDS");
+    // chunk swizzle of a row: the 16 rows of a fragment read hit 16 distinct 16-B bank slots
+    __device__ static int swz(int row) { return (row / kRowsPerWin) % kChunks; }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
 // byte offset of 16-B chunk c (8 bf16) of row r in the [256][256] bf16 epilogue image
 __device__ __forceinline__ int img_off(int r, int c) { return r * 512 + ((c ^ ((r & 7) << 1)) << 4); }
 
-template <int EPI>
+int g_lmhead_pipe = 0;  // skyrl_tune("lmhead_pipe"): 0 = BK 64 x 2 stages, 1 = BK 32 x 4, 2 = BK 32 x 3
+
+template <int EPI, int BKT, int S>
 __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
     int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt) {
+    using P = Pipe<BKT, S>;
     __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
@@ -63,37 +83,38 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = w >> 2, wn = w & 3;
 
-    // staging: waves 0-3 copy the H tile, waves 4-7 the W tile, 8 pieces of 8 rows x 128 B each
-    const int opnd = w >> 2, grp0 = (w & 3) * 8, lrow = lane >> 3, pc = lane & 7;
-    const uint16_t* gsrc[8];
+    // staging: waves 0-3 copy the H tile, waves 4-7 the W tile, kPieces 1-KB pieces each
+    const int opnd = w >> 2, piece0 = (w & 3) * P::kPieces;
+    const int lrow = lane / P::kChunks, pc = lane % P::kChunks;
+    const uint16_t* gsrc[P::kPieces];
     {
         const uint16_t* base = opnd ? W : H;
         const int64_t ld = opnd ? ldw : ldh;
         const int r0 = opnd ? n0 : m0, lim = (opnd ? N : M) - 1;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int row = (grp0 + j) * 8 + lrow;
-            const int c = pc ^ ((row >> 1) & 7);  // the logical chunk that lands in physical chunk pc
+        for (int j = 0; j < P::kPieces; ++j) {
+            const int row = (piece0 + j) * P::kRowsPerPiece + lrow;
+            const int c = pc ^ P::swz(row);  // the logical chunk that lands in physical chunk pc
             gsrc[j] = base + (int64_t)min(r0 + row, lim) * ld + c * 8;
         }
     }
-    char* const sdst = smem + opnd * kOpBytes + grp0 * 1024;
+    char* const sdst = smem + opnd * P::kOpBytes + piece0 * 1024;
     auto stage = [&](int buf, int k0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + k0), (lds_void*)(sdst + buf * kStageBytes + j * 1024),
-                                             16, 0, 0);
+        for (int j = 0; j < P::kPieces; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + k0),
+                                             (lds_void*)(sdst + buf * P::kStageBytes + j * 1024), 16, 0, 0);
     };
     // fragment offsets: rows wm*128 + mb*16 + (lane & 15) of H, wn*64 + nb*16 + (lane & 15) of W;
-    // k chunk ks*4 + (lane >> 4) (16x16x32 operand map); the swizzle term is ((lane & 15) >> 1)
-    int aoff[2], boff[2];
+    // k chunk ks*4 + (lane >> 4) (16x16x32 operand map); the swizzle depends on lane & 15 only
+    int aoff[P::KS], boff[P::KS];
     {
-        const int sw = (lane & 15) >> 1;
+        const int sw = P::swz(lane & 15);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < P::KS; ++ks) {
             const int c = (ks * 4 + (lane >> 4)) ^ sw;
-            aoff[ks] = (wm * 128 + (lane & 15)) * 128 + c * 16;
-            boff[ks] = kOpBytes + (wn * 64 + (lane & 15)) * 128 + c * 16;
+            aoff[ks] = (wm * 128 + (lane & 15)) * P::kRowBytes + c * 16;
+            boff[ks] = P::kOpBytes + (wn * 64 + (lane & 15)) * P::kRowBytes + c * 16;
         }
     }
     f32x4 acc[8][4];
@@ -102,31 +123,38 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = K / BK;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    for (int t = 0; t < nk; ++t) {
-        const char* sb = smem + (t & 1) * kStageBytes;
-        if (t + 1 < nk) stage((t + 1) & 1, (t + 1) * BK);
+    const int nk = K / BKT;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+    for (int p = 0; p < S - 1; ++p)
+        if (p < nk) stage(p, p * BKT);
+    for (int t = 0; t < nk; ++t) {
+        // tile t has landed once at most min(S - 2, nk - 1 - t) younger tiles are outstanding;
+        // every wave's fragment reads of the buffer restaged below are done (WAR), then the barrier
+        const int ahead = min(S - 2, nk - 1 - t);
+        if (ahead <= 0) wait_vmcnt<0>();
+        else if (ahead == 1) wait_vmcnt<P::kPieces>();
+        else wait_vmcnt<2 * P::kPieces>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+        const char* sb = smem + (t % S) * P::kStageBytes;
+#pragma unroll
+        for (int ks = 0; ks < P::KS; ++ks) {
             bf16x8 b[4];
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 2048);
+            for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * P::kRowBytes);
 #pragma unroll
             for (int mb = 0; mb < 8; ++mb) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 2048);
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * P::kRowBytes);
 #pragma unroll
                 for (int nb = 0; nb < 4; ++nb)
                     acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[nb], acc[mb][nb], 0, 0, 0);
             }
         }
-        // this wave's fragment reads are done (the next stage overwrites this buffer) and its
-        // staging of tile t+1 has landed; the barrier makes both hold for every wave
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
     }
+    // every wave's last fragment reads are done before the image overwrites the stages
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 
     // ---- epilogue: bf16 tile into the LDS image (C map: row (lane >> 4) * 4 + i, col lane & 15)
 #pragma unroll
@@ -164,31 +192,23 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
         constexpr bool greedy = EPI == EPI_GREEDY;
         const int r = threadIdx.x >> 1, hh = threadIdx.x & 1;
         const int grow = m0 + r;
-        const bool row_ok = grow < M;
-        uint32_t key = 0u, key2 = 0u, keyb = 0u;
-        if (!greedy && row_ok) {
-            key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
-            key2 = noise_key2(key);
-            keyb = noise_keyb(key);
-        }
-        const float temp = greedy ? 1.f : 1.0f / inv_t;
-        const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-        float best_s = -INFINITY, best_x = __builtin_nanf("");
-        int best_i = 0x7fffffff;
-        float m = -1e30f, s = 0.f;
-        float thr = -INFINITY;  // (best exact score so far - kNoiseC) * T
-        bool seeded = false;
-        // thread hh visits chunks 2i + hh (ascending): the image swizzle makes a 16-lane read group
-        // (8 rows x 2 parities) hit 16 distinct bank slots
-#pragma unroll 2
+        if (grow >= M) return;  // both threads of a row leave together (the pair shuffle below)
+        // thread hh owns chunks 2i + hh, i = 0..15 (ascending columns); the image swizzle makes a
+        // 16-lane read group (8 rows x 2 parities) hit 16 distinct bank slots
+        uint4 pk[16];
+        float vmx[16];
+        float m = -1e30f, s = 0.f;   // raw online (max, sum-exp)
+        float xbest = -INFINITY;     // this thread's largest logit, first occurrence
+        int ibest = 0x7fffffff;
+        // pass 1: LSE, per-vector max and the thread's argmax (the greedy answer)
+#pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int c = 2 * i + hh;
             const int v0 = n0 + c * 8;
             const int cnt = min(8, N - v0);
-            if (cnt <= 0) break;
-            const uint4 pk = *reinterpret_cast<const uint4*>(smem + img_off(r, c));
-            const uint32_t wds[4] = {pk.x, pk.y, pk.z, pk.w};
+            pk[i] = *reinterpret_cast<const uint4*>(smem + img_off(r, c));
             float x[8];
+            const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 x[2 * k] = __uint_as_float(wds[k] << 16);
@@ -199,51 +219,78 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
             float vmax = x[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) vmax = fmaxf(vmax, x[k]);
-            {  // raw online (max, sum-exp)
+            vmx[i] = vmax;
+            if (cnt > 0) {
                 const float mn = fmaxf(m, vmax);
                 float acc_e = 0.f;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) acc_e += fast_exp2((x[k] - mn) * kLog2eG);
                 s = s * fast_exp2((m - mn) * kLog2eG) + acc_e;
                 m = mn;
-            }
-            if constexpr (greedy) {
-                if (vmax > best_s) {
+                if (vmax > xbest) {
                     int kk = 7;
 #pragma unroll
                     for (int k = 6; k >= 0; --k) kk = (x[k] == vmax) ? k : kk;
-                    best_s = vmax;
-                    best_i = v0 + kk;
-                    best_x = vmax;
+                    xbest = vmax;
+                    ibest = v0 + kk;
                 }
-                continue;
-            } else {
-                const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
-                if (!seeded) {  // the exact score of this thread's first largest element sets its bar
-                    seeded = true;
-                    int kb = 0;
+            }
+        }
+        float best_s = xbest, best_x = xbest;
+        int best_i = ibest;
+        if constexpr (!greedy) {
+            const uint32_t key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
+            const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
+            const float temp = 1.0f / inv_t;
+            const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+            // bar: the exact score of the thread's largest logit, raised to the row pair's best
+            best_s = -INFINITY;
+            best_i = 0x7fffffff;
+            if (ibest != 0x7fffffff) {
+                const uint32_t h = ehash(key, keyb, (uint32_t)ibest >> 3);
+                best_s = noise_score(xbest, inv_t, ibest, h, group_min_e(h), key2);
+                best_i = ibest;
+            }
+            const float bar = fmaxf(best_s, __shfl_xor(best_s, 1, kWave));
+            const float thr = (bar - kNoiseC) * temp;
+            // pass 2: candidate elements (group bound vs the bar) as a 128-bit mask, bit 8 i + k
+            uint32_t cm[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-                    for (int k = 7; k >= 0; --k) kb = (x[k] == vmax) ? k : kb;
-                    best_s = noise_score(x[kb], inv_t, v0 + kb, h, group_min_e(h), key2);
-                    best_i = v0 + kb;
-                    best_x = x[kb];
-                    thr = (best_s - kNoiseC) * temp;
-                }
+            for (int i = 0; i < 16; ++i) {
+                const int v0 = n0 + (2 * i + hh) * 8;
+                const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
                 const float bits = noise_bits(h);
-                if (fmaf(bits, -kT, vmax) - thr < 0.f) continue;  // no element of the group can reach the bar
-                const float Eg = group_min_e(h);
+                if (fmaf(bits, -kT, vmx[i]) - thr < 0.f) continue;  // no element of the group reaches the bar
+                const int cnt = min(8, N - v0);
+                const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
+                uint32_t bm = 0u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    if (k < cnt && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
-                        const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
-                        if (sc > best_s) {  // ascending visit order: strict keeps the lowest index
-                            best_s = sc;
-                            best_i = v0 + k;
-                            best_x = x[k];
-                        }
+                    const float xk = __uint_as_float((k & 1) ? (wds[k >> 1] & 0xffff0000u) : (wds[k >> 1] << 16));
+                    if (k < cnt && !(fmaf(bits, -kT, xk) - thr < 0.f)) bm |= 1u << k;
+                }
+                cm[i >> 2] |= bm << ((i & 3) * 8);
+            }
+            // exact scores of the candidates, one per lane per trip (the wave loops max-count times,
+            // not 16 x 8 divergent slots)
+#pragma unroll
+            for (int wd = 0; wd < 4; ++wd) {
+                uint32_t bm = cm[wd];
+                while (bm) {
+                    const int b = __builtin_ctz(bm);
+                    bm &= bm - 1u;
+                    const int i = wd * 4 + (b >> 3), k = b & 7;
+                    const int c = 2 * i + hh;
+                    const int v = n0 + c * 8 + k;
+                    const float xk = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + img_off(r, c) + k * 2));
+                    const uint32_t h = ehash(key, keyb, (uint32_t)v >> 3);
+                    const float sc = noise_score(xk, inv_t, v, h, group_min_e(h), key2);
+                    if (better(sc, v, Best{best_s, best_i})) {
+                        best_s = sc;
+                        best_i = v;
+                        best_x = xk;
                     }
                 }
-                thr = (best_s - kNoiseC) * temp;
             }
         }
         // the row's two threads are lanes 2j, 2j + 1
@@ -261,7 +308,7 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
             s = s * fast_exp2((m - mn) * kLog2eG) + oss * fast_exp2((om - mn) * kLog2eG);
             m = mn;
         }
-        if (hh == 0 && row_ok) {
+        if (hh == 0) {
             const int64_t pi = (int64_t)grow * nt + ntile;
             parts[pi] = make_float4(best_s, __int_as_float(best_i), m, s);
             part_x[pi] = best_x;
@@ -311,9 +358,20 @@ __global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* _
 
 inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
+using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
+                            float, uint64_t, const int64_t*, int64_t, float4*, float*, int);
+template <int EPI>
+GemmKernel pick_kernel() {
+    switch (g_lmhead_pipe) {
+        case 1: return lmhead_gemm_kernel<EPI, 32, 4>;
+        case 2: return lmhead_gemm_kernel<EPI, 32, 3>;
+        default: return lmhead_gemm_kernel<EPI, 64, 2>;
+    }
+}
+
 int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M, int N, int K) {
     SKYRL_REQUIRE(M >= 0 && N > 0 && K > 0, "lmhead_gemm: bad sizes");
-    SKYRL_REQUIRE(K % BK == 0, "lmhead_gemm: K must be a multiple of 64");
+    SKYRL_REQUIRE(K % 64 == 0, "lmhead_gemm: K must be a multiple of 64");
     SKYRL_REQUIRE(ldh >= K && ldw >= K && ldh % 8 == 0 && ldw % 8 == 0, "lmhead_gemm: row strides must be >= K and 16-B multiples");
     SKYRL_REQUIRE(h && w, "lmhead_gemm: null operand");
     SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(h) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
@@ -322,6 +380,12 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }
 
 }  // namespace
+
+int lmhead_tune(int value) {
+    SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: lmhead_pipe must be 0, 1 or 2");
+    g_lmhead_pipe = value;
+    return SKYRL_OK;
+}
 }  // namespace skyrl
 
 using namespace skyrl;
@@ -333,7 +397,7 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
     if (M == 0) return SKYRL_OK;
     SKYRL_REQUIRE(out && ld_out >= N, "lmhead_gemm: bad output");
     const int mt = tiles(M, BM), nt = tiles(N, BN);
-    hipLaunchKernelGGL(lmhead_gemm_kernel<EPI_STORE>, dim3(mt * nt), dim3(NT), 0, as_stream(stream),
+    hipLaunchKernelGGL(pick_kernel<EPI_STORE>(), dim3(mt * nt), dim3(NT), 0, as_stream(stream),
                        reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
                        ld_weight, M, N, K, mt, reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
                        nullptr, nullptr, nt);
@@ -360,7 +424,7 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     float* part_x = reinterpret_cast<float*>(parts + (size_t)M * nt);
     const bool greedy = temperature == 0.f;
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
-    auto kern = greedy ? lmhead_gemm_kernel<EPI_GREEDY> : lmhead_gemm_kernel<EPI_SAMPLE>;
+    auto kern = greedy ? pick_kernel<EPI_GREEDY>() : pick_kernel<EPI_SAMPLE>();
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(NT), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt, nullptr, 0ll, inv_t,
                        seed, seq_ids, step, parts, part_x, nt);

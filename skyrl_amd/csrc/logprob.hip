@@ -215,6 +215,7 @@ extern int g_train_resident_nt;
 extern int g_train_ntstore;
 extern int g_grpo_slices;
 extern int g_loss_units;
+int lmhead_tune(int value);
 }
 
 extern "C" int skyrl_tune(const char* key, int value) {
@@ -247,6 +248,7 @@ extern "C" int skyrl_tune(const char* key, int value) {
         g_loss_units = value;
         return SKYRL_OK;
     }
+    if (k == "lmhead_pipe") return lmhead_tune(value);
     if (k == "logprob_nt") {
         g_tune.nt = value != 0;
         return SKYRL_OK;

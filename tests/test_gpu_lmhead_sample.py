@@ -33,6 +33,26 @@ def test_gemm_exact_small_integers(dev, M, V, K):
     assert torch.equal(z.cpu(), ref)
 
 
+@pytest.mark.parametrize("pipe", [0, 1, 2])
+@pytest.mark.parametrize("K", [64, 128, 192, 1536])
+def test_gemm_pipeline_variants_exact(dev, pipe, K):
+    """Every K pipeline (BK 64 x 2 stages, BK 32 x 4 / x 3) incl. fewer K tiles than stages."""
+    from skyrl_amd import _ffi
+
+    g = torch.Generator().manual_seed(K + pipe)
+    M, V = 300, 700
+    h, w = _ints((M, K), g, -2, 3), _ints((V, K), g, -2, 3)
+    _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
+    try:
+        z = ops.lmhead_gemm(h.to(dev), w.to(dev))
+        tf, _ = ops.lmhead_sample(h.to(dev), w.to(dev), seed=3, step=1)
+    finally:
+        _ffi.call("skyrl_tune", b"lmhead_pipe", 0)
+    assert torch.equal(z.cpu(), (h.float() @ w.float().T).to(torch.bfloat16))
+    tu, _ = ops.sample(z, seed=3, step=1)
+    assert torch.equal(tf, tu)
+
+
 def test_gemm_strided_operands(dev):
     """Row strides larger than K (a [n, S, H] hidden slice) and an output with ld > V."""
     g = torch.Generator().manual_seed(5)
@@ -121,8 +141,9 @@ def test_fused_sample_distribution_small_vocab(dev):
         counts = np.bincount(tok.cpu().numpy(), minlength=V)
         p = torch.softmax(logits / temp, 0).double().numpy()
         keep = p * M >= 5
-        obs = np.append(counts[keep], counts[~keep].sum())
-        exp = np.append(p[keep], p[~keep].sum()) * M
+        obs = np.append(counts[keep], counts[~keep].sum()).astype(np.float64)
+        exp = np.append(p[keep], p[~keep].sum())
+        exp = exp / exp.sum() * obs.sum()
         pval = stats.chisquare(obs, exp).pvalue
         assert pval > 1e-3, (temp, pval)
 
