@@ -33,8 +33,7 @@
 namespace skyrl {
 namespace {
 
-constexpr int BM = 256, BN = 256, NT = 512;
-constexpr int kLdsBytes = 131072;  // the pipeline stages, then the [256][256] bf16 epilogue image
+constexpr int BM = 256;
 constexpr float kLog2eG = 1.4426950408889634f;
 constexpr float kLn2G = 0.6931471805599453f;
 
@@ -45,76 +44,87 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2 };
 
-// K pipeline: BKT-deep K tiles in S LDS stages (S - 1 tiles in flight while one feeds the MFMAs)
-template <int BKT, int S>
-struct Pipe {
-    static constexpr int kRowBytes = BKT * 2;                 // one operand row of a K tile
-    static constexpr int kChunks = kRowBytes / 16;            // 16-B chunks per row
-    static constexpr int kRowsPerWin = 256 / kRowBytes;       // rows per 256-B LDS bank window
-    static constexpr int kOpBytes = 256 * kRowBytes;          // one operand tile
-    static constexpr int kStageBytes = 2 * kOpBytes;          // H tile + W tile
-    static constexpr int kRowsPerPiece = 1024 / kRowBytes;    // rows per 1-KB wave copy (64 x 16 B)
-    static constexpr int kPieces = 256 / kRowsPerPiece / 4;   // copies per wave per operand tile
-    static constexpr int KS = BKT / 32;                       // 16x16x32 k-steps per K tile
-    static_assert(S >= 2 && S * kStageBytes <= kLdsBytes, "LDS");
-    // chunk swizzle of a row: the 16 rows of a fragment read hit 16 distinct 16-B bank slots
+// Tile geometry: BM (256) x BN output columns, NT = 2 BN threads as 2 (M) x BN/64 (N) waves of
+// 128 x 64 outputs; K in BKT-deep tiles through S LDS stages (S - 1 tiles in flight).
+template <int BN, int BKT, int S>
+struct Geo {
+    static constexpr int NT = 2 * BN;
+    static constexpr int kWaves = NT / 64;
+    static constexpr int kRowBytes = BKT * 2;                  // one operand row of a K tile
+    static constexpr int kChunks = kRowBytes / 16;             // 16-B chunks per operand row
+    static constexpr int kRowsPerWin = 256 / kRowBytes;        // operand rows per 256-B LDS bank window
+    static constexpr int kOpABytes = BM * kRowBytes;           // H tile
+    static constexpr int kStageBytes = (BM + BN) * kRowBytes;  // H tile + W tile
+    static constexpr int kRowsPerPiece = 1024 / kRowBytes;     // rows per 1-KB wave copy (64 x 16 B)
+    static constexpr int kPieces = (BM + BN) / kRowsPerPiece / kWaves;  // copies per wave per stage
+    static constexpr int KS = BKT / 32;                        // 16x16x32 k-steps per K tile
+    // epilogue image [BM][BN] bf16; TPR threads per row, thread hh of a row owns chunks TPR i + hh
+    static constexpr int kImgRow = BN * 2;
+    static constexpr int kImgBytes = BM * kImgRow;
+    static constexpr int kCpr = BN / 8;
+    static constexpr int TPR = NT / BM;
+    static constexpr int kChunksPerThread = kCpr / TPR;
+    static constexpr int kLds = S * kStageBytes > kImgBytes ? S * kStageBytes : kImgBytes;
+    static_assert(S >= 2 && kLds <= 160 * 1024, "LDS");
+    static_assert((BM + BN) % (kRowsPerPiece * kWaves) == 0, "staging split");
+    // operand chunk swizzle: the 16 rows of a fragment read hit 16 distinct 16-B bank slots
     __device__ static int swz(int row) { return (row / kRowsPerWin) % kChunks; }
+    // image chunk swizzle: a 16-lane read group (16 / TPR rows x TPR parities) is conflict-free
+    __device__ static int img_off(int r, int c) { return r * kImgRow + ((c ^ ((r & (16 / TPR - 1)) * TPR)) << 4); }
 };
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// byte offset of 16-B chunk c (8 bf16) of row r in the [256][256] bf16 epilogue image
-__device__ __forceinline__ int img_off(int r, int c) { return r * 512 + ((c ^ ((r & 7) << 1)) << 4); }
+// skyrl_tune("lmhead_pipe"): 0 = 256 x 256 tiles, BK 64, 2 stages, one 512-thread workgroup per CU;
+// 1 = 256 x 128 tiles, BK 32, 3 stages, two 256-thread workgroups per CU (one's epilogue
+// overlaps the other's MFMA loop); 2 = 256 x 256, BK 32, 4 stages.
+int g_lmhead_pipe = 1;
 
-int g_lmhead_pipe = 0;  // skyrl_tune("lmhead_pipe"): 0 = BK 64 x 2 stages, 1 = BK 32 x 4, 2 = BK 32 x 3
-
-template <int EPI, int BKT, int S>
-__global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
+template <int EPI, int BN, int BKT, int S>
+__global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
     int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt) {
-    using P = Pipe<BKT, S>;
-    __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+    using G = Geo<BN, BKT, S>;
+    __shared__ __attribute__((aligned(16))) char smem[G::kLds];
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
     const int mtile = wg % mt, ntile = wg / mt;
     const int m0 = mtile * BM, n0 = ntile * BN;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int wm = w >> 2, wn = w & 3;
+    const int wm = w & 1, wn = w >> 1;
 
-    // staging: waves 0-3 copy the H tile, waves 4-7 the W tile, kPieces 1-KB pieces each
-    const int opnd = w >> 2, piece0 = (w & 3) * P::kPieces;
-    const int lrow = lane / P::kChunks, pc = lane % P::kChunks;
-    const uint16_t* gsrc[P::kPieces];
-    {
-        const uint16_t* base = opnd ? W : H;
-        const int64_t ld = opnd ? ldw : ldh;
-        const int r0 = opnd ? n0 : m0, lim = (opnd ? N : M) - 1;
+    // staging: the stage is (BM + BN) operand rows (H rows, then W rows), copied as 1-KB pieces;
+    // wave w copies pieces w * kPieces + j (the piece's LDS offset is wave-uniform: p * 1 KB)
+    const int lrow = lane / G::kChunks, pc = lane % G::kChunks;
+    const uint16_t* gsrc[G::kPieces];
 #pragma unroll
-        for (int j = 0; j < P::kPieces; ++j) {
-            const int row = (piece0 + j) * P::kRowsPerPiece + lrow;
-            const int c = pc ^ P::swz(row);  // the logical chunk that lands in physical chunk pc
-            gsrc[j] = base + (int64_t)min(r0 + row, lim) * ld + c * 8;
-        }
+    for (int j = 0; j < G::kPieces; ++j) {
+        const int row = (w * G::kPieces + j) * G::kRowsPerPiece + lrow;  // stage row
+        const int c = pc ^ G::swz(row);  // the logical chunk that lands in physical chunk pc
+        const bool isw = row >= BM;
+        const int rloc = isw ? row - BM : row;
+        const int grow = isw ? min(n0 + rloc, N - 1) : min(m0 + rloc, M - 1);
+        gsrc[j] = (isw ? W + (int64_t)grow * ldw : H + (int64_t)grow * ldh) + c * 8;
     }
-    char* const sdst = smem + opnd * P::kOpBytes + piece0 * 1024;
+    char* const sdst = smem + w * G::kPieces * 1024;
     auto stage = [&](int buf, int k0) {
 #pragma unroll
-        for (int j = 0; j < P::kPieces; ++j)
+        for (int j = 0; j < G::kPieces; ++j)
             __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + k0),
-                                             (lds_void*)(sdst + buf * P::kStageBytes + j * 1024), 16, 0, 0);
+                                             (lds_void*)(sdst + buf * G::kStageBytes + j * 1024), 16, 0, 0);
     };
     // fragment offsets: rows wm*128 + mb*16 + (lane & 15) of H, wn*64 + nb*16 + (lane & 15) of W;
     // k chunk ks*4 + (lane >> 4) (16x16x32 operand map); the swizzle depends on lane & 15 only
-    int aoff[P::KS], boff[P::KS];
+    int aoff[G::KS], boff[G::KS];
     {
-        const int sw = P::swz(lane & 15);
+        const int sw = G::swz(lane & 15);
 #pragma unroll
-        for (int ks = 0; ks < P::KS; ++ks) {
+        for (int ks = 0; ks < G::KS; ++ks) {
             const int c = (ks * 4 + (lane >> 4)) ^ sw;
-            aoff[ks] = (wm * 128 + (lane & 15)) * P::kRowBytes + c * 16;
-            boff[ks] = P::kOpBytes + (wn * 64 + (lane & 15)) * P::kRowBytes + c * 16;
+            aoff[ks] = (wm * 128 + (lane & 15)) * G::kRowBytes + c * 16;
+            boff[ks] = G::kOpABytes + (wn * 64 + (lane & 15)) * G::kRowBytes + c * 16;
         }
     }
     f32x4 acc[8][4];
@@ -132,20 +142,20 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
         // every wave's fragment reads of the buffer restaged below are done (WAR), then the barrier
         const int ahead = min(S - 2, nk - 1 - t);
         if (ahead <= 0) wait_vmcnt<0>();
-        else if (ahead == 1) wait_vmcnt<P::kPieces>();
-        else wait_vmcnt<2 * P::kPieces>();
+        else if (ahead == 1) wait_vmcnt<G::kPieces>();
+        else wait_vmcnt<2 * G::kPieces>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
-        const char* sb = smem + (t % S) * P::kStageBytes;
+        const char* sb = smem + (t % S) * G::kStageBytes;
 #pragma unroll
-        for (int ks = 0; ks < P::KS; ++ks) {
+        for (int ks = 0; ks < G::KS; ++ks) {
             bf16x8 b[4];
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * P::kRowBytes);
+            for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
 #pragma unroll
             for (int mb = 0; mb < 8; ++mb) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * P::kRowBytes);
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * G::kRowBytes);
 #pragma unroll
                 for (int nb = 0; nb < 4; ++nb)
                     acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[nb], acc[mb][nb], 0, 0, 0);
@@ -165,19 +175,20 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
             for (int i = 0; i < 4; ++i) {
                 const int r = wm * 128 + mb * 16 + (lane >> 4) * 4 + i;
                 const int c = wn * 64 + nb * 16 + (lane & 15);
-                *reinterpret_cast<uint16_t*>(smem + img_off(r, c >> 3) + (c & 7) * 2) = f32_to_bf16(acc[mb][nb][i]);
+                *reinterpret_cast<uint16_t*>(smem + G::img_off(r, c >> 3) + (c & 7) * 2) = f32_to_bf16(acc[mb][nb][i]);
             }
     __syncthreads();
 
     if constexpr (EPI == EPI_STORE) {
         const bool vec = (ldz & 7) == 0 && (reinterpret_cast<uintptr_t>(Z) & 15) == 0;
+        constexpr int kIters = BM * G::kCpr / G::NT;
 #pragma unroll 4
-        for (int it = 0; it < 16; ++it) {
-            const int lin = it * NT + threadIdx.x;
-            const int r = lin >> 5, c = lin & 31;
+        for (int it = 0; it < kIters; ++it) {
+            const int lin = it * G::NT + threadIdx.x;
+            const int r = lin / G::kCpr, c = lin % G::kCpr;
             const int grow = m0 + r, col = n0 + c * 8;
             if (grow >= M || col >= N) continue;
-            const uint4 v = *reinterpret_cast<const uint4*>(smem + img_off(r, c));
+            const uint4 v = *reinterpret_cast<const uint4*>(smem + G::img_off(r, c));
             uint16_t* dst = Z + (int64_t)grow * ldz + col;
             if (vec && col + 8 <= N) {
                 *reinterpret_cast<uint4*>(dst) = v;
@@ -190,23 +201,22 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
         return;
     } else {
         constexpr bool greedy = EPI == EPI_GREEDY;
-        const int r = threadIdx.x >> 1, hh = threadIdx.x & 1;
+        constexpr int TPR = G::TPR, NC = G::kChunksPerThread;
+        const int r = threadIdx.x / TPR, hh = threadIdx.x % TPR;
         const int grow = m0 + r;
-        if (grow >= M) return;  // both threads of a row leave together (the pair shuffle below)
-        // thread hh owns chunks 2i + hh, i = 0..15 (ascending columns); the image swizzle makes a
-        // 16-lane read group (8 rows x 2 parities) hit 16 distinct bank slots
-        uint4 pk[16];
-        float vmx[16];
+        if (grow >= M) return;  // the threads of a row leave together (the row shuffle below)
+        uint4 pk[NC];
+        float vmx[NC];
         float m = -1e30f, s = 0.f;   // raw online (max, sum-exp)
         float xbest = -INFINITY;     // this thread's largest logit, first occurrence
         int ibest = 0x7fffffff;
         // pass 1: LSE, per-vector max and the thread's argmax (the greedy answer)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int c = 2 * i + hh;
+        for (int i = 0; i < NC; ++i) {
+            const int c = TPR * i + hh;
             const int v0 = n0 + c * 8;
             const int cnt = min(8, N - v0);
-            pk[i] = *reinterpret_cast<const uint4*>(smem + img_off(r, c));
+            pk[i] = *reinterpret_cast<const uint4*>(smem + G::img_off(r, c));
             float x[8];
             const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
 #pragma unroll
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
             const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
             const float temp = 1.0f / inv_t;
             const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-            // bar: the exact score of the thread's largest logit, raised to the row pair's best
+            // bar: the exact score of the thread's largest logit, raised to the row's best
             best_s = -INFINITY;
             best_i = 0x7fffffff;
             if (ibest != 0x7fffffff) {
@@ -251,13 +261,17 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
                 best_s = noise_score(xbest, inv_t, ibest, h, group_min_e(h), key2);
                 best_i = ibest;
             }
-            const float bar = fmaxf(best_s, __shfl_xor(best_s, 1, kWave));
-            const float thr = (bar - kNoiseC) * temp;
-            // pass 2: candidate elements (group bound vs the bar) as a 128-bit mask, bit 8 i + k
-            uint32_t cm[4] = {0u, 0u, 0u, 0u};
+            float bar = best_s;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int v0 = n0 + (2 * i + hh) * 8;
+            for (int o = 1; o < TPR; o <<= 1) bar = fmaxf(bar, __shfl_xor(bar, o, kWave));
+            const float thr = (bar - kNoiseC) * temp;
+            // pass 2: candidate elements (group bound vs the bar) as a bit mask, bit 8 i + k
+            uint32_t cm[NC / 4];
+#pragma unroll
+            for (int j = 0; j < NC / 4; ++j) cm[j] = 0u;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                const int v0 = n0 + (TPR * i + hh) * 8;
                 const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
                 const float bits = noise_bits(h);
                 if (fmaf(bits, -kT, vmx[i]) - thr < 0.f) continue;  // no element of the group reaches the bar
@@ -272,17 +286,17 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
                 cm[i >> 2] |= bm << ((i & 3) * 8);
             }
             // exact scores of the candidates, one per lane per trip (the wave loops max-count times,
-            // not 16 x 8 divergent slots)
+            // not NC x 8 divergent slots)
 #pragma unroll
-            for (int wd = 0; wd < 4; ++wd) {
+            for (int wd = 0; wd < NC / 4; ++wd) {
                 uint32_t bm = cm[wd];
                 while (bm) {
                     const int b = __builtin_ctz(bm);
                     bm &= bm - 1u;
                     const int i = wd * 4 + (b >> 3), k = b & 7;
-                    const int c = 2 * i + hh;
+                    const int c = TPR * i + hh;
                     const int v = n0 + c * 8 + k;
-                    const float xk = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + img_off(r, c) + k * 2));
+                    const float xk = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + G::img_off(r, c) + k * 2));
                     const uint32_t h = ehash(key, keyb, (uint32_t)v >> 3);
                     const float sc = noise_score(xk, inv_t, v, h, group_min_e(h), key2);
                     if (better(sc, v, Best{best_s, best_i})) {
@@ -293,17 +307,18 @@ __global__ __launch_bounds__(NT, 1) void lmhead_gemm_kernel(
                 }
             }
         }
-        // the row's two threads are lanes 2j, 2j + 1
-        {
-            const float os = __shfl_xor(best_s, 1, kWave);
-            const int oi = __shfl_xor(best_i, 1, kWave);
-            const float ox = __shfl_xor(best_x, 1, kWave);
+        // fold the row's TPR threads (adjacent lanes)
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) {
+            const float os = __shfl_xor(best_s, o, kWave);
+            const int oi = __shfl_xor(best_i, o, kWave);
+            const float ox = __shfl_xor(best_x, o, kWave);
             if (better(os, oi, Best{best_s, best_i})) {
                 best_s = os;
                 best_i = oi;
                 best_x = ox;
             }
-            const float om = __shfl_xor(m, 1, kWave), oss = __shfl_xor(s, 1, kWave);
+            const float om = __shfl_xor(m, o, kWave), oss = __shfl_xor(s, o, kWave);
             const float mn = fmaxf(m, om);
             s = s * fast_exp2((m - mn) * kLog2eG) + oss * fast_exp2((om - mn) * kLog2eG);
             m = mn;
@@ -360,12 +375,13 @@ inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
                             float, uint64_t, const int64_t*, int64_t, float4*, float*, int);
+int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }
 template <int EPI>
 GemmKernel pick_kernel() {
     switch (g_lmhead_pipe) {
-        case 1: return lmhead_gemm_kernel<EPI, 32, 4>;
-        case 2: return lmhead_gemm_kernel<EPI, 32, 3>;
-        default: return lmhead_gemm_kernel<EPI, 64, 2>;
+        case 1: return lmhead_gemm_kernel<EPI, 128, 32, 3>;
+        case 2: return lmhead_gemm_kernel<EPI, 256, 32, 4>;
+        default: return lmhead_gemm_kernel<EPI, 256, 64, 2>;
     }
 }
 
@@ -382,8 +398,8 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }  // namespace
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: lmhead_pipe must be 0, 1 or 2");
-    g_lmhead_pipe = value;
+    SKYRL_REQUIRE(value >= -1 && value <= 2, "skyrl_tune: lmhead_pipe must be -1 (default), 0, 1 or 2");
+    g_lmhead_pipe = value < 0 ? 1 : value;
     return SKYRL_OK;
 }
 }  // namespace skyrl
@@ -396,8 +412,8 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
     if (rc) return rc;
     if (M == 0) return SKYRL_OK;
     SKYRL_REQUIRE(out && ld_out >= N, "lmhead_gemm: bad output");
-    const int mt = tiles(M, BM), nt = tiles(N, BN);
-    hipLaunchKernelGGL(pick_kernel<EPI_STORE>(), dim3(mt * nt), dim3(NT), 0, as_stream(stream),
+    const int bn = tile_n(), mt = tiles(M, BM), nt = tiles(N, bn);
+    hipLaunchKernelGGL(pick_kernel<EPI_STORE>(), dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream),
                        reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
                        ld_weight, M, N, K, mt, reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
                        nullptr, nullptr, nt);
@@ -405,7 +421,7 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
 }
 
 extern "C" size_t skyrl_lmhead_sample_workspace_bytes(int32_t M, int32_t V) {
-    const size_t n = (size_t)(M > 0 ? M : 1) * tiles(V > 0 ? V : 1, BN);
+    const size_t n = (size_t)(M > 0 ? M : 1) * tiles(V > 0 ? V : 1, 128);  // the smallest tile width
     return n * sizeof(float4) + n * sizeof(float) + 256;
 }
 
@@ -419,13 +435,13 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     SKYRL_REQUIRE(tokens_out && workspace, "lmhead_sample: null pointer");
     SKYRL_REQUIRE(temperature >= 0.f, "lmhead_sample: temperature must be >= 0");
     SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_sample: workspace must be 16-B aligned");
-    const int mt = tiles(M, BM), nt = tiles(V, BN);
+    const int bn = tile_n(), mt = tiles(M, BM), nt = tiles(V, bn);
     float4* parts = reinterpret_cast<float4*>(workspace);
     float* part_x = reinterpret_cast<float*>(parts + (size_t)M * nt);
     const bool greedy = temperature == 0.f;
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
     auto kern = greedy ? pick_kernel<EPI_GREEDY>() : pick_kernel<EPI_SAMPLE>();
-    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(NT), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
+    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt, nullptr, 0ll, inv_t,
                        seed, seq_ids, step, parts, part_x, nt);
     rc = check_launch("lmhead_gemm_kernel<sample>");

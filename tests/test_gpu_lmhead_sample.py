@@ -36,7 +36,8 @@ def test_gemm_exact_small_integers(dev, M, V, K):
 @pytest.mark.parametrize("pipe", [0, 1, 2])
 @pytest.mark.parametrize("K", [64, 128, 192, 1536])
 def test_gemm_pipeline_variants_exact(dev, pipe, K):
-    """Every K pipeline (BK 64 x 2 stages, BK 32 x 4 / x 3) incl. fewer K tiles than stages."""
+    """Every tile/pipeline variant (256x256 BK 64 x 2 stages, 256x128 BK 32 x 3, 256x256 BK 32 x 4),
+    incl. fewer K tiles than stages."""
     from skyrl_amd import _ffi
 
     g = torch.Generator().manual_seed(K + pipe)
@@ -47,7 +48,7 @@ def test_gemm_pipeline_variants_exact(dev, pipe, K):
         z = ops.lmhead_gemm(h.to(dev), w.to(dev))
         tf, _ = ops.lmhead_sample(h.to(dev), w.to(dev), seed=3, step=1)
     finally:
-        _ffi.call("skyrl_tune", b"lmhead_pipe", 0)
+        _ffi.call("skyrl_tune", b"lmhead_pipe", -1)
     assert torch.equal(z.cpu(), (h.float() @ w.float().T).to(torch.bfloat16))
     tu, _ = ops.sample(z, seed=3, step=1)
     assert torch.equal(tf, tu)
