@@ -79,7 +79,7 @@ __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)
 // skyrl_tune("lmhead_pipe"): 0 = 256 x 256 tiles, BK 64, 2 stages, one 512-thread workgroup per CU;
 // 1 = 256 x 128 tiles, BK 32, 3 stages, two 256-thread workgroups per CU (one's epilogue
 // overlaps the other's MFMA loop); 2 = 256 x 256, BK 32, 4 stages.
-int g_lmhead_pipe = 1;
+int g_lmhead_pipe = 0;
 
 template <int EPI, int BN, int BKT, int S>
 __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
@@ -206,11 +206,19 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         const int grow = m0 + r;
         if (grow >= M) return;  // the threads of a row leave together (the row shuffle below)
         uint4 pk[NC];
-        float vmx[NC];
         float m = -1e30f, s = 0.f;   // raw online (max, sum-exp)
-        float xbest = -INFINITY;     // this thread's largest logit, first occurrence
-        int ibest = 0x7fffffff;
-        // pass 1: LSE, per-vector max and the thread's argmax (the greedy answer)
+        float best_s = -INFINITY, best_x = -INFINITY;
+        int best_i = 0x7fffffff;
+        float lng[NC], slack[NC];    // per group: -ln E_g and the non-min-slot bound slack
+        uint32_t key = 0u, key2 = 0u, keyb = 0u;
+        if constexpr (!greedy) {
+            key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
+            key2 = noise_key2(key);
+            keyb = noise_keyb(key);
+        }
+        // pass 1, every group: LSE; greedy: the first maximum; sampling: the exact score of the
+        // group's minimum-E slot p = h & 7 (its E is E_g itself, so the score needs no per-element
+        // hash) -- the best of those is the bar for everything else
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
             const int c = TPR * i + hh;
@@ -229,64 +237,73 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
             float vmax = x[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) vmax = fmaxf(vmax, x[k]);
-            vmx[i] = vmax;
-            if (cnt > 0) {
+            lng[i] = 0.f;
+            slack[i] = 0.f;
+            if (cnt <= 0) continue;
+            {
                 const float mn = fmaxf(m, vmax);
                 float acc_e = 0.f;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) acc_e += fast_exp2((x[k] - mn) * kLog2eG);
                 s = s * fast_exp2((m - mn) * kLog2eG) + acc_e;
                 m = mn;
-                if (vmax > xbest) {
+            }
+            if constexpr (greedy) {
+                if (vmax > best_s) {
                     int kk = 7;
 #pragma unroll
                     for (int k = 6; k >= 0; --k) kk = (x[k] == vmax) ? k : kk;
-                    xbest = vmax;
-                    ibest = v0 + kk;
+                    best_s = vmax;
+                    best_i = v0 + kk;
+                    best_x = vmax;
+                }
+            } else {
+                const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+                const int p = (int)(h & 7u);
+                const float Eg = group_min_e(h);
+                const float L = -det_ln(Eg);
+                lng[i] = L;
+                // a non-min slot's E = E_g + (-det_ln U) >= E_g - 1.2e-6 (det_ln error), so its exact
+                // score is <= x inv_t + L + 1.4e-6 / E_g + 4e-6 (det_ln and rounding errors); slack is
+                // generous on both, and infinite (every slot a candidate) when E_g is too small for it
+                slack[i] = Eg < 1e-5f ? INFINITY : 1e-4f + 4e-6f / Eg;
+                float xp = x[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k) xp = (k == p) ? x[k] : xp;
+                if (p < cnt) {
+                    const float sc = xp * inv_t + L;  // = noise_score(xp, inv_t, v0 + p, h, Eg, key2)
+                    if (better(sc, v0 + p, Best{best_s, best_i})) {
+                        best_s = sc;
+                        best_i = v0 + p;
+                        best_x = xp;
+                    }
                 }
             }
         }
-        float best_s = xbest, best_x = xbest;
-        int best_i = ibest;
         if constexpr (!greedy) {
-            const uint32_t key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
-            const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
-            const float temp = 1.0f / inv_t;
-            const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-            // bar: the exact score of the thread's largest logit, raised to the row's best
-            best_s = -INFINITY;
-            best_i = 0x7fffffff;
-            if (ibest != 0x7fffffff) {
-                const uint32_t h = ehash(key, keyb, (uint32_t)ibest >> 3);
-                best_s = noise_score(xbest, inv_t, ibest, h, group_min_e(h), key2);
-                best_i = ibest;
-            }
             float bar = best_s;
 #pragma unroll
             for (int o = 1; o < TPR; o <<= 1) bar = fmaxf(bar, __shfl_xor(bar, o, kWave));
-            const float thr = (bar - kNoiseC) * temp;
-            // pass 2: candidate elements (group bound vs the bar) as a bit mask, bit 8 i + k
+            // pass 2: non-min slots whose bound reaches the bar, as a bit mask (bit 8 i + k)
             uint32_t cm[NC / 4];
 #pragma unroll
             for (int j = 0; j < NC / 4; ++j) cm[j] = 0u;
 #pragma unroll
             for (int i = 0; i < NC; ++i) {
                 const int v0 = n0 + (TPR * i + hh) * 8;
-                const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
-                const float bits = noise_bits(h);
-                if (fmaf(bits, -kT, vmx[i]) - thr < 0.f) continue;  // no element of the group reaches the bar
                 const int cnt = min(8, N - v0);
                 const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
+                const float lim = bar - lng[i] - slack[i];  // x inv_t >= lim can reach the bar
                 uint32_t bm = 0u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const float xk = __uint_as_float((k & 1) ? (wds[k >> 1] & 0xffff0000u) : (wds[k >> 1] << 16));
-                    if (k < cnt && !(fmaf(bits, -kT, xk) - thr < 0.f)) bm |= 1u << k;
+                    if (k < cnt && !(xk * inv_t < lim)) bm |= 1u << k;
                 }
                 cm[i >> 2] |= bm << ((i & 3) * 8);
             }
-            // exact scores of the candidates, one per lane per trip (the wave loops max-count times,
-            // not NC x 8 divergent slots)
+            // exact scores of the candidates, one per lane per trip (the min slot re-scores to the
+            // value pass 1 already has: harmless)
 #pragma unroll
             for (int wd = 0; wd < NC / 4; ++wd) {
                 uint32_t bm = cm[wd];
@@ -399,7 +416,7 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 
 int lmhead_tune(int value) {
     SKYRL_REQUIRE(value >= -1 && value <= 2, "skyrl_tune: lmhead_pipe must be -1 (default), 0, 1 or 2");
-    g_lmhead_pipe = value < 0 ? 1 : value;
+    g_lmhead_pipe = value < 0 ? 0 : value;
     return SKYRL_OK;
 }
 }  // namespace skyrl

@@ -70,29 +70,86 @@ SCRIPTS = {
 }
 
 
+# the reply once a session's script is exhausted (the re-tokenizing mode checks the input length
+# before adding a turn, so a length-cut trajectory asks for one more turn)
+EXTRA_TURN = ("<think>more</think><solution>SELECT 1</solution>", "stop", False)
+
+
 class ScriptedClient:
     """InferenceEngineClient stand-in: per session id, returns the next scripted turn (token ids
-    through the shared tokenizer; eos appended when the script says the engine stopped on it)."""
+    through the shared tokenizer; eos appended when the script says the engine stopped on it).
+    Text-in requests ("prompts": conversations, the batched generator) are answered per
+    conversation with the first turn of the script named by the last message's "<name>:" prefix.
+    logprobs=False leaves response_logprobs out, as an engine asked for no logprobs does."""
 
-    def __init__(self, tokenizer):
+    def __init__(self, tokenizer, logprobs=True):
         self.tok = tokenizer
         self.turn = {}
         self.prompts = []
+        self.logprobs = logprobs
+
+    def _reply(self, text, reason, with_eos):
+        ids = self.tok.encode(text, add_special_tokens=False)
+        if with_eos:
+            ids = ids + [self.tok.eos_token_id]
+            text = text + self.tok.eos_token
+        return text, ids, reason, [-0.01 * (i + 1) for i in range(len(ids))]
 
     async def generate(self, inp):
+        if inp.get("prompts") is not None:
+            outs = []
+            for conv in inp["prompts"]:
+                name = conv[-1]["content"].split(":")[0].split()[-1]
+                self.prompts.append((name, [m["content"] for m in conv]))
+                outs.append(self._reply(*SCRIPTS[f"{name}_0"][0]))
+            res = {"responses": [o[0] for o in outs], "response_ids": [o[1] for o in outs],
+                   "stop_reasons": [o[2] for o in outs]}
+            if self.logprobs:
+                res["response_logprobs"] = [o[3] for o in outs]
+            return res
         sid = inp["session_ids"][0]
         k = self.turn.get(sid, 0)
         self.turn[sid] = k + 1
-        text, reason, with_eos = SCRIPTS[sid][k]
+        script = SCRIPTS[sid]
+        text, reason, with_eos = script[k] if k < len(script) else EXTRA_TURN
         self.prompts.append((sid, list(inp["prompt_token_ids"][0])))
-        ids = self.tok.encode(text, add_special_tokens=False)
-        out_text = text
-        if with_eos:
-            ids = ids + [self.tok.eos_token_id]
-            out_text = text + self.tok.eos_token
-        lps = [-0.01 * (i + 1) for i in range(len(ids))]
-        return {"responses": [out_text], "response_ids": [ids], "stop_reasons": [reason],
-                "response_logprobs": [lps]}
+        out_text, ids, reason, lps = self._reply(text, reason, with_eos)
+        res = {"responses": [out_text], "response_ids": [ids], "stop_reasons": [reason]}
+        if self.logprobs:
+            res["response_logprobs"] = [lps]
+        return res
+
+
+# generator-mode cases beyond the two chat modes (tools/gen_golden_agent.py MODE_CASES):
+#   name -> GeneratorConfig overrides, whether the engine returns logprobs, scenario subset
+MODE_CASES = {
+    "retokenize_qwen3_without_thinking": (dict(use_conversation_multi_turn=True,
+                                               chat_template={"source": "name",
+                                                              "name_or_path": "qwen3_without_thinking"}),
+                                          False, "all"),
+    "retokenize_qwen3_with_thinking": (dict(use_conversation_multi_turn=True,
+                                            chat_template={"source": "name", "name_or_path": "qwen3_with_thinking"}),
+                                       False, "all"),
+    "custom_template_single_turn_chat": (dict(use_conversation_multi_turn=False,
+                                              chat_template={"source": "name",
+                                                             "name_or_path": "qwen3_without_thinking"}),
+                                         False, "all"),
+    "step_wise": (dict(use_conversation_multi_turn=True, step_wise_trajectories=True), True, "all"),
+    "step_wise_flags": (dict(use_conversation_multi_turn=True, step_wise_trajectories=True,
+                             zero_reward_on_non_stop=True, apply_overlong_filtering=True), True, "all"),
+    "batched": (dict(batched=True, use_conversation_multi_turn=False), True, "single_turn"),
+    "batched_overlong": (dict(batched=True, use_conversation_multi_turn=False, apply_overlong_filtering=True),
+                         True, "single_turn"),
+}
+
+
+def scenario_subset(multi_turn, subset):
+    prompts, classes, extras, tids = scenario(multi_turn)
+    if subset == "single_turn":  # the GSM8K trajectories (one turn each)
+        keep = [i for i, c in enumerate(classes) if c == "gsm8k"]
+        return ([prompts[i] for i in keep], [classes[i] for i in keep], [extras[i] for i in keep],
+                [tids[i] for i in keep])
+    return prompts, classes, extras, tids
 
 
 def scenario(multi_turn):

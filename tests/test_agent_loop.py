@@ -90,3 +90,54 @@ def test_sql_env_turns_and_validation(tmp_path):
     with pytest.raises(FileNotFoundError):
         make("text2sql", env_config={"db_path": root},
              extras={"db_id": "missing", "data": "spider", "reward_spec": {"ground_truth": "x"}})
+
+
+MODES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "agent_loop_modes.json")
+
+
+@pytest.mark.parametrize("name", sorted(af.MODE_CASES))
+def test_generator_modes_match_reference(name):
+    """Re-tokenized chat history (custom chat templates, incl. the single-assistant-message chat
+    with a custom template), step-wise trajectories and the batched single-call mode against the
+    reference generator's outputs on the same scripted scenario (tests/golden/agent_loop_modes.json)."""
+    with open(MODES) as f:
+        g = json.load(f)
+    exp = g["cases"][name]
+    over, with_lp, subset = af.MODE_CASES[name]
+    af.make_sql_root(g["db_root"])
+    tok = af.make_tokenizer()
+    cfg = GeneratorConfig(max_turns=3, max_input_length=g["max_input_length"],
+                          sampling_params=SamplingParams(max_generate_length=64, logprobs=0 if with_lp else None,
+                                                         stop=["</sql>", "</solution>"]), **over)
+    client = af.ScriptedClient(tok, logprobs=with_lp)
+    gen = SkyRLGymGenerator(cfg, {"text2sql": {"db_path": g["db_root"]}}, client, tok)
+    prompts, classes, extras, tids = af.scenario_subset(cfg.use_conversation_multi_turn, subset)
+    out = asyncio.run(gen.generate({"prompts": prompts, "env_classes": classes, "env_extras": extras,
+                                    "sampling_params": None,
+                                    "trajectory_ids": [TrajectoryID(a, b) for a, b in tids]}))
+    for key in ("prompt_token_ids", "response_ids", "rewards", "loss_masks", "stop_reasons", "rollout_logprobs",
+                "is_last_step"):
+        assert out.get(key) == exp[key], key
+    assert ("trajectory_ids" in out) == exp["has_trajectory_keys"]
+    got_tids = [t.to_string() for t in out["trajectory_ids"]] if out.get("trajectory_ids") is not None else None
+    assert got_tids == exp["trajectory_ids"]
+    assert sorted(client.prompts) == [tuple(x) for x in exp["engine_prompts"]]
+    for k, v in exp["rollout_metrics"].items():
+        assert out["rollout_metrics"][k] == pytest.approx(v, abs=1e-9), k
+
+
+def test_generator_mode_validation():
+    tok = af.make_tokenizer()
+    sp = SamplingParams(max_generate_length=8)
+    with pytest.raises(ValueError, match="batched"):
+        SkyRLGymGenerator(GeneratorConfig(step_wise_trajectories=True, batched=True, sampling_params=sp), {}, None, tok)
+    with pytest.raises(ValueError, match="custom chat template"):
+        SkyRLGymGenerator(GeneratorConfig(step_wise_trajectories=True, sampling_params=sp,
+                                          chat_template={"source": "name", "name_or_path": "qwen3_with_thinking"}),
+                          {}, None, tok)
+    with pytest.raises(ValueError, match="use_conversation_multi_turn"):
+        SkyRLGymGenerator(GeneratorConfig(step_wise_trajectories=True, use_conversation_multi_turn=False,
+                                          sampling_params=sp), {}, None, tok)
+    with pytest.raises(ValueError, match="not found"):
+        SkyRLGymGenerator(GeneratorConfig(chat_template={"source": "name", "name_or_path": "nope"},
+                                          sampling_params=sp), {}, None, tok)

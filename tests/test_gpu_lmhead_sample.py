@@ -158,3 +158,30 @@ def test_lmhead_rejects_bad_operands(dev):
         ops.lmhead_gemm(h, w)
     with pytest.raises(TypeError):
         ops.lmhead_gemm(h.float(), w)
+
+
+@pytest.mark.parametrize("temp", [1.0, 0.7, 0.0])
+def test_fused_sample_many_rows_steps_and_ties(dev, temp):
+    """512 rows x 3 steps at the config-2 shape (every noise-bound branch, incl. groups whose
+    E_g is tiny, occurs), and logits with few distinct values (exact ties in x and in score order
+    are broken by the lowest index, as the unfused sampler does)."""
+    V, K = 151936, 1536
+    h, w, ids = _case(512, V, K, 1234)
+    hd, wd, idd = h.to(dev), w.to(dev), ids.to(dev)
+    z = ops.lmhead_gemm(hd, wd)
+    for step in (0, 1, 999):
+        tu, lu = ops.sample(z, temperature=temp, seed=9, seq_ids=idd, step=step)
+        tf, lf = ops.lmhead_sample(hd, wd, temperature=temp, seed=9, seq_ids=idd, step=step)
+        assert torch.equal(tf.cpu(), tu.cpu())
+        torch.testing.assert_close(lf.cpu(), lu.cpu(), atol=1e-4, rtol=1e-5)
+    g = torch.Generator().manual_seed(3)
+    hq = torch.ones(64, 64, dtype=torch.bfloat16)
+    hq[:, 1:] = 0
+    wq = torch.zeros(4099, 64, dtype=torch.bfloat16)
+    wq[:, 0] = torch.randint(-2, 3, (4099,), generator=g).to(torch.bfloat16)  # logits in {-2..2}
+    hd, wd = hq.to(dev), wq.to(dev)
+    z = ops.lmhead_gemm(hd, wd)
+    ids = torch.arange(64, device=dev)
+    tu, _ = ops.sample(z, temperature=temp, seed=4, seq_ids=ids, step=0)
+    tf, _ = ops.lmhead_sample(hd, wd, temperature=temp, seed=4, seq_ids=ids, step=0)
+    assert torch.equal(tf.cpu(), tu.cpu())

@@ -62,6 +62,39 @@ def main():
         json.dump(out, f)
     print(f"wrote {path}")
 
+    # the other generator modes: re-tokenized chat history (custom chat templates), step-wise
+    # trajectories, the batched single-call mode (tests/agent_fixtures.py MODE_CASES)
+    from skyrl_train.config.config import ChatTemplateConfig
+
+    modes = {"db_root": DB_ROOT, "max_input_length": MAX_INPUT, "cases": {}}
+    for name, (over, with_lp, subset) in af.MODE_CASES.items():
+        tok = af.make_tokenizer()
+        over = dict(over)
+        if "chat_template" in over:
+            over["chat_template"] = ChatTemplateConfig(**over["chat_template"])
+        cfg = GeneratorConfig(max_turns=3, max_input_length=MAX_INPUT,
+                              sampling_params=SamplingParams(max_generate_length=64, logprobs=0 if with_lp else None,
+                                                             stop=["</sql>", "</solution>"]), **over)
+        env_cfg = SkyRLGymConfig(max_env_workers=0, text2sql=Text2SQLEnvConfig(db_path=DB_ROOT))
+        client = af.ScriptedClient(tok, logprobs=with_lp)
+        gen = SkyRLGymGenerator(cfg, env_cfg, client, tok, model_name="scripted")
+        prompts, classes, extras, tids = af.scenario_subset(cfg.use_conversation_multi_turn, subset)
+        res = asyncio.run(gen.generate({"prompts": prompts, "env_classes": classes, "env_extras": extras,
+                                        "sampling_params": None,
+                                        "trajectory_ids": [TrajectoryID(a, b) for a, b in tids]}, disable_tqdm=True))
+        rec = {k: res.get(k) for k in ("prompt_token_ids", "response_ids", "rewards", "loss_masks", "stop_reasons",
+                                      "rollout_logprobs", "is_last_step")}
+        rec["trajectory_ids"] = ([t.to_string() for t in res["trajectory_ids"]]
+                                 if res.get("trajectory_ids") is not None else None)
+        rec["has_trajectory_keys"] = "trajectory_ids" in res
+        rec["rollout_metrics"] = {k: float(v) for k, v in res["rollout_metrics"].items()}
+        rec["engine_prompts"] = sorted(client.prompts)
+        modes["cases"][name] = rec
+    path = os.path.join(ROOT, "tests", "golden", "agent_loop_modes.json")
+    with open(path, "w") as f:
+        json.dump(modes, f)
+    print(f"wrote {path}")
+
 
 if __name__ == "__main__":
     main()
