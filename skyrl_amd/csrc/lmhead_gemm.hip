@@ -78,7 +78,9 @@ __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)
 
 // skyrl_tune("lmhead_pipe"): 0 = 256 x 256 tiles, BK 64, 2 stages, one 512-thread workgroup per CU;
 // 1 = 256 x 128 tiles, BK 32, 3 stages, two 256-thread workgroups per CU (one's epilogue
-// overlaps the other's MFMA loop); 2 = 256 x 256, BK 32, 4 stages.
+// overlaps the other's MFMA loop); 2 = 256 x 256, BK 32, 4 stages. Measured at the config-2
+// decode shape (512 x 151,936 x 1536): 0 is fastest (260-276 us), 1 313 us, 2 284 us. (Spreading
+// the copies over the MFMA groups with sched_group_barrier produced a worse schedule: dropped.)
 int g_lmhead_pipe = 0;
 
 template <int EPI, int BN, int BKT, int S>
@@ -146,8 +148,8 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         else wait_vmcnt<2 * G::kPieces>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
         const char* sb = smem + (t % S) * G::kStageBytes;
+        if (t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
             bf16x8 b[4];

@@ -452,11 +452,22 @@ class ModelRunner:
     BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 192, 256, 384, 512, 768, 1024)
 
     def __init__(self, model, num_blocks: int, max_num_seqs: int, seed: int = 0, use_graphs: bool = True,
-                 tunable_gemm: Optional[str] = None):
+                 tunable_gemm: Optional[str] = None, fused_lmhead: str = "greedy"):
         # tunable_gemm: a results-file path enables PyTorch TunableOp (runtime GEMM solution search)
         # around this runner's forwards only; the decode buckets' skinny GEMMs gain most (measured
         # 3.28 -> 2.32 ms per 28-layer decode step at 8 rows, `scripts/probe/tunable_probe.py`).
         self.tunable_gemm = tunable_gemm
+        # fused_lmhead: when the lm_head GEMM runs with the sampler in its epilogue
+        # (skyrl_lmhead_sample, csrc/lmhead_gemm.hip; no [n, V] logits in HBM) instead of a library
+        # GEMM + skyrl_sample. "greedy" (default): batches that are all T = 0 without filters or
+        # suppressed ids (measured 268 vs 294 us at 512 x 151,936 x 1536); "always": every
+        # unfiltered single-parameter batch (at T = 1 the exact per-tile noise evaluation makes it
+        # 338 vs 319 us, profiles/r02_lmhead_sample_bench.json); "off".
+        if fused_lmhead not in ("greedy", "always", "off"):
+            raise ValueError(f"fused_lmhead must be 'greedy', 'always' or 'off', got {fused_lmhead!r}")
+        fits = model.spec.hidden_size % 64 == 0 and str(getattr(model, "dtype", "")) == "torch.bfloat16"
+        self.fused_lmhead = fused_lmhead if fits else "off"
+        self.fused_steps = 0  # decode/prefill steps sampled by the fused kernel
         import torch
 
         self.torch = torch
@@ -526,8 +537,8 @@ class ModelRunner:
                           block_tables=self.d_i32[:nb], context_lens=self.d_ctx[:nb], max_ctx=max_ctx or 0,
                           nparts=nparts)
 
-    def _forward_logits(self, inp):
-        return self.model.logits(self.model.forward_decode(inp, self.cache))
+    def _forward_hidden(self, inp):
+        return self.model.forward_decode(inp, self.cache)
 
     def _graph(self, nb: int):
         g = self._graphs.get(nb)
@@ -546,14 +557,14 @@ class ModelRunner:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
-            self._forward_logits(inp)  # warm-up outside capture (library handles, workspaces)
+            self._forward_hidden(inp)  # warm-up outside capture (library handles, workspaces)
         torch.cuda.current_stream(self.device).wait_stream(side)
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, pool=self._pool):
-            logits = self._forward_logits(inp)
-        self._graphs[nb] = (graph, logits)
+            hidden = self._forward_hidden(inp)
+        self._graphs[nb] = (graph, hidden)
         return self._graphs[nb]
 
     def _stage_decode(self, reqs: List["Request"], nb: int) -> None:
@@ -616,7 +627,7 @@ class ModelRunner:
                 bt = self._h2d(bt_np)
             inp = StepInputs(tokens=packed[:T], positions=packed[T:2 * T], slots=packed[2 * T:], seq_lens=lens,
                              cached_lens=cached, block_tables=bt)
-            logits = self.model.logits(self.model.forward_prefill(inp, self.cache))
+            hidden = self.model.forward_prefill(inp, self.cache)
             for r in reqs:
                 self._nblk[r.row] = 0  # (re)admitted row: restage its whole table
             rows = np.arange(n)
@@ -625,30 +636,45 @@ class ModelRunner:
             nb = next(b for b in self.buckets if b >= hi)
             self._stage_decode(reqs, nb)
             if self.use_graphs:
-                graph, logits = self._graph(nb)
+                graph, hidden = self._graph(nb)
                 graph.replay()
             else:
                 inp = self._decode_inputs(nb, fixed=False)
                 inp.max_ctx = int(max(r.num_tokens for r in reqs))
-                logits = self._forward_logits(inp)
+                hidden = self._forward_hidden(inp)
             rows = np.fromiter((r.row for r in reqs), dtype=np.int64, count=n)
-        return self._sample(logits, batch, rows)
+        return self._sample(hidden, batch, rows)
 
-    def _sample(self, logits, batch: ScheduledBatch, rows: np.ndarray):
+    def _fused_ok(self, groups, batch: ScheduledBatch) -> bool:
+        if self.fused_lmhead == "off" or len(groups) != 1 or any(batch.suppress):
+            return False
+        temp, top_k, top_p, min_p = next(iter(groups))
+        unfiltered = (top_k is None or top_k < 0) and (top_p is None or top_p >= 1.0) and not min_p
+        return unfiltered and (temp == 0.0 or self.fused_lmhead == "always")
+
+    def _sample(self, hidden, batch: ScheduledBatch, rows: np.ndarray):
         torch = self.torch
-        from .. import _ffi
+        from .. import _ffi, ops
         from ..ops import _ptr, _stream
 
-        nb, V = logits.shape
-        for r_i, ids in zip(rows.tolist(), batch.suppress):
-            if ids:
-                logits[r_i, list(ids)] = float("-inf")
+        nb = hidden.shape[0]
         self.n_keys[:nb] = 0
         self.n_keys[rows] = batch.keys
         self.d_keys[:nb].copy_(self.h_keys[:nb], non_blocking=True)
         groups: Dict[Tuple, List[int]] = {}
         for r_i, r in zip(rows.tolist(), batch.requests):
             groups.setdefault(r.params.sampler_key(), []).append(r_i)
+        if self._fused_ok(groups, batch):  # lm_head GEMM with the sampler in its epilogue
+            temp = next(iter(groups))[0]
+            ops.lmhead_sample(hidden, self.model.lm_head, temperature=float(temp), seed=self.seed,
+                              seq_ids=self.d_keys[:nb], step=0, tokens_out=self.tokens[:nb], logp_out=self.lps[:nb])
+            self.fused_steps += 1
+            return self._fetch(nb, rows)
+        logits = self.model.logits(hidden)
+        V = logits.shape[1]
+        for r_i, ids in zip(rows.tolist(), batch.suppress):
+            if ids:
+                logits[r_i, list(ids)] = float("-inf")
         ws_bytes = _ffi.query("skyrl_sample_workspace_bytes", max(nb, self.max_num_seqs), V)
         if self._sampler_ws is None or self._sampler_ws.numel() < ws_bytes:
             self._sampler_ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
@@ -667,6 +693,10 @@ class ModelRunner:
             if len(groups) != 1:
                 self.tokens.index_copy_(0, idx, to)
                 self.lps.index_copy_(0, idx, lo)
+        return self._fetch(nb, rows)
+
+    def _fetch(self, nb: int, rows: np.ndarray):
+        torch = self.torch
         m = max(nb, int(rows.max()) + 1)
         out = self.h_out[:, :m]
         out[0].copy_(self.tokens[:m], non_blocking=True)
@@ -698,7 +728,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
     def __init__(self, model, num_blocks: Optional[int] = None, max_num_seqs: int = 512,
                  max_prefill_tokens: int = 32768, seed: int = 0, kv_cache_fraction: float = 0.5,
                  tokenizer=None, runner=None, use_graphs: bool = True, enable_prefix_caching: bool = True,
-                 tunable_gemm: Optional[str] = None):
+                 tunable_gemm: Optional[str] = None, fused_lmhead: str = "greedy"):
         self.model = model
         self.tokenizer = tokenizer
         if num_blocks is None:
@@ -713,7 +743,8 @@ class AMDInferenceEngine(InferenceEngineInterface):
         self.num_blocks = num_blocks
         self.runner = runner if runner is not None else ModelRunner(model, num_blocks, max_num_seqs, seed,
                                                                          use_graphs=use_graphs,
-                                                                         tunable_gemm=tunable_gemm)
+                                                                         tunable_gemm=tunable_gemm,
+                                                                         fused_lmhead=fused_lmhead)
         self.core = EngineCore(self.runner, num_blocks, max_num_seqs=max_num_seqs,
                                max_model_len=model.max_model_len, max_prefill_tokens=max_prefill_tokens,
                                eos_token_id=model.spec.eos_token_id, seed=seed,

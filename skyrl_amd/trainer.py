@@ -226,10 +226,15 @@ class GRPOTrainer:
         policy updates. Advances global_step; the caller syncs the engine's weights."""
         cfg, alg = self.cfg, self.cfg.algorithm
         G = cfg.n_samples_per_prompt
-        uids = [str(i // G) for i in range(len(gen["response_ids"]))]
-        gen, metrics = trainer_utils.postprocess_generator_output(gen, uids, G)
+        step_wise = gen.get("is_last_step") is not None
+        if step_wise:  # one sample per turn: a step's group is its trajectory's prompt
+            uids = [t.instance_id for t in gen["trajectory_ids"]]
+        else:
+            uids = [str(i // G) for i in range(len(gen["response_ids"]))]
+        gen, metrics = trainer_utils.postprocess_generator_output(gen, uids, G, step_wise=step_wise)
         data = trainer_utils.convert_to_training_input(gen, uids, self.pad_token_id, dp_size=1,
-                                                       device=next(self.policy.parameters()).device)
+                                                       device=next(self.policy.parameters()).device,
+                                                       step_wise=step_wise)
         self._mark("reward_and_pack")
         # fwd_logprobs_values_reward: old (policy) and ref log-probs, no grad
         data["action_log_probs"] = self._fwd_logprobs(self.policy, data)

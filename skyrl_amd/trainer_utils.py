@@ -90,12 +90,23 @@ def validate_generator_output(num_prompts: int, generator_output: Dict[str, Any]
                 f"Token rewards and response ids must have the same length, for sample {i} got {len(rew)} and {len(resp)}")
 
 
+def _last_steps(generator_output: Dict[str, Any], uids: List[str]):
+    """The last-step samples of step-wise output, for metrics (trainer.py:700-713)."""
+    last = generator_output["is_last_step"]
+    out = {k: [v[i] for i in range(len(v)) if last[i]] for k, v in generator_output.items() if isinstance(v, list)}
+    return out, [u for u, ls in zip(uids, last) if ls]
+
+
 def postprocess_generator_output(generator_output: Dict[str, Any], uids: List[str], n_samples_per_prompt: int,
-                                 zero_variance_filter_enabled: bool = False
+                                 zero_variance_filter_enabled: bool = False, step_wise: bool = False
                                  ) -> Tuple[Dict[str, Any], Dict[str, float]]:
-    """trainer.py:680-757 (non step-wise): response-level rewards go on the last response token;
-    returns (generator_output with per-token rewards, reward metrics)."""
-    m = get_metrics_from_generator_output(generator_output, uids)
+    """trainer.py:680-757: response-level rewards go on the last response token; returns
+    (generator_output with per-token rewards, reward metrics). Step-wise output is measured on
+    each trajectory's last step only."""
+    if step_wise:
+        m = get_metrics_from_generator_output(*_last_steps(generator_output, uids))
+    else:
+        m = get_metrics_from_generator_output(generator_output, uids)
     rewards = generator_output["rewards"]
     responses = generator_output["response_ids"]
     if rewards and isinstance(rewards[0], list):
@@ -203,8 +214,11 @@ def pad_batch(training_input: TrainingInputBatch, dp_size: int) -> TrainingInput
 
 
 def convert_to_training_input(generator_output: Dict[str, Any], uids: List[str], tokenizer, dp_size: int = 1,
-                              device=None, off_policy_correction_enabled: bool = False) -> TrainingInputBatch:
-    """trainer.py:592-666 (non step-wise) with pad_batch fused into the pack kernel."""
+                              device=None, off_policy_correction_enabled: bool = False,
+                              step_wise: bool = False) -> TrainingInputBatch:
+    """trainer.py:592-666 with pad_batch fused into the pack kernel. Step-wise output also
+    carries is_last_step and the trajectory ids (metadata), and its average response length
+    counts last steps only (trainer.py:645-660)."""
     resp = generator_output["response_ids"]
     N = len(resp)
     pad = pad_size_for(N, dp_size)
@@ -227,6 +241,14 @@ def convert_to_training_input(generator_output: Dict[str, Any], uids: List[str],
         "avg_response_length": sum(len(r) for r in resp) / N,
         "pad_size": pad,
     }
+    if step_wise:
+        assert generator_output.get("trajectory_ids") is not None, \
+            "Expected `trajectory_ids` in generator output for step wise training"
+        batch.metadata["trajectory_ids"] = [t.to_string() if hasattr(t, "to_string") else str(t)
+                                            for t in generator_output["trajectory_ids"]] + \
+            [f"pad{i}" for i in range(pad)]
+        last = generator_output["is_last_step"]
+        batch.metadata["avg_response_length"] = sum(len(r) for r, ls in zip(resp, last) if ls) / N
     return batch
 
 
@@ -239,10 +261,27 @@ def compute_advantages_and_returns(data: TrainingInputBatch, algorithm_cfg) -> T
     from . import ppo_utils
 
     rewards = data["rewards"]
-    adv, ret = ppo_utils.compute_advantages_and_returns(
-        token_level_rewards=rewards, response_mask=data["response_mask"], index=data.metadata["uids"],
-        adv_estimator=algorithm_cfg.advantage_estimator, config=algorithm_cfg, values=data.get("values"),
-        gamma=algorithm_cfg.gamma, lambd=algorithm_cfg.lambd, grpo_norm_by_std=algorithm_cfg.grpo_norm_by_std)
+    kw = dict(adv_estimator=algorithm_cfg.advantage_estimator, config=algorithm_cfg, gamma=algorithm_cfg.gamma,
+              lambd=algorithm_cfg.lambd, grpo_norm_by_std=algorithm_cfg.grpo_norm_by_std)
+    values = data.get("values")
+    step_wise = data.get("is_last_step") is not None and data.metadata.get("trajectory_ids") is not None
+    if step_wise:
+        # trainer.py:777-808: estimate on each trajectory's last step, then give every step of a
+        # trajectory its last step's advantages/returns (steps of a trajectory are contiguous)
+        last = data["is_last_step"].bool()
+        idx = np.array(data.metadata["uids"])[last.cpu().numpy()]
+        la, lr = ppo_utils.compute_advantages_and_returns(
+            token_level_rewards=rewards[last], response_mask=data["response_mask"][last], index=list(idx),
+            values=values[last] if values is not None else None, **kw)
+        traj = torch.cat([torch.zeros(1, dtype=torch.int64, device=last.device), last[:-1].long()]).cumsum(0)
+        assert int(traj[-1]) + 1 == len(la), (
+            f"number of groups {int(traj[-1]) + 1} doesn't match the number of trajectories as given by "
+            f"`is_last_step` {len(la)}. The `is_last_step` tensor is likely malformed")
+        adv, ret = la[traj], lr[traj]
+    else:
+        adv, ret = ppo_utils.compute_advantages_and_returns(
+            token_level_rewards=rewards, response_mask=data["response_mask"], index=data.metadata["uids"],
+            values=values, **kw)
     data["returns"] = ret
     data["advantages"] = adv
     pad = data.metadata.get("pad_size", 0)
@@ -250,7 +289,9 @@ def compute_advantages_and_returns(data: TrainingInputBatch, algorithm_cfg) -> T
     m = data["response_mask"][:n].to(torch.float32)
     a = adv[:n]
     cnt = m.sum()
-    stats = torch.stack([rewards.sum(-1)[:n].mean(), (a * m).sum() / cnt, (a.abs() * m).sum() / cnt]).tolist()
+    rs = rewards.sum(-1)[:n]
+    avg_reward = rs[data["is_last_step"][:n].bool()].mean() if step_wise else rs.mean()
+    stats = torch.stack([avg_reward, (a * m).sum() / cnt, (a.abs() * m).sum() / cnt]).tolist()
     data.metadata.setdefault("metrics", {}).update({
         "avg_final_rewards": stats[0],
         "avg_response_length": data.metadata["avg_response_length"],

@@ -364,3 +364,29 @@ def test_engine_prefix_cache_matches_uncached_prefill():
     same = torch.tensor(outs[True]["response_ids"]) == torch.tensor(outs[False]["response_ids"])
     assert float(same.float().mean()) > 0.9
     torch.testing.assert_close(la[same], lb[same], atol=3e-2, rtol=0)
+
+
+@pytest.mark.parametrize("temp", [0.0, 1.0])
+def test_engine_fused_lmhead_sampler_equals_unfused(temp):
+    """§8(f)1 decode side inside the engine: the lm_head GEMM with the sampler in its epilogue
+    (fused_lmhead) gives the same tokens as the library GEMM + skyrl_sample whenever the bf16
+    logits agree (the GEMMs' fp32 sums round to bf16; compared here against the fused kernel's own
+    plain-GEMM output, skyrl_lmhead_gemm), and logprobs to 1e-4; the fused path really ran."""
+    from skyrl_amd import ops
+
+    cfg, hf = tiny_hf("qwen2", seed=2)
+    m = our_model(cfg, hf)
+    g = torch.Generator().manual_seed(6)
+    prompts = [torch.randint(3, cfg.vocab_size, (L,), generator=g).tolist() for L in (4, 11, 27, 2)]
+    sp = {"temperature": temp, "max_tokens": 16, "logprobs": 0, "ignore_eos": True, "seed": 5}
+    fused = AMDInferenceEngine(m, num_blocks=256, max_num_seqs=8, fused_lmhead="always")
+    a = asyncio.run(fused.generate({"prompt_token_ids": prompts, "sampling_params": sp}))
+    assert fused.runner.fused_steps >= 16
+    # reference: the unfused sampler over the fused kernel's own logits (identical bf16 values)
+    plain = AMDInferenceEngine(m, num_blocks=256, max_num_seqs=8, fused_lmhead="off")
+    plain.runner.model.logits = lambda h: ops.lmhead_gemm(h.contiguous(), m.lm_head)
+    b = asyncio.run(plain.generate({"prompt_token_ids": prompts, "sampling_params": sp}))
+    assert plain.runner.fused_steps == 0
+    assert a["response_ids"] == b["response_ids"]
+    for x, y in zip(a["response_logprobs"], b["response_logprobs"]):
+        torch.testing.assert_close(torch.tensor(x), torch.tensor(y), atol=1e-4, rtol=0)
