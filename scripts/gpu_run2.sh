@@ -1,5 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_lmhead_sample.py tests/test_gpu_engine.py tests/test_gpu_pause_continue.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r02_lms_test.log 2>&1; rc=$?; echo "tests rc=$rc" >> gpurun_out/r02_lms_test.log
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python scripts/probe/lmhead_sample_bench.py --T 1.0 0.0 --M 512 256 64 8 --pipes 0 > gpurun_out/r02_lms_bench.json 2> gpurun_out/r02_lms_bench.err
+timeout -k 10 600 python -u -m pytest tests/test_gpu_engine.py -x -q --timeout 200 --timeout-method thread -k "penalt or n_samples or fused or greedy" > gpurun_out/r02_eng_test.log 2>&1; rc=$?; echo "tests rc=$rc" >> gpurun_out/r02_eng_test.log

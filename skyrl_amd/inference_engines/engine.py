@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import dataclasses
 import heapq
 import itertools
 import time
@@ -56,10 +57,17 @@ class RequestParams:
     stop: Tuple[str, ...] = ()  # stop strings (need the engine's tokenizer), kept in the output text
     ignore_eos: bool = False
     seed: Optional[int] = None
+    n: int = 1
+    # vLLM penalties (additional_kwargs / the Hydra sampling_params keys): repetition divides positive
+    # (multiplies negative) logits of tokens in prompt + output; presence / frequency subtract
+    # presence * [count > 0] + frequency * count for output tokens. Returned logprobs stay raw
+    # (vLLM's default logprobs_mode): log_softmax of the unpenalized logits.
+    repetition_penalty: float = 1.0
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
 
     _ACCEPTED_NOOP = ("skip_special_tokens", "include_stop_str_in_output", "spaces_between_special_tokens",
-                      "detokenize", "repetition_penalty", "presence_penalty", "frequency_penalty",
-                      "max_completion_tokens")
+                      "detokenize", "max_completion_tokens")
 
     @classmethod
     def from_dict(cls, d: Optional[Dict[str, Any]]) -> "RequestParams":
@@ -68,12 +76,13 @@ class RequestParams:
         if "max_completion_tokens" in d and "max_tokens" not in d:
             d["max_tokens"] = d["max_completion_tokens"]
         for k, v in d.items():
-            if k in ("max_tokens", "min_tokens", "top_k", "seed", "logprobs"):
+            if k in ("max_tokens", "min_tokens", "top_k", "seed", "logprobs", "n"):
                 if v is not None:
                     setattr(p, k, int(v))
                 elif k in ("logprobs", "seed"):
                     setattr(p, k, None)
-            elif k in ("temperature", "top_p", "min_p"):
+            elif k in ("temperature", "top_p", "min_p", "repetition_penalty", "presence_penalty",
+                       "frequency_penalty"):
                 setattr(p, k, float(v) if v is not None else getattr(cls, k))
             elif k == "stop_token_ids":
                 p.stop_token_ids = tuple(int(x) for x in (v or ()))
@@ -81,24 +90,28 @@ class RequestParams:
                 p.ignore_eos = bool(v)
             elif k == "stop":
                 p.stop = tuple([v] if isinstance(v, str) else (v or ()))
-            elif k == "n":
-                if v not in (None, 1):
-                    raise ValueError("n > 1 is not supported: replicate prompts (vllm_engine.py:133-136)")
-            elif k in ("repetition_penalty", "presence_penalty", "frequency_penalty"):
-                if v not in (None, 1.0, 0.0):
-                    raise ValueError(f"{k}={v} is not supported by the MI355X sampler")
             elif k in cls._ACCEPTED_NOOP:
                 continue
             else:
                 raise ValueError(f"unsupported sampling parameter {k!r}")
         if p.max_tokens < 1:
             raise ValueError("max_tokens must be >= 1")
+        if p.n is None or p.n < 1:
+            raise ValueError("n must be >= 1")
+        if p.repetition_penalty <= 0:
+            raise ValueError("repetition_penalty must be > 0")
+        for k in ("presence_penalty", "frequency_penalty"):
+            if not -2.0 <= getattr(p, k) <= 2.0:
+                raise ValueError(f"{k} must be in [-2, 2]")
         if p.temperature < 0:
             raise ValueError("temperature must be >= 0")
         return p
 
     def sampler_key(self) -> Tuple[float, int, float, float]:
         return (self.temperature, self.top_k, self.top_p, self.min_p)
+
+    def has_penalty(self) -> bool:
+        return self.repetition_penalty != 1.0 or self.presence_penalty != 0.0 or self.frequency_penalty != 0.0
 
 
 @dataclass
@@ -468,6 +481,7 @@ class ModelRunner:
         fits = model.spec.hidden_size % 64 == 0 and str(getattr(model, "dtype", "")) == "torch.bfloat16"
         self.fused_lmhead = fused_lmhead if fits else "off"
         self.fused_steps = 0  # decode/prefill steps sampled by the fused kernel
+        self._last_nb = 0
         import torch
 
         self.torch = torch
@@ -635,6 +649,7 @@ class ModelRunner:
             hi = 1 + max(r.row for r in reqs)
             nb = next(b for b in self.buckets if b >= hi)
             self._stage_decode(reqs, nb)
+            self._last_nb = nb
             if self.use_graphs:
                 graph, hidden = self._graph(nb)
                 graph.replay()
@@ -648,9 +663,16 @@ class ModelRunner:
     def _fused_ok(self, groups, batch: ScheduledBatch) -> bool:
         if self.fused_lmhead == "off" or len(groups) != 1 or any(batch.suppress):
             return False
+        if any(r.params.has_penalty() for r in batch.requests):
+            return False
         temp, top_k, top_p, min_p = next(iter(groups))
         unfiltered = (top_k is None or top_k < 0) and (top_p is None or top_p >= 1.0) and not min_p
-        return unfiltered and (temp == 0.0 or self.fused_lmhead == "always")
+        if self.fused_lmhead == "always":
+            return unfiltered
+        # greedy: where the fused kernel measured faster (256 x 256 tiles waste MFMA work on
+        # mid-size batches: 149 vs 128 us at 64 rows, 149 vs 174 at 8, 260 vs 288 at 512)
+        nb = len(batch.requests) if batch.kind == "prefill" else self._last_nb
+        return unfiltered and temp == 0.0 and (nb >= 192 or nb <= 16)
 
     def _sample(self, hidden, batch: ScheduledBatch, rows: np.ndarray):
         torch = self.torch
@@ -672,6 +694,7 @@ class ModelRunner:
             return self._fetch(nb, rows)
         logits = self.model.logits(hidden)
         V = logits.shape[1]
+        pen = self._apply_penalties(logits, batch, rows)
         for r_i, ids in zip(rows.tolist(), batch.suppress):
             if ids:
                 logits[r_i, list(ids)] = float("-inf")
@@ -693,7 +716,45 @@ class ModelRunner:
             if len(groups) != 1:
                 self.tokens.index_copy_(0, idx, to)
                 self.lps.index_copy_(0, idx, lo)
+        if pen is not None:  # raw logprobs of the penalized rows: restore the logits, recompute
+            flat, saved, prow = pen
+            logits.view(-1).index_copy_(0, flat, saved)
+            x = logits.index_select(0, prow)
+            lp, _ = ops.logprobs_and_entropy(x[None], self.tokens.index_select(0, prow).long()[None],
+                                             compute_entropy=False)
+            self.lps.index_copy_(0, prow, lp[0])
         return self._fetch(nb, rows)
+
+    def _apply_penalties(self, logits, batch: ScheduledBatch, rows: np.ndarray):
+        """vLLM's apply_penalties on the rows that ask for one (sparse: only the tokens of their
+        prompt + output). Returns (flat indices, original values, rows) to restore, or None."""
+        torch = self.torch
+        V = logits.shape[1]
+        fi, rep, add, prow = [], [], [], []
+        for r_i, r in zip(rows.tolist(), batch.requests):
+            p = r.params
+            if not p.has_penalty():
+                continue
+            prow.append(r_i)
+            counts = collections.Counter(r.out_tokens)
+            toks = sorted(set(r.prompt) | set(counts)) if p.repetition_penalty != 1.0 else sorted(counts)
+            for t in toks:
+                if 0 <= t < V:
+                    c = counts.get(t, 0)
+                    fi.append(r_i * V + t)
+                    rep.append(p.repetition_penalty)
+                    add.append(-(p.frequency_penalty * c + (p.presence_penalty if c > 0 else 0.0)))
+        if not prow:
+            return None
+        dev = self.device
+        flat = torch.tensor(fi, dtype=torch.int64).to(dev, non_blocking=True)
+        r = torch.tensor(rep, dtype=torch.float32).to(dev, non_blocking=True)
+        a = torch.tensor(add, dtype=torch.float32).to(dev, non_blocking=True)
+        saved = logits.view(-1).index_select(0, flat)
+        v = saved.float()
+        v = torch.where(v > 0, v / r, v * r) + a
+        logits.view(-1).index_copy_(0, flat, v.to(logits.dtype))
+        return flat, saved, torch.tensor(prow, dtype=torch.int64).to(dev, non_blocking=True)
 
     def _fetch(self, nb: int, rows: np.ndarray):
         torch = self.torch
@@ -814,7 +875,17 @@ class AMDInferenceEngine(InferenceEngineInterface):
             raise ValueError("AMDInferenceEngine only accepts `prompt_token_ids`, not `prompts` "
                              "(vllm_engine.py:112-114)")
         params = RequestParams.from_dict(input_batch.get("sampling_params"))
-        futs = [self._submit(p, params) for p in ids]
+        if params.n > 1:
+            # n samples per prompt, prompt-major in the output (the reference copies prompts instead:
+            # vllm_engine.py:133-136); a seeded request's j-th sample uses seed + j, as vLLM's
+            # parallel sampling does
+            subs = []
+            for j in range(params.n):
+                pj = dataclasses.replace(params, n=1, seed=None if params.seed is None else params.seed + j)
+                subs.append(pj)
+            futs = [self._submit(p, subs[j]) for p in ids for j in range(params.n)]
+        else:
+            futs = [self._submit(p, params) for p in ids]
         reqs = await asyncio.gather(*futs)
         return self._output(list(reqs), params.logprobs is not None)
 

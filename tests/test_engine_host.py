@@ -85,8 +85,13 @@ def test_request_params_parse():
                                  "min_p": 0.0, "logprobs": 0, "stop": None, "skip_special_tokens": True,
                                  "include_stop_str_in_output": True})
     assert (p.max_tokens, p.min_tokens, p.top_k, p.logprobs) == (8, 1, 50, 0)
-    with pytest.raises(ValueError):
-        RequestParams.from_dict({"n": 2})
+    q = RequestParams.from_dict({"n": 3, "repetition_penalty": 1.1, "presence_penalty": 0.5,
+                                 "frequency_penalty": -0.2, "logprobs": 5})
+    assert (q.n, q.repetition_penalty, q.presence_penalty, q.frequency_penalty, q.logprobs) == (3, 1.1, 0.5, -0.2, 5)
+    assert q.has_penalty() and not p.has_penalty()
+    for bad in ({"n": 0}, {"repetition_penalty": 0.0}, {"presence_penalty": 2.5}, {"frequency_penalty": -3}):
+        with pytest.raises(ValueError):
+            RequestParams.from_dict(bad)
     assert RequestParams.from_dict({"stop": ["</sql>", "x"]}).stop == ("</sql>", "x")
     assert RequestParams.from_dict({"stop": "\n"}).stop == ("\n",)
     with pytest.raises(ValueError):  # stop strings need a tokenizer in the engine

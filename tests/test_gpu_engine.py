@@ -390,3 +390,73 @@ def test_engine_fused_lmhead_sampler_equals_unfused(temp):
     assert a["response_ids"] == b["response_ids"]
     for x, y in zip(a["response_logprobs"], b["response_logprobs"]):
         torch.testing.assert_close(torch.tensor(x), torch.tensor(y), atol=1e-4, rtol=0)
+
+
+def _penalized(logits, prompt, out, rep, pres, freq):
+    """vLLM apply_penalties on one row (repetition over prompt + output, presence / frequency
+    over output counts)."""
+    from collections import Counter
+
+    x = logits.clone()
+    c = Counter(out)
+    seen = set(prompt) | set(c)
+    if rep != 1.0:
+        idx = torch.tensor(sorted(seen), device=x.device)
+        v = x[idx]
+        x[idx] = torch.where(v > 0, v / rep, v * rep)
+    if c:
+        idx = torch.tensor(sorted(c), device=x.device)
+        cnt = torch.tensor([c[t] for t in sorted(c)], device=x.device, dtype=x.dtype)
+        x[idx] -= freq * cnt + pres
+    return x
+
+
+@pytest.mark.parametrize("pen", [(1.3, 0.0, 0.0), (1.0, 0.8, 0.3), (0.7, -0.5, 0.2)])
+def test_engine_penalties_greedy_vs_hf(pen):
+    """repetition / presence / frequency penalties (vLLM semantics) on greedy decoding: every token
+    is the argmax of HF's penalized logits wherever that margin exceeds 0.1, and the returned
+    logprob is the RAW one (vLLM's default logprobs_mode), not the penalized one."""
+    rep, pres, freq = pen
+    cfg, hf = tiny_hf("qwen2", seed=3)
+    m = our_model(cfg, hf)
+    eng = AMDInferenceEngine(m, num_blocks=256, max_num_seqs=8)
+    g = torch.Generator().manual_seed(8)
+    prompts = [torch.randint(3, cfg.vocab_size, (L,), generator=g).tolist() for L in (5, 13)]
+    sp = {"temperature": 0.0, "max_tokens": 20, "logprobs": 0, "ignore_eos": True, "repetition_penalty": rep,
+          "presence_penalty": pres, "frequency_penalty": freq}
+    out = asyncio.run(eng.generate({"prompt_token_ids": prompts, "sampling_params": sp}))
+    assert eng.runner.fused_steps == 0  # penalties take the unfused path
+    checked = 0
+    with torch.no_grad():
+        for p, ids, lps in zip(prompts, out["response_ids"], out["response_logprobs"]):
+            for k, tok in enumerate(ids):
+                raw = hf(torch.tensor(p + ids[:k], device=DEV)[None]).logits[0, -1].float()
+                x = _penalized(raw, p, ids[:k], rep, pres, freq)
+                top2 = torch.topk(x, 2)
+                if float(top2.values[0] - top2.values[1]) < 0.1:
+                    break
+                assert tok == int(top2.indices[0]), (k, tok, int(top2.indices[0]))
+                assert abs(lps[k] - float(torch.log_softmax(raw, -1)[tok])) < 5e-2
+                checked += 1
+    assert checked >= 10
+
+
+def test_engine_n_samples_and_top_logprobs():
+    """n > 1: n consecutive samples per prompt; a seeded request's j-th sample is the n = 1
+    request with seed + j (vLLM parallel sampling). logprobs = 5 returns the sampled token's
+    logprob, as logprobs = 0 does (the reference reads only that one, vllm_engine.py:139-149)."""
+    cfg, hf = tiny_hf("qwen2", seed=4)
+    m = our_model(cfg, hf)
+    eng = AMDInferenceEngine(m, num_blocks=256, max_num_seqs=16)
+    prompts = [[5, 6, 7, 8], [9, 10, 11]]
+    sp = {"temperature": 1.0, "max_tokens": 12, "logprobs": 0, "ignore_eos": True, "seed": 7}
+    a = asyncio.run(eng.generate({"prompt_token_ids": prompts, "sampling_params": dict(sp, n=3)}))
+    assert len(a["response_ids"]) == 6
+    for i, p in enumerate(prompts):
+        for j in range(3):
+            b = asyncio.run(eng.generate({"prompt_token_ids": [p], "sampling_params": dict(sp, seed=7 + j)}))
+            assert a["response_ids"][3 * i + j] == b["response_ids"][0]
+        assert len({tuple(x) for x in a["response_ids"][3 * i:3 * i + 3]}) > 1
+    c = asyncio.run(eng.generate({"prompt_token_ids": prompts[:1], "sampling_params": dict(sp, logprobs=5)}))
+    d = asyncio.run(eng.generate({"prompt_token_ids": prompts[:1], "sampling_params": sp}))
+    assert c["response_ids"] == d["response_ids"] and c["response_logprobs"] == d["response_logprobs"]
