@@ -446,6 +446,8 @@ def test_engine_n_samples_and_top_logprobs():
     request with seed + j (vLLM parallel sampling). logprobs = 5 returns the sampled token's
     logprob, as logprobs = 0 does (the reference reads only that one, vllm_engine.py:139-149)."""
     cfg, hf = tiny_hf("qwen2", seed=4)
+    with torch.no_grad():  # undo tiny_hf's sharpening: samples at T = 1 should differ
+        hf.lm_head.weight.div_(20.0)
     m = our_model(cfg, hf)
     eng = AMDInferenceEngine(m, num_blocks=256, max_num_seqs=16)
     prompts = [[5, 6, 7, 8], [9, 10, 11]]
