@@ -83,7 +83,7 @@ __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)
 // the copies over the MFMA groups with sched_group_barrier produced a worse schedule: dropped.)
 int g_lmhead_pipe = 0;
 
-template <int EPI, int BN, int BKT, int S>
+template <int EPI, int BN, int BKT, int S, int STAGGER>
 __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
@@ -149,9 +149,14 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         const char* sb = smem + (t % S) * G::kStageBytes;
-        if (t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+        // STAGGER: the waves of the upper half (the second wave of each SIMD) issue their copies
+        // after the first half of the k-steps, so a SIMD's MFMA pipe is never idle for both waves'
+        // copy issue at once
+        const bool late = STAGGER && __builtin_amdgcn_readfirstlane(w) >= G::kWaves / 2;
+        if (!late && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
+            if (late && ks == G::KS / 2 && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
             bf16x8 b[4];
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
@@ -394,13 +399,14 @@ inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
                             float, uint64_t, const int64_t*, int64_t, float4*, float*, int);
-int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }
+int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }  // pipe 3: 256, staggered copies
 template <int EPI>
 GemmKernel pick_kernel() {
     switch (g_lmhead_pipe) {
-        case 1: return lmhead_gemm_kernel<EPI, 128, 32, 3>;
-        case 2: return lmhead_gemm_kernel<EPI, 256, 32, 4>;
-        default: return lmhead_gemm_kernel<EPI, 256, 64, 2>;
+        case 1: return lmhead_gemm_kernel<EPI, 128, 32, 3, 0>;
+        case 2: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0>;
+        case 3: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1>;
+        default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0>;
     }
 }
 
@@ -417,7 +423,7 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }  // namespace
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 2, "skyrl_tune: lmhead_pipe must be -1 (default), 0, 1 or 2");
+    SKYRL_REQUIRE(value >= -1 && value <= 3, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..3");
     g_lmhead_pipe = value < 0 ? 0 : value;
     return SKYRL_OK;
 }
