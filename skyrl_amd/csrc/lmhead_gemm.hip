@@ -83,7 +83,7 @@ __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)
 // the copies over the MFMA groups with sched_group_barrier produced a worse schedule: dropped.)
 int g_lmhead_pipe = 0;
 
-template <int EPI, int BN, int BKT, int S, int STAGGER>
+template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
 __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
@@ -154,6 +154,43 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         // copy issue at once
         const bool late = STAGGER && __builtin_amdgcn_readfirstlane(w) >= G::kWaves / 2;
         if (!late && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+        if constexpr (DB) {
+            // explicit fragment pipeline: groups of 2 A fragments x 4 B fragments (8 MFMAs); the next
+            // group's ds_reads are issued before this group's MFMAs, and sched_barriers keep the
+            // compiler from sinking them (left alone it waits lgkmcnt(0) before every 8 MFMAs)
+            constexpr int NG = G::KS * 4;
+            bf16x8 bq[G::KS][4], aq[2][2];
+            auto ldA = [&](int ks, int mp, bf16x8 (&dst)[2]) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    dst[u] = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + (2 * mp + u) * 16 * G::kRowBytes);
+            };
+            auto ldB = [&](int ks) {
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+            };
+            ldB(0);
+            ldA(0, 0, aq[0]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const int ks = g / 4, mp = g % 4;
+                if (late && g == NG / 2 && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+                if (g + 1 < NG) {
+                    if ((g + 1) % 4 == 0) ldB((g + 1) / 4);
+                    ldA((g + 1) / 4, (g + 1) % 4, aq[(g + 1) & 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[2 * mp + u][nb] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[g & 1][u], bq[ks][nb], acc[2 * mp + u][nb], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            continue;
+        }
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
             if (late && ks == G::KS / 2 && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
@@ -403,10 +440,12 @@ int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }  // pipe 3: 256, stagger
 template <int EPI>
 GemmKernel pick_kernel() {
     switch (g_lmhead_pipe) {
-        case 1: return lmhead_gemm_kernel<EPI, 128, 32, 3, 0>;
-        case 2: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0>;
-        case 3: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1>;
-        default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0>;
+        case 1: return lmhead_gemm_kernel<EPI, 128, 32, 3, 0, 0>;
+        case 2: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 0>;
+        case 3: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1, 0>;
+        case 4: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 1>;
+        case 5: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1, 1>;
+        default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
 
@@ -423,7 +462,7 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }  // namespace
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 3, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..3");
+    SKYRL_REQUIRE(value >= -1 && value <= 5, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..5");
     g_lmhead_pipe = value < 0 ? 0 : value;
     return SKYRL_OK;
 }
