@@ -358,6 +358,8 @@ def run(args):
                                     "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
     if not args.no_attention_leg:
         result["rollout_attention"] = rollout_attention_leg(dev, N)
+    if not args.no_lmhead_leg:
+        result["rollout_lmhead_sample"] = lmhead_sample_leg(dev, N)
     if not args.no_vocab_legs:
         result["policy_train_vocabs"] = policy_train_vocab_legs(dev, mb, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -535,6 +537,55 @@ def policy_train_vocab_legs(dev, mb, R, reps=10):
     return out
 
 
+def lmhead_sample_leg(dev, nseq, reps=30):
+    """One rollout decode step's logits projection + sampling at the headline shape (SURVEY
+    §8(f)1 decode side): hidden [nseq, 1536] (Qwen2.5-1.5B) x lm_head [151,936, 1536] bf16.
+    fused   = skyrl_lmhead_sample (MFMA GEMM with the sampler in its epilogue, one merge launch)
+    unfused = library GEMM (torch/hipBLASLt) writing bf16 logits + skyrl_sample reading them.
+    Random operands (logits ~ N(0, 9)). The MFMA roofline is against the 2.5 PF/s dense bf16 peak."""
+    from skyrl_amd import ops
+
+    H, V = 1536, VOCAB
+    g = torch.Generator(device=dev).manual_seed(5)
+    w = (torch.randn(V, H, device=dev, generator=g) * (3.0 / H ** 0.5)).to(torch.bfloat16)
+    h = torch.randn(nseq, H, device=dev, generator=g).to(torch.bfloat16)
+    ids = torch.arange(nseq, device=dev)
+    z = torch.empty(nseq, V, dtype=torch.bfloat16, device=dev)
+    tok = torch.empty(nseq, dtype=torch.int32, device=dev)
+    lp = torch.empty(nseq, dtype=torch.float32, device=dev)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        return round(a.elapsed_time(b) * 1e3 / reps, 2)
+
+    out = {"rows": nseq, "hidden": H, "vocab": V}
+    for name, T in (("t1", 1.0), ("greedy", 0.0)):
+        out[f"fused_{name}_us"] = timed(lambda: ops.lmhead_sample(h, w, temperature=T, seed=1, seq_ids=ids, step=3,
+                                                                   tokens_out=tok, logp_out=lp))
+
+        def unfused():
+            torch.matmul(h, w.T, out=z)
+            ops.sample(z, temperature=T, seed=1, seq_ids=ids, step=3, tokens_out=tok, logp_out=lp)
+        out[f"unfused_{name}_us"] = timed(unfused)
+    out["gemm_only_us"] = timed(lambda: ops.lmhead_gemm(h, w, out=z))
+    out["library_gemm_only_us"] = timed(lambda: torch.matmul(h, w.T, out=z))
+    flops = 2.0 * nseq * H * V
+    tf = flops / (out["fused_t1_us"] * 1e-6) / 1e12
+    out["roofline"] = {"kernel": "lmhead_gemm_kernel<sample> + merge", "bound": "mfma", "achieved": round(tf, 1),
+                       "peak": 2500.0, "unit": "TFLOP/s", "frac": round(tf / 2500.0, 4)}
+    out["gemm_TFs"] = round(flops / (out["gemm_only_us"] * 1e-6) / 1e12, 1)
+    out["logits_bytes_not_written"] = nseq * V * 2
+    return out
+
+
 def rollout_attention_leg(dev, nseq, reps=20):
     """Rollout decode attention (csrc/attention.hip paged_decode_kernel) at the
     headline shape: Qwen2.5-1.5B heads (12 q / 2 kv, D=128), one decode step of all nseq
@@ -670,6 +721,7 @@ def main():
     ap.add_argument("--no-adv-loss-leg", action="store_true", help="skip the graph-replayed advantage+loss leg")
     ap.add_argument("--adv-loss-variants", action="store_true", help="also time the A/B variants of that leg")
     ap.add_argument("--no-attention-leg", action="store_true", help="skip the rollout paged-attention leg")
+    ap.add_argument("--no-lmhead-leg", action="store_true", help="skip the decode lm_head + sampler leg")
     ap.add_argument("--no-vocab-legs", action="store_true", help="skip the per-vocabulary fused training pass legs")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)

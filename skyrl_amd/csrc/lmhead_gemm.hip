@@ -249,31 +249,28 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         const int r = threadIdx.x / TPR, hh = threadIdx.x % TPR;
         const int grow = m0 + r;
         if (grow >= M) return;  // the threads of a row leave together (the row shuffle below)
+        uint4 pk[NC];
         float m = -1e30f, s = 0.f;   // raw online (max, sum-exp)
         float best_s = -INFINITY, best_x = -INFINITY;
         int best_i = 0x7fffffff;
-        float vmx[NC], lhi[NC];      // per group: max logit, upper bound of -ln E over the group
+        float lng[NC], slack[NC];    // per group: -ln E_g and the non-min-slot bound slack
         uint32_t key = 0u, key2 = 0u, keyb = 0u;
         if constexpr (!greedy) {
             key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
             key2 = noise_key2(key);
             keyb = noise_keyb(key);
         }
-        float bar = -INFINITY;  // a lower bound of some element's exact score (sampling)
-        // pass 1, every group: LSE; greedy: the first maximum; sampling: bounds from the hardware
-        // log (not on the decision path): L = -ln E_g within +-mg, so the group's minimum-E slot p
-        // scores at least x_p / T + L - mg (a bar every winner must reach) and every slot of the
-        // group at most x / T + L + mg (E_v >= E_g). Groups with E_g < 1e-5 get an infinite upper
-        // bound. Only slots whose upper bound reaches the bar are scored exactly (det_ln, noise.h),
-        // so decisions are the exact argmax, as in sample_kernel.
+        // pass 1, every group: LSE; greedy: the first maximum; sampling: the exact score of the
+        // group's minimum-E slot p = h & 7 (its E is E_g itself, so the score needs no per-element
+        // hash) -- the best of those is the bar for everything else
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
             const int c = TPR * i + hh;
             const int v0 = n0 + c * 8;
             const int cnt = min(8, N - v0);
-            const uint4 pk = *reinterpret_cast<const uint4*>(smem + G::img_off(r, c));
+            pk[i] = *reinterpret_cast<const uint4*>(smem + G::img_off(r, c));
             float x[8];
-            const uint32_t wds[4] = {pk.x, pk.y, pk.z, pk.w};
+            const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 x[2 * k] = __uint_as_float(wds[k] << 16);
@@ -284,16 +281,15 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
             float vmax = x[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) vmax = fmaxf(vmax, x[k]);
-            vmx[i] = vmax;
-            lhi[i] = -INFINITY;
+            lng[i] = 0.f;
+            slack[i] = 0.f;
             if (cnt <= 0) continue;
             {
                 const float mn = fmaxf(m, vmax);
-                const float c2 = -mn * kLog2eG;
                 float acc_e = 0.f;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) acc_e += fast_exp2(fmaf(x[k], kLog2eG, c2));
-                s = fmaf(s, fast_exp2(fmaf(m, kLog2eG, c2)), acc_e);
+                for (int k = 0; k < 8; ++k) acc_e += fast_exp2((x[k] - mn) * kLog2eG);
+                s = s * fast_exp2((m - mn) * kLog2eG) + acc_e;
                 m = mn;
             }
             if constexpr (greedy) {
@@ -308,54 +304,65 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
             } else {
                 const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
                 const int p = (int)(h & 7u);
-                const uint32_t t16 = (h >> 16) ^ 0xffffu;
-                const float ug = (float)(((t16 << 8) | ((h >> 8) & 0xffu)) | 1u) * kNoiseU24;  // group_min_e's u_g
-                const float ea = fast_log2(ug) * (-kLn2G * 0.125f);
-                if (ea < 1e-5f) {
-                    lhi[i] = INFINITY;
-                } else {
-                    const float l = -fast_log2(ea) * kLn2G;
-                    // det_ln's 1.1e-6 error on ln u_g and on ln U (a non-min slot's E may sit 1.2e-6
-                    // below E_g), rounding of the scores: all well inside mg
-                    const float mg = 1e-4f + 4e-6f / ea;
-                    lhi[i] = l + mg;
-                    float xp = x[0];
+                const float Eg = group_min_e(h);
+                const float L = -det_ln(Eg);
+                lng[i] = L;
+                // a non-min slot's E = E_g + (-det_ln U) >= E_g - 1.2e-6 (det_ln error), so its exact
+                // score is <= x inv_t + L + 1.4e-6 / E_g + 4e-6 (det_ln and rounding errors); slack is
+                // generous on both, and infinite (every slot a candidate) when E_g is too small for it
+                slack[i] = Eg < 1e-5f ? INFINITY : 1e-4f + 4e-6f / Eg;
+                float xp = x[0];
 #pragma unroll
-                    for (int k = 1; k < 8; ++k) xp = (k == p) ? x[k] : xp;
-                    if (p < cnt) bar = fmaxf(bar, fmaf(xp, inv_t, l - mg));
+                for (int k = 1; k < 8; ++k) xp = (k == p) ? x[k] : xp;
+                if (p < cnt) {
+                    const float sc = xp * inv_t + L;  // = noise_score(xp, inv_t, v0 + p, h, Eg, key2)
+                    if (better(sc, v0 + p, Best{best_s, best_i})) {
+                        best_s = sc;
+                        best_i = v0 + p;
+                        best_x = xp;
+                    }
                 }
             }
         }
         if constexpr (!greedy) {
+            float bar = best_s;
 #pragma unroll
             for (int o = 1; o < TPR; o <<= 1) bar = fmaxf(bar, __shfl_xor(bar, o, kWave));
-            // pass 2: groups whose upper bound reaches the bar (usually 1-2 of 16 per thread)
-            uint32_t gm = 0u;
+            // pass 2: non-min slots whose bound reaches the bar, as a bit mask (bit 8 i + k)
+            uint32_t cm[NC / 4];
 #pragma unroll
-            for (int i = 0; i < NC; ++i)
-                if (!(fmaf(vmx[i], inv_t, lhi[i]) < bar)) gm |= 1u << i;
-            // exact scores (noise.h) of the candidate groups' slots that reach the bar, one group per
-            // lane per trip
-            while (gm) {
-                const int i = __builtin_ctz(gm);
-                gm &= gm - 1u;
-                const int c = TPR * i + hh;
-                const int v0 = n0 + c * 8;
+            for (int j = 0; j < NC / 4; ++j) cm[j] = 0u;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                const int v0 = n0 + (TPR * i + hh) * 8;
                 const int cnt = min(8, N - v0);
-                const uint4 pk = *reinterpret_cast<const uint4*>(smem + G::img_off(r, c));
-                const uint32_t wds[4] = {pk.x, pk.y, pk.z, pk.w};
-                const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
-                const float Eg = group_min_e(h);
-                float li = 0.f;
+                const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
+                const float lim = bar - lng[i] - slack[i];  // x inv_t >= lim can reach the bar
+                uint32_t bm = 0u;
 #pragma unroll
-                for (int j = 0; j < NC; ++j) li = (j == i) ? lhi[j] : li;
-                for (int k = 0; k < cnt; ++k) {
+                for (int k = 0; k < 8; ++k) {
                     const float xk = __uint_as_float((k & 1) ? (wds[k >> 1] & 0xffff0000u) : (wds[k >> 1] << 16));
-                    if (fmaf(xk, inv_t, li) < bar) continue;
-                    const float sc = noise_score(xk, inv_t, v0 + k, h, Eg, key2);
-                    if (better(sc, v0 + k, Best{best_s, best_i})) {
+                    if (k < cnt && !(xk * inv_t < lim)) bm |= 1u << k;
+                }
+                cm[i >> 2] |= bm << ((i & 3) * 8);
+            }
+            // exact scores of the candidates, one per lane per trip (the min slot re-scores to the
+            // value pass 1 already has: harmless)
+#pragma unroll
+            for (int wd = 0; wd < NC / 4; ++wd) {
+                uint32_t bm = cm[wd];
+                while (bm) {
+                    const int b = __builtin_ctz(bm);
+                    bm &= bm - 1u;
+                    const int i = wd * 4 + (b >> 3), k = b & 7;
+                    const int c = TPR * i + hh;
+                    const int v = n0 + c * 8 + k;
+                    const float xk = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + G::img_off(r, c) + k * 2));
+                    const uint32_t h = ehash(key, keyb, (uint32_t)v >> 3);
+                    const float sc = noise_score(xk, inv_t, v, h, group_min_e(h), key2);
+                    if (better(sc, v, Best{best_s, best_i})) {
                         best_s = sc;
-                        best_i = v0 + k;
+                        best_i = v;
                         best_x = xk;
                     }
                 }
