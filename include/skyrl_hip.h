@@ -238,6 +238,15 @@ int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int32_t vc, in
 int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
                       int32_t N, int32_t K, void* out, int64_t ld_out, void* stream);
 size_t skyrl_lmhead_sample_workspace_bytes(int32_t M, int32_t V);
+/* Learner side (old / ref log-probs, no grad): logp/entropy/lse f32 [T] of log_softmax(bf16(h W^T) / T)
+ * at labels (int64, token r at labels[r*label_stride]) with the same kernel's online-softmax
+ * epilogue (no [T,V] logits in HBM), one 16-B state per (token, 256-column tile) folded by
+ * skyrl_lmhead_state_merge. entropy_out / lse_out may be NULL. Workspace:
+ * skyrl_lmhead_logprob_workspace_bytes(T, V), 16-B aligned.                              */
+size_t skyrl_lmhead_logprob_workspace_bytes(int32_t T, int32_t V);
+int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t T,
+                             int32_t V, int32_t K, const int64_t* labels, int64_t label_stride, float temperature,
+                             float* logp_out, float* entropy_out, float* lse_out, void* workspace, void* stream);
 int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
                         int32_t V, int32_t K, float temperature, uint64_t seed, const int64_t* seq_ids, int64_t step,
                         int32_t* tokens_out, float* logp_out, void* workspace, void* stream);

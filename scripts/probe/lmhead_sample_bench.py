@@ -73,5 +73,31 @@ def main():
             print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in res.items()}), flush=True)
 
 
+
+
+def learner_main():
+    """Learner-side forward logprob at T tokens: chunked hipBLASLt path vs the fused epilogue."""
+    import sys as _s
+    from skyrl_amd import lmhead
+
+    dev = torch.device("cuda")
+    H, V = 1536, 151936
+    w = (torch.randn(V, H, device=dev) * (3.0 / H ** 0.5)).to(torch.bfloat16)
+    for T in (4096, 8192, 16384):
+        h = torch.randn(T, H, device=dev).to(torch.bfloat16)
+        lab = torch.randint(0, V, (T,), device=dev)
+        with torch.no_grad():
+            chunked = timeit(lambda: lmhead.lmhead_logprobs_and_entropy(h, w, lab), 5)
+            fused = timeit(lambda: ops.lmhead_logprob_fwd(h, w, lab), 5)
+        flops = 2.0 * T * H * V
+        print(json.dumps({"T": T, "chunked_us": round(chunked, 1), "fused_us": round(fused, 1),
+                          "fused_TFs": round(flops / (fused * 1e-6) / 1e12, 1),
+                          "chunked_TFs": round(flops / (chunked * 1e-6) / 1e12, 1)}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    import sys as _sys
+    if "--learner" in _sys.argv:
+        learner_main()
+    else:
+        main()

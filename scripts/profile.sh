@@ -11,7 +11,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 if [ "${PMC:-1}" = 1 ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex "${PMC_REGEX:-logprob|grpo|ppo_loss|sample_kernel|pack|policy_train|paged_decode}" --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py $ARGS > $OUT/pmc_$c.log 2>&1
+    timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex "${PMC_REGEX:-logprob|grpo|ppo_loss|sample_kernel|pack|policy_train|paged_decode|lmhead_gemm}" --output-format csv -d $OUT/pmc_$c -o run -- python3 bench.py $ARGS > $OUT/pmc_$c.log 2>&1
     rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
   done
 fi

@@ -115,6 +115,9 @@ SIGNATURES = {
     "skyrl_lmhead_state_merge": (_INT, [_P, _I32, _I32, _P, _P, _P, _P]),
     "skyrl_lmhead_gemm": (_INT, [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _I64, _P]),
     "skyrl_lmhead_sample_workspace_bytes": (_SZ, [_I32, _I32]),
+    "skyrl_lmhead_logprob_workspace_bytes": (_SZ, [_I32, _I32]),
+    "skyrl_lmhead_logprob_fwd": (
+        _INT, [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _I64, _F, _P, _P, _P, _P, _P]),
     "skyrl_lmhead_sample": (
         _INT, [_P, _I64, _P, _I64, _I32, _I32, _I32, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),
     "skyrl_policy_train_workspace_bytes": (_SZ, [_I32, _I32]),

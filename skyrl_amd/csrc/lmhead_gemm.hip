@@ -29,6 +29,7 @@
 // the token and its logprob log_softmax(raw logits)[token]. Decisions equal skyrl_sample's /
 // oracle/sampler_ref.c's on the bf16 logits this GEMM produces (STORE), bit for bit.
 #include "noise.h"
+#include "softmax.h"
 
 namespace skyrl {
 namespace {
@@ -42,7 +43,7 @@ typedef __attribute__((address_space(1))) void gbl_void;
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2 };
+enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2, EPI_LOGPROB = 3 };
 
 // Tile geometry: BM (256) x BN output columns, NT = 2 BN threads as 2 (M) x BN/64 (N) waves of
 // 128 x 64 outputs; K in BKT-deep tiles through S LDS stages (S - 1 tiles in flight).
@@ -87,7 +88,8 @@ template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
 __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
-    int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt) {
+    int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt, const int64_t* __restrict__ labels,
+    int64_t lstride) {
     using G = Geo<BN, BKT, S>;
     __shared__ __attribute__((aligned(16))) char smem[G::kLds];
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
@@ -243,6 +245,49 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
             }
         }
         return;
+    } else if constexpr (EPI == EPI_LOGPROB) {
+        // learner forward (old / ref log-probs): the per-token online-softmax state of the tile's
+        // columns (logprob.hip's state: m, S = sum 2^y, W = sum 2^y y in log2 units, after the
+        // reference's bf16 division by T) and the label's logit when the label is in this tile;
+        // state [ntile][M] for skyrl_lmhead_state_merge. inv_t carries T (> 0), seed != 0 = T != 1.
+        using E = Elem<uint16_t>;
+        const float temp = inv_t;
+        const bool has_t = seed != 0ull;
+        const int r = threadIdx.x / G::TPR, hh = threadIdx.x % G::TPR;
+        const int grow = m0 + r;
+        if (grow >= M) return;
+        SoftState st;
+        state_init(st);
+#pragma unroll 4
+        for (int i = 0; i < G::kChunksPerThread; ++i) {
+            const int c = G::TPR * i + hh;
+            const int v0 = n0 + c * 8;
+            const int cnt = min(8, N - v0);
+            if (cnt <= 0) break;
+            const uint4 pk = *reinterpret_cast<const uint4*>(smem + G::img_off(r, c));
+            float x[8];
+            E::unpack(pk, x);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = k < cnt ? E::apply_t(x[k], temp, has_t) : -INFINITY;
+            state_add<8>(st, x);
+        }
+#pragma unroll
+        for (int o = 1; o < G::TPR; o <<= 1) {
+            SoftState ot;
+            ot.m = __shfl_xor(st.m, o, kWave);
+            ot.s = __shfl_xor(st.s, o, kWave);
+            ot.w = __shfl_xor(st.w, o, kWave);
+            state_merge(st, ot);
+        }
+        if (hh == 0) {
+            const int64_t lab = labels[(int64_t)grow * lstride] - n0;
+            float xl = __builtin_nanf("");
+            if (lab >= 0 && lab < BN && n0 + lab < N)
+                xl = E::apply_t(bf16_to_f32(*reinterpret_cast<const uint16_t*>(
+                                    smem + G::img_off(r, (int)lab >> 3) + ((int)lab & 7) * 2)),
+                                temp, has_t);
+            parts[(int64_t)ntile * M + grow] = make_float4(st.m, st.s, st.w, xl);
+        }
     } else {
         constexpr bool greedy = EPI == EPI_GREEDY;
         constexpr int TPR = G::TPR, NC = G::kChunksPerThread;
@@ -435,7 +480,7 @@ __global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* _
 inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
-                            float, uint64_t, const int64_t*, int64_t, float4*, float*, int);
+                            float, uint64_t, const int64_t*, int64_t, float4*, float*, int, const int64_t*, int64_t);
 int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }  // pipe 3: 256, staggered copies
 template <int EPI>
 GemmKernel pick_kernel() {
@@ -480,7 +525,7 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
     hipLaunchKernelGGL(pick_kernel<EPI_STORE>(), dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream),
                        reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
                        ld_weight, M, N, K, mt, reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
-                       nullptr, nullptr, nt);
+                       nullptr, nullptr, nt, nullptr, 0ll);
     return check_launch("lmhead_gemm_kernel<store>");
 }
 
@@ -507,10 +552,36 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     auto kern = greedy ? pick_kernel<EPI_GREEDY>() : pick_kernel<EPI_SAMPLE>();
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt, nullptr, 0ll, inv_t,
-                       seed, seq_ids, step, parts, part_x, nt);
+                       seed, seq_ids, step, parts, part_x, nt, nullptr, 0ll);
     rc = check_launch("lmhead_gemm_kernel<sample>");
     if (rc) return rc;
     hipLaunchKernelGGL(lmhead_sample_merge_kernel, dim3(M), dim3(64), 0, as_stream(stream), parts, part_x, nt, tokens_out,
                        logp_out);
     return check_launch("lmhead_sample_merge_kernel");
+}
+
+extern "C" size_t skyrl_lmhead_logprob_workspace_bytes(int32_t T, int32_t V) {
+    return (size_t)(T > 0 ? T : 1) * tiles(V > 0 ? V : 1, 128) * sizeof(float4) + 256;
+}
+
+extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight,
+                                        int32_t T, int32_t V, int32_t K, const int64_t* labels, int64_t label_stride,
+                                        float temperature, float* logp_out, float* entropy_out, float* lse_out,
+                                        void* workspace, void* stream) {
+    int rc = check_operands(hidden, ld_hidden, weight, ld_weight, T, V, K);
+    if (rc) return rc;
+    if (T == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(labels && logp_out && workspace, "lmhead_logprob_fwd: null pointer");
+    SKYRL_REQUIRE(temperature > 0.f, "lmhead_logprob_fwd: temperature must be > 0");
+    SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_logprob_fwd: workspace must be 16-B aligned");
+    const int bn = tile_n(), mt = tiles(T, BM), nt = tiles(V, bn);
+    float4* states = reinterpret_cast<float4*>(workspace);
+    auto kern = pick_kernel<EPI_LOGPROB>();
+    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
+                       ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt, nullptr, 0ll,
+                       temperature, temperature != 1.0f ? 1ull : 0ull, nullptr, 0ll, states, nullptr, nt, labels,
+                       label_stride);
+    rc = check_launch("lmhead_gemm_kernel<logprob>");
+    if (rc) return rc;
+    return skyrl_lmhead_state_merge(states, nt, T, logp_out, entropy_out, lse_out, stream);
 }

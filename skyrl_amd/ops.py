@@ -602,6 +602,24 @@ def lmhead_sample(
     return tokens, logp
 
 
+def lmhead_logprob_fwd(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, temperature: float = 1.0,
+                       compute_entropy: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """No-grad log_softmax(hidden @ weight^T / T)[labels] (+ entropy) for hidden [T, K], labels [T]
+    (int64, any stride), through the MFMA GEMM's online-softmax epilogue: no [T, V] logits."""
+    dev = _lmhead_operands(hidden, weight)
+    T, K = hidden.shape
+    V = weight.shape[0]
+    lab = labels.to(device=dev, dtype=torch.int64)
+    if lab.dim() != 1 or lab.numel() != T:
+        raise ValueError("labels must be [T]")
+    logp = torch.empty(T, dtype=torch.float32, device=dev)
+    ent = torch.empty(T, dtype=torch.float32, device=dev) if compute_entropy else None
+    ws = WORKSPACES.get(dev, "lmhead_logprob", _ffi.query("skyrl_lmhead_logprob_workspace_bytes", T, V))
+    _ffi.call("skyrl_lmhead_logprob_fwd", _ptr(hidden), hidden.stride(0), _ptr(weight), weight.stride(0), T, V, K,
+              _ptr(lab), lab.stride(0), float(temperature), _ptr(logp), _ptr(ent), None, _ptr(ws), _stream(dev))
+    return logp, ent
+
+
 # ---------------------------------------------------------------------------- a9 pack
 def pack_experience(
     prompt_tokens: torch.Tensor, prompt_off: torch.Tensor,

@@ -185,3 +185,30 @@ def test_fused_sample_many_rows_steps_and_ties(dev, temp):
     tu, _ = ops.sample(z, temperature=temp, seed=4, seq_ids=ids, step=0)
     tf, _ = ops.lmhead_sample(hd, wd, temperature=temp, seed=4, seq_ids=ids, step=0)
     assert torch.equal(tf.cpu(), tu.cpu())
+
+
+@pytest.mark.parametrize("V,K,temp", [(151936, 1536, 1.0), (50257, 768, 0.6), (4099, 128, 1.0)])
+def test_lmhead_logprob_fwd_matches_oracle_and_chunked(dev, V, K, temp):
+    """Learner-side forward (old / ref log-probs): the GEMM's online-softmax epilogue equals the
+    fp32 oracle on the same bf16 logits (the kernel's own plain-GEMM output) and the chunked
+    hipBLASLt path (skyrl_amd.lmhead) -- ragged last tile, odd V, temperature (bf16 division
+    as the reference), labels at tile edges."""
+    from oracle import cpu_ref
+    from skyrl_amd import lmhead
+
+    g = torch.Generator().manual_seed(V + K)
+    T = 300
+    h = torch.randn(T, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(V, K, generator=g) * (3.0 / K ** 0.5)).to(torch.bfloat16)
+    lab = torch.randint(0, V, (T,), generator=g)
+    lab[:4] = torch.tensor([0, 255, 256, V - 1])
+    hd, wd = h.to(dev), w.to(dev)
+    lp, ent = ops.lmhead_logprob_fwd(hd, wd, lab.to(dev), temperature=temp)
+    z = ops.lmhead_gemm(hd, wd).cpu()
+    zt = (z.float() / temp).to(torch.bfloat16) if temp != 1.0 else z
+    torch.testing.assert_close(lp.cpu(), cpu_ref.logprobs_from_logits(zt, lab), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(ent.cpu(), cpu_ref.entropy_from_logits(zt), atol=1e-4, rtol=1e-5)
+    with torch.no_grad():
+        lc, ec = lmhead.lmhead_logprobs_and_entropy(hd, wd, lab.to(dev), temperature=temp)
+    torch.testing.assert_close(lp, lc, atol=2e-2, rtol=0)  # different GEMMs: bf16 logits may differ by an ulp
+    torch.testing.assert_close(ent, ec, atol=2e-2, rtol=0)
