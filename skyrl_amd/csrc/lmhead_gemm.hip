@@ -446,16 +446,28 @@ __global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* _
     const int row = blockIdx.x, lane = threadIdx.x;
     Best b{-INFINITY, 0x7fffffff};
     float bx = __builtin_nanf(""), m = -1e30f, s = 0.f;
-    for (int j = lane; j < nt; j += 64) {
-        const float4 p = parts[(int64_t)row * nt + j];
-        const int idx = __float_as_int(p.y);
-        if (better(p.x, idx, b)) {
-            b = Best{p.x, idx};
-            bx = part_x[(int64_t)row * nt + j];
+    // 8 partials per lane in flight before folding them (the fold is a dependent chain)
+    for (int j0 = lane; j0 < nt; j0 += 8 * 64) {
+        float4 pv[8];
+        float px[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u * 64;
+            pv[u] = j < nt ? parts[(int64_t)row * nt + j] : make_float4(-INFINITY, __int_as_float(0x7fffffff), -1e30f, 0.f);
+            px[u] = j < nt ? part_x[(int64_t)row * nt + j] : 0.f;
         }
-        const float mn = fmaxf(m, p.z);
-        s = s * fast_exp2((m - mn) * kLog2eG) + p.w * fast_exp2((p.z - mn) * kLog2eG);
-        m = mn;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float4 p = pv[u];
+            const int idx = __float_as_int(p.y);
+            if (better(p.x, idx, b)) {
+                b = Best{p.x, idx};
+                bx = px[u];
+            }
+            const float mn = fmaxf(m, p.z);
+            s = s * fast_exp2((m - mn) * kLog2eG) + p.w * fast_exp2((p.z - mn) * kLog2eG);
+            m = mn;
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
