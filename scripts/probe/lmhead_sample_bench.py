@@ -95,9 +95,33 @@ def learner_main():
                           "chunked_TFs": round(flops / (chunked * 1e-6) / 1e12, 1)}), flush=True)
 
 
+def gemm_sweep():
+    """Plain GEMM (STORE epilogue) per pipeline variant vs torch, interleaved passes."""
+    from skyrl_amd import _ffi
+
+    dev = torch.device("cuda")
+    H, V = 1536, 151936
+    w = (torch.randn(V, H, device=dev) * (3.0 / H ** 0.5)).to(torch.bfloat16)
+    for M in (512, 8192):
+        h = torch.randn(M, H, device=dev).to(torch.bfloat16)
+        z = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
+        flops = 2.0 * M * H * V
+        it = 20 if M <= 512 else 4
+        for rep in range(2):
+            res = {"M": M, "rep": rep, "torch_us": round(timeit(lambda: torch.matmul(h, w.T, out=z), it), 1)}
+            for pipe in (0, 4, 5, 6, 7, 2):
+                _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
+                res[f"pipe{pipe}_us"] = round(timeit(lambda: ops.lmhead_gemm(h, w, out=z), it), 1)
+            _ffi.call("skyrl_tune", b"lmhead_pipe", -1)
+            res["best_TFs"] = round(flops / (min(v for k, v in res.items() if k.startswith("pipe")) * 1e-6) / 1e12, 1)
+            print(json.dumps(res), flush=True)
+
+
 if __name__ == "__main__":
     import sys as _sys
-    if "--learner" in _sys.argv:
+    if "--gemm-sweep" in _sys.argv:
+        gemm_sweep()
+    elif "--learner" in _sys.argv:
         learner_main()
     else:
         main()

@@ -502,6 +502,8 @@ GemmKernel pick_kernel() {
         case 3: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1, 0>;
         case 4: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 1>;
         case 5: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1, 1>;
+        case 6: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 1>;
+        case 7: return lmhead_gemm_kernel<EPI, 256, 32, 3, 0, 1>;
         default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
@@ -519,7 +521,7 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }  // namespace
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 5, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..5");
+    SKYRL_REQUIRE(value >= -1 && value <= 7, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..7");
     g_lmhead_pipe = value < 0 ? 4 : value;
     return SKYRL_OK;
 }
