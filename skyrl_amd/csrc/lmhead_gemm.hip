@@ -155,7 +155,8 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         // after the first half of the k-steps, so a SIMD's MFMA pipe is never idle for both waves'
         // copy issue at once
         const bool late = STAGGER && __builtin_amdgcn_readfirstlane(w) >= G::kWaves / 2;
-        if (!late && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+        const bool more = t + S - 1 < nk;
+        if (DB != 2 && !late && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
         if constexpr (DB) {
             // explicit fragment pipeline: groups of 2 A fragments x 4 B fragments (8 MFMAs); the next
             // group's ds_reads are issued before this group's MFMAs, and sched_barriers keep the
@@ -177,7 +178,15 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
                 const int ks = g / 4, mp = g % 4;
-                if (late && g == NG / 2 && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+                if (late && g == NG / 2 && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
+                if (DB == 2 && more) {  // copies spread over the groups, in the pinned prefetch slot
+#pragma unroll
+                    for (int j = 0; j < G::kPieces; ++j)
+                        if (j * NG / G::kPieces == g)
+                            __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + (t + S - 1) * BKT),
+                                                             (lds_void*)(sdst + ((t + S - 1) % S) * G::kStageBytes + j * 1024),
+                                                             16, 0, 0);
+                }
                 if (g + 1 < NG) {
                     if ((g + 1) % 4 == 0) ldB((g + 1) / 4);
                     ldA((g + 1) / 4, (g + 1) % 4, aq[(g + 1) & 1]);
@@ -504,6 +513,8 @@ GemmKernel pick_kernel() {
         case 5: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1, 1>;
         case 6: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 1>;
         case 7: return lmhead_gemm_kernel<EPI, 256, 32, 3, 0, 1>;
+        case 8: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 2>;
+        case 9: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 2>;
         default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
@@ -521,7 +532,7 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }  // namespace
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 7, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..7");
+    SKYRL_REQUIRE(value >= -1 && value <= 9, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..9");
     g_lmhead_pipe = value < 0 ? 4 : value;
     return SKYRL_OK;
 }
