@@ -157,6 +157,38 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
         const bool late = STAGGER && __builtin_amdgcn_readfirstlane(w) >= G::kWaves / 2;
         const bool more = t + S - 1 < nk;
         if (DB != 2 && !late && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
+        if constexpr (DB == 3) {
+            // k-step granularity: all fragments of k-step ks + 1 are read while k-step ks's MFMAs run
+            // (issued after its first 8 MFMAs, so the compiler's lgkmcnt(0) -- it never counts LDS
+            // waits while an LDS DMA is in flight -- only waits for reads that had 24 MFMAs of time)
+            bf16x8 bq[G::KS][4], aq[G::KS][8];
+            auto ld = [&](int ks) {
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+#pragma unroll
+                for (int mb = 0; mb < 8; ++mb)
+                    aq[ks][mb] = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * G::kRowBytes);
+            };
+            ld(0);
+#pragma unroll
+            for (int ks = 0; ks < G::KS; ++ks) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int mb = 0; mb < 8; ++mb) {
+                    if (mb == 2 && ks + 1 < G::KS) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        ld(ks + 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks][mb], bq[ks][nb], acc[mb][nb], 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+        }
         if constexpr (DB) {
             // explicit fragment pipeline: groups of 2 A fragments x 4 B fragments (8 MFMAs); the next
             // group's ds_reads are issued before this group's MFMAs, and sched_barriers keep the
@@ -515,6 +547,7 @@ GemmKernel pick_kernel() {
         case 7: return lmhead_gemm_kernel<EPI, 256, 32, 3, 0, 1>;
         case 8: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 2>;
         case 9: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 2>;
+        case 10: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 3>;
         default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
@@ -532,7 +565,7 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 }  // namespace
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 9, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..9");
+    SKYRL_REQUIRE(value >= -1 && value <= 10, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..10");
     g_lmhead_pipe = value < 0 ? 4 : value;
     return SKYRL_OK;
 }
