@@ -366,3 +366,43 @@ def test_prefix_caching_shares_prompt_blocks_and_keeps_outputs():
             assert all(len(v) == 1 for v in first_blocks.values())  # siblings share block 0
             assert core.allocator.hits >= 9
     assert results[True] == results[False]
+
+
+def test_apply_penalties_matches_vllm_formula():
+    """ModelRunner._apply_penalties (CPU tensors, no kernel): repetition over prompt + output,
+    presence / frequency over output counts, only on rows that ask for them; the saved values
+    restore the raw logits exactly."""
+    import torch
+    from collections import Counter
+
+    from transformers import Qwen2Config
+
+    from skyrl_amd.inference_engines.engine import ModelRunner, Request, ScheduledBatch
+    from skyrl_amd.inference_engines.model import PagedDecoder
+
+    cfg = Qwen2Config(vocab_size=64, hidden_size=256, intermediate_size=256, num_hidden_layers=1,
+                      num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=128)
+    runner = ModelRunner(PagedDecoder(cfg, "cpu", seed=None), num_blocks=8, max_num_seqs=4)
+    g = torch.Generator().manual_seed(2)
+    V = 64
+    raw = (torch.randn(3, V, generator=g) * 2).to(torch.bfloat16)
+    pen = RequestParams(repetition_penalty=1.3, presence_penalty=0.5, frequency_penalty=0.25)
+    reqs = [Request(rid=0, prompt=[1, 2, 3], params=pen, key=0, out_tokens=[3, 3, 9, 40], row=0),
+            Request(rid=1, prompt=[5], params=RequestParams(), key=1, out_tokens=[5, 6], row=1),
+            Request(rid=2, prompt=[7, 8], params=RequestParams(presence_penalty=-1.0), key=2, out_tokens=[8, 8],
+                    row=2)]
+    logits = raw.clone()
+    batch = ScheduledBatch("decode", reqs, np.zeros(3, dtype=np.int64), [(), (), ()])
+    flat, saved, prow = runner._apply_penalties(logits, batch, np.arange(3))
+    assert prow.tolist() == [0, 2]
+    exp = raw.float().clone()
+    for i, r in ((0, reqs[0]), (2, reqs[2])):
+        p, c = r.params, Counter(r.out_tokens)
+        for t in sorted(set(r.prompt) | set(c)) if p.repetition_penalty != 1.0 else sorted(c):
+            x = exp[i, t]
+            x = x / p.repetition_penalty if x > 0 else x * p.repetition_penalty
+            exp[i, t] = x - (p.frequency_penalty * c[t] + (p.presence_penalty if c[t] else 0.0))
+    torch.testing.assert_close(logits.float(), exp.to(torch.bfloat16).float())
+    assert torch.equal(logits[1], raw[1])  # no penalty, untouched
+    logits.view(-1).index_copy_(0, flat, saved)
+    assert torch.equal(logits, raw)
