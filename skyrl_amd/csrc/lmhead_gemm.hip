@@ -77,149 +77,134 @@ struct Geo {
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// skyrl_tune("lmhead_pipe"): 0 = 256 x 256 tiles, BK 64, 2 stages, one 512-thread workgroup per CU;
-// 1 = 256 x 128 tiles, BK 32, 3 stages, two 256-thread workgroups per CU (one's epilogue
-// overlaps the other's MFMA loop); 2 = 256 x 256, BK 32, 4 stages. Measured at the config-2
-// decode shape (512 x 151,936 x 1536): 0 is fastest (260-276 us), 1 313 us, 2 284 us. (Spreading
-// the copies over the MFMA groups with sched_group_barrier produced a worse schedule: dropped.)
-int g_lmhead_pipe = 4;
+// skyrl_tune("lmhead_pipe") selects the K pipeline (pick_kernel): 0 = 256 x 256 tiles, BK 64, 2
+// stages, one 512-thread workgroup per CU; 1 = 256 x 128 tiles, BK 32, 3 stages, two workgroups
+// per CU; 2 = 256 x 256, BK 32, 4 stages; 3-10 = staggered copies / fragment double buffer /
+// spread copies; 11 = ping-pong wave groups (4 phases per K step); 12 (default) = the fragment
+// double buffer of 4 with three W stages and two H stages. All produce identical Z. Measured
+// (profiles/r02_gemm_*): 12 is the fastest at 512, 2048 and 8192 rows; 11 is slower
+// even without copies (8 barriers per K step).
+int g_lmhead_pipe = 12;
+
+// scripts/probe/gemm_noload.py only (never in the product build): the K loop re-reads the
+// prologue's tiles instead of copying new ones, to time the loop structure without memory.
+#ifdef SKYRL_GEMM_NOLOAD
+constexpr bool kNoLoad = true;
+#else
+constexpr bool kNoLoad = false;
+#endif
 
 template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
 __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
-    int mt, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
+    int mtg, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
     int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt, const int64_t* __restrict__ labels,
     int64_t lstride) {
     using G = Geo<BN, BKT, S>;
-    __shared__ __attribute__((aligned(16))) char smem[G::kLds];
+    // DB 5 keeps two H stages and three W stages: the whole 160 KB
+    __shared__ __attribute__((aligned(16))) char smem[DB == 5 ? 163840 : G::kLds];
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-    const int mtile = wg % mt, ntile = wg / mt;
+    // tile order: mtg = mt | gm << 16. gm = 0: M fastest over all M tiles (the M tiles sharing a W
+    // tile run together); gm > 0: groups of gm M tiles, M fastest inside a group, so an XCD's
+    // concurrent tiles share gm H tiles that stay L2-resident across the W tiles it walks
+    const int mt = mtg & 0xffff, gm = mtg >> 16;
+    int mtile, ntile;
+    if (gm <= 0 || gm >= mt) {
+        mtile = wg % mt;
+        ntile = wg / mt;
+    } else {
+        const int per = gm * nt, gi = wg / per, r = wg - gi * per, gsz = min(gm, mt - gi * gm);
+        mtile = gi * gm + r % gsz;
+        ntile = r / gsz;
+    }
     const int m0 = mtile * BM, n0 = ntile * BN;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int wm = w & 1, wn = w >> 1;
+    // DB 4 (ping-pong): wave group wm = w >> 2 holds one wave of each SIMD; otherwise wm = w & 1
+    const int wm = DB == 4 ? (w >> 2) : (w & 1), wn = DB == 4 ? (w & 3) : (w >> 1);
 
-    // staging: the stage is (BM + BN) operand rows (H rows, then W rows), copied as 1-KB pieces;
-    // wave w copies pieces w * kPieces + j (the piece's LDS offset is wave-uniform: p * 1 KB)
-    const int lrow = lane / G::kChunks, pc = lane % G::kChunks;
-    const uint16_t* gsrc[G::kPieces];
-#pragma unroll
-    for (int j = 0; j < G::kPieces; ++j) {
-        const int row = (w * G::kPieces + j) * G::kRowsPerPiece + lrow;  // stage row
-        const int c = pc ^ G::swz(row);  // the logical chunk that lands in physical chunk pc
-        const bool isw = row >= BM;
-        const int rloc = isw ? row - BM : row;
-        const int grow = isw ? min(n0 + rloc, N - 1) : min(m0 + rloc, M - 1);
-        gsrc[j] = (isw ? W + (int64_t)grow * ldw : H + (int64_t)grow * ldh) + c * 8;
-    }
-    char* const sdst = smem + w * G::kPieces * 1024;
-    auto stage = [&](int buf, int k0) {
-#pragma unroll
-        for (int j = 0; j < G::kPieces; ++j)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + k0),
-                                             (lds_void*)(sdst + buf * G::kStageBytes + j * 1024), 16, 0, 0);
-    };
-    // fragment offsets: rows wm*128 + mb*16 + (lane & 15) of H, wn*64 + nb*16 + (lane & 15) of W;
-    // k chunk ks*4 + (lane >> 4) (16x16x32 operand map); the swizzle depends on lane & 15 only
-    int aoff[G::KS], boff[G::KS];
-    {
-        const int sw = G::swz(lane & 15);
-#pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-            const int c = (ks * 4 + (lane >> 4)) ^ sw;
-            aoff[ks] = (wm * 128 + (lane & 15)) * G::kRowBytes + c * 16;
-            boff[ks] = G::kOpABytes + (wn * 64 + (lane & 15)) * G::kRowBytes + c * 16;
-        }
-    }
     f32x4 acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = K / BKT;
+    if constexpr (DB == 5) {
+        // Asymmetric stages: the W tile of K step t + 2 and the H tile of step t + 1 are in flight
+        // while step t computes. At the decode shape H (a few hundred rows) is L2-resident and W
+        // streams from HBM once, so the slow operand gets two steps of latency cover. LDS: H
+        // stages at [0, 64 KB), W stages at [64 KB, 160 KB), 256 rows x 128 B each, the 16-B
+        // chunk swizzle of Geo. Every wave copies 4 H and 4 W pieces per step, H first, so at the
+        // top of step t only W(t + 1)'s 4 copies may stay outstanding.
+        static_assert(BN == 256 && BKT == 64 && S == 2, "asymmetric-stage geometry");
+        constexpr int kT = 32768, kWBase = 2 * kT, kRow = 128;
+        const uint16_t* hs[4];
+        const uint16_t* wsrc[4];
 #pragma unroll
-    for (int p = 0; p < S - 1; ++p)
-        if (p < nk) stage(p, p * BKT);
-    for (int t = 0; t < nk; ++t) {
-        // tile t has landed once at most min(S - 2, nk - 1 - t) younger tiles are outstanding;
-        // every wave's fragment reads of the buffer restaged below are done (WAR), then the barrier
-        const int ahead = min(S - 2, nk - 1 - t);
-        if (ahead <= 0) wait_vmcnt<0>();
-        else if (ahead == 1) wait_vmcnt<G::kPieces>();
-        else wait_vmcnt<2 * G::kPieces>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        const char* sb = smem + (t % S) * G::kStageBytes;
-        // STAGGER: the waves of the upper half (the second wave of each SIMD) issue their copies
-        // after the first half of the k-steps, so a SIMD's MFMA pipe is never idle for both waves'
-        // copy issue at once
-        const bool late = STAGGER && __builtin_amdgcn_readfirstlane(w) >= G::kWaves / 2;
-        const bool more = t + S - 1 < nk;
-        if (DB != 2 && !late && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
-        if constexpr (DB == 3) {
-            // k-step granularity: all fragments of k-step ks + 1 are read while k-step ks's MFMAs run
-            // (issued after its first 8 MFMAs, so the compiler's lgkmcnt(0) -- it never counts LDS
-            // waits while an LDS DMA is in flight -- only waits for reads that had 24 MFMAs of time)
-            bf16x8 bq[G::KS][4], aq[G::KS][8];
-            auto ld = [&](int ks) {
-#pragma unroll
-                for (int nb = 0; nb < 4; ++nb)
-                    bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
-#pragma unroll
-                for (int mb = 0; mb < 8; ++mb)
-                    aq[ks][mb] = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * G::kRowBytes);
-            };
-            ld(0);
-#pragma unroll
-            for (int ks = 0; ks < G::KS; ++ks) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int mb = 0; mb < 8; ++mb) {
-                    if (mb == 2 && ks + 1 < G::KS) {
-                        __builtin_amdgcn_sched_barrier(0);
-                        ld(ks + 1);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-#pragma unroll
-                    for (int nb = 0; nb < 4; ++nb)
-                        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks][mb], bq[ks][nb], acc[mb][nb], 0, 0, 0);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            continue;
+        for (int j = 0; j < 4; ++j) {
+            const int row = (w * 4 + j) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ G::swz(row);
+            hs[j] = H + (int64_t)min(m0 + row, M - 1) * ldh + c * 8;
+            wsrc[j] = W + (int64_t)min(n0 + row, N - 1) * ldw + c * 8;
         }
-        if constexpr (DB) {
-            // explicit fragment pipeline: groups of 2 A fragments x 4 B fragments (8 MFMAs); the next
-            // group's ds_reads are issued before this group's MFMAs, and sched_barriers keep the
-            // compiler from sinking them (left alone it waits lgkmcnt(0) before every 8 MFMAs)
-            constexpr int NG = G::KS * 4;
-            bf16x8 bq[G::KS][4], aq[2][2];
+        char* const hdst = smem + w * 4 * 1024;
+        char* const wdst = smem + kWBase + w * 4 * 1024;
+        auto copyH = [&](int tile) {
+            if (kNoLoad && tile >= 1) return;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(hs[j] + tile * 64),
+                                                 (lds_void*)(hdst + (tile & 1) * kT + j * 1024), 16, 0, 0);
+        };
+        auto copyW = [&](int tile) {
+            if (kNoLoad && tile >= 2) return;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[j] + tile * 64),
+                                                 (lds_void*)(wdst + (tile % 3) * kT + j * 1024), 16, 0, 0);
+        };
+        int aoff[2], boff[2];
+        {
+            const int sw = G::swz(lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int c = (ks * 4 + (lane >> 4)) ^ sw;
+                aoff[ks] = (wm * 128 + (lane & 15)) * kRow + c * 16;
+                boff[ks] = kWBase + (wn * 64 + (lane & 15)) * kRow + c * 16;
+            }
+        }
+        const int nk = K / 64;
+        copyH(0);
+        copyW(0);
+        if (nk > 1) copyW(1);
+        for (int t = 0; t < nk; ++t) {
+            if (t + 1 < nk) wait_vmcnt<4>();
+            else wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            const char* sa = smem + (t & 1) * kT;
+            const char* sbw = smem + (t % 3) * kT;  // + boff's kWBase
+            if (t + 1 < nk) copyH(t + 1);
+            if (t + 2 < nk) copyW(t + 2);
+            // fragment pipeline of DB 1: groups of 2 A x 4 B fragments (8 MFMAs), the next group's
+            // ds_reads issued before this group's MFMAs
+            bf16x8 bq[2][4], aq[2][2];
             auto ldA = [&](int ks, int mp, bf16x8 (&dst)[2]) {
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
-                    dst[u] = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + (2 * mp + u) * 16 * G::kRowBytes);
+                    dst[u] = *reinterpret_cast<const bf16x8*>(sa + aoff[ks] + (2 * mp + u) * 16 * kRow);
             };
             auto ldB = [&](int ks) {
 #pragma unroll
                 for (int nb = 0; nb < 4; ++nb)
-                    bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+                    bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sbw + boff[ks] + nb * 16 * kRow);
             };
             ldB(0);
             ldA(0, 0, aq[0]);
 #pragma unroll
-            for (int g = 0; g < NG; ++g) {
+            for (int g = 0; g < 8; ++g) {
                 const int ks = g / 4, mp = g % 4;
-                if (late && g == NG / 2 && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
-                if (DB == 2 && more) {  // copies spread over the groups, in the pinned prefetch slot
-#pragma unroll
-                    for (int j = 0; j < G::kPieces; ++j)
-                        if (j * NG / G::kPieces == g)
-                            __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + (t + S - 1) * BKT),
-                                                             (lds_void*)(sdst + ((t + S - 1) % S) * G::kStageBytes + j * 1024),
-                                                             16, 0, 0);
-                }
-                if (g + 1 < NG) {
+                if (g + 1 < 8) {
                     if ((g + 1) % 4 == 0) ldB((g + 1) / 4);
                     ldA((g + 1) / 4, (g + 1) % 4, aq[(g + 1) & 1]);
                 }
@@ -232,20 +217,264 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
                             __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[g & 1][u], bq[ks][nb], acc[2 * mp + u][nb], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            continue;
         }
+    } else if constexpr (DB == 4) {
+        // Ping-pong schedule. The K tile's LDS buffer holds four 16-KB operand halves: A0 / A1 are
+        // the H rows of output-quadrant row 0 / 1 of both wave groups (group g's rows g*128 + q*64
+        // + r), B0 / B1 the W rows of quadrant column 0 / 1 of the four wave columns (wn*64 + q*32
+        // + r). A tile runs as four phases, one 64 x 32 output quadrant of every wave per phase
+        // ((0,0), (0,1), (1,1), (1,0): A0+B0, B1, A1, B0 fragment reads), each phase a load
+        // interval (fragment reads, one half-tile copy, counted vmcnt, lgkmcnt(0)), s_barrier,
+        // 16 MFMAs, s_barrier. Group 1 runs one barrier behind group 0, so on every SIMD one
+        // wave's MFMAs overlap the other wave's loads.
+        // Copies: phase 0 of tile t stages B0 of t + 1, phase 1 A1 of t + 1, phase 2 A0 of t + 2,
+        // phase 3 B1 of t + 2 -- each one phase after the last read of the half it overwrites (the
+        // reads were retired by lgkmcnt(0) before the barrier that ends their load interval), and
+        // at least four phases before its first read. The wait after a phase's copy retires the
+        // copies of three phases earlier and older (vmcnt <= 6), so a half staged at phase f is
+        // complete in every wave before the barrier that precedes the reads of phase f + 4.
+        static_assert(BN == 256 && BKT == 64 && S == 2, "ping-pong geometry");
+        constexpr int kHalf = 16384, kBuf = 4 * kHalf, kRow = 128;
+        const uint16_t* src[4][2];
 #pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-            if (late && ks == G::KS / 2 && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
-            bf16x8 b[4];
+        for (int h = 0; h < 4; ++h)
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+            for (int j = 0; j < 2; ++j) {
+                const int hr = (2 * w + j) * 8 + (lane >> 3);    // half row of this lane's 16 B
+                const int c = (lane & 7) ^ ((hr >> 1) & 7);      // logical chunk landing in chunk lane & 7
+                if (h < 2) {
+                    const int grow = min(m0 + (hr >> 6) * 128 + h * 64 + (hr & 63), M - 1);
+                    src[h][j] = H + (int64_t)grow * ldh + c * 8;
+                } else {
+                    const int grow = min(n0 + (hr >> 5) * 64 + (h - 2) * 32 + (hr & 31), N - 1);
+                    src[h][j] = W + (int64_t)grow * ldw + c * 8;
+                }
+            }
+        char* const cdst = smem + 2 * w * 1024;
+        auto copy = [&](int h, int tile) {
+            if (kNoLoad && tile >= 2) return;
 #pragma unroll
-            for (int mb = 0; mb < 8; ++mb) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * G::kRowBytes);
+            for (int j = 0; j < 2; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(src[h][j] + tile * 64),
+                                                 (lds_void*)(cdst + (tile & 1) * kBuf + h * kHalf + j * 1024), 16, 0, 0);
+        };
+        int aoff[2], boff[2];
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[nb], acc[mb][nb], 0, 0, 0);
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = (ks * 4 + (lane >> 4)) ^ ((lane & 15) >> 1);
+            aoff[ks] = (wm * 64 + (lane & 15)) * kRow + c * 16;
+            boff[ks] = 2 * kHalf + (wn * 32 + (lane & 15)) * kRow + c * 16;
+        }
+        const int nk = K / 64;
+        // copies issued by global phase f (0 or 1 half-tile)
+        auto issued = [&](int f) -> int { return f >= 0 && ((f & 3) < 2 ? (f >> 2) + 1 : (f >> 2) + 2) < nk; };
+        copy(0, 0);
+        copy(2, 0);
+        copy(3, 0);
+        copy(1, 0);
+        if (nk > 1) {
+            copy(0, 1);
+            copy(3, 1);
+            wait_vmcnt<4>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (wm == 1) __builtin_amdgcn_s_barrier();
+        bf16x8 fa[2][4], fb[2][2];
+        for (int t = 0; t < nk; ++t) {
+            const char* sb = smem + (t & 1) * kBuf;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int qm = p >> 1, qn = (p == 1 || p == 2) ? 1 : 0;
+                __builtin_amdgcn_sched_barrier(0);
+                if (p != 2) {
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                        for (int nb = 0; nb < 2; ++nb)
+                            fb[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + qn * kHalf + boff[ks] + nb * 16 * kRow);
+                }
+                if (p == 0 || p == 2) {
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                        for (int mb = 0; mb < 4; ++mb)
+                            fa[ks][mb] = *reinterpret_cast<const bf16x8*>(sb + qm * kHalf + aoff[ks] + mb * 16 * kRow);
+                }
+                const int f = 4 * t + p;
+                const int tc = p < 2 ? t + 1 : t + 2;
+                if (tc < nk) copy(p == 0 ? 2 : p == 1 ? 1 : p == 2 ? 0 : 3, tc);
+                switch (issued(f) + issued(f - 1) + issued(f - 2)) {
+                    case 0: wait_vmcnt<0>(); break;
+                    case 1: wait_vmcnt<2>(); break;
+                    case 2: wait_vmcnt<4>(); break;
+                    default: wait_vmcnt<6>(); break;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                        for (int nb = 0; nb < 2; ++nb)
+                            acc[4 * qm + mb][2 * qn + nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                fa[ks][mb], fb[ks][nb], acc[4 * qm + mb][2 * qn + nb], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+        if (wm == 0) __builtin_amdgcn_s_barrier();
+    } else {
+        // staging: the stage is (BM + BN) operand rows (H rows, then W rows), copied as 1-KB pieces;
+        // wave w copies pieces w * kPieces + j (the piece's LDS offset is wave-uniform: p * 1 KB)
+        const int lrow = lane / G::kChunks, pc = lane % G::kChunks;
+        const uint16_t* gsrc[G::kPieces];
+#pragma unroll
+        for (int j = 0; j < G::kPieces; ++j) {
+            const int row = (w * G::kPieces + j) * G::kRowsPerPiece + lrow;  // stage row
+            const int c = pc ^ G::swz(row);  // the logical chunk that lands in physical chunk pc
+            const bool isw = row >= BM;
+            const int rloc = isw ? row - BM : row;
+            const int grow = isw ? min(n0 + rloc, N - 1) : min(m0 + rloc, M - 1);
+            gsrc[j] = (isw ? W + (int64_t)grow * ldw : H + (int64_t)grow * ldh) + c * 8;
+        }
+        char* const sdst = smem + w * G::kPieces * 1024;
+        auto stage = [&](int buf, int k0) {
+            if (kNoLoad && k0 >= (S - 1) * BKT) return;
+#pragma unroll
+            for (int j = 0; j < G::kPieces; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + k0),
+                                                 (lds_void*)(sdst + buf * G::kStageBytes + j * 1024), 16, 0, 0);
+        };
+        // fragment offsets: rows wm*128 + mb*16 + (lane & 15) of H, wn*64 + nb*16 + (lane & 15) of W;
+        // k chunk ks*4 + (lane >> 4) (16x16x32 operand map); the swizzle depends on lane & 15 only
+        int aoff[G::KS], boff[G::KS];
+        {
+            const int sw = G::swz(lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < G::KS; ++ks) {
+                const int c = (ks * 4 + (lane >> 4)) ^ sw;
+                aoff[ks] = (wm * 128 + (lane & 15)) * G::kRowBytes + c * 16;
+                boff[ks] = G::kOpABytes + (wn * 64 + (lane & 15)) * G::kRowBytes + c * 16;
+            }
+        }
+
+        const int nk = K / BKT;
+#pragma unroll
+        for (int p = 0; p < S - 1; ++p)
+            if (p < nk) stage(p, p * BKT);
+        for (int t = 0; t < nk; ++t) {
+            // tile t has landed once at most min(S - 2, nk - 1 - t) younger tiles are outstanding;
+            // every wave's fragment reads of the buffer restaged below are done (WAR), then the barrier
+            const int ahead = min(S - 2, nk - 1 - t);
+            if (ahead <= 0) wait_vmcnt<0>();
+            else if (ahead == 1) wait_vmcnt<G::kPieces>();
+            else wait_vmcnt<2 * G::kPieces>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            const char* sb = smem + (t % S) * G::kStageBytes;
+            // STAGGER: the waves of the upper half (the second wave of each SIMD) issue their copies
+            // after the first half of the k-steps, so a SIMD's MFMA pipe is never idle for both waves'
+            // copy issue at once
+            const bool late = STAGGER && __builtin_amdgcn_readfirstlane(w) >= G::kWaves / 2;
+            const bool more = t + S - 1 < nk;
+            if (DB != 2 && !late && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
+            if constexpr (DB == 3) {
+                // k-step granularity: all fragments of k-step ks + 1 are read while k-step ks's MFMAs run
+                // (issued after its first 8 MFMAs, so the compiler's lgkmcnt(0) -- it never counts LDS
+                // waits while an LDS DMA is in flight -- only waits for reads that had 24 MFMAs of time)
+                bf16x8 bq[G::KS][4], aq[G::KS][8];
+                auto ld = [&](int ks) {
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+#pragma unroll
+                    for (int mb = 0; mb < 8; ++mb)
+                        aq[ks][mb] = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * G::kRowBytes);
+                };
+                ld(0);
+#pragma unroll
+                for (int ks = 0; ks < G::KS; ++ks) {
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int mb = 0; mb < 8; ++mb) {
+                        if (mb == 2 && ks + 1 < G::KS) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            ld(ks + 1);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+#pragma unroll
+                        for (int nb = 0; nb < 4; ++nb)
+                            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks][mb], bq[ks][nb], acc[mb][nb], 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                continue;
+            }
+            if constexpr (DB) {
+                // explicit fragment pipeline: groups of 2 A fragments x 4 B fragments (8 MFMAs); the next
+                // group's ds_reads are issued before this group's MFMAs, and sched_barriers keep the
+                // compiler from sinking them (left alone it waits lgkmcnt(0) before every 8 MFMAs)
+                constexpr int NG = G::KS * 4;
+                bf16x8 bq[G::KS][4], aq[2][2];
+                auto ldA = [&](int ks, int mp, bf16x8 (&dst)[2]) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+                        dst[u] = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + (2 * mp + u) * 16 * G::kRowBytes);
+                };
+                auto ldB = [&](int ks) {
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+                };
+                ldB(0);
+                ldA(0, 0, aq[0]);
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    const int ks = g / 4, mp = g % 4;
+                    if (late && g == NG / 2 && more) stage((t + S - 1) % S, (t + S - 1) * BKT);
+                    if (DB == 2 && more) {  // copies spread over the groups, in the pinned prefetch slot
+#pragma unroll
+                        for (int j = 0; j < G::kPieces; ++j)
+                            if (j * NG / G::kPieces == g)
+                                __builtin_amdgcn_global_load_lds((gbl_void*)(gsrc[j] + (t + S - 1) * BKT),
+                                                                 (lds_void*)(sdst + ((t + S - 1) % S) * G::kStageBytes + j * 1024),
+                                                                 16, 0, 0);
+                    }
+                    if (g + 1 < NG) {
+                        if ((g + 1) % 4 == 0) ldB((g + 1) / 4);
+                        ldA((g + 1) / 4, (g + 1) % 4, aq[(g + 1) & 1]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int nb = 0; nb < 4; ++nb)
+                            acc[2 * mp + u][nb] =
+                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[g & 1][u], bq[ks][nb], acc[2 * mp + u][nb], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                continue;
+            }
+#pragma unroll
+            for (int ks = 0; ks < G::KS; ++ks) {
+                if (late && ks == G::KS / 2 && t + S - 1 < nk) stage((t + S - 1) % S, (t + S - 1) * BKT);
+                bf16x8 b[4];
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const bf16x8*>(sb + boff[ks] + nb * 16 * G::kRowBytes);
+#pragma unroll
+                for (int mb = 0; mb < 8; ++mb) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(sb + aoff[ks] + mb * 16 * G::kRowBytes);
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[nb], acc[mb][nb], 0, 0, 0);
+                }
             }
         }
     }
@@ -534,6 +763,8 @@ inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
                             float, uint64_t, const int64_t*, int64_t, float4*, float*, int, const int64_t*, int64_t);
+int g_lmhead_group = 8;  // skyrl_tune("lmhead_group"): M tiles per group of the tile order (0: all)
+int group_for(int mt) { return g_lmhead_group > 0 && g_lmhead_group < mt ? g_lmhead_group : 0; }
 int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }  // pipe 3: 256, staggered copies
 template <int EPI>
 GemmKernel pick_kernel() {
@@ -548,6 +779,8 @@ GemmKernel pick_kernel() {
         case 8: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 2>;
         case 9: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 2>;
         case 10: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 3>;
+        case 11: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 4>;
+        case 12: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 5>;
         default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
@@ -564,9 +797,15 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 
 }  // namespace
 
+int lmhead_group_tune(int value) {
+    SKYRL_REQUIRE(value >= 0 && value < 4096, "skyrl_tune: lmhead_group must be in [0, 4096)");
+    g_lmhead_group = value;
+    return SKYRL_OK;
+}
+
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 10, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..10");
-    g_lmhead_pipe = value < 0 ? 4 : value;
+    SKYRL_REQUIRE(value >= -1 && value <= 12, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..12");
+    g_lmhead_pipe = value < 0 ? 12 : value;
     return SKYRL_OK;
 }
 }  // namespace skyrl
@@ -582,7 +821,7 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
     const int bn = tile_n(), mt = tiles(M, BM), nt = tiles(N, bn);
     hipLaunchKernelGGL(pick_kernel<EPI_STORE>(), dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream),
                        reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
-                       ld_weight, M, N, K, mt, reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
+                       ld_weight, M, N, K, mt | (group_for(mt) << 16), reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
                        nullptr, nullptr, nt, nullptr, 0ll);
     return check_launch("lmhead_gemm_kernel<store>");
 }
@@ -609,7 +848,7 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
     auto kern = greedy ? pick_kernel<EPI_GREEDY>() : pick_kernel<EPI_SAMPLE>();
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
-                       ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt, nullptr, 0ll, inv_t,
+                       ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt | (group_for(mt) << 16), nullptr, 0ll, inv_t,
                        seed, seq_ids, step, parts, part_x, nt, nullptr, 0ll);
     rc = check_launch("lmhead_gemm_kernel<sample>");
     if (rc) return rc;
@@ -636,7 +875,7 @@ extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, c
     float4* states = reinterpret_cast<float4*>(workspace);
     auto kern = pick_kernel<EPI_LOGPROB>();
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
-                       ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt, nullptr, 0ll,
+                       ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt | (group_for(mt) << 16), nullptr, 0ll,
                        temperature, temperature != 1.0f ? 1ull : 0ull, nullptr, 0ll, states, nullptr, nt, labels,
                        label_stride);
     rc = check_launch("lmhead_gemm_kernel<logprob>");

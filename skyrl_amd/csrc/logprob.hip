@@ -216,6 +216,7 @@ extern int g_train_ntstore;
 extern int g_grpo_slices;
 extern int g_loss_units;
 int lmhead_tune(int value);
+int lmhead_group_tune(int value);
 }
 
 extern "C" int skyrl_tune(const char* key, int value) {
@@ -249,6 +250,7 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "lmhead_pipe") return lmhead_tune(value);
+    if (k == "lmhead_group") return lmhead_group_tune(value);
     if (k == "logprob_nt") {
         g_tune.nt = value != 0;
         return SKYRL_OK;
