@@ -47,9 +47,9 @@ enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2, EPI_LOGPROB = 3 };
 
 // Tile geometry: BM (256) x BN output columns, NT = 2 BN threads as 2 (M) x BN/64 (N) waves of
 // 128 x 64 outputs; K in BKT-deep tiles through S LDS stages (S - 1 tiles in flight).
-template <int BN, int BKT, int S>
+template <int BN, int BKT, int S, int NTH = 2 * BN>
 struct Geo {
-    static constexpr int NT = 2 * BN;
+    static constexpr int NT = NTH;
     static constexpr int kWaves = NT / 64;
     static constexpr int kRowBytes = BKT * 2;                  // one operand row of a K tile
     static constexpr int kChunks = kRowBytes / 16;             // 16-B chunks per operand row
@@ -95,14 +95,17 @@ constexpr bool kNoLoad = false;
 #endif
 
 template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
-__global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_gemm_kernel(
+// DB 6 runs 4 waves of 128 x 128 outputs (one per SIMD, accumulators in AGPRs); the others run
+// 2 BN threads, two waves per SIMD.
+__global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves_per_eu(DB == 6 ? 1 : 2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mtg, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
     int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt, const int64_t* __restrict__ labels,
     int64_t lstride) {
-    using G = Geo<BN, BKT, S>;
-    // DB 5 keeps two H stages and three W stages: the whole 160 KB
-    __shared__ __attribute__((aligned(16))) char smem[DB == 5 ? 163840 : G::kLds];
+    using G = Geo<BN, BKT, S, DB == 6 ? 256 : 2 * BN>;
+    constexpr int NB = DB == 6 ? 8 : 4;  // 16-column accumulator tiles per wave
+    // DB 5 and 6 keep two H stages and three W stages: the whole 160 KB
+    __shared__ __attribute__((aligned(16))) char smem[DB == 5 || DB == 6 ? 163840 : G::kLds];
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
     // tile order: mtg = mt | gm << 16. gm = 0: M fastest over all M tiles (the M tiles sharing a W
@@ -121,15 +124,106 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
     const int m0 = mtile * BM, n0 = ntile * BN;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // DB 4 (ping-pong): wave group wm = w >> 2 holds one wave of each SIMD; otherwise wm = w & 1
+    // (DB 6: 2 x 2 waves of 128 x 128)
     const int wm = DB == 4 ? (w >> 2) : (w & 1), wn = DB == 4 ? (w & 3) : (w >> 1);
 
-    f32x4 acc[8][4];
+    f32x4 acc[8][NB];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (DB == 5) {
+    if constexpr (DB == 6) {
+        // Four waves, 128 x 128 outputs each (8 x 8 accumulators): per MFMA a wave reads 2/3 of
+        // the LDS bytes of the 128 x 64 layout (A and B fragments reused 8 times instead of 4 and
+        // 8), which matters because the glds writes share the LDS with the fragment reads.
+        // Staging as DB 5 (three W stages, two H stages); each wave copies 8 H and 8 W pieces.
+        static_assert(BN == 256 && BKT == 64 && S == 2, "4-wave geometry");
+        constexpr int kT = 32768, kWBase = 2 * kT, kRow = 128;
+        // piece j of wave w covers operand rows w*64 + 8j .. + 7; lane -> row + lane / 8, chunk
+        // lane & 7 (the chunk swizzle (row >> 1) & 7 alternates with j's parity)
+        const int brow = w * 64 + (lane >> 3);
+        // 32-bit element offsets (the host picks this pipeline only when M ldh and N ldw < 2^31)
+        uint32_t hoff[8], woff[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int row = brow + 8 * j;
+            const int c = (lane & 7) ^ G::swz(row);
+            hoff[j] = (uint32_t)min(m0 + row, M - 1) * (uint32_t)ldh + c * 8;
+            woff[j] = (uint32_t)min(n0 + row, N - 1) * (uint32_t)ldw + c * 8;
+        }
+        char* const hdst = smem + w * 8 * 1024;
+        char* const wdst = smem + kWBase + w * 8 * 1024;
+        auto copyH = [&](int tile) {
+            if (kNoLoad && tile >= 1) return;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(H + hoff[j] + tile * 64),
+                                                 (lds_void*)(hdst + (tile & 1) * kT + j * 1024), 16, 0, 0);
+        };
+        auto copyW = [&](int tile) {
+            if (kNoLoad && tile >= 2) return;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(W + woff[j] + tile * 64),
+                                                 (lds_void*)(wdst + (tile % 3) * kT + j * 1024), 16, 0, 0);
+        };
+        int aoff[2], boff[2];
+        {
+            const int sw = G::swz(lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int c = (ks * 4 + (lane >> 4)) ^ sw;
+                aoff[ks] = (wm * 128 + (lane & 15)) * kRow + c * 16;
+                boff[ks] = kWBase + (wn * 128 + (lane & 15)) * kRow + c * 16;
+            }
+        }
+        const int nk = K / 64;
+        copyH(0);
+        copyW(0);
+        if (nk > 1) copyW(1);
+        for (int t = 0; t < nk; ++t) {
+            if (t + 1 < nk) wait_vmcnt<8>();
+            else wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            const char* sa = smem + (t & 1) * kT;
+            const char* sbw = smem + (t % 3) * kT;  // + boff's kWBase
+            if (t + 1 < nk) copyH(t + 1);
+            if (t + 2 < nk) copyW(t + 2);
+            // groups of 2 A fragments x 8 B fragments (16 MFMAs); the next group's ds_reads (and
+            // the next k-step's 8 B fragments) are issued before this group's MFMAs
+            bf16x8 bq[2][8], aq[2][2];
+            auto ldA = [&](int ks, int mp, bf16x8 (&dst)[2]) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    dst[u] = *reinterpret_cast<const bf16x8*>(sa + aoff[ks] + (2 * mp + u) * 16 * kRow);
+            };
+            auto ldB = [&](int ks) {
+#pragma unroll
+                for (int nb = 0; nb < 8; ++nb)
+                    bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sbw + boff[ks] + nb * 16 * kRow);
+            };
+            ldB(0);
+            ldA(0, 0, aq[0]);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const int ks = g / 4, mp = g % 4;
+                if (g + 1 < 8) {
+                    if ((g + 1) % 4 == 0) ldB((g + 1) / 4);
+                    ldA((g + 1) / 4, (g + 1) % 4, aq[(g + 1) & 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int nb = 0; nb < 8; ++nb)
+                        acc[2 * mp + u][nb] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[g & 1][u], bq[ks][nb], acc[2 * mp + u][nb], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    } else if constexpr (DB == 5) {
         // Asymmetric stages: the W tile of K step t + 2 and the H tile of step t + 1 are in flight
         // while step t computes. At the decode shape H (a few hundred rows) is L2-resident and W
         // streams from HBM once, so the slow operand gets two steps of latency cover. LDS: H
@@ -486,11 +580,11 @@ __global__ __launch_bounds__(2 * BN) __attribute__((amdgpu_waves_per_eu(2))) voi
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+        for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = wm * 128 + mb * 16 + (lane >> 4) * 4 + i;
-                const int c = wn * 64 + nb * 16 + (lane & 15);
+                const int c = wn * (NB * 16) + nb * 16 + (lane & 15);
                 *reinterpret_cast<uint16_t*>(smem + G::img_off(r, c >> 3) + (c & 7) * 2) = f32_to_bf16(acc[mb][nb][i]);
             }
     __syncthreads();
@@ -765,10 +859,16 @@ using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, 
                             float, uint64_t, const int64_t*, int64_t, float4*, float*, int, const int64_t*, int64_t);
 int g_lmhead_group = 8;  // skyrl_tune("lmhead_group"): M tiles per group of the tile order (0: all)
 int group_for(int mt) { return g_lmhead_group > 0 && g_lmhead_group < mt ? g_lmhead_group : 0; }
-int tile_n() { return g_lmhead_pipe == 1 ? 128 : 256; }  // pipe 3: 256, staggered copies
+int tile_threads(int pipe) { return pipe == 13 ? 256 : 2 * (pipe == 1 ? 128 : 256); }
+// the pipeline for these operands: pipe 13 addresses them with 32-bit element offsets
+int pipe_for(int64_t M, int64_t ldh, int64_t N, int64_t ldw) {
+    if (g_lmhead_pipe == 13 && (M * ldh >= (int64_t(1) << 31) || N * ldw >= (int64_t(1) << 31))) return 12;
+    return g_lmhead_pipe;
+}
+int tile_n(int pipe) { return pipe == 1 ? 128 : 256; }  // pipe 3: 256, staggered copies
 template <int EPI>
-GemmKernel pick_kernel() {
-    switch (g_lmhead_pipe) {
+GemmKernel pick_kernel(int pipe) {
+    switch (pipe) {
         case 1: return lmhead_gemm_kernel<EPI, 128, 32, 3, 0, 0>;
         case 2: return lmhead_gemm_kernel<EPI, 256, 32, 4, 0, 0>;
         case 3: return lmhead_gemm_kernel<EPI, 256, 64, 2, 1, 0>;
@@ -781,6 +881,7 @@ GemmKernel pick_kernel() {
         case 10: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 3>;
         case 11: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 4>;
         case 12: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 5>;
+        case 13: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 6>;
         default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
@@ -804,7 +905,7 @@ int lmhead_group_tune(int value) {
 }
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 12, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..12");
+    SKYRL_REQUIRE(value >= -1 && value <= 13, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..13");
     g_lmhead_pipe = value < 0 ? 12 : value;
     return SKYRL_OK;
 }
@@ -818,8 +919,9 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
     if (rc) return rc;
     if (M == 0) return SKYRL_OK;
     SKYRL_REQUIRE(out && ld_out >= N, "lmhead_gemm: bad output");
-    const int bn = tile_n(), mt = tiles(M, BM), nt = tiles(N, bn);
-    hipLaunchKernelGGL(pick_kernel<EPI_STORE>(), dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream),
+    const int pipe = pipe_for(M, ld_hidden, N, ld_weight);
+    const int bn = tile_n(pipe), mt = tiles(M, BM), nt = tiles(N, bn);
+    hipLaunchKernelGGL(pick_kernel<EPI_STORE>(pipe), dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream),
                        reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
                        ld_weight, M, N, K, mt | (group_for(mt) << 16), reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
                        nullptr, nullptr, nt, nullptr, 0ll);
@@ -841,13 +943,14 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     SKYRL_REQUIRE(tokens_out && workspace, "lmhead_sample: null pointer");
     SKYRL_REQUIRE(temperature >= 0.f, "lmhead_sample: temperature must be >= 0");
     SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_sample: workspace must be 16-B aligned");
-    const int bn = tile_n(), mt = tiles(M, BM), nt = tiles(V, bn);
+    const int pipe = pipe_for(M, ld_hidden, V, ld_weight);
+    const int bn = tile_n(pipe), mt = tiles(M, BM), nt = tiles(V, bn);
     float4* parts = reinterpret_cast<float4*>(workspace);
     float* part_x = reinterpret_cast<float*>(parts + (size_t)M * nt);
     const bool greedy = temperature == 0.f;
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
-    auto kern = greedy ? pick_kernel<EPI_GREEDY>() : pick_kernel<EPI_SAMPLE>();
-    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
+    auto kern = greedy ? pick_kernel<EPI_GREEDY>(pipe) : pick_kernel<EPI_SAMPLE>(pipe);
+    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt | (group_for(mt) << 16), nullptr, 0ll, inv_t,
                        seed, seq_ids, step, parts, part_x, nt, nullptr, 0ll);
     rc = check_launch("lmhead_gemm_kernel<sample>");
@@ -871,10 +974,11 @@ extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, c
     SKYRL_REQUIRE(labels && logp_out && workspace, "lmhead_logprob_fwd: null pointer");
     SKYRL_REQUIRE(temperature > 0.f, "lmhead_logprob_fwd: temperature must be > 0");
     SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_logprob_fwd: workspace must be 16-B aligned");
-    const int bn = tile_n(), mt = tiles(T, BM), nt = tiles(V, bn);
+    const int pipe = pipe_for(T, ld_hidden, V, ld_weight);
+    const int bn = tile_n(pipe), mt = tiles(T, BM), nt = tiles(V, bn);
     float4* states = reinterpret_cast<float4*>(workspace);
-    auto kern = pick_kernel<EPI_LOGPROB>();
-    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(2 * bn), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
+    auto kern = pick_kernel<EPI_LOGPROB>(pipe);
+    hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt | (group_for(mt) << 16), nullptr, 0ll,
                        temperature, temperature != 1.0f ? 1ull : 0ull, nullptr, 0ll, states, nullptr, nt, labels,
                        label_stride);
