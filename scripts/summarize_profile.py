@@ -48,13 +48,18 @@ def main(tag):
         out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes ({tag})",
                "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch (gfx950)",
                "kernels": {}}
-        for k, d in pmc.items():
+        # one record per kernel base name: the template instance with the most dispatches (the
+        # bench's own launch shape; the per-vocab legs run other instances a few times each),
+        # every instance listed under "instances"
+        for k, d in sorted(pmc.items(), key=lambda kv: -len(kv[1]["FETCH_SIZE"])):
             f = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
             w = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
+            rec = {"fetch_KB": round(f, 1), "write_KB": round(w, 1), "hbm_bytes_per_launch": int((2 * f + w) * 1024),
+                   "dispatches": len(d["FETCH_SIZE"])}
             key = k.split("<")[0]
-            out["kernels"][key] = {"fetch_KB": round(f, 1), "write_KB": round(w, 1),
-                                   "hbm_bytes_per_launch": int((2 * f + w) * 1024),
-                                   "dispatches": len(d["FETCH_SIZE"])}
+            if key not in out["kernels"]:
+                out["kernels"][key] = dict(rec, instance=k, instances={})
+            out["kernels"][key]["instances"][k] = rec
         with open(os.path.join(DST, "pmc_traffic.json"), "w") as fh:
             json.dump(out, fh, indent=1)
     print("profiles written for", tag)
