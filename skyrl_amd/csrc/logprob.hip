@@ -215,6 +215,7 @@ extern int g_train_resident_nt;
 extern int g_train_ntstore;
 extern int g_grpo_slices;
 extern int g_loss_units;
+extern int g_sampler_row;
 int lmhead_tune(int value);
 int lmhead_group_tune(int value);
 }
@@ -250,6 +251,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "lmhead_pipe") return lmhead_tune(value);
+    if (k == "sampler_row") {
+        SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_row must be 0 or 1");
+        g_sampler_row = value;
+        return SKYRL_OK;
+    }
     if (k == "lmhead_group") return lmhead_group_tune(value);
     if (k == "logprob_nt") {
         g_tune.nt = value != 0;

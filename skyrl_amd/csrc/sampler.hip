@@ -28,6 +28,7 @@
 #pragma clang fp contract(off)
 
 namespace skyrl {
+int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 namespace {
 
 constexpr int kThreads = 256;
@@ -376,13 +377,35 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
 // 3 Gumbel-max without filters at T == 1 (the bound test reuses the lse exponentials).
 // NT threads per workgroup. Grid (row, split): with one split the workgroup owns the whole
 // row and finishes it alone; with several, the last-arriving split folds the partials.
-template <typename T, int MODE, int NT>
+// Phase timestamps for scripts/probe/sampler_phase_probe (compiled only there, never in the product).
+#ifdef SKYRL_SAMPLER_PHASE_PROBE
+__device__ uint64_t g_sphase[4096 * 8];
+#define SPHASE(k)                                                                              \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < 4096 && blockIdx.y == 0) {                        \
+            g_sphase[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                 \
+            if ((k) == 0) g_sphase[blockIdx.x * 8 + 7] = (uint64_t)__smid();                   \
+            if ((k) == 0) g_sphase[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg(20 | (3 << 11)); \
+        }                                                                                      \
+    } while (0)
+#else
+#define SPHASE(k) \
+    do {          \
+    } while (0)
+#endif
+
+// PRIO: the waves raise their issue priority with the fraction of their row still to stream
+// (3 in the first quarter ... 0 in the last), so of the two row workgroups sharing a CU the one
+// behind is issued first and both finish together (otherwise age priority lets the first-
+// dispatched one finish ~9 us ahead at T = 1 and the other streams its tail alone).
+template <typename T, int MODE, int NT, bool PRIO = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     int use_topp_rt, const RowFilter* __restrict__ filt, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters) {
     constexpr int NW = NT / kWave;
+    SPHASE(0);
     __shared__ Part s_part[NW];
     __shared__ int s_last;
     __shared__ float s_bar;  // best exact score found by any wave of this workgroup
@@ -718,9 +741,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
                 __syncthreads();
                 refresh_bar();
             }
+            SPHASE(1);
         }
         for (int base = 0; base < nfull; base += kStep) {
             const bool more = base + kStep < nfull;
+            if constexpr (PRIO) {
+                switch (((nfull - base) * 4 - 1) / nfull) {  // quarter of the row still ahead
+                    case 3: __builtin_amdgcn_s_setprio(3); break;
+                    case 2: __builtin_amdgcn_s_setprio(2); break;
+                    case 1: __builtin_amdgcn_s_setprio(1); break;
+                    default: __builtin_amdgcn_s_setprio(0); break;
+                }
+            }
             if (more) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
@@ -776,6 +808,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
         visit_vec(vals, g0, cnt, kPart);
     }
     Best best{best_s, best_i};
+    SPHASE(2);
 
     // wave reduce: best (score desc, idx asc) and (m, s)
 #pragma unroll
@@ -791,6 +824,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     }
     if (lane == 0) s_part[threadIdx.x / kWave] = Part{best.score, best.idx, m, s};
     __syncthreads();
+    SPHASE(3);
     Part p;
     if (threadIdx.x == 0) {
         p = s_part[0];
@@ -831,6 +865,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
         }
     }
     if (threadIdx.x == 0) {
+        SPHASE(4);
         tokens[row_i] = p.idx;
         if (logp_out) {
             const float lse = p.m + fast_log2(p.s) * kLn2;
@@ -853,7 +888,11 @@ template <typename T, int MODE>
 void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int64_t ld, int V, int chunk, float inv_t,
                  int use_topk, int use_minp, float ln_min_p, uint64_t seed, const int64_t* seq_ids, int64_t step,
                  int use_topp, const RowFilter* filt, int32_t* tokens, float* logp, Part* parts, unsigned* counters) {
-    if (row_mode)
+    if (row_mode && g_sampler_row == 1)
+        hipLaunchKernelGGL((sample_kernel<T, MODE, 512, true>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t,
+                           use_topk, use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts,
+                           counters);
+    else if (row_mode)
         hipLaunchKernelGGL((sample_kernel<T, MODE, 512>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
                            use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts, counters);
     else
