@@ -128,6 +128,37 @@ def main():
         _ffi.call("skyrl_tune", b"train_ntstore", 1)
         _ffi.call("skyrl_tune", b"train_resident_nt", 1024)
 
+    if on("fused_mb"):  # the fused pass at smaller micro-batches (bytes per launch vs rate)
+        from skyrl_amd import ppo_utils as pu
+        import ctypes
+
+        params = pu.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=True)
+        old = torch.randn((mb, R), device=dev, generator=gen) - 12
+        adv = torch.randn((mb, R), device=dev, generator=gen)
+        msk = torch.ones((mb, R), device=dev)
+        ref = old + 0.01
+        loss = torch.empty((), device=dev)
+        met = torch.empty(8, device=dev)
+        ws = torch.zeros(_ffi.query("skyrl_policy_train_workspace_bytes", mb, R), dtype=torch.uint8, device=dev)
+
+        def fused_m(x, m, off):
+            _ffi.call("skyrl_policy_train_fwd", ops._ptr(x[off:off + m]), _ffi.BF16, x.stride(0), x.stride(1), m, R, V,
+                      ops._ptr(labels), labels.stride(0), labels.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
+                      ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met), ops._ptr(lp),
+                      ops._ptr(ent), ops._ptr(dlog[off:off + m]), R * V, V, ops._ptr(ws), st)
+        times = {m: [] for m in (4, 8, 16)}
+        for _ in range(args.rounds):
+            for m in times:
+                # the same 2 x 16 sequences in launches of m
+                def run():
+                    for x in (x0, x1):
+                        for off in range(0, mb, m):
+                            fused_m(x, m, off)
+                times[m].append(timeit(run) / 2)
+        for m, t in times.items():
+            ms = statistics.median(t)
+            res[f"policy_train_fused_mb{m}"] = {"ms_per_16_seqs": ms, "GBps_hbm_algorithmic": rows * (V * 4 + 40) / ms / 1e6}
+
     if on("sample"):
         from skyrl_amd.config import SamplingParams
         from skyrl_amd.sampler import TokenSampler
