@@ -212,3 +212,31 @@ def test_lmhead_logprob_fwd_matches_oracle_and_chunked(dev, V, K, temp):
         lc, ec = lmhead.lmhead_logprobs_and_entropy(hd, wd, lab.to(dev), temperature=temp)
     torch.testing.assert_close(lp, lc, atol=2e-2, rtol=0)  # different GEMMs: bf16 logits may differ by an ulp
     torch.testing.assert_close(ent, ec, atol=2e-2, rtol=0)
+
+
+@pytest.mark.parametrize("group", [8, 4, 3, 0])
+def test_gemm_grouped_tile_order_exact(dev, group):
+    """The grouped tile order (skyrl_tune lmhead_group: M tiles per group, M fastest inside a group)
+    with a partial last group (M = 2600 -> 11 M tiles), exact on small-integer operands; the fused
+    sampler and the learner logprob epilogue give the same results under every order."""
+    from skyrl_amd import _ffi
+
+    g = torch.Generator().manual_seed(2600 + group)
+    M, V, K = 2600, 3000, 128
+    h, w = _ints((M, K), g, -2, 3), _ints((V, K), g, -2, 3)
+    w[:, 0] += torch.arange(V).remainder(5).to(torch.bfloat16)
+    hd, wd = h.to(dev), w.to(dev)
+    lab = torch.randint(0, V, (M,), generator=g).to(dev)
+    _ffi.call("skyrl_tune", b"lmhead_group", group)
+    try:
+        z = ops.lmhead_gemm(hd, wd)
+        tok, lp = ops.lmhead_sample(hd, wd, temperature=1.0, seed=9, step=2)
+        lpf, entf = ops.lmhead_logprob_fwd(hd, wd, lab)
+    finally:
+        _ffi.call("skyrl_tune", b"lmhead_group", 8)
+    assert torch.equal(z.cpu(), (h.float() @ w.float().T).to(torch.bfloat16))
+    tok_u, lp_u = ops.sample(z, temperature=1.0, seed=9, step=2)
+    assert torch.equal(tok, tok_u)
+    torch.testing.assert_close(lp, lp_u, atol=1e-4, rtol=0)
+    lpf_d, entf_d = ops.lmhead_logprob_fwd(hd, wd, lab)  # default order
+    assert torch.equal(lpf, lpf_d) and torch.equal(entf, entf_d)
