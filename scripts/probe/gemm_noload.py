@@ -14,19 +14,23 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(ROOT, "skyrl_amd", "csrc")
-OUT = os.path.join(HERE, "libgemm_noload.so")
+
+
+VARIANTS = {"noload": "-DSKYRL_GEMM_NOLOAD", "noload_h": "-DSKYRL_GEMM_NOLOAD_H", "noload_w": "-DSKYRL_GEMM_NOLOAD_W"}
 
 
 def build():
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
              "-Wno-unused-function", "-Wno-unused-parameter"]
-    obj = "/tmp/lmhead_gemm_noload.o"
-    subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-DSKYRL_GEMM_NOLOAD", "-c", os.path.join(CSRC, "lmhead_gemm.hip"),
-                    "-o", obj], check=True)
     others = [o for o in glob.glob(os.path.join(ROOT, "build", "obj", "*.o")) if not o.endswith("lmhead_gemm.o")]
-    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", obj, *others, "-o", OUT],
-                   check=True)
-    print("built", OUT)
+    for name, flag in VARIANTS.items():
+        obj = f"/tmp/lmhead_gemm_{name}.o"
+        subprocess.run(["/opt/rocm/bin/hipcc", *flags, flag, "-c", os.path.join(CSRC, "lmhead_gemm.hip"), "-o", obj],
+                       check=True)
+        out = os.path.join(HERE, f"libgemm_{name}.so")
+        subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", obj, *others, "-o", out],
+                       check=True)
+        print("built", out)
 
 
 def run():
@@ -38,13 +42,15 @@ def run():
     spec = importlib.util.spec_from_file_location("lsb", os.path.join(HERE, "lmhead_sample_bench.py"))
     lsb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(lsb)
-    shapes = ((8192, 8192), (512, 151936))
+    shapes = ((8192, 151936), (512, 151936))
+    lsb.PIPES = (12,)
     print(json.dumps({"lib": "product"}), flush=True)
     lsb.gemm_sweep(shapes)
-    _ffi._lib = None
-    _ffi.LIB_PATH = OUT
-    print(json.dumps({"lib": "noload"}), flush=True)
-    lsb.gemm_sweep(shapes)
+    for name in VARIANTS:
+        _ffi._lib = None
+        _ffi.LIB_PATH = os.path.join(HERE, f"libgemm_{name}.so")
+        print(json.dumps({"lib": name}), flush=True)
+        lsb.gemm_sweep(shapes)
 
 
 if __name__ == "__main__":

@@ -93,6 +93,17 @@ constexpr bool kNoLoad = true;
 #else
 constexpr bool kNoLoad = false;
 #endif
+// probe-only: drop only the H (NOLOAD_H) or only the W (NOLOAD_W) copies of pipe 12's K loop
+#ifdef SKYRL_GEMM_NOLOAD_H
+constexpr bool kNoLoadH = true;
+#else
+constexpr bool kNoLoadH = kNoLoad;
+#endif
+#ifdef SKYRL_GEMM_NOLOAD_W
+constexpr bool kNoLoadW = true;
+#else
+constexpr bool kNoLoadW = kNoLoad;
+#endif
 
 template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
 // DB 6 runs 4 waves of 128 x 128 outputs (one per SIMD, accumulators in AGPRs); the others run
@@ -244,14 +255,14 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
         char* const hdst = smem + w * 4 * 1024;
         char* const wdst = smem + kWBase + w * 4 * 1024;
         auto copyH = [&](int tile) {
-            if (kNoLoad && tile >= 1) return;
+            if (kNoLoadH && tile >= 1) return;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 __builtin_amdgcn_global_load_lds((gbl_void*)(hs[j] + tile * 64),
                                                  (lds_void*)(hdst + (tile & 1) * kT + j * 1024), 16, 0, 0);
         };
         auto copyW = [&](int tile) {
-            if (kNoLoad && tile >= 2) return;
+            if (kNoLoadW && tile >= 2) return;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[j] + tile * 64),
