@@ -39,7 +39,7 @@ def main():
                 b.record()
                 b.synchronize()
                 res.setdefault(f"T{T}_v{var}_us", []).append(round(a.elapsed_time(b) / 64 * 1e3, 2))
-    _ffi.call("skyrl_tune", b"sampler_row", 0)
+    _ffi.call("skyrl_tune", b"sampler_row", 1)
     print(json.dumps(res), flush=True)
 
 

@@ -33,6 +33,12 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kRowModeMinSeqs = 256;  // enough rows to fill the chip with one workgroup each
+// Workspace: a fixed-size region of per-row arrival counters first (only split mode, i.e. fewer
+// than kRowModeMinSeqs rows, uses them), so that the counters sit at the same place for every
+// batch size and never overlap another call's row filters or partials in a reused workspace (a
+// split-mode call after one with fewer rows would otherwise read that call's partials as
+// counters): every counter is zero at allocation and re-armed by its user.
+constexpr size_t kCounterBytes = (size_t)kRowModeMinSeqs * 4;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -398,20 +404,19 @@ __device__ uint64_t g_sphase[4096 * 8];
 // (3 in the first quarter ... 0 in the last), so of the two row workgroups sharing a CU the one
 // behind is issued first and both finish together (otherwise age priority lets the first-
 // dispatched one finish ~9 us ahead at T = 1 and the other streams its tail alone).
-template <typename T, int MODE, int NT, bool PRIO = false>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(
+// One work unit: split `split` of `nsplit` of row row_i (the whole row when nsplit == 1).
+template <typename T, int MODE, int NT, bool PRIO>
+__device__ __forceinline__ void sample_unit(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     int use_topp_rt, const RowFilter* __restrict__ filt, int32_t* __restrict__ tokens,
-    float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters) {
+    float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters, const int row_i,
+    const int split, const int nsplit) {
     constexpr int NW = NT / kWave;
     SPHASE(0);
     __shared__ Part s_part[NW];
     __shared__ int s_last;
     __shared__ float s_bar;  // best exact score found by any wave of this workgroup
-    const int row_i = blockIdx.x;
-    const int split = blockIdx.y;
-    const int nsplit = gridDim.y;
     const int lane = threadIdx.x & (kWave - 1);
     const T* row = logits + (int64_t)row_i * ld;
     const int v_beg = split * chunk;
@@ -875,6 +880,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
     if (nsplit > 1) rearm(counters + row_i);
 }
 
+#define SKYRL_SAMPLE_ARGS                                                                                     \
+    const T *__restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt, int use_minp_rt, \
+        float ln_min_p, uint64_t seed, const int64_t *__restrict__ seq_ids, int64_t step, int use_topp_rt,     \
+        const RowFilter *__restrict__ filt, int32_t *__restrict__ tokens, float *__restrict__ logp_out,         \
+        Part *__restrict__ parts, unsigned *__restrict__ counters
+#define SKYRL_SAMPLE_PASS                                                                                   \
+    logits, ld, V, chunk, inv_t, use_topk_rt, use_minp_rt, ln_min_p, seed, seq_ids, step, use_topp_rt, filt, \
+        tokens, logp_out, parts, counters
+
+// Static grid: block (row, split).
+template <typename T, int MODE, int NT, bool PRIO = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(SKYRL_SAMPLE_ARGS) {
+    sample_unit<T, MODE, NT, PRIO>(SKYRL_SAMPLE_PASS, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
 int splits_for(int nseq, int V) {
     if (nseq <= 0 || V <= 0 || nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
     int s = (2048 + nseq - 1) / nseq;
@@ -912,7 +932,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     chunk = (chunk + 15) & ~15;
     char* w = reinterpret_cast<char*>(ws);
     unsigned* counters = reinterpret_cast<unsigned*>(w);
-    size_t off = ws_align((size_t)nseq * 4);
+    size_t off = kCounterBytes;
     RowFilter* filt = reinterpret_cast<RowFilter*>(w + off);
     off += ws_align((size_t)nseq * sizeof(RowFilter));
     Part* parts = reinterpret_cast<Part*>(w + off);
@@ -952,7 +972,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
 using namespace skyrl;
 
 extern "C" size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V) {
-    return ws_align((size_t)nseq * 4) + ws_align((size_t)nseq * sizeof(RowFilter)) +
+    return kCounterBytes + ws_align((size_t)nseq * sizeof(RowFilter)) +
            (size_t)nseq * splits_for(nseq, V) * sizeof(Part) + 256;
 }
 

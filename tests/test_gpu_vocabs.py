@@ -48,6 +48,24 @@ def test_sampler_bit_exact_per_vocab(dev, V, cfg):
         close(lp, elp, atol=1e-4)
 
 
+def test_sampler_workspace_reused_across_batch_sizes(dev):
+    """One cached sampler workspace serves calls of any batch size (the engine's decode batches
+    grow and shrink): split-mode calls after calls with fewer or more rows, with and without the
+    filter pre-pass, keep the oracle's tokens (the arrival counters sit in a fixed region that no
+    other call's filters or partials overlap)."""
+    from oracle import sampler as osamp
+
+    V = 4100
+    g = torch.Generator().manual_seed(4100)
+    for step, (n, top_p) in enumerate([(6, 0.9), (200, 1.0), (3, 1.0), (130, 0.8), (300, 1.0), (64, 1.0)]):
+        x = (torch.randn(n, V, generator=g) * 3).to(torch.bfloat16)
+        ids = torch.arange(n, dtype=torch.int64) + 1
+        tok, lp = ops.sample(x.to(dev), temperature=1.0, top_p=top_p, seed=21, seq_ids=ids.to(dev), step=step)
+        etok, elp = osamp.sample(x, 1.0, -1, top_p, 0.0, 21, ids, step)
+        assert torch.equal(tok.cpu(), etok), (n, top_p)
+        close(lp, elp, atol=1e-4)
+
+
 @pytest.mark.parametrize("V", VOCABS)
 def test_logprob_entropy_per_vocab(dev, V):
     """The model-wrapper slice logits[:, -R-1:-1] of [n, S, V] (model_wrapper.py:370), fwd + bwd."""
