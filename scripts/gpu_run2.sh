@@ -1,4 +1,8 @@
 set -eu
 mkdir -p gpurun_out
-timeout -k 10 120 python -u scripts/probe/ws_reuse_check.py > gpurun_out/ws_reuse_old.log 2>&1 || true
-grep -v amdgpu.ids gpurun_out/ws_reuse_old.log | tail -8
+export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests/test_gpu_lmhead_sample.py tests/test_gpu_engine.py -x -q --timeout 200 --timeout-method thread > gpurun_out/lm_coop_tests.log 2>&1 || { tail -30 gpurun_out/lm_coop_tests.log; exit 1; }
+tail -1 gpurun_out/lm_coop_tests.log
+timeout -k 10 200 python -u scripts/probe/lmhead_phase_probe.py run > gpurun_out/lmhead_phase2.json 2> gpurun_out/lmhead_phase2.err
+timeout -k 10 300 python -u scripts/probe/lmhead_sample_bench.py --T 1.0 0.0 --M 512 256 64 8 > gpurun_out/lms_bench_coop.json 2> gpurun_out/lms_bench_coop.err
+cat gpurun_out/lms_bench_coop.json

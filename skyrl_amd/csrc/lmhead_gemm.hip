@@ -105,9 +105,23 @@ constexpr bool kNoLoadW = true;
 constexpr bool kNoLoadW = kNoLoad;
 #endif
 
-template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
+// Phase timestamps for scripts/probe/lmhead_phase_probe (compiled only there, never in the product).
+#ifdef SKYRL_GEMM_PHASE_PROBE
+__device__ uint64_t g_gphase[4096 * 8];
+#define GPHASE(k)                                                                   \
+    do {                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                  \
+            g_gphase[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();      \
+    } while (0)
+#else
+#define GPHASE(k) \
+    do {          \
+    } while (0)
+#endif
+
 // DB 6 runs 4 waves of 128 x 128 outputs (one per SIMD, accumulators in AGPRs); the others run
 // 2 BN threads, two waves per SIMD.
+template <int EPI, int BN, int BKT, int S, int STAGGER, int DB>
 __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves_per_eu(DB == 6 ? 1 : 2))) void lmhead_gemm_kernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mtg, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
@@ -122,6 +136,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
     // tile order: mtg = mt | gm << 16. gm = 0: M fastest over all M tiles (the M tiles sharing a W
     // tile run together); gm > 0: groups of gm M tiles, M fastest inside a group, so an XCD's
     // concurrent tiles share gm H tiles that stay L2-resident across the W tiles it walks
+    GPHASE(0);
     const int mt = mtg & 0xffff, gm = mtg >> 16;
     int mtile, ntile;
     if (gm <= 0 || gm >= mt) {
@@ -587,6 +602,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 
+    GPHASE(1);
     // ---- epilogue: bf16 tile into the LDS image (C map: row (lane >> 4) * 4 + i, col lane & 15)
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb)
@@ -599,6 +615,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                 *reinterpret_cast<uint16_t*>(smem + G::img_off(r, c >> 3) + (c & 7) * 2) = f32_to_bf16(acc[mb][nb][i]);
             }
     __syncthreads();
+    GPHASE(2);
 
     if constexpr (EPI == EPI_STORE) {
         const bool vec = (ldz & 7) == 0 && (reinterpret_cast<uintptr_t>(Z) & 15) == 0;
@@ -745,6 +762,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
             }
         }
         if constexpr (!greedy) {
+            GPHASE(3);
             float bar = best_s;
 #pragma unroll
             for (int o = 1; o < TPR; o <<= 1) bar = fmaxf(bar, __shfl_xor(bar, o, kWave));
@@ -788,6 +806,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                 }
             }
         }
+        GPHASE(4);
         // fold the row's TPR threads (adjacent lanes)
 #pragma unroll
         for (int o = 1; o < TPR; o <<= 1) {
@@ -804,6 +823,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
             s = s * fast_exp2((m - mn) * kLog2eG) + oss * fast_exp2((om - mn) * kLog2eG);
             m = mn;
         }
+        GPHASE(5);
         if (hh == 0) {
             const int64_t pi = (int64_t)grow * nt + ntile;
             parts[pi] = make_float4(best_s, __int_as_float(best_i), m, s);
