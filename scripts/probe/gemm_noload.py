@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(ROOT, "skyrl_amd", "csrc")
 
 
-VARIANTS = {"noload": "-DSKYRL_GEMM_NOLOAD", "noload_h": "-DSKYRL_GEMM_NOLOAD_H", "noload_w": "-DSKYRL_GEMM_NOLOAD_W"}
+VARIANTS = {"noload": "-DSKYRL_GEMM_NOLOAD"}
 
 
 def build():
@@ -43,7 +43,7 @@ def run():
     lsb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(lsb)
     shapes = ((8192, 151936), (512, 151936))
-    lsb.PIPES = (12,)
+    lsb.PIPES = (12, 14)
     print(json.dumps({"lib": "product"}), flush=True)
     lsb.gemm_sweep(shapes)
     for name in VARIANTS:

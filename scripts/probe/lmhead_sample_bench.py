@@ -95,7 +95,7 @@ def learner_main():
                           "chunked_TFs": round(flops / (chunked * 1e-6) / 1e12, 1)}), flush=True)
 
 
-PIPES = (12, 13)
+PIPES = (12, 14)
 
 
 def gemm_sweep(shapes=((512, 151936), (8192, 151936))):

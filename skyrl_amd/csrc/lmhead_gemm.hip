@@ -159,7 +159,88 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (DB == 6) {
+    if constexpr (DB == 7) {
+        // W fragments straight from global memory into registers (no LDS write or read for W), H
+        // through two LDS stages with global_load_lds. Step t's W fragments are loaded at the top of
+        // step t - 1 into the other register buffer; each row's 128 B of a K step are read as two
+        // 64-B halves by the 16-lane groups (ks = 0, 1), and the two waves of a wave column read the
+        // same fragments (the second from L1).
+        static_assert(BN == 256 && BKT == 64 && S == 2, "W-in-registers geometry");
+        constexpr int kT = 32768, kRow = 128;
+        const uint16_t* hs[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = (w * 4 + j) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ G::swz(row);
+            hs[j] = H + (int64_t)min(m0 + row, M - 1) * ldh + c * 8;
+        }
+        char* const hdst = smem + w * 4 * 1024;
+        auto copyH = [&](int tile) {
+            if (kNoLoad && tile >= 1) return;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(hs[j] + tile * 64),
+                                                 (lds_void*)(hdst + (tile & 1) * kT + j * 1024), 16, 0, 0);
+        };
+        const uint16_t* wrow[4];  // this lane's W row of each 16-column fragment, at its k offset
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+            wrow[nb] = W + (int64_t)min(n0 + wn * 64 + nb * 16 + (lane & 15), N - 1) * ldw + (lane >> 4) * 8;
+        bf16x8 bw[2][2][4];  // [buffer][ks][nb]
+        auto loadW = [&](int buf, int tile) {
+            if (kNoLoad && tile >= 1) return;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    bw[buf][ks][nb] = *reinterpret_cast<const bf16x8*>(wrow[nb] + tile * 64 + ks * 32);
+        };
+        int aoff[2];
+        {
+            const int sw = G::swz(lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) aoff[ks] = (wm * 128 + (lane & 15)) * kRow + (((ks * 4 + (lane >> 4)) ^ sw) * 16);
+        }
+        const int nk = K / 64;
+        copyH(0);
+        loadW(0, 0);
+        // one K step with the W fragments in register buffer CB (compile-time: no selects)
+        auto kstep = [&](int t, auto cb_tag) {
+            constexpr int CB = decltype(cb_tag)::value;
+            wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            const char* sa = smem + (t & 1) * kT;
+            if (t + 1 < nk) {
+                copyH(t + 1);
+                loadW(1 - CB, t + 1);
+            }
+            bf16x8 aq[2][2];
+            auto ldA = [&](int ks, int mp, bf16x8 (&dst)[2]) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    dst[u] = *reinterpret_cast<const bf16x8*>(sa + aoff[ks] + (2 * mp + u) * 16 * kRow);
+            };
+            ldA(0, 0, aq[0]);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const int ks = g / 4, mp = g % 4;
+                if (g + 1 < 8) ldA((g + 1) / 4, (g + 1) % 4, aq[(g + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[2 * mp + u][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            aq[g & 1][u], bw[CB][ks][nb], acc[2 * mp + u][nb], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        for (int t = 0; t < nk; t += 2) {
+            kstep(t, std::integral_constant<int, 0>{});
+            if (t + 1 < nk) kstep(t + 1, std::integral_constant<int, 1>{});
+        }
+    } else if constexpr (DB == 6) {
         // Four waves, 128 x 128 outputs each (8 x 8 accumulators): per MFMA a wave reads 2/3 of
         // the LDS bytes of the 128 x 64 layout (A and B fragments reused 8 times instead of 4 and
         // 8), which matters because the glds writes share the LDS with the fragment reads.
@@ -913,6 +994,7 @@ GemmKernel pick_kernel(int pipe) {
         case 11: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 4>;
         case 12: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 5>;
         case 13: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 6>;
+        case 14: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 7>;
         default: return lmhead_gemm_kernel<EPI, 256, 64, 2, 0, 0>;
     }
 }
@@ -936,7 +1018,7 @@ int lmhead_group_tune(int value) {
 }
 
 int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 13, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..13");
+    SKYRL_REQUIRE(value >= -1 && value <= 14, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..14");
     g_lmhead_pipe = value < 0 ? 12 : value;
     return SKYRL_OK;
 }

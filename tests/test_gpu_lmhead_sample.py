@@ -33,7 +33,7 @@ def test_gemm_exact_small_integers(dev, M, V, K):
     assert torch.equal(z.cpu(), ref)
 
 
-@pytest.mark.parametrize("pipe", list(range(14)))
+@pytest.mark.parametrize("pipe", list(range(15)))
 @pytest.mark.parametrize("K", [64, 128, 192, 1536])
 def test_gemm_pipeline_variants_exact(dev, pipe, K):
     """Every tile/pipeline variant (256x256 BK 64 x 2 stages, 256x128 BK 32 x 3, 256x256 BK 32 x 4),
