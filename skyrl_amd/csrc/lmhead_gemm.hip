@@ -74,6 +74,20 @@ struct Geo {
     __device__ static int img_off(int r, int c) { return r * kImgRow + ((c ^ ((r & (16 / TPR - 1)) * TPR)) << 4); }
 };
 
+// Cross-tile row bar of the sampling epilogue: the best exact score any finished tile of the row
+// found, as an order-preserving 32-bit key (atomic max in global memory); 0 = none yet (also the
+// zeroed workspace and what the merge kernel re-arms it to).
+__device__ __forceinline__ unsigned bar_key(float sc) {
+    const uint32_t u = __float_as_uint(sc + 0.0f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float bar_value(unsigned k) {
+    if (k <= 0x007fffffu) return -INFINITY;  // none yet (or -inf)
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+// hardware natural log (v_log_f32 is log2): within ~3e-6 of det_ln for the arguments here
+__device__ __forceinline__ float hw_ln(float x) { return __builtin_amdgcn_logf(x) * kLn2G; }
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
@@ -126,7 +140,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
     int mtg, uint16_t* __restrict__ Z, int64_t ldz, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
     int64_t step, float4* __restrict__ parts, float* __restrict__ part_x, int nt, const int64_t* __restrict__ labels,
-    int64_t lstride) {
+    int64_t lstride, unsigned* __restrict__ rowbar) {
     using G = Geo<BN, BKT, S, DB == 6 ? 256 : 2 * BN>;
     constexpr int NB = DB == 6 ? 8 : 4;  // 16-column accumulator tiles per wave
     // DB 5 and 6 keep two H stages and three W stages: the whole 160 KB
@@ -820,33 +834,49 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                     best_x = vmax;
                 }
             } else {
+                // Bounds only: L~ = -ln E_g by the hardware log of the exact E_g (absolute error
+                // < 1e-6 against -det_ln(E_g) for E_g >= 7e-9, the smallest E_g there is); the slack
+                // of a non-min slot (E = E_g + (-det_ln U) >= E_g - 1.2e-6, so its exact score is
+                // <= x inv_t + L + 1.4e-6 / E_g + 4e-6) is generous on both and infinite when E_g is
+                // too small for it. The group whose minimum slot has the best approximate score gets
+                // one exact score below: the tile's bar.
                 const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
                 const int p = (int)(h & 7u);
-                const float Eg = group_min_e(h);
-                const float L = -det_ln(Eg);
+                const float eg = group_min_e(h);
+                const float L = -hw_ln(eg);
                 lng[i] = L;
-                // a non-min slot's E = E_g + (-det_ln U) >= E_g - 1.2e-6 (det_ln error), so its exact
-                // score is <= x inv_t + L + 1.4e-6 / E_g + 4e-6 (det_ln and rounding errors); slack is
-                // generous on both, and infinite (every slot a candidate) when E_g is too small for it
-                slack[i] = Eg < 1e-5f ? INFINITY : 1e-4f + 4e-6f / Eg;
+                slack[i] = eg < 1e-5f ? INFINITY : 2e-4f + 5e-6f / eg;
                 float xp = x[0];
 #pragma unroll
                 for (int k = 1; k < 8; ++k) xp = (k == p) ? x[k] : xp;
                 if (p < cnt) {
-                    const float sc = xp * inv_t + L;  // = noise_score(xp, inv_t, v0 + p, h, Eg, key2)
-                    if (better(sc, v0 + p, Best{best_s, best_i})) {
-                        best_s = sc;
+                    const float ap = xp * inv_t + L;
+                    if (ap > best_s) {  // approximate: which minimum slot to score exactly
+                        best_s = ap;
                         best_i = v0 + p;
-                        best_x = xp;
                     }
                 }
             }
         }
         if constexpr (!greedy) {
             GPHASE(3);
-            float bar = best_s;
+            // the tile's bar: the exact score of the approximately best minimum slot of this thread
+            // (max over the row's threads), raised to the best exact score the row's finished tiles
+            // published (rowbar); both are exact scores of elements some tile reports
+            float bar = -INFINITY;
+            if (best_i != 0x7fffffff) {
+                const int c = (best_i - n0) >> 3, k = (best_i - n0) & 7;
+                const float xp = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + G::img_off(r, c) + k * 2));
+                const uint32_t h = ehash(key, keyb, (uint32_t)best_i >> 3);
+                bar = noise_score(xp, inv_t, best_i, h, group_min_e(h), key2);
+                best_s = bar;
+                best_x = xp;
+            } else {
+                best_s = -INFINITY;
+            }
 #pragma unroll
             for (int o = 1; o < TPR; o <<= 1) bar = fmaxf(bar, __shfl_xor(bar, o, kWave));
+            if (rowbar) bar = fmaxf(bar, bar_value(rowbar[grow]));
             // pass 2: non-min slots whose bound reaches the bar, as a bit mask (bit 8 i + k)
             uint32_t cm[NC / 4];
 #pragma unroll
@@ -856,7 +886,8 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                 const int v0 = n0 + (TPR * i + hh) * 8;
                 const int cnt = min(8, N - v0);
                 const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
-                const float lim = bar - lng[i] - slack[i];  // x inv_t >= lim can reach the bar
+                // x inv_t >= lim can reach the bar (the rounding of x inv_t + L is inside 1e-6 |bar|)
+                const float lim = bar - lng[i] - slack[i] - 1e-6f * fabsf(bar);
                 uint32_t bm = 0u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
@@ -865,8 +896,7 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                 }
                 cm[i >> 2] |= bm << ((i & 3) * 8);
             }
-            // exact scores of the candidates, one per lane per trip (the min slot re-scores to the
-            // value pass 1 already has: harmless)
+            // exact scores of the candidates (minimum slots included), one per lane per trip
 #pragma unroll
             for (int wd = 0; wd < NC / 4; ++wd) {
                 uint32_t bm = cm[wd];
@@ -906,6 +936,10 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
         }
         GPHASE(5);
         if (hh == 0) {
+            if constexpr (!greedy) {
+                if (rowbar && best_i != 0x7fffffff)
+                    __hip_atomic_fetch_max(rowbar + grow, bar_key(best_s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             const int64_t pi = (int64_t)grow * nt + ntile;
             parts[pi] = make_float4(best_s, __int_as_float(best_i), m, s);
             part_x[pi] = best_x;
@@ -918,8 +952,10 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
 __global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* __restrict__ parts,
                                                                  const float* __restrict__ part_x, int nt,
                                                                  int32_t* __restrict__ tokens,
-                                                                 float* __restrict__ logp_out) {
+                                                                 float* __restrict__ logp_out,
+                                                                 unsigned* __restrict__ rowbar) {
     const int row = blockIdx.x, lane = threadIdx.x;
+    if (rowbar && lane == 0) rowbar[row] = 0u;  // re-arm the row's cross-tile bar (every tile is done)
     Best b{-INFINITY, 0x7fffffff};
     float bx = __builtin_nanf(""), m = -1e30f, s = 0.f;
     // 8 partials per lane in flight before folding them (the fold is a dependent chain)
@@ -968,7 +1004,8 @@ __global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* _
 inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
-                            float, uint64_t, const int64_t*, int64_t, float4*, float*, int, const int64_t*, int64_t);
+                            float, uint64_t, const int64_t*, int64_t, float4*, float*, int, const int64_t*, int64_t,
+                            unsigned*);
 int g_lmhead_group = 8;  // skyrl_tune("lmhead_group"): M tiles per group of the tile order (0: all)
 int group_for(int mt) { return g_lmhead_group > 0 && g_lmhead_group < mt ? g_lmhead_group : 0; }
 int tile_threads(int pipe) { return pipe == 13 ? 256 : 2 * (pipe == 1 ? 128 : 256); }
@@ -1037,13 +1074,19 @@ extern "C" int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const vo
     hipLaunchKernelGGL(pick_kernel<EPI_STORE>(pipe), dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream),
                        reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
                        ld_weight, M, N, K, mt | (group_for(mt) << 16), reinterpret_cast<uint16_t*>(out), ld_out, 1.f, 0ull, nullptr, 0ll,
-                       nullptr, nullptr, nt, nullptr, 0ll);
+                       nullptr, nullptr, nt, nullptr, 0ll, nullptr);
     return check_launch("lmhead_gemm_kernel<store>");
 }
 
+// Sampling workspace: the cross-tile row bars first, in a fixed region (the same place for every
+// row count: zero at allocation, re-armed by the merge kernel; calls of more rows than the region
+// holds run without them), then the tile partials.
+constexpr int kBarRows = 16384;
+constexpr size_t kBarBytes = (size_t)kBarRows * 4;
+
 extern "C" size_t skyrl_lmhead_sample_workspace_bytes(int32_t M, int32_t V) {
     const size_t n = (size_t)(M > 0 ? M : 1) * tiles(V > 0 ? V : 1, 128);  // the smallest tile width
-    return n * sizeof(float4) + n * sizeof(float) + 256;
+    return kBarBytes + n * sizeof(float4) + n * sizeof(float) + 256;
 }
 
 extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight,
@@ -1058,18 +1101,20 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_sample: workspace must be 16-B aligned");
     const int pipe = pipe_for(M, ld_hidden, V, ld_weight);
     const int bn = tile_n(pipe), mt = tiles(M, BM), nt = tiles(V, bn);
-    float4* parts = reinterpret_cast<float4*>(workspace);
+    unsigned* rowbar = M <= kBarRows ? reinterpret_cast<unsigned*>(workspace) : nullptr;
+    float4* parts = reinterpret_cast<float4*>(reinterpret_cast<char*>(workspace) + kBarBytes);
     float* part_x = reinterpret_cast<float*>(parts + (size_t)M * nt);
     const bool greedy = temperature == 0.f;
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
+    if (greedy) rowbar = nullptr;
     auto kern = greedy ? pick_kernel<EPI_GREEDY>(pipe) : pick_kernel<EPI_SAMPLE>(pipe);
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt | (group_for(mt) << 16), nullptr, 0ll, inv_t,
-                       seed, seq_ids, step, parts, part_x, nt, nullptr, 0ll);
+                       seed, seq_ids, step, parts, part_x, nt, nullptr, 0ll, rowbar);
     rc = check_launch("lmhead_gemm_kernel<sample>");
     if (rc) return rc;
     hipLaunchKernelGGL(lmhead_sample_merge_kernel, dim3(M), dim3(64), 0, as_stream(stream), parts, part_x, nt, tokens_out,
-                       logp_out);
+                       logp_out, rowbar);
     return check_launch("lmhead_sample_merge_kernel");
 }
 
@@ -1094,7 +1139,7 @@ extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, c
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt | (group_for(mt) << 16), nullptr, 0ll,
                        temperature, temperature != 1.0f ? 1ull : 0ull, nullptr, 0ll, states, nullptr, nt, labels,
-                       label_stride);
+                       label_stride, nullptr);
     rc = check_launch("lmhead_gemm_kernel<logprob>");
     if (rc) return rc;
     return skyrl_lmhead_state_merge(states, nt, T, logp_out, entropy_out, lse_out, stream);
