@@ -465,19 +465,22 @@ class ModelRunner:
     BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 192, 256, 384, 512, 768, 1024)
 
     def __init__(self, model, num_blocks: int, max_num_seqs: int, seed: int = 0, use_graphs: bool = True,
-                 tunable_gemm: Optional[str] = None, fused_lmhead: str = "greedy"):
+                 tunable_gemm: Optional[str] = None, fused_lmhead: str = "auto"):
         # tunable_gemm: a results-file path enables PyTorch TunableOp (runtime GEMM solution search)
         # around this runner's forwards only; the decode buckets' skinny GEMMs gain most (measured
         # 3.28 -> 2.32 ms per 28-layer decode step at 8 rows, `scripts/probe/tunable_probe.py`).
         self.tunable_gemm = tunable_gemm
         # fused_lmhead: when the lm_head GEMM runs with the sampler in its epilogue
         # (skyrl_lmhead_sample, csrc/lmhead_gemm.hip; no [n, V] logits in HBM) instead of a library
-        # GEMM + skyrl_sample. "greedy" (default): batches that are all T = 0 without filters or
-        # suppressed ids (measured 268 vs 294 us at 512 x 151,936 x 1536); "always": every
-        # unfiltered single-parameter batch (at T = 1 the exact per-tile noise evaluation makes it
-        # 338 vs 319 us, profiles/r02_lmhead_sample_bench.json); "off".
-        if fused_lmhead not in ("greedy", "always", "off"):
-            raise ValueError(f"fused_lmhead must be 'greedy', 'always' or 'off', got {fused_lmhead!r}")
+        # GEMM + skyrl_sample. "auto" (default; "greedy" is its older name): unfiltered
+        # single-parameter batches without penalties or suppressed ids where the fused kernel
+        # measured faster (greedy at >= 192 or <= 16 rows, T > 0 at >= 480 rows; see _fused_ok and
+        # profiles/r02_lmhead_sample_bench.json); "always": every unfiltered single-parameter
+        # batch; "off".
+        if fused_lmhead == "greedy":  # the r02 name of "auto"
+            fused_lmhead = "auto"
+        if fused_lmhead not in ("auto", "always", "off"):
+            raise ValueError(f"fused_lmhead must be 'auto', 'always' or 'off', got {fused_lmhead!r}")
         fits = model.spec.hidden_size % 64 == 0 and str(getattr(model, "dtype", "")) == "torch.bfloat16"
         self.fused_lmhead = fused_lmhead if fits else "off"
         self.fused_steps = 0  # decode/prefill steps sampled by the fused kernel
@@ -669,10 +672,13 @@ class ModelRunner:
         unfiltered = (top_k is None or top_k < 0) and (top_p is None or top_p >= 1.0) and not min_p
         if self.fused_lmhead == "always":
             return unfiltered
-        # greedy: where the fused kernel measured faster (256 x 256 tiles waste MFMA work on
-        # mid-size batches: 149 vs 128 us at 64 rows, 149 vs 174 at 8, 260 vs 288 at 512)
+        # where the fused kernel measured faster (256 x 256 tiles waste MFMA work on mid-size
+        # batches). Greedy: 143 vs 128 us at 64 rows, 143 vs 175 at 8, 248 vs 292 at 512. T > 0
+        # (cross-tile row bar): 314 vs 319 us at 512 rows, 198 vs 188 at 256, so only full tiles.
         nb = len(batch.requests) if batch.kind == "prefill" else self._last_nb
-        return unfiltered and temp == 0.0 and (nb >= 192 or nb <= 16)
+        if temp == 0.0:
+            return unfiltered and (nb >= 192 or nb <= 16)
+        return unfiltered and nb >= 480
 
     def _sample(self, hidden, batch: ScheduledBatch, rows: np.ndarray):
         torch = self.torch
@@ -789,7 +795,7 @@ class AMDInferenceEngine(InferenceEngineInterface):
     def __init__(self, model, num_blocks: Optional[int] = None, max_num_seqs: int = 512,
                  max_prefill_tokens: int = 32768, seed: int = 0, kv_cache_fraction: float = 0.5,
                  tokenizer=None, runner=None, use_graphs: bool = True, enable_prefix_caching: bool = True,
-                 tunable_gemm: Optional[str] = None, fused_lmhead: str = "greedy"):
+                 tunable_gemm: Optional[str] = None, fused_lmhead: str = "auto"):
         self.model = model
         self.tokenizer = tokenizer
         if num_blocks is None:
