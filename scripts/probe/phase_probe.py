@@ -54,7 +54,8 @@ buf = np.zeros(8192 * 8, dtype=np.uint64)
 for rep in range(3):
     lib.probe_clear()
     torch.cuda.synchronize()
-    launch()
+    for _ in range(1 if rep == 0 else 30):  # rep 0 cold (after a sync), later reps warm (last of 30)
+        launch()
     torch.cuda.synchronize()
     assert lib.probe_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
     t = buf.reshape(-1, 8).astype(np.int64)
