@@ -51,8 +51,9 @@ int skyrl_abi_version(void);
  * register-resident row at Qwen2.5's vocabulary), "grpo_slices" {1, 2, 4} (column slices
  * per group of the contiguous-group GRPO kernel), "loss_units" {0 auto, 1, 2, 4} (row chunks
  * per block of the fused PPO loss), "sampler_row" {0, 1} (row-mode sampler without / with
- * the progress-based wave priority), "lmhead_pipe" {-1 default, 0..13} (K pipeline of the
- * lm_head MFMA GEMM), "lmhead_group" {0 all, n} (M tiles per group of its tile order).
+ * the progress-based wave priority), "lmhead_pipe" {-1 default, 0..14} (K pipeline of the
+ * lm_head MFMA GEMM), "lmhead_group" {0 all, n} (M tiles per group of its tile order),
+ * "attn_pf" {0 default (4), 4, 6, 8} (K/V cache blocks in flight per D = 128 decode wave).
  * Every variant gives identical results. Not thread-safe.                               */
 int skyrl_tune(const char* key, int value);
 

@@ -102,9 +102,27 @@ __global__ __launch_bounds__(64) void rope_kv_write_kernel(
     }
 }
 
+// Per-wave timestamps for scripts/probe/attn_phase_probe (compiled only there, never in the product).
+#ifdef SKYRL_ATTN_PHASE_PROBE
+__device__ uint64_t g_aphase[8192 * 8];
+#define APHASE(k, extra)                                                                                    \
+    do {                                                                                                    \
+        const unsigned wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                \
+        if (threadIdx.x == 0 && wg_ < 8192) {                                                               \
+            g_aphase[wg_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                     \
+            if ((k) == 0) g_aphase[wg_ * 8 + 7] = (uint64_t)__smid() | ((uint64_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32); \
+            if ((k) == 0) g_aphase[wg_ * 8 + 6] = (uint64_t)(extra);                                        \
+        }                                                                                                   \
+    } while (0)
+#else
+#define APHASE(k, extra) \
+    do {                 \
+    } while (0)
+#endif
+
 // ---- decode attention over the paged cache -------------------------------------------
-template <int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void paged_decode_kernel(
+template <int D, int PF, int MINW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
     const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_min,
@@ -121,6 +139,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void
     if (part >= np) return;
     const int t0 = part * part_tokens;
     const int t1 = min(ctx, t0 + part_tokens);
+    APHASE(0, t1 - t0);
     const int lane = threadIdx.x;
     const int c = lane & 15;  // MFMA column: query head within the GQA group / token row of K
     const int g = lane >> 4;  // lane group: k-slice of the operands, 4-row slice of the result
@@ -155,24 +174,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void
 #pragma unroll
         for (int n = 0; n < NT; ++n) vd[n] = *reinterpret_cast<const s16x4*>(vbase + blk * blk_stride + 16 * n * kBS);
     };
-    // three blocks in flight per wave (current + two ahead): the loop is bound by the load
-    // latency, and the extra 32 VGPRs keep the occupancy tier (3 waves / SIMD) unchanged
-    s16x8 kf[KS], k1[KS];
-    s16x4 vf[NT], v1[NT];
-    load_blk(0, kf, vf);
-    if (nb > 1) load_blk(1, k1, v1);
-    for (int j = 0; j < nb; ++j) {
+    // One block step: S^T = K.Q^T, online softmax, O^T += V^T.P^T.
+    auto step = [&](int j, const s16x8 (&kf)[KS], s16x4 (&vf)[NT]) {
         const int tb = t0 + j * kBS;
-        const bool more2 = j + 2 < nb;
-        s16x8 k2[KS];
-        s16x4 v2[NT];
-        if (more2) {
-            if (((j + 2) & 63) == 0) tbl = (j + 2 + lane < nb) ? bt[j + 2 + lane] : 0;
-            load_blk(j + 2, k2, v2);
-        }
         f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], qf[s], sacc, 0, 0, 0);
+        if (j == 0) APHASE(1, 0);  // first block's K has arrived
         // sacc[i] = S[token tb + 4g + i][head c]; tokens past the partition end are masked
         // (their K/V slots hold stale data: select, never multiply).
         const int nv = t1 - (tb + 4 * g);  // valid tokens among this lane's 4
@@ -196,8 +204,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (j >= nv) vf[n][j] = 0;
+                for (int i = 0; i < 4; ++i)
+                    if (i >= nv) vf[n][i] = 0;
             }
         }
         s16x4 pf;
@@ -212,17 +220,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void
             o[n] = o[n] * alpha;
             o[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[n], pf, o[n], 0, 0, 0);
         }
+    };
+    // PF blocks in flight per wave (the current one + PF - 1 prefetched) in a register ring;
+    // the loop is unrolled by PF so every ring slot is a static register set (no moves). A
+    // wave is bound by its loads' latency (bytes in flight / latency), so the depth sets the
+    // per-wave stream rate; the launch's ~1024 waves fit one per SIMD, where the extra
+    // registers cost no occupancy.
+    s16x8 kb[PF][KS];
+    s16x4 vb[PF][NT];
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            kf[s] = k1[s];
-            if (more2) k1[s] = k2[s];
-        }
+    for (int i = 0; i < PF - 1; ++i)
+        if (i < nb) load_blk(i, kb[i], vb[i]);
+    for (int j0 = 0; j0 < nb; j0 += PF) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            vf[n] = v1[n];
-            if (more2) v1[n] = v2[n];
+        for (int u = 0; u < PF; ++u) {
+            const int j = j0 + u;
+            if (j < nb) {
+                const int jn = j + PF - 1;
+                if (jn < nb) {
+                    if ((jn & 63) == 0) tbl = (jn + lane < nb) ? bt[jn + lane] : 0;
+                    load_blk(jn, kb[(u + PF - 1) % PF], vb[(u + PF - 1) % PF]);
+                }
+                step(j, kb[u], vb[u]);
+            }
         }
     }
+    APHASE(2, 0);
     // o[n][i] = O^T[dim 16n + 4g + i][head c]; l is this lane's share of the row sum
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
@@ -311,6 +334,10 @@ extern "C" size_t skyrl_paged_decode_workspace_bytes(int32_t nseq, int32_t nh, i
     return recs * ((size_t)head_dim + 2) * sizeof(float);
 }
 
+namespace skyrl {
+int g_attn_pf = 0;  // skyrl_tune("attn_pf", 0 default / 4 / 6 / 8): K/V blocks in flight per D = 128 decode wave
+}
+
 extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                                   const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens,
                                   int32_t nseq, int32_t nh, int32_t nkv, int32_t head_dim, float scale,
@@ -338,14 +365,24 @@ extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k
     auto* kp = reinterpret_cast<const uint16_t*>(k_cache);
     auto* vp = reinterpret_cast<const uint16_t*>(v_cache);
     auto* op = reinterpret_cast<uint16_t*>(out);
-    if (head_dim == 128)
-        hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(64), 0, as_stream(stream), qp, q_stride, kp, vp,
-                           block_tables, bt_stride, context_lens, nh, nkv, qpk, scale_log2, part_tokens, nparts, op,
-                           out_stride, ws_o, ws_ml);
-    else
-        hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(64), 0, as_stream(stream), qp, q_stride, kp, vp,
-                           block_tables, bt_stride, context_lens, nh, nkv, qpk, scale_log2, part_tokens, nparts, op,
-                           out_stride, ws_o, ws_ml);
+    // D = 128: 4 blocks in flight (205 VGPRs, 2 waves / SIMD). Measured on the ragged rollout mix
+    // (512 x U[17,1536]): 92 us vs 101 for the earlier 3-deep loop; 6 and 8 deep (1 wave / SIMD,
+    // ring partly in AGPRs) 94-96 us; 3 deep in this unrolled form spills at 3 waves / SIMD.
+    const int pf = g_attn_pf > 0 ? g_attn_pf : 4;
+#define SKYRL_PD_LAUNCH(DD, PF, MINW)                                                                          \
+    hipLaunchKernelGGL((paged_decode_kernel<DD, PF, MINW>), grid, dim3(64), 0, as_stream(stream), qp, q_stride, kp, \
+                       vp, block_tables, bt_stride, context_lens, nh, nkv, qpk, scale_log2, part_tokens, nparts, op, \
+                       out_stride, ws_o, ws_ml)
+    if (head_dim == 128) {
+        switch (pf) {
+            case 6: SKYRL_PD_LAUNCH(128, 6, 1); break;
+            case 8: SKYRL_PD_LAUNCH(128, 8, 1); break;
+            default: SKYRL_PD_LAUNCH(128, 4, 2); break;
+        }
+    } else {
+        SKYRL_PD_LAUNCH(64, 3, 3);
+    }
+#undef SKYRL_PD_LAUNCH
     int rc = check_launch("paged_decode_kernel");
     if (rc || nparts == 1) return rc;
     dim3 rgrid(nh, nseq);

@@ -216,6 +216,7 @@ extern int g_train_ntstore;
 extern int g_grpo_slices;
 extern int g_loss_units;
 extern int g_sampler_row;
+extern int g_attn_pf;
 int lmhead_tune(int value);
 int lmhead_group_tune(int value);
 }
@@ -257,6 +258,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "lmhead_group") return lmhead_group_tune(value);
+    if (k == "attn_pf") {
+        SKYRL_REQUIRE(value == 0 || value == 4 || value == 6 || value == 8, "skyrl_tune: attn_pf must be 0, 4, 6 or 8");
+        g_attn_pf = value;
+        return SKYRL_OK;
+    }
     if (k == "logprob_nt") {
         g_tune.nt = value != 0;
         return SKYRL_OK;

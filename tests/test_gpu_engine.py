@@ -111,6 +111,30 @@ def test_paged_decode_matches_fp32_reference(nh, nkv, D, nparts, part_min):
         assert torch.equal(big, kernels.paged_decode(q, kc, vc, bt, cl, max(ctx), scale, nparts=4096 // 64 + 5))
 
 
+@pytest.mark.parametrize("pf", [4, 6, 8])
+def test_paged_decode_prefetch_depths(pf):
+    """Every K/V prefetch depth of the D = 128 kernel (skyrl_tune attn_pf: blocks in flight per
+    wave, a register ring unrolled by the depth) matches the fp32 reference and the default
+    bit for bit: ragged contexts that end mid-ring and past the 64-entry block-table window
+    (2051 tokens = 129 blocks in one wave), unsplit and split."""
+    g = torch.Generator(device=DEV).manual_seed(pf)
+    ctx = [1, 16, 47, 63 * 16, 64 * 16 + 1, 129 * 16 - 13, 2051, 5]
+    kc, vc, bt, dense = build_paged(ctx, 2, 128, g)
+    q = torch.randn(len(ctx), 12, 128, device=DEV, generator=g).to(torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(128)
+    ref = attn_ref(q, dense, scale)
+    for nparts in (1, 3):
+        base = kernels.paged_decode(q, kc, vc, bt, cl, max(ctx), scale, nparts=nparts)
+        kernels._ffi.call("skyrl_tune", b"attn_pf", pf)
+        try:
+            out = kernels.paged_decode(q, kc, vc, bt, cl, max(ctx), scale, nparts=nparts)
+        finally:
+            kernels._ffi.call("skyrl_tune", b"attn_pf", 0)
+        torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+        assert torch.equal(out, base)
+
+
 def test_paged_decode_large_batch_and_strided_q():
     g = torch.Generator(device=DEV).manual_seed(5)
     ctx = torch.randint(1, 1500, (300,), generator=torch.Generator().manual_seed(1)).tolist()
