@@ -391,6 +391,18 @@ int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, con
                        const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens, int32_t nseq,
                        int32_t nh, int32_t nkv, int32_t head_dim, float scale, int32_t part_tokens, int32_t nparts,
                        void* out, int64_t out_stride, void* workspace, void* stream);
+/* skyrl_paged_decode_balanced: the same attention with the work split by blocks instead of by
+ *                        sequence: the cache blocks of all sequences (per kv head) are laid end
+ *                        to end and each of `waves` waves streams an equal share, so a ragged
+ *                        batch costs what a uniform one of the same total does. Three launches on
+ *                        `stream` (plan: block prefix sums; attention; merge of the sequences
+ *                        split across waves). nseq <= 8192; the workspace is
+ *                        skyrl_paged_decode_balanced_workspace_bytes(nseq, nh, head_dim, waves). */
+size_t skyrl_paged_decode_balanced_workspace_bytes(int32_t nseq, int32_t nh, int32_t head_dim, int32_t waves);
+int skyrl_paged_decode_balanced(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                                const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens,
+                                int32_t nseq, int32_t nh, int32_t nkv, int32_t head_dim, float scale, int32_t waves,
+                                void* out, int64_t out_stride, void* workspace, void* stream);
 /* Decoder-layer glue (HF Qwen2DecoderLayer/LlamaDecoderLayer), bf16 [n, H] rows:
  *   skyrl_add_rmsnorm  hidden = bf16(hidden + delta) (delta may be NULL), then
  *                      out = bf16(weight * bf16(hidden * rsqrt(mean(hidden^2) + eps)));

@@ -145,6 +145,9 @@ SIGNATURES = {
     "skyrl_paged_decode_workspace_bytes": (_SZ, [_I32, _I32, _I32, _I32]),
     "skyrl_paged_decode": (_INT, [_P, _I64, _P, _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _F, _I32, _I32, _P, _I64,
                                   _P, _P]),
+    "skyrl_paged_decode_balanced_workspace_bytes": (_SZ, [_I32, _I32, _I32, _I32]),
+    "skyrl_paged_decode_balanced": (_INT, [_P, _I64, _P, _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _F, _I32, _P, _I64,
+                                           _P, _P]),
     "skyrl_add_rmsnorm": (_INT, [_P, _P, _P, _I32, _I32, _F, _P, _P]),
     "skyrl_silu_mul": (_INT, [_P, _I64, _I32, _P, _P]),
 }

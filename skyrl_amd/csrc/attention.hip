@@ -121,25 +121,17 @@ __device__ uint64_t g_aphase[8192 * 8];
 #endif
 
 // ---- decode attention over the paged cache -------------------------------------------
-template <int D, int PF, int MINW>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void paged_decode_kernel(
-    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
-    const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_min,
-    int nparts, uint16_t* __restrict__ out, int64_t out_stride, float* __restrict__ ws_o,
-    float* __restrict__ ws_ml) {
+// Attention of one kv head's query group over context tokens [t0, t1) of one sequence, one
+// wave: o[n][i] = unnormalised O^T[dim 16n + 4g + i][head c], m / l this lane's running max
+// and its share of the row sum (log2 domain). PF blocks in flight (see the ring below).
+template <int D, int PF>
+__device__ __forceinline__ void attend_range(const uint16_t* __restrict__ q, int64_t q_stride,
+                                             const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+                                             const int32_t* __restrict__ bt_row, int seq, int kvh, int t0, int t1,
+                                             int nkv, int qpk, float scale_log2, f32x4 (&o)[D / 16], float& m,
+                                             float& l) {
     constexpr int KS = D / 32;  // k-steps of the Q.K^T MFMA
     constexpr int NT = D / 16;  // 16-dim output tiles of the P.V MFMA
-    const int seq = blockIdx.z;
-    const int kvh = blockIdx.y;
-    const int part = blockIdx.x;
-    const int ctx = ctx_lens[seq];
-    int part_tokens, np;
-    seq_split(ctx, part_min, nparts, part_tokens, np);
-    if (part >= np) return;
-    const int t0 = part * part_tokens;
-    const int t1 = min(ctx, t0 + part_tokens);
-    APHASE(0, t1 - t0);
     const int lane = threadIdx.x;
     const int c = lane & 15;  // MFMA column: query head within the GQA group / token row of K
     const int g = lane >> 4;  // lane group: k-slice of the operands, 4-row slice of the result
@@ -153,14 +145,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW, 8))) v
         qf[s] = *reinterpret_cast<const s16x8*>(qrow + 32 * s + 8 * g);
         if (!hv) qf[s] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
-    f32x4 o[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY, l = 0.f;
+    m = -INFINITY;
+    l = 0.f;
 
     // Block ids of this partition: one vector load of up to 64 table entries (one per lane),
     // read back with readlane, so the per-block address chain has no dependent table load.
-    const int32_t* bt = block_tables + (int64_t)seq * bt_stride + t0 / kBS;
+    const int32_t* bt = bt_row + t0 / kBS;
     const int nb = (t1 - t0 + kBS - 1) / kBS;
     int tbl = lane < nb ? bt[lane] : 0;
     const int64_t head_tile = (int64_t)kBS * D;
@@ -245,6 +237,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW, 8))) v
             }
         }
     }
+}
+
+template <int D, int PF, int MINW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void paged_decode_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
+    const int32_t* __restrict__ ctx_lens, int nh, int nkv, int qpk, float scale_log2, int part_min,
+    int nparts, uint16_t* __restrict__ out, int64_t out_stride, float* __restrict__ ws_o,
+    float* __restrict__ ws_ml) {
+    constexpr int NT = D / 16;  // 16-dim output tiles of the P.V MFMA
+    const int seq = blockIdx.z;
+    const int kvh = blockIdx.y;
+    const int part = blockIdx.x;
+    const int ctx = ctx_lens[seq];
+    int part_tokens, np;
+    seq_split(ctx, part_min, nparts, part_tokens, np);
+    if (part >= np) return;
+    const int t0 = part * part_tokens;
+    const int t1 = min(ctx, t0 + part_tokens);
+    APHASE(0, t1 - t0);
+    const int lane = threadIdx.x;
+    const int c = lane & 15;
+    const int g = lane >> 4;
+    const int h = kvh * qpk + c;
+    const bool hv = c < qpk;
+    f32x4 o[NT];
+    float m, l;
+    attend_range<D, PF>(q, q_stride, kc, vc, block_tables + (int64_t)seq * bt_stride, seq, kvh, t0, t1, nkv, qpk,
+                        scale_log2, o, m, l);
     APHASE(2, 0);
     // o[n][i] = O^T[dim 16n + 4g + i][head c]; l is this lane's share of the row sum
     l += __shfl_xor(l, 16, kWave);
@@ -296,6 +317,155 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const float* __r
         acc += w * ws_o[(rec0 + p) * D + d];
     }
     out[(int64_t)seq * out_stride + (int64_t)h * D + d] = f32_to_bf16(np > 0 ? acc / L : 0.f);
+}
+
+// ---- balanced decode: every wave streams the same number of cache blocks ------------------
+// The per-sequence split above gives a wave a whole context (or a fixed share of one), so on a
+// ragged batch the waves' work differs by up to 90x and the CUs that drew the long contexts set
+// the launch time (per-wave timeline: CU end time follows CU token count, correlation 0.79).
+// Here the blocks of all sequences of one kv head are laid end to end (sequence-major) and wave
+// w of W takes blocks [floor(w B / W), floor((w+1) B / W)) of that list: every wave streams
+// B / W blocks whatever the context mix. A wave walks the sequences its range touches; a
+// sequence wholly inside one wave is written directly, a split one leaves (o, m, l) records
+// for the merge. A wave has at most two split segments (its first and its last), so records
+// are addressed by (wave, 0 = first segment / 1 = last segment). Plan: one workgroup scans
+// the block counts (pre[s] = blocks before sequence s) and finds each wave's first sequence.
+constexpr int kPlanThreads = 1024;
+constexpr int kPlanMaxSeqs = 8192;  // LDS prefix array (32 KB)
+
+__device__ __forceinline__ int64_t wave_start(int w, int64_t B, int W) { return (int64_t)w * B / W; }
+// the non-empty wave whose range holds block x: the largest w with wave_start(w) <= x
+__device__ __forceinline__ int wave_of(int64_t x, int64_t B, int W) { return (int)(((x + 1) * W + B - 1) / B - 1); }
+
+__global__ __launch_bounds__(kPlanThreads) void decode_plan_kernel(const int32_t* __restrict__ ctx_lens, int nseq,
+                                                                   int W, int32_t* __restrict__ pre,
+                                                                   int32_t* __restrict__ wave_seq) {
+    __shared__ int32_t s_pre[kPlanMaxSeqs + 1];
+    __shared__ int32_t s_wsum[kPlanThreads / kWave];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+    const int per = (nseq + kPlanThreads - 1) / kPlanThreads;
+    const int lo = min(nseq, tid * per), hi = min(nseq, lo + per);
+    int sum = 0;
+    for (int i = lo; i < hi; ++i) sum += (ctx_lens[i] + kBS - 1) / kBS;
+    int incl = sum;  // inclusive scan over the wave
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int v = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += v;
+    }
+    if (lane == kWave - 1) s_wsum[wid] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int k = 0; k < wid; ++k) base += s_wsum[k];
+    for (int i = lo; i < hi; ++i) {
+        s_pre[i] = base;
+        base += (ctx_lens[i] + kBS - 1) / kBS;
+    }
+    if (tid == kPlanThreads - 1) s_pre[nseq] = base;  // the last thread's running sum is the total
+    __syncthreads();
+    for (int i = tid; i <= nseq; i += kPlanThreads) pre[i] = s_pre[i];
+    const int64_t B = s_pre[nseq];
+    for (int w = tid; w < W; w += kPlanThreads) {
+        const int64_t x = wave_start(w, B, W);
+        int a = 0, b = nseq - 1;  // largest s with s_pre[s] <= x (contexts are >= 1 token)
+        while (a < b) {
+            const int mid = (a + b + 1) >> 1;
+            if (s_pre[mid] <= x) a = mid;
+            else b = mid - 1;
+        }
+        wave_seq[w] = x < B ? a : nseq;
+    }
+}
+
+template <int D, int PF, int MINW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void paged_decode_balanced_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int64_t bt_stride,
+    const int32_t* __restrict__ ctx_lens, const int32_t* __restrict__ pre, const int32_t* __restrict__ wave_seq,
+    int nseq, int W, int nh, int nkv, int qpk, float scale_log2, uint16_t* __restrict__ out, int64_t out_stride,
+    float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+    constexpr int NT = D / 16;
+    const int w = blockIdx.x;
+    const int kvh = blockIdx.y;
+    const int64_t B = pre[nseq];
+    int64_t x0 = wave_start(w, B, W);
+    const int64_t x1 = wave_start(w + 1, B, W);
+    if (x0 >= x1) return;
+    int s = wave_seq[w];
+    const int lane = threadIdx.x;
+    const int c = lane & 15;
+    const int g = lane >> 4;
+    const int h = kvh * qpk + c;
+    const bool hv = c < qpk;
+    int slot = 0;
+    while (x0 < x1) {
+        const int64_t ps = pre[s], pe = pre[s + 1];
+        const int a = (int)(x0 - ps);
+        const int b = (int)((x1 < pe ? x1 : pe) - ps);
+        const int ctx = ctx_lens[s];
+        const int t0 = a * kBS;
+        const int t1 = min(ctx, b * kBS);
+        f32x4 o[NT];
+        float m, l;
+        attend_range<D, PF>(q, q_stride, kc, vc, block_tables + (int64_t)s * bt_stride, s, kvh, t0, t1, nkv, qpk,
+                            scale_log2, o, m, l);
+        l += __shfl_xor(l, 16, kWave);
+        l += __shfl_xor(l, 32, kWave);
+        if (hv) {
+            if (a == 0 && ps + b == pe) {  // the whole context in this wave
+                const float inv = 1.f / l;
+                uint16_t* orow = out + (int64_t)s * out_stride + (int64_t)h * D;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    uint2 v;
+                    v.x = pack_bf16x2(o[n][0] * inv, o[n][1] * inv);
+                    v.y = pack_bf16x2(o[n][2] * inv, o[n][3] * inv);
+                    *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g) = v;
+                }
+            } else {
+                const int64_t rec = ((int64_t)w * 2 + slot) * nh + h;
+                float* wo = ws_o + rec * D;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) *reinterpret_cast<f32x4*>(wo + 16 * n + 4 * g) = o[n];
+                if (g == 0) {
+                    ws_ml[rec * 2 + 0] = m;
+                    ws_ml[rec * 2 + 1] = l;
+                }
+            }
+        }
+        x0 = pe;
+        ++s;
+        slot = 1;
+    }
+}
+
+// Merge the split sequences' records: grid (nh, nseq), D threads; sequences inside one wave exit.
+template <int D>
+__global__ __launch_bounds__(D) void paged_decode_balanced_merge_kernel(
+    const float* __restrict__ ws_o, const float* __restrict__ ws_ml, const int32_t* __restrict__ pre,
+    const int32_t* __restrict__ wave_seq, int nseq, int W, int nh, uint16_t* __restrict__ out, int64_t out_stride) {
+    const int h = blockIdx.x;
+    const int s = blockIdx.y;
+    const int d = threadIdx.x;
+    const int64_t B = pre[nseq];
+    const int64_t ps = pre[s], pe = pre[s + 1];
+    const int wf = wave_of(ps, B, W), wl = wave_of(pe - 1, B, W);
+    if (wf == wl) return;
+    auto rec_of = [&](int w) -> int64_t { return ((int64_t)w * 2 + ((w == wf && wave_seq[w] != s) ? 1 : 0)) * nh + h; };
+    float M = -INFINITY;
+    for (int w = wf; w <= wl; ++w)
+        if (wave_start(w, B, W) < wave_start(w + 1, B, W)) M = fmaxf(M, ws_ml[rec_of(w) * 2]);
+    float L = 0.f, acc = 0.f;
+    for (int w = wf; w <= wl; ++w) {
+        if (wave_start(w, B, W) == wave_start(w + 1, B, W)) continue;
+        const int64_t r = rec_of(w);
+        const float e = fast_exp2(ws_ml[r * 2] - M);
+        L += e * ws_ml[r * 2 + 1];
+        acc += e * ws_o[r * D + d];
+    }
+    out[(int64_t)s * out_stride + (int64_t)h * D + d] = f32_to_bf16(acc / L);
 }
 
 }  // namespace
@@ -393,4 +563,65 @@ extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k
         hipLaunchKernelGGL(paged_decode_reduce_kernel<64>, rgrid, dim3(64), 0, as_stream(stream), ws_o, ws_ml,
                            context_lens, nh, part_tokens, nparts, op, out_stride);
     return check_launch("paged_decode_reduce_kernel");
+}
+
+extern "C" size_t skyrl_paged_decode_balanced_workspace_bytes(int32_t nseq, int32_t nh, int32_t head_dim,
+                                                              int32_t waves) {
+    const size_t ints = (((size_t)(nseq > 0 ? nseq : 0) + 1 + (size_t)(waves > 0 ? waves : 0)) * 4 + 255) / 256 * 256;
+    const size_t recs = (size_t)(waves > 0 ? waves : 0) * 2 * (size_t)nh;
+    return ints + recs * (size_t)head_dim * 4 + recs * 2 * 4;
+}
+
+extern "C" int skyrl_paged_decode_balanced(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                                           const int32_t* block_tables, int64_t bt_stride,
+                                           const int32_t* context_lens, int32_t nseq, int32_t nh, int32_t nkv,
+                                           int32_t head_dim, float scale, int32_t waves, void* out,
+                                           int64_t out_stride, void* workspace, void* stream) {
+    SKYRL_REQUIRE(nseq >= 0 && nseq <= kPlanMaxSeqs, "paged_decode_balanced: nseq must be in [0, 8192]");
+    SKYRL_REQUIRE(nh > 0 && nkv > 0 && nh % nkv == 0 && nh / nkv <= 16, "paged_decode_balanced: bad head counts");
+    SKYRL_REQUIRE(head_dim == 64 || head_dim == 128, "paged_decode_balanced: head_dim must be 64 or 128");
+    SKYRL_REQUIRE(waves >= 1, "paged_decode_balanced: waves must be >= 1");
+    if (nseq == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(q && k_cache && v_cache && block_tables && context_lens && out && workspace,
+                  "paged_decode_balanced: null pointer");
+    SKYRL_REQUIRE(q_stride >= (int64_t)nh * head_dim && out_stride >= (int64_t)nh * head_dim,
+                  "paged_decode_balanced: row stride smaller than nh * head_dim");
+    SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(q) % 16) == 0 && (q_stride % 8) == 0,
+                  "paged_decode_balanced: q must be 16-B aligned with a row stride multiple of 8");
+    const float scale_log2 = scale * 1.4426950408889634f;
+    const int qpk = nh / nkv;
+    char* wsb = reinterpret_cast<char*>(workspace);
+    int32_t* pre = reinterpret_cast<int32_t*>(wsb);
+    int32_t* wave_seq = pre + nseq + 1;
+    const size_t ints = (((size_t)nseq + 1 + (size_t)waves) * 4 + 255) / 256 * 256;
+    float* ws_o = reinterpret_cast<float*>(wsb + ints);
+    float* ws_ml = ws_o + (size_t)waves * 2 * nh * head_dim;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(decode_plan_kernel, dim3(1), dim3(kPlanThreads), 0, st, context_lens, nseq, waves, pre,
+                       wave_seq);
+    int rc = check_launch("decode_plan_kernel");
+    if (rc) return rc;
+    auto* qp = reinterpret_cast<const uint16_t*>(q);
+    auto* kp = reinterpret_cast<const uint16_t*>(k_cache);
+    auto* vp = reinterpret_cast<const uint16_t*>(v_cache);
+    auto* op = reinterpret_cast<uint16_t*>(out);
+    dim3 grid(waves, nkv);
+    if (head_dim == 128)
+        hipLaunchKernelGGL((paged_decode_balanced_kernel<128, 4, 2>), grid, dim3(64), 0, st, qp, q_stride, kp, vp,
+                           block_tables, bt_stride, context_lens, pre, wave_seq, nseq, waves, nh, nkv, qpk,
+                           scale_log2, op, out_stride, ws_o, ws_ml);
+    else
+        hipLaunchKernelGGL((paged_decode_balanced_kernel<64, 3, 3>), grid, dim3(64), 0, st, qp, q_stride, kp, vp,
+                           block_tables, bt_stride, context_lens, pre, wave_seq, nseq, waves, nh, nkv, qpk,
+                           scale_log2, op, out_stride, ws_o, ws_ml);
+    rc = check_launch("paged_decode_balanced_kernel");
+    if (rc) return rc;
+    dim3 rgrid(nh, nseq);
+    if (head_dim == 128)
+        hipLaunchKernelGGL(paged_decode_balanced_merge_kernel<128>, rgrid, dim3(128), 0, st, ws_o, ws_ml, pre,
+                           wave_seq, nseq, waves, nh, op, out_stride);
+    else
+        hipLaunchKernelGGL(paged_decode_balanced_merge_kernel<64>, rgrid, dim3(64), 0, st, ws_o, ws_ml, pre,
+                           wave_seq, nseq, waves, nh, op, out_stride);
+    return check_launch("paged_decode_balanced_merge_kernel");
 }

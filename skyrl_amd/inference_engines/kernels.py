@@ -89,6 +89,12 @@ def choose_nparts(nseq: int, nkv: int, max_ctx: int, target_waves: int = 1024, m
     return max(1, min(want, math.ceil(max(max_ctx, 1) / MIN_PARTITION)))
 
 
+def balanced_waves(nkv: int, total_blocks_hint: Optional[int] = None, target_waves: int = 1024) -> int:
+    """Waves per kv head for paged_decode_balanced: about ``target_waves`` in flight (one per SIMD)."""
+    w = max(1, target_waves // max(1, nkv))
+    return w if total_blocks_hint is None else max(1, min(w, total_blocks_hint))
+
+
 class DecodeWorkspace:
     """Grows-only fp32 scratch for the partition merge (reused every layer and step)."""
 
@@ -136,5 +142,38 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
         ws = (workspace or DecodeWorkspace(dev)).get(nbytes)
     _ffi.call("skyrl_paged_decode", _ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
               block_tables.stride(0), _ptr(context_lens), n, nh, nkv, D, float(scale), part_min, nparts, _ptr(out),
+              out.stride(0), _ptr(ws), _stream(dev))
+    return out
+
+
+def paged_decode_balanced(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                          block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float,
+                          out: Optional[torch.Tensor] = None, workspace: Optional[DecodeWorkspace] = None,
+                          waves: Optional[int] = None) -> torch.Tensor:
+    """paged_decode with the work split by cache blocks: every wave streams the same number of
+    blocks across sequence boundaries (plan + attention + merge on the device), so a ragged
+    batch streams at the uniform batch's rate. Same arguments and result as paged_decode
+    (no max_ctx / split arguments: the plan reads context_lens on the device)."""
+    dev = _require_gpu(q, k_cache, v_cache, block_tables, context_lens)
+    n, nh, D = q.shape
+    nb, nkv = k_cache.shape[0], k_cache.shape[1]
+    if q.dtype != torch.bfloat16 or q.stride(2) != 1 or q.stride(1) != D:
+        raise ValueError("q must be bf16 [n, nh, D] with contiguous heads")
+    if k_cache.shape != (nb, nkv, BLOCK_SIZE, D) or v_cache.shape != (nb, nkv, D, BLOCK_SIZE):
+        raise ValueError("cache shapes do not match q")
+    if block_tables.dtype != torch.int32 or block_tables.dim() != 2 or block_tables.shape[0] != n \
+            or block_tables.stride(1) != 1:
+        raise ValueError("block_tables must be int32 [n, max_blocks] with unit column stride")
+    if context_lens.dtype != torch.int32 or context_lens.numel() != n or not context_lens.is_contiguous():
+        raise ValueError("context_lens must be contiguous int32 [n]")
+    if out is None:
+        out = torch.empty((n, nh, D), dtype=torch.bfloat16, device=dev)
+    if n == 0:
+        return out
+    waves = waves or balanced_waves(nkv)
+    nbytes = _ffi.query("skyrl_paged_decode_balanced_workspace_bytes", n, nh, D, waves)
+    ws = (workspace or DecodeWorkspace(dev)).get(nbytes)
+    _ffi.call("skyrl_paged_decode_balanced", _ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
+              block_tables.stride(0), _ptr(context_lens), n, nh, nkv, D, float(scale), waves, _ptr(out),
               out.stride(0), _ptr(ws), _stream(dev))
     return out

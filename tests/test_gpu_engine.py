@@ -135,6 +135,41 @@ def test_paged_decode_prefetch_depths(pf):
         assert torch.equal(out, base)
 
 
+@pytest.mark.parametrize("nh,nkv,D", [(12, 2, 128), (28, 4, 128), (16, 1, 64)])
+@pytest.mark.parametrize("waves", [1, 3, 7, 64, 1024, 5000])
+def test_paged_decode_balanced_matches_fp32_reference(nh, nkv, D, waves):
+    """Block-balanced decode (every wave streams total_blocks / waves blocks across sequence
+    boundaries; split sequences merged from per-wave records) vs the fp32 reference: one wave
+    (everything in it), a few waves (long sequences split 2-3 ways, short ones whole), one per
+    block, and more waves than blocks (empty waves). Contexts end mid-block and span > 64 blocks."""
+    g = torch.Generator(device=DEV).manual_seed(waves * 3 + D)
+    ctx = [1, 15, 16, 17, 33, 200, 1000, 2051, 5, 64 * 16 + 1, 700]
+    kc, vc, bt, dense = build_paged(ctx, nkv, D, g)
+    q = torch.randn(len(ctx), nh, D, device=DEV, generator=g).to(torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    out = kernels.paged_decode_balanced(q, kc, vc, bt, cl, scale, waves=waves)
+    torch.testing.assert_close(out.float(), attn_ref(q, dense, scale), atol=2e-2, rtol=2e-2)
+    # a strided q (a view into a fused qkv row) and a reused workspace give the same answer
+    qkv = torch.zeros(len(ctx), (nh + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    qkv[:, :nh * D] = q.reshape(len(ctx), -1)
+    ws = kernels.DecodeWorkspace(DEV)
+    for _ in range(2):
+        again = kernels.paged_decode_balanced(qkv[:, :nh * D].view(len(ctx), nh, D), kc, vc, bt, cl, scale,
+                                              waves=waves, workspace=ws)
+        assert torch.equal(again, out)
+
+
+def test_paged_decode_balanced_large_ragged_batch():
+    g = torch.Generator(device=DEV).manual_seed(9)
+    ctx = torch.randint(1, 1537, (512,), generator=torch.Generator().manual_seed(2)).tolist()
+    kc, vc, bt, dense = build_paged(ctx, 2, 128, g)
+    q = torch.randn(len(ctx), 12, 128, device=DEV, generator=g).to(torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    out = kernels.paged_decode_balanced(q, kc, vc, bt, cl, 1 / math.sqrt(128))
+    torch.testing.assert_close(out.float(), attn_ref(q, dense, 1 / math.sqrt(128)), atol=2e-2, rtol=2e-2)
+
+
 def test_paged_decode_large_batch_and_strided_q():
     g = torch.Generator(device=DEV).manual_seed(5)
     ctx = torch.randint(1, 1500, (300,), generator=torch.Generator().manual_seed(1)).tolist()
