@@ -413,8 +413,11 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
     on [N, R]: the SURVEY §8(d) "advantage+loss" kernels (12 + 20 + 24 = 56 algorithmic
     B/token). Launched through the C ABI inside a captured HIP graph and replayed, so host
     launch cost is excluded and inter-kernel gaps are included. The loss-mask row sums are
-    the pack kernel's (skyrl_pack_experience emits them with the batch). Returns per-kernel
-    and total microseconds."""
+    the pack kernel's (skyrl_pack_experience emits them with the batch). `total_us` is the
+    product path: skyrl_grpo_ppo_loss_fwd (GRPO inside the loss launch, one launch up to
+    2048 row chunks, two above) + the backward; `two_call_total_us` is GRPO, loss, backward
+    as three launches. Both keep the 56 B/token figure. Returns per-kernel and total
+    microseconds."""
     from skyrl_amd import _ffi, ppo_utils
     from skyrl_amd.config import AlgorithmConfig
     from skyrl_amd.ops import _ptr
@@ -450,6 +453,11 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
     def bwd(s):
         _ffi.call("skyrl_ppo_loss_bwd", _ptr(gout), N * R, _ptr(glp), None, s)
 
+    def fused(s):  # GRPO inside the loss launch (skyrl_grpo_ppo_loss_fwd), same outputs
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", _ptr(rew), _ptr(rmask), _ffi.I64, ng, 1e-6, 1, _ptr(lp), _ptr(old),
+                  _ptr(lmask), _ptr(ref), None, _ptr(rows), N, R, ctypes.byref(params), _ptr(adv), _ptr(loss),
+                  _ptr(met), _ptr(glp), None, _ptr(ws), s)
+
     def timed(fns):
         side = torch.cuda.Stream(dev)
         with torch.cuda.stream(side):
@@ -476,7 +484,8 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
 
     out = {}
     for name, fns in (("grpo_us", (grpo,)), ("loss_fwd_us", (fwd,)), ("loss_bwd_us", (bwd,)),
-                      ("total_us", (grpo, fwd, bwd))):
+                      ("grpo_loss_fused_us", (fused,)), ("two_call_total_us", (grpo, fwd, bwd)),
+                      ("total_us", (fused, bwd))):
         out[name] = timed(fns)
     if variants:
         out["variants"] = {"total_without_row_sums_us": timed((grpo, lambda s: fwd(s, False), bwd)),

@@ -157,6 +157,23 @@ int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const
                        float* loss_out /* [1] */, float* metrics_out /* [SKYRL_M_COUNT] */,
                        float* grad_logp /* [n,R] */, float* grad_entropy /* [n,R] or NULL */,
                        void* workspace, void* stream);
+/* a4 + a7 for a batch that is one micro-batch: skyrl_grpo_advantage (contiguous groups of
+ * G = n/num_groups rows) followed by skyrl_ppo_loss_fwd on its advantages, in ONE launch
+ * when G <= 16, R % 4 == 0, buffers are 16-B aligned, row_mask_sum is given and n*ceil(R/1024)
+ * <= 2048 (two launches otherwise). Outputs are bit-identical to the two calls: advantages
+ * (adv*response_mask, f32 [n,R]), loss, metrics, grad_logp, grad_entropy. Replaces
+ * compute_grpo_outcome_advantage (ppo_utils.py:1132-1182) + the loss of
+ * PolicyWorkerBase._forward_backward_micro (workers/worker.py:810-876) when the mini-batch is
+ * the whole batch. workspace: skyrl_ppo_loss_workspace_bytes(n, R), zeroed once.           */
+int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* response_mask, int mask_dtype,
+                            int32_t num_groups, float epsilon, int32_t norm_by_std,
+                            const float* log_probs, const float* old_log_probs,
+                            const float* loss_mask /* NULL = all ones */, const float* ref_log_probs,
+                            const float* entropy, const float* row_mask_sum /* [n] or NULL */,
+                            int32_t n, int32_t R, const skyrl_ppo_params* params,
+                            float* advantages /* [n,R] */, float* loss_out /* [1] */,
+                            float* metrics_out /* [SKYRL_M_COUNT] */, float* grad_logp /* [n,R] */,
+                            float* grad_entropy /* [n,R] or NULL */, void* workspace, void* stream);
 /* Autograd backward of the loss: grad_logp (and grad_entropy, if given) *= grad_out[0] in
  * place; no memory is touched when grad_out[0] == 1 (loss.backward()).                    */
 int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, int64_t numel, float* grad_logp,

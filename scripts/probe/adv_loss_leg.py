@@ -1,13 +1,14 @@
-"""Run bench.py's graph-replayed advantage+loss leg alone (batch and 16x batch)."""
+"""Times bench.advantage_loss_leg alone (the graph-replayed GRPO + loss + backward leg) at the
+batch size and 16x, for A/B runs of the loss kernels without the whole bench."""
 import json
-import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-import torch  # noqa: E402
+import torch
 
+sys.path.insert(0, ".")
 import bench  # noqa: E402
 
-dev = torch.device("cuda", 0)
-print(json.dumps({"batch": bench.advantage_loss_leg(dev, 512, 1024),
-                  "batch_x16": bench.advantage_loss_leg(dev, 8192, 1024, reps=5)}))
+dev = torch.device("cuda:0")
+out = {"batch": bench.advantage_loss_leg(dev, 512, 1024, variants=True),
+       "batch_x16": bench.advantage_loss_leg(dev, 16 * 512, 1024, reps=5)}
+print(json.dumps(out))

@@ -101,6 +101,11 @@ SIGNATURES = {
         _INT,
         [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P, _P, _P],
     ),
+    "skyrl_grpo_ppo_loss_fwd": (
+        _INT,
+        [_P, _P, _INT, _I32, _F, _I32, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams),
+         _P, _P, _P, _P, _P, _P, _P],
+    ),
     "skyrl_ppo_loss_bwd": (_INT, [_P, _I64, _P, _P, _P]),
     "skyrl_critic_loss_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_critic_loss_fwd": (_INT, [_P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),

@@ -343,6 +343,185 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
     PHASE(3);
 }
 
+// ---- a4 + a7 in ONE launch: GRPO advantage inside the loss launch ----------------------
+// For a batch that is one micro-batch (the north_star's advantage+loss leg), the GRPO
+// advantage (grpo.hip) and the loss above are two dependent launches joined by a 4 B/token
+// advantage round trip. Here every loss block derives its own row's advantage: it sums the
+// reward rows of its group (contiguous uniform groups of G <= 16 rows, the trainer's layout,
+// generators/utils.py:373-393) with the per-lane order and wave tree of grpo.hip's
+// grpo_adv_contig_kernel, so the scores, the fp64 group stats and the fp32 normalisation are
+// bit-identical to skyrl_grpo_advantage's; it writes adv*response_mask for its own chunk (the
+// product output, kept in the batch like the reference's advantages) and feeds the same
+// values to ppo_token. The G*nchunks blocks of a group sit on one XCD (block b runs on XCD
+// b % 8), so the group's repeated reward reads (G*R*4 B) hit that XCD's L2.
+constexpr int kGroupMax = 16;
+
+template <int MDT>
+__global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
+    const float* __restrict__ rewards, const void* __restrict__ resp_mask, int num_groups, int G, float epsilon,
+    int norm_by_std, int xcd_map, const float* __restrict__ lp, const float* __restrict__ old,
+    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent,
+    const float* __restrict__ row_msum, int n, int R, int nchunks, skyrl_ppo_params p, float* __restrict__ adv_out,
+    float* __restrict__ glp, float* __restrict__ gent, unsigned long long* __restrict__ gran,
+    unsigned* __restrict__ epoch_word, float* __restrict__ loss_out, float* __restrict__ metrics) {
+    __shared__ float s_red[kFW * kNP];
+    __shared__ double s_redd[kFW * kNP];
+    __shared__ float s_scores[kGroupMax];
+    __shared__ unsigned s_epoch;
+    if (threadIdx.x == 0) s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const int nb = gridDim.x;
+    const int wb = blockIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int gu = G * nchunks;  // units (row chunks) per group
+    int group, local;
+    if (xcd_map) {
+        const int k = wb >> 3;
+        group = (k / gu) * 8 + (wb & 7);
+        local = k % gu;
+    } else {
+        group = wb / gu;
+        local = wb % gu;
+    }
+    const bool unit_live = group < num_groups;
+    const int row = unit_live ? group * G + local / nchunks : 0;
+    const int chunk = local % nchunks;
+    const int c0 = chunk * kFT + threadIdx.x * 4;
+    const bool live = unit_live && c0 < R;  // R % 4 == 0 on this path
+    const int64_t e = (int64_t)row * R + c0;
+    float4 l4 = make_float4(0.f, 0.f, 0.f, 0.f), o4 = l4, r4 = l4, e4 = l4, m4 = make_float4(1.f, 1.f, 1.f, 1.f);
+    float rm[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        l4 = *reinterpret_cast<const float4*>(lp + e);
+        o4 = *reinterpret_cast<const float4*>(old + e);
+        if (mask) m4 = *reinterpret_cast<const float4*>(mask + e);
+        if (p.use_kl_loss) r4 = *reinterpret_cast<const float4*>(ref + e);
+        if (ent) e4 = *reinterpret_cast<const float4*>(ent + e);
+        load_mask4(resp_mask, MDT, e, rm);
+    }
+    // group scores: wave wv sums rows wv, wv + kFW, ... (grpo_adv_contig_kernel's lane order)
+    const int n4 = R >> 2;
+    if (unit_live && n4 <= 4 * kWave) {
+        // R <= 1024: every reward vector of the wave's (up to 4) rows in flight at once, so
+        // the scores cost one memory round trip, overlapped with the loss inputs' loads
+        float4 v[kGroupMax / kFW][4];
+#pragma unroll
+        for (int q = 0; q < kGroupMax / kFW; ++q) {
+            const int j = wv + q * kFW;
+            const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = lane + u * kWave;
+                v[q][u] = (j < G && i < n4) ? rrow[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kGroupMax / kFW; ++q) {
+            const int j = wv + q * kFW;
+            if (j < G) {
+                float acc = 0.f;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc += (v[q][u].x + v[q][u].y) + (v[q][u].z + v[q][u].w);
+                acc = wave_sum(acc);
+                if (lane == 0) s_scores[j] = acc;
+            }
+        }
+    } else if (unit_live) {
+        for (int j = wv; j < G; j += kFW) {
+            const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
+            float acc = 0.f;
+            int i = lane;
+            for (; i + 3 * kWave < n4; i += 4 * kWave) {
+                const float4 v0 = rrow[i], v1 = rrow[i + kWave], v2 = rrow[i + 2 * kWave], v3 = rrow[i + 3 * kWave];
+                acc += (v0.x + v0.y) + (v0.z + v0.w);
+                acc += (v1.x + v1.y) + (v1.z + v1.w);
+                acc += (v2.x + v2.y) + (v2.z + v2.w);
+                acc += (v3.x + v3.y) + (v3.z + v3.w);
+            }
+            for (; i < n4; i += kWave) {
+                const float4 v = rrow[i];
+                acc += (v.x + v.y) + (v.z + v.w);
+            }
+            acc = wave_sum(acc);
+            if (lane == 0) s_scores[j] = acc;
+        }
+    }
+    // the mask-only scales while the loads are in flight (as ppo_loss_grad_kernel)
+    const bool need_total = p.loss_reduction == 0 || (p.use_entropy_loss && gent);
+    float total = 0.f;
+    if (need_total) {
+        for (int r = lane; r < n; r += kWave) total += row_msum[r];
+        total = wave_sum(total);
+    }
+    const float tok_scale = 1.f / (total > 1.f ? total : 1.f);
+    const float escale = need_total ? -(p.entropy_loss_coef / (total > 1.f ? total : 1.f)) : 0.f;
+    __syncthreads();
+    // group stats (grpo.hip, ppo_utils.py:1164-1175): fp64 mean / unbiased std, fp32 normalisation
+    float adv_row = 0.f;
+    if (unit_live) {
+        float mean_f, denom_f;
+        if (G <= 1) {
+            mean_f = 0.f;
+            denom_f = norm_by_std ? (1.f + epsilon) : 1.f;
+        } else {
+            double sum = 0.0;
+            for (int j = 0; j < G; ++j) sum += (double)s_scores[j];
+            const double mean = sum / (double)G;
+            double m2 = 0.0;
+            for (int j = 0; j < G; ++j) {
+                const double d = (double)s_scores[j] - mean;
+                m2 += d * d;
+            }
+            mean_f = (float)mean;
+            const float std_f = (float)sqrt(m2 / (double)(G - 1));
+            denom_f = norm_by_std ? (std_f + epsilon) : 1.f;
+        }
+        const float sc = s_scores[row - group * G];
+        adv_row = norm_by_std ? (sc - mean_f) / denom_f : (sc - mean_f);
+    }
+    const float4 a4 = make_float4(adv_row * rm[0], adv_row * rm[1], adv_row * rm[2], adv_row * rm[3]);
+    const float lo = (float)(1.0 - (double)p.eps_clip_low);
+    const float hi = (float)(1.0 + (double)p.eps_clip_high);
+    float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        *reinterpret_cast<float4*>(adv_out + e) = a4;
+        const double mr = (double)row_msum[row];
+        const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
+        float scale, w;
+        if (p.loss_reduction == 0) { scale = tok_scale; w = 1.f; }
+        else if (p.loss_reduction == 1) { scale = (float)(1.0 / ((double)n * (mr > 1.0 ? mr : 1.0))); w = inv_mrow; }
+        else { scale = (float)(1.0 / ((double)n * (double)p.max_seq_len)); w = (float)(1.0 / (double)p.max_seq_len); }
+        float a[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        auto tok = [&](float L, float O, float A, float M, float RF, float E) -> float {
+            const TokenOut t = ppo_token(L, O, A, lo, hi, p.clip_ratio_c, p.dual_clip);
+            a[0] += t.loss * M;
+            a[1] += M;
+            a[2] += t.clip * M;
+            if (p.use_kl_loss) a[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
+            a[4] += E * M;
+            return (t.dldlp * M) * scale;
+        };
+        float4 g;
+        g.x = tok(l4.x, o4.x, a4.x, m4.x, r4.x, e4.x);
+        g.y = tok(l4.y, o4.y, a4.y, m4.y, r4.y, e4.y);
+        g.z = tok(l4.z, o4.z, a4.z, m4.z, r4.z, e4.z);
+        g.w = tok(l4.w, o4.w, a4.w, m4.w, r4.w, e4.w);
+        *reinterpret_cast<float4*>(glp + e) = g;
+        if (gent) *reinterpret_cast<float4*>(gent + e) = make_float4(escale * m4.x, escale * m4.y, escale * m4.z, escale * m4.w);
+        acc[0] = a[0] * w;
+        acc[1] = a[1];
+        acc[2] = a[2];
+        acc[3] = a[3] * inv_mrow;
+        acc[4] = a[4];
+    }
+    block_sum<kFW, kNP>(acc, s_red);
+    const unsigned epoch = s_epoch;
+    if (threadIdx.x < kNP) store_granule(gran + (int64_t)threadIdx.x * nb + wb, epoch, acc[threadIdx.x]);
+    if (wb != nb - 1) return;
+    fold_granules(gran, epoch, nb, n, p, s_redd, loss_out, metrics);
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)epoch_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // In-place x *= g[0] (the autograd backward of the fused loss); nothing is touched when g == 1.
 __global__ void rescale_kernel(const float* __restrict__ g, float* __restrict__ x, float* __restrict__ y, int64_t n) {
     const float s = g[0];
@@ -552,6 +731,60 @@ extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_p
                        entropy, rows, tot, n, R, nchunks, *params, grad_logp, grad_entropy, gran, epoch_word, loss_out,
                        metrics_out);
     return check_launch("ppo_loss_grad_kernel");
+}
+
+extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* response_mask, int mask_dtype,
+                                       int32_t num_groups, float epsilon, int32_t norm_by_std, const float* log_probs,
+                                       const float* old_log_probs, const float* loss_mask, const float* ref_log_probs,
+                                       const float* entropy, const float* row_mask_sum, int32_t n, int32_t R,
+                                       const skyrl_ppo_params* params, float* advantages, float* loss_out,
+                                       float* metrics_out, float* grad_logp, float* grad_entropy, void* workspace,
+                                       void* stream) {
+    SKYRL_REQUIRE(params, "grpo_ppo_loss_fwd: params is null");
+    SKYRL_REQUIRE(n > 0 && R > 0 && num_groups > 0, "grpo_ppo_loss_fwd: empty batch");
+    SKYRL_REQUIRE(n % num_groups == 0, "grpo_ppo_loss_fwd: contiguous groups need n % num_groups == 0");
+    SKYRL_REQUIRE(rewards && response_mask && advantages && log_probs && old_log_probs && loss_out && metrics_out &&
+                      grad_logp && workspace,
+                  "grpo_ppo_loss_fwd: null pointer");
+    SKYRL_REQUIRE(mask_dtype == SKYRL_F32 || mask_dtype == SKYRL_I64 || mask_dtype == SKYRL_I32 ||
+                      mask_dtype == SKYRL_U8,
+                  "grpo_ppo_loss_fwd: unsupported mask dtype");
+    const int G = n / num_groups;
+    const int nchunks = (R + kFT - 1) / kFT;
+    const int units = n * nchunks;
+    const bool need_total = params->loss_reduction == 0 || (params->use_entropy_loss && grad_entropy);
+    const bool one_launch = row_mask_sum && G <= kGroupMax && (R % 4) == 0 && units <= 2048 &&
+                            !(need_total && n > kInlineTotalRows) && aligned16(rewards) && aligned16(response_mask) &&
+                            aligned16(log_probs) && aligned16(old_log_probs) && aligned16(loss_mask) &&
+                            aligned16(ref_log_probs) && aligned16(entropy) && aligned16(advantages) &&
+                            aligned16(grad_logp) && aligned16(grad_entropy);
+    if (!one_launch) {  // larger batches (the fold would dominate) or other layouts: the two launches
+        int rc = skyrl_grpo_advantage(rewards, response_mask, mask_dtype, nullptr, nullptr, num_groups, n, R, epsilon,
+                                      norm_by_std, advantages, nullptr, stream);
+        if (rc) return rc;
+        return skyrl_ppo_loss_fwd(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy,
+                                  row_mask_sum, n, R, params, loss_out, metrics_out, grad_logp, grad_entropy,
+                                  workspace, stream);
+    }
+    SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "grpo_ppo_loss_fwd: use_kl_loss needs ref_log_probs");
+    SKYRL_REQUIRE(params->loss_reduction >= 0 && params->loss_reduction <= 2, "grpo_ppo_loss_fwd: bad loss_reduction");
+    SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
+                  "grpo_ppo_loss_fwd: seq_mean_token_sum_norm needs max_seq_len");
+    SKYRL_REQUIRE(params->kl_type >= 0 && params->kl_type <= 3, "grpo_ppo_loss_fwd: bad kl_type");
+    SKYRL_REQUIRE(!grad_entropy || params->use_entropy_loss, "grpo_ppo_loss_fwd: grad_entropy needs use_entropy_loss");
+    char* w = reinterpret_cast<char*>(workspace);
+    unsigned* epoch_word = reinterpret_cast<unsigned*>(w);
+    unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + 256);
+    const int xcd_map = (num_groups % 8) == 0 ? 1 : 0;  // grid stays n * nchunks blocks either way
+    auto k = mask_dtype == SKYRL_I64   ? grpo_loss_grad_kernel<SKYRL_I64>
+             : mask_dtype == SKYRL_F32 ? grpo_loss_grad_kernel<SKYRL_F32>
+             : mask_dtype == SKYRL_I32 ? grpo_loss_grad_kernel<SKYRL_I32>
+                                       : grpo_loss_grad_kernel<SKYRL_U8>;
+    hipLaunchKernelGGL(k, dim3(units), dim3(kThreads), 0, as_stream(stream), rewards, response_mask, num_groups, G,
+                       epsilon, norm_by_std, xcd_map, log_probs, old_log_probs, loss_mask, ref_log_probs, entropy,
+                       row_mask_sum, n, R, nchunks, *params, advantages, grad_logp, grad_entropy, gran, epoch_word,
+                       loss_out, metrics_out);
+    return check_launch("grpo_loss_grad_kernel");
 }
 
 extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, int64_t numel, float* grad_logp, float* grad_entropy,

@@ -336,6 +336,84 @@ class PPOLossFunction(torch.autograd.Function):
         return glp, None, None, None, None, gent, None, None
 
 
+class GRPOPPOLossFunction(torch.autograd.Function):
+    """GRPO advantage (contiguous groups) + the fused policy loss for a batch that is one
+    micro-batch: ``skyrl_grpo_ppo_loss_fwd``, ONE launch when the layout allows (see the
+    header), with outputs bit-identical to ``grpo_advantage`` followed by ``ppo_loss``.
+    forward returns (advantages [n,R], loss 0-d, metrics f32[8]); gradients flow to
+    log_probs (and entropy), exactly as ``PPOLossFunction``."""
+
+    @staticmethod
+    def forward(ctx, token_level_rewards, response_mask, num_groups, epsilon, norm_by_std, log_probs, old_log_probs,
+                loss_mask, ref_log_probs, entropy, params, loss_mask_row_sum):
+        dev = _require_gpu(token_level_rewards, response_mask, log_probs, old_log_probs, loss_mask, ref_log_probs,
+                           entropy)
+        rew = _f32c(token_level_rewards.detach(), "token_level_rewards")
+        rmask = response_mask.detach().contiguous()
+        if rmask.dtype not in _MASK_DTYPES:
+            raise TypeError(f"unsupported response_mask dtype {rmask.dtype}")
+        lp = _f32c(log_probs.detach(), "log_probs")
+        old = _f32c(old_log_probs.detach(), "old_log_probs")
+        mask = None if loss_mask is None else loss_mask.detach().to(torch.float32).contiguous()
+        ref = None if ref_log_probs is None else _f32c(ref_log_probs.detach(), "ref_log_probs")
+        ent = None if entropy is None else _f32c(entropy.detach(), "entropy")
+        if lp.dim() != 2:
+            raise ValueError(f"log_probs must be [n,R], got {tuple(lp.shape)}")
+        for name, t in (("token_level_rewards", rew), ("response_mask", rmask), ("old_log_probs", old),
+                        ("loss_mask", mask), ("ref", ref), ("entropy", ent)):
+            if t is not None and t.shape != lp.shape:
+                raise ValueError(f"{name} shape {tuple(t.shape)} != log_probs shape {tuple(lp.shape)}")
+        n, R = lp.shape
+        rows = None if loss_mask_row_sum is None else _f32c(loss_mask_row_sum.detach(), "loss_mask_row_sum")
+        adv = torch.empty_like(lp)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
+        glp = torch.empty_like(lp)
+        want_ent = bool(params.use_entropy_loss) and entropy is not None and ctx.needs_input_grad[9]
+        gent = torch.empty_like(lp) if want_ent else None
+        ws = WORKSPACES.get(dev, "ppo", _ffi.query("skyrl_ppo_loss_workspace_bytes", n, R))
+        _ffi.call(
+            "skyrl_grpo_ppo_loss_fwd", _ptr(rew), _ptr(rmask), _MASK_DTYPES[rmask.dtype], int(num_groups),
+            float(epsilon), int(bool(norm_by_std)), _ptr(lp), _ptr(old), _ptr(mask), _ptr(ref), _ptr(ent), _ptr(rows),
+            n, R, ctypes.byref(params), _ptr(adv), _ptr(loss), _ptr(metrics), _ptr(glp), _ptr(gent), _ptr(ws),
+            _stream(dev),
+        )
+        ctx.save_for_backward(glp, gent)
+        ctx.mark_non_differentiable(adv, metrics)
+        ctx.used = False
+        return adv, loss, metrics
+
+    @staticmethod
+    def backward(ctx, grad_adv, grad_loss, grad_metrics):
+        if ctx.used:
+            raise RuntimeError("the fused PPO loss supports a single backward pass")
+        ctx.used = True
+        glp, gent = ctx.saved_tensors
+        g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
+        _ffi.call("skyrl_ppo_loss_bwd", _ptr(g), glp.numel(), _ptr(glp), _ptr(gent), _stream(glp.device))
+        return None, None, None, None, None, glp, None, None, None, gent, None, None
+
+
+def grpo_ppo_loss(token_level_rewards, response_mask, num_groups, log_probs, old_log_probs, loss_mask, params,
+                  ref_log_probs=None, entropy=None, loss_mask_row_sum=None, epsilon=1e-6, norm_by_std=True):
+    """GRPO advantage + fused loss in one call; returns (advantages, loss, metrics). Layouts
+    the C entry's contiguous form cannot take (R % 4 != 0, groups > 16 rows, unaligned
+    buffers) run the two HIP calls, with the CSR GRPO kernel."""
+    n, R = log_probs.shape
+    ng = int(num_groups)
+    if ng > 0 and n % ng == 0:
+        tens = (token_level_rewards, response_mask, log_probs, old_log_probs, loss_mask, ref_log_probs, entropy)
+        contiguous_ok = R % 4 == 0 and n // ng <= 16 and all(
+            t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in tens)
+        if not contiguous_ok:
+            adv = grpo_advantage(token_level_rewards, response_mask, None, None, ng, epsilon, norm_by_std)
+            loss, metrics = ppo_loss(log_probs, old_log_probs, adv, loss_mask, params, ref_log_probs, entropy,
+                                     loss_mask_row_sum)
+            return adv, loss, metrics
+    return GRPOPPOLossFunction.apply(token_level_rewards, response_mask, num_groups, epsilon, norm_by_std, log_probs,
+                                     old_log_probs, loss_mask, ref_log_probs, entropy, params, loss_mask_row_sum)
+
+
 def ppo_loss(log_probs, old_log_probs, advantages, loss_mask, params, ref_log_probs=None, entropy=None,
              loss_mask_row_sum=None):
     """Fused loss; returns (loss 0-d tensor, metrics device tensor [8]). ``loss_mask_row_sum``

@@ -1,0 +1,123 @@
+"""a4 + a7 in one launch (skyrl_grpo_ppo_loss_fwd): the GRPO advantage computed inside the
+loss launch must give BIT-IDENTICAL advantages, loss, metrics and gradients to the two-call
+path (skyrl_grpo_advantage, then skyrl_ppo_loss_fwd), whose parity with the reference-made
+golden vectors and the oracle is pinned in test_gpu_parity.py; one case is also checked
+against the oracle directly (advantages 1e-6, loss 1e-6 / 1e-5 rel, gradients 1e-4 rel).
+Cases cover the one-launch kernel (XCD group map and plain map, every mask dtype, singleton
+groups, two column chunks) and the two-launch fallback (R % 4 != 0, > 2048 row chunks)."""
+
+import pytest
+import torch
+
+from oracle import cpu_ref
+from skyrl_amd import ops, ppo_utils
+from skyrl_amd.config import AlgorithmConfig
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # n, G, R, response-mask dtype, reduction, dual_clip, entropy loss, loss mask != response mask
+    (512, 8, 1024, torch.int64, "token_mean", False, False, False),  # the bench's leg: XCD map
+    (48, 4, 1024, torch.float32, "sequence_mean", True, True, True),  # 12 groups: plain map
+    (64, 8, 2048, torch.uint8, "seq_mean_token_sum_norm", True, False, False),  # two chunks per row
+    (40, 1, 1024, torch.int32, "token_mean", False, True, True),  # singleton groups
+    (96, 16, 300, torch.int64, "token_mean", True, False, False),  # R % 4 != 0: ops composes the two calls
+    (2560, 8, 1024, torch.int64, "token_mean", False, False, True),  # > 2048 chunks: two launches
+]
+
+
+def _inputs(n, R, G, mdt, seed):
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(0, R + 1, (n,), generator=g)
+    rmask = (torch.arange(R)[None] < lens[:, None]).to(mdt)
+    rew = torch.zeros(n, R)
+    hit = lens > 0
+    rew[torch.arange(n)[hit], lens[hit] - 1] = (torch.rand(int(hit.sum()), generator=g) < 0.4).float()
+    rew += 0.01 * torch.randn(n, R, generator=g) * rmask.float()  # dense token rewards too
+    lp = -2 + 0.1 * torch.randn(n, R, generator=g)
+    old = lp + 0.1 * torch.randn(n, R, generator=g)  # ratios far enough from 1 to clip
+    ref = lp + 0.05 * torch.randn(n, R, generator=g)
+    ent = torch.rand(n, R, generator=g)
+    return rew, rmask, lp, old, ref, ent
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"n{c[0]}_G{c[1]}_R{c[2]}" for c in CASES])
+def test_fused_matches_two_calls_bit_exact(dev, case):
+    n, G, R, mdt, red, dual, use_ent, sep_mask = case
+    rew, rmask, lp, old, ref, ent = _inputs(n, R, G, mdt, n * 7 + R)
+    lmask = rmask.float()
+    if sep_mask:  # multi-turn style: some response tokens carry no loss
+        lmask = lmask * (torch.arange(R)[None] % 5 != 2).float()
+    ng = n // G
+    cfg = AlgorithmConfig(loss_reduction=red, max_seq_len=R, use_entropy_loss=use_ent, entropy_loss_coef=0.01,
+                          policy_loss_type="dual_clip" if dual else "regular")
+    params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=use_ent, has_entropy=True)
+    d = {k: v.to(dev) for k, v in dict(rew=rew, rmask=rmask, lp=lp, old=old, ref=ref, ent=ent, lmask=lmask).items()}
+    rows = d["lmask"].sum(-1)
+    runs = []
+    for fused in (True, False):
+        x = d["lp"].clone().requires_grad_(True)
+        en = d["ent"].clone().requires_grad_(use_ent)
+        if fused:
+            adv, loss, m = ops.grpo_ppo_loss(d["rew"], d["rmask"], ng, x, d["old"], d["lmask"], params, d["ref"], en,
+                                             loss_mask_row_sum=rows)
+        else:
+            adv = ops.grpo_advantage(d["rew"], d["rmask"], None, None, ng)
+            loss, m = ops.ppo_loss(x, d["old"], adv, d["lmask"], params, d["ref"], en, loss_mask_row_sum=rows)
+        (loss * 1.5).backward()
+        runs.append((adv.cpu(), loss.detach().cpu(), m.cpu(), x.grad.cpu(), en.grad.cpu() if use_ent else None))
+    (a0, l0, m0, g0, e0), (a1, l1, m1, g1, e1) = runs
+    assert torch.equal(a0, a1), "advantages differ from skyrl_grpo_advantage"
+    assert torch.equal(l0, l1) and torch.equal(m0[:6], m1[:6]), (l0, l1, m0, m1)
+    assert m0[6] == 0  # the fold did not time out
+    assert torch.equal(g0, g1), "dL/dlogp differs from the two-call path"
+    if use_ent:
+        assert torch.equal(e0, e1)
+    assert float(m0[4]) > 0  # the clip branch ran
+
+
+def test_fused_vs_oracle(dev):
+    n, G, R = 512, 8, 1024
+    rew, rmask, lp, old, ref, ent = _inputs(n, R, G, torch.int64, 99)
+    mask = rmask.float()
+    cfg = AlgorithmConfig(policy_loss_type="dual_clip")
+    params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, has_entropy=True)
+    x = lp.to(dev).requires_grad_(True)
+    adv, loss, m = ops.grpo_ppo_loss(rew.to(dev), rmask.to(dev), n // G, x, old.to(dev), mask.to(dev), params,
+                                     ref.to(dev), ent.to(dev), loss_mask_row_sum=mask.sum(-1).to(dev))
+    loss.backward()
+    uids = [str(i // G) for i in range(n)]
+    eadv = cpu_ref.grpo_advantage(rew, rmask, uids)
+    torch.testing.assert_close(adv.cpu(), eadv, atol=1e-6, rtol=1e-6)
+    xc = lp.clone().requires_grad_(True)
+    e, em = cpu_ref.policy_loss_assembly(xc, old, eadv, mask, ref, ent, dual_clip=True)
+    e.backward()
+    torch.testing.assert_close(loss.detach().cpu(), e.detach(), atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(m[4].cpu(), torch.as_tensor(em["clip_ratio"]).detach().float(), atol=1e-6, rtol=0)
+    torch.testing.assert_close(x.grad.cpu(), xc.grad, atol=1e-9, rtol=1e-4)
+
+
+def test_fused_graph_replay_and_errors(dev):
+    """Replayed from a HIP graph the launch stays correct (the fold's epoch advances per
+    launch); bad layouts raise through the C ABI."""
+    n, G, R = 512, 8, 1024
+    rew, rmask, lp, old, ref, ent = _inputs(n, R, G, torch.int64, 5)
+    d = [t.to(dev) for t in (rew, rmask, lp, old, ref)]
+    mask = d[1].float()
+    rows = mask.sum(-1)
+    params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
+    adv0, loss0, m0 = ops.grpo_ppo_loss(d[0], d[1], n // G, d[2], d[3], mask, params, d[4], loss_mask_row_sum=rows)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        ops.grpo_ppo_loss(d[0], d[1], n // G, d[2], d[3], mask, params, d[4], loss_mask_row_sum=rows)
+    torch.cuda.synchronize(dev)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=side):
+        adv, loss, m = ops.grpo_ppo_loss(d[0], d[1], n // G, d[2], d[3], mask, params, d[4], loss_mask_row_sum=rows)
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(adv, adv0) and torch.equal(loss, loss0) and torch.equal(m[:7], m0[:7])
+    del graph
+    with pytest.raises(RuntimeError, match="n % num_groups"):
+        ops.grpo_ppo_loss(d[0], d[1], 7, d[2], d[3], mask, params, d[4], loss_mask_row_sum=rows)
