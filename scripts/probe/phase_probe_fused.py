@@ -1,5 +1,5 @@
-"""Where does the ppo_loss forward's launch time go? Builds the phase-timestamp variant
-(phase_probe.hip) and prints per-phase spans (us) for the first/last blocks and the launch."""
+"""Phase timeline of the GRPO-inside-the-loss launch (skyrl_grpo_ppo_loss_fwd), as
+phase_probe.py does for the loss alone; phase 5 = group scores ready (after the barrier)."""
 import ctypes
 import os
 import subprocess
@@ -11,7 +11,7 @@ import torch
 here = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(here))
 sys.path.insert(0, ROOT)
-so = "/tmp/libphase.so"
+so = "/tmp/libphase_fused.so"
 subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC",
                        "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "skyrl_amd", "csrc"),
                        os.path.join(here, "phase_probe.hip"), os.path.join(ROOT, "skyrl_amd", "csrc", "grpo.hip"), "-o", so])
@@ -25,8 +25,11 @@ g = torch.Generator(device=dev).manual_seed(0)
 lp = -2 + 0.1 * torch.randn(N, R, device=dev, generator=g)
 old = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
 ref = lp + 0.05 * torch.randn(N, R, device=dev, generator=g)
-adv = torch.randn(N, R, device=dev, generator=g)
+adv = torch.empty(N, R, device=dev)
 mask = torch.ones(N, R, device=dev)
+rmask = torch.ones(N, R, device=dev, dtype=torch.int64)
+rew = torch.zeros(N, R, device=dev)
+rew[:, -1] = (torch.rand(N, device=dev, generator=g) < 0.3).float()
 params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
 loss = torch.empty(1, device=dev)
 metrics = torch.empty(8, device=dev)
@@ -35,15 +38,16 @@ rows = mask.sum(-1)
 ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", N, R), dtype=torch.uint8, device=dev)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 P = ctypes.c_void_p
-fn = lib.skyrl_ppo_loss_fwd
+fn = lib.skyrl_grpo_ppo_loss_fwd
 fn.restype = ctypes.c_int
-fn.argtypes = [P, P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, P, P]
+I32 = ctypes.c_int32
+fn.argtypes = [P, P, ctypes.c_int, I32, ctypes.c_float, I32, P, P, P, P, P, P, I32, I32, P, P, P, P, P, P, P, P]
 
 
 def launch():
-    rc = fn(P(lp.data_ptr()), P(old.data_ptr()), P(adv.data_ptr()), P(mask.data_ptr()), P(ref.data_ptr()), None,
-            P(rows.data_ptr()), N, R, ctypes.byref(params), P(loss.data_ptr()), P(metrics.data_ptr()),
-            P(glp.data_ptr()), None, P(ws.data_ptr()), st)
+    rc = fn(P(rew.data_ptr()), P(rmask.data_ptr()), _ffi.I64, N // 8, 1e-6, 1, P(lp.data_ptr()), P(old.data_ptr()),
+            P(mask.data_ptr()), P(ref.data_ptr()), None, P(rows.data_ptr()), N, R, ctypes.byref(params),
+            P(adv.data_ptr()), P(loss.data_ptr()), P(metrics.data_ptr()), P(glp.data_ptr()), None, P(ws.data_ptr()), st)
     assert rc == 0
 
 
@@ -64,6 +68,6 @@ for rep in range(3):
     us = lambda x: (x - t0) / 100.0  # noqa: E731  (s_memrealtime: 100 MHz)
     f = len(t) - 1  # the folding block (the last of the grid)
     print(f"rep {rep}: {len(t)} blocks: entries {us(t[:, 0]).min():.2f}..{us(t[:, 0]).max():.2f} us; "
-          f"total ready (median span) {np.median((t[1:, 4] - t[1:, 0]) / 100):.2f}; "
+          f"scores ready (median span) {np.median((t[1:, 5] - t[1:, 0]) / 100):.2f}, last at {us(t[1:, 5]).max():.2f}; "
           f"token pass done (median span) {np.median((t[1:, 1] - t[1:, 0]) / 100):.2f}, last at {us(t[1:, 1]).max():.2f}; "
           f"folder: entry {us(t[f, 0]):.2f}, fold start {us(t[f, 2]):.2f}, end {us(t[f, 3]):.2f}")

@@ -368,6 +368,7 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
     __shared__ double s_redd[kFW * kNP];
     __shared__ float s_scores[kGroupMax];
     __shared__ unsigned s_epoch;
+    PHASE(0);
     if (threadIdx.x == 0) s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int nb = gridDim.x;
     const int wb = blockIdx.x;
@@ -391,19 +392,35 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
     const int64_t e = (int64_t)row * R + c0;
     float4 l4 = make_float4(0.f, 0.f, 0.f, 0.f), o4 = l4, r4 = l4, e4 = l4, m4 = make_float4(1.f, 1.f, 1.f, 1.f);
     float rm[4] = {0.f, 0.f, 0.f, 0.f};
-    if (live) {
-        l4 = *reinterpret_cast<const float4*>(lp + e);
-        o4 = *reinterpret_cast<const float4*>(old + e);
-        if (mask) m4 = *reinterpret_cast<const float4*>(mask + e);
-        if (p.use_kl_loss) r4 = *reinterpret_cast<const float4*>(ref + e);
-        if (ent) e4 = *reinterpret_cast<const float4*>(ent + e);
-        load_mask4(resp_mask, MDT, e, rm);
-    }
+    const float mrow_in = live ? row_msum[row] : 0.f;  // issued with the loads, not after the barrier
+    auto issue_loss_loads = [&]() {
+        if (live) {
+            l4 = *reinterpret_cast<const float4*>(lp + e);
+            o4 = *reinterpret_cast<const float4*>(old + e);
+            if (mask) m4 = *reinterpret_cast<const float4*>(mask + e);
+            if (p.use_kl_loss) r4 = *reinterpret_cast<const float4*>(ref + e);
+            if (ent) e4 = *reinterpret_cast<const float4*>(ent + e);
+            load_mask4(resp_mask, MDT, e, rm);
+        }
+    };
+    // token_mean total: this lane's row sums (n <= kInlineTotalRows on this path) issued with
+    // the other loads, summed after the barrier in ppo_loss_grad_kernel's order
+    const bool need_total = p.loss_reduction == 0 || (p.use_entropy_loss && gent);
+    constexpr int kTotPerLane = kInlineTotalRows / kWave;
+    float tv[kTotPerLane];
+    auto issue_total_loads = [&]() {
+#pragma unroll
+        for (int k = 0; k < kTotPerLane; ++k) {
+            const int r = lane + k * kWave;
+            tv[k] = (need_total && r < n) ? row_msum[r] : 0.f;
+        }
+    };
     // group scores: wave wv sums rows wv, wv + kFW, ... (grpo_adv_contig_kernel's lane order)
     const int n4 = R >> 2;
     if (unit_live && n4 <= 4 * kWave) {
-        // R <= 1024: every reward vector of the wave's (up to 4) rows in flight at once, so
-        // the scores cost one memory round trip, overlapped with the loss inputs' loads
+        // R <= 1024: every reward vector of the wave's (up to 4) rows in flight at once, issued
+        // BEFORE the loss inputs (loads retire in order), so the score reduction and the
+        // barrier overlap the loss inputs' flight
         float4 v[kGroupMax / kFW][4];
 #pragma unroll
         for (int q = 0; q < kGroupMax / kFW; ++q) {
@@ -415,6 +432,8 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
                 v[q][u] = (j < G && i < n4) ? rrow[i] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
+        issue_loss_loads();
+        issue_total_loads();
 #pragma unroll
         for (int q = 0; q < kGroupMax / kFW; ++q) {
             const int j = wv + q * kFW;
@@ -426,7 +445,11 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
                 if (lane == 0) s_scores[j] = acc;
             }
         }
-    } else if (unit_live) {
+    } else {
+        issue_loss_loads();
+        issue_total_loads();
+    }
+    if (unit_live && n4 > 4 * kWave) {
         for (int j = wv; j < G; j += kFW) {
             const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
             float acc = 0.f;
@@ -446,16 +469,17 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
             if (lane == 0) s_scores[j] = acc;
         }
     }
-    // the mask-only scales while the loads are in flight (as ppo_loss_grad_kernel)
-    const bool need_total = p.loss_reduction == 0 || (p.use_entropy_loss && gent);
+    __syncthreads();
+    PHASE(5);
     float total = 0.f;
     if (need_total) {
-        for (int r = lane; r < n; r += kWave) total += row_msum[r];
+#pragma unroll
+        for (int k = 0; k < kTotPerLane; ++k)
+            if (lane + k * kWave < n) total += tv[k];
         total = wave_sum(total);
     }
     const float tok_scale = 1.f / (total > 1.f ? total : 1.f);
     const float escale = need_total ? -(p.entropy_loss_coef / (total > 1.f ? total : 1.f)) : 0.f;
-    __syncthreads();
     // group stats (grpo.hip, ppo_utils.py:1164-1175): fp64 mean / unbiased std, fp32 normalisation
     float adv_row = 0.f;
     if (unit_live) {
@@ -485,7 +509,7 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
     float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
     if (live) {
         *reinterpret_cast<float4*>(adv_out + e) = a4;
-        const double mr = (double)row_msum[row];
+        const double mr = (double)mrow_in;
         const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
         float scale, w;
         if (p.loss_reduction == 0) { scale = tok_scale; w = 1.f; }
@@ -514,12 +538,15 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
         acc[3] = a[3] * inv_mrow;
         acc[4] = a[4];
     }
+    PHASE(1);
     block_sum<kFW, kNP>(acc, s_red);
     const unsigned epoch = s_epoch;
     if (threadIdx.x < kNP) store_granule(gran + (int64_t)threadIdx.x * nb + wb, epoch, acc[threadIdx.x]);
     if (wb != nb - 1) return;
+    PHASE(2);
     fold_granules(gran, epoch, nb, n, p, s_redd, loss_out, metrics);
     if (threadIdx.x == 0) __hip_atomic_store((gu32*)epoch_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PHASE(3);
 }
 
 // In-place x *= g[0] (the autograd backward of the fused loss); nothing is touched when g == 1.
