@@ -158,9 +158,10 @@ int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const
                        float* grad_logp /* [n,R] */, float* grad_entropy /* [n,R] or NULL */,
                        void* workspace, void* stream);
 /* a4 + a7 for a batch that is one micro-batch: skyrl_grpo_advantage (contiguous groups of
- * G = n/num_groups rows) followed by skyrl_ppo_loss_fwd on its advantages, in ONE launch
- * when G <= 16, R % 4 == 0, buffers are 16-B aligned, row_mask_sum is given and n*ceil(R/1024)
- * <= 2048 (two launches otherwise). Outputs are bit-identical to the two calls: advantages
+ * G = n/num_groups rows; its contiguous-form conditions apply: G <= 16, R % 4 == 0, 16-B
+ * aligned rewards/mask/advantages) followed by skyrl_ppo_loss_fwd on its advantages. ONE
+ * launch when row_mask_sum is given, every buffer is 16-B aligned, n*ceil(R/1024) <= 2048 and
+ * (token_mean) n <= 1024; the two launches otherwise. Outputs are bit-identical to the two calls: advantages
  * (adv*response_mask, f32 [n,R]), loss, metrics, grad_logp, grad_entropy. Replaces
  * compute_grpo_outcome_advantage (ppo_utils.py:1132-1182) + the loss of
  * PolicyWorkerBase._forward_backward_micro (workers/worker.py:810-876) when the mini-batch is
