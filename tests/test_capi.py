@@ -70,3 +70,19 @@ def test_cpu_tensor_is_rejected_not_computed():
 
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.approx_kl(torch.zeros(4), torch.zeros(4))
+
+
+def test_grpo_ppo_loss_entry_validates_on_host():
+    """skyrl_grpo_ppo_loss_fwd checks its layout before any launch: no GPU needed."""
+    params = _ffi.PPOParams(0.2, 0.2, 3.0, 0, 0, 0.0, 1, 3, 0.001, 0, 0.0, 0)
+    p = ctypes.c_void_p(16)
+    args = lambda ng, mdt: (p, p, mdt, ng, 1e-6, 1, p, p, p, p, None, p, 512, 1024, ctypes.byref(params),  # noqa: E731
+                            p, p, p, p, None, p, None)
+    with pytest.raises(_ffi.SkyrlHipError, match="n % num_groups"):
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", *args(7, _ffi.I64))
+    with pytest.raises(_ffi.SkyrlHipError, match="mask dtype"):
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", *args(64, 99))
+    with pytest.raises(_ffi.SkyrlHipError, match="params is null"):
+        a = list(args(64, _ffi.I64))
+        a[14] = None
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", *a)
