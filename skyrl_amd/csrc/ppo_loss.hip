@@ -687,6 +687,7 @@ using namespace skyrl;
 
 namespace skyrl {
 int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
+int g_loss_bwd_blocks = 256;  // skyrl_tune("loss_bwd_blocks"): grid cap of the backward rescale
 }
 
 extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
@@ -821,7 +822,7 @@ extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, int64_t numel, float* g
     if (numel == 0) return SKYRL_OK;
     // a small grid: at unit upstream gradient (the common case) the launch only dispatches
     int64_t blocks = (numel + kThreads - 1) / kThreads;
-    if (blocks > 256) blocks = 256;
+    if (blocks > g_loss_bwd_blocks) blocks = g_loss_bwd_blocks;
     hipLaunchKernelGGL(rescale_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, as_stream(stream), grad_out,
                        grad_logp, grad_entropy, numel);
     return check_launch("rescale_kernel");
