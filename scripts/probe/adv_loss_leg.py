@@ -13,9 +13,9 @@ out = {"batch": bench.advantage_loss_leg(dev, 512, 1024, variants=True),
        "batch_x16": bench.advantage_loss_leg(dev, 16 * 512, 1024, reps=5)}
 from skyrl_amd import _ffi  # noqa: E402
 
-for nb in (8, 32, 64, 256, 1024):  # backward node grid cap (unit gradient: every block exits at once)
-    _ffi.call("skyrl_tune", b"loss_bwd_blocks", nb)
-    out[f"bwd_blocks{nb}"] = {k: v for k, v in bench.advantage_loss_leg(dev, 512, 1024).items()
-                              if k in ("loss_bwd_us", "total_us")}
-_ffi.call("skyrl_tune", b"loss_bwd_blocks", 256)
+for rpb in (1, 2):  # row chunks per fused GRPO+loss block
+    _ffi.call("skyrl_tune", b"grpo_loss_rpb", rpb)
+    out[f"rpb{rpb}"] = {k: v for k, v in bench.advantage_loss_leg(dev, 512, 1024).items()
+                        if k in ("grpo_loss_fused_us", "total_us")}
+_ffi.call("skyrl_tune", b"grpo_loss_rpb", 1)
 print(json.dumps(out))

@@ -216,6 +216,7 @@ extern int g_train_ntstore;
 extern int g_grpo_slices;
 extern int g_loss_units;
 extern int g_loss_bwd_blocks;
+extern int g_grpo_loss_rpb;
 extern int g_sampler_row;
 extern int g_attn_pf;
 int lmhead_tune(int value);
@@ -250,6 +251,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "loss_units") {
         SKYRL_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "skyrl_tune: loss_units must be 0, 1, 2 or 4");
         g_loss_units = value;
+        return SKYRL_OK;
+    }
+    if (k == "grpo_loss_rpb") {
+        SKYRL_REQUIRE(value == 1 || value == 2, "skyrl_tune: grpo_loss_rpb must be 1 or 2");
+        g_grpo_loss_rpb = value;
         return SKYRL_OK;
     }
     if (k == "loss_bwd_blocks") {

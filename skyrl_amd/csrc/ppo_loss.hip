@@ -141,12 +141,15 @@ __device__ __forceinline__ unsigned long long load_granule(const unsigned long l
 
 // Sum the nb blocks' granules (value-major [kNP][nb]) into the loss and the metric vector;
 // run by the whole folding block. Thread t owns blocks t, t + kThreads, ... (fixed order).
+// NW = waves of the calling block (its threads >= kThreads hold zeros and only join the
+// barriers, so the fold order and the result are those of a kThreads block).
+template <int NW = kThreads / kWave>
 __device__ void fold_granules(const unsigned long long* gran, unsigned epoch, int nb, int n,
                               const skyrl_ppo_params& p, double* s_redd, float* __restrict__ loss_out,
                               float* __restrict__ metrics) {
     double tot[kNP] = {0, 0, 0, 0, 0};  // sum l*m*w, sum m, sum clip*m, sum kl*m*m/mrow, sum ent*m
     bool timed_out = false;
-    for (int b0 = threadIdx.x; b0 < nb && !timed_out; b0 += kThreads * kMaxGranPerThread) {
+    for (int b0 = threadIdx.x; b0 < nb && !timed_out && threadIdx.x < kThreads; b0 += kThreads * kMaxGranPerThread) {
         float v[kMaxGranPerThread][kNP];
         for (unsigned polls = 0;; ++polls) {
             bool ok = true;
@@ -176,7 +179,7 @@ __device__ void fold_granules(const unsigned long long* gran, unsigned epoch, in
                 for (int k = 0; k < kNP; ++k) tot[k] += (double)v[u][k];
     }
     const int any_timeout = __syncthreads_or(timed_out ? 1 : 0);
-    block_sum_d<kFW, kNP>(tot, s_redd);
+    block_sum_d<NW, kNP>(tot, s_redd);
     if (threadIdx.x == 0) {
         const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
         float pg = p.loss_reduction == 0 ? (float)(tot[0] / msum) : (float)(tot[0] / (double)n);
@@ -356,38 +359,44 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
 // b % 8), so the group's repeated reward reads (G*R*4 B) hit that XCD's L2.
 constexpr int kGroupMax = 16;
 
-template <int MDT>
-__global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
+// RPB row chunks per block (RPB x 256 threads, one chunk per 256-thread half): the group's
+// reward rows are read once per RPB units, each wave sums fewer of them, and every half
+// still publishes its own unit's granules (same fp32 partials, same fold as RPB = 1).
+template <int MDT, int RPB>
+__global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
     const float* __restrict__ rewards, const void* __restrict__ resp_mask, int num_groups, int G, float epsilon,
     int norm_by_std, int xcd_map, const float* __restrict__ lp, const float* __restrict__ old,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent,
     const float* __restrict__ row_msum, int n, int R, int nchunks, skyrl_ppo_params p, float* __restrict__ adv_out,
     float* __restrict__ glp, float* __restrict__ gent, unsigned long long* __restrict__ gran,
     unsigned* __restrict__ epoch_word, float* __restrict__ loss_out, float* __restrict__ metrics) {
-    __shared__ float s_red[kFW * kNP];
-    __shared__ double s_redd[kFW * kNP];
+    constexpr int kW = kFW * RPB;  // waves per block
+    __shared__ float s_red[kW * kNP];
+    __shared__ double s_redd[kW * kNP];
     __shared__ float s_scores[kGroupMax];
     __shared__ unsigned s_epoch;
     PHASE(0);
     if (threadIdx.x == 0) s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    const int nb = gridDim.x;
-    const int wb = blockIdx.x;
+    const int nb = gridDim.x * RPB;  // granule sets = units
+    const int half = threadIdx.x / kThreads;
+    const int tid = threadIdx.x % kThreads;
+    const int wb = blockIdx.x * RPB + half;  // this half's granule slot
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
-    const int gu = G * nchunks;  // units (row chunks) per group
+    const int gb = G * nchunks / RPB;  // blocks per group
     int group, local;
     if (xcd_map) {
-        const int k = wb >> 3;
-        group = (k / gu) * 8 + (wb & 7);
-        local = k % gu;
+        const int k = blockIdx.x >> 3;
+        group = (k / gb) * 8 + (blockIdx.x & 7);
+        local = (k % gb) * RPB + half;
     } else {
-        group = wb / gu;
-        local = wb % gu;
+        group = blockIdx.x / gb;
+        local = (blockIdx.x % gb) * RPB + half;
     }
     const bool unit_live = group < num_groups;
     const int row = unit_live ? group * G + local / nchunks : 0;
     const int chunk = local % nchunks;
-    const int c0 = chunk * kFT + threadIdx.x * 4;
+    const int c0 = chunk * kFT + tid * 4;
     const bool live = unit_live && c0 < R;  // R % 4 == 0 on this path
     const int64_t e = (int64_t)row * R + c0;
     float4 l4 = make_float4(0.f, 0.f, 0.f, 0.f), o4 = l4, r4 = l4, e4 = l4, m4 = make_float4(1.f, 1.f, 1.f, 1.f);
@@ -421,10 +430,10 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
         // R <= 1024: every reward vector of the wave's (up to 4) rows in flight at once, issued
         // BEFORE the loss inputs (loads retire in order), so the score reduction and the
         // barrier overlap the loss inputs' flight
-        float4 v[kGroupMax / kFW][4];
+        float4 v[kGroupMax / kW][4];
 #pragma unroll
-        for (int q = 0; q < kGroupMax / kFW; ++q) {
-            const int j = wv + q * kFW;
+        for (int q = 0; q < kGroupMax / kW; ++q) {
+            const int j = wv + q * kW;
             const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -435,8 +444,8 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
         issue_loss_loads();
         issue_total_loads();
 #pragma unroll
-        for (int q = 0; q < kGroupMax / kFW; ++q) {
-            const int j = wv + q * kFW;
+        for (int q = 0; q < kGroupMax / kW; ++q) {
+            const int j = wv + q * kW;
             if (j < G) {
                 float acc = 0.f;
 #pragma unroll
@@ -450,7 +459,7 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
         issue_total_loads();
     }
     if (unit_live && n4 > 4 * kWave) {
-        for (int j = wv; j < G; j += kFW) {
+        for (int j = wv; j < G; j += kW) {
             const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
             float acc = 0.f;
             int i = lane;
@@ -539,12 +548,23 @@ __global__ __launch_bounds__(kThreads) void grpo_loss_grad_kernel(
         acc[4] = a[4];
     }
     PHASE(1);
-    block_sum<kFW, kNP>(acc, s_red);
+    // per-half reduction: block_sum<kFW>'s wave tree and order over the half's own waves
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) acc[k] = wave_sum(acc[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < kNP; ++k) s_red[wv * kNP + k] = acc[k];
+    __syncthreads();
     const unsigned epoch = s_epoch;
-    if (threadIdx.x < kNP) store_granule(gran + (int64_t)threadIdx.x * nb + wb, epoch, acc[threadIdx.x]);
-    if (wb != nb - 1) return;
+    if (tid < kNP) {
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < kFW; ++j) sum += s_red[(half * kFW + j) * kNP + tid];
+        store_granule(gran + (int64_t)tid * nb + wb, epoch, sum);
+    }
+    if (blockIdx.x != gridDim.x - 1) return;
     PHASE(2);
-    fold_granules(gran, epoch, nb, n, p, s_redd, loss_out, metrics);
+    fold_granules<kW>(gran, epoch, nb, n, p, s_redd, loss_out, metrics);
     if (threadIdx.x == 0) __hip_atomic_store((gu32*)epoch_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PHASE(3);
 }
@@ -687,7 +707,9 @@ using namespace skyrl;
 
 namespace skyrl {
 int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
-int g_loss_bwd_blocks = 256;  // skyrl_tune("loss_bwd_blocks"): grid cap of the backward rescale
+int g_loss_bwd_blocks = 256;
+int g_grpo_loss_rpb = 1;  // skyrl_tune("grpo_loss_rpb", 1 / 2): row chunks per fused GRPO+loss block (2 measured slower: 12.1 vs 11.0 us)
+  // skyrl_tune("loss_bwd_blocks"): grid cap of the backward rescale
 }
 
 extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
@@ -804,11 +826,13 @@ extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* respons
     unsigned* epoch_word = reinterpret_cast<unsigned*>(w);
     unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + 256);
     const int xcd_map = (num_groups % 8) == 0 ? 1 : 0;  // grid stays n * nchunks blocks either way
-    auto k = mask_dtype == SKYRL_I64   ? grpo_loss_grad_kernel<SKYRL_I64>
-             : mask_dtype == SKYRL_F32 ? grpo_loss_grad_kernel<SKYRL_F32>
-             : mask_dtype == SKYRL_I32 ? grpo_loss_grad_kernel<SKYRL_I32>
-                                       : grpo_loss_grad_kernel<SKYRL_U8>;
-    hipLaunchKernelGGL(k, dim3(units), dim3(kThreads), 0, as_stream(stream), rewards, response_mask, num_groups, G,
+    const int rpb = (g_grpo_loss_rpb == 2 && (G * nchunks) % 2 == 0) ? 2 : 1;
+    auto pick = [&](auto k1, auto k2) { return rpb == 2 ? k2 : k1; };
+    auto k = mask_dtype == SKYRL_I64   ? pick(grpo_loss_grad_kernel<SKYRL_I64, 1>, grpo_loss_grad_kernel<SKYRL_I64, 2>)
+             : mask_dtype == SKYRL_F32 ? pick(grpo_loss_grad_kernel<SKYRL_F32, 1>, grpo_loss_grad_kernel<SKYRL_F32, 2>)
+             : mask_dtype == SKYRL_I32 ? pick(grpo_loss_grad_kernel<SKYRL_I32, 1>, grpo_loss_grad_kernel<SKYRL_I32, 2>)
+                                       : pick(grpo_loss_grad_kernel<SKYRL_U8, 1>, grpo_loss_grad_kernel<SKYRL_U8, 2>);
+    hipLaunchKernelGGL(k, dim3(units / rpb), dim3(kThreads * rpb), 0, as_stream(stream), rewards, response_mask, num_groups, G,
                        epsilon, norm_by_std, xcd_map, log_probs, old_log_probs, loss_mask, ref_log_probs, entropy,
                        row_mask_sum, n, R, nchunks, *params, advantages, grad_logp, grad_entropy, gran, epoch_word,
                        loss_out, metrics_out);

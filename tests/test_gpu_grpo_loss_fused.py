@@ -121,3 +121,17 @@ def test_fused_graph_replay_and_errors(dev):
     del graph
     with pytest.raises(RuntimeError, match="n % num_groups"):
         ops.grpo_ppo_loss(d[0], d[1], 7, d[2], d[3], mask, params, d[4], loss_mask_row_sum=rows)
+
+
+@pytest.mark.parametrize("rpb", [1, 2])
+def test_rows_per_block_variants(dev, rpb):
+    """Both block shapes of the one-launch kernel (skyrl_tune "grpo_loss_rpb") give the two
+    calls' outputs bit for bit."""
+    from skyrl_amd import _ffi
+
+    _ffi.call("skyrl_tune", b"grpo_loss_rpb", rpb)
+    try:
+        test_fused_matches_two_calls_bit_exact(dev, CASES[0])
+        test_fused_matches_two_calls_bit_exact(dev, CASES[2])
+    finally:
+        _ffi.call("skyrl_tune", b"grpo_loss_rpb", 1)
