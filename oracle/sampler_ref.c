@@ -6,10 +6,13 @@
  * third-party and absent here; its token stream is not pinned by any reference test
  * (tests/gpu/utils.py:222-236 compares text similarity only). The build therefore
  * defines its own counter-based sampler with the reference's filter semantics
- * (skyrl-tx/tx/utils/generator.py:213-227,398-449: temperature, top_k keeping values
- * >= the k-th largest, min_p relative to the max probability, top_p keeping tokens in
- * descending order while the mass strictly before them is < p (top token always, ties
- * in index order), greedy at T == 0, logprob of the sampled token from the raw logits),
+ * (skyrl-tx/tx/utils/generator.py:213-227,398-449: temperature; top_k keeping exactly k
+ * tokens, the k largest with equal values taken in index order (lax.top_k + the first-k
+ * mask, :410-418; fixture skyrl-tx/tests/utils/test_generator.py:197-207); min_p relative
+ * to the max probability (vLLM's, not in tx); top_p on the top_k-filtered distribution
+ * keeping tokens in descending order (stable argsort, ties in index order) while the mass
+ * strictly before them is < p, the top token always (:433-449; fixture :210-238); greedy at
+ * T == 0; logprob of the sampled token from the raw logits),
  * and this file is its oracle:
  * one thread, elements in index order, every decision-path float operation an IEEE
  * basic op or fmaf, compiled with -ffp-contract=off. Tokens must match bit for bit.
@@ -143,105 +146,150 @@ static int cmp_kept(const void* a, const void* b) {
     return (x->idx > y->idx) - (x->idx < y->idx);          /* index ascending */
 }
 
-/* k-th largest key (1-based k): sort a copy descending. */
-static int cmp_desc(const void* a, const void* b) {
-    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
-    return (x < y) - (x > y);
+/* top_k cut (1-based k): sort (key, index) by key descending / index ascending, keep the
+ * first k; the cut is the k-th entry's (key, index), and a key equal to the cut key stays
+ * only at an index <= the cut index (INT_MAX when the whole tie group fits in k). */
+static void topk_cut(kept_t* all, int V, int k, uint32_t* tk, int* ik) {
+    qsort(all, (size_t)V, sizeof(kept_t), cmp_kept);
+    *tk = all[k - 1].key;
+    *ik = (k < V && all[k].key == all[k - 1].key) ? all[k - 1].idx : 0x7fffffff;
 }
-static uint32_t kth_key(uint32_t* keys, int V, int k) {
-    qsort(keys, (size_t)V, sizeof(uint32_t), cmp_desc);
-    return keys[k - 1];
+static int in_cut(uint32_t kk, int v, uint32_t kcut, int icut) { return kk > kcut || (kk == kcut && v <= icut); }
+
+/* The filtered support of one row (temperature, top_k, min_p, top_p): a token v stays iff
+ * in_cut(key, v, tk, ik) (top_k), x/T >= mthr (min_p) and in_cut(key, v, kc, ic) (top_p). */
+typedef struct {
+    int use_topk, use_minp, use_topp;
+    uint32_t tk, kc;
+    int ik, ic;
+    float inv_t, mthr, mx;
+} row_filter_t;
+
+static float row_x(const uint16_t* rb, const float* rf, int v) { return rb ? bf16f(rb[v]) : rf[v]; }
+static uint32_t row_key_of(const uint16_t* rb, const float* rf, int v) { return rb ? okey_bf16(rb[v]) : okey_f32(rf[v]); }
+
+static row_filter_t row_filter(const uint16_t* rb, const float* rf, int V, float temperature, int top_k, float top_p,
+                               float min_p, kept_t* kept) {
+    row_filter_t f;
+    int v;
+    const int greedy = temperature == 0.0f;
+    f.use_topk = !greedy && top_k > 0 && top_k < V;
+    f.use_minp = !greedy && min_p > 0.0f;
+    f.use_topp = !greedy && top_p < 1.0f;
+    f.tk = 0;
+    f.ik = 0x7fffffff;
+    f.kc = 0;
+    f.ic = 0x7fffffff;
+    f.inv_t = greedy ? 1.0f : 1.0f / temperature;
+    f.mthr = 0.0f;
+    f.mx = -3.402823466e38f;
+    for (v = 0; v < V; ++v) f.mx = fmaxf(f.mx, row_x(rb, rf, v));
+    if (f.use_topk) {
+        for (v = 0; v < V; ++v) {
+            kept[v].key = row_key_of(rb, rf, v);
+            kept[v].idx = v;
+            kept[v].q = 0;
+        }
+        topk_cut(kept, V, top_k, &f.tk, &f.ik);
+    }
+    if (f.use_minp) f.mthr = f.mx * f.inv_t + det_ln(min_p);
+    if (f.use_topp) {
+        /* kept set (top_k and min_p), sorted by key desc / index asc; first key group whose
+         * cumulative mass reaches p*Z is the cut; its first c tokens (index order) stay */
+        int nk = 0, g;
+        uint64_t Z = 0, cum = 0;
+        double target;
+        for (v = 0; v < V; ++v) {
+            const uint32_t kk = row_key_of(rb, rf, v);
+            const float x = row_x(rb, rf, v);
+            if (f.use_topk && !in_cut(kk, v, f.tk, f.ik)) continue;
+            if (f.use_minp && x * f.inv_t < f.mthr) continue;
+            kept[nk].key = kk;
+            kept[nk].idx = v;
+            kept[nk].q = mass_q(x, f.mx, f.inv_t);
+            Z += kept[nk].q;
+            ++nk;
+        }
+        qsort(kept, (size_t)nk, sizeof(kept_t), cmp_kept);
+        target = (double)top_p * (double)Z;
+        for (g = 0; g < nk;) {
+            uint64_t gm = 0;
+            int e = g;
+            while (e < nk && kept[e].key == kept[g].key) gm += kept[e++].q;
+            if ((double)(cum + gm) >= target || e == nk) {
+                const uint64_t qc = kept[g].q;
+                long long c;
+                f.kc = kept[g].key;
+                if (qc == 0) {
+                    c = e - g;
+                } else {
+                    c = 0;
+                    while ((double)(cum + (uint64_t)c * qc) < target) ++c;
+                }
+                if (g == 0 && c < 1) c = 1;
+                if (c < e - g) f.ic = kept[g + c - 1].idx;
+                break;
+            }
+            cum += gm;
+            g = e;
+        }
+    }
+    return f;
+}
+
+static int row_keeps(const row_filter_t* f, const uint16_t* rb, const float* rf, int v) {
+    const uint32_t kk = row_key_of(rb, rf, v);
+    if (f->use_topk && !in_cut(kk, v, f->tk, f->ik)) return 0;
+    if (f->use_minp && row_x(rb, rf, v) * f->inv_t < f->mthr) return 0;
+    if (f->use_topp && !in_cut(kk, v, f->kc, f->ic)) return 0;
+    return 1;
+}
+
+/*
+ * The filtered support as a 0/1 mask per element (keep: uint8 [nseq, V]); the -inf pattern of
+ * apply_top_k_batch / apply_top_p_batch, checked against tx's fixtures by the CPU tests.
+ */
+void sampler_ref_support(const void* logits, int is_bf16, int64_t ld, int nseq, int V, float temperature, int top_k,
+                         float top_p, float min_p, uint8_t* keep) {
+    int i, v;
+    kept_t* kept = (kept_t*)malloc(sizeof(kept_t) * (size_t)V);
+    for (i = 0; i < nseq; ++i) {
+        const uint16_t* rb = is_bf16 ? (const uint16_t*)logits + (int64_t)i * ld : NULL;
+        const float* rf = is_bf16 ? NULL : (const float*)logits + (int64_t)i * ld;
+        const row_filter_t f = row_filter(rb, rf, V, temperature, top_k, top_p, min_p, kept);
+        for (v = 0; v < V; ++v) keep[(int64_t)i * V + v] = (uint8_t)(temperature == 0.0f || row_keeps(&f, rb, rf, v));
+    }
+    free(kept);
 }
 
 /*
  * logits: nseq rows of V elements, row stride ld; is_bf16 selects uint16 bf16 vs f32.
- * keys: scratch uint32[V]. tokens/logp: outputs.
+ * keys: unused (kept for the binding's signature). tokens/logp: outputs.
  */
 void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, float temperature, int top_k,
                  float top_p, float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens,
                  float* logp, uint32_t* keys) {
     int i, v;
     kept_t* kept = (kept_t*)malloc(sizeof(kept_t) * (size_t)V);
+    (void)keys;
     for (i = 0; i < nseq; ++i) {
         const uint16_t* rb = is_bf16 ? (const uint16_t*)logits + (int64_t)i * ld : NULL;
         const float* rf = is_bf16 ? NULL : (const float*)logits + (int64_t)i * ld;
-#define X(vv) (is_bf16 ? bf16f(rb[vv]) : rf[vv])
         const int greedy = temperature == 0.0f;
-        const int use_topk = !greedy && top_k > 0 && top_k < V;
-        const int use_minp = !greedy && min_p > 0.0f;
-        const int use_topp = !greedy && top_p < 1.0f;
-        uint32_t kc = 0;
-        int ic = 0x7fffffff;
-        const float inv_t = greedy ? 1.0f : 1.0f / temperature;
         const uint32_t key = row_key(seed, seq_ids ? seq_ids[i] : (int64_t)i, step);
-        uint32_t tk = 0;
-        float mthr = 0.0f, mx = -3.402823466e38f, best = -INFINITY;
+        const row_filter_t f = row_filter(rb, rf, V, temperature, top_k, top_p, min_p, kept);
+        float best = -INFINITY;
         int best_i = 0x7fffffff;
         double s = 0.0;
-        for (v = 0; v < V; ++v) mx = fmaxf(mx, X(v));
-        if (use_topk) {
-            for (v = 0; v < V; ++v) keys[v] = is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v]);
-            tk = kth_key(keys, V, top_k);
-        }
-        if (use_minp) mthr = mx * inv_t + det_ln(min_p);
-        if (use_topp) {
-            /* kept set (top_k and min_p), sorted by key desc / index asc; first key group whose
-             * cumulative mass reaches p*Z is the cut; its first c tokens (index order) stay */
-            int nk = 0, g, j;
-            uint64_t Z = 0, cum = 0;
-            for (v = 0; v < V; ++v) {
-                const uint32_t kk = is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v]);
-                const float x = X(v);
-                if (use_topk && kk < tk) continue;
-                if (use_minp && x * inv_t < mthr) continue;
-                kept[nk].key = kk;
-                kept[nk].idx = v;
-                kept[nk].q = mass_q(x, mx, inv_t);
-                Z += kept[nk].q;
-                ++nk;
-            }
-            qsort(kept, (size_t)nk, sizeof(kept_t), cmp_kept);
-            {
-                const double target = (double)top_p * (double)Z;
-                for (g = 0; g < nk;) {
-                    uint64_t gm = 0;
-                    int e = g;
-                    while (e < nk && kept[e].key == kept[g].key) gm += kept[e++].q;
-                    if ((double)(cum + gm) >= target || e == nk) {
-                        const uint64_t qc = kept[g].q;
-                        long long c;
-                        kc = kept[g].key;
-                        if (qc == 0) {
-                            c = e - g;
-                        } else {
-                            c = 0;
-                            while ((double)(cum + (uint64_t)c * qc) < target) ++c;
-                        }
-                        if (g == 0 && c < 1) c = 1;
-                        if (c < e - g) ic = kept[g + c - 1].idx;
-                        break;
-                    }
-                    cum += gm;
-                    g = e;
-                }
-            }
-            (void)j;
-        }
         for (v = 0; v < V; ++v) {
-            const float x = X(v);
+            const float x = row_x(rb, rf, v);
             float sc;
-            s += exp((double)x - (double)mx);
+            s += exp((double)x - (double)f.mx);
             if (greedy) {
                 sc = x;
             } else {
-                const float xs = x * inv_t;
-                if (use_topk && (is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v])) < tk) continue;
-                if (use_minp && xs < mthr) continue;
-                if (use_topp) {
-                    const uint32_t kk = is_bf16 ? okey_bf16(rb[v]) : okey_f32(rf[v]);
-                    if (kk < kc || (kk == kc && v > ic)) continue;
-                }
-                sc = xs + gumbel(key, (uint32_t)v);
+                if (!row_keeps(&f, rb, rf, v)) continue;
+                sc = x * f.inv_t + gumbel(key, (uint32_t)v);
             }
             if (sc > best || (sc == best && v < best_i)) {
                 best = sc;
@@ -249,8 +297,7 @@ void sampler_ref(const void* logits, int is_bf16, int64_t ld, int nseq, int V, f
             }
         }
         tokens[i] = best_i;
-        if (logp) logp[i] = (float)((double)X(best_i) - ((double)mx + log(s)));
-#undef X
+        if (logp) logp[i] = (float)((double)row_x(rb, rf, best_i) - ((double)f.mx + log(s)));
     }
     free(kept);
 }

@@ -5,7 +5,8 @@
 // logprob extraction :139-149; params inference_engines/utils.py:15-42,
 // defaults config/ppo_base_config.yaml:316-324). Filter semantics follow
 // skyrl-tx/tx/utils/generator.py:213-227,398-449: temperature first, then
-// top_k (keep values >= k-th largest, ties kept), then min_p; T == 0 is greedy
+// top_k (exactly k: the k largest, equal values in index order, as lax.top_k + the first-k
+// mask of apply_top_k_batch :410-418), then min_p, then top_p; T == 0 is greedy
 // over the raw logits; the returned logprob is log_softmax(raw logits)[token].
 //
 // Sampling is Gumbel-max, argmax_v (x_v/T - ln E_v) with E_v iid Exp(1), drawn per group of 8
@@ -106,19 +107,25 @@ __host__ __device__ __forceinline__ uint32_t mass_q(float x, float mx, float inv
 
 struct RowFilter {  // per row, written by the filter pre-pass
     float rmax;     // raw max logit
-    uint32_t tk;    // top_k: keep keys >= tk
+    uint32_t tk;    // top_k: keep keys > tk, and key == tk at indices <= ik
+    int32_t ik;
     uint32_t kc;    // top_p: keep keys > kc, and key == kc at indices <= ic
     int32_t ic;
 };
+// a key at index i inside a (key, index) cut: keys above it, or equal at an index up to it
+__device__ __forceinline__ bool in_cut(uint32_t kk, int i, uint32_t kcut, int icut) {
+    return kk > kcut || (kk == kcut && i <= icut);
+}
 
 // ---- filter pre-pass: one 1024-thread workgroup per row ---------------------------------
-// top_k (over all logits, ties kept: vLLM's `logits < kth` mask) and top_p (tx generator.py:
-// 424-449 on the top_k- and min_p-filtered distribution: tokens in descending order are kept
-// while the probability mass strictly before them is < p, the top token always, equal logits
-// in index order) by MSB-first radix selection over d = key(max) - key with 8-bit digits
+// top_k (tx generator.py:398-420: lax.top_k keeps exactly k, equal logits in index order, the
+// fixture tests/utils/test_generator.py:197-207) and top_p (tx generator.py:424-449 on the
+// top_k- and min_p-filtered distribution: tokens in descending order, equal logits in index
+// order (a stable argsort), are kept while the probability mass strictly before them is < p,
+// the top token always) by MSB-first radix selection over d = key(max) - key with 8-bit digits
 // (2 levels for bf16, 4 for f32): a 256-bin LDS histogram of counts (top_k) or of the
-// fixed-point masses (top_p) per level. The tie group at the top_p cut is resolved by an
-// index-ordered count.
+// fixed-point masses (top_p) per level. The tie group at either cut is resolved by an
+// index-ordered count: the cut is a (key, last index) pair.
 constexpr int kFT = 1024;
 template <typename T>
 __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict__ logits, int64_t ld, int V, int top_k,
@@ -265,29 +272,82 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
         return r;
     };
 
+    // index of the c-th (1-based) element in index order with pred(raw, i): rounds of kFT
+    // contiguous chunks of CH elements (thread t owns [base + t*CH, base + (t+1)*CH))
+    auto nth_index = [&](auto pred, long long c) -> int {
+        constexpr int CH = 16;
+        if (threadIdx.x == 0) s_ic = 0x7fffffff;
+        long long seen = 0;
+        for (int base = 0; base < V; base += kFT * CH) {
+            const int i0 = base + threadIdx.x * CH;
+            int cntt = 0;
+            for (int k = 0; k < CH; ++k) {
+                const int i = i0 + k;
+                if (i < V && pred(row[i], i)) ++cntt;
+            }
+            // block exclusive scan of cntt (wave scan + per-wave totals)
+            int incl = cntt;
+#pragma unroll
+            for (int off = 1; off < kWave; off <<= 1) {
+                const int o = __shfl_up(incl, off, kWave);
+                if (lane >= off) incl += o;
+            }
+            if (lane == kWave - 1) s_u[w] = (uint32_t)incl;
+            __syncthreads();
+            long long off_w = 0, tot = 0;
+            for (int j = 0; j < NW; ++j) {
+                if (j < w) off_w += s_u[j];
+                tot += s_u[j];
+            }
+            const long long before = seen + off_w + (incl - cntt);
+            if (cntt > 0 && before < c && before + cntt >= c) {  // the c-th is in my chunk
+                long long r2 = before;
+                for (int k = 0; k < CH; ++k) {
+                    const int i = i0 + k;
+                    if (i < V && pred(row[i], i) && ++r2 == c) s_ic = i;
+                }
+            }
+            seen += tot;
+            __syncthreads();
+            if (seen >= c) break;
+        }
+        const int r = s_ic;
+        __syncthreads();
+        return r;
+    };
+
     uint32_t tk = 0u;
+    int ik = 0x7fffffff;
     if (top_k > 0 && top_k < V) {
         bool done = false;
+        unsigned long long kbelow = 0ull, kat = 0ull;
         if constexpr (sizeof(T) == 2) {
             const Sel f = fine([&](T, int) -> unsigned long long { return 1ull; }, (double)top_k, false);
             if (f.ok) {
                 tk = kmax - f.d;
+                kbelow = f.below;
+                kat = f.at;
                 done = true;
             }
         }
         if (!done) {
             const auto r = radix([&](T, int) -> unsigned long long { return 1ull; }, (double)top_k);
             tk = kmax - r.d;
+            kbelow = r.below;
+            kat = r.at;
         }
+        // exactly k: the first (k - #above) of the tk tie group in index order
+        const long long c = (long long)top_k - (long long)kbelow;
+        if (c < (long long)kat) ik = nth_index([&](T raw, int) -> bool { return okey<T>(raw) == tk; }, c);
     }
     uint32_t kc = 0u;
     int ic = 0x7fffffff;
     if (top_p < 1.0f) {
-        auto kept = [&](T raw) -> bool {
-            return okey<T>(raw) >= tk && (!use_minp || to_f<T>(raw) * inv_t >= mthr);
+        auto kept = [&](T raw, int i) -> bool {
+            return in_cut(okey<T>(raw), i, tk, ik) && (!use_minp || to_f<T>(raw) * inv_t >= mthr);
         };
-        auto wmass = [&](T raw, int) -> unsigned long long {
-            return kept(raw) ? (unsigned long long)mass_q(to_f<T>(raw), mx, inv_t) : 0ull; };
+        auto wmass = [&](T raw, int i) -> unsigned long long {
+            return kept(raw, i) ? (unsigned long long)mass_q(to_f<T>(raw), mx, inv_t) : 0ull; };
         uint32_t dsel = 0u;
         unsigned long long below = 0ull, at = 0ull, Z = 0ull;
         double target = 0.0;
@@ -333,50 +393,11 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
             while ((double)(A + (unsigned long long)c * qc) < target) ++c;
             if (kc == kmax && c < 1) c = 1;
             const long long cnt = (long long)(r.at / qc);
-            if (c < cnt) {
-                // index of the c-th tie token (1-based) in index order: rounds of kFT contiguous
-                // chunks of CH elements (thread t owns [base + t*CH, base + (t+1)*CH))
-                constexpr int CH = 16;
-                if (threadIdx.x == 0) s_ic = 0x7fffffff;
-                long long seen = 0;
-                for (int base = 0; base < V; base += kFT * CH) {
-                    const int i0 = base + threadIdx.x * CH;
-                    int cntt = 0;
-                    for (int k = 0; k < CH; ++k) {
-                        const int i = i0 + k;
-                        if (i < V && okey<T>(row[i]) == kc && kept(row[i])) ++cntt;
-                    }
-                    // block exclusive scan of cntt (wave scan + per-wave totals)
-                    int incl = cntt;
-#pragma unroll
-                    for (int off = 1; off < kWave; off <<= 1) {
-                        const int o = __shfl_up(incl, off, kWave);
-                        if (lane >= off) incl += o;
-                    }
-                    if (lane == kWave - 1) s_u[w] = (uint32_t)incl;
-                    __syncthreads();
-                    long long off_w = 0, tot = 0;
-                    for (int j = 0; j < NW; ++j) {
-                        if (j < w) off_w += s_u[j];
-                        tot += s_u[j];
-                    }
-                    const long long before = seen + off_w + (incl - cntt);
-                    if (cntt > 0 && before < c && before + cntt >= c) {  // the c-th is in my chunk
-                        long long r2 = before;
-                        for (int k = 0; k < CH; ++k) {
-                            const int i = i0 + k;
-                            if (i < V && okey<T>(row[i]) == kc && kept(row[i]) && ++r2 == c) s_ic = i;
-                        }
-                    }
-                    seen += tot;
-                    __syncthreads();
-                    if (seen >= c) break;
-                }
-                ic = s_ic;
-            }
+            if (c < cnt)
+                ic = nth_index([&](T raw, int i) -> bool { return okey<T>(raw) == kc && kept(raw, i); }, c);
         }
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = RowFilter{mx, tk, kc, ic};
+    if (threadIdx.x == 0) out[blockIdx.x] = RowFilter{mx, tk, ik, kc, ic};
 }
 
 // MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p,
@@ -427,6 +448,7 @@ __device__ __forceinline__ void sample_unit(
     const bool use_minp = MODE == 2 && use_minp_rt;
     const bool use_topp = MODE == 2 && use_topp_rt;
     const uint32_t tk = use_topk ? filt[row_i].tk : 0u;
+    const int ik = use_topk ? filt[row_i].ik : 0;
     const float mthr = use_minp ? filt[row_i].rmax * inv_t + ln_min_p : 0.f;
     const uint32_t kc = use_topp ? filt[row_i].kc : 0u;
     const int ic = use_topp ? filt[row_i].ic : 0;
@@ -434,9 +456,9 @@ __device__ __forceinline__ void sample_unit(
     auto admissible = [&](T rawk, float xk, int v) -> bool {
         bool keep = true;
         const uint32_t kk = okey<T>(rawk);
-        if (use_topk) keep = keep && kk >= tk;
+        if (use_topk) keep = keep && in_cut(kk, v, tk, ik);
         if (use_minp) keep = keep && xk * inv_t >= mthr;
-        if (use_topp) keep = keep && (kk > kc || (kk == kc && v <= ic));
+        if (use_topp) keep = keep && in_cut(kk, v, kc, ic);
         return keep;
     };
     if (!greedy) {
@@ -984,7 +1006,7 @@ extern "C" int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t n
     SKYRL_REQUIRE(logits && tokens_out && workspace, "sample: null pointer");
     SKYRL_REQUIRE(temperature >= 0.f, "sample: temperature must be >= 0");
     SKYRL_REQUIRE(min_p >= 0.f && min_p <= 1.f, "sample: min_p must be in [0,1]");
-    SKYRL_REQUIRE(top_p > 0.f && top_p <= 1.f, "sample: top_p must be in (0,1]");
+    SKYRL_REQUIRE(top_p >= 0.f && top_p <= 1.f, "sample: top_p must be in [0,1]");
     if (dtype == SKYRL_BF16)
         return launch_sample<uint16_t>(logits, ld, nseq, V, temperature, top_k, top_p, min_p, seed, seq_ids, step,
                                        tokens_out, logp_out, workspace, as_stream(stream));

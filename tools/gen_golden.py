@@ -13,7 +13,9 @@ The reference never travels to the GPU box: only the .npz data does.
 
 from __future__ import annotations
 
+import dataclasses
 import enum
+import json
 import importlib.machinery
 import os
 import sys
@@ -439,6 +441,137 @@ def gen_reward_kl(trainer_mod, tb, cfgmod):
          **out)
 
 
+def _metrics(out, tag, m):
+    keys = sorted(m)
+    out[f"mkeys_{tag}"] = np.array(keys)
+    out[f"mvals_{tag}"] = np.array([float(m[k]) for k in keys], dtype=np.float64)
+
+
+def gen_secondary(pu, cfgmod):
+    """The secondary registry entries (ppo_utils.py:589-981 losses, :1013-1098 estimators) on the
+    reference's own KAT inputs (tests/cpu/algorithms/test_losses.py:85-137, 291-402, 442-615;
+    tests/cpu/utils/test_ppo_utils.py:65-129) and on seeded ragged batches, with every
+    reduction and (where the loss applies it) off-policy correction. Records loss, metrics and
+    dL/dlog_probs (autograd). clip_cov draws torch.randperm: the global seed is set right before
+    each call (the restatement consumes the generator identically)."""
+    out = {}
+    null_opc = cfgmod.OffPolicyCorrectionConfig(tis_ratio_type=None, sequence_mask_metric=None,
+                                                outlier_token_is_threshold_low=None,
+                                                outlier_token_is_threshold_high=None)
+    cases = []  # (tag, loss name, lp, old, adv, mask or None, rollout or None, cfg kwargs, seed)
+    # --- the reference's KAT inputs
+    adv3 = torch.tensor([[1.0, -1.0, -4.0]])
+    old3 = torch.tensor([[-1.0, -1.0, -3.0]])
+    lp3 = torch.tensor([[-1.69315, -1.0, -0.69741]])
+    cases.append(("kat_cispo", "cispo", lp3, old3, adv3, None, None,
+                  dict(cispo=cfgmod.CISPOConfig(cispo_eps_clip_low=0.2, cispo_eps_clip_high=0.2),
+                       loss_reduction="token_mean", max_seq_len=4), 0))
+    gadv = torch.tensor([[1.5, 2.0, 1.0, 0.8, 0.5, 0.0, 0.0, 0.0], [3.0, 1.5, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0],
+                         [0.5, 0.8, 1.2, 2.5, 0.0, 0.0, 0.0, 0.0]])
+    gold = torch.full((3, 8), -1.0)
+    glp = torch.tensor([[0.2, -2.5, -0.3, 0.1, -1.8, -1.0, -1.0, -1.0], [0.8, -0.2, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0],
+                        [-0.5, 0.3, -1.7, 0.4, -1.0, -1.0, -1.0, -1.0]])
+    gmask = torch.tensor([[1.0, 1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0], [1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0],
+                          [1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0]])
+    cases.append(("kat_gspo", "gspo", glp, gold, gadv, gmask, None,
+                  dict(eps_clip_low=0.2, eps_clip_high=0.2, clip_ratio_c=3.0, loss_reduction="sequence_mean",
+                       max_seq_len=4), 0))
+    cadv = torch.tensor([[2.0, -1.0, 1.5, 0.8], [1.0, 0.5, -2.0, 1.2]])
+    cold = torch.full((2, 4), -1.0)
+    clp = torch.tensor([[-0.5, -1.5, -0.8, -1.2], [-1.3, -0.7, -1.8, -0.9]])
+    cmask = torch.tensor([[1.0, 1.0, 1.0, 1.0], [1.0, 1.0, 1.0, 0.0]])
+    cases.append(("kat_clip_cov", "clip_cov", clp, cold, cadv, cmask, None,
+                  dict(eps_clip_low=0.2, eps_clip_high=0.2, loss_reduction="token_mean", max_seq_len=4,
+                       clip_cov=cfgmod.ClipCovConfig(clip_ratio=0.5, clip_cov_lb=-5.0, clip_cov_ub=5.0)), 42))
+    kadv = torch.tensor([[1.5, -0.5, 2.0, 0.8], [0.5, 1.0, -1.5, 1.2]])
+    klp = torch.tensor([[-0.8, -1.2, -0.6, -1.1], [-1.1, -0.9, -1.4, -0.7]])
+    cases.append(("kat_kl_cov", "kl_cov", klp, cold, kadv, cmask, None,
+                  dict(loss_reduction="token_mean", max_seq_len=4,
+                       kl_cov=cfgmod.KLCovConfig(kl_cov_frac=0.5, ppo_kl_coef=1.0)), 42))
+    sadv = torch.tensor([[1.0, -1.0, 0.5]])
+    slp = torch.tensor([[-1.5, -0.8, -1.1]])
+    cases.append(("kat_sapo", "sapo", slp, torch.full((1, 3), -1.0), sadv, None, None,
+                  dict(loss_reduction="sequence_mean", max_seq_len=4,
+                       sapo=cfgmod.SAPOConfig(tau_pos=1.0, tau_neg=2.0)), 0))
+    # --- seeded ragged batches: every reduction, off-policy correction where the loss applies it
+    g = torch.Generator().manual_seed(2024)
+    n, R = 6, 37
+    lp, old, adv, mask, ref, ent = _ppo_inputs(g, n, R)
+    rollout = old + torch.randn(n, R, generator=g) * 0.05
+    rollout[3] = old[3] - 1.5
+    extra = {"gspo": dict(eps_clip_low=0.2, eps_clip_high=0.28),
+             "sapo": dict(sapo=cfgmod.SAPOConfig(tau_pos=1.0, tau_neg=1.05)),
+             "cispo": dict(cispo=cfgmod.CISPOConfig(cispo_eps_clip_low=0.2, cispo_eps_clip_high=0.3)),
+             "clip_cov": dict(eps_clip_low=0.2, eps_clip_high=0.28,
+                              clip_cov=cfgmod.ClipCovConfig(clip_ratio=0.05, clip_cov_lb=-1.0, clip_cov_ub=2.0)),
+             "kl_cov": dict(kl_cov=cfgmod.KLCovConfig(kl_cov_frac=0.1, ppo_kl_coef=0.5)),
+             "cross_entropy": {}, "importance_sampling": {}}
+    for name, kw in extra.items():
+        reds = ("token_mean",) if name in ("cross_entropy", "importance_sampling") else (
+            "token_mean", "sequence_mean", "seq_mean_token_sum_norm")
+        for red in reds:
+            cases.append((f"rand_{name}_{red}", name, lp, old, adv, mask, None,
+                          dict(kw, loss_reduction=red, max_seq_len=50), 7))
+        if name in ("gspo", "sapo", "cispo"):  # these apply apply_off_policy_correction
+            opc = cfgmod.OffPolicyCorrectionConfig(tis_ratio_type="token", token_tis_ratio_clip_high=2.0,
+                                                   sequence_mask_metric="product", product_mask_high=2.0,
+                                                   product_mask_low=0.5)
+            cases.append((f"rand_{name}_offpolicy", name, lp, old, adv, mask, rollout,
+                          dict(kw, loss_reduction="token_mean", max_seq_len=50, off_policy_correction=opc), 7))
+    tags = []
+    for tag, name, x0, o, a, m, ro, kw, seed in cases:
+        kw = dict(kw)
+        kw.setdefault("off_policy_correction", null_opc)
+        cfg = cfgmod.AlgorithmConfig(policy_loss_type=name, **kw)
+        x = x0.clone().requires_grad_(True)
+        torch.manual_seed(seed)
+        loss, met = pu.PolicyLossRegistry.get(name)(x, o, a, cfg, loss_mask=m, rollout_logprobs=ro)
+        loss.backward()
+        out[f"lp_{tag}"] = x0
+        out[f"old_{tag}"] = o
+        out[f"adv_{tag}"] = a
+        if m is not None:
+            out[f"mask_{tag}"] = m
+        if ro is not None:
+            out[f"rollout_{tag}"] = ro
+        out[f"loss_{tag}"] = loss.detach()
+        out[f"grad_{tag}"] = x.grad if x.grad is not None else torch.zeros_like(x0)
+        _metrics(out, tag, met)
+        cfgd = {k: (dataclasses.asdict(v) if dataclasses.is_dataclass(v) else v) for k, v in kw.items()}
+        cfgd["policy_loss_type"] = name
+        out[f"cfg_{tag}"] = np.array(json.dumps(cfgd, sort_keys=True))
+        out[f"seed_{tag}"] = np.int64(seed)
+        tags.append(tag)
+    # --- estimators: the KAT inputs and a seeded ragged batch
+    est = []
+    r3 = torch.tensor([[1.0, 2.0, 3.0]])
+    est.append(("kat_rpp_g1", "reinforce++", r3, torch.tensor([[1.0, 1.0, 0.0]]), None, 1.0))
+    est.append(("kat_rpp_g05", "reinforce++", r3, torch.ones(1, 3), None, 0.5))
+    rl = torch.tensor([[0.0, 0.0, 6.0], [0.0, 0.0, 3.0], [0.0, 0.0, 9.0], [0.0, 0.0, 12.0], [0.0, 0.0, 1.0]])
+    est.append(("kat_rloo", "rloo", rl, torch.ones_like(rl), np.array([0, 0, 1, 1, 2]), 1.0))
+    g2 = torch.Generator().manual_seed(77)
+    rn, rR = 12, 19
+    lens = torch.randint(1, rR + 1, (rn,), generator=g2)
+    rmask = (torch.arange(rR)[None, :] < lens[:, None]).float()
+    rrew = torch.randn(rn, rR, generator=g2) * rmask
+    ridx = np.array([str(i // 4) for i in range(rn - 1)] + ["solo"])
+    est.append(("rand_rpp", "reinforce++", rrew, rmask, None, 0.97))
+    est.append(("rand_rloo", "rloo", rrew, rmask, ridx, 1.0))
+    etags = []
+    for tag, name, rew, rm, idx, gamma in est:
+        fn = pu.AdvantageEstimatorRegistry.get(name)
+        a, r = fn(token_level_rewards=rew.clone(), response_mask=rm, index=idx, gamma=gamma)
+        out[f"rew_{tag}"] = rew
+        out[f"rmask_{tag}"] = rm
+        if idx is not None:
+            out[f"index_{tag}"] = np.asarray(idx).astype(str)
+        out[f"gamma_{tag}"] = np.float64(gamma)
+        out[f"eadv_{tag}"] = a
+        out[f"eret_{tag}"] = r
+        etags.append(tag)
+    save("secondary", loss_tags=np.array(tags), est_tags=np.array(etags), **out)
+
+
 def main():
     install_shim()
     torch.set_num_threads(4)
@@ -460,6 +593,7 @@ def main():
         "logprob": lambda: gen_logprob(tu),
         "pack": lambda: gen_pack(pre, trainer_mod, tb),
         "reward_kl": lambda: gen_reward_kl(trainer_mod, tb, cfgmod),
+        "secondary": lambda: gen_secondary(pu, cfgmod),
     }
     for name in (sys.argv[1:] or list(jobs)):  # `python -B tools/gen_golden.py ppo_offpolicy` regenerates one
         jobs[name]()
