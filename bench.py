@@ -8,7 +8,7 @@ path over one synthetic batch:
   rollout   R decode steps of skyrl_sample over [512, V] logits (T=1, top_p=1, top_k=-1)
   pack      skyrl_pack_experience: ragged prompts/responses -> padded training tensors
   ref/old   skyrl_logprob_fwd over all 512x1024 response positions (2 passes)
-  advantage skyrl_grpo_advantage over [512, 1024]
+  advantage skyrl_grpo_advantage over [512, 1024] (contiguous groups, pack's reward row sums)
   update    per micro-batch (16 seqs): skyrl_policy_train_fwd, ONE pass per token computing
             logprob + entropy + PPO/KL loss and writing dlogits (bf16); metrics read once per step
   optimizer grad norm + clip + AdamW over Qwen2.5-1.5B's 1.54 B fp32 params, writing the bf16
@@ -175,8 +175,7 @@ def run(args):
 
     sampler = TokenSampler(N, V, R, dev, SamplingParams(), seed=0, seq_ids=seq_ids)
     base_ptr = logits.data_ptr()
-    goff, grows, ng = ops.groups_from_index(uids)
-    goff, grows = goff.to(dev), grows.to(dev)
+    _, _, ng = ops.groups_from_index(uids)  # contiguous groups of GROUP rows (uid = i // GROUP)
     cfg = AlgorithmConfig()
     params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, has_entropy=True)
     fwd_timer = KernelTimer()
@@ -208,9 +207,9 @@ def run(args):
         # ---- pack ragged rollout output into the padded training tensors
         rtok = sampler.tokens[tok_t, tok_n]
         rlp_sampled = sampler.logprobs[tok_t, tok_n]
-        seqs, att, rmask, rew, lmask, rlp = ops.pack_experience(
+        seqs, att, rmask, rew, lmask, rlp, _, scores = ops.pack_experience(
             data["ptok"], data["poff"], rtok, roff, data["rew"], roff, data["lmask"],
-            roff, rlp_sampled, roff, N=N, P=P_MAX, R=R, pad=0, pad_token_id=0)
+            roff, rlp_sampled, roff, N=N, P=P_MAX, R=R, pad=0, pad_token_id=0, return_row_sums=True)
         labels = seqs[:, P_MAX:]  # the sampled response tokens (int64 view, row stride P+R)
         # ---- ref + old policy logprobs over all response positions (no grad). The old policy is the
         #      rollout policy (on-policy, one mini-batch per step: ratio 1 as in the reference); the ref
@@ -223,8 +222,9 @@ def run(args):
                 fwd_timer.wrap(lambda: ops._ffi.call(
                     "skyrl_logprob_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V, ops._ptr(lab),
                     lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None, ops._stream(dev)))
-        # ---- GRPO advantage over the whole batch
-        adv = ops.grpo_advantage(rew, rmask, goff, grows, ng)
+        # ---- GRPO advantage over the whole batch: contiguous groups of G (the rollout layout), the
+        #      pack kernel's per-row reward sums as the scores
+        adv = ops.grpo_advantage(rew, rmask, None, None, ng, scores=scores)
         # ---- update: per micro-batch fused policy pass (logprob/entropy fwd + PPO/KL loss +
         #      logprob bwd -> dlogits); --unfused runs the four separate kernels instead
         metrics_acc.zero_()
@@ -408,16 +408,22 @@ def pmc_traffic(kernel_name, algorithmic_bytes):
 
 
 def advantage_loss_leg(dev, N, R, reps=20, variants=False):
-    """GRPO advantage + fused PPO/KL loss (forward, gradient and loss fold in ONE launch) +
-    the loss backward (an in-place rescale that touches nothing at unit upstream gradient)
-    on [N, R]: the SURVEY §8(d) "advantage+loss" kernels (12 + 20 + 24 = 56 algorithmic
-    B/token). Launched through the C ABI inside a captured HIP graph and replayed, so host
-    launch cost is excluded and inter-kernel gaps are included. The loss-mask row sums are
-    the pack kernel's (skyrl_pack_experience emits them with the batch). `total_us` is the
-    product path: skyrl_grpo_ppo_loss_fwd (GRPO inside the loss launch, one launch up to
-    2048 row chunks, two above) + the backward; `two_call_total_us` is GRPO, loss, backward
-    as three launches. Both keep the 56 B/token figure. Returns per-kernel and total
-    microseconds."""
+    """GRPO advantage + fused PPO/KL loss + the loss backward on [N, R]: the SURVEY §8(d)
+    "advantage+loss" kernels (12 + 20 + 24 = 56 algorithmic B/token). Launched through the C
+    ABI inside a captured HIP graph and replayed, so host launch cost is excluded and
+    inter-kernel gaps are included. The loss-mask row sums and the GRPO scores (per-row reward
+    sums) are the pack kernel's (skyrl_pack_experience emits both with the batch).
+
+    `total_us` is the product path (GRPOTrainer._loss -> ops.grpo_ppo_loss(defer_fold=True,
+    want_advantages=False) and its backward): skyrl_grpo_ppo_loss_fwd with the scores and
+    SKYRL_LOSS_DEFER_FOLD (GRPO, loss and gradient in one launch that leaves per-block records;
+    no advantages output, so the int64 response mask is not read: the loss mask is 0 outside the
+    response) + skyrl_ppo_loss_finish (the backward: folds the records into loss/metrics,
+    rescales when the upstream gradient != 1). `deferred_with_adv_out_total_us` also writes the
+    advantages.
+    `in_launch_fold_total_us` is the r02 form (the fold spins in the forward's last block,
+    then a separate backward); `two_call_total_us` GRPO, loss, backward as three launches.
+    All keep the 56 B/token figure. Returns per-kernel and total microseconds."""
     from skyrl_amd import _ffi, ppo_utils
     from skyrl_amd.config import AlgorithmConfig
     from skyrl_amd.ops import _ptr
@@ -440,23 +446,38 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
     ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", N, R), dtype=torch.uint8, device=dev)
     params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
     ng = N // GROUP
+    scores = rew.sum(-1)  # = pack's reward_row_sum (one nonzero per row: any summation order is exact)
 
-    def grpo(s):
-        _ffi.call("skyrl_grpo_advantage", _ptr(rew), _ptr(rmask), _ffi.I64, None, None, ng, N, R, 1e-6, 1,
+    def grpo(s, sc=None):
+        _ffi.call("skyrl_grpo_advantage", _ptr(rew), _ptr(sc), _ptr(rmask), _ffi.I64, None, None, ng, N, R, 1e-6, 1,
                   _ptr(adv), None, s)
 
-    def fwd(s, with_rows=True):
+    def fwd(s, with_rows=True, flags=0):
         _ffi.call("skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(lmask), _ptr(ref), None,
                   _ptr(rows) if with_rows else None, N, R, ctypes.byref(params), _ptr(loss), _ptr(met), _ptr(glp),
-                  None, _ptr(ws), s)
+                  None, flags, _ptr(ws), s)
 
     def bwd(s):
         _ffi.call("skyrl_ppo_loss_bwd", _ptr(gout), N * R, _ptr(glp), None, s)
 
-    def fused(s):  # GRPO inside the loss launch (skyrl_grpo_ppo_loss_fwd), same outputs
-        _ffi.call("skyrl_grpo_ppo_loss_fwd", _ptr(rew), _ptr(rmask), _ffi.I64, ng, 1e-6, 1, _ptr(lp), _ptr(old),
-                  _ptr(lmask), _ptr(ref), None, _ptr(rows), N, R, ctypes.byref(params), _ptr(adv), _ptr(loss),
-                  _ptr(met), _ptr(glp), None, _ptr(ws), s)
+    def fused(s, sc=None, flags=0, adv_out=True):  # GRPO inside the loss launch (skyrl_grpo_ppo_loss_fwd)
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", _ptr(rew), _ptr(sc), _ptr(rmask) if adv_out else None, _ffi.I64, ng,
+                  1e-6, 1, _ptr(lp), _ptr(old), _ptr(lmask), _ptr(ref), None, _ptr(rows), N, R,
+                  ctypes.byref(params), _ptr(adv) if adv_out else None, _ptr(loss), _ptr(met), _ptr(glp), None, flags,
+                  _ptr(ws), s)
+
+    one_launch = N * ((R + 1023) // 1024) <= 2048  # skyrl_grpo_ppo_loss_fwd's one-launch layout
+
+    def fused_deferred(s):  # the product path (GRPOTrainer._loss): pack's scores, no advantages output (the
+        # trainer has them; ops passes the buffers when the layout runs two launches), fold left to the backward
+        fused(s, scores, _ffi.LOSS_DEFER_FOLD, adv_out=not one_launch)
+
+    def fused_deferred_adv(s):  # the same, writing adv * response_mask as well
+        fused(s, scores, _ffi.LOSS_DEFER_FOLD)
+
+    def finish(s):  # backward of the deferred forward: fold + rescale (nothing to rescale at g == 1)
+        _ffi.call("skyrl_ppo_loss_finish", _ptr(gout), _ptr(glp), None, N, R, ctypes.byref(params), _ptr(loss),
+                  _ptr(met), _ptr(ws), s)
 
     def timed(fns):
         side = torch.cuda.Stream(dev)
@@ -485,7 +506,10 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
     out = {}
     for name, fns in (("grpo_us", (grpo,)), ("loss_fwd_us", (fwd,)), ("loss_bwd_us", (bwd,)),
                       ("grpo_loss_fused_us", (fused,)), ("two_call_total_us", (grpo, fwd, bwd)),
-                      ("total_us", (fused, bwd))):
+                      ("in_launch_fold_total_us", (fused, bwd)),
+                      ("grpo_loss_deferred_us", (fused_deferred,)), ("finish_us", (finish,)),
+                      ("deferred_with_adv_out_total_us", (fused_deferred_adv, finish)),
+                      ("total_us", (fused_deferred, finish))):
         out[name] = timed(fns)
     if variants:
         out["variants"] = {"total_without_row_sums_us": timed((grpo, lambda s: fwd(s, False), bwd)),

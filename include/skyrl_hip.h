@@ -41,7 +41,9 @@ extern "C" {
 const char* skyrl_last_error(void);
 /* ABI version; bumped on any signature change (2: skyrl_sample takes top_p; 3: one-launch
  * skyrl_ppo_loss_fwd writing final gradients, in-place skyrl_ppo_loss_bwd, pack emits
- * loss-mask row sums; 4: skyrl_policy_train_fwd takes grad_logits strides). */
+ * loss-mask row sums; 4: skyrl_policy_train_fwd takes grad_logits strides; 5: pack emits
+ * reward row sums (GRPO scores), skyrl_grpo_advantage / skyrl_grpo_ppo_loss_fwd take them,
+ * the loss forwards take flags (SKYRL_LOSS_DEFER_FOLD) and skyrl_ppo_loss_finish). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -62,13 +64,16 @@ int skyrl_tune(const char* key, int value);
  * reached through compute_advantages_and_returns (ppo_utils.py:1190-1214).
  * score[i] = sum_t rewards[i,t]; per uid group: mean, unbiased std (singleton:
  * mean 0, std 1); adv = (score-mean)/(std+eps) (or score-mean); out = adv*mask.
+ * scores_in (f32 [N], e.g. skyrl_pack_experience's reward_row_sum) replaces the reward
+ * reads when given (rewards may then be NULL).
  * Groups are given in CSR form: rows of group g are group_rows[group_off[g] ..
  * group_off[g+1]) (the host maps the reference's `index` uids to groups).
  * group_off == group_rows == NULL means contiguous groups of G = N/num_groups
  * rows each (the trainer's layout, generators/utils.py:373-393); that form needs
  * G <= 16, R % 4 == 0 and 16-B aligned buffers, and skips the index loads.
  * rewards/out: f32 [N,R] row-major contiguous; mask: [N,R] of mask_dtype.   */
-int skyrl_grpo_advantage(const float* rewards, const void* response_mask, int mask_dtype,
+int skyrl_grpo_advantage(const float* rewards, const float* scores_in /* [N] or NULL */,
+                         const void* response_mask, int mask_dtype,
                          const int32_t* group_off, const int32_t* group_rows, int32_t num_groups,
                          int32_t N, int32_t R, float epsilon, int32_t norm_by_std,
                          float* advantages, float* scores_out /* [N] or NULL */, void* stream);
@@ -140,6 +145,10 @@ typedef struct skyrl_ppo_params {
 #define SKYRL_M_COUNT 8
 
 size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R);
+/* flags of the loss forwards */
+#define SKYRL_LOSS_DEFER_FOLD 1 /* leave the loss/metric fold to skyrl_ppo_loss_finish: the
+                                   forward writes gradients and per-block records only, and
+                                   loss_out/metrics_out are written by the finish launch */
 /* ONE launch (two when row_mask_sum is NULL, plus one when a token_mean total over
  * n > 1024 rows is needed): writes the scalar loss, the metric vector and the FINAL
  * gradients for a unit upstream gradient:
@@ -156,7 +165,7 @@ int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const
                        int32_t n, int32_t R, const skyrl_ppo_params* params,
                        float* loss_out /* [1] */, float* metrics_out /* [SKYRL_M_COUNT] */,
                        float* grad_logp /* [n,R] */, float* grad_entropy /* [n,R] or NULL */,
-                       void* workspace, void* stream);
+                       int32_t flags, void* workspace, void* stream);
 /* a4 + a7 for a batch that is one micro-batch: skyrl_grpo_advantage (contiguous groups of
  * G = n/num_groups rows; its contiguous-form conditions apply: G <= 16, R % 4 == 0, 16-B
  * aligned rewards/mask/advantages) followed by skyrl_ppo_loss_fwd on its advantages. ONE
@@ -165,8 +174,14 @@ int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const
  * (adv*response_mask, f32 [n,R]), loss, metrics, grad_logp, grad_entropy. Replaces
  * compute_grpo_outcome_advantage (ppo_utils.py:1132-1182) + the loss of
  * PolicyWorkerBase._forward_backward_micro (workers/worker.py:810-876) when the mini-batch is
- * the whole batch. workspace: skyrl_ppo_loss_workspace_bytes(n, R), zeroed once.           */
-int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* response_mask, int mask_dtype,
+ * the whole batch. scores (f32 [n], pack's reward_row_sum, or NULL) replaces the reward-row
+ * reads of the group statistics (rewards may then be NULL). advantages may be NULL on the
+ * one-launch layout (not written); response_mask may then be NULL too, and every token of a
+ * row uses the row's advantage, which gives the same loss and gradients whenever loss_mask is
+ * 0 outside the response (the pack layout). workspace:
+ * skyrl_ppo_loss_workspace_bytes(n, R), zeroed once.                                      */
+int skyrl_grpo_ppo_loss_fwd(const float* rewards, const float* scores /* [n] or NULL */,
+                            const void* response_mask, int mask_dtype,
                             int32_t num_groups, float epsilon, int32_t norm_by_std,
                             const float* log_probs, const float* old_log_probs,
                             const float* loss_mask /* NULL = all ones */, const float* ref_log_probs,
@@ -174,11 +189,21 @@ int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* response_mask, int
                             int32_t n, int32_t R, const skyrl_ppo_params* params,
                             float* advantages /* [n,R] */, float* loss_out /* [1] */,
                             float* metrics_out /* [SKYRL_M_COUNT] */, float* grad_logp /* [n,R] */,
-                            float* grad_entropy /* [n,R] or NULL */, void* workspace, void* stream);
+                            float* grad_entropy /* [n,R] or NULL */, int32_t flags, void* workspace,
+                            void* stream);
 /* Autograd backward of the loss: grad_logp (and grad_entropy, if given) *= grad_out[0] in
  * place; no memory is touched when grad_out[0] == 1 (loss.backward()).                    */
 int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, int64_t numel, float* grad_logp,
                        float* grad_entropy /* or NULL */, void* stream);
+/* The backward of a forward run with SKYRL_LOSS_DEFER_FOLD (same workspace, same stream):
+ * folds its per-block records into loss_out and metrics_out (bit-identical to the in-launch
+ * fold; stream-ordered, no polling) and, when grad_out is given and grad_out[0] != 1,
+ * rescales grad_logp (and grad_entropy) [n,R] in place, as skyrl_ppo_loss_bwd. grad_out
+ * NULL: fold only. n, R and params as given to the forward. The reference reads loss and
+ * metrics after backward (workers/worker.py:876-894).                                      */
+int skyrl_ppo_loss_finish(const float* grad_out /* [1] device or NULL */, float* grad_logp,
+                          float* grad_entropy /* or NULL */, int32_t n, int32_t R, const skyrl_ppo_params* params,
+                          float* loss_out, float* metrics_out, void* workspace, void* stream);
 
 /* ---- a8: clipped value loss ---------------------------------------------
  * Replaces ppo_critic_loss (ppo_utils.py:175-193): 0.5*mean_rows(masked_mean(
@@ -302,10 +327,11 @@ int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* 
  * (inference_engines/vllm/vllm_engine.py:196-218) with sampled-token logprob
  * extraction (vllm_engine.py:139-149) and SamplingParams defaults
  * (config/ppo_base_config.yaml:316-324). Filters on the temperature-scaled
- * logits: top_k (keep >= the k-th largest, ties kept; <= 0 off), min_p
+ * logits: top_k (exactly the k largest, equal values taken in index order, as
+ * skyrl-tx/tx/utils/generator.py:398-420 lax.top_k + first-k mask; <= 0 off), min_p
  * (p >= min_p * p_max), then top_p (skyrl-tx/tx/utils/generator.py:424-449:
  * in descending order keep tokens while the mass strictly before them is
- * < top_p, the top token always, ties in index order; 1.0 off); the top_p
+ * < top_p, the top token always, ties in index order; 1.0 off, 0 keeps one); the top_p
  * masses are fixed-point 2^31 e^((x-max)/T) summed exactly, so decisions are
  * reproducible. temperature==0 => greedy (lowest index wins ties). Otherwise
  * Gumbel-max with a counter-based hash keyed by (seed, seq_ids[i], step,
@@ -327,7 +353,9 @@ size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V);
  * response), attention_mask i64 [Np,P+R], response_mask i64 [Np,R],
  * rewards f32 [Np,R], loss_mask f32 [Np,R], rollout_logprobs f32 [Np,R]
  * (NULL when logprob_vals is NULL), loss_mask_row_sum f32 [Np] (per-row sum of
- * loss_mask, the input of skyrl_ppo_loss_fwd's reduction scales; may be NULL).
+ * loss_mask, the input of skyrl_ppo_loss_fwd's reduction scales; may be NULL),
+ * reward_row_sum f32 [Np] (per-row sum of rewards = the GRPO score of
+ * ppo_utils.py:1156, in skyrl_grpo_advantage's summation order; may be NULL).
  * Np = N + pad.                                                               */
 typedef struct skyrl_pack_inputs {
     const int64_t* prompt_tokens;   const int64_t* prompt_off;
@@ -339,7 +367,8 @@ typedef struct skyrl_pack_inputs {
 int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int32_t pad, int32_t P, int32_t R,
                           int64_t pad_token_id, int64_t* sequences, int64_t* attention_mask,
                           int64_t* response_mask, float* rewards, float* loss_mask,
-                          float* rollout_logprobs, float* loss_mask_row_sum, void* stream);
+                          float* rollout_logprobs, float* loss_mask_row_sum, float* reward_row_sum,
+                          void* stream);
 
 /* ---- a12: gradient scale ------------------------------------------------
  * grads *= scale over a flat fp32 bucket (optim_step's 1/n_micro scaling,

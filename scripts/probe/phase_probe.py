@@ -37,13 +37,13 @@ st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 P = ctypes.c_void_p
 fn = lib.skyrl_ppo_loss_fwd
 fn.restype = ctypes.c_int
-fn.argtypes = [P, P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, P, P]
+fn.argtypes = [P, P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, ctypes.c_int32, P, P]
 
 
 def launch():
     rc = fn(P(lp.data_ptr()), P(old.data_ptr()), P(adv.data_ptr()), P(mask.data_ptr()), P(ref.data_ptr()), None,
             P(rows.data_ptr()), N, R, ctypes.byref(params), P(loss.data_ptr()), P(metrics.data_ptr()),
-            P(glp.data_ptr()), None, P(ws.data_ptr()), st)
+            P(glp.data_ptr()), None, 0, P(ws.data_ptr()), st)
     assert rc == 0
 
 

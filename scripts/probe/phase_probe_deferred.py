@@ -1,5 +1,6 @@
-"""Phase timeline of the GRPO-inside-the-loss launch (skyrl_grpo_ppo_loss_fwd), as
-phase_probe.py does for the loss alone; phase 5 = group scores ready (after the barrier)."""
+"""Phase timeline of the product form of the GRPO-inside-the-loss launch (skyrl_grpo_ppo_loss_fwd
+with the pack scores, SKYRL_LOSS_DEFER_FOLD, no advantages output): phase 5 = after the score
+barrier, 1 = token pass done, 6 = records stored. Measurement only."""
 import ctypes
 import os
 import subprocess
@@ -11,9 +12,11 @@ import torch
 here = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(here))
 sys.path.insert(0, ROOT)
-so = "/tmp/libphase_fused.so"
-subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC",
-                       "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "skyrl_amd", "csrc"),
+VARIANT = sys.argv[1] if len(sys.argv) > 1 else ""  # "", NOSTATS, NOMATH (timing-only probe builds)
+so = f"/tmp/libphase_fused{VARIANT}.so"
+subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC"]
+                      + ([f"-DSKYRL_PROBE_{VARIANT}"] if VARIANT else []) +
+                      ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "skyrl_amd", "csrc"),
                        os.path.join(here, "phase_probe.hip"), os.path.join(ROOT, "skyrl_amd", "csrc", "grpo.hip"), "-o", so])
 lib = ctypes.CDLL(so, mode=ctypes.RTLD_LOCAL)
 from skyrl_amd import _ffi, ppo_utils  # noqa: E402
@@ -35,6 +38,7 @@ loss = torch.empty(1, device=dev)
 metrics = torch.empty(8, device=dev)
 glp = torch.empty(N, R, device=dev)
 rows = mask.sum(-1)
+scores = rew.sum(-1)
 ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", N, R), dtype=torch.uint8, device=dev)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 P = ctypes.c_void_p
@@ -46,10 +50,10 @@ fn.argtypes = [P, P, P, ctypes.c_int, I32, ctypes.c_float, I32, P, P, P, P, P, P
 
 
 def launch():
-    rc = fn(P(rew.data_ptr()), None, P(rmask.data_ptr()), _ffi.I64, N // 8, 1e-6, 1, P(lp.data_ptr()), P(old.data_ptr()),
-            P(mask.data_ptr()), P(ref.data_ptr()), None, P(rows.data_ptr()), N, R, ctypes.byref(params),
-            P(adv.data_ptr()), P(loss.data_ptr()), P(metrics.data_ptr()), P(glp.data_ptr()), None, 0, P(ws.data_ptr()),
-            st)
+    rc = fn(P(rew.data_ptr()), P(scores.data_ptr()), None, _ffi.I64, N // 8, 1e-6, 1, P(lp.data_ptr()),
+            P(old.data_ptr()), P(mask.data_ptr()), P(ref.data_ptr()), None, P(rows.data_ptr()), N, R,
+            ctypes.byref(params), None, P(loss.data_ptr()), P(metrics.data_ptr()), P(glp.data_ptr()), None,
+            _ffi.LOSS_DEFER_FOLD, P(ws.data_ptr()), st)
     assert rc == 0
 
 
@@ -68,8 +72,8 @@ for rep in range(3):
     t = t[: int(np.nonzero(t[:, 0])[0].max()) + 1]
     t0 = t[:, 0].min()
     us = lambda x: (x - t0) / 100.0  # noqa: E731  (s_memrealtime: 100 MHz)
-    f = len(t) - 1  # the folding block (the last of the grid)
-    print(f"rep {rep}: {len(t)} blocks: entries {us(t[:, 0]).min():.2f}..{us(t[:, 0]).max():.2f} us; "
-          f"scores ready (median span) {np.median((t[1:, 5] - t[1:, 0]) / 100):.2f}, last at {us(t[1:, 5]).max():.2f}; "
-          f"token pass done (median span) {np.median((t[1:, 1] - t[1:, 0]) / 100):.2f}, last at {us(t[1:, 1]).max():.2f}; "
-          f"folder: entry {us(t[f, 0]):.2f}, fold start {us(t[f, 2]):.2f}, end {us(t[f, 3]):.2f}")
+    med = lambda k: np.median((t[:, k] - t[:, 0]) / 100)  # noqa: E731
+    print(f"{VARIANT or 'default'} rep {rep}: {len(t)} blocks: entries {us(t[:, 0]).min():.2f}..{us(t[:, 0]).max():.2f} us; "
+          f"median span to barrier {med(5):.2f}, token pass {med(1):.2f}, records {med(6):.2f}; "
+          f"last barrier {us(t[:, 5]).max():.2f}, last token pass {us(t[:, 1]).max():.2f}, "
+          f"last records {us(t[:, 6]).max():.2f}", flush=True)

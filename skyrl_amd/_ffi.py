@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libs
 F32, BF16, I64, I32, U8 = 0, 1, 2, 3, 4
 M_FINAL_LOSS, M_POLICY_LOSS, M_ENTROPY, M_KL, M_CLIP_RATIO, M_MASK_SUM = 0, 1, 2, 3, 4, 5
 M_COUNT = 8
+LOSS_DEFER_FOLD = 1  # SKYRL_LOSS_DEFER_FOLD
 
 
 class SkyrlHipError(RuntimeError):
@@ -90,7 +91,7 @@ SIGNATURES = {
     "skyrl_last_error": (ctypes.c_char_p, []),
     "skyrl_abi_version": (_INT, []),
     "skyrl_tune": (_INT, [ctypes.c_char_p, _INT]),
-    "skyrl_grpo_advantage": (_INT, [_P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
+    "skyrl_grpo_advantage": (_INT, [_P, _P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
     "skyrl_gae_workspace_bytes": (_SZ, [_I32]),
     "skyrl_gae_advantage_return": (_INT, [_P, _P, _P, _INT, _I32, _I32, _F, _F, _P, _P, _P, _P, _P]),
     "skyrl_approx_kl": (_INT, [_P, _P, _P, _INT, _I64, _I32, _P, _P]),
@@ -99,14 +100,15 @@ SIGNATURES = {
     "skyrl_ppo_loss_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_ppo_loss_fwd": (
         _INT,
-        [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P, _P, _P],
+        [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P, _I32, _P, _P],
     ),
     "skyrl_grpo_ppo_loss_fwd": (
         _INT,
-        [_P, _P, _INT, _I32, _F, _I32, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams),
-         _P, _P, _P, _P, _P, _P, _P],
+        [_P, _P, _P, _INT, _I32, _F, _I32, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams),
+         _P, _P, _P, _P, _P, _I32, _P, _P],
     ),
     "skyrl_ppo_loss_bwd": (_INT, [_P, _I64, _P, _P, _P]),
+    "skyrl_ppo_loss_finish": (_INT, [_P, _P, _P, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P]),
     "skyrl_critic_loss_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_critic_loss_fwd": (_INT, [_P, _P, _P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),
     "skyrl_logprob_fwd": (_INT, [_P, _INT, _I64, _I64, _I32, _I32, _I32, _P, _I64, _I64, _F, _P, _P, _P, _P]),
@@ -136,7 +138,7 @@ SIGNATURES = {
     "skyrl_sample": (_INT, [_P, _INT, _I64, _I32, _I32, _F, _I32, _F, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),
     "skyrl_pack_experience": (
         _INT,
-        [ctypes.POINTER(PackInputs), _I32, _I32, _I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+        [ctypes.POINTER(PackInputs), _I32, _I32, _I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "skyrl_scale_and_sumsq": (_INT, [_P, _I64, _F, _P, _P]),
     "skyrl_scale_by_device_scalar": (_INT, [_P, _P, _P, _I64, _P]),

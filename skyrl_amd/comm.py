@@ -577,6 +577,166 @@ class BucketedGradAllReduce:
 
 
 
+class ShardedModuleOptimizer:
+    """The HIP a12/a14 path for a module's parameters (the HF learner of GRPOTrainer): the
+    reference's FSDP2 reduce-scatter + clip + AdamW (fsdp_strategy.py:155-191, 216-271) with
+    the grad scale of optim_step (workers/worker.py:902-924), and the bf16 copy the rollout
+    engine loads (broadcast_to_inference_engines, fsdp_worker.py:201-228).
+
+    Every trainable parameter becomes a view into flat buffers laid out in reverse parameter
+    order (the order the backward produces gradients) and cut into FlatLayout buckets:
+      * ``.grad``  -> GradReducer.grad (fp32); the backward accumulates into it in place;
+      * ``.data``  -> the fp32 master (world 1: ShardedAdamW.param itself; world > 1 a full copy
+                      re-assembled from the updated shards by an fp32 all-gather per bucket);
+      * the engine -> ShardedAdamW.weights_bf16 (written by the update pass at world 1, the bf16
+                      all-gather at world > 1): :meth:`named_bf16` hands out named views, no copy.
+    :meth:`arm` before the last micro-batch's backward: from then on a post-accumulate-grad hook
+    counts each bucket's parameters and fires the bucket's SUM reduce-scatter on the comm stream
+    as soon as it is complete (buckets strictly in index order, the same collective sequence on
+    every rank). :meth:`step` (n_micro) = wait, sharded grad norm + clip + AdamW in one HIP pass
+    (non-finite norm: skipped on device), zero grads, re-assemble. Every parameter is updated
+    every step (a parameter that got no gradient in a step sees a zero gradient: AdamW's weight
+    decay and moment decay still apply, where torch.optim.AdamW would skip a None grad).
+    """
+
+    def __init__(self, module: torch.nn.Module, config: AdamWConfig, group=None,
+                 bucket_bytes: int = DEFAULT_BUCKET_BYTES):
+        named = []
+        seen = set()
+        for n, p in module.named_parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                named.append((n, p))
+        if not named:
+            raise ValueError("no trainable parameters")
+        for n, p in named:
+            if p.dtype != torch.float32:
+                raise TypeError(f"ShardedModuleOptimizer keeps an fp32 master; {n} is {p.dtype}")
+        self.named = list(reversed(named))  # backward order
+        dev = self.named[0][1].device
+        numel = sum(p.numel() for _, p in self.named)
+        self.reducer = GradReducer(numel, dev, group=group, bucket_bytes=bucket_bytes)
+        lay = self.reducer.layout
+        self.world, self.rank = self.reducer.world, self.reducer.rank
+        self.offsets = []
+        off = 0
+        init = torch.empty(numel, dtype=torch.float32, device=dev)
+        for _, p in self.named:
+            self.offsets.append(off)
+            init[off:off + p.numel()] = p.detach().reshape(-1)
+            off += p.numel()
+        self.opt = ShardedAdamW(self.reducer, init, config, shadow_bf16=True)
+        del init
+        if self.world == 1:
+            self.full = self.opt.param
+        else:
+            self.full = torch.zeros(lay.padded, dtype=torch.float32, device=dev)
+            self._gather_full(sync=True)
+        self._bucket_count = [0] * len(lay.buckets)  # parameters overlapping each bucket
+        self._param_buckets: List[Tuple[int, int]] = []  # first / last bucket of each parameter
+        for (_, p), o in zip(self.named, self.offsets):
+            p.data = self.full[o:o + p.numel()].view_as(p)
+            p.grad = self.reducer.grad[o:o + p.numel()].view_as(p)
+            b0, b1 = self._bucket_at(o), self._bucket_at(o + p.numel() - 1)
+            self._param_buckets.append((b0, b1))
+            for b in range(b0, b1 + 1):
+                self._bucket_count[b] += 1
+        self._index = {id(p): i for i, (_, p) in enumerate(self.named)}
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p in self.named]
+        self._armed = False
+        self.launched_during_backward = 0
+
+    def _bucket_at(self, x: int) -> int:
+        for b, (s, e) in enumerate(self.reducer.layout.buckets):
+            if s <= x < e:
+                return b
+        raise IndexError(x)
+
+    # ---------------------------------------------------------------- gradient exchange
+    def arm(self) -> None:
+        """Call before the backward of the mini-batch's last micro-batch."""
+        if self.world == 1:
+            return
+        self._armed = True
+        self._pending = list(self._bucket_count)
+        self._fired = [False] * len(self.named)
+        self._ready = [n == 0 for n in self._pending]
+        self._next = 0
+        self.launched_during_backward = 0
+        self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self._ready) and self._ready[self._next]:
+            self.reducer.launch([self._next])
+            self._next += 1
+            self.launched_during_backward += 1
+
+    def _on_grad(self, p) -> None:
+        if not self._armed:
+            return
+        i = self._index[id(p)]
+        if self._fired[i]:
+            return
+        self._fired[i] = True
+        b0, b1 = self._param_buckets[i]
+        for b in range(b0, b1 + 1):
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._ready[b] = True
+        self._launch_ready()
+
+    def _finish_exchange(self) -> None:
+        if self.world == 1 or not self._armed:
+            return
+        while self._next < len(self._ready):  # buckets whose parameters got no gradient
+            self.reducer.launch([self._next])
+            self._next += 1
+        self._armed = False
+
+    # ---------------------------------------------------------------- step
+    def step(self, n_micro: int = 1, lr: Optional[float] = None) -> torch.Tensor:
+        """optim_step: grads * 1/n_micro (and 1/world), clip, AdamW, zero grads; then the updated
+        master is re-assembled on every rank and the bf16 engine copy is all-gathered. Returns
+        the pre-clip grad norm (device scalar)."""
+        self._finish_exchange()
+        self._check_grad_views()  # the .grad views must still be the buckets' storage
+        gn = self.opt.step(n_micro=n_micro, lr=lr, zero_grad=True)
+        if self.world > 1:
+            self._gather_full(sync=False)
+            self.opt.sync_weights()
+            self.opt.wait_weights()  # the next forward (and the engine) read them
+        return gn
+
+    def _check_grad_views(self) -> None:
+        base = self.reducer.grad.data_ptr()
+        for (n, p), o in zip(self.named, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != base + 4 * o:
+                raise RuntimeError(f"{n}.grad is no longer a view of the flat gradient buffer "
+                                   "(set_to_none / reassigned); the exchange would miss it")
+
+    def _gather_full(self, sync: bool) -> None:
+        r = self.reducer
+        lay = r.layout
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.full.device))
+        r.stream.wait_event(ready)
+        with torch.cuda.stream(r.stream):
+            for b, (s, e) in enumerate(lay.buckets):
+                po = lay.piece_off[b]
+                nb = (e - s) // r.world
+                dist.all_gather_into_tensor(self.full[s:e], self.opt.param[po:po + nb], group=r.group)
+        if sync:
+            torch.cuda.current_stream(self.full.device).wait_stream(r.stream)
+
+    # ---------------------------------------------------------------- weight sync
+    def named_bf16(self) -> List[Tuple[str, torch.Tensor]]:
+        """(HF name, bf16 view) of every parameter in the engine copy: the weight update request
+        of broadcast_to_inference_engines without a per-parameter cast."""
+        w = self.opt.weights_bf16
+        return [(n, w[o:o + p.numel()].view(p.shape)) for (n, p), o in zip(reversed(self.named),
+                                                                          reversed(self.offsets))]
+
+
 def allreduce_grads(params: Iterable[torch.Tensor], group=None, bucket_bytes: int = 64 << 20) -> int:
     """Mean of `.grad` over the DP group for parameters that are not views of a flat buffer
     (a HF module under the GRPOTrainer): grads are packed into ~bucket_bytes fp32 buckets, one

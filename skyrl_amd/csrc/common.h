@@ -55,6 +55,45 @@ __device__ __forceinline__ float load_mask(const void* m, int dtype, int64_t i) 
     }
 }
 
+// Four consecutive mask values loaded raw and converted later, so the load stays in flight past
+// the code between (a float conversion right after the load makes the compiler wait for it,
+// and with it for every load issued before).
+struct Mask4Raw {
+    uint4 a, b;
+};
+template <int MDT>
+__device__ __forceinline__ Mask4Raw load_mask4_raw(const void* m, int64_t idx) {
+    Mask4Raw r;
+    r.b = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (MDT == SKYRL_I64) {
+        const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const int64_t*>(m) + idx);
+        r.a = p[0];
+        r.b = p[1];
+    } else if constexpr (MDT == SKYRL_U8) {
+        r.a = make_uint4(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(m) + idx), 0u, 0u, 0u);
+    } else {
+        r.a = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(m) + idx);
+    }
+    return r;
+}
+template <int MDT>
+__device__ __forceinline__ void mask4_to_float(const Mask4Raw& r, float (&o)[4]) {
+    if constexpr (MDT == SKYRL_I64) {
+        o[0] = (float)(int64_t)(((uint64_t)r.a.y << 32) | r.a.x);
+        o[1] = (float)(int64_t)(((uint64_t)r.a.w << 32) | r.a.z);
+        o[2] = (float)(int64_t)(((uint64_t)r.b.y << 32) | r.b.x);
+        o[3] = (float)(int64_t)(((uint64_t)r.b.w << 32) | r.b.z);
+    } else if constexpr (MDT == SKYRL_F32) {
+        o[0] = __uint_as_float(r.a.x); o[1] = __uint_as_float(r.a.y);
+        o[2] = __uint_as_float(r.a.z); o[3] = __uint_as_float(r.a.w);
+    } else if constexpr (MDT == SKYRL_I32) {
+        o[0] = (float)(int)r.a.x; o[1] = (float)(int)r.a.y; o[2] = (float)(int)r.a.z; o[3] = (float)(int)r.a.w;
+    } else {
+        o[0] = (float)(r.a.x & 0xffu); o[1] = (float)((r.a.x >> 8) & 0xffu);
+        o[2] = (float)((r.a.x >> 16) & 0xffu); o[3] = (float)(r.a.x >> 24);
+    }
+}
+
 // ---- wave / block reductions ------------------------------------------------
 // Four consecutive mask values from a 16-B-aligned (f32/i64/i32) or 4-B-aligned (u8) address.
 __device__ __forceinline__ void load_mask4(const void* m, int dtype, int64_t idx, float (&o)[4]) {

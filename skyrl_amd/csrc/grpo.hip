@@ -38,7 +38,7 @@ __device__ float row_sum_wave(const float* __restrict__ row, int R, bool vec4) {
 }
 
 __global__ __launch_bounds__(kThreads) void grpo_adv_kernel(
-    const float* __restrict__ rewards, const void* __restrict__ mask, int mask_dtype,
+    const float* __restrict__ rewards, const float* __restrict__ scores_in, const void* __restrict__ mask, int mask_dtype,
     const int32_t* __restrict__ group_off, const int32_t* __restrict__ group_rows, int R,
     float epsilon, int norm_by_std, bool vec4, float* __restrict__ out, float* __restrict__ scores_out) {
     __shared__ float s_scores[kMaxCachedRows];
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void grpo_adv_kernel(
     // Phase 1: row sums (score = token_level_rewards.sum(-1), ppo_utils.py:1156).
     for (int j = w; j < n && j < kMaxCachedRows; j += kWaves) {
         const int row = group_rows[beg + j];
-        float s = row_sum_wave(rewards + (int64_t)row * R, R, vec4);
+        float s = scores_in ? scores_in[row] : row_sum_wave(rewards + (int64_t)row * R, R, vec4);
         if (lane == 0) {
             s_scores[j] = s;
             if (scores_out && slice == 0) scores_out[row] = s;
@@ -67,6 +67,7 @@ __global__ __launch_bounds__(kThreads) void grpo_adv_kernel(
         auto score_of = [&](int j) -> float {
             if (j < kMaxCachedRows) return s_scores[j];
             const int row = group_rows[beg + j];
+            if (scores_in) return scores_in[row];
             const float* r = rewards + (int64_t)row * R;
             float acc = 0.f;
             for (int i = 0; i < R; ++i) acc += r[i];
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kThreads) void grpo_adv_kernel(
         if (j < kMaxCachedRows) {
             score = s_scores[j];
         } else {
-            score = row_sum_wave(rewards + (int64_t)row * R, R, vec4);
+            score = scores_in ? scores_in[row] : row_sum_wave(rewards + (int64_t)row * R, R, vec4);
         }
         const float a = norm_by_std ? (score - mean) / denom : (score - mean);
         const int64_t base = (int64_t)row * R;
@@ -135,8 +136,8 @@ constexpr int kFastUnroll = 4;  // 16-B vectors per lane issued together
 
 template <int MDT>
 __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_contig_kernel(
-    const float* __restrict__ rewards, const void* __restrict__ mask, int G, int R, float epsilon, int norm_by_std,
-    float* __restrict__ out, float* __restrict__ scores_out) {
+    const float* __restrict__ rewards, const float* __restrict__ scores_in, const void* __restrict__ mask, int G, int R,
+    float epsilon, int norm_by_std, float* __restrict__ out, float* __restrict__ scores_out) {
     __shared__ float s_scores[kMaxFastG];
     const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;  // row within the group
@@ -146,23 +147,32 @@ __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_contig_kernel(
     float acc = 0.f;
     float m[kFastUnroll][4];
     int i0 = lane;
-    // first kFastUnroll vectors of rewards and mask in flight together (R = 1024: the whole row)
-    {
-        float4 v[kFastUnroll];
+    if (scores_in) {  // given scores: only the mask is read
+        acc = scores_in[row];
 #pragma unroll
         for (int u = 0; u < kFastUnroll; ++u) {
             const int i = i0 + u * kWave;
-            v[u] = i < n4 ? reinterpret_cast<const float4*>(rrow)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
             if (i < n4) load_mask4(mask, MDT, row * R + 4 * i, m[u]);
         }
+    } else {
+        // first kFastUnroll vectors of rewards and mask in flight together (R = 1024: the whole row)
+        {
+            float4 v[kFastUnroll];
 #pragma unroll
-        for (int u = 0; u < kFastUnroll; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+            for (int u = 0; u < kFastUnroll; ++u) {
+                const int i = i0 + u * kWave;
+                v[u] = i < n4 ? reinterpret_cast<const float4*>(rrow)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (i < n4) load_mask4(mask, MDT, row * R + 4 * i, m[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < kFastUnroll; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+        }
+        for (int i = i0 + kFastUnroll * kWave; i < n4; i += kWave) {  // longer rows (same per-lane order)
+            const float4 v = reinterpret_cast<const float4*>(rrow)[i];
+            acc += (v.x + v.y) + (v.z + v.w);
+        }
+        acc = wave_sum(acc);
     }
-    for (int i = i0 + kFastUnroll * kWave; i < n4; i += kWave) {  // longer rows (same per-lane order)
-        const float4 v = reinterpret_cast<const float4*>(rrow)[i];
-        acc += (v.x + v.y) + (v.z + v.w);
-    }
-    acc = wave_sum(acc);
     if (lane == 0) {
         s_scores[w] = acc;
         if (scores_out) scores_out[row] = acc;
@@ -210,8 +220,9 @@ __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_contig_kernel(
 // mask/advantage bytes as in the one-block-per-group form.
 template <int MDT, int S>
 __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_sliced_kernel(
-    const float* __restrict__ rewards, const void* __restrict__ mask, int num_groups, int G, int R, float epsilon,
-    int norm_by_std, float* __restrict__ out, float* __restrict__ scores_out) {
+    const float* __restrict__ rewards, const float* __restrict__ scores_in, const void* __restrict__ mask,
+    int num_groups, int G, int R, float epsilon, int norm_by_std, float* __restrict__ out,
+    float* __restrict__ scores_out) {
     __shared__ float s_scores[kMaxFastG];
     const int b = blockIdx.x;
     const int xcd = b & 7;
@@ -232,21 +243,25 @@ __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_sliced_kernel(
     float m[4] = {0.f, 0.f, 0.f, 0.f};
     if (vi < s1) load_mask4(mask, MDT, row * R + 4 * vi, m);
     float acc = 0.f;
-    {
-        float4 v[kFastUnroll];
+    if (scores_in) {
+        acc = scores_in[row];
+    } else {
+        {
+            float4 v[kFastUnroll];
 #pragma unroll
-        for (int u = 0; u < kFastUnroll; ++u) {
-            const int i = lane + u * kWave;
-            v[u] = i < n4 ? reinterpret_cast<const float4*>(rrow)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int u = 0; u < kFastUnroll; ++u) {
+                const int i = lane + u * kWave;
+                v[u] = i < n4 ? reinterpret_cast<const float4*>(rrow)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < kFastUnroll; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
         }
-#pragma unroll
-        for (int u = 0; u < kFastUnroll; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+        for (int i = lane + kFastUnroll * kWave; i < n4; i += kWave) {
+            const float4 v = reinterpret_cast<const float4*>(rrow)[i];
+            acc += (v.x + v.y) + (v.z + v.w);
+        }
+        acc = wave_sum(acc);
     }
-    for (int i = lane + kFastUnroll * kWave; i < n4; i += kWave) {
-        const float4 v = reinterpret_cast<const float4*>(rrow)[i];
-        acc += (v.x + v.y) + (v.z + v.w);
-    }
-    acc = wave_sum(acc);
     if (lane == 0) {
         s_scores[w] = acc;
         if (scores_out && slice == 0) scores_out[row] = acc;
@@ -285,7 +300,8 @@ int g_grpo_slices = 4;  // skyrl_tune("grpo_slices", 1/2/4): column slices per g
 
 }  // namespace skyrl
 
-extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_mask, int mask_dtype,
+extern "C" int skyrl_grpo_advantage(const float* rewards, const float* scores_in, const void* response_mask,
+                                    int mask_dtype,
                                     const int32_t* group_off, const int32_t* group_rows,
                                     int32_t num_groups, int32_t N, int32_t R, float epsilon,
                                     int32_t norm_by_std, float* advantages, float* scores_out,
@@ -293,11 +309,11 @@ extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_m
     using namespace skyrl;
     SKYRL_REQUIRE(N >= 0 && R >= 0 && num_groups >= 0, "grpo: negative size");
     if (N == 0 || R == 0 || num_groups == 0) return SKYRL_OK;
-    SKYRL_REQUIRE(rewards && response_mask && advantages, "grpo: null pointer");
+    SKYRL_REQUIRE((rewards || scores_in) && response_mask && advantages, "grpo: null pointer");
     SKYRL_REQUIRE(mask_dtype == SKYRL_F32 || mask_dtype == SKYRL_I64 || mask_dtype == SKYRL_I32 ||
                       mask_dtype == SKYRL_U8,
                   "grpo: unsupported mask dtype");
-    const bool vec4 = (R % 4) == 0 && (reinterpret_cast<uintptr_t>(rewards) % 16) == 0 &&
+    const bool vec4 = (R % 4) == 0 && (reinterpret_cast<uintptr_t>(rewards) % 16) == 0 &&  // (NULL is aligned)
                       (reinterpret_cast<uintptr_t>(advantages) % 16) == 0 &&
                       (reinterpret_cast<uintptr_t>(response_mask) % 16) == 0;
     dim3 grid(num_groups, (R + kSlice - 1) / kSlice);
@@ -312,8 +328,8 @@ extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_m
                      : mask_dtype == SKYRL_I32 ? pick(grpo_adv_sliced_kernel<SKYRL_I32, 2>, grpo_adv_sliced_kernel<SKYRL_I32, 4>)
                                                : pick(grpo_adv_sliced_kernel<SKYRL_U8, 2>, grpo_adv_sliced_kernel<SKYRL_U8, 4>);
             const int ngp = (num_groups + 7) / 8 * 8;
-            hipLaunchKernelGGL(k, dim3(ngp * S), dim3(G * kWave), 0, as_stream(stream), rewards, response_mask,
-                               num_groups, G, R, epsilon, norm_by_std, advantages, scores_out);
+            hipLaunchKernelGGL(k, dim3(ngp * S), dim3(G * kWave), 0, as_stream(stream), rewards, scores_in,
+                               response_mask, num_groups, G, R, epsilon, norm_by_std, advantages, scores_out);
             return check_launch("grpo_adv_sliced_kernel");
         }
         if (vec4 && G <= kMaxFastG) {
@@ -321,15 +337,15 @@ extern "C" int skyrl_grpo_advantage(const float* rewards, const void* response_m
                      : mask_dtype == SKYRL_F32 ? grpo_adv_contig_kernel<SKYRL_F32>
                      : mask_dtype == SKYRL_I32 ? grpo_adv_contig_kernel<SKYRL_I32>
                                                : grpo_adv_contig_kernel<SKYRL_U8>;
-            hipLaunchKernelGGL(k, dim3(num_groups), dim3(G * kWave), 0, as_stream(stream), rewards, response_mask, G,
-                               R, epsilon, norm_by_std, advantages, scores_out);
+            hipLaunchKernelGGL(k, dim3(num_groups), dim3(G * kWave), 0, as_stream(stream), rewards, scores_in,
+                               response_mask, G, R, epsilon, norm_by_std, advantages, scores_out);
             return check_launch("grpo_adv_contig_kernel");
         }
         return fail(SKYRL_ERR_INVALID, "grpo: contiguous form needs R % 4 == 0, 16-B alignment and G <= 16; "
                                        "pass CSR groups otherwise");
     }
     SKYRL_REQUIRE(group_off && group_rows, "grpo: group_off and group_rows are both given or both NULL");
-    hipLaunchKernelGGL(grpo_adv_kernel, grid, dim3(kThreads), 0, as_stream(stream), rewards,
+    hipLaunchKernelGGL(grpo_adv_kernel, grid, dim3(kThreads), 0, as_stream(stream), rewards, scores_in,
                        response_mask, mask_dtype, group_off, group_rows, R, epsilon, norm_by_std, vec4,
                        advantages, scores_out);
     return check_launch("grpo_adv_kernel");

@@ -217,6 +217,7 @@ extern int g_grpo_slices;
 extern int g_loss_units;
 extern int g_loss_bwd_blocks;
 extern int g_grpo_loss_rpb;
+extern int g_finish_mode;
 extern int g_sampler_row;
 extern int g_attn_pf;
 int lmhead_tune(int value);
@@ -261,6 +262,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "loss_bwd_blocks") {
         SKYRL_REQUIRE(value >= 1 && value <= 4096, "skyrl_tune: loss_bwd_blocks must be in [1, 4096]");
         g_loss_bwd_blocks = value;
+        return SKYRL_OK;
+    }
+    if (k == "finish_mode") {
+        SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: finish_mode must be 0, 1 or 2");
+        g_finish_mode = value;
         return SKYRL_OK;
     }
     if (k == "lmhead_pipe") return lmhead_tune(value);

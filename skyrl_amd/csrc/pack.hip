@@ -29,7 +29,7 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, in
                                                         int64_t* __restrict__ seq, int64_t* __restrict__ att,
                                                         int64_t* __restrict__ rmask, float* __restrict__ rew,
                                                         float* __restrict__ lmask, float* __restrict__ rlp,
-                                                        float* __restrict__ lm_rowsum) {
+                                                        float* __restrict__ lm_rowsum, float* __restrict__ rw_rowsum) {
     const int i = blockIdx.x;
     const int src = i < N ? i : i - N;
     const bool is_pad = i >= N;
@@ -74,6 +74,23 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(skyrl_pack_inputs in, in
         for (int c = threadIdx.x; c < ml && c < R; c += kThreads) acc[0] += in.loss_mask_vals[m0 + c];
         block_sum<kThreads / kWave, 1>(acc, s_red);
         if (threadIdx.x == 0) lm_rowsum[i] = acc[0];
+    }
+    if (rw_rowsum && blockIdx.y == 0 && threadIdx.x < kWave) {
+        // GRPO score = sum of the padded reward row, summed in grpo.hip's order (row_sum_wave: lane
+        // l adds the 4-element groups l, l + 64, ... as (x0 + x1) + (x2 + x3), then the wave tree),
+        // so skyrl_grpo_advantage / skyrl_grpo_ppo_loss_fwd given these scores produce what they
+        // compute from the padded rewards themselves
+        const int lane = threadIdx.x;
+        const int lim = wl < R ? wl : R;
+        float acc = 0.f;
+        for (int q = lane; 4 * q < lim; q += kWave) {
+            float x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = 4 * q + k < lim ? in.reward_vals[w0 + 4 * q + k] : 0.f;
+            acc += (x[0] + x[1]) + (x[2] + x[3]);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) rw_rowsum[i] = acc;
     }
     if (VEC) {
         if (c0 < S) {
@@ -144,7 +161,8 @@ using namespace skyrl;
 extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int32_t pad, int32_t P, int32_t R,
                                      int64_t pad_token_id, int64_t* sequences, int64_t* attention_mask,
                                      int64_t* response_mask, float* rewards, float* loss_mask,
-                                     float* rollout_logprobs, float* loss_mask_row_sum, void* stream) {
+                                     float* rollout_logprobs, float* loss_mask_row_sum, float* reward_row_sum,
+                                     void* stream) {
     SKYRL_REQUIRE(in, "pack: inputs is null");
     SKYRL_REQUIRE(N > 0 && pad >= 0 && pad <= N && P >= 0 && R >= 0, "pack: bad sizes");
     SKYRL_REQUIRE(in->prompt_tokens && in->prompt_off && in->response_tokens && in->response_off && in->reward_vals &&
@@ -154,7 +172,7 @@ extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int
     SKYRL_REQUIRE(sequences && attention_mask && response_mask && rewards && loss_mask, "pack: null output pointer");
     const int S = P + R;
     int cols = S > R ? S : R;
-    if (cols == 0 && !loss_mask_row_sum) return SKYRL_OK;
+    if (cols == 0 && !loss_mask_row_sum && !reward_row_sum) return SKYRL_OK;
     if (cols == 0) cols = 1;
     dim3 grid(N + pad, (cols + kCols - 1) / kCols);
     auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -163,11 +181,11 @@ extern "C" int skyrl_pack_experience(const skyrl_pack_inputs* in, int32_t N, int
     if (vec)
         hipLaunchKernelGGL(pack_kernel<true>, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id,
                            sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs,
-                           loss_mask_row_sum);
+                           loss_mask_row_sum, reward_row_sum);
     else
         hipLaunchKernelGGL(pack_kernel<false>, grid, dim3(kThreads), 0, as_stream(stream), *in, N, P, R, pad_token_id,
                            sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs,
-                           loss_mask_row_sum);
+                           loss_mask_row_sum, reward_row_sum);
     return check_launch("pack_kernel");
 }
 

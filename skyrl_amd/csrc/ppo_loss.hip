@@ -15,6 +15,9 @@
 // ref), writes the final dL/dlogp for a unit upstream gradient (4 B/token) and a 5-float
 // record per block, and the last-arriving block folds the records into the scalar loss and
 // the metric vector. The backward rescales in place only when the upstream gradient != 1.
+// Deferred form (SKYRL_LOSS_DEFER_FOLD): the forward only writes the records, and the
+// backward launch (skyrl_ppo_loss_finish) folds them stream-ordered -- no polling -- and
+// rescales; loss and metrics are valid once that launch has run.
 #include "arrive.h"
 
 // Phase timestamps for scripts/probe/phase_probe (compiled only there, never in the product).
@@ -139,6 +142,10 @@ __device__ __forceinline__ unsigned long long load_granule(const unsigned long l
     return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int NW>
+__device__ void fold_finalize(double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p, double* s_redd,
+                              float* __restrict__ loss_out, float* __restrict__ metrics);
+
 // Sum the nb blocks' granules (value-major [kNP][nb]) into the loss and the metric vector;
 // run by the whole folding block. Thread t owns blocks t, t + kThreads, ... (fixed order).
 // NW = waves of the calling block (its threads >= kThreads hold zeros and only join the
@@ -179,6 +186,13 @@ __device__ void fold_granules(const unsigned long long* gran, unsigned epoch, in
                 for (int k = 0; k < kNP; ++k) tot[k] += (double)v[u][k];
     }
     const int any_timeout = __syncthreads_or(timed_out ? 1 : 0);
+    fold_finalize<NW>(tot, any_timeout, n, p, s_redd, loss_out, metrics);
+}
+
+// fp64 per-thread totals -> the loss and the metric vector (block tree, thread 0 writes).
+template <int NW>
+__device__ void fold_finalize(double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p, double* s_redd,
+                              float* __restrict__ loss_out, float* __restrict__ metrics) {
     block_sum_d<NW, kNP>(tot, s_redd);
     if (threadIdx.x == 0) {
         const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
@@ -200,6 +214,100 @@ __device__ void fold_granules(const unsigned long long* gran, unsigned epoch, in
         metrics[6] = any_timeout ? 1.f : 0.f;  // fold timed out
         metrics[7] = 0.f;
     }
+}
+
+// Deferred form: the forward left plain fp32 records (value-major [kNP][nb], nb in the
+// workspace header); the kernel boundary has published them, so block 0 of this launch sums
+// them in the order fold_granules does (thread t: records t, t + kThreads, ... in fp64) and
+// the result is bit-identical to the one-launch fold. The other blocks rescale the gradients
+// when the upstream gradient is not 1 (the autograd backward); at 1 they exit at once.
+// Records are laid out [kNP][units] (units = n * ceil(R / 1024), the most a forward writes) and
+// a forward with nb < units records zeroes the slots [nb, units), so the fold sums every slot:
+// no dependent load of nb before the record loads, and the added zeros leave the fp64 sums
+// bit-identical to summing the nb records.
+__global__ __launch_bounds__(kThreads) void loss_finish_kernel(const float* __restrict__ g,
+                                                               const float* __restrict__ parts,
+                                                               const int* __restrict__ nb_word, int n, int units,
+                                                               skyrl_ppo_params p, float* __restrict__ loss_out,
+                                                               float* __restrict__ metrics, float* __restrict__ glp,
+                                                               float* __restrict__ gent, int64_t numel, int mode) {
+    if (blockIdx.x == 0) {
+        __shared__ double s_redd[kFW * kNP];
+        if (mode == 2) return;  // timing probe only (skyrl_tune "finish_mode" 2): no fold
+        double tot[kNP] = {0, 0, 0, 0, 0};
+        if (mode == 0) {  // two records per thread in flight per pass (512 units: one pass); clamped
+            // indices, no branch around a load (its end would wait for every load before it)
+            for (int b = threadIdx.x; b < units; b += 2 * kThreads) {
+                const int b2 = b + kThreads < units ? b + kThreads : b;
+                float v0[kNP], v1[kNP];
+#pragma unroll
+                for (int k = 0; k < kNP; ++k) {
+                    v0[k] = parts[(int64_t)k * units + b];
+                    v1[k] = parts[(int64_t)k * units + b2];
+                }
+#pragma unroll
+                for (int k = 0; k < kNP; ++k) tot[k] += (double)v0[k];
+                if (b + kThreads < units)
+#pragma unroll
+                    for (int k = 0; k < kNP; ++k) tot[k] += (double)v1[k];
+            }
+        } else {  // nb first, then the records (the variant A/B'd against mode 0)
+            const int nb = *nb_word;
+            for (int b = threadIdx.x; b < nb; b += kThreads)
+#pragma unroll
+                for (int k = 0; k < kNP; ++k) tot[k] += (double)parts[(int64_t)k * units + b];
+        }
+        fold_finalize<kFW>(tot, 0, n, p, s_redd, loss_out, metrics);
+        return;
+    }
+    if (!g) return;
+    const float sc = g[0];
+    if (sc == 1.0f) return;
+    const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
+    for (int64_t i = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < numel; i += stride) {
+        glp[i] *= sc;
+        if (gent) gent[i] *= sc;
+    }
+}
+
+// token_mean total over n <= kInlineTotalRows loss-mask row sums, computed by every wave that
+// needs it, identically in ppo_loss_grad_kernel and grpo_loss_grad_kernel (so the two-call and
+// the one-launch paths scale their gradients by the same bits): lane l adds the 4-row groups l,
+// l + 64, l + 128, l + 192 as (r0 + r1) + (r2 + r3) (rows >= n read as 0), then the wave tree.
+// Four 16-B loads per lane when the row sums are 16-B aligned and n % 4 == 0, else 16 scalar
+// loads; every address is clamped in bounds, so the loads carry no divergent branch.
+struct TotalLoads {
+    float4 v[kInlineTotalRows / (4 * kWave)];
+};
+__device__ __forceinline__ void total_issue(const float* __restrict__ rms, int n, bool vec, TotalLoads& t) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nv = (n + 3) >> 2;
+#pragma unroll
+    for (int u = 0; u < kInlineTotalRows / (4 * kWave); ++u) {
+        const int vi = lane + u * kWave;
+        const int vc = vi < nv ? vi : nv - 1;
+        if (vec) {
+            t.v[u] = reinterpret_cast<const float4*>(rms)[vc];
+        } else {
+            const int r = 4 * vc;
+            t.v[u].x = rms[r < n ? r : n - 1];
+            t.v[u].y = rms[r + 1 < n ? r + 1 : n - 1];
+            t.v[u].z = rms[r + 2 < n ? r + 2 : n - 1];
+            t.v[u].w = rms[r + 3 < n ? r + 3 : n - 1];
+        }
+    }
+}
+__device__ __forceinline__ float total_sum(const TotalLoads& t, int n) {
+    const int lane = threadIdx.x & (kWave - 1);
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < kInlineTotalRows / (4 * kWave); ++u) {
+        const int r = 4 * (lane + u * kWave);
+        const float x = r < n ? t.v[u].x : 0.f, y = r + 1 < n ? t.v[u].y : 0.f;
+        const float z = r + 2 < n ? t.v[u].z : 0.f, w = r + 3 < n ? t.v[u].w : 0.f;
+        acc += (x + y) + (z + w);
+    }
+    return wave_sum(acc);
 }
 
 // Per-row sums of the loss mask (one wave per row), for callers that do not carry them.
@@ -228,27 +336,33 @@ __global__ __launch_bounds__(kThreads) void mask_total_kernel(const float* __res
 // Work unit = one 1024-column chunk of one row; block b takes units [b*U, b*U + U). U = 1 up
 // to 2048 units (512 rows: 8.4 us vs 10.1 at U = 2 and 13.6 at U = 4, measured), U = 4 above
 // (8192 rows: 63 us vs 80 at U = 1: a quarter of the granules to fold).
-template <bool VEC4, int U>
+template <bool VEC4, int U, bool DEFER>
 __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
     const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent,
     const float* __restrict__ row_msum, const float* __restrict__ msum_total, int n, int R, int nchunks,
     skyrl_ppo_params p, float* __restrict__ glp, float* __restrict__ gent, unsigned long long* __restrict__ gran,
-    unsigned* __restrict__ epoch_word, float* __restrict__ loss_out, float* __restrict__ metrics) {
+    unsigned* __restrict__ epoch_word, int* __restrict__ nb_word, float* __restrict__ loss_out,
+    float* __restrict__ metrics) {
     __shared__ float s_red[kFW * kNP];
-    __shared__ double s_redd[kFW * kNP];
+    __shared__ double s_redd[DEFER ? 1 : kFW * kNP];
     __shared__ unsigned s_epoch;
     PHASE(0);
-    if (threadIdx.x == 0) s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (!DEFER && threadIdx.x == 0)
+        s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int units = n * nchunks;
     const int nb = gridDim.x;
     const int wb = blockIdx.x;
     const float lo = (float)(1.0 - (double)p.eps_clip_low);
     const float hi = (float)(1.0 + (double)p.eps_clip_high);
     // issue every 16-B load of all U units first (R % 4 == 0 on the VEC4 path)
+    // Loads are unconditional from addresses valid for every thread (a dead unit reads element 0
+    // and drops it): a load under a divergent branch makes the compiler wait for it, and for
+    // every load before it, at the branch's end, which serialised the round trips.
     float4 l4[U], o4[U], a4[U], m4[U], r4[U], e4[U];
     int row_u[U];
     bool live[U];
+    float mrow_u[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int unit = wb * U + u;
@@ -257,8 +371,8 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
         live[u] = VEC4 && unit < units && c0 + 3 < R;
         l4[u] = o4[u] = a4[u] = r4[u] = e4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         m4[u] = make_float4(1.f, 1.f, 1.f, 1.f);
-        if (live[u]) {
-            const int64_t e = (int64_t)row_u[u] * R + c0;
+        if (VEC4) {
+            const int64_t e = live[u] ? (int64_t)row_u[u] * R + c0 : 0;
             l4[u] = *reinterpret_cast<const float4*>(lp + e);
             o4[u] = *reinterpret_cast<const float4*>(old + e);
             a4[u] = *reinterpret_cast<const float4*>(adv + e);
@@ -266,19 +380,21 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
             if (p.use_kl_loss) r4[u] = *reinterpret_cast<const float4*>(ref + e);
             if (ent) e4[u] = *reinterpret_cast<const float4*>(ent + e);
         }
+        mrow_u[u] = row_msum[row_u[u]];
     }
     // the mask-only scales while the loads are in flight
     const bool need_total = p.loss_reduction == 0 || (p.use_entropy_loss && gent);
     // every wave sums the n row sums itself (same lanes, same order, xor tree: the same value
-    // in every wave of every block), so no barrier stands between the loads and the math
+    // in every wave of every block), so no barrier stands between the loads and the math; the
+    // loads are issued together (a dependent per-iteration loop serialised them)
     float total = 0.f;
     if (need_total) {
         if (msum_total) {
             total = msum_total[0];
-        } else {
-            const int lane = threadIdx.x & (kWave - 1);
-            for (int r = lane; r < n; r += kWave) total += row_msum[r];
-            total = wave_sum(total);
+        } else {  // n <= kInlineTotalRows
+            TotalLoads tl;
+            total_issue(row_msum, n, (n & 3) == 0 && (reinterpret_cast<uintptr_t>(row_msum) & 15) == 0, tl);
+            total = total_sum(tl, n);
         }
     }
     const float tok_scale = 1.f / (total > 1.f ? total : 1.f);  // token_mean
@@ -291,7 +407,7 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
         const int unit = wb * U + u;
         if (unit >= units) break;
         const int row = row_u[u];
-        const double mr = (double)row_msum[row];
+        const double mr = (double)mrow_u[u];
         const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
         float scale, w;  // gradient scale; weight of the row's l*m in the pg sum
         if (p.loss_reduction == 0) { scale = tok_scale; w = 1.f; }
@@ -337,6 +453,15 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
     }
     PHASE(1);
     block_sum<kFW, kNP>(acc, s_red);  // (its barrier also publishes s_epoch)
+    if constexpr (DEFER) {  // plain records, folded by loss_finish_kernel after the kernel boundary
+        float* parts = reinterpret_cast<float*>(gran);  // [kNP][units]: see loss_finish_kernel
+        if (threadIdx.x < kNP) {
+            parts[(int64_t)threadIdx.x * units + wb] = acc[threadIdx.x];
+            for (int z = nb + wb; z < units; z += nb) parts[(int64_t)threadIdx.x * units + z] = 0.f;  // U > 1
+        }
+        if (wb == 0 && threadIdx.x == 0) *nb_word = nb;
+        return;
+    }
     const unsigned epoch = s_epoch;
     if (threadIdx.x < kNP) store_granule(gran + (int64_t)threadIdx.x * nb + wb, epoch, acc[threadIdx.x]);
     if (wb != nb - 1) return;
@@ -362,21 +487,27 @@ constexpr int kGroupMax = 16;
 // RPB row chunks per block (RPB x 256 threads, one chunk per 256-thread half): the group's
 // reward rows are read once per RPB units, each wave sums fewer of them, and every half
 // still publishes its own unit's granules (same fp32 partials, same fold as RPB = 1).
-template <int MDT, int RPB>
+// scores (f32 [n], the per-row reward sums skyrl_pack_experience emits, in grpo.hip's summation
+// order) replace the group's reward-row reads: the block then loads G floats instead of G*R*4 B.
+// DEFER: plain records for loss_finish_kernel instead of the in-launch fold.
+template <int MDT, int RPB, bool DEFER>
 __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
-    const float* __restrict__ rewards, const void* __restrict__ resp_mask, int num_groups, int G, float epsilon,
-    int norm_by_std, int xcd_map, const float* __restrict__ lp, const float* __restrict__ old,
-    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ ent,
-    const float* __restrict__ row_msum, int n, int R, int nchunks, skyrl_ppo_params p, float* __restrict__ adv_out,
-    float* __restrict__ glp, float* __restrict__ gent, unsigned long long* __restrict__ gran,
-    unsigned* __restrict__ epoch_word, float* __restrict__ loss_out, float* __restrict__ metrics) {
+    const float* __restrict__ rewards, const float* __restrict__ scores, const void* __restrict__ resp_mask,
+    int num_groups, int G, float epsilon, int norm_by_std, int xcd_map, const float* __restrict__ lp,
+    const float* __restrict__ old, const float* __restrict__ mask, const float* __restrict__ ref,
+    const float* __restrict__ ent, const float* __restrict__ row_msum, int n, int R, int nchunks, skyrl_ppo_params p,
+    float* __restrict__ adv_out, float* __restrict__ glp, float* __restrict__ gent,
+    unsigned long long* __restrict__ gran, unsigned* __restrict__ epoch_word, int* __restrict__ nb_word,
+    float* __restrict__ loss_out, float* __restrict__ metrics) {
     constexpr int kW = kFW * RPB;  // waves per block
     __shared__ float s_red[kW * kNP];
-    __shared__ double s_redd[kW * kNP];
-    __shared__ float s_scores[kGroupMax];
+    __shared__ double s_redd[DEFER ? 1 : kW * kNP];
+    __shared__ float s_scores[kGroupMax];  // summed from the reward rows
+    __shared__ float s_given[kGroupMax];   // the given scores, written by every wave (see below)
     __shared__ unsigned s_epoch;
     PHASE(0);
-    if (threadIdx.x == 0) s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (!DEFER && threadIdx.x == 0)
+        s_epoch = __hip_atomic_load((gu32*)epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int nb = gridDim.x * RPB;  // granule sets = units
     const int half = threadIdx.x / kThreads;
     const int tid = threadIdx.x % kThreads;
@@ -398,51 +529,96 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
     const int chunk = local % nchunks;
     const int c0 = chunk * kFT + tid * 4;
     const bool live = unit_live && c0 < R;  // R % 4 == 0 on this path
-    const int64_t e = (int64_t)row * R + c0;
+    // Every load below is unconditional, from an address valid for every thread (dead threads
+    // read element 0 and drop it): a load under a divergent branch makes the compiler wait for
+    // it (and for every load before it) at the branch's end, which serialised the round trips.
+    const int64_t e = live ? (int64_t)row * R + c0 : 0;
     float4 l4 = make_float4(0.f, 0.f, 0.f, 0.f), o4 = l4, r4 = l4, e4 = l4, m4 = make_float4(1.f, 1.f, 1.f, 1.f);
-    float rm[4] = {0.f, 0.f, 0.f, 0.f};
-    const float mrow_in = live ? row_msum[row] : 0.f;  // issued with the loads, not after the barrier
+    // response mask NULL (only with adv_out NULL): the row's advantage on every token, exact
+    // wherever the loss mask is nonzero when the loss mask is 0 outside the response (pack's layout)
+    // The same loads on every path (absent inputs read lp instead and are replaced after the
+    // barrier): with a path-dependent number of loads in flight the compiler's wait counts go
+    // conservative and wait for nearly everything at the first use.
+    Mask4Raw rm_raw;
+    const float mrow_in = row_msum[row];  // issued with the loads, not after the barrier
     auto issue_loss_loads = [&]() {
-        if (live) {
-            l4 = *reinterpret_cast<const float4*>(lp + e);
-            o4 = *reinterpret_cast<const float4*>(old + e);
-            if (mask) m4 = *reinterpret_cast<const float4*>(mask + e);
-            if (p.use_kl_loss) r4 = *reinterpret_cast<const float4*>(ref + e);
-            if (ent) e4 = *reinterpret_cast<const float4*>(ent + e);
-            load_mask4(resp_mask, MDT, e, rm);
-        }
+        l4 = *reinterpret_cast<const float4*>(lp + e);
+        o4 = *reinterpret_cast<const float4*>(old + e);
+        m4 = *reinterpret_cast<const float4*>((mask ? mask : lp) + e);
+        r4 = *reinterpret_cast<const float4*>((p.use_kl_loss ? ref : lp) + e);
+        e4 = *reinterpret_cast<const float4*>((ent ? ent : lp) + e);
+        rm_raw = load_mask4_raw<MDT>(resp_mask ? resp_mask : (const void*)lp, resp_mask ? e : 0);  // converted later
     };
     // token_mean total: this lane's row sums (n <= kInlineTotalRows on this path) issued with
     // the other loads, summed after the barrier in ppo_loss_grad_kernel's order
     const bool need_total = p.loss_reduction == 0 || (p.use_entropy_loss && gent);
-    constexpr int kTotPerLane = kInlineTotalRows / kWave;
-    float tv[kTotPerLane];
-    auto issue_total_loads = [&]() {
-#pragma unroll
-        for (int k = 0; k < kTotPerLane; ++k) {
-            const int r = lane + k * kWave;
-            tv[k] = (need_total && r < n) ? row_msum[r] : 0.f;
-        }
-    };
-    // group scores: wave wv sums rows wv, wv + kFW, ... (grpo_adv_contig_kernel's lane order)
+    TotalLoads tl;
+    const bool tot_vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(row_msum) & 15) == 0;
+    auto issue_total_loads = [&]() { total_issue(row_msum, n, tot_vec, tl); };
+    // group scores: wave wv sums rows wv, wv + kFW, ... (grpo_adv_contig_kernel's lane order).
+    // One load sequence for both sources: the score (scores given; from rewards otherwise, where
+    // it is dropped), the total and the loss inputs, then the reward vectors; the reward-first
+    // order of r02 measured the same (11.02 vs 11.07 us).
     const int n4 = R >> 2;
-    if (unit_live && n4 <= 4 * kWave) {
-        // R <= 1024: every reward vector of the wave's (up to 4) rows in flight at once, issued
-        // BEFORE the loss inputs (loads retire in order), so the score reduction and the
-        // barrier overlap the loss inputs' flight
+    const int g0 = unit_live ? group * G : 0;
+    const int si = threadIdx.x & (kGroupMax - 1);
+    const float sc = (scores ? scores : rewards)[g0 + (si < G ? si : G - 1)];
+    issue_total_loads();
+    issue_loss_loads();
+    // group stats (grpo.hip, ppo_utils.py:1164-1175): fp64 mean / unbiased std, fp32 normalisation
+    auto group_adv = [&](auto score_of) -> float {
+        float mean_f, denom_f;
+        if (G <= 1) {
+            mean_f = 0.f;
+            denom_f = norm_by_std ? (1.f + epsilon) : 1.f;
+        } else {
+            double sum = 0.0;
+            for (int j = 0; j < G; ++j) sum += (double)score_of(j);
+            const double mean = sum / (double)G;
+            double m2 = 0.0;
+            for (int j = 0; j < G; ++j) {
+                const double d = (double)score_of(j) - mean;
+                m2 += d * d;
+            }
+            mean_f = (float)mean;
+            const float std_f = (float)sqrt(m2 / (double)(G - 1));
+            denom_f = norm_by_std ? (std_f + epsilon) : 1.f;
+        }
+        const float s = score_of(row - group * G);
+        return norm_by_std ? (s - mean_f) / denom_f : (s - mean_f);
+    };
+    // given scores: every wave writes all 16 slots of s_given (lane l writes slot l & 15; equal
+    // values per slot whichever wave writes), so each wave reads back slots it wrote itself (LDS
+    // operations of one wave complete in order): no block barrier, and the advantage is derived
+    // while the loss inputs are in flight. Every lane executes the write, so the score load is
+    // not sunk into a branch (whose end would wait for every load issued after it).
+    s_given[si] = sc;
+    __builtin_amdgcn_wave_barrier();
+    float adv_row = 0.f;
+    if (scores) {
+#ifdef SKYRL_PROBE_NOSTATS  // scripts/probe/phase_probe_deferred only: timing, wrong advantages
+        const float a = s_given[0];
+#else
+        const float a = group_adv([&](int j) { return s_given[j]; });
+#endif
+        if (unit_live) adv_row = a;
+    }
+    if (!scores && unit_live && n4 <= 4 * kWave) {
+        // R <= 1024: every reward vector of the wave's (up to 4) rows in flight at once (clamped
+        // addresses, dropped after the loads)
         float4 v[kGroupMax / kW][4];
 #pragma unroll
         for (int q = 0; q < kGroupMax / kW; ++q) {
             const int j = wv + q * kW;
-            const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
+            const float4* rrow =
+                reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + (j < G ? j : G - 1)) * R);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int i = lane + u * kWave;
-                v[q][u] = (j < G && i < n4) ? rrow[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[q][u] = rrow[i < n4 ? i : n4 - 1];
+                if (!(j < G && i < n4)) v[q][u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        issue_loss_loads();
-        issue_total_loads();
 #pragma unroll
         for (int q = 0; q < kGroupMax / kW; ++q) {
             const int j = wv + q * kW;
@@ -454,11 +630,8 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
                 if (lane == 0) s_scores[j] = acc;
             }
         }
-    } else {
-        issue_loss_loads();
-        issue_total_loads();
     }
-    if (unit_live && n4 > 4 * kWave) {
+    if (!scores && unit_live && n4 > 4 * kWave) {
         for (int j = wv; j < G; j += kW) {
             const float4* rrow = reinterpret_cast<const float4*>(rewards + (int64_t)(group * G + j) * R);
             float acc = 0.f;
@@ -478,46 +651,23 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
             if (lane == 0) s_scores[j] = acc;
         }
     }
-    __syncthreads();
+    if (!scores) __syncthreads();  // (kernel-uniform)
     PHASE(5);
-    float total = 0.f;
-    if (need_total) {
-#pragma unroll
-        for (int k = 0; k < kTotPerLane; ++k)
-            if (lane + k * kWave < n) total += tv[k];
-        total = wave_sum(total);
-    }
+    const float total = need_total ? total_sum(tl, n) : 0.f;
     const float tok_scale = 1.f / (total > 1.f ? total : 1.f);
     const float escale = need_total ? -(p.entropy_loss_coef / (total > 1.f ? total : 1.f)) : 0.f;
-    // group stats (grpo.hip, ppo_utils.py:1164-1175): fp64 mean / unbiased std, fp32 normalisation
-    float adv_row = 0.f;
-    if (unit_live) {
-        float mean_f, denom_f;
-        if (G <= 1) {
-            mean_f = 0.f;
-            denom_f = norm_by_std ? (1.f + epsilon) : 1.f;
-        } else {
-            double sum = 0.0;
-            for (int j = 0; j < G; ++j) sum += (double)s_scores[j];
-            const double mean = sum / (double)G;
-            double m2 = 0.0;
-            for (int j = 0; j < G; ++j) {
-                const double d = (double)s_scores[j] - mean;
-                m2 += d * d;
-            }
-            mean_f = (float)mean;
-            const float std_f = (float)sqrt(m2 / (double)(G - 1));
-            denom_f = norm_by_std ? (std_f + epsilon) : 1.f;
-        }
-        const float sc = s_scores[row - group * G];
-        adv_row = norm_by_std ? (sc - mean_f) / denom_f : (sc - mean_f);
-    }
+    float rm[4] = {1.f, 1.f, 1.f, 1.f};
+    if (resp_mask) mask4_to_float<MDT>(rm_raw, rm);
+    if (!mask) m4 = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (!p.use_kl_loss) r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!ent) e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!scores && unit_live) adv_row = group_adv([&](int j) { return s_scores[j]; });
     const float4 a4 = make_float4(adv_row * rm[0], adv_row * rm[1], adv_row * rm[2], adv_row * rm[3]);
     const float lo = (float)(1.0 - (double)p.eps_clip_low);
     const float hi = (float)(1.0 + (double)p.eps_clip_high);
     float acc[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
     if (live) {
-        *reinterpret_cast<float4*>(adv_out + e) = a4;
+        if (adv_out) *reinterpret_cast<float4*>(adv_out + e) = a4;
         const double mr = (double)mrow_in;
         const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
         float scale, w;
@@ -526,6 +676,12 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
         else { scale = (float)(1.0 / ((double)n * (double)p.max_seq_len)); w = (float)(1.0 / (double)p.max_seq_len); }
         float a[kNP] = {0.f, 0.f, 0.f, 0.f, 0.f};
         auto tok = [&](float L, float O, float A, float M, float RF, float E) -> float {
+#ifdef SKYRL_PROBE_NOMATH  // scripts/probe/phase_probe_deferred only: timing, wrong values
+            a[0] += L * M;
+            a[1] += M;
+            a[3] += RF * M;
+            return (O + A) * scale;
+#else
             const TokenOut t = ppo_token(L, O, A, lo, hi, p.clip_ratio_c, p.dual_clip);
             a[0] += t.loss * M;
             a[1] += M;
@@ -533,6 +689,7 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
             if (p.use_kl_loss) a[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
             a[4] += E * M;
             return (t.dldlp * M) * scale;
+#endif
         };
         float4 g;
         g.x = tok(l4.x, o4.x, a4.x, m4.x, r4.x, e4.x);
@@ -560,7 +717,13 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
         float sum = 0.f;
 #pragma unroll
         for (int j = 0; j < kFW; ++j) sum += s_red[(half * kFW + j) * kNP + tid];
-        store_granule(gran + (int64_t)tid * nb + wb, epoch, sum);
+        if constexpr (DEFER) reinterpret_cast<float*>(gran)[(int64_t)tid * nb + wb] = sum;  // nb == units here
+        else store_granule(gran + (int64_t)tid * nb + wb, epoch, sum);
+    }
+    if constexpr (DEFER) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *nb_word = nb;
+        PHASE(6);
+        return;
     }
     if (blockIdx.x != gridDim.x - 1) return;
     PHASE(2);
@@ -708,6 +871,7 @@ using namespace skyrl;
 namespace skyrl {
 int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
 int g_loss_bwd_blocks = 256;
+int g_finish_mode = 0;  // skyrl_tune("finish_mode"): 0 record loads issued with the nb load, 1 after it, 2 probe (no fold)
 int g_grpo_loss_rpb = 1;  // skyrl_tune("grpo_loss_rpb", 1 / 2): row chunks per fused GRPO+loss block (2 measured slower: 12.1 vs 11.0 us)
   // skyrl_tune("loss_bwd_blocks"): grid cap of the backward rescale
 }
@@ -721,11 +885,15 @@ extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
     return 256 + ((parts + 255) / 256) * 256 + rows;
 }
 
+// workspace header: [0] epoch word (in-launch fold), [64] token_mean total, [128] record count nb
+// (deferred fold), then the records from byte 256
+static int* nb_word_of(void* workspace) { return reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 128); }
+
 extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const float* advantages,
                                   const float* loss_mask, const float* ref_log_probs, const float* entropy,
                                   const float* row_mask_sum, int32_t n, int32_t R, const skyrl_ppo_params* params,
                                   float* loss_out, float* metrics_out, float* grad_logp, float* grad_entropy,
-                                  void* workspace, void* stream) {
+                                  int32_t flags, void* workspace, void* stream) {
     SKYRL_REQUIRE(params, "ppo_loss_fwd: params is null");
     SKYRL_REQUIRE(n > 0 && R > 0, "ppo_loss_fwd: empty batch");
     SKYRL_REQUIRE(log_probs && old_log_probs && advantages && loss_out && metrics_out && grad_logp && workspace,
@@ -736,6 +904,8 @@ extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_p
                   "ppo_loss_fwd: seq_mean_token_sum_norm needs max_seq_len");
     SKYRL_REQUIRE(params->kl_type >= 0 && params->kl_type <= 3, "ppo_loss_fwd: bad kl_type");
     SKYRL_REQUIRE(!grad_entropy || params->use_entropy_loss, "ppo_loss_fwd: grad_entropy needs use_entropy_loss");
+    SKYRL_REQUIRE((flags & ~SKYRL_LOSS_DEFER_FOLD) == 0, "ppo_loss_fwd: unknown flags");
+    const bool defer = (flags & SKYRL_LOSS_DEFER_FOLD) != 0;
     const int nchunks = (R + kFT - 1) / kFT;
     char* w = reinterpret_cast<char*>(workspace);
     unsigned* epoch_word = reinterpret_cast<unsigned*>(w);
@@ -774,28 +944,32 @@ extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_p
     int U = g_loss_units > 0 ? g_loss_units : (units > 2048 ? 4 : 1);
     if (!vec4) U = 1;
     const int nb = (units + U - 1) / U;
-    auto k = !vec4 ? ppo_loss_grad_kernel<false, 1>
-             : U == 1 ? ppo_loss_grad_kernel<true, 1> : U == 2 ? ppo_loss_grad_kernel<true, 2>
-                                                            : ppo_loss_grad_kernel<true, 4>;
+    auto pick = [&](auto kd, auto kf) { return defer ? kd : kf; };
+    auto k = !vec4    ? pick(ppo_loss_grad_kernel<false, 1, true>, ppo_loss_grad_kernel<false, 1, false>)
+             : U == 1 ? pick(ppo_loss_grad_kernel<true, 1, true>, ppo_loss_grad_kernel<true, 1, false>)
+             : U == 2 ? pick(ppo_loss_grad_kernel<true, 2, true>, ppo_loss_grad_kernel<true, 2, false>)
+                      : pick(ppo_loss_grad_kernel<true, 4, true>, ppo_loss_grad_kernel<true, 4, false>);
     hipLaunchKernelGGL(k, dim3(nb), dim3(kThreads), 0, s, log_probs, old_log_probs, advantages, loss_mask, ref_log_probs,
-                       entropy, rows, tot, n, R, nchunks, *params, grad_logp, grad_entropy, gran, epoch_word, loss_out,
-                       metrics_out);
+                       entropy, rows, tot, n, R, nchunks, *params, grad_logp, grad_entropy, gran, epoch_word,
+                       nb_word_of(workspace), loss_out, metrics_out);
     return check_launch("ppo_loss_grad_kernel");
 }
 
-extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* response_mask, int mask_dtype,
-                                       int32_t num_groups, float epsilon, int32_t norm_by_std, const float* log_probs,
-                                       const float* old_log_probs, const float* loss_mask, const float* ref_log_probs,
-                                       const float* entropy, const float* row_mask_sum, int32_t n, int32_t R,
-                                       const skyrl_ppo_params* params, float* advantages, float* loss_out,
-                                       float* metrics_out, float* grad_logp, float* grad_entropy, void* workspace,
-                                       void* stream) {
+extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const float* scores, const void* response_mask,
+                                       int mask_dtype, int32_t num_groups, float epsilon, int32_t norm_by_std,
+                                       const float* log_probs, const float* old_log_probs, const float* loss_mask,
+                                       const float* ref_log_probs, const float* entropy, const float* row_mask_sum,
+                                       int32_t n, int32_t R, const skyrl_ppo_params* params, float* advantages,
+                                       float* loss_out, float* metrics_out, float* grad_logp, float* grad_entropy,
+                                       int32_t flags, void* workspace, void* stream) {
     SKYRL_REQUIRE(params, "grpo_ppo_loss_fwd: params is null");
     SKYRL_REQUIRE(n > 0 && R > 0 && num_groups > 0, "grpo_ppo_loss_fwd: empty batch");
     SKYRL_REQUIRE(n % num_groups == 0, "grpo_ppo_loss_fwd: contiguous groups need n % num_groups == 0");
-    SKYRL_REQUIRE(rewards && response_mask && advantages && log_probs && old_log_probs && loss_out && metrics_out &&
-                      grad_logp && workspace,
+    SKYRL_REQUIRE((rewards || scores) && (response_mask || !advantages) && log_probs && old_log_probs && loss_out &&
+                      metrics_out && grad_logp && workspace,
                   "grpo_ppo_loss_fwd: null pointer");
+    SKYRL_REQUIRE((flags & ~SKYRL_LOSS_DEFER_FOLD) == 0, "grpo_ppo_loss_fwd: unknown flags");
+    const bool defer = (flags & SKYRL_LOSS_DEFER_FOLD) != 0;
     SKYRL_REQUIRE(mask_dtype == SKYRL_F32 || mask_dtype == SKYRL_I64 || mask_dtype == SKYRL_I32 ||
                       mask_dtype == SKYRL_U8,
                   "grpo_ppo_loss_fwd: unsupported mask dtype");
@@ -804,16 +978,19 @@ extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* respons
     const int units = n * nchunks;
     const bool need_total = params->loss_reduction == 0 || (params->use_entropy_loss && grad_entropy);
     const bool one_launch = row_mask_sum && G <= kGroupMax && (R % 4) == 0 && units <= 2048 &&
-                            !(need_total && n > kInlineTotalRows) && aligned16(rewards) && aligned16(response_mask) &&
+                            !(need_total && n > kInlineTotalRows) && aligned16(rewards) && aligned16(scores) &&
+                            aligned16(response_mask) &&
                             aligned16(log_probs) && aligned16(old_log_probs) && aligned16(loss_mask) &&
                             aligned16(ref_log_probs) && aligned16(entropy) && aligned16(advantages) &&
                             aligned16(grad_logp) && aligned16(grad_entropy);
     if (!one_launch) {  // larger batches (the fold would dominate) or other layouts: the two launches
-        int rc = skyrl_grpo_advantage(rewards, response_mask, mask_dtype, nullptr, nullptr, num_groups, n, R, epsilon,
-                                      norm_by_std, advantages, nullptr, stream);
+        SKYRL_REQUIRE(advantages && response_mask,
+                      "grpo_ppo_loss_fwd: this layout runs two launches and needs advantages and response_mask");
+        int rc = skyrl_grpo_advantage(rewards, scores, response_mask, mask_dtype, nullptr, nullptr, num_groups, n, R,
+                                      epsilon, norm_by_std, advantages, nullptr, stream);
         if (rc) return rc;
         return skyrl_ppo_loss_fwd(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy,
-                                  row_mask_sum, n, R, params, loss_out, metrics_out, grad_logp, grad_entropy,
+                                  row_mask_sum, n, R, params, loss_out, metrics_out, grad_logp, grad_entropy, flags,
                                   workspace, stream);
     }
     SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "grpo_ppo_loss_fwd: use_kl_loss needs ref_log_probs");
@@ -827,16 +1004,38 @@ extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const void* respons
     unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + 256);
     const int xcd_map = (num_groups % 8) == 0 ? 1 : 0;  // grid stays n * nchunks blocks either way
     const int rpb = (g_grpo_loss_rpb == 2 && (G * nchunks) % 2 == 0) ? 2 : 1;
-    auto pick = [&](auto k1, auto k2) { return rpb == 2 ? k2 : k1; };
-    auto k = mask_dtype == SKYRL_I64   ? pick(grpo_loss_grad_kernel<SKYRL_I64, 1>, grpo_loss_grad_kernel<SKYRL_I64, 2>)
-             : mask_dtype == SKYRL_F32 ? pick(grpo_loss_grad_kernel<SKYRL_F32, 1>, grpo_loss_grad_kernel<SKYRL_F32, 2>)
-             : mask_dtype == SKYRL_I32 ? pick(grpo_loss_grad_kernel<SKYRL_I32, 1>, grpo_loss_grad_kernel<SKYRL_I32, 2>)
-                                       : pick(grpo_loss_grad_kernel<SKYRL_U8, 1>, grpo_loss_grad_kernel<SKYRL_U8, 2>);
-    hipLaunchKernelGGL(k, dim3(units / rpb), dim3(kThreads * rpb), 0, as_stream(stream), rewards, response_mask, num_groups, G,
-                       epsilon, norm_by_std, xcd_map, log_probs, old_log_probs, loss_mask, ref_log_probs, entropy,
-                       row_mask_sum, n, R, nchunks, *params, advantages, grad_logp, grad_entropy, gran, epoch_word,
-                       loss_out, metrics_out);
+    using KT = decltype(&grpo_loss_grad_kernel<SKYRL_I64, 1, false>);
+    KT k = nullptr;
+#define SKYRL_GL_PICK(MDT)                                                                              \
+    k = defer ? (rpb == 2 ? grpo_loss_grad_kernel<MDT, 2, true> : grpo_loss_grad_kernel<MDT, 1, true>) \
+              : (rpb == 2 ? grpo_loss_grad_kernel<MDT, 2, false> : grpo_loss_grad_kernel<MDT, 1, false>)
+    if (mask_dtype == SKYRL_I64) SKYRL_GL_PICK(SKYRL_I64);
+    else if (mask_dtype == SKYRL_F32) SKYRL_GL_PICK(SKYRL_F32);
+    else if (mask_dtype == SKYRL_I32) SKYRL_GL_PICK(SKYRL_I32);
+    else SKYRL_GL_PICK(SKYRL_U8);
+#undef SKYRL_GL_PICK
+    hipLaunchKernelGGL(k, dim3(units / rpb), dim3(kThreads * rpb), 0, as_stream(stream), rewards, scores, response_mask,
+                       num_groups, G, epsilon, norm_by_std, xcd_map, log_probs, old_log_probs, loss_mask, ref_log_probs,
+                       entropy, row_mask_sum, n, R, nchunks, *params, advantages, grad_logp, grad_entropy, gran,
+                       epoch_word, nb_word_of(workspace), loss_out, metrics_out);
     return check_launch("grpo_loss_grad_kernel");
+}
+
+extern "C" int skyrl_ppo_loss_finish(const float* grad_out, float* grad_logp, float* grad_entropy, int32_t n,
+                                     int32_t R, const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                                     void* workspace, void* stream) {
+    SKYRL_REQUIRE(params && loss_out && metrics_out && workspace, "ppo_loss_finish: null pointer");
+    SKYRL_REQUIRE(n > 0 && R > 0, "ppo_loss_finish: bad sizes");
+    SKYRL_REQUIRE(!grad_out || grad_logp, "ppo_loss_finish: grad_out needs grad_logp");
+    const int64_t numel = (int64_t)n * R;
+    const int units = n * ((R + kFT - 1) / kFT);
+    int64_t blocks = grad_out ? (numel + kThreads - 1) / kThreads : 0;
+    if (blocks > g_loss_bwd_blocks) blocks = g_loss_bwd_blocks;
+    const float* parts = reinterpret_cast<const float*>(reinterpret_cast<char*>(workspace) + 256);
+    hipLaunchKernelGGL(loss_finish_kernel, dim3((unsigned)(1 + blocks)), dim3(kThreads), 0, as_stream(stream), grad_out,
+                       parts, nb_word_of(workspace), n, units, *params, loss_out, metrics_out, grad_logp, grad_entropy,
+                       numel, g_finish_mode);
+    return check_launch("loss_finish_kernel");
 }
 
 extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, int64_t numel, float* grad_logp, float* grad_entropy,

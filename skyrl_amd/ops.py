@@ -129,8 +129,11 @@ def grpo_advantage(
     epsilon: float = 1e-6,
     norm_by_std: bool = True,
     scores_out: Optional[torch.Tensor] = None,
+    scores: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
-    dev = _require_gpu(token_level_rewards, response_mask)
+    """a4 GRPO advantage. ``scores`` (f32 [N], the per-row reward sums pack_experience returns
+    with ``return_row_sums``) skips the reward reads; the result is the same as computing them."""
+    dev = _require_gpu(token_level_rewards, response_mask, scores)
     rew = _f32c(token_level_rewards, "token_level_rewards")
     if rew.dim() != 2 or response_mask.shape != rew.shape:
         raise ValueError(f"rewards {tuple(rew.shape)} and response_mask {tuple(response_mask.shape)} must match [N,R]")
@@ -148,9 +151,14 @@ def grpo_advantage(
     else:
         goff = group_off.to(device=dev, dtype=torch.int32)
         grows = group_rows.to(device=dev, dtype=torch.int32)
+    sc = None
+    if scores is not None:
+        sc = _f32c(scores.detach(), "scores")
+        if tuple(sc.shape) != (N,):
+            raise ValueError(f"scores shape {tuple(sc.shape)} != {(N,)}")
     out = torch.empty((N, R), dtype=torch.float32, device=dev)
     _ffi.call(
-        "skyrl_grpo_advantage", _ptr(rew), _ptr(mask), _MASK_DTYPES[mask.dtype], _ptr(goff), _ptr(grows),
+        "skyrl_grpo_advantage", _ptr(rew), _ptr(sc), _ptr(mask), _MASK_DTYPES[mask.dtype], _ptr(goff), _ptr(grows),
         int(num_groups), N, R, float(epsilon), int(bool(norm_by_std)), _ptr(out), _ptr(scores_out), _stream(dev),
     )
     return out
@@ -279,6 +287,47 @@ def make_ppo_params(
     )
 
 
+FOLD_TIMEOUT_SLOT = 6  # metrics[6] = 1: an in-launch fold's bounded spin timed out (loss/metrics NaN)
+
+
+def check_loss_metrics(metrics) -> None:
+    """Raise when a loss launch's in-launch fold timed out (metrics[6] != 0): its loss and
+    metrics are NaN while the gradients were written, so training must not go on silently.
+    ``metrics`` is one [8] vector or rows of them, device or host; one host read."""
+    m = torch.as_tensor(metrics)
+    flag = m.reshape(-1, m.shape[-1])[:, FOLD_TIMEOUT_SLOT]
+    if bool((flag != 0).any()):
+        raise RuntimeError("fused PPO loss: the in-launch fold of the per-block records timed out "
+                           "(metrics[6] = 1; loss and metrics are NaN)")
+
+
+def _loss_workspace(dev, n, R, defer):
+    nbytes = _ffi.query("skyrl_ppo_loss_workspace_bytes", n, R)
+    if defer:  # the records live until this call's backward: a workspace of its own (no zeroing needed)
+        return torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    return WORKSPACES.get(dev, "ppo", nbytes)
+
+
+def _loss_backward(ctx, grad_loss):
+    if ctx.used:  # the gradients are rescaled in place
+        raise RuntimeError("the fused PPO loss supports a single backward pass")
+    ctx.used = True
+    glp, gent, loss, metrics = ctx.saved_tensors
+    g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
+    if ctx.defer:  # fold the forward's records into loss/metrics + rescale, one launch
+        _ffi.call("skyrl_ppo_loss_finish", _ptr(g), _ptr(glp), _ptr(gent), glp.shape[0], glp.shape[1],
+                  ctypes.byref(ctx.params), _ptr(loss), _ptr(metrics), _ptr(ctx.ws), _stream(glp.device))
+    else:
+        _ffi.call("skyrl_ppo_loss_bwd", _ptr(g), glp.numel(), _ptr(glp), _ptr(gent), _stream(glp.device))
+    return glp, gent
+
+
+def _loss_finish_now(n, R, params, loss, metrics, ws, dev):
+    """A deferred forward whose backward will not run (no grad): fold now."""
+    _ffi.call("skyrl_ppo_loss_finish", None, None, None, n, R, ctypes.byref(params), _ptr(loss), _ptr(metrics),
+              _ptr(ws), _stream(dev))
+
+
 class PPOLossFunction(torch.autograd.Function):
     """Fused policy loss (+KL(ref) +entropy term): ONE HIP launch computes the loss, the
     metrics and the final dL/dlogp (and dL/dentropy) for a unit upstream gradient; the
@@ -287,11 +336,18 @@ class PPOLossFunction(torch.autograd.Function):
     forward returns (loss 0-d, metrics f32[8] device). Gradients flow to log_probs and,
     when params.use_entropy_loss, to entropy. The KL term has no gradient (reference:
     compute_approx_kl is @torch.no_grad(), ppo_utils.py:87).
+
+    defer_fold: the forward writes gradients and per-block records only, and the backward's
+    single launch (skyrl_ppo_loss_finish) folds them into loss/metrics and rescales: one
+    launch less and no in-launch fold. loss/metrics are then valid after backward (the
+    reference reads them there, workers/worker.py:876-894); when no backward can follow
+    (grad disabled or no differentiable input) the fold runs at once. One backward per call
+    (the gradients are rescaled in place).
     """
 
     @staticmethod
     def forward(ctx, log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params,
-                loss_mask_row_sum):
+                loss_mask_row_sum, defer_fold=False):
         dev = _require_gpu(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy)
         lp = _f32c(log_probs.detach(), "log_probs")
         old = _f32c(old_log_probs.detach(), "old_log_probs")
@@ -315,25 +371,25 @@ class PPOLossFunction(torch.autograd.Function):
         glp = torch.empty_like(lp)
         want_ent = bool(params.use_entropy_loss) and entropy is not None and ctx.needs_input_grad[5]
         gent = torch.empty_like(lp) if want_ent else None
-        ws = WORKSPACES.get(dev, "ppo", _ffi.query("skyrl_ppo_loss_workspace_bytes", n, R))
+        defer = bool(defer_fold)
+        ws = _loss_workspace(dev, n, R, defer)
         _ffi.call(
             "skyrl_ppo_loss_fwd", _ptr(lp), _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), _ptr(ent), _ptr(rows), n, R,
-            ctypes.byref(params), _ptr(loss), _ptr(metrics), _ptr(glp), _ptr(gent), _ptr(ws), _stream(dev),
+            ctypes.byref(params), _ptr(loss), _ptr(metrics), _ptr(glp), _ptr(gent),
+            _ffi.LOSS_DEFER_FOLD if defer else 0, _ptr(ws), _stream(dev),
         )
-        ctx.save_for_backward(glp, gent)
+        if defer and not (ctx.needs_input_grad[0] or ctx.needs_input_grad[5]):
+            _loss_finish_now(n, R, params, loss, metrics, ws, dev)
+            defer = False
+        ctx.save_for_backward(glp, gent, loss, metrics)
         ctx.mark_non_differentiable(metrics)
-        ctx.used = False
+        ctx.used, ctx.defer, ctx.n, ctx.params, ctx.ws = False, defer, n, params, ws
         return loss, metrics
 
     @staticmethod
     def backward(ctx, grad_loss, grad_metrics):
-        if ctx.used:  # the gradients are rescaled in place
-            raise RuntimeError("the fused PPO loss supports a single backward pass")
-        ctx.used = True
-        glp, gent = ctx.saved_tensors
-        g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
-        _ffi.call("skyrl_ppo_loss_bwd", _ptr(g), glp.numel(), _ptr(glp), _ptr(gent), _stream(glp.device))
-        return glp, None, None, None, None, gent, None, None
+        glp, gent = _loss_backward(ctx, grad_loss)
+        return glp, None, None, None, None, gent, None, None, None
 
 
 class GRPOPPOLossFunction(torch.autograd.Function):
@@ -341,13 +397,14 @@ class GRPOPPOLossFunction(torch.autograd.Function):
     micro-batch: ``skyrl_grpo_ppo_loss_fwd``, ONE launch when the layout allows (see the
     header), with outputs bit-identical to ``grpo_advantage`` followed by ``ppo_loss``.
     forward returns (advantages [n,R], loss 0-d, metrics f32[8]); gradients flow to
-    log_probs (and entropy), exactly as ``PPOLossFunction``."""
+    log_probs (and entropy), exactly as ``PPOLossFunction`` (defer_fold included)."""
 
     @staticmethod
     def forward(ctx, token_level_rewards, response_mask, num_groups, epsilon, norm_by_std, log_probs, old_log_probs,
-                loss_mask, ref_log_probs, entropy, params, loss_mask_row_sum):
+                loss_mask, ref_log_probs, entropy, params, loss_mask_row_sum, scores=None, defer_fold=False,
+                want_advantages=True, mask_within_response=False):
         dev = _require_gpu(token_level_rewards, response_mask, log_probs, old_log_probs, loss_mask, ref_log_probs,
-                           entropy)
+                           entropy, scores)
         rew = _f32c(token_level_rewards.detach(), "token_level_rewards")
         rmask = response_mask.detach().contiguous()
         if rmask.dtype not in _MASK_DTYPES:
@@ -365,61 +422,87 @@ class GRPOPPOLossFunction(torch.autograd.Function):
                 raise ValueError(f"{name} shape {tuple(t.shape)} != log_probs shape {tuple(lp.shape)}")
         n, R = lp.shape
         rows = None if loss_mask_row_sum is None else _f32c(loss_mask_row_sum.detach(), "loss_mask_row_sum")
-        adv = torch.empty_like(lp)
+        sc = None
+        if scores is not None:
+            sc = _f32c(scores.detach(), "scores")
+            if tuple(sc.shape) != (n,):
+                raise ValueError(f"scores shape {tuple(sc.shape)} != {(n,)}")
+        want_ent = bool(params.use_entropy_loss) and entropy is not None and ctx.needs_input_grad[9]
+        # the C entry's one-launch conditions (skyrl_grpo_ppo_loss_fwd); the two-launch form needs
+        # the advantages buffer and the response mask
+        need_total = params.loss_reduction == 0 or want_ent
+        one_launch = rows is not None and n * ((R + 1023) // 1024) <= 2048 and not (need_total and n > 1024)
+        want_adv = bool(want_advantages) or not one_launch
+        adv = torch.empty_like(lp) if want_adv else None
+        # without the advantages output the response mask is not read when the caller guarantees
+        # loss_mask == 0 outside the response (pack's layout): then every loss token uses its row's
+        # advantage, exactly what adv * response_mask gives it
+        rm_arg = rmask if (want_adv or not mask_within_response) else None
         loss = torch.empty((), dtype=torch.float32, device=dev)
         metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
         glp = torch.empty_like(lp)
-        want_ent = bool(params.use_entropy_loss) and entropy is not None and ctx.needs_input_grad[9]
         gent = torch.empty_like(lp) if want_ent else None
-        ws = WORKSPACES.get(dev, "ppo", _ffi.query("skyrl_ppo_loss_workspace_bytes", n, R))
+        defer = bool(defer_fold)
+        ws = _loss_workspace(dev, n, R, defer)
         _ffi.call(
-            "skyrl_grpo_ppo_loss_fwd", _ptr(rew), _ptr(rmask), _MASK_DTYPES[rmask.dtype], int(num_groups),
+            "skyrl_grpo_ppo_loss_fwd", _ptr(rew), _ptr(sc), _ptr(rm_arg), _MASK_DTYPES[rmask.dtype], int(num_groups),
             float(epsilon), int(bool(norm_by_std)), _ptr(lp), _ptr(old), _ptr(mask), _ptr(ref), _ptr(ent), _ptr(rows),
-            n, R, ctypes.byref(params), _ptr(adv), _ptr(loss), _ptr(metrics), _ptr(glp), _ptr(gent), _ptr(ws),
-            _stream(dev),
+            n, R, ctypes.byref(params), _ptr(adv), _ptr(loss), _ptr(metrics), _ptr(glp), _ptr(gent),
+            _ffi.LOSS_DEFER_FOLD if defer else 0, _ptr(ws), _stream(dev),
         )
-        ctx.save_for_backward(glp, gent)
-        ctx.mark_non_differentiable(adv, metrics)
-        ctx.used = False
-        return adv, loss, metrics
+        if defer and not (ctx.needs_input_grad[5] or ctx.needs_input_grad[9]):
+            _loss_finish_now(n, R, params, loss, metrics, ws, dev)
+            defer = False
+        ctx.save_for_backward(glp, gent, loss, metrics)
+        if adv is not None:
+            ctx.mark_non_differentiable(adv, metrics)
+        else:
+            ctx.mark_non_differentiable(metrics)
+        ctx.used, ctx.defer, ctx.n, ctx.params, ctx.ws = False, defer, n, params, ws
+        return (adv if want_advantages else None), loss, metrics
 
     @staticmethod
     def backward(ctx, grad_adv, grad_loss, grad_metrics):
-        if ctx.used:
-            raise RuntimeError("the fused PPO loss supports a single backward pass")
-        ctx.used = True
-        glp, gent = ctx.saved_tensors
-        g = grad_loss.detach().to(torch.float32).reshape(1).contiguous()
-        _ffi.call("skyrl_ppo_loss_bwd", _ptr(g), glp.numel(), _ptr(glp), _ptr(gent), _stream(glp.device))
-        return None, None, None, None, None, glp, None, None, None, gent, None, None
+        glp, gent = _loss_backward(ctx, grad_loss)
+        return None, None, None, None, None, glp, None, None, None, gent, None, None, None, None, None, None
 
 
 def grpo_ppo_loss(token_level_rewards, response_mask, num_groups, log_probs, old_log_probs, loss_mask, params,
-                  ref_log_probs=None, entropy=None, loss_mask_row_sum=None, epsilon=1e-6, norm_by_std=True):
+                  ref_log_probs=None, entropy=None, loss_mask_row_sum=None, epsilon=1e-6, norm_by_std=True,
+                  scores=None, defer_fold=False, want_advantages=True, mask_within_response=False):
     """GRPO advantage + fused loss in one call; returns (advantages, loss, metrics). Layouts
     the C entry's contiguous form cannot take (R % 4 != 0, groups > 16 rows, unaligned
-    buffers) run the two HIP calls, with the CSR GRPO kernel."""
+    buffers) run the two HIP calls, with the CSR GRPO kernel. ``scores``: the per-row reward
+    sums (pack_experience(return_row_sums=True)); ``defer_fold``: see PPOLossFunction.
+    ``want_advantages=False`` skips the advantages output (returned as None) on the one-launch
+    layout; with ``mask_within_response`` (the caller guarantees loss_mask is 0 outside the
+    response, as pack's output is) the response mask is not read either."""
     n, R = log_probs.shape
     ng = int(num_groups)
     if ng > 0 and n % ng == 0:
-        tens = (token_level_rewards, response_mask, log_probs, old_log_probs, loss_mask, ref_log_probs, entropy)
+        tens = (token_level_rewards, response_mask, log_probs, old_log_probs, loss_mask, ref_log_probs, entropy,
+                scores)
         contiguous_ok = R % 4 == 0 and n // ng <= 16 and all(
             t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in tens)
         if not contiguous_ok:
-            adv = grpo_advantage(token_level_rewards, response_mask, None, None, ng, epsilon, norm_by_std)
+            adv = grpo_advantage(token_level_rewards, response_mask, None, None, ng, epsilon, norm_by_std,
+                                 scores=scores)
             loss, metrics = ppo_loss(log_probs, old_log_probs, adv, loss_mask, params, ref_log_probs, entropy,
-                                     loss_mask_row_sum)
-            return adv, loss, metrics
+                                     loss_mask_row_sum, defer_fold=defer_fold)
+            return (adv if want_advantages else None), loss, metrics
     return GRPOPPOLossFunction.apply(token_level_rewards, response_mask, num_groups, epsilon, norm_by_std, log_probs,
-                                     old_log_probs, loss_mask, ref_log_probs, entropy, params, loss_mask_row_sum)
+                                     old_log_probs, loss_mask, ref_log_probs, entropy, params, loss_mask_row_sum,
+                                     scores, defer_fold, want_advantages, mask_within_response)
 
 
 def ppo_loss(log_probs, old_log_probs, advantages, loss_mask, params, ref_log_probs=None, entropy=None,
-             loss_mask_row_sum=None):
+             loss_mask_row_sum=None, defer_fold=False):
     """Fused loss; returns (loss 0-d tensor, metrics device tensor [8]). ``loss_mask_row_sum``
-    (f32 [n], per-row sums of ``loss_mask``, as pack_experience emits them) saves one launch."""
+    (f32 [n], per-row sums of ``loss_mask``, as pack_experience emits them) saves one launch.
+    One backward per call. ``defer_fold`` moves the loss/metric fold into the backward launch
+    (loss and metrics valid after backward; see PPOLossFunction)."""
     return PPOLossFunction.apply(log_probs, old_log_probs, advantages, loss_mask, ref_log_probs, entropy, params,
-                                 loss_mask_row_sum)
+                                 loss_mask_row_sum, defer_fold)
 
 
 # ---------------------------------------------------------------------------- a8 critic loss
@@ -708,7 +791,8 @@ def pack_experience(
     *, N: int, P: int, R: int, pad: int = 0, pad_token_id: int = 0, return_row_sums: bool = False,
 ):
     """Device CSR inputs -> (sequences, attention_mask, response_mask, rewards, loss_mask, rollout_logprobs)
-    [+ loss_mask_row_sum f32 [N+pad] when ``return_row_sums``]."""
+    [+ loss_mask_row_sum, reward_row_sum f32 [N+pad] when ``return_row_sums``: the loss's
+    reduction scales and the GRPO scores, see grpo_advantage(scores=) / ppo_loss]."""
     dev = _require_gpu(prompt_tokens, response_tokens, reward_vals, loss_mask_vals)
 
     def i64(t):
@@ -732,12 +816,13 @@ def pack_experience(
     lmask = torch.empty((Np, R), dtype=torch.float32, device=dev)
     rlp = torch.empty((Np, R), dtype=torch.float32, device=dev) if has_lp else None
     rows = torch.empty(Np, dtype=torch.float32, device=dev) if return_row_sums else None
+    wrows = torch.empty(Np, dtype=torch.float32, device=dev) if return_row_sums else None
     _ffi.call(
         "skyrl_pack_experience", ctypes.byref(ins), N, pad, P, R, int(pad_token_id), _ptr(seq), _ptr(att),
-        _ptr(rmask), _ptr(rew), _ptr(lmask), _ptr(rlp), _ptr(rows), _stream(dev),
+        _ptr(rmask), _ptr(rew), _ptr(lmask), _ptr(rlp), _ptr(rows), _ptr(wrows), _stream(dev),
     )
     if return_row_sums:
-        return seq, att, rmask, rew, lmask, rlp, rows
+        return seq, att, rmask, rew, lmask, rlp, rows, wrows
     return seq, att, rmask, rew, lmask, rlp
 
 

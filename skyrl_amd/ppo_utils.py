@@ -302,13 +302,16 @@ def reduce_loss(loss, loss_mask, loss_reduction, max_seq_len=None):
 
 # ----------------------------------------------------------------------------- a4 / a5 estimators
 def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6,
-                                   grpo_norm_by_std: bool = True, **kwargs):
-    """HIP GRPO advantage (ppo_utils.py:1132-1182). Returns (advantages, returns) aliased."""
+                                   grpo_norm_by_std: bool = True, scores=None, **kwargs):
+    """HIP GRPO advantage (ppo_utils.py:1132-1182). Returns (advantages, returns) aliased.
+    ``scores`` (f32 [N], the pack kernel's per-row reward sums, in the kernel's own summation
+    order) skips the reward reads."""
     off, rows, ng = ops.groups_from_index(index)
     R = token_level_rewards.shape[-1]
     if R % 4 == 0 and ops.contiguous_group_size(off, rows, ng):
         off = rows = None  # contiguous equal groups: the index-free kernel
-    adv = ops.grpo_advantage(token_level_rewards, response_mask, off, rows, ng, epsilon, grpo_norm_by_std)
+    adv = ops.grpo_advantage(token_level_rewards, response_mask, off, rows, ng, epsilon, grpo_norm_by_std,
+                             scores=scores)
     return adv, adv
 
 

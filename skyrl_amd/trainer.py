@@ -44,6 +44,10 @@ class TrainerConfig:
     max_grad_norm: float = 1.0
     temperature: float = 1.0
     use_sample_packing: bool = True             # trainer.use_sample_packing (config.py:457): padding-free learner
+    # "hip": comm.ShardedModuleOptimizer (flat fp32 master, reduce-scatter from the backward hooks,
+    # one HIP clip + AdamW pass that also writes the engine's bf16 weights); "torch": torch.optim.AdamW
+    # + clip_grad_norm_ + bucketed all-reduce (the A/B reference)
+    optimizer: str = "hip"
     sampling_params: Dict[str, Any] = field(default_factory=lambda: {"max_tokens": 1024, "min_tokens": 1})
     algorithm: AlgorithmConfig = field(default_factory=AlgorithmConfig)
 
@@ -109,15 +113,23 @@ class GRPOTrainer:
             raise ValueError("use_kl_loss needs a reference model")
         self.loss_params = ppo_utils.ppo_params_from_config(
             alg, use_kl_loss=alg.use_kl_loss, use_entropy_loss=alg.use_entropy_loss, has_entropy=True)
-        self.optimizer = torch.optim.AdamW(policy.parameters(), lr=cfg.lr, betas=tuple(cfg.betas),
-                                           weight_decay=cfg.weight_decay, eps=1e-8)
         if cfg.use_sample_packing:
             for m in (policy, ref, critic.model if critic is not None else None):
                 if m is not None:
                     enable_sample_packing(m)
         world = torch.distributed.get_world_size(dp_group) if (
             torch.distributed.is_available() and torch.distributed.is_initialized()) else 1
-        self.grad_sync = comm.BucketedGradAllReduce(policy.parameters(), dp_group) if world > 1 else None
+        if cfg.optimizer not in ("hip", "torch"):
+            raise ValueError(f"optimizer must be 'hip' or 'torch', got {cfg.optimizer!r}")
+        self.optimizer = self.grad_sync = self.optim = None
+        if cfg.optimizer == "hip":  # optim_step / FSDP2 (worker.py:902-924, fsdp_strategy.py:155-191)
+            self.optim = comm.ShardedModuleOptimizer(
+                policy, comm.AdamWConfig(lr=cfg.lr, betas=tuple(cfg.betas), eps=1e-8, weight_decay=cfg.weight_decay,
+                                         max_grad_norm=cfg.max_grad_norm), group=dp_group)
+        else:
+            self.optimizer = torch.optim.AdamW(policy.parameters(), lr=cfg.lr, betas=tuple(cfg.betas),
+                                               weight_decay=cfg.weight_decay, eps=1e-8)
+            self.grad_sync = comm.BucketedGradAllReduce(policy.parameters(), dp_group) if world > 1 else None
         self.critic_grad_sync = (comm.BucketedGradAllReduce(critic.parameters(), dp_group)
                                  if world > 1 and critic is not None else None)
         self.global_step = 0
@@ -297,8 +309,11 @@ class GRPOTrainer:
     def _train_policy(self, data) -> Dict[str, float]:
         """_execute_training_step: mini-batches of policy_mini_batch_size prompts (no shuffle,
         trainer.py:1067-1081), micro-batches inside, loss scaled by 1/n_micro, grad clip, AdamW."""
+        from . import ops
+
         self.policy.train()  # worker.py:750
         cfg = self.cfg
+        self._grpo_G = self._fused_grpo_group_size(data)
         n = len(data["sequences"])
         mini = cfg.policy_mini_batch_size * cfg.n_samples_per_prompt
         mb = cfg.micro_train_batch_size_per_gpu
@@ -314,34 +329,82 @@ class GRPOTrainer:
                                              grad=True)
                     ref = data["base_action_log_probs"][i:j] if self.ref is not None else None
                     loss, met = self._loss(lp, data, i, j, ref, ent)
-                    if self.grad_sync is not None and j == s1:
-                        self.grad_sync.arm()  # the last micro-batch: buckets all-reduce during its backward
-                    (loss / n_micro).backward()
+                    if self.optim is not None:
+                        if j == s1:
+                            self.optim.arm()  # the last micro-batch: buckets reduce-scatter during its backward
+                        loss.backward()  # 1/n_micro is applied by the optimizer step (worker.py:909-914)
+                    else:
+                        if self.grad_sync is not None and j == s1:
+                            self.grad_sync.arm()  # the last micro-batch: buckets all-reduce during its backward
+                        (loss / n_micro).backward()
                     mets.append(met)
-                if self.grad_sync is not None:
-                    self.grad_sync.wait()
-                grad_norm = torch.nn.utils.clip_grad_norm_(self.policy.parameters(), cfg.max_grad_norm)
-                self.optimizer.step()
-                if self.grad_sync is not None:
-                    self.grad_sync.zero_grad()
+                if self.optim is not None:
+                    grad_norm = self.optim.step(n_micro)
                 else:
-                    self.optimizer.zero_grad(set_to_none=True)
-                mt = torch.stack(mets).mean(0).tolist()
+                    if self.grad_sync is not None:
+                        self.grad_sync.wait()
+                    grad_norm = torch.nn.utils.clip_grad_norm_(self.policy.parameters(), cfg.max_grad_norm)
+                    self.optimizer.step()
+                    if self.grad_sync is not None:
+                        self.grad_sync.zero_grad()
+                    else:
+                        self.optimizer.zero_grad(set_to_none=True)
+                allm = torch.cat([torch.stack(mets), grad_norm.reshape(1, 1).float().expand(1, len(mets[0]))]).cpu()
+                ops.check_loss_metrics(allm[:-1])  # the one host read of the mini-batch's metrics
+                grad_norm = float(allm[-1, 0])
+                mt = allm[:-1].mean(0).tolist()
                 for k, v in (("final_loss", mt[0]), ("policy_loss", mt[1]), ("policy_entropy", mt[2]),
                              ("policy_kl", mt[3]), ("ppo_clip_ratio", mt[4]), ("grad_norm", float(grad_norm))):
                     acc.setdefault(k, []).append(v)
         return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
                                        device=next(self.policy.parameters()).device)
 
+    def _fused_grpo_group_size(self, data) -> int:
+        """G when the loss may compute GRPO itself (ops.grpo_ppo_loss): the grpo estimator on the
+        pack kernel's scores, contiguous groups of G rows (the rollout layout), no pad rows, no
+        batch-level advantage normalisation or step-wise trajectories; else 0."""
+        alg, G = self.cfg.algorithm, self.cfg.n_samples_per_prompt
+        if (alg.advantage_estimator != "grpo" or alg.advantage_batch_normalize or G > 16
+                or data.get("reward_row_sum") is None or data.get("is_last_step") is not None
+                or data.metadata.get("pad_size", 0)):
+            return 0
+        uids = data.metadata["uids"]
+        if len(uids) % G or any(uids[k] != uids[k - k % G] or (k % G == 0 and k and uids[k] == uids[k - 1])
+                                for k in range(len(uids))):
+            return 0
+        return G
+
     def _loss(self, lp, data, i, j, ref, ent):
+        """The micro-batch's policy loss (worker.py:801-876) on the fused HIP loss, with the pack
+        kernel's loss-mask row sums and the fold deferred to the backward launch (loss and metrics
+        are read after backward, as the reference does). When the micro-batch holds whole GRPO
+        groups the loss computes their advantages itself from the pack kernel's scores (one launch
+        for a4 + a6 + a7, bit-identical to data["advantages"])."""
         from . import ops
 
+        rows = data.get("loss_mask_row_sum")
+        rows = rows[i:j] if rows is not None else None
+        G = getattr(self, "_grpo_G", 0)
+        if G and i % G == 0 and (j - i) % G == 0:
+            _, loss, met = ops.grpo_ppo_loss(
+                data["rewards"][i:j], data["response_mask"][i:j], (j - i) // G, lp, data["action_log_probs"][i:j],
+                data["loss_mask"][i:j], self.loss_params, ref_log_probs=ref, entropy=ent, loss_mask_row_sum=rows,
+                norm_by_std=self.cfg.algorithm.grpo_norm_by_std, scores=data["reward_row_sum"][i:j],
+                defer_fold=True, want_advantages=False,
+                mask_within_response=bool(data.metadata.get("loss_mask_within_response", False)))
+            return loss, met
         return ops.ppo_loss(lp, data["action_log_probs"][i:j], data["advantages"][i:j], data["loss_mask"][i:j],
-                            self.loss_params, ref_log_probs=ref, entropy=ent)
+                            self.loss_params, ref_log_probs=ref, entropy=ent, loss_mask_row_sum=rows,
+                            defer_fold=True)
 
     @torch.no_grad()
     def weight_update_request(self) -> Dict[str, Any]:
-        """broadcast_to_inference_engines: bf16 copies of every parameter under its HF name."""
+        """broadcast_to_inference_engines: the bf16 weights of every parameter under its HF name.
+        With the HIP optimizer these are views of the bf16 copy its update pass (world 1) or its
+        bf16 all-gather (world > 1) wrote: no per-parameter cast."""
+        if self.optim is not None:
+            named = self.optim.named_bf16()
+            return {"names": [n for n, _ in named], "tensors": [t for _, t in named]}
         names, tensors = [], []
         for name, p in self.policy.named_parameters():
             names.append(name)

@@ -149,12 +149,14 @@ def _pad_id(tokenizer_or_pad_id) -> int:
 def convert_prompts_responses_to_batch_tensors(tokenizer, prompts: List[List[int]], responses: List[List[int]],
                                                rewards: List[List[float]], loss_masks: List[List[int]],
                                                logprobs: Optional[List[List[float]]] = None, *, device=None,
-                                               pad_rows: int = 0):
+                                               pad_rows: int = 0, return_row_sums: bool = False):
     """dataset/preprocess.py:28-132 on the HIP pack kernel. ``tokenizer`` may be the pad id.
 
     Returns (sequences int64[N,P+R], attention_mask int64, response_mask int64[N,R],
     rewards f32[N,R], loss_mask f32[N,R], rollout_logprobs f32[N,R] | None) on ``device``,
-    with ``pad_rows`` extra rows appended as pad_batch does (fused into the same kernel).
+    with ``pad_rows`` extra rows appended as pad_batch does (fused into the same kernel);
+    with ``return_row_sums`` also the per-row loss-mask and reward sums (f32 [N]: the fused
+    loss's reduction scales and the GRPO scores) from the same kernel.
     """
     from . import ops
 
@@ -177,7 +179,8 @@ def convert_prompts_responses_to_batch_tensors(tokenizer, prompts: List[List[int
         return None if a is None else torch.from_numpy(a).pin_memory().to(device, non_blocking=True)
 
     return ops.pack_experience(dev(pv), dev(po), dev(rv), dev(ro), dev(wv), dev(wo), dev(mv), dev(mo), dev(lv),
-                               dev(lo), N=N, P=P, R=R, pad=pad_rows, pad_token_id=_pad_id(tokenizer))
+                               dev(lo), N=N, P=P, R=R, pad=pad_rows, pad_token_id=_pad_id(tokenizer),
+                               return_row_sums=return_row_sums)
 
 
 def pad_size_for(batch_size: int, dp_size: int) -> int:
@@ -223,14 +226,17 @@ def convert_to_training_input(generator_output: Dict[str, Any], uids: List[str],
     N = len(resp)
     pad = pad_size_for(N, dp_size)
     logprobs = generator_output.get("rollout_logprobs", None)
-    seq, att, rmask, rew, lmask, rlp = convert_prompts_responses_to_batch_tensors(
+    seq, att, rmask, rew, lmask, rlp, lm_rows, rw_rows = convert_prompts_responses_to_batch_tensors(
         tokenizer, generator_output["prompt_token_ids"], resp, generator_output["rewards"],
-        generator_output["loss_masks"], logprobs, device=device, pad_rows=pad)
+        generator_output["loss_masks"], logprobs, device=device, pad_rows=pad, return_row_sums=True)
     if off_policy_correction_enabled:
         assert rlp is not None, "expected non-null rollout logprobs tensor when off_policy_correction is enabled"
         assert rlp.shape == lmask.shape, "Logprobs should look like responses"
     fields = {"sequences": seq, "attention_mask": att, "response_mask": rmask, "rewards": rew, "loss_mask": lmask,
-              "rollout_logprobs": rlp}
+              "rollout_logprobs": rlp,
+              # with the batch, from the pack kernel: the fused loss's reduction scales and the GRPO
+              # scores (kept only while "rewards" is unchanged; apply_reward_kl_penalty drops it)
+              "loss_mask_row_sum": lm_rows, "reward_row_sum": rw_rows}
     if generator_output.get("is_last_step", None) is not None:
         ils = torch.tensor(generator_output["is_last_step"], dtype=torch.bool)
         fields["is_last_step"] = torch.cat([ils, torch.ones(pad, dtype=torch.bool)]).to(seq.device)
@@ -240,6 +246,8 @@ def convert_to_training_input(generator_output: Dict[str, Any], uids: List[str],
         "response_length": rmask.shape[1],
         "avg_response_length": sum(len(r) for r in resp) / N,
         "pad_size": pad,
+        # every loss mask no longer than its response: loss_mask is 0 outside response_mask
+        "loss_mask_within_response": all(len(m) <= len(r) for m, r in zip(generator_output["loss_masks"], resp)),
     }
     if step_wise:
         assert generator_output.get("trajectory_ids") is not None, \
@@ -279,6 +287,8 @@ def compute_advantages_and_returns(data: TrainingInputBatch, algorithm_cfg) -> T
             f"`is_last_step` {len(la)}. The `is_last_step` tensor is likely malformed")
         adv, ret = la[traj], lr[traj]
     else:
+        if algorithm_cfg.advantage_estimator == "grpo" and data.get("reward_row_sum") is not None:
+            kw["scores"] = data["reward_row_sum"]  # the pack kernel's row sums: no reward re-read
         adv, ret = ppo_utils.compute_advantages_and_returns(
             token_level_rewards=rewards, response_mask=data["response_mask"], index=data.metadata["uids"],
             values=values, **kw)
@@ -310,6 +320,8 @@ def apply_reward_kl_penalty(data: TrainingInputBatch, algorithm_cfg, reward_kl_c
     new_rewards, m = ops.reward_kl_penalty(data["rewards"], data["action_log_probs"], data["base_action_log_probs"],
                                            data["loss_mask"], algorithm_cfg.kl_estimator_type, max(0, coef))
     data["rewards"] = new_rewards
+    if data.get("reward_row_sum") is not None:  # the pack's GRPO scores summed the old rewards
+        del data["reward_row_sum"]
     avg_kl, avg_kl_max = m.tolist()
     if reward_kl_controller is not None:
         reward_kl_controller.update(current=avg_kl, n_steps=data["rewards"].shape[0])

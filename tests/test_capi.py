@@ -34,7 +34,7 @@ def test_ffi_signatures_cover_header():
 
 def test_abi_version_and_error_path():
     lib = _ffi.load()
-    assert lib.skyrl_abi_version() == 4
+    assert lib.skyrl_abi_version() == 5
     # argument validation happens on the host before any launch: no GPU needed
     with pytest.raises(_ffi.SkyrlHipError, match="temperature"):
         _ffi.call("skyrl_logprob_fwd", ctypes.c_void_p(16), _ffi.BF16, 8, 8, 1, 1, 8, ctypes.c_void_p(16), 1, 1,
@@ -76,13 +76,32 @@ def test_grpo_ppo_loss_entry_validates_on_host():
     """skyrl_grpo_ppo_loss_fwd checks its layout before any launch: no GPU needed."""
     params = _ffi.PPOParams(0.2, 0.2, 3.0, 0, 0, 0.0, 1, 3, 0.001, 0, 0.0, 0)
     p = ctypes.c_void_p(16)
-    args = lambda ng, mdt: (p, p, mdt, ng, 1e-6, 1, p, p, p, p, None, p, 512, 1024, ctypes.byref(params),  # noqa: E731
-                            p, p, p, p, None, p, None)
+    args = lambda ng, mdt: (p, None, p, mdt, ng, 1e-6, 1, p, p, p, p, None, p, 512, 1024,  # noqa: E731
+                            ctypes.byref(params), p, p, p, p, None, 0, p, None)
     with pytest.raises(_ffi.SkyrlHipError, match="n % num_groups"):
         _ffi.call("skyrl_grpo_ppo_loss_fwd", *args(7, _ffi.I64))
     with pytest.raises(_ffi.SkyrlHipError, match="mask dtype"):
         _ffi.call("skyrl_grpo_ppo_loss_fwd", *args(64, 99))
     with pytest.raises(_ffi.SkyrlHipError, match="params is null"):
         a = list(args(64, _ffi.I64))
-        a[14] = None
+        a[15] = None
         _ffi.call("skyrl_grpo_ppo_loss_fwd", *a)
+    with pytest.raises(_ffi.SkyrlHipError, match="unknown flags"):
+        a = list(args(64, _ffi.I64))
+        a[21] = 6
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", *a)
+    with pytest.raises(_ffi.SkyrlHipError, match="null pointer"):
+        a = list(args(64, _ffi.I64))
+        a[0] = None  # neither rewards nor scores
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", *a)
+
+
+def test_ppo_loss_finish_validates_on_host():
+    params = _ffi.PPOParams(0.2, 0.2, 3.0, 0, 0, 0.0, 1, 3, 0.001, 0, 0.0, 0)
+    p = ctypes.c_void_p(16)
+    with pytest.raises(_ffi.SkyrlHipError, match="ppo_loss_finish: null pointer"):
+        _ffi.call("skyrl_ppo_loss_finish", None, None, None, 4, 4, ctypes.byref(params), p, p, None, None)
+    with pytest.raises(_ffi.SkyrlHipError, match="grad_out needs grad_logp"):
+        _ffi.call("skyrl_ppo_loss_finish", p, None, None, 4, 4, ctypes.byref(params), p, p, p, None)
+    with pytest.raises(_ffi.SkyrlHipError, match="bad sizes"):
+        _ffi.call("skyrl_ppo_loss_finish", None, None, None, 0, 4, ctypes.byref(params), p, p, p, None)

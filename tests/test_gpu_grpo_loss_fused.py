@@ -4,7 +4,11 @@ path (skyrl_grpo_advantage, then skyrl_ppo_loss_fwd), whose parity with the refe
 golden vectors and the oracle is pinned in test_gpu_parity.py; one case is also checked
 against the oracle directly (advantages 1e-6, loss 1e-6 / 1e-5 rel, gradients 1e-4 rel).
 Cases cover the one-launch kernel (XCD group map and plain map, every mask dtype, singleton
-groups, two column chunks) and the two-launch fallback (R % 4 != 0, > 2048 row chunks)."""
+groups, two column chunks) and the two-launch fallback (R % 4 != 0, > 2048 row chunks).
+
+Every case also runs the product forms: the pack kernel's GRPO scores instead of the reward
+reads (``scores=``), and the fold deferred to the backward launch (``defer_fold=True``:
+skyrl_ppo_loss_finish folds the per-block records and rescales); both bit-identical too."""
 
 import pytest
 import torch
@@ -53,25 +57,38 @@ def test_fused_matches_two_calls_bit_exact(dev, case):
     params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=use_ent, has_entropy=True)
     d = {k: v.to(dev) for k, v in dict(rew=rew, rmask=rmask, lp=lp, old=old, ref=ref, ent=ent, lmask=lmask).items()}
     rows = d["lmask"].sum(-1)
+    scores = torch.empty(n, device=dev)  # the GRPO kernel's own row sums (= pack's reward_row_sum)
+    ops.grpo_advantage(d["rew"], d["rmask"], None, None, ng, scores_out=scores)
     runs = []
-    for fused in (True, False):
+    # (fused, scores given, deferred fold, advantages output); the first is the two-call reference.
+    # Without the advantages output the response mask is not read (loss_mask <= response_mask here)
+    for fused, with_scores, defer, want_adv in ((False, False, False, True), (True, False, False, True),
+                                                (True, True, True, True), (True, False, True, True),
+                                                (False, True, True, True), (True, True, True, False)):
         x = d["lp"].clone().requires_grad_(True)
         en = d["ent"].clone().requires_grad_(use_ent)
+        sc = scores if with_scores else None
         if fused:
             adv, loss, m = ops.grpo_ppo_loss(d["rew"], d["rmask"], ng, x, d["old"], d["lmask"], params, d["ref"], en,
-                                             loss_mask_row_sum=rows)
+                                             loss_mask_row_sum=rows, scores=sc, defer_fold=defer,
+                                             want_advantages=want_adv, mask_within_response=not want_adv)
+            if not want_adv:
+                assert adv is None
+                adv = runs[0][0]
         else:
-            adv = ops.grpo_advantage(d["rew"], d["rmask"], None, None, ng)
-            loss, m = ops.ppo_loss(x, d["old"], adv, d["lmask"], params, d["ref"], en, loss_mask_row_sum=rows)
+            adv = ops.grpo_advantage(d["rew"], d["rmask"], None, None, ng, scores=sc)
+            loss, m = ops.ppo_loss(x, d["old"], adv, d["lmask"], params, d["ref"], en, loss_mask_row_sum=rows,
+                                   defer_fold=defer)
         (loss * 1.5).backward()
         runs.append((adv.cpu(), loss.detach().cpu(), m.cpu(), x.grad.cpu(), en.grad.cpu() if use_ent else None))
-    (a0, l0, m0, g0, e0), (a1, l1, m1, g1, e1) = runs
-    assert torch.equal(a0, a1), "advantages differ from skyrl_grpo_advantage"
-    assert torch.equal(l0, l1) and torch.equal(m0[:6], m1[:6]), (l0, l1, m0, m1)
-    assert m0[6] == 0  # the fold did not time out
-    assert torch.equal(g0, g1), "dL/dlogp differs from the two-call path"
-    if use_ent:
-        assert torch.equal(e0, e1)
+    a0, l0, m0, g0, e0 = runs[0]
+    for k, (a1, l1, m1, g1, e1) in enumerate(runs[1:], 1):
+        assert torch.equal(a0, a1), (k, "advantages differ from skyrl_grpo_advantage")
+        assert torch.equal(l0, l1) and torch.equal(m0[:6], m1[:6]), (k, l0, l1, m0, m1)
+        assert m1[6] == 0  # no fold timed out
+        assert torch.equal(g0, g1), (k, "dL/dlogp differs from the two-call path")
+        if use_ent:
+            assert torch.equal(e0, e1), k
     assert float(m0[4]) > 0  # the clip branch ran
 
 
@@ -121,6 +138,66 @@ def test_fused_graph_replay_and_errors(dev):
     del graph
     with pytest.raises(RuntimeError, match="n % num_groups"):
         ops.grpo_ppo_loss(d[0], d[1], 7, d[2], d[3], mask, params, d[4], loss_mask_row_sum=rows)
+
+
+def test_deferred_fold_graph_replay_and_no_grad(dev):
+    """The product leg as the bench replays it (C ABI, HIP graph): the deferred forward with the
+    scores + skyrl_ppo_loss_finish, replayed several times, gives the eager in-launch-fold results
+    bit for bit; a non-unit upstream gradient is applied by the finish launch; and a deferred call
+    under no_grad folds at once (loss and metrics valid without a backward)."""
+    import ctypes
+
+    from skyrl_amd import _ffi
+    from skyrl_amd.ops import _ptr
+
+    n, G, R = 512, 8, 1024
+    rew, rmask, lp, old, ref, ent = _inputs(n, R, G, torch.int64, 11)
+    d = [t.to(dev) for t in (rew, rmask, lp, old, ref)]
+    mask = d[1].float()
+    rows = mask.sum(-1)
+    scores = d[0].sum(-1)
+    params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
+    x = d[2].clone().requires_grad_(True)
+    adv0, loss0, m0 = ops.grpo_ppo_loss(d[0], d[1], n // G, x, d[3], mask, params, d[4], loss_mask_row_sum=rows,
+                                        scores=scores)
+    (g0,) = torch.autograd.grad(loss0 * 0.25, x)
+    adv, glp = torch.empty_like(d[2]), torch.empty_like(d[2])
+    loss, met = torch.empty(1, device=dev), torch.empty(8, device=dev)
+    gout = torch.full((1,), 0.25, device=dev)
+    ws = torch.zeros(_ffi.query("skyrl_ppo_loss_workspace_bytes", n, R), dtype=torch.uint8, device=dev)
+
+    def leg(s):
+        _ffi.call("skyrl_grpo_ppo_loss_fwd", _ptr(d[0]), _ptr(scores), _ptr(d[1]), _ffi.I64, n // G, 1e-6, 1,
+                  _ptr(d[2]), _ptr(d[3]), _ptr(mask), _ptr(d[4]), None, _ptr(rows), n, R, ctypes.byref(params),
+                  _ptr(adv), _ptr(loss), _ptr(met), _ptr(glp), None, _ffi.LOSS_DEFER_FOLD, _ptr(ws), s)
+        _ffi.call("skyrl_ppo_loss_finish", _ptr(gout), _ptr(glp), None, n, R, ctypes.byref(params), _ptr(loss),
+                  _ptr(met), _ptr(ws), s)
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        leg(torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=side):
+        leg(torch.cuda.current_stream(dev).cuda_stream)
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(adv, adv0) and torch.equal(loss[0], loss0) and torch.equal(met[:7], m0[:7])
+        assert torch.equal(glp, g0)
+    del graph
+    with torch.no_grad():
+        adv1, loss1, m1 = ops.grpo_ppo_loss(d[0], d[1], n // G, d[2], d[3], mask, params, d[4],
+                                            loss_mask_row_sum=rows, scores=scores, defer_fold=True)
+        l2, m2 = ops.ppo_loss(d[2], d[3], adv0, mask, params, d[4], loss_mask_row_sum=rows, defer_fold=True)
+    assert torch.equal(loss1, loss0) and torch.equal(m1[:7], m0[:7]) and torch.equal(adv1, adv0)
+    assert torch.equal(l2, loss0) and torch.equal(m2[:7], m0[:7])
+    ops.check_loss_metrics(torch.stack([m0, m1, m2]))
+    bad = m0.clone()
+    bad[6] = 1.0
+    with pytest.raises(RuntimeError, match="timed out"):
+        ops.check_loss_metrics(bad)
 
 
 @pytest.mark.parametrize("rpb", [1, 2])

@@ -259,9 +259,41 @@ def test_pack_emits_loss_mask_row_sums(golden, dev):
                               d["response_off"], d["reward_vals"].to(dev), d["reward_off"],
                               d["loss_mask_vals"].to(dev), d["loss_mask_off"], d["logprob_vals"].to(dev),
                               d["logprob_off"], N=N, P=P, R=R, pad=pad, pad_token_id=0, return_row_sums=True)
-    assert len(out) == 7
+    assert len(out) == 8
     assert torch.equal(out[4].cpu(), d["p_loss_mask"])
     assert torch.equal(out[6].cpu(), d["p_loss_mask"].sum(-1))
+    # reward row sums = the GRPO scores of the padded rewards (ppo_utils.py:1156)
+    torch.testing.assert_close(out[7].cpu(), d["p_rewards"].sum(-1), atol=1e-6, rtol=1e-6)
+
+
+def test_pack_reward_row_sums_are_the_grpo_scores_bit_exact(dev):
+    """pack's reward_row_sum is summed in the GRPO kernel's order: scores given to
+    skyrl_grpo_advantage reproduce what it computes from the rewards, bit for bit (R % 4 == 0;
+    dense per-token rewards so the summation order matters)."""
+    g = torch.Generator().manual_seed(17)
+    N, R, G = 96, 1024, 8
+    rl = torch.randint(1, R + 1, (N,), generator=g)
+    pl = torch.randint(1, 40, (N,), generator=g)
+    roff = torch.zeros(N + 1, dtype=torch.int64)
+    roff[1:] = torch.cumsum(rl, 0)
+    poff = torch.zeros(N + 1, dtype=torch.int64)
+    poff[1:] = torch.cumsum(pl, 0)
+    tot = int(roff[-1])
+    vals = torch.randn(tot, generator=g) * 0.1
+    out = ops.pack_experience(torch.randint(0, 100, (int(poff[-1]),), generator=g).to(dev), poff.to(dev),
+                              torch.randint(0, 100, (tot,), generator=g).to(dev), roff.to(dev), vals.to(dev),
+                              roff.to(dev), torch.ones(tot, device=dev), roff.to(dev), None, None, N=N, P=40, R=R,
+                              return_row_sums=True)
+    rew, rmask, scores = out[3], out[2], out[7]
+    own = torch.empty(N, device=dev)
+    a0 = ops.grpo_advantage(rew, rmask, None, None, N // G, scores_out=own)
+    a1 = ops.grpo_advantage(rew, rmask, None, None, N // G, scores=scores)
+    assert torch.equal(own, scores)
+    assert torch.equal(a0, a1)
+    goff, grows, ng = ops.groups_from_index([str(i % 12) for i in range(N)])  # CSR groups
+    a2 = ops.grpo_advantage(rew, rmask, goff, grows, ng)
+    a3 = ops.grpo_advantage(rew, rmask, goff, grows, ng, scores=scores)
+    assert torch.equal(a2, a3)
 
 
 @pytest.mark.parametrize("case", ["tis_token", "tis_seq", "mask_geo", "mask_prod", "tis_outlier"])
