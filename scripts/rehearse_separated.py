@@ -127,7 +127,9 @@ def main():
     rec = check("fully_async")
     rec.update(steps=len(hist), staleness_max=max(h["async/staleness_max"] for h in hist),
                aborted_then_retried=aborted["n"],
-               finite=all(torch.isfinite(torch.tensor(h["final_loss"])).item() for h in hist))
+               final_loss=[h.get("final_loss") for h in hist], keys=sorted(hist[-1]),
+               finite=all(torch.isfinite(torch.tensor(float(v))).item() for h in hist for v in h.values()
+                          if isinstance(v, (int, float))))
     out["fully_async"] = rec
     asyncio.run(client.teardown())
     ok = all(r["weights_bit_exact"] and r["greedy_equal_colocated"] for r in out["sync"] + [rec]) and rec["finite"] \
@@ -140,4 +142,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        import traceback
+
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "ok": False, "error": traceback.format_exc()}),
+              flush=True)
+        raise

@@ -63,7 +63,9 @@ class RemoteEngine(InferenceEngineInterface):
         while True:
             rep = _recv(self.peer, self.rep_group)
             fut = self._pending.pop(rep["id"], None)
-            if fut is not None:
+            # a caller that was cancelled meanwhile (a generation worker stopped while its request
+            # was in flight) has cancelled the future: drop the reply, keep reading
+            if fut is not None and fut.set_running_or_notify_cancel():
                 if rep["ok"]:
                     fut.set_result(rep["result"])
                 else:

@@ -30,3 +30,4 @@ def test_separated_trainer_feeds_remote_engine():
     res = json.loads(lines[-1])
     assert p.returncode == 0 and res["ok"], json.dumps(res)[:3000] + p.stderr[-2000:]
     assert len(res["sync"]) == 2 and res["fully_async"]["steps"] == 3
+    print(json.dumps(res))

@@ -142,6 +142,17 @@ def _case(rank, world):
         for p, o in zip(prompts, got):
             assert o["stop_reasons"] == ["abort"] and 0 < len(o["response_ids"][0]) < 400
             assert o["response_ids"][0] == _uninterrupted(p, len(o["response_ids"][0]))
+        # callers cancelled while their requests are in flight (stopped generation workers): the
+        # late replies are dropped and the channel keeps serving
+        gone = [asyncio.create_task(remote.generate({"prompt_token_ids": [p], "sampling_params": {"max_tokens": 400}}))
+                for p in prompts]
+        await asyncio.sleep(0.1)
+        for t in gone:
+            t.cancel()
+        await asyncio.gather(*gone, return_exceptions=True)
+        await remote.abort_generation()
+        o = await remote.generate({"prompt_token_ids": [[3]], "sampling_params": {"max_tokens": 5}})
+        assert o["response_ids"][0] == _uninterrupted([3], 5)
         # pause -> update -> resume with a request in flight (client retry, token-in/token-out)
         client = InferenceEngineClient([remote], abort_grace_seconds=0.0)
         t = asyncio.create_task(client.generate({"prompt_token_ids": [[8, 1]], "sampling_params": {"max_tokens": 60}}))
