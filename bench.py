@@ -10,7 +10,8 @@ path over one synthetic batch:
   ref/old   skyrl_logprob_fwd over all 512x1024 response positions (2 passes)
   advantage skyrl_grpo_advantage over [512, 1024] (contiguous groups, pack's reward row sums)
   update    per micro-batch (16 seqs): skyrl_policy_train_fwd, ONE pass per token computing
-            logprob + entropy + PPO/KL loss and writing dlogits (bf16); metrics read once per step
+            logprob + entropy + PPO/KL loss and writing dlogits (bf16), each row held in the
+            registers of 8 workgroups; metrics read once per step
   optimizer grad norm + clip + AdamW over Qwen2.5-1.5B's 1.54 B fp32 params, writing the bf16
             rollout copy (reduce-scatter / all-gather over RCCL when N > 1)
 
@@ -316,7 +317,7 @@ def run(args):
          CEILING_READ_GBS),
         ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
          2 * (N // mb) + (N // mb if args.unfused else 0), CEILING_READ_GBS),
-        ("skyrl_policy_train_fwd (policy_train_resident_kernel)", train_timer,
+        ("skyrl_policy_train_fwd (policy_train_split_kernel: each row in 8 pieces of 128 threads)", train_timer,
          rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb, CEILING_RW_GBS),
         ("skyrl_adamw_step (sumsq + plan + adamw_update_kernel<shadow>)", adam_timer,
          (reducer.layout.shard_numel * (4 + 30)) if reducer is not None else 0, 1, CEILING_RW_GBS),

@@ -110,18 +110,24 @@ def main():
                       ops._ptr(labels), labels.stride(0), labels.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
                       ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met), ops._ptr(lp),
                       ops._ptr(ent), ops._ptr(dlog), R * V, V, ops._ptr(ws), st)
-        variants = ((1, 1, 768), (1, 1, 1024), (1, 0, 1024), (0, 1, 1024))
+        # (split, resident, nt stores, resident threads)
+        # (split, resident, nt stores, resident threads, 100 * split parts)
+        variants = [(1, 1, 1, 1024, 800), (1, 1, 1, 1024, 400), (1, 1, 0, 1024, 800), (0, 1, 1, 1024, 800)]
         times = {v: [] for v in variants}
         for _ in range(args.rounds):  # interleaved rounds
             for v in variants:
-                resident, nts, nt = v
+                split, resident, nts, nt, sm = v
+                _ffi.call("skyrl_tune", b"train_split_parts", sm // 100)
+                _ffi.call("skyrl_tune", b"train_split", split)
                 _ffi.call("skyrl_tune", b"train_resident", resident)
                 _ffi.call("skyrl_tune", b"train_ntstore", nts)
                 _ffi.call("skyrl_tune", b"train_resident_nt", nt)
                 times[v].append(timeit(lambda: (fused(x0), fused(x1))) / 2)
-        for (resident, nts, nt), t in times.items():
+        _ffi.call("skyrl_tune", b"train_split", 1)
+        _ffi.call("skyrl_tune", b"train_split_parts", 8)
+        for (split, resident, nts, nt, sm), t in times.items():
             ms = statistics.median(t)
-            res[f"policy_train_fused_resident{resident}_nts{nts}_nt{nt}"] = {
+            res[f"policy_train_fused_split{split}_mode{sm}_resident{resident}_nts{nts}_nt{nt}"] = {
                 "ms": ms, "GBps_hbm_algorithmic": rows * (V * 4 + 40) / ms / 1e6,
                 "vs_unfused_bytes": rows * (V * 6) / ms / 1e6}
         _ffi.call("skyrl_tune", b"train_resident", 1)

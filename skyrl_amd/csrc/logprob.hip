@@ -213,6 +213,8 @@ namespace skyrl {
 extern int g_train_resident;
 extern int g_train_resident_nt;
 extern int g_train_ntstore;
+extern int g_train_split;
+extern int g_train_split_parts;
 extern int g_grpo_slices;
 extern int g_loss_units;
 extern int g_loss_bwd_blocks;
@@ -229,6 +231,16 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "logprob_unroll") {
         SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: logprob_unroll must be 4 or 8");
         g_tune.unroll = value;
+        return SKYRL_OK;
+    }
+    if (k == "train_split_parts") {
+        SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: train_split_parts must be 4 or 8");
+        g_train_split_parts = value;
+        return SKYRL_OK;
+    }
+    if (k == "train_split") {
+        SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: train_split must be 0 or 1");
+        g_train_split = value;
         return SKYRL_OK;
     }
     if (k == "train_ntstore") {

@@ -169,6 +169,10 @@ __global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __r
         scal[0] = (float)all;
         scal[1] = p.use_entropy_loss ? (float)(-(double)p.entropy_loss_coef / d) : 0.f;
         scal[2] = (float)(1.0 / d);
+        // this launch's tag for the split kernel's exchange granules (header word 16, see
+        // skyrl_policy_train_fwd); the previous launch's granules carry the previous tag
+        unsigned* epoch = reinterpret_cast<unsigned*>(scal) + 16;
+        epoch[0] = epoch[0] + 1u;
     }
     if (p.loss_reduction == 0) {
         const float sc = (float)(1.0 / d);
@@ -484,6 +488,184 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
     TPHASE(4);
 }
 
+// ---- 2c. split rows: each row is cut into P contiguous pieces (P = 8 by default: 128-thread
+// workgroups; 4: 256 threads), NV 16-B vectors per thread held in registers across both
+// sweeps, so HBM still sees V*2 read + V*2 written per token. Several pieces of DIFFERENT rows
+// share a CU at different phases (eighths: 6 workgroups of 143 VGPRs; quarters: 4 of 115):
+// one piece's barrier and store drain overlap the others' loads, where the one-row-per-CU
+// resident kernel left its CU without loads in flight for about half of each row
+// (profiles/r02_policy_train_phases.log). Measured per 16 x 1024 tokens at V = 151,936
+// (profiles/r03_kbench_split.json, one box): eighths 1.71 ms = 5.83 TB/s, quarters 1.74 ms,
+// sixteenths 1.99 ms, resident 1.94 ms. Copy-shaped probe: split rows 5.76 TB/s vs 5.13
+// resident (profiles/r03_rw_split_probe.log).
+// The pieces exchange their online-softmax states (m, s, w) as epoch-tagged 64-bit granules
+// (write-through agent-scope stores, polled with agent-scope loads: the pieces sit on
+// different XCDs, whose L2s are not coherent); every piece merges the P states in piece
+// order, so all derive bit-identical lse / entropy / loss terms, and piece 0 writes the
+// token's outputs. The epoch is advanced once per launch by train_scales_kernel, so a piece
+// never mistakes the previous launch's granules for its partners'. The pieces of a row are
+// consecutive blocks (blocks are dispatched in order, so a waiting piece's partners are
+// resident or next to be), every poll is bounded, and a timeout raises the error word
+// (metrics[6] = 1 via the epilogue; ops.check_loss_metrics raises) and leaves NaN in that
+// row's terms instead of hanging.
+constexpr int kSplitP = 4;     // the template default; the host picks g_train_split_parts
+constexpr int kSplitMaxP = 8;  // skyrl_tune("train_split_parts", 4/8): pieces of 1024/P threads
+constexpr unsigned kSplitMaxPolls = 1u << 20;
+
+typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
+typedef __attribute__((address_space(1))) unsigned ptr_gu32;
+
+template <int NV, bool HAS_T, int P = kSplitP>
+__global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_kernel(
+    const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int V, const int64_t* __restrict__ labels,
+    int64_t lsb, int64_t lst, float temp, const float* __restrict__ old, const float* __restrict__ adv,
+    const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
+    const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
+    float* __restrict__ tok, uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts,
+    unsigned long long* __restrict__ gran, unsigned* __restrict__ err_word) {
+    constexpr int NT = 1024 / P;
+    __shared__ St s_st[NT / 64];
+    __shared__ float s_g[4];
+    __shared__ float s_part[P * 3];
+    // block -> (row, piece): consecutive blocks. (Placing a row's pieces on one XCD, so the
+    // exchange stays in that XCD's L2, measured slower: 2.05 vs 1.71 ms per 16 x 1024 tokens,
+    // profiles/r03_kbench_split.json; so did longer sleeps between polls, no change.)
+    const int64_t r = blockIdx.x / P;
+    const int part = blockIdx.x % P;
+    const int64_t b = r / R, t = r % R;
+    const uint16_t* row = logits + b * sb + t * st_;
+    uint16_t* out = dx + b * gsb + t * gst;
+    const int lane = threadIdx.x & 63;
+    const int nvec = V >> 3;
+    const int per = (nvec + P - 1) / P;  // host: (NV-1)*NT < the last quarter's length, per <= NV*NT
+    const int lo = part * per;
+    const int hi = min(nvec, lo + per);
+    const uint4* rv = reinterpret_cast<const uint4*>(row) + lo;
+    auto tval = [&](float x) { return HAS_T ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
+    const unsigned epoch = __hip_atomic_load((const ptr_gu32*)(reinterpret_cast<const unsigned*>(scal) + 16),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t lab = labels[b * lsb + t * lst];
+    const float o_old = old[r];
+    const float o_adv = adv[r];
+    const float o_m = mask ? mask[r] : 1.f;
+    const float o_ref = p.use_kl_loss ? ref[r] : 0.f;
+    const float o_rs = row_scale[b];
+    const float o_ge = scal[1];
+    float xl = 0.f;
+    if (threadIdx.x == 0) xl = (lab >= 0 && lab < V) ? bf16_to_f32(row[lab]) : __builtin_nanf("");
+    constexpr uint32_t kNinf2 = 0xff80ff80u;
+    uint4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV - 1; ++k) v[k] = ld_nt(rv + threadIdx.x + k * NT);
+    const int nq = hi - lo;
+    {
+        const int idx = threadIdx.x + (NV - 1) * NT;
+        const bool ok = idx < nq;
+        const uint4 t4 = ld_nt(rv + (ok ? idx : nq - 1));
+        v[NV - 1] = make_uint4(ok ? t4.x : kNinf2, ok ? t4.y : kNinf2, ok ? t4.z : kNinf2, ok ? t4.w : kNinf2);
+    }
+    St st{-3.402823466e38f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        float x[8];
+        unpack8(v[k], x);
+        if constexpr (HAS_T) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = tval(x[j]);
+        }
+        st_add8(st, x);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        St o{__shfl_xor(st.m, off, kWave), __shfl_xor(st.s, off, kWave), __shfl_xor(st.w, off, kWave)};
+        st_merge(st, o);
+    }
+    if (lane == 0) s_st[threadIdx.x / kWave] = st;
+    __syncthreads();
+    if (threadIdx.x < kWave) {
+        // this piece's state: an xor tree over the NT/64 wave states (lanes beyond them hold the
+        // empty state), at least 4 lanes wide so lanes 0..2, which publish m, s, w, all hold it
+        St a = threadIdx.x < NT / 64 ? s_st[threadIdx.x] : St{-3.402823466e38f, 0.f, 0.f};
+#pragma unroll
+        for (int off = (NT / 128 > 2 ? NT / 128 : 2); off > 0; off >>= 1) {
+            St o{__shfl_xor(a.m, off, kWave), __shfl_xor(a.s, off, kWave), __shfl_xor(a.w, off, kWave)};
+            st_merge(a, o);
+        }
+        unsigned long long* g = gran + r * (P * 3);
+        // lanes 0..2 publish (m, s, w) of this quarter; lanes 3q..3q+2 of the other quarters poll
+        const int q = lane / 3, f = lane % 3;
+        const float mine = f == 0 ? a.m : (f == 1 ? a.s : a.w);
+        if (lane < 3) {
+            s_part[part * 3 + f] = mine;
+            __hip_atomic_store((ptr_gu64*)(g + part * 3 + f),
+                               ((unsigned long long)epoch << 32) | __float_as_uint(mine), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane < P * 3 && q != part) {
+            unsigned long long x = 0;
+            for (unsigned polls = 0; polls < kSplitMaxPolls; ++polls) {
+                x = __hip_atomic_load((const ptr_gu64*)(g + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((unsigned)(x >> 32) == epoch) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            const bool ok = (unsigned)(x >> 32) == epoch;
+            s_part[lane] = ok ? __uint_as_float((unsigned)x) : __builtin_nanf("");
+            if (!ok) __hip_atomic_store((ptr_gu32*)err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_wave_barrier();  // wave 0's LDS writes above precede its reads below
+        if (threadIdx.x == 0) {
+            St m{s_part[0], s_part[1], s_part[2]};
+#pragma unroll
+            for (int j = 1; j < P; ++j) st_merge(m, St{s_part[3 * j], s_part[3 * j + 1], s_part[3 * j + 2]});
+            const float logs = fast_log2(m.s) * kLn2;
+            const float lse = m.m + logs;
+            const float H = logs - kLn2 * (m.w / m.s);
+            const float lp = tval(xl) - lse;
+            const float lo_c = (float)(1.0 - (double)p.eps_clip_low), hi_c = (float)(1.0 + (double)p.eps_clip_high);
+            float loss, dl, clip;
+            ppo_token(lp, o_old, o_adv, lo_c, hi_c, p.clip_ratio_c, p.dual_clip, loss, dl, clip);
+            const float kl = p.use_kl_loss ? (approx_kl(lp, o_ref, p.kl_type) * o_m) * o_m : 0.f;
+            if (part == 0) {
+                logp_out[r] = lp;
+                if (ent_out) ent_out[r] = H;
+                *reinterpret_cast<float4*>(tok + r * 4) = make_float4(loss * o_m, clip * o_m, kl, H * o_m);
+            }
+            s_g[0] = lse;
+            s_g[1] = (dl * o_m) * o_rs;
+            s_g[2] = o_ge * o_m;
+            s_g[3] = H;
+        }
+    }
+    __syncthreads();
+    const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
+    const int lab_s = (lab >= 0 && lab < V) ? (int)lab - 8 * lo : -1;  // label's slot in this quarter
+#pragma unroll
+    for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
+    const float inv_t = HAS_T ? 1.f / temp : 1.f;
+    uint4* ov = reinterpret_cast<uint4*>(out) + lo;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int idx = threadIdx.x + k * NT;
+        if (k < NV - 1 || idx < nq) {
+            float x[8];
+            unpack8(v[k], x);
+            const int v0 = idx * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float lpv = tval(x[j]) - L;
+                const float pv = fast_exp2(lpv * kLog2e);
+                float gg = -glp * pv - gent * pv * (lpv + H);
+                if (v0 + j == lab_s) gg += glp;
+                x[j] = HAS_T ? gg * inv_t : gg;
+            }
+            st_out(ov + idx, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                        pack_bf16x2(x[6], x[7])), nts);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // ---- 3. loss scalar + metrics ---------------------------------------------------------
 // One wave per row: row sums of loss*m, kl*m*m, m -> sequence-level terms in fp64;
 // token-level sums (loss*m, clip*m, ent*m) folded over the block; same metric layout as
@@ -543,8 +725,10 @@ __global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* _
         metrics[SKYRL_M_KL] = kl;
         metrics[SKYRL_M_CLIP_RATIO] = (float)(v[3] / msum);
         metrics[SKYRL_M_MASK_SUM] = scal[0];
-        metrics[6] = 0.f;
+        unsigned* err = reinterpret_cast<unsigned*>(const_cast<float*>(scal)) + 32;  // header word 32
+        metrics[6] = err[0] ? 1.f : 0.f;  // split-row exchange timed out (never expected)
         metrics[7] = 0.f;
+        err[0] = 0u;
     }
 }
 
@@ -569,13 +753,26 @@ __global__ void scale_bf16_kernel(const float* __restrict__ g, uint16_t* __restr
 int g_train_resident = 1;  // skyrl_tune("train_resident", 0/1)
 int g_train_resident_nt = 1024;  // skyrl_tune("train_resident_nt", 768/1024)
 int g_train_ntstore = 1;   // skyrl_tune("train_ntstore", 0/1): non-temporal dlogits stores
+int g_train_split = 1;     // skyrl_tune("train_split", 0/1): split-row kernel where it applies
+int g_train_split_parts = 8;  // skyrl_tune("train_split_parts", 4/8): pieces per row
 
 }  // namespace skyrl
 
 using namespace skyrl;
 
+// Workspace: [0, 256) header (scal[0..2] floats; word 16: the split kernel's exchange epoch;
+// word 32: its timeout flag), row scales (n floats, 256-B padded), per-token terms (n*R x 16 B,
+// 256-B padded), the split kernel's exchange granules (n*R x kSplitMaxP x 3 x 8 B). Zeroed once at
+// allocation; the kernels keep it consistent from launch to launch.
+namespace {
+size_t pt_pad(size_t x) { return (x + 255) / 256 * 256; }
+size_t pt_tok_off(int32_t n) { return 256 + pt_pad((size_t)n * 4); }
+size_t pt_gran_off(int32_t n, int32_t R) { return pt_tok_off(n) + pt_pad((size_t)n * R * 16); }
+}  // namespace
+
 extern "C" size_t skyrl_policy_train_workspace_bytes(int32_t n, int32_t R) {
-    return 256 + (size_t)n * 4 + 256 + (size_t)n * R * 16 + 256;
+    if (n <= 0 || R <= 0) return 256;
+    return pt_gran_off(n, R) + (size_t)n * R * kSplitMaxP * 3 * 8;
 }
 
 namespace {
@@ -602,6 +799,53 @@ TrainKernel resident_edge_for(int nv, bool has_t) {
         case 12: return pick_resident<12, true>(has_t);
         default: return pick_resident<14, true>(has_t);
     }
+}
+using SplitKernel = void (*)(const uint16_t*, int64_t, int64_t, int, int, const int64_t*, int64_t, int64_t, float,
+                             const float*, const float*, const float*, const float*, const float*, const float*,
+                             skyrl_ppo_params, float*, float*, float*, uint16_t*, int64_t, int64_t, bool,
+                             unsigned long long*, unsigned*);
+template <int NV, int P>
+SplitKernel pick_split(bool has_t) {
+    return has_t ? policy_train_split_kernel<NV, true, P> : policy_train_split_kernel<NV, false, P>;
+}
+template <int P>
+SplitKernel split_for_p(int nv, bool has_t) {
+    switch (nv) {
+        case 1: return pick_split<1, P>(has_t);
+        case 2: return pick_split<2, P>(has_t);
+        case 3: return pick_split<3, P>(has_t);
+        case 4: return pick_split<4, P>(has_t);
+        case 5: return pick_split<5, P>(has_t);
+        case 6: return pick_split<6, P>(has_t);
+        case 7: return pick_split<7, P>(has_t);
+        case 8: return pick_split<8, P>(has_t);
+        case 9: return pick_split<9, P>(has_t);
+        case 10: return pick_split<10, P>(has_t);
+        case 11: return pick_split<11, P>(has_t);
+        case 12: return pick_split<12, P>(has_t);
+        case 13: return pick_split<13, P>(has_t);
+        case 14: return pick_split<14, P>(has_t);
+        case 15: return pick_split<15, P>(has_t);
+        case 16: return pick_split<16, P>(has_t);
+        case 17: return pick_split<17, P>(has_t);
+        case 18: return pick_split<18, P>(has_t);
+        default: return pick_split<19, P>(has_t);
+    }
+}
+SplitKernel split_for(int nv, bool has_t, int parts) {
+    return parts == 8 ? split_for_p<8>(nv, has_t) : split_for_p<4>(nv, has_t);
+}
+// the split kernel's vectors per thread for nvec row vectors cut into `parts` pieces of
+// 1024 / parts threads, or 0 if its layout does not fit: pieces of per = ceil(nvec / parts)
+// vectors, NV = ceil(per / threads) <= 19, and the last piece still covers the NV-1
+// unconditional loads of every thread
+int split_nv(int nvec, int parts) {
+    const int nt = 1024 / parts;
+    const int per = (nvec + parts - 1) / parts;
+    const int nv = (per + nt - 1) / nt;
+    const int last = nvec - (parts - 1) * per;
+    if (nv < 1 || nv > 19 || last <= (nv - 1) * nt) return 0;
+    return nv;
 }
 // aligned rows: NV = ceil(nvec / 1024) exactly, 1..19 (V <= 155,648)
 TrainKernel resident_aligned_for(int nv, bool has_t) {
@@ -651,7 +895,9 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
     char* w = reinterpret_cast<char*>(workspace);
     float* scal = reinterpret_cast<float*>(w);
     float* row_scale = reinterpret_cast<float*>(w + 256);
-    float* tok = reinterpret_cast<float*>(w + 256 + (((size_t)n * 4 + 255) / 256) * 256);
+    float* tok = reinterpret_cast<float*>(w + pt_tok_off(n));
+    auto* gran = reinterpret_cast<unsigned long long*>(w + pt_gran_off(n, R));
+    unsigned* err_word = reinterpret_cast<unsigned*>(w) + 32;
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL(train_scales_kernel, dim3(1), dim3(kThreads), 0, s, loss_mask, n, R, *params, row_scale, scal);
     int rc = check_launch("train_scales_kernel");
@@ -681,7 +927,15 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
             if (span <= cand * 1024) { nv = cand; break; }
     }
     const bool resident_ok = g_train_resident && same_align && nv > 0;
-    if (g_train_resident && use768 && aligned) {
+    const int parts = g_train_split_parts;
+    const int snv = aligned ? split_nv(nvec, parts) : 0;
+    if (g_train_split && g_train_resident && same_align && snv > 0 && (int64_t)n * R * parts < (1ll << 31)) {
+        hipLaunchKernelGGL(split_for(snv, has_t, parts), dim3((unsigned)((int64_t)n * R * parts)), dim3(1024 / parts),
+                           0, s, in,
+                           stride_b, stride_t, R, V, labels, lstride_b, lstride_t, temperature, old_log_probs,
+                           advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok,
+                           out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word);
+    } else if (g_train_resident && use768 && aligned) {
         auto kern = has_t ? policy_train_resident_kernel<768, 25, true, false>
                           : policy_train_resident_kernel<768, 25, false, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(768), 0, s, in, stride_b, stride_t, R, V, labels,

@@ -291,14 +291,16 @@ FOLD_TIMEOUT_SLOT = 6  # metrics[6] = 1: an in-launch fold's bounded spin timed 
 
 
 def check_loss_metrics(metrics) -> None:
-    """Raise when a loss launch's in-launch fold timed out (metrics[6] != 0): its loss and
-    metrics are NaN while the gradients were written, so training must not go on silently.
-    ``metrics`` is one [8] vector or rows of them, device or host; one host read."""
+    """Raise when a loss launch's cross-workgroup exchange timed out (metrics[6] != 0): the
+    in-launch fold of skyrl_ppo_loss_fwd / skyrl_grpo_ppo_loss_fwd (loss and metrics NaN, the
+    gradients written), or a split row's state exchange in skyrl_policy_train_fwd (that row's
+    outputs NaN). Training must not go on silently. ``metrics`` is one [8] vector or rows of
+    them, device or host; one host read."""
     m = torch.as_tensor(metrics)
     flag = m.reshape(-1, m.shape[-1])[:, FOLD_TIMEOUT_SLOT]
     if bool((flag != 0).any()):
-        raise RuntimeError("fused PPO loss: the in-launch fold of the per-block records timed out "
-                           "(metrics[6] = 1; loss and metrics are NaN)")
+        raise RuntimeError("fused PPO loss: a cross-workgroup exchange (loss fold or split-row softmax state) "
+                           "timed out (metrics[6] = 1; the affected outputs are NaN)")
 
 
 def _loss_workspace(dev, n, R, defer):

@@ -59,6 +59,7 @@ class PolicyMicroStep:
             if backward:
                 loss.backward()
             m = metrics.tolist()
+            ops.check_loss_metrics(torch.tensor(m))  # the split rows' exchange never timed out
             status = {"final_loss": m[ops._ffi.M_FINAL_LOSS], "policy_loss": m[ops._ffi.M_POLICY_LOSS],
                       "policy_entropy": m[ops._ffi.M_ENTROPY], "response_length": R, "policy_lr": self.lr_fn(),
                       "loss_metrics/clip_ratio": m[ops._ffi.M_CLIP_RATIO]}

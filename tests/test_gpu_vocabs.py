@@ -90,8 +90,9 @@ def test_logprob_entropy_per_vocab(dev, V):
 @pytest.mark.parametrize("V", VOCABS)
 @pytest.mark.parametrize("temp", [1.0, 0.7])
 def test_policy_train_per_vocab(dev, V, temp):
-    """Fused training pass on the [:, -R-1:-1] slice (GPT-2: misaligned rows), resident vs
-    two-sweep kernel, and vs torch-CPU autograd of the oracle's loss assembly."""
+    """Fused training pass on the [:, -R-1:-1] slice (GPT-2: misaligned rows): the default
+    kernel (split rows where the layout allows, else resident) vs the resident and the
+    two-sweep kernels, and vs torch-CPU autograd of the oracle's loss assembly."""
     g = torch.Generator().manual_seed(V % 991)
     n, S, R = 2, 11, 6
     logits = (torch.randn(n, S, V, generator=g) * 3).to(torch.bfloat16)
@@ -105,7 +106,8 @@ def test_policy_train_per_vocab(dev, V, temp):
     cfg = AlgorithmConfig(use_entropy_loss=True, policy_loss_type="dual_clip", clip_ratio_c=1.5)
     params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=True, has_entropy=True)
     outs = []
-    for resident in (1, 0):
+    for split, resident in ((1, 1), (0, 1), (0, 0)):
+        ops._ffi.call("skyrl_tune", b"train_split", split)
         ops._ffi.call("skyrl_tune", b"train_resident", resident)
         try:
             full = logits.to(dev).requires_grad_(True)
@@ -115,9 +117,15 @@ def test_policy_train_per_vocab(dev, V, temp):
             (loss * 1.5).backward()
         finally:
             ops._ffi.call("skyrl_tune", b"train_resident", 1)
+            ops._ffi.call("skyrl_tune", b"train_split", 1)
         outs.append((loss.detach(), m.clone(), lp, ent, full.grad))
-    for a, b in zip(outs[0], outs[1]):
+    for a, b in zip(outs[1], outs[2]):  # resident vs two-sweep: the same per-thread order
         close(a, b, atol=1e-6, rtol=1e-5)
+    # split vs resident: another softmax summation order (fp32), dlogits within a bf16 rounding
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        close(a, b, atol=1e-5, rtol=1e-5)
+    close(outs[0][4], outs[1][4], atol=2e-6, rtol=1e-2)
+    assert float(outs[0][1][6]) == 0.0  # no split-exchange timeout
     loss, m, lp, ent, grad = outs[0]
     assert torch.count_nonzero(grad[:, :S - R - 1]) == 0 and torch.count_nonzero(grad[:, -1]) == 0
     # the reference divides the bf16 logits by T in place (model_wrapper.py:314), then the fp32 path
