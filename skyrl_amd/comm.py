@@ -482,6 +482,13 @@ class BucketedGradAllReduce:
     (before clipping) launches any bucket whose parameters got no gradient and makes the
     compute stream wait for the comm stream. World size 1: the buckets are still the grads'
     storage and nothing is launched.
+
+    torch semantics are kept: a parameter that got no gradient on ANY rank during the
+    mini-batch (one MAX all-reduce of per-parameter flags) has ``.grad = None`` after
+    :meth:`wait`, so AdamW skips it as it would at world size 1, and :meth:`zero_grad`
+    re-attaches the bucket views. :meth:`wait` raises if a ``.grad`` was detached from its
+    bucket meanwhile (``zero_grad(set_to_none=True)``, a restore that assigned new tensors):
+    the all-reduce would then average the stale buckets while each rank kept its own grads.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], group=None, bucket_bytes: int = 64 << 20):
@@ -507,14 +514,18 @@ class BucketedGradAllReduce:
             groups.append(cur)
         self.buckets: List[Tuple[torch.Tensor, List[torch.nn.Parameter]]] = []
         self._bucket_of: Dict[int, int] = {}
+        self._views: List[Tuple[torch.nn.Parameter, torch.Tensor]] = []
         for b, plist in enumerate(groups):
             flat = torch.zeros(sum(p.numel() for p in plist), dtype=torch.float32, device=self.device)
             off = 0
             for p in plist:
-                p.grad = flat[off:off + p.numel()].view_as(p)
+                view = flat[off:off + p.numel()].view_as(p)
+                p.grad = view
+                self._views.append((p, view))
                 self._bucket_of[id(p)] = b
                 off += p.numel()
             self.buckets.append((flat, plist))
+        self._touched: set = set()  # params whose grad hook fired since the last zero_grad
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in ps]
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._armed = False
@@ -534,6 +545,7 @@ class BucketedGradAllReduce:
         self.launched_during_backward = 0
 
     def _on_grad(self, p) -> None:
+        self._touched.add(id(p))
         if not self._armed:
             return
         b = self._bucket_of[id(p)]
@@ -563,17 +575,32 @@ class BucketedGradAllReduce:
         buckets launched from inside the backward."""
         if not self._armed:
             return 0
+        for p, view in self._views:
+            if p.grad is None or p.grad.data_ptr() != view.data_ptr():
+                raise RuntimeError("BucketedGradAllReduce: a parameter's .grad is no longer its bucket view "
+                                   "(zero_grad(set_to_none=True) or a reassigned grad); use "
+                                   "BucketedGradAllReduce.zero_grad() between steps")
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
         if self.stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
         self._armed = False
+        # parameters no rank produced a gradient for: None, as at world size 1
+        flags = torch.tensor([1 if id(p) in self._touched else 0 for p, _ in self._views], dtype=torch.int32,
+                             device=self.device)
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
+        for (p, _), f in zip(self._views, flags.tolist()):
+            if not f:
+                p.grad = None
         return self.launched_during_backward
 
     def zero_grad(self) -> None:
         for flat, _ in self.buckets:
             flat.zero_()
+        for p, view in self._views:
+            p.grad = view
+        self._touched.clear()
 
 
 

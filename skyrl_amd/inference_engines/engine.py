@@ -476,7 +476,11 @@ class ModelRunner:
         # single-parameter batches without penalties or suppressed ids where the fused kernel
         # measured faster (greedy at >= 192 or <= 16 rows, T > 0 at >= 480 rows; see _fused_ok and
         # profiles/r02_lmhead_sample_bench.json); "always": every unfiltered single-parameter
-        # batch; "off".
+        # batch; "off". Under "auto" a request's logits come from either GEMM depending on how many
+        # rows share its step. Both round fp32 sums to bf16 and agree within one bf16 rounding,
+        # argmax included wherever the top-2 margin exceeds it
+        # (tests/test_gpu_engine.py::test_lmhead_gemm_vs_flinear_logits_and_argmax); a run that
+        # must not depend on batch composition at all (seeded evaluation) sets "off" or "always".
         if fused_lmhead == "greedy":  # the r02 name of "auto"
             fused_lmhead = "auto"
         if fused_lmhead not in ("auto", "always", "off"):

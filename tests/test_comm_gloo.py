@@ -253,3 +253,32 @@ def _bucketed_case(rank, world):
 
 def test_bucketed_grad_allreduce_during_backward_gloo():
     _run(_bucketed_case)
+
+
+def _bucketed_unused_case(rank, world):
+    """A parameter no rank produced a gradient for ends with .grad None (AdamW skips it, as at
+    world size 1); one that only rank 1 used is averaged on both; a .grad detached from its
+    bucket raises instead of averaging stale buckets."""
+    torch.manual_seed(0)
+    used, only1, unused = torch.nn.Linear(4, 4), torch.nn.Linear(4, 4), torch.nn.Linear(4, 4)
+    params = list(used.parameters()) + list(only1.parameters()) + list(unused.parameters())
+    sync = comm.BucketedGradAllReduce(params, bucket_bytes=16 * 4)
+    x = torch.randn(3, 4, generator=torch.Generator().manual_seed(rank))
+    sync.arm()
+    y = used(x).sum() + (only1(x).sum() if rank == 1 else 0.0)
+    y.backward()
+    sync.wait()
+    assert all(p.grad is not None for p in used.parameters())
+    assert all(p.grad is not None for p in only1.parameters())  # rank 0 too: the mean is nonzero
+    assert all(p.grad is None for p in unused.parameters())
+    sync.zero_grad()  # views re-attached, zeroed
+    assert all(p.grad is not None and not p.grad.any() for p in params)
+    sync.arm()
+    used(x).sum().backward()
+    used.weight.grad = None  # detached (e.g. zero_grad(set_to_none=True))
+    with pytest.raises(RuntimeError, match="bucket view"):
+        sync.wait()
+
+
+def test_bucketed_grad_allreduce_unused_and_detached_gloo():
+    _run(_bucketed_unused_case)

@@ -521,3 +521,28 @@ def test_engine_n_samples_and_top_logprobs():
     c = asyncio.run(eng.generate({"prompt_token_ids": prompts[:1], "sampling_params": dict(sp, logprobs=5)}))
     d = asyncio.run(eng.generate({"prompt_token_ids": prompts[:1], "sampling_params": sp}))
     assert c["response_ids"] == d["response_ids"] and c["response_logprobs"] == d["response_logprobs"]
+
+
+@pytest.mark.parametrize("shape", [(192, 1536, 151936), (16, 1536, 151936), (512, 896, 50257)])
+def test_lmhead_gemm_vs_flinear_logits_and_argmax(shape):
+    """The engine's default fused_lmhead="auto" picks the MFMA GEMM (with or without the sampler
+    in its epilogue) or F.linear by batch occupancy, so a request's logits can come from either.
+    Both round fp32 sums to bf16: they agree within one bf16 rounding (rtol 2^-7), almost all
+    elements bit for bit, and the greedy token (argmax) is the same wherever the F.linear top-2
+    margin exceeds that rounding."""
+    import torch.nn.functional as F
+
+    from skyrl_amd import ops
+
+    M, H, V = shape
+    g = torch.Generator(device="cuda").manual_seed(M + V)
+    h = torch.randn(M, H, device="cuda", generator=g).to(torch.bfloat16)
+    w = (0.02 * torch.randn(V, H, device="cuda", generator=g)).to(torch.bfloat16)
+    a = ops.lmhead_gemm(h, w).float()
+    b = F.linear(h, w).float()
+    torch.testing.assert_close(a, b, atol=1e-3, rtol=2 ** -7)
+    assert float((a != b).float().mean()) < 0.02
+    top2 = b.topk(2, dim=-1).values
+    decisive = (top2[:, 0] - top2[:, 1]) > 2 ** -6 * top2[:, 0].abs().clamp(min=1e-3)
+    assert bool(decisive.any())
+    assert torch.equal(a.argmax(-1)[decisive], b.argmax(-1)[decisive])
