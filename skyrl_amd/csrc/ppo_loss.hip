@@ -189,12 +189,21 @@ __device__ void fold_granules(const unsigned long long* gran, unsigned epoch, in
     fold_finalize<NW>(tot, any_timeout, n, p, s_redd, loss_out, metrics);
 }
 
+__device__ void fold_write(const double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p,
+                           float* __restrict__ loss_out, float* __restrict__ metrics);
+
 // fp64 per-thread totals -> the loss and the metric vector (block tree, thread 0 writes).
 template <int NW>
 __device__ void fold_finalize(double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p, double* s_redd,
                               float* __restrict__ loss_out, float* __restrict__ metrics) {
     block_sum_d<NW, kNP>(tot, s_redd);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) fold_write(tot, any_timeout, n, p, loss_out, metrics);
+}
+
+// the folded sums -> loss and metrics (one thread)
+__device__ void fold_write(const double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p,
+                           float* __restrict__ loss_out, float* __restrict__ metrics) {
+    {
         const double msum = tot[1] > 1.0 ? tot[1] : 1.0;
         float pg = p.loss_reduction == 0 ? (float)(tot[0] / msum) : (float)(tot[0] / (double)n);
         float clip_ratio = (float)(tot[2] / msum);
@@ -871,7 +880,9 @@ using namespace skyrl;
 namespace skyrl {
 int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
 int g_loss_bwd_blocks = 256;
-int g_finish_mode = 0;  // skyrl_tune("finish_mode"): 0 record loads issued with the nb load, 1 after it, 2 probe (no fold)
+int g_finish_mode = 0;  // skyrl_tune("finish_mode"): 0 block tree, 1 nb first, 2 probe (no fold). A one-wave
+                        // fold standing for the 256 threads (no LDS / barrier) measured slower: 4.02 vs
+                        // 3.05 us (profiles/r03_adv_leg_finish_one_wave.log)
 int g_grpo_loss_rpb = 1;  // skyrl_tune("grpo_loss_rpb", 1 / 2): row chunks per fused GRPO+loss block (2 measured slower: 12.1 vs 11.0 us)
   // skyrl_tune("loss_bwd_blocks"): grid cap of the backward rescale
 }

@@ -212,3 +212,23 @@ def test_rows_per_block_variants(dev, rpb):
         test_fused_matches_two_calls_bit_exact(dev, CASES[2])
     finally:
         _ffi.call("skyrl_tune", b"grpo_loss_rpb", 1)
+
+
+@pytest.mark.parametrize("n", [4096, 777])
+def test_deferred_fold_many_records_bit_identical(dev, n):
+    """Many records (several passes of the fold) and a ragged count: the deferred fold gives the
+    in-launch fold's loss and metrics bit for bit."""
+    R = 1024
+    g = torch.Generator().manual_seed(n)
+    lp = (-2 + 0.1 * torch.randn(n, R, generator=g)).to(dev)
+    old = lp + 0.05 * torch.randn(n, R, generator=g).to(dev)
+    ref = lp + 0.05 * torch.randn(n, R, generator=g).to(dev)
+    adv = torch.randn(n, R, generator=g).to(dev)
+    mask = (torch.rand(n, R, generator=g) < 0.8).float().to(dev)
+    rows = mask.sum(-1)
+    params = ppo_utils.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=False)
+    l0, m0 = ops.ppo_loss(lp, old, adv, mask, params, ref, loss_mask_row_sum=rows)
+    x = lp.clone().requires_grad_(True)
+    l1, m1 = ops.ppo_loss(x, old, adv, mask, params, ref, loss_mask_row_sum=rows, defer_fold=True)
+    l1.backward()
+    assert torch.equal(l1.detach(), l0) and torch.equal(m1[:7], m0[:7])
