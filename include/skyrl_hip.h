@@ -43,7 +43,8 @@ const char* skyrl_last_error(void);
  * skyrl_ppo_loss_fwd writing final gradients, in-place skyrl_ppo_loss_bwd, pack emits
  * loss-mask row sums; 4: skyrl_policy_train_fwd takes grad_logits strides; 5: pack emits
  * reward row sums (GRPO scores), skyrl_grpo_advantage / skyrl_grpo_ppo_loss_fwd take them,
- * the loss forwards take flags (SKYRL_LOSS_DEFER_FOLD) and skyrl_ppo_loss_finish). */
+ * the loss forwards take flags (SKYRL_LOSS_DEFER_FOLD) and skyrl_ppo_loss_finish; 6:
+ * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -319,6 +320,21 @@ int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int6
                            float* logp_out, float* entropy_out, void* grad_logits, int64_t gstride_b,
                            int64_t gstride_t, void* workspace,
                            void* stream);
+/* The same pass over a sample-packed batch (the learner's padding-free layout,
+ * model_wrapper.py:272-330 with the lm_head of :308-363): ntok tokens with dense logits rows
+ * (row q at logits + q*ld, bf16, V % 8 == 0, 16-B-aligned rows), labels int64 [ntok], and
+ * token_pos int32 [ntok]: token q's position in the padded [n,R] per-token arrays (old / adv /
+ * loss_mask / ref in, logp_out / entropy_out out; positions no token maps to must have
+ * loss_mask 0 and are left untouched in the outputs). loss / metrics / gradients are those of
+ * skyrl_policy_train_fwd on the padded batch, for every loss reduction; grad_logits rows
+ * [ntok, V] at grad_logits + q*ld_grad. Same workspace query (n, R). */
+int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
+                                  const int64_t* labels, const int32_t* token_pos, int32_t n, int32_t R,
+                                  float temperature, const float* old_log_probs, const float* advantages,
+                                  const float* loss_mask, const float* ref_log_probs,
+                                  const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                                  float* logp_out, float* entropy_out, void* grad_logits, int64_t ld_grad,
+                                  void* workspace, void* stream);
 /* x[i] *= g[0] over a bf16 buffer; a no-op kernel when g[0] == 1. */
 int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream);
 

@@ -75,6 +75,35 @@ def main():
         res["unfused_fwdbwd_ms"] = timeit(unfused_fb, max(2, args.iters // 2))
         h.grad = None
         W.grad = None
+
+        # the training pass with the PPO loss included: (a) chunked lm_head logprob + HIP loss,
+        # (b) whole-V GEMM + the fused policy pass (logprob + entropy + loss + dlogits in one
+        # memory pass, split rows) + the dh / dW GEMMs
+        from skyrl_amd import ppo_utils
+        from skyrl_amd.config import AlgorithmConfig
+
+        params = ppo_utils.ppo_params_from_config(AlgorithmConfig(use_entropy_loss=True), use_kl_loss=False,
+                                                  use_entropy_loss=True, has_entropy=True)
+        old = (-12 + torch.randn(1, T, device=dev))
+        adv = torch.randn(1, T, device=dev)
+        msk = torch.ones(1, T, device=dev)
+
+        def chunked_loss_fb():
+            lp, ent = lmhead.lmhead_logprobs_and_entropy(h, W, lab, 1.0, True, None)
+            loss, _ = ops.ppo_loss(lp.view(1, T), old, adv, msk, params, entropy=ent.view(1, T))
+            loss.backward()
+
+        def policy_train_fb():
+            z = torch.mm(h, W.t())
+            loss, _, _, _ = ops.policy_train(z.view(1, T, V), lab.view(1, T), old, adv, msk, params)
+            loss.backward()
+
+        res["chunked_loss_fwdbwd_ms"] = timeit(chunked_loss_fb, max(2, args.iters // 2))
+        h.grad = None
+        W.grad = None
+        res["policy_train_fwdbwd_ms"] = timeit(policy_train_fb, max(2, args.iters // 2))
+        h.grad = None
+        W.grad = None
         res["addmm_f32"] = lmhead._ADDMM_F32[0]
         res["fused_fwd_TFLOPs"] = fl / res[f"fused_fwd_ms_c{args.chunks[0]}"] / 1e9
         res["peak_mem_GB"] = torch.cuda.max_memory_allocated() / 1e9

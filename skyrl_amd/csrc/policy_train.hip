@@ -522,7 +522,7 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
     const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
     float* __restrict__ tok, uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts,
-    unsigned long long* __restrict__ gran, unsigned* __restrict__ err_word) {
+    unsigned long long* __restrict__ gran, unsigned* __restrict__ err_word, const int32_t* __restrict__ tpos) {
     constexpr int NT = 1024 / P;
     __shared__ St s_st[NT / 64];
     __shared__ float s_g[4];
@@ -530,11 +530,14 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
     // block -> (row, piece): consecutive blocks. (Placing a row's pieces on one XCD, so the
     // exchange stays in that XCD's L2, measured slower: 2.05 vs 1.71 ms per 16 x 1024 tokens,
     // profiles/r03_kbench_split.json; so did longer sleeps between polls, no change.)
-    const int64_t r = blockIdx.x / P;
+    // tpos (ragged launches, skyrl_policy_train_ragged_fwd): token q of the launch has logits row
+    // q (stride st_ / gst) and sits at [n, R] position tpos[q] of the per-token arrays
+    const int64_t q = blockIdx.x / P;
     const int part = blockIdx.x % P;
+    const int64_t r = tpos ? (int64_t)tpos[q] : q;
     const int64_t b = r / R, t = r % R;
-    const uint16_t* row = logits + b * sb + t * st_;
-    uint16_t* out = dx + b * gsb + t * gst;
+    const uint16_t* row = tpos ? logits + q * st_ : logits + b * sb + t * st_;
+    uint16_t* out = tpos ? dx + q * gst : dx + b * gsb + t * gst;
     const int lane = threadIdx.x & 63;
     const int nvec = V >> 3;
     const int per = (nvec + P - 1) / P;  // host: (NV-1)*NT < the last quarter's length, per <= NV*NT
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
     auto tval = [&](float x) { return HAS_T ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
     const unsigned epoch = __hip_atomic_load((const ptr_gu32*)(reinterpret_cast<const unsigned*>(scal) + 16),
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t lab = labels[b * lsb + t * lst];
+    const int64_t lab = tpos ? labels[q * lst] : labels[b * lsb + t * lst];
     const float o_old = old[r];
     const float o_adv = adv[r];
     const float o_m = mask ? mask[r] : 1.f;
@@ -803,7 +806,7 @@ TrainKernel resident_edge_for(int nv, bool has_t) {
 using SplitKernel = void (*)(const uint16_t*, int64_t, int64_t, int, int, const int64_t*, int64_t, int64_t, float,
                              const float*, const float*, const float*, const float*, const float*, const float*,
                              skyrl_ppo_params, float*, float*, float*, uint16_t*, int64_t, int64_t, bool,
-                             unsigned long long*, unsigned*);
+                             unsigned long long*, unsigned*, const int32_t*);
 template <int NV, int P>
 SplitKernel pick_split(bool has_t) {
     return has_t ? policy_train_split_kernel<NV, true, P> : policy_train_split_kernel<NV, false, P>;
@@ -934,7 +937,7 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
                            0, s, in,
                            stride_b, stride_t, R, V, labels, lstride_b, lstride_t, temperature, old_log_probs,
                            advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok,
-                           out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word);
+                           out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word, nullptr);
     } else if (g_train_resident && use768 && aligned) {
         auto kern = has_t ? policy_train_resident_kernel<768, 25, true, false>
                           : policy_train_resident_kernel<768, 25, false, false>;
@@ -954,6 +957,62 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
                        advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok, out,
                        gstride_b, gstride_t, g_train_ntstore != 0);
     rc = check_launch("policy_train_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
+                       loss_out, metrics_out);
+    return check_launch("train_epilogue_kernel");
+}
+
+// Ragged (sample-packed) form: ntok tokens whose logits rows are dense [ntok, V] (row q at
+// logits + q * ld), token q standing at [n, R] position token_pos[q] of the per-token arrays
+// (old / adv / mask / ref / logp_out / entropy_out, all [n, R]); positions no token maps to must
+// carry mask 0 (the padding of a packed batch). Loss, metrics and per-row scales are those of
+// the dense call on the padded [n, R] batch; dlogits rows are [ntok, V] at grad_logits + q * ld_grad.
+// Runs the split-row kernel only (V % 8 == 0, 16-B-aligned rows).
+extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
+                                             const int64_t* labels, const int32_t* token_pos, int32_t n, int32_t R,
+                                             float temperature, const float* old_log_probs, const float* advantages,
+                                             const float* loss_mask, const float* ref_log_probs,
+                                             const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                                             float* logp_out, float* entropy_out, void* grad_logits, int64_t ld_grad,
+                                             void* workspace, void* stream) {
+    SKYRL_REQUIRE(params && logits && labels && token_pos && old_log_probs && advantages && loss_mask && loss_out &&
+                      metrics_out && logp_out && grad_logits && workspace,
+                  "policy_train_ragged_fwd: null pointer");
+    SKYRL_REQUIRE(dtype == SKYRL_BF16, "policy_train_ragged_fwd: logits must be bf16");
+    SKYRL_REQUIRE(ntok > 0 && n > 0 && R > 0 && V > 0 && (int64_t)ntok <= (int64_t)n * R,
+                  "policy_train_ragged_fwd: bad sizes");
+    SKYRL_REQUIRE(temperature > 0.f, "policy_train_ragged_fwd: temperature must be > 0");
+    SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "policy_train_ragged_fwd: use_kl_loss needs ref_log_probs");
+    SKYRL_REQUIRE(params->loss_reduction >= 0 && params->loss_reduction <= 2,
+                  "policy_train_ragged_fwd: bad loss_reduction");
+    SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
+                  "policy_train_ragged_fwd: seq_mean_token_sum_norm needs max_seq_len");
+    const int parts = g_train_split_parts;
+    const int snv = split_nv(V / 8, parts);
+    SKYRL_REQUIRE((V % 8) == 0 && snv > 0, "policy_train_ragged_fwd: needs V % 8 == 0 and V <= 155,648");
+    SKYRL_REQUIRE(ld >= V && ld_grad >= V && (ld % 8) == 0 && (ld_grad % 8) == 0 &&
+                      (reinterpret_cast<uintptr_t>(logits) % 16) == 0 && (reinterpret_cast<uintptr_t>(grad_logits) % 16) == 0,
+                  "policy_train_ragged_fwd: logits / grad rows must be 16-B aligned");
+    SKYRL_REQUIRE((int64_t)ntok * parts < (1ll << 31), "policy_train_ragged_fwd: too many tokens for one launch");
+    char* w = reinterpret_cast<char*>(workspace);
+    float* scal = reinterpret_cast<float*>(w);
+    float* row_scale = reinterpret_cast<float*>(w + 256);
+    float* tok = reinterpret_cast<float*>(w + pt_tok_off(n));
+    auto* gran = reinterpret_cast<unsigned long long*>(w + pt_gran_off(n, R));
+    unsigned* err_word = reinterpret_cast<unsigned*>(w) + 32;
+    hipStream_t s = as_stream(stream);
+    // positions no token maps to are folded by the epilogue with mask 0: their terms must be 0
+    SKYRL_REQUIRE(hipMemsetAsync(tok, 0, (size_t)n * R * 16, s) == hipSuccess, "policy_train_ragged_fwd: memset");
+    hipLaunchKernelGGL(train_scales_kernel, dim3(1), dim3(kThreads), 0, s, loss_mask, n, R, *params, row_scale, scal);
+    int rc = check_launch("train_scales_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(split_for(snv, temperature != 1.0f, parts), dim3((unsigned)((int64_t)ntok * parts)),
+                       dim3(1024 / parts), 0, s, reinterpret_cast<const uint16_t*>(logits), (int64_t)0, ld, R, V,
+                       labels, (int64_t)0, (int64_t)1, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
+                       row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
+                       (int64_t)0, ld_grad, g_train_ntstore != 0, gran, err_word, token_pos);
+    rc = check_launch("policy_train_split_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
                        loss_out, metrics_out);

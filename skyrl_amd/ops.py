@@ -673,6 +673,60 @@ def policy_train(logits, labels, old_log_probs, advantages, loss_mask, params, r
                                      temperature)
 
 
+class PolicyTrainRaggedFunction(torch.autograd.Function):
+    """Packed logits [ntok, V] (the live response tokens of a sample-packed micro-batch) ->
+    (loss, metrics, logp [n,R], entropy [n,R]) with dlogits [ntok, V] from the same pass
+    (skyrl_policy_train_ragged_fwd); `token_pos` maps each token to its [n, R] position."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, token_pos, old_log_probs, advantages, loss_mask, ref_log_probs, params,
+                temperature):
+        dev = _require_gpu(logits, labels, token_pos, old_log_probs, advantages, loss_mask, ref_log_probs)
+        lg = logits.detach()
+        if lg.dtype != torch.bfloat16 or lg.dim() != 2 or lg.stride(1) != 1:
+            raise TypeError("ragged policy pass: logits must be bf16 [ntok, V] with unit vocab stride")
+        ntok, V = lg.shape
+        nb, nt = old_log_probs.shape
+        lab = labels.detach().to(device=dev, dtype=torch.int64).contiguous().view(-1)
+        pos = token_pos.detach().to(device=dev, dtype=torch.int32).contiguous().view(-1)
+        if lab.numel() != ntok or pos.numel() != ntok:
+            raise ValueError(f"labels / token_pos need {ntok} entries, got {lab.numel()} / {pos.numel()}")
+        old = _f32c(old_log_probs.detach(), "old_log_probs")
+        adv = _f32c(advantages.detach(), "advantages")
+        mask = loss_mask.detach().to(torch.float32).contiguous()
+        ref = None if ref_log_probs is None else _f32c(ref_log_probs.detach(), "ref_log_probs")
+        for name, t in (("advantages", adv), ("loss_mask", mask), ("ref_log_probs", ref)):
+            if t is not None and tuple(t.shape) != (nb, nt):
+                raise ValueError(f"{name} shape {tuple(t.shape)} != {(nb, nt)}")
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        metrics = torch.empty(_ffi.M_COUNT, dtype=torch.float32, device=dev)
+        logp = torch.zeros((nb, nt), dtype=torch.float32, device=dev)
+        ent = torch.zeros((nb, nt), dtype=torch.float32, device=dev)
+        dx = torch.empty((ntok, V), dtype=torch.bfloat16, device=dev)
+        ws = WORKSPACES.get(dev, "policy_train", _ffi.query("skyrl_policy_train_workspace_bytes", nb, nt))
+        _ffi.call("skyrl_policy_train_ragged_fwd", _ptr(lg), BF16, lg.stride(0), ntok, V, _ptr(lab), _ptr(pos), nb, nt,
+                  float(temperature), _ptr(old), _ptr(adv), _ptr(mask), _ptr(ref), ctypes.byref(params), _ptr(loss),
+                  _ptr(metrics), _ptr(logp), _ptr(ent), _ptr(dx), dx.stride(0), _ptr(ws), _stream(dev))
+        ctx.save_for_backward(dx)
+        ctx.mark_non_differentiable(metrics, logp, ent)
+        return loss, metrics, logp, ent
+
+    @staticmethod
+    def backward(ctx, g_loss, g_metrics, g_logp, g_ent):
+        (dx,) = ctx.saved_tensors
+        g = g_loss.detach().to(torch.float32).reshape(1).contiguous()
+        _ffi.call("skyrl_scale_bf16_by_device_scalar", _ptr(g), _ptr(dx), dx.numel(), _stream(dx.device))
+        return dx, None, None, None, None, None, None, None, None
+
+
+def policy_train_ragged(logits, labels, token_pos, old_log_probs, advantages, loss_mask, params,
+                        ref_log_probs=None, temperature: float = 1.0):
+    """Fused policy pass over packed tokens (see PolicyTrainRaggedFunction); returns
+    (loss 0-d, metrics [8], logp [n,R], entropy [n,R]); positions no token maps to read 0."""
+    return PolicyTrainRaggedFunction.apply(logits, labels, token_pos, old_log_probs, advantages, loss_mask,
+                                           ref_log_probs, params, temperature)
+
+
 # ---------------------------------------------------------------------------- a1 sampler
 def sample(
     logits: torch.Tensor,

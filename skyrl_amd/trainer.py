@@ -48,6 +48,11 @@ class TrainerConfig:
     # one HIP clip + AdamW pass that also writes the engine's bf16 weights); "torch": torch.optim.AdamW
     # + clip_grad_norm_ + bucketed all-reduce (the A/B reference)
     optimizer: str = "hip"
+    # policy micro-batches through ONE fused memory pass over the lm_head logits (logprob +
+    # entropy + PPO/KL loss + dlogits, ops.policy_train_ragged) between the lm_head GEMM and its
+    # backward GEMMs, instead of the chunked lm_head logprob + loss + chunk recompute (falls back
+    # for V % 8 != 0 or V > 155,648, and for loss types other than regular / dual_clip)
+    fused_policy_pass: bool = True
     sampling_params: Dict[str, Any] = field(default_factory=lambda: {"max_tokens": 1024, "min_tokens": 1})
     algorithm: AlgorithmConfig = field(default_factory=AlgorithmConfig)
 
@@ -325,10 +330,13 @@ class GRPOTrainer:
                 mets = []
                 for i in range(s0, s1, mb):
                     j = min(i + mb, s1)
-                    lp, ent = self._logprobs(self.policy, data["sequences"][i:j], data["attention_mask"][i:j], R,
-                                             grad=True)
                     ref = data["base_action_log_probs"][i:j] if self.ref is not None else None
-                    loss, met = self._loss(lp, data, i, j, ref, ent)
+                    if self._fused_pass_ok():
+                        loss, met = self._fused_policy_pass(data, i, j, R, ref)
+                    else:
+                        lp, ent = self._logprobs(self.policy, data["sequences"][i:j], data["attention_mask"][i:j],
+                                                 R, grad=True)
+                        loss, met = self._loss(lp, data, i, j, ref, ent)
                     if self.optim is not None:
                         if j == s1:
                             self.optim.arm()  # the last micro-batch: buckets reduce-scatter during its backward
@@ -358,6 +366,39 @@ class GRPOTrainer:
                     acc.setdefault(k, []).append(v)
         return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
                                        device=next(self.policy.parameters()).device)
+
+    def _fused_pass_ok(self) -> bool:
+        if not self.cfg.fused_policy_pass or self.cfg.algorithm.policy_loss_type not in ("regular", "dual_clip"):
+            return False
+        V = self.policy.get_output_embeddings().weight.shape[0]
+        return V % 8 == 0 and V <= 155648
+
+    def _fused_policy_pass(self, data, i, j, R, ref):
+        """The micro-batch's policy forward + loss with the lm_head logits feeding one fused pass:
+        hidden states of the live response tokens (packed), z = h W^T (bf16, the reference's
+        lm_head under autocast, model_wrapper.py:308-363), then ops.policy_train_ragged computes
+        logprob, entropy, the PPO/KL/entropy loss (worker.py:801-876) and dL/dz in one read of z;
+        autograd's lm_head backward takes dL/dz into the dh / dW GEMMs. Same loss, metrics and
+        gradients as _logprobs + _loss (tests/test_gpu_trainer_e2e.py)."""
+        from . import ops
+
+        seq, att = data["sequences"][i:j], data["attention_mask"][i:j]
+        model = self.policy
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            base = model.base_model
+            if self.cfg.use_sample_packing:
+                h = packed_hidden_states(base, seq, att, R).to(torch.bfloat16)
+            else:
+                hidden = base(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
+                h = hidden[:, -R - 1:-1].to(torch.bfloat16)
+            w = model.get_output_embeddings().weight.to(torch.bfloat16)
+            live = att[:, -R:].bool()
+            z = torch.matmul(h[live], w.t())  # [live tokens, V] bf16
+        pos = torch.nonzero(live.reshape(-1)).reshape(-1).to(torch.int32)
+        loss, met, _, _ = ops.policy_train_ragged(z, seq[:, -R:][live], pos, data["action_log_probs"][i:j],
+                                                  data["advantages"][i:j], data["loss_mask"][i:j], self.loss_params,
+                                                  ref_log_probs=ref, temperature=self.cfg.temperature)
+        return loss, met
 
     def _fused_grpo_group_size(self, data) -> int:
         """G when the loss may compute GRPO itself (ops.grpo_ppo_loss): the grpo estimator on the

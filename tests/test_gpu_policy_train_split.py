@@ -90,3 +90,37 @@ def test_split_matches_resident_at_metric_vocab(dev, temp):
     diff = (split[4] != res[4]).float().mean().item()
     assert diff < 0.01, diff
     assert float(split[1][6]) == 0.0
+
+
+@pytest.mark.parametrize("V", [512, 151936])
+@pytest.mark.parametrize("red", [0, 1, 2])
+def test_ragged_matches_dense_on_padded_batch(dev, V, red):
+    """skyrl_policy_train_ragged_fwd on the live tokens of a ragged batch == skyrl_policy_train_fwd
+    on the padded batch (dead positions: loss mask 0, arbitrary logits): loss and metrics bit for
+    bit under every loss reduction, logp / entropy at the live positions, and the live rows'
+    dlogits; the dead positions of logp / entropy stay 0."""
+    n, R = 4, 24
+    g = torch.Generator().manual_seed(V + red)
+    lens = torch.tensor([24, 1, 13, 7])
+    live = torch.arange(R)[None] < lens[:, None]
+    logits = (torch.randn(n, R, V, generator=g) * 3).to(torch.bfloat16).to(dev)
+    labels = torch.randint(0, V, (n, R), generator=g).to(dev)
+    old = (-6 + torch.randn(n, R, generator=g)).to(dev)
+    adv = torch.randn(n, R, generator=g).to(dev)
+    ref = (-6 + torch.randn(n, R, generator=g)).to(dev)
+    mask = (live & (torch.rand(n, R, generator=g) < 0.9)).float().to(dev)
+    cfg = AlgorithmConfig(use_entropy_loss=True, policy_loss_type="dual_clip", loss_reduction=
+                          ("token_mean", "sequence_mean", "seq_mean_token_sum_norm")[red], max_seq_len=R)
+    params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=True, has_entropy=True)
+    x = logits.clone().requires_grad_(True)
+    loss_d, m_d, lp_d, ent_d = ops.policy_train(x, labels, old, adv, mask, params, ref_log_probs=ref)
+    loss_d.backward()
+    lv = live.to(dev)
+    z = logits[lv].contiguous().requires_grad_(True)
+    pos = torch.nonzero(lv.reshape(-1)).reshape(-1).to(torch.int32)
+    loss_r, m_r, lp_r, ent_r = ops.policy_train_ragged(z, labels[lv], pos, old, adv, mask, params, ref_log_probs=ref)
+    loss_r.backward()
+    assert torch.equal(loss_r, loss_d) and torch.equal(m_r[:7], m_d[:7])
+    assert torch.equal(lp_r[lv], lp_d[lv]) and torch.equal(ent_r[lv], ent_d[lv])
+    assert not lp_r[~lv].any() and not ent_r[~lv].any()
+    assert torch.equal(z.grad, x.grad[lv])
