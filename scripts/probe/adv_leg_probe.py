@@ -25,7 +25,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "nt":  # non-temporal dlogp stores x fin
     _ffi.call("skyrl_tune", b"loss_bwd_blocks", 256)
     sys.exit(0)
 for rep in range(2):
-    for mode in (0, 1, 2):
+    for mode in (0, 2, 3, 4):
         for blocks in (256,):
             _ffi.call("skyrl_tune", b"finish_mode", mode)
             _ffi.call("skyrl_tune", b"loss_bwd_blocks", blocks)

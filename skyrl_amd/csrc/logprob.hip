@@ -277,7 +277,7 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "finish_mode") {
-        SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: finish_mode must be 0, 1 or 2");
+        SKYRL_REQUIRE(value >= 0 && value <= 4, "skyrl_tune: finish_mode must be in [0, 4]");
         g_finish_mode = value;
         return SKYRL_OK;
     }

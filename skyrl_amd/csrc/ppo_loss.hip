@@ -43,18 +43,21 @@ constexpr int kNP = 5;                // partials: sum l*m, m, clip*m, kl*m*m, e
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
-// compute_approx_kl on one element (before the mask multiply).
+// compute_approx_kl on one element (before the mask multiply). Branch-free: every estimator is
+// evaluated and the uniform kl_type selects one, so a token's code is one basic block and the
+// compiler can interleave the tokens of a thread (a switch split each token into blocks that
+// serialised them). Same operations on the same inputs as the switch: identical bits.
 __device__ __forceinline__ float approx_kl(float lp, float base, int kl_type) {
-    switch (kl_type) {
-        case 0: return lp - base;
-        case 1: return fabsf(lp - base);
-        case 2: { float d = lp - base; return 0.5f * (d * d); }
-        default: {
-            float kl = clampf(base - lp, -20.f, 20.f);
-            float r = expf(kl);
-            return clampf((r - kl) - 1.f, -10.f, 10.f);
-        }
-    }
+    // every operand computed first: a conditional operator over plain values becomes a select,
+    // one over expressions (or a call) becomes branches that serialise the thread's tokens
+    const float d = lp - base;
+    const float k1a = fabsf(d);
+    const float k2 = 0.5f * (d * d);
+    const float k3x = clampf(base - lp, -20.f, 20.f);
+    const float k3 = clampf((expf(k3x) - k3x) - 1.f, -10.f, 10.f);
+    const float k23 = kl_type == 2 ? k2 : k3;
+    const float k123 = kl_type == 1 ? k1a : k23;
+    return kl_type == 0 ? d : k123;
 }
 
 struct TokenOut {
@@ -73,30 +76,25 @@ __device__ __forceinline__ TokenOut ppo_token(float lp, float old, float A, floa
     const float rc = clampf(ratio, lo, hi);
     const float surr2 = rc * A;
     const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-    float loss1, d1;  // loss1 = -min(surr1, surr2); d1 = d loss1 / d ratio
-    if (surr1 < surr2) {
-        loss1 = -surr1;
-        d1 = -A;
-    } else if (surr2 < surr1) {
-        loss1 = -surr2;
-        d1 = -A * inr;
-    } else {  // tie: torch.min splits the gradient in half
-        loss1 = -surr1;
-        d1 = -(0.5f * A + 0.5f * A * inr);
-    }
+    // Branch-free (selects only, so the tokens of a thread interleave; divergent if / else here
+    // serialised them): loss1 = -min(surr1, surr2), d1 = d loss1 / d ratio, a tie splitting the
+    // gradient in half as torch.min does; the same operations as the branchy form.
+    const bool lt = surr1 < surr2, gt = surr2 < surr1;
+    const float ns1 = -surr1, ns2 = -surr2;
+    const float loss1 = gt ? ns2 : ns1;
+    const float d_lt = -A, d_gt = -A * inr, d_tie = -(0.5f * A + 0.5f * A * inr);
+    const float d_ge = gt ? d_gt : d_tie;
+    const float d1 = lt ? d_lt : d_ge;
     TokenOut o;
-    o.clip = (-surr2 > -surr1) ? 1.f : 0.f;
-    o.loss = loss1;
-    float d = d1;
-    if (dual_clip && A < 0.f) {
-        const float pg3 = -A * c;
-        if (pg3 < loss1) {
-            o.loss = pg3;
-            d = 0.f;
-        } else if (loss1 == pg3) {
-            d = 0.5f * d1;
-        }
-    }
+    o.clip = (ns2 > ns1) ? 1.f : 0.f;
+    const float pg3 = -A * c;
+    const bool neg = dual_clip && A < 0.f;
+    const bool take3 = neg && pg3 < loss1;
+    const bool tie3 = neg && !(pg3 < loss1) && loss1 == pg3;
+    o.loss = take3 ? pg3 : loss1;
+    const float half_d1 = 0.5f * d1;
+    const float d_nt = tie3 ? half_d1 : d1;
+    const float d = take3 ? 0.f : d_nt;
     o.dldlp = d * dratio;
     return o;
 }
@@ -266,6 +264,15 @@ __global__ __launch_bounds__(kThreads) void loss_finish_kernel(const float* __re
 #pragma unroll
                 for (int k = 0; k < kNP; ++k) tot[k] += (double)parts[(int64_t)k * units + b];
         }
+        if (mode == 3) {  // timing probe only: no block reduction (thread 0's own sums)
+            if (threadIdx.x == 0) fold_write(tot, 0, n, p, loss_out, metrics);
+            return;
+        }
+        if (mode == 4) {  // timing probe only: block reduction, raw sums written (no divisions)
+            block_sum_d<kFW, kNP>(tot, s_redd);
+            if (threadIdx.x < kNP) metrics[threadIdx.x] = (float)tot[threadIdx.x];
+            return;
+        }
         fold_finalize<kFW>(tot, 0, n, p, s_redd, loss_out, metrics);
         return;
     }
@@ -417,7 +424,10 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
         if (unit >= units) break;
         const int row = row_u[u];
         const double mr = (double)mrow_u[u];
-        const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
+        // 1 / max(mrow, 1) in fp32: the correctly rounded fp32 quotient equals the fp64 one
+        // rounded to fp32 (53 >= 2 * 24 + 2: double rounding is innocuous for division), so the
+        // bits are those of (float)(1.0 / mr) without the fp64 division on the critical path
+        const float inv_mrow = 1.f / (mrow_u[u] > 1.f ? mrow_u[u] : 1.f);
         float scale, w;  // gradient scale; weight of the row's l*m in the pg sum
         if (p.loss_reduction == 0) { scale = tok_scale; w = 1.f; }
         else if (p.loss_reduction == 1) { scale = (float)(1.0 / ((double)n * (mr > 1.0 ? mr : 1.0))); w = inv_mrow; }
@@ -428,7 +438,8 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_grad_kernel(
             a[0] += t.loss * M;
             a[1] += M;
             a[2] += t.clip * M;
-            if (p.use_kl_loss) a[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
+            const float klm = (approx_kl(L, RF, p.kl_type) * M) * M;
+            a[3] += p.use_kl_loss ? klm : 0.f;
             a[4] += E * M;
             return (t.dldlp * M) * scale;
         };
@@ -678,7 +689,7 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
     if (live) {
         if (adv_out) *reinterpret_cast<float4*>(adv_out + e) = a4;
         const double mr = (double)mrow_in;
-        const float inv_mrow = (float)(1.0 / (mr > 1.0 ? mr : 1.0));
+        const float inv_mrow = 1.f / (mrow_in > 1.f ? mrow_in : 1.f);  // = (float)(1.0 / mr), see above
         float scale, w;
         if (p.loss_reduction == 0) { scale = tok_scale; w = 1.f; }
         else if (p.loss_reduction == 1) { scale = (float)(1.0 / ((double)n * (mr > 1.0 ? mr : 1.0))); w = inv_mrow; }
@@ -695,7 +706,8 @@ __global__ __launch_bounds__(kThreads * RPB) void grpo_loss_grad_kernel(
             a[0] += t.loss * M;
             a[1] += M;
             a[2] += t.clip * M;
-            if (p.use_kl_loss) a[3] += (approx_kl(L, RF, p.kl_type) * M) * M;
+            const float klm = (approx_kl(L, RF, p.kl_type) * M) * M;
+            a[3] += p.use_kl_loss ? klm : 0.f;
             a[4] += E * M;
             return (t.dldlp * M) * scale;
 #endif
