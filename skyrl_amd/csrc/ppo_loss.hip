@@ -190,12 +190,32 @@ __device__ void fold_granules(const unsigned long long* gran, unsigned epoch, in
 __device__ void fold_write(const double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p,
                            float* __restrict__ loss_out, float* __restrict__ metrics);
 
-// fp64 per-thread totals -> the loss and the metric vector (block tree, thread 0 writes).
+// fp64 per-thread totals -> the loss and the metric vector: each wave's DPP tree
+// (wave_sum_dpp), the NW wave sums added in wave order by thread 0, which writes. Every fold of
+// the loss records (in-launch, deferred finish, no-grad) goes through here, so they agree bit
+// for bit. s_redd: NW * kNP doubles.
 template <int NW>
 __device__ void fold_finalize(double (&tot)[kNP], int any_timeout, int n, const skyrl_ppo_params& p, double* s_redd,
                               float* __restrict__ loss_out, float* __restrict__ metrics) {
-    block_sum_d<NW, kNP>(tot, s_redd);
-    if (threadIdx.x == 0) fold_write(tot, any_timeout, n, p, loss_out, metrics);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    double ws[kNP];
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) ws[k] = wave_sum_dpp(tot[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < kNP; ++k) s_redd[w * kNP + k] = ws[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t[kNP];
+#pragma unroll
+        for (int k = 0; k < kNP; ++k) {
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < NW; ++j) acc += s_redd[j * kNP + k];
+            t[k] = acc;
+        }
+        fold_write(t, any_timeout, n, p, loss_out, metrics);
+    }
 }
 
 // the folded sums -> loss and metrics (one thread)
