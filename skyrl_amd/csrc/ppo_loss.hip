@@ -912,7 +912,8 @@ using namespace skyrl;
 namespace skyrl {
 int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
 int g_loss_bwd_blocks = 256;
-int g_finish_mode = 0;  // skyrl_tune("finish_mode"): 0 block tree, 1 nb first, 2 probe (no fold). A one-wave
+int g_finish_mode = 0;  // skyrl_tune("finish_mode"): 0 block tree, 1 nb first; timing probes (wrong values):
+                        // 2 no fold, 3 no block reduction, 4 no divisions. A one-wave
                         // fold standing for the 256 threads (no LDS / barrier) measured slower: 4.02 vs
                         // 3.05 us (profiles/r03_adv_leg_finish_one_wave.log)
 int g_grpo_loss_rpb = 1;  // skyrl_tune("grpo_loss_rpb", 1 / 2): row chunks per fused GRPO+loss block (2 measured slower: 12.1 vs 11.0 us)
