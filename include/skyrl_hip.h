@@ -327,7 +327,8 @@ int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int6
                            void* stream);
 /* The same pass over a sample-packed batch (the learner's padding-free layout,
  * model_wrapper.py:272-330 with the lm_head of :308-363): ntok tokens with dense logits rows
- * (row q at logits + q*ld, bf16, V % 8 == 0, 16-B-aligned rows), labels int64 [ntok], and
+ * (row q at logits + q*ld, bf16; V <= 155,648, or <= 114,688 when V % 8 != 0 or rows are not
+ * 16-B aligned; each grad_logits row at its logits row's offset within 16 B), labels int64 [ntok], and
  * token_pos int32 [ntok]: token q's position in the padded [n,R] per-token arrays (old / adv /
  * loss_mask / ref in, logp_out / entropy_out out; positions no token maps to must have
  * loss_mask 0 and are left untouched in the outputs). loss / metrics / gradients are those of

@@ -165,6 +165,48 @@ def main():
             ms = statistics.median(t)
             res[f"policy_train_fused_mb{m}"] = {"ms_per_16_seqs": ms, "GBps_hbm_algorithmic": rows * (V * 4 + 40) / ms / 1e6}
 
+    if on("fused_vocab"):  # split pieces per row vs vocabulary (odd V = 50,257: EDGE forms)
+        from skyrl_amd import ppo_utils as pu
+        import ctypes
+
+        params = pu.ppo_params_from_config(AlgorithmConfig(), use_kl_loss=True, has_entropy=True)
+        old = torch.randn((mb, R), device=dev, generator=gen) - 10
+        adv = torch.randn((mb, R), device=dev, generator=gen)
+        msk = torch.ones((mb, R), device=dev)
+        ref = old + 0.01
+        loss = torch.empty((), device=dev)
+        met = torch.empty(8, device=dev)
+        ws = torch.zeros(_ffi.query("skyrl_policy_train_workspace_bytes", mb, R), dtype=torch.uint8, device=dev)
+        del logits
+        for V2 in (50257, 50264, 128256, 151936):
+            lab2 = torch.randint(0, V2, (mb, R), device=dev, generator=gen)
+            g2 = [torch.empty((mb, R, V2), dtype=torch.bfloat16, device=dev).normal_(0, 3, generator=gen)
+                  for _ in range(2)]
+            d2 = torch.empty((mb, R, V2), dtype=torch.bfloat16, device=dev)
+
+            def fused2(x):
+                _ffi.call("skyrl_policy_train_fwd", ops._ptr(x), _ffi.BF16, x.stride(0), x.stride(1), mb, R, V2,
+                          ops._ptr(lab2), lab2.stride(0), lab2.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
+                          ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met),
+                          ops._ptr(lp), ops._ptr(ent), ops._ptr(d2), R * V2, V2, ops._ptr(ws), st)
+            variants = [(1, 8), (1, 4), (1, 2), (0, 8)]  # (split, parts); split 0 = the resident kernel
+            times = {v: [] for v in variants}
+            for _ in range(args.rounds):
+                for v in variants:
+                    _ffi.call("skyrl_tune", b"train_split", v[0])
+                    _ffi.call("skyrl_tune", b"train_split_parts", v[1])
+                    times[v].append(timeit(lambda: (fused2(g2[0]), fused2(g2[1]))) / 2)
+            _ffi.call("skyrl_tune", b"train_split", 1)
+            _ffi.call("skyrl_tune", b"train_split_parts", 8)
+            for (split, parts), t in times.items():
+                ms = statistics.median(t)
+                res[f"policy_train_V{V2}_split{split}_parts{parts}"] = {
+                    "ms": ms, "GBps_hbm_algorithmic": rows * (V2 * 4 + 40) / ms / 1e6}
+            del g2, d2
+            torch.cuda.empty_cache()
+        print(json.dumps(res, indent=1))
+        return
+
     if on("sample"):
         from skyrl_amd.config import SamplingParams
         from skyrl_amd.sampler import TokenSampler

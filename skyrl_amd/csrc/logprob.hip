@@ -234,7 +234,7 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "train_split_parts") {
-        SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: train_split_parts must be 4 or 8");
+        SKYRL_REQUIRE(value == 2 || value == 4 || value == 8, "skyrl_tune: train_split_parts must be 2, 4 or 8");
         g_train_split_parts = value;
         return SKYRL_OK;
     }

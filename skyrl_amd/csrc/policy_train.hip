@@ -515,8 +515,8 @@ constexpr unsigned kSplitMaxPolls = 1u << 20;
 typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
 typedef __attribute__((address_space(1))) unsigned ptr_gu32;
 
-template <int NV, bool HAS_T, int P = kSplitP>
-__global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_kernel(
+template <int NV, bool HAS_T, int P = kSplitP, bool EDGE = false>
+__global__ __launch_bounds__(1024 / P, P == 8 ? 3 : (P == 4 ? 4 : 2)) void policy_train_split_kernel(
     const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int V, const int64_t* __restrict__ labels,
     int64_t lsb, int64_t lst, float temp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
@@ -539,11 +539,16 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
     const uint16_t* row = tpos ? logits + q * st_ : logits + b * sb + t * st_;
     uint16_t* out = tpos ? dx + q * gst : dx + b * gsb + t * gst;
     const int lane = threadIdx.x & 63;
-    const int nvec = V >> 3;
-    const int per = (nvec + P - 1) / P;  // host: (NV-1)*NT < the last quarter's length, per <= NV*NT
+    // EDGE: rows not 16-B aligned or V % 8 != 0 (GPT-2's 50,257): the row's aligned-down span
+    // (h slots before it) is what is cut into pieces; its first and last vectors are partial
+    const int h = EDGE ? (int)((reinterpret_cast<uintptr_t>(row) >> 1) & 7) : 0;
+    const int nvec = EDGE ? (h + V + 7) >> 3 : V >> 3;
+    // host (split_nv / split_nv_edge): per <= NV*NT, every piece non-empty, and without EDGE
+    // (NV-1)*NT < the last piece's length
+    const int per = (nvec + P - 1) / P;
     const int lo = part * per;
     const int hi = min(nvec, lo + per);
-    const uint4* rv = reinterpret_cast<const uint4*>(row) + lo;
+    const uint4* rv = reinterpret_cast<const uint4*>(row - h) + lo;
     auto tval = [&](float x) { return HAS_T ? bf16_to_f32(f32_to_bf16(x / temp)) : x; };
     const unsigned epoch = __hip_atomic_load((const ptr_gu32*)(reinterpret_cast<const unsigned*>(scal) + 16),
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -558,14 +563,39 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
     if (threadIdx.x == 0) xl = (lab >= 0 && lab < V) ? bf16_to_f32(row[lab]) : __builtin_nanf("");
     constexpr uint32_t kNinf2 = 0xff80ff80u;
     uint4 v[NV];
-#pragma unroll
-    for (int k = 0; k < NV - 1; ++k) v[k] = ld_nt(rv + threadIdx.x + k * NT);
     const int nq = hi - lo;
-    {
+    if constexpr (!EDGE) {
+#pragma unroll
+        for (int k = 0; k < NV - 1; ++k) v[k] = ld_nt(rv + threadIdx.x + k * NT);
         const int idx = threadIdx.x + (NV - 1) * NT;
         const bool ok = idx < nq;
         const uint4 t4 = ld_nt(rv + (ok ? idx : nq - 1));
         v[NV - 1] = make_uint4(ok ? t4.x : kNinf2, ok ? t4.y : kNinf2, ok ? t4.z : kNinf2, ok ? t4.w : kNinf2);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int idx = threadIdx.x + k * NT;
+            const bool ok = idx < nq;
+            const uint4 t4 = ld_nt(rv + (ok ? idx : 0));
+            v[k] = make_uint4(ok ? t4.x : kNinf2, ok ? t4.y : kNinf2, ok ? t4.z : kNinf2, ok ? t4.w : kNinf2);
+        }
+        // the span's first and last vectors hold slots of the neighbouring rows: -inf them
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int idx = threadIdx.x + k * NT;
+            const int sl = h - 8 * (lo + idx), sh = V + h - 8 * (lo + idx);  // own slots: sl <= j < sh
+            if (idx < nq && (sl > 0 || sh < 8)) {
+                uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (j < sl || j >= sh) {
+                        const uint32_t keep = (j & 1) ? 0x0000ffffu : 0xffff0000u;
+                        w[j >> 1] = (w[j >> 1] & keep) | (kNinf2 & ~keep);
+                    }
+                }
+                v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
     }
     St st{-3.402823466e38f, 0.f, 0.f};
 #pragma unroll
@@ -642,15 +672,15 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
     }
     __syncthreads();
     const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
-    const int lab_s = (lab >= 0 && lab < V) ? (int)lab - 8 * lo : -1;  // label's slot in this quarter
+    const int lab_s = (lab >= 0 && lab < V) ? (int)lab + h - 8 * lo : -1;  // label's slot in this piece
 #pragma unroll
     for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
     const float inv_t = HAS_T ? 1.f / temp : 1.f;
-    uint4* ov = reinterpret_cast<uint4*>(out) + lo;
+    uint4* ov = reinterpret_cast<uint4*>(out - h) + lo;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int idx = threadIdx.x + k * NT;
-        if (k < NV - 1 || idx < nq) {
+        if ((!EDGE && k < NV - 1) || idx < nq) {
             float x[8];
             unpack8(v[k], x);
             const int v0 = idx * 8;
@@ -662,8 +692,16 @@ __global__ __launch_bounds__(1024 / P, P == 4 ? 4 : 3) void policy_train_split_k
                 if (v0 + j == lab_s) gg += glp;
                 x[j] = HAS_T ? gg * inv_t : gg;
             }
-            st_out(ov + idx, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
-                                        pack_bf16x2(x[6], x[7])), nts);
+            const int sl = h - 8 * (lo + idx), sh = V + h - 8 * (lo + idx);
+            if (!EDGE || (sl <= 0 && sh >= 8)) {
+                st_out(ov + idx, make_uint4(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
+                                            pack_bf16x2(x[4], x[5]), pack_bf16x2(x[6], x[7])), nts);
+            } else {  // the span's first / last vector: only this row's slots
+                uint16_t* o16 = reinterpret_cast<uint16_t*>(ov + idx);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j >= sl && j < sh) o16[j] = f32_to_bf16(x[j]);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -836,7 +874,45 @@ SplitKernel split_for_p(int nv, bool has_t) {
     }
 }
 SplitKernel split_for(int nv, bool has_t, int parts) {
-    return parts == 8 ? split_for_p<8>(nv, has_t) : split_for_p<4>(nv, has_t);
+    return parts == 8 ? split_for_p<8>(nv, has_t) : parts == 4 ? split_for_p<4>(nv, has_t) : split_for_p<2>(nv, has_t);
+}
+// rows with partial vectors: the smallest listed NV covering a piece (as kEdgeNV, the edge
+// logic costs VGPRs; NV <= 14 covers V <= 114,688)
+constexpr int kSplitEdgeNV[] = {1, 2, 4, 7, 10, 14};
+template <int NV, int P>
+SplitKernel pick_split_edge(bool has_t) {
+    return has_t ? policy_train_split_kernel<NV, true, P, true> : policy_train_split_kernel<NV, false, P, true>;
+}
+template <int P>
+SplitKernel split_edge_for_p(int nv, bool has_t) {
+    switch (nv) {
+        case 1: return pick_split_edge<1, P>(has_t);
+        case 2: return pick_split_edge<2, P>(has_t);
+        case 4: return pick_split_edge<4, P>(has_t);
+        case 7: return pick_split_edge<7, P>(has_t);
+        case 10: return pick_split_edge<10, P>(has_t);
+        default: return pick_split_edge<14, P>(has_t);
+    }
+}
+SplitKernel split_edge_for(int nv, bool has_t, int parts) {
+    return parts == 8 ? split_edge_for_p<8>(nv, has_t)
+                      : parts == 4 ? split_edge_for_p<4>(nv, has_t) : split_edge_for_p<2>(nv, has_t);
+}
+// EDGE layout: a row's span is (h + V + 7) / 8 vectors for its offset h = 0..7 within 16 B, so
+// two span lengths occur; both must give pieces of at most NV*NT vectors and a non-empty last
+// piece. Returns the listed NV, or 0.
+int split_nv_edge(int V, int parts) {
+    const int nt = 1024 / parts;
+    const int spans[2] = {(V + 7) / 8, (V + 14) / 8};
+    int need = 0;
+    for (int nvec : spans) {
+        const int per = (nvec + parts - 1) / parts;
+        if (nvec - (parts - 1) * per < 1) return 0;
+        need = max(need, (per + nt - 1) / nt);
+    }
+    for (int cand : kSplitEdgeNV)
+        if (need <= cand) return cand;
+    return 0;
 }
 // the split kernel's vectors per thread for nvec row vectors cut into `parts` pieces of
 // 1024 / parts threads, or 0 if its layout does not fit: pieces of per = ceil(nvec / parts)
@@ -931,9 +1007,9 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
     }
     const bool resident_ok = g_train_resident && same_align && nv > 0;
     const int parts = g_train_split_parts;
-    const int snv = aligned ? split_nv(nvec, parts) : 0;
+    const int snv = aligned ? split_nv(nvec, parts) : split_nv_edge(V, parts);
     if (g_train_split && g_train_resident && same_align && snv > 0 && (int64_t)n * R * parts < (1ll << 31)) {
-        hipLaunchKernelGGL(split_for(snv, has_t, parts), dim3((unsigned)((int64_t)n * R * parts)), dim3(1024 / parts),
+        hipLaunchKernelGGL(aligned ? split_for(snv, has_t, parts) : split_edge_for(snv, has_t, parts), dim3((unsigned)((int64_t)n * R * parts)), dim3(1024 / parts),
                            0, s, in,
                            stride_b, stride_t, R, V, labels, lstride_b, lstride_t, temperature, old_log_probs,
                            advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok,
@@ -968,7 +1044,7 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
 // (old / adv / mask / ref / logp_out / entropy_out, all [n, R]); positions no token maps to must
 // carry mask 0 (the padding of a packed batch). Loss, metrics and per-row scales are those of
 // the dense call on the padded [n, R] batch; dlogits rows are [ntok, V] at grad_logits + q * ld_grad.
-// Runs the split-row kernel only (V % 8 == 0, 16-B-aligned rows).
+// Runs the split-row kernel only (its EDGE form for rows not 16-B aligned or V % 8 != 0).
 extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
                                              const int64_t* labels, const int32_t* token_pos, int32_t n, int32_t R,
                                              float temperature, const float* old_log_probs, const float* advantages,
@@ -989,11 +1065,15 @@ extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int6
     SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
                   "policy_train_ragged_fwd: seq_mean_token_sum_norm needs max_seq_len");
     const int parts = g_train_split_parts;
-    const int snv = split_nv(V / 8, parts);
-    SKYRL_REQUIRE((V % 8) == 0 && snv > 0, "policy_train_ragged_fwd: needs V % 8 == 0 and V <= 155,648");
-    SKYRL_REQUIRE(ld >= V && ld_grad >= V && (ld % 8) == 0 && (ld_grad % 8) == 0 &&
-                      (reinterpret_cast<uintptr_t>(logits) % 16) == 0 && (reinterpret_cast<uintptr_t>(grad_logits) % 16) == 0,
-                  "policy_train_ragged_fwd: logits / grad rows must be 16-B aligned");
+    const auto lgp = reinterpret_cast<uintptr_t>(logits), grp = reinterpret_cast<uintptr_t>(grad_logits);
+    // rows without partial vectors take the plain split kernel, others (GPT-2's odd V) its EDGE
+    // form; either way every dlogits row must sit at its logits row's offset within 16 B
+    const bool aligned = (V % 8) == 0 && (ld % 8) == 0 && (ld_grad % 8) == 0 && lgp % 16 == 0 && grp % 16 == 0;
+    const int snv = aligned ? split_nv(V / 8, parts) : split_nv_edge(V, parts);
+    SKYRL_REQUIRE(snv > 0, "policy_train_ragged_fwd: V outside the split kernel's range (V <= 155,648, or "
+                           "114,688 for rows not 16-B aligned)");
+    SKYRL_REQUIRE(ld >= V && ld_grad >= V && lgp % 2 == 0 && (grp - lgp) % 16 == 0 && (ld_grad - ld) % 8 == 0,
+                  "policy_train_ragged_fwd: dlogits rows must share the logits rows' offset within 16 B");
     SKYRL_REQUIRE((int64_t)ntok * parts < (1ll << 31), "policy_train_ragged_fwd: too many tokens for one launch");
     char* w = reinterpret_cast<char*>(workspace);
     float* scal = reinterpret_cast<float*>(w);
@@ -1007,7 +1087,8 @@ extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int6
     hipLaunchKernelGGL(train_scales_kernel, dim3(1), dim3(kThreads), 0, s, loss_mask, n, R, *params, row_scale, scal);
     int rc = check_launch("train_scales_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(split_for(snv, temperature != 1.0f, parts), dim3((unsigned)((int64_t)ntok * parts)),
+    hipLaunchKernelGGL(aligned ? split_for(snv, temperature != 1.0f, parts) : split_edge_for(snv, temperature != 1.0f, parts),
+                       dim3((unsigned)((int64_t)ntok * parts)),
                        dim3(1024 / parts), 0, s, reinterpret_cast<const uint16_t*>(logits), (int64_t)0, ld, R, V,
                        labels, (int64_t)0, (int64_t)1, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
                        row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),

@@ -371,7 +371,7 @@ class GRPOTrainer:
         if not self.cfg.fused_policy_pass or self.cfg.algorithm.policy_loss_type not in ("regular", "dual_clip"):
             return False
         V = self.policy.get_output_embeddings().weight.shape[0]
-        return V % 8 == 0 and V <= 155648
+        return V <= (155648 if V % 8 == 0 else 114688)  # the split kernel's range (policy_train.hip)
 
     def _fused_policy_pass(self, data, i, j, R, ref):
         """The micro-batch's policy forward + loss with the lm_head logits feeding one fused pass:

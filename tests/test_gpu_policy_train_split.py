@@ -92,13 +92,15 @@ def test_split_matches_resident_at_metric_vocab(dev, temp):
     assert float(split[1][6]) == 0.0
 
 
-@pytest.mark.parametrize("V", [512, 151936])
+@pytest.mark.parametrize("V", [512, 151936, 50257])
 @pytest.mark.parametrize("red", [0, 1, 2])
 def test_ragged_matches_dense_on_padded_batch(dev, V, red):
     """skyrl_policy_train_ragged_fwd on the live tokens of a ragged batch == skyrl_policy_train_fwd
     on the padded batch (dead positions: loss mask 0, arbitrary logits): loss and metrics bit for
     bit under every loss reduction, logp / entropy at the live positions, and the live rows'
-    dlogits; the dead positions of logp / entropy stay 0."""
+    dlogits; the dead positions of logp / entropy stay 0. GPT-2's odd V (the EDGE form): a packed
+    row sits at another offset within 16 B than its padded row, so the pieces cut its span
+    elsewhere: another fp32 summation order, compared at 1e-5 (dlogits within a bf16 rounding)."""
     n, R = 4, 24
     g = torch.Generator().manual_seed(V + red)
     lens = torch.tensor([24, 1, 13, 7])
@@ -120,7 +122,53 @@ def test_ragged_matches_dense_on_padded_batch(dev, V, red):
     pos = torch.nonzero(lv.reshape(-1)).reshape(-1).to(torch.int32)
     loss_r, m_r, lp_r, ent_r = ops.policy_train_ragged(z, labels[lv], pos, old, adv, mask, params, ref_log_probs=ref)
     loss_r.backward()
+    assert not lp_r[~lv].any() and not ent_r[~lv].any()
+    if V % 8:
+        for a, b in ((loss_r, loss_d), (m_r[:7], m_d[:7]), (lp_r[lv], lp_d[lv]), (ent_r[lv], ent_d[lv])):
+            torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(z.grad.float(), x.grad[lv].float(), atol=2e-6, rtol=1e-2)
+        return
     assert torch.equal(loss_r, loss_d) and torch.equal(m_r[:7], m_d[:7])
     assert torch.equal(lp_r[lv], lp_d[lv]) and torch.equal(ent_r[lv], ent_d[lv])
     assert not lp_r[~lv].any() and not ent_r[~lv].any()
     assert torch.equal(z.grad, x.grad[lv])
+
+
+@pytest.mark.parametrize("V", [1001, 8191, 50257, 100003])
+@pytest.mark.parametrize("parts", [8, 4])
+def test_split_edge_rows_match_resident(dev, V, parts):
+    """Rows with partial vectors (odd V on the model-wrapper slice [:, -R-1:-1], so each row sits
+    at another offset within 16 B): the split kernel's EDGE form vs the resident EDGE kernel, and
+    the dlogits of positions outside the slice stay exactly 0 (partial vectors write only their
+    own row's slots)."""
+    params = _params()
+    n, S, R = 3, 21, 17
+    g = torch.Generator().manual_seed(V + parts)
+    logits = (torch.randn(n, S, V, generator=g) * 3).to(torch.bfloat16).to(dev)
+    labels = torch.randint(0, V, (n, R), generator=g).to(dev)
+    labels[0, 0], labels[1, 1], labels[2, 2] = 0, V - 1, V - 2  # labels in the partial vectors
+    old = (-6 + torch.randn(n, R, generator=g)).to(dev)
+    adv = torch.randn(n, R, generator=g).to(dev)
+    mask = (torch.rand(n, R, generator=g) < 0.9).float().to(dev)
+    ref = (-6 + torch.randn(n, R, generator=g)).to(dev)
+    outs = []
+    ops._ffi.call("skyrl_tune", b"train_split_parts", parts)
+    try:
+        for split in (1, 0):
+            ops._ffi.call("skyrl_tune", b"train_split", split)
+            full = logits.clone().requires_grad_(True)
+            loss, m, lp, ent = ops.policy_train(full[:, -R - 1:-1], labels, old, adv, mask, params, ref_log_probs=ref,
+                                                temperature=0.8)
+            loss.backward()
+            outs.append((loss.detach(), m.clone(), lp, ent, full.grad))
+    finally:
+        ops._ffi.call("skyrl_tune", b"train_split", 1)
+        ops._ffi.call("skyrl_tune", b"train_split_parts", 8)
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(outs[0][4].float(), outs[1][4].float(), atol=2e-6, rtol=1e-2)
+    assert float(outs[0][1][6]) == 0.0
+    grad = outs[0][4]
+    assert torch.count_nonzero(grad[:, :S - R - 1]) == 0 and torch.count_nonzero(grad[:, -1]) == 0
+    live = grad[:, -R - 1:-1][mask.bool()]  # masked tokens have zero dlogits
+    assert torch.count_nonzero(live) > 0.9 * live.numel()

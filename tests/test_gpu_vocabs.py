@@ -1,7 +1,7 @@
 """Every BASELINE.json configuration's vocabulary through the sampler (a1), the logprob/entropy
 kernels (a2/a3) and the fused training pass (a2+a3+a6+a7) against the oracle:
 
-  GPT-2-small      V =  50,257  (config 1; odd V: misaligned rows, the EDGE resident kernel)
+  GPT-2-small      V =  50,257  (config 1; odd V: misaligned rows, the split kernel's EDGE form)
   Llama-3-8B       V = 128,256  (config 4; resident kernel, 16 vectors per thread)
   Qwen2.5-1.5B     V = 151,936  (config 2; resident kernel, 19 vectors per thread)
   Qwen2.5-7B       V = 152,064  (configs 3 and 5)
