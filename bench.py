@@ -317,7 +317,7 @@ def run(args):
          CEILING_READ_GBS),
         ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
          2 * (N // mb) + (N // mb if args.unfused else 0), CEILING_READ_GBS),
-        ("skyrl_policy_train_fwd (policy_train_split_kernel: each row in 8 pieces of 128 threads)", train_timer,
+        ("skyrl_policy_train_fwd (policy_train_split_kernel: each row in 6 pieces of 256 threads)", train_timer,
          rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb, CEILING_RW_GBS),
         ("skyrl_adamw_step (sumsq + plan + adamw_update_kernel<shadow>)", adam_timer,
          (reducer.layout.shard_numel * (4 + 30)) if reducer is not None else 0, 1, CEILING_RW_GBS),

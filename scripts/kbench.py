@@ -112,22 +112,23 @@ def main():
                       ops._ptr(ent), ops._ptr(dlog), R * V, V, ops._ptr(ws), st)
         # (split, resident, nt stores, resident threads)
         # (split, resident, nt stores, resident threads, 100 * split parts)
-        variants = [(1, 1, 1, 1024, 800), (1, 1, 1, 1024, 400), (1, 1, 0, 1024, 800), (0, 1, 1, 1024, 800)]
+        # (split, resident, nt stores, resident threads, split shape: skyrl_tune "train_split_shape")
+        variants = [(1, 1, 1, 1024, 0), (1, 1, 1, 1024, 1), (1, 1, 0, 1024, 0), (0, 1, 1, 1024, 0)]
         times = {v: [] for v in variants}
         for _ in range(args.rounds):  # interleaved rounds
             for v in variants:
                 split, resident, nts, nt, sm = v
-                _ffi.call("skyrl_tune", b"train_split_parts", sm // 100)
+                _ffi.call("skyrl_tune", b"train_split_shape", sm)
                 _ffi.call("skyrl_tune", b"train_split", split)
                 _ffi.call("skyrl_tune", b"train_resident", resident)
                 _ffi.call("skyrl_tune", b"train_ntstore", nts)
                 _ffi.call("skyrl_tune", b"train_resident_nt", nt)
                 times[v].append(timeit(lambda: (fused(x0), fused(x1))) / 2)
         _ffi.call("skyrl_tune", b"train_split", 1)
-        _ffi.call("skyrl_tune", b"train_split_parts", 8)
+        _ffi.call("skyrl_tune", b"train_split_shape", 0)
         for (split, resident, nts, nt, sm), t in times.items():
             ms = statistics.median(t)
-            res[f"policy_train_fused_split{split}_mode{sm}_resident{resident}_nts{nts}_nt{nt}"] = {
+            res[f"policy_train_fused_split{split}_shape{sm}_resident{resident}_nts{nts}_nt{nt}"] = {
                 "ms": ms, "GBps_hbm_algorithmic": rows * (V * 4 + 40) / ms / 1e6,
                 "vs_unfused_bytes": rows * (V * 6) / ms / 1e6}
         _ffi.call("skyrl_tune", b"train_resident", 1)
@@ -189,18 +190,19 @@ def main():
                           ops._ptr(lab2), lab2.stride(0), lab2.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
                           ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met),
                           ops._ptr(lp), ops._ptr(ent), ops._ptr(d2), R * V2, V2, ops._ptr(ws), st)
-            variants = [(1, 8), (1, 4), (1, 2), (0, 8)]  # (split, parts); split 0 = the resident kernel
+            # (split, shape: skyrl_tune "train_split_shape"); split 0 = the resident kernel
+            variants = [(1, sh) for sh in range(0, 6)] + [(0, 0)]  # shape 0: the default by vocabulary
             times = {v: [] for v in variants}
             for _ in range(args.rounds):
                 for v in variants:
                     _ffi.call("skyrl_tune", b"train_split", v[0])
-                    _ffi.call("skyrl_tune", b"train_split_parts", v[1])
+                    _ffi.call("skyrl_tune", b"train_split_shape", v[1])
                     times[v].append(timeit(lambda: (fused2(g2[0]), fused2(g2[1]))) / 2)
             _ffi.call("skyrl_tune", b"train_split", 1)
-            _ffi.call("skyrl_tune", b"train_split_parts", 8)
-            for (split, parts), t in times.items():
+            _ffi.call("skyrl_tune", b"train_split_shape", 0)
+            for (split, shape), t in times.items():
                 ms = statistics.median(t)
-                res[f"policy_train_V{V2}_split{split}_parts{parts}"] = {
+                res[f"policy_train_V{V2}_split{split}_shape{shape}"] = {
                     "ms": ms, "GBps_hbm_algorithmic": rows * (V2 * 4 + 40) / ms / 1e6}
             del g2, d2
             torch.cuda.empty_cache()

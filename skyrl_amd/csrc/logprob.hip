@@ -214,7 +214,7 @@ extern int g_train_resident;
 extern int g_train_resident_nt;
 extern int g_train_ntstore;
 extern int g_train_split;
-extern int g_train_split_parts;
+extern int g_train_split_shape;
 extern int g_grpo_slices;
 extern int g_loss_units;
 extern int g_loss_bwd_blocks;
@@ -233,9 +233,9 @@ extern "C" int skyrl_tune(const char* key, int value) {
         g_tune.unroll = value;
         return SKYRL_OK;
     }
-    if (k == "train_split_parts") {
-        SKYRL_REQUIRE(value == 2 || value == 4 || value == 8, "skyrl_tune: train_split_parts must be 2, 4 or 8");
-        g_train_split_parts = value;
+    if (k == "train_split_shape") {
+        SKYRL_REQUIRE(value >= 0 && value <= 5, "skyrl_tune: train_split_shape must be 0..5");
+        g_train_split_shape = value;
         return SKYRL_OK;
     }
     if (k == "train_split") {

@@ -22,6 +22,8 @@
 //   3. train_epilogue_kernel (1 block): folds the per-token terms into the loss scalar
 //      and the metric vector (same layout as skyrl_ppo_loss_fwd).
 // HBM traffic per token: V*2 (read) + V*2 (write) vs V*2 + V*2 + V*2 unfused.
+#include <utility>
+
 #include "arrive.h"
 
 // Phase timestamps for scripts/probe/train_phase_probe (compiled only there, never in the product).
@@ -508,22 +510,21 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
 // resident or next to be), every poll is bounded, and a timeout raises the error word
 // (metrics[6] = 1 via the epilogue; ops.check_loss_metrics raises) and leaves NaN in that
 // row's terms instead of hanging.
-constexpr int kSplitP = 4;     // the template default; the host picks g_train_split_parts
-constexpr int kSplitMaxP = 8;  // skyrl_tune("train_split_parts", 4/8): pieces of 1024/P threads
+constexpr int kSplitMaxP = 12;  // most pieces per row of any built shape (split_shapes below)
 constexpr unsigned kSplitMaxPolls = 1u << 20;
 
 typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
 typedef __attribute__((address_space(1))) unsigned ptr_gu32;
 
-template <int NV, bool HAS_T, int P = kSplitP, bool EDGE = false>
-__global__ __launch_bounds__(1024 / P, P == 8 ? 3 : (P == 4 ? 4 : 2)) void policy_train_split_kernel(
+template <int NV, bool HAS_T, int P, bool EDGE, int W, int NT>
+__global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
     const uint16_t* __restrict__ logits, int64_t sb, int64_t st_, int R, int V, const int64_t* __restrict__ labels,
     int64_t lsb, int64_t lst, float temp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
     const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
     float* __restrict__ tok, uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts,
     unsigned long long* __restrict__ gran, unsigned* __restrict__ err_word, const int32_t* __restrict__ tpos) {
-    constexpr int NT = 1024 / P;
+    static_assert(P <= 16 && NT % 64 == 0 && NT <= 1024, "split shape");
     __shared__ St s_st[NT / 64];
     __shared__ float s_g[4];
     __shared__ float s_part[P * 3];
@@ -647,10 +648,18 @@ __global__ __launch_bounds__(1024 / P, P == 8 ? 3 : (P == 4 ? 4 : 2)) void polic
             if (!ok) __hip_atomic_store((ptr_gu32*)err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __builtin_amdgcn_wave_barrier();  // wave 0's LDS writes above precede its reads below
-        if (threadIdx.x == 0) {
-            St m{s_part[0], s_part[1], s_part[2]};
+        // the row's state: a fixed xor tree over lanes 0..P-1 (lane j holds piece j), the same
+        // operations on the same values in every piece, so all pieces get the same bits (a
+        // serial fold in lane 0 held 3P more VGPRs across the exchange)
+        constexpr int kTop = P > 8 ? 8 : P > 4 ? 4 : P > 2 ? 2 : 1;
+        St m = lane < P ? St{s_part[3 * lane], s_part[3 * lane + 1], s_part[3 * lane + 2]}
+                        : St{-3.402823466e38f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 1; j < P; ++j) st_merge(m, St{s_part[3 * j], s_part[3 * j + 1], s_part[3 * j + 2]});
+        for (int off = kTop; off > 0; off >>= 1) {
+            St o{__shfl_xor(m.m, off, kWave), __shfl_xor(m.s, off, kWave), __shfl_xor(m.w, off, kWave)};
+            st_merge(m, o);
+        }
+        if (threadIdx.x == 0) {
             const float logs = fast_log2(m.s) * kLn2;
             const float lse = m.m + logs;
             const float H = logs - kLn2 * (m.w / m.s);
@@ -795,7 +804,7 @@ int g_train_resident = 1;  // skyrl_tune("train_resident", 0/1)
 int g_train_resident_nt = 1024;  // skyrl_tune("train_resident_nt", 768/1024)
 int g_train_ntstore = 1;   // skyrl_tune("train_ntstore", 0/1): non-temporal dlogits stores
 int g_train_split = 1;     // skyrl_tune("train_split", 0/1): split-row kernel where it applies
-int g_train_split_parts = 8;  // skyrl_tune("train_split_parts", 4/8): pieces per row
+int g_train_split_shape = 0;  // skyrl_tune("train_split_shape", 0 = by vocabulary, 1..7: kSplitShapes)
 
 }  // namespace skyrl
 
@@ -845,64 +854,60 @@ using SplitKernel = void (*)(const uint16_t*, int64_t, int64_t, int, int, const 
                              const float*, const float*, const float*, const float*, const float*, const float*,
                              skyrl_ppo_params, float*, float*, float*, uint16_t*, int64_t, int64_t, bool,
                              unsigned long long*, unsigned*, const int32_t*);
-template <int NV, int P>
+// Split shapes: P pieces per row of NT threads each, W waves per SIMD (the __launch_bounds__
+// occupancy target, i.e. the VGPR cap 512 / W in granules of 8 the compiler schedules the
+// piece's registers under). skyrl_tune("train_split_shape", i) picks one; 0 = by vocabulary.
+template <int P, bool EDGE, int W, int NT, int NV>
 SplitKernel pick_split(bool has_t) {
-    return has_t ? policy_train_split_kernel<NV, true, P> : policy_train_split_kernel<NV, false, P>;
+    return has_t ? policy_train_split_kernel<NV, true, P, EDGE, W, NT>
+                 : policy_train_split_kernel<NV, false, P, EDGE, W, NT>;
 }
-template <int P>
-SplitKernel split_for_p(int nv, bool has_t) {
-    switch (nv) {
-        case 1: return pick_split<1, P>(has_t);
-        case 2: return pick_split<2, P>(has_t);
-        case 3: return pick_split<3, P>(has_t);
-        case 4: return pick_split<4, P>(has_t);
-        case 5: return pick_split<5, P>(has_t);
-        case 6: return pick_split<6, P>(has_t);
-        case 7: return pick_split<7, P>(has_t);
-        case 8: return pick_split<8, P>(has_t);
-        case 9: return pick_split<9, P>(has_t);
-        case 10: return pick_split<10, P>(has_t);
-        case 11: return pick_split<11, P>(has_t);
-        case 12: return pick_split<12, P>(has_t);
-        case 13: return pick_split<13, P>(has_t);
-        case 14: return pick_split<14, P>(has_t);
-        case 15: return pick_split<15, P>(has_t);
-        case 16: return pick_split<16, P>(has_t);
-        case 17: return pick_split<17, P>(has_t);
-        case 18: return pick_split<18, P>(has_t);
-        default: return pick_split<19, P>(has_t);
-    }
+// aligned rows need NV exactly (the first NV-1 loads are unconditional); EDGE rows take the
+// smallest listed NV >= nv
+template <int P, bool EDGE, int W, int NT, int... NVs>
+SplitKernel split_table(int nv, bool has_t, std::integer_sequence<int, NVs...>) {
+    SplitKernel k = nullptr;
+    ((k = (k == nullptr && (EDGE ? nv <= NVs : nv == NVs)) ? pick_split<P, EDGE, W, NT, NVs>(has_t) : k), ...);
+    return k;
 }
-SplitKernel split_for(int nv, bool has_t, int parts) {
-    return parts == 8 ? split_for_p<8>(nv, has_t) : parts == 4 ? split_for_p<4>(nv, has_t) : split_for_p<2>(nv, has_t);
-}
-// rows with partial vectors: the smallest listed NV covering a piece (as kEdgeNV, the edge
-// logic costs VGPRs; NV <= 14 covers V <= 114,688)
+using AlignedNV = std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19>;
+// the edge logic costs VGPRs: NV <= 14 (V <= 114,688 at 1024 threads per row)
+using EdgeNV = std::integer_sequence<int, 1, 2, 4, 7, 10, 14>;
 constexpr int kSplitEdgeNV[] = {1, 2, 4, 7, 10, 14};
-template <int NV, int P>
-SplitKernel pick_split_edge(bool has_t) {
-    return has_t ? policy_train_split_kernel<NV, true, P, true> : policy_train_split_kernel<NV, false, P, true>;
-}
-template <int P>
-SplitKernel split_edge_for_p(int nv, bool has_t) {
-    switch (nv) {
-        case 1: return pick_split_edge<1, P>(has_t);
-        case 2: return pick_split_edge<2, P>(has_t);
-        case 4: return pick_split_edge<4, P>(has_t);
-        case 7: return pick_split_edge<7, P>(has_t);
-        case 10: return pick_split_edge<10, P>(has_t);
-        default: return pick_split_edge<14, P>(has_t);
+struct SplitShape {
+    int parts, threads, waves;
+};
+constexpr SplitShape kSplitShapes[] = {
+    {0, 0, 0},       // 0: by vocabulary (split_plan)
+    {8, 128, 3},     // 1
+    {4, 256, 4},     // 2
+    {2, 512, 2},     // 3
+    {5, 256, 4},     // 4
+    {6, 256, 5},     // 5
+};
+constexpr int kSplitShapeCount = sizeof(kSplitShapes) / sizeof(kSplitShapes[0]);
+SplitKernel split_for(int nv, bool has_t, int shape, bool edge) {
+    if (edge) {  // EDGE forms are built for the power-of-two shapes only
+        switch (shape) {
+            case 1: return split_table<8, true, 3, 128>(nv, has_t, EdgeNV{});
+            case 2: return split_table<4, true, 4, 256>(nv, has_t, EdgeNV{});
+            case 3: return split_table<2, true, 2, 512>(nv, has_t, EdgeNV{});
+            default: return nullptr;
+        }
     }
-}
-SplitKernel split_edge_for(int nv, bool has_t, int parts) {
-    return parts == 8 ? split_edge_for_p<8>(nv, has_t)
-                      : parts == 4 ? split_edge_for_p<4>(nv, has_t) : split_edge_for_p<2>(nv, has_t);
+    switch (shape) {
+        case 1: return split_table<8, false, 3, 128>(nv, has_t, AlignedNV{});
+        case 2: return split_table<4, false, 4, 256>(nv, has_t, AlignedNV{});
+        case 3: return split_table<2, false, 2, 512>(nv, has_t, AlignedNV{});
+        case 4: return split_table<5, false, 4, 256>(nv, has_t, AlignedNV{});
+        case 5: return split_table<6, false, 5, 256>(nv, has_t, AlignedNV{});
+        default: return nullptr;
+    }
 }
 // EDGE layout: a row's span is (h + V + 7) / 8 vectors for its offset h = 0..7 within 16 B, so
 // two span lengths occur; both must give pieces of at most NV*NT vectors and a non-empty last
 // piece. Returns the listed NV, or 0.
-int split_nv_edge(int V, int parts) {
-    const int nt = 1024 / parts;
+int split_nv_edge(int V, int parts, int nt) {
     const int spans[2] = {(V + 7) / 8, (V + 14) / 8};
     int need = 0;
     for (int nvec : spans) {
@@ -915,16 +920,34 @@ int split_nv_edge(int V, int parts) {
     return 0;
 }
 // the split kernel's vectors per thread for nvec row vectors cut into `parts` pieces of
-// 1024 / parts threads, or 0 if its layout does not fit: pieces of per = ceil(nvec / parts)
+// nt threads, or 0 if its layout does not fit: pieces of per = ceil(nvec / parts)
 // vectors, NV = ceil(per / threads) <= 19, and the last piece still covers the NV-1
 // unconditional loads of every thread
-int split_nv(int nvec, int parts) {
-    const int nt = 1024 / parts;
+int split_nv(int nvec, int parts, int nt) {
     const int per = (nvec + parts - 1) / parts;
     const int nv = (per + nt - 1) / nt;
     const int last = nvec - (parts - 1) * per;
     if (nv < 1 || nv > 19 || last <= (nv - 1) * nt) return 0;
     return nv;
+}
+// the split launch for a vocabulary: skyrl_tune("train_split_shape") if set, else by V
+struct SplitPlan {
+    SplitKernel kern = nullptr;
+    int parts = 0, threads = 0;
+};
+SplitPlan split_plan(int V, bool aligned, bool has_t) {
+    SplitPlan sp;
+    // by vocabulary (profiles/r03_split_shapes.json, 16 x 1024 tokens per launch): rows over
+    // 128 KB in six 256-thread pieces (13 vectors per thread at V = 151,936: 79 VGPRs, so 6
+    // waves per SIMD and 6 pieces per CU in flight), shorter rows and rows with partial
+    // vectors (GPT-2) in four
+    const int shape = g_train_split_shape ? g_train_split_shape : (aligned && V > 65536 ? 5 : 2);
+    const SplitShape& sh = kSplitShapes[shape];
+    const int nv = aligned ? split_nv(V / 8, sh.parts, sh.threads) : split_nv_edge(V, sh.parts, sh.threads);
+    if (nv > 0) sp.kern = split_for(nv, has_t, shape, !aligned);
+    sp.parts = sh.parts;
+    sp.threads = sh.threads;
+    return sp;
 }
 // aligned rows: NV = ceil(nvec / 1024) exactly, 1..19 (V <= 155,648)
 TrainKernel resident_aligned_for(int nv, bool has_t) {
@@ -1006,11 +1029,9 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
             if (span <= cand * 1024) { nv = cand; break; }
     }
     const bool resident_ok = g_train_resident && same_align && nv > 0;
-    const int parts = g_train_split_parts;
-    const int snv = aligned ? split_nv(nvec, parts) : split_nv_edge(V, parts);
-    if (g_train_split && g_train_resident && same_align && snv > 0 && (int64_t)n * R * parts < (1ll << 31)) {
-        hipLaunchKernelGGL(aligned ? split_for(snv, has_t, parts) : split_edge_for(snv, has_t, parts), dim3((unsigned)((int64_t)n * R * parts)), dim3(1024 / parts),
-                           0, s, in,
+    const SplitPlan sp = split_plan(V, aligned, has_t);
+    if (g_train_split && g_train_resident && same_align && sp.kern && (int64_t)n * R * sp.parts < (1ll << 31)) {
+        hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)n * R * sp.parts)), dim3(sp.threads), 0, s, in,
                            stride_b, stride_t, R, V, labels, lstride_b, lstride_t, temperature, old_log_probs,
                            advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok,
                            out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word, nullptr);
@@ -1064,17 +1085,16 @@ extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int6
                   "policy_train_ragged_fwd: bad loss_reduction");
     SKYRL_REQUIRE(params->loss_reduction != 2 || params->max_seq_len > 0.f,
                   "policy_train_ragged_fwd: seq_mean_token_sum_norm needs max_seq_len");
-    const int parts = g_train_split_parts;
     const auto lgp = reinterpret_cast<uintptr_t>(logits), grp = reinterpret_cast<uintptr_t>(grad_logits);
     // rows without partial vectors take the plain split kernel, others (GPT-2's odd V) its EDGE
     // form; either way every dlogits row must sit at its logits row's offset within 16 B
     const bool aligned = (V % 8) == 0 && (ld % 8) == 0 && (ld_grad % 8) == 0 && lgp % 16 == 0 && grp % 16 == 0;
-    const int snv = aligned ? split_nv(V / 8, parts) : split_nv_edge(V, parts);
-    SKYRL_REQUIRE(snv > 0, "policy_train_ragged_fwd: V outside the split kernel's range (V <= 155,648, or "
+    const SplitPlan sp = split_plan(V, aligned, temperature != 1.0f);
+    SKYRL_REQUIRE(sp.kern != nullptr, "policy_train_ragged_fwd: V outside the split kernel's range (V <= 155,648, or "
                            "114,688 for rows not 16-B aligned)");
     SKYRL_REQUIRE(ld >= V && ld_grad >= V && lgp % 2 == 0 && (grp - lgp) % 16 == 0 && (ld_grad - ld) % 8 == 0,
                   "policy_train_ragged_fwd: dlogits rows must share the logits rows' offset within 16 B");
-    SKYRL_REQUIRE((int64_t)ntok * parts < (1ll << 31), "policy_train_ragged_fwd: too many tokens for one launch");
+    SKYRL_REQUIRE((int64_t)ntok * sp.parts < (1ll << 31), "policy_train_ragged_fwd: too many tokens for one launch");
     char* w = reinterpret_cast<char*>(workspace);
     float* scal = reinterpret_cast<float*>(w);
     float* row_scale = reinterpret_cast<float*>(w + 256);
@@ -1087,9 +1107,7 @@ extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int6
     hipLaunchKernelGGL(train_scales_kernel, dim3(1), dim3(kThreads), 0, s, loss_mask, n, R, *params, row_scale, scal);
     int rc = check_launch("train_scales_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(aligned ? split_for(snv, temperature != 1.0f, parts) : split_edge_for(snv, temperature != 1.0f, parts),
-                       dim3((unsigned)((int64_t)ntok * parts)),
-                       dim3(1024 / parts), 0, s, reinterpret_cast<const uint16_t*>(logits), (int64_t)0, ld, R, V,
+    hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)ntok * sp.parts)), dim3(sp.threads), 0, s, reinterpret_cast<const uint16_t*>(logits), (int64_t)0, ld, R, V,
                        labels, (int64_t)0, (int64_t)1, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
                        row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
                        (int64_t)0, ld_grad, g_train_ntstore != 0, gran, err_word, token_pos);

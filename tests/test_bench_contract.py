@@ -37,7 +37,7 @@ def test_bench_line_has_the_contract_keys():
 def test_pmc_traffic_lookup_matches_committed_profile():
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
         table = json.load(f)["kernels"]
-    assert bench.pmc_traffic("skyrl_policy_train_fwd (policy_train_split_kernel: 8 pieces)", 0) == \
+    assert bench.pmc_traffic("skyrl_policy_train_fwd (policy_train_split_kernel: 6 pieces)", 0) == \
         table["policy_train_split_kernel"]["hbm_bytes_per_launch"]
     assert bench.pmc_traffic("paged_decode_kernel", 0) == table["paged_decode_kernel"]["hbm_bytes_per_launch"]
     assert bench.pmc_traffic("no_such_kernel", 0) is None

@@ -1,10 +1,10 @@
-"""Split-row fused training pass (policy_train_split_kernel: eight 128-thread workgroups per row by
-default, four of 256 threads as the alternative, exchanging their softmax states through
-epoch-tagged granules in the workspace).
+"""Split-row fused training pass (policy_train_split_kernel: each row cut into pieces, one
+workgroup each -- by default six of 256 threads for rows over 128 KB, four of 256 otherwise --
+exchanging their softmax states through epoch-tagged granules in the workspace).
 
 * a launch never reads the previous launch's granules: inputs B after inputs A on the same
   workspace give bit-for-bit what B gives on a fresh workspace (and again on replay);
-* the quarters merge in one fixed order: every output is identical across repeated launches;
+* the pieces merge in one fixed order: every output is identical across repeated launches;
 * rows at the metric's shape (V = 151,936, 16 x 128 tokens) against the resident kernel.
 """
 
@@ -48,13 +48,14 @@ def _same(a, b):
 
 @pytest.mark.parametrize("V", [512, 151936])
 @pytest.mark.parametrize("R", [40, 41])
-@pytest.mark.parametrize("parts", [8, 4])
-def test_split_fresh_granules_every_launch(dev, V, R, parts):
-    """Eighths (the default) and quarters; 120 and 123 rows."""
+@pytest.mark.parametrize("shape", [1, 2, 3, 4, 5])
+def test_split_fresh_granules_every_launch(dev, V, R, shape):
+    """Every built split shape (pieces x threads: 8 x 128, 4 x 256, 2 x 512, 5 x 256, 6 x 256;
+    shapes whose pieces do not fit V fall back to the resident kernel); 120 and 123 rows."""
     params = _params()
     n = 3
     A, B = _inputs(1, n, R, V, dev), _inputs(2, n, R, V, dev)
-    ops._ffi.call("skyrl_tune", b"train_split_parts", parts)
+    ops._ffi.call("skyrl_tune", b"train_split_shape", shape)
     try:
         ops.WORKSPACES._bufs.clear()
         ref_b = _run(B, params)  # B on a fresh workspace
@@ -64,9 +65,9 @@ def test_split_fresh_granules_every_launch(dev, V, R, parts):
         _same(got, ref_b)
         _same(_run(B, params), ref_b)  # replay
     finally:
-        ops._ffi.call("skyrl_tune", b"train_split_parts", 8)
+        ops._ffi.call("skyrl_tune", b"train_split_shape", 0)
     assert float(ref_b[1][6]) == 0.0
-    if parts != 8:  # quarters vs eighths: another fp32 summation order only
+    if shape != 5:  # vs the default shape: another fp32 summation order only
         q = _run(B, params)
         for a, b in zip(ref_b[:4], q[:4]):
             torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
@@ -135,15 +136,15 @@ def test_ragged_matches_dense_on_padded_batch(dev, V, red):
 
 
 @pytest.mark.parametrize("V", [1001, 8191, 50257, 100003])
-@pytest.mark.parametrize("parts", [8, 4])
-def test_split_edge_rows_match_resident(dev, V, parts):
+@pytest.mark.parametrize("shape", [1, 2, 3])
+def test_split_edge_rows_match_resident(dev, V, shape):
     """Rows with partial vectors (odd V on the model-wrapper slice [:, -R-1:-1], so each row sits
     at another offset within 16 B): the split kernel's EDGE form vs the resident EDGE kernel, and
     the dlogits of positions outside the slice stay exactly 0 (partial vectors write only their
     own row's slots)."""
     params = _params()
     n, S, R = 3, 21, 17
-    g = torch.Generator().manual_seed(V + parts)
+    g = torch.Generator().manual_seed(V + shape)
     logits = (torch.randn(n, S, V, generator=g) * 3).to(torch.bfloat16).to(dev)
     labels = torch.randint(0, V, (n, R), generator=g).to(dev)
     labels[0, 0], labels[1, 1], labels[2, 2] = 0, V - 1, V - 2  # labels in the partial vectors
@@ -152,7 +153,7 @@ def test_split_edge_rows_match_resident(dev, V, parts):
     mask = (torch.rand(n, R, generator=g) < 0.9).float().to(dev)
     ref = (-6 + torch.randn(n, R, generator=g)).to(dev)
     outs = []
-    ops._ffi.call("skyrl_tune", b"train_split_parts", parts)
+    ops._ffi.call("skyrl_tune", b"train_split_shape", shape)
     try:
         for split in (1, 0):
             ops._ffi.call("skyrl_tune", b"train_split", split)
@@ -163,7 +164,7 @@ def test_split_edge_rows_match_resident(dev, V, parts):
             outs.append((loss.detach(), m.clone(), lp, ent, full.grad))
     finally:
         ops._ffi.call("skyrl_tune", b"train_split", 1)
-        ops._ffi.call("skyrl_tune", b"train_split_parts", 8)
+        ops._ffi.call("skyrl_tune", b"train_split_shape", 0)
     for a, b in zip(outs[0][:4], outs[1][:4]):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(outs[0][4].float(), outs[1][4].float(), atol=2e-6, rtol=1e-2)
