@@ -139,7 +139,10 @@ def run(args):
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # SKYRL_FORCE_COLLECTIVES=1 under a one-rank torchrun: the group is initialized and every
+    # exchange runs as a (one-rank) RCCL collective, so the N>1 code path runs on one GPU
+    dist_on = world > 1 or os.environ.get("SKYRL_FORCE_COLLECTIVES", "0") == "1"
+    if dist_on:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:  # rehearsal of the N>1 path with several ranks on one GPU (RCCL refuses duplicate GPUs)
@@ -269,7 +272,7 @@ def run(args):
                     ctypes.byref(params), ops._ptr(loss_buf), ops._ptr(met_buf), ops._ptr(lp), ops._ptr(ent),
                     ops._ptr(dlogits), R * V, V, ops._ptr(train_ws), ops._stream(dev)))
                 metrics_acc.add_(met_buf)
-        if world > 1:
+        if dist_on:
             dist.all_reduce(metrics_acc)
         # ---- optimizer step (one mini-batch per step at 64 prompts): DP gradient reduce-scatter on
         #      the comm stream, sharded clip + AdamW (one HIP pass, bf16 copy written in the same
@@ -285,7 +288,7 @@ def run(args):
         step(w)
         torch.cuda.synchronize()
         log(f"warmup {w}: {time.time() - t0:.3f}s")
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     for tm in timers:
@@ -295,7 +298,7 @@ def run(args):
         m = step(1000 + k)
         if k == args.steps - 1 or (k % 2 == 0):
             log(f"step {k} enqueued ({time.perf_counter() - t0:.2f}s)")
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -303,7 +306,7 @@ def run(args):
         tm.active = False
     mvals = m.tolist()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -353,6 +356,8 @@ def run(args):
             "final_loss_sum_last_step": round(mvals[0], 6),
             "policy_params": args.params, "grad_bucket_mb": args.bucket_mb,
             "optimizer": "sharded AdamW (fp32 master, bf16 rollout copy), reduce-scatter + all-gather over RCCL",
+            "collectives": (dist.get_backend() + (" (one-rank group, SKYRL_FORCE_COLLECTIVES)" if world == 1 else ""))
+            if dist_on else "none (world size 1)",
         },
         "roofline": {
             "kernel": dom_name,
@@ -389,7 +394,7 @@ def run(args):
         result["end_to_end"] = end_to_end_leg()
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -56,12 +56,19 @@ def fixed_generation(step, rank, n_prompts=4, G=4, vocab=512):
 
 def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        dist.init_process_group("gloo")
-    rank = dist.get_rank() if world > 1 else 0
-    group = dist.group.WORLD if world > 1 else None
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
+    # REHEARSE_BACKEND=nccl with SKYRL_FORCE_COLLECTIVES=1 under a one-rank torchrun: every
+    # exchange of the trainer runs as a one-rank RCCL collective on the comm stream
+    backend = os.environ.get("REHEARSE_BACKEND", "gloo")
+    dist_on = world > 1 or os.environ.get("SKYRL_FORCE_COLLECTIVES", "0") == "1"
+    if dist_on:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    rank = dist.get_rank() if dist_on else 0
+    group = dist.group.WORLD if dist_on else None
     from transformers import AutoModelForCausalLM, Qwen2Config
 
     cfg = Qwen2Config(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
@@ -88,7 +95,7 @@ def main():
 
     def checked_step(n_micro=1, lr=None):
         local = opt.reducer.grad[: opt.reducer.layout.numel].clone()  # this rank's gradient sum
-        if world > 1:
+        if dist_on:
             dist.all_reduce(local, op=dist.ReduceOp.SUM, group=group)
         mean = local / (world * n_micro)
         for (_, p), o, r in zip(opt.named, opt.offsets, ref):
@@ -129,8 +136,11 @@ def main():
         ok_all = ok_all and ok
         out.append(rec)
     if rank == 0:
-        print(json.dumps({"world": world, "ok": ok_all, "steps": out}), flush=True)
-    if world > 1:
+        print(json.dumps({"world": world, "backend": dist.get_backend() if dist_on else None,
+                          "collective_path": bool(opt.collective),
+                          "reduce_scatters_from_backward": opt.launched_during_backward,
+                          "ok": ok_all, "steps": out}), flush=True)
+    if dist_on:
         dist.destroy_process_group()
     if not ok_all:
         sys.exit(1)

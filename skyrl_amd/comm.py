@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import asdict, dataclass
 from typing import Callable, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
@@ -51,12 +52,22 @@ def _world(group) -> Tuple[int, int]:
     return 1, 0
 
 
+def _collective(world: int) -> bool:
+    """True when the exchanges must run as collectives. World size 1 normally short-cuts them;
+    ``SKYRL_FORCE_COLLECTIVES=1`` under an initialized one-rank group keeps them, so the RCCL
+    code path (comm-stream reduce-scatter / all-gather / all-reduce) runs on a one-GPU box."""
+    if world > 1:
+        return True
+    return (os.environ.get("SKYRL_FORCE_COLLECTIVES", "0") == "1" and dist.is_available()
+            and dist.is_initialized())
+
+
 # ------------------------------------------------------------------------------------ a13
 def all_reduce_metrics(metrics: Dict[str, float], group=None, device=None) -> Dict[str, float]:
     """Mirror of ``all_reduce_metrics`` (worker_utils.py:25-35): keys ending in ``_min`` are
     min-reduced, ``_max`` max-reduced, the rest averaged over ranks. Two collectives total."""
     world, _ = _world(group)
-    if world == 1 or not metrics:
+    if not _collective(world) or not metrics:
         return {k: float(v) for k, v in metrics.items()}
     keys = list(metrics)
     mean_keys = [k for k in keys if not (k.endswith("_min") or k.endswith("_max"))]
@@ -131,10 +142,11 @@ class GradReducer:
                  dtype: torch.dtype = torch.float32):
         self.group = group
         self.world, self.rank = _world(group)
+        self.collective = _collective(self.world)
         self.device = torch.device(device)
         self.layout = FlatLayout(numel, self.world, bucket_bytes // torch.tensor([], dtype=dtype).element_size())
         self.grad = torch.zeros(self.layout.padded, dtype=dtype, device=self.device)
-        if self.world > 1:
+        if self.collective:
             self.grad_shard = torch.zeros(self.layout.shard_numel, dtype=dtype, device=self.device)
         else:
             self.grad_shard = self.grad
@@ -145,7 +157,7 @@ class GradReducer:
     def launch(self, buckets: Optional[Sequence[int]] = None) -> None:
         """Reduce-scatter the given buckets (default: all) after the work already queued on the
         current stream. Asynchronous with respect to the current stream."""
-        if self.world == 1:
+        if not self.collective:
             return
         lay = self.layout
         idx = range(len(lay.buckets)) if buckets is None else buckets
@@ -224,7 +236,7 @@ class ShardedAdamW:
             raise ValueError(f"init_params has {init_params.numel()} elements, layout expects {lay.numel}")
         flat = torch.zeros(lay.padded, dtype=torch.float32, device=dev)
         flat[: lay.numel] = init_params.reshape(-1).to(device=dev, dtype=torch.float32)
-        if reducer.world > 1:
+        if reducer.collective:
             self.param = torch.cat([flat[slice(*lay.piece(b, reducer.rank))] for b in range(len(lay.buckets))])
             del flat
         else:
@@ -232,7 +244,7 @@ class ShardedAdamW:
         self.exp_avg = torch.zeros_like(self.param)
         self.exp_avg_sq = torch.zeros_like(self.param)
         self.weights_bf16 = torch.empty(lay.padded, dtype=torch.bfloat16, device=dev) if shadow_bf16 else None
-        if shadow_bf16 and reducer.world == 1:
+        if shadow_bf16 and not reducer.collective:
             self.weights_bf16.copy_(flat)
             self.shard_bf16 = self.weights_bf16
         elif shadow_bf16:
@@ -258,7 +270,7 @@ class ShardedAdamW:
         r.wait()
         g = r.grad_shard
         self._ffi.call("skyrl_sumsq", _ptr(g), g.numel(), _ptr(self.sumsq), _ptr(self._ws), self._stream())
-        if r.world > 1:
+        if r.collective:
             dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=r.group)
         hp = self._ffi.AdamWParams(float(cfg.lr if lr is None else lr), float(cfg.betas[0]), float(cfg.betas[1]),
                                    float(cfg.eps), float(cfg.weight_decay), float(cfg.max_grad_norm),
@@ -275,7 +287,7 @@ class ShardedAdamW:
     def sync_weights(self) -> None:
         """Start the learner -> rollout weight all-gather (bf16) on the comm stream; the rollout
         side calls :meth:`wait_weights` before it reads ``weights_bf16``."""
-        if self.weights_bf16 is None or self.reducer.world == 1:
+        if self.weights_bf16 is None or not self.reducer.collective:
             return
         self._all_gather_weights(sync=False)
 
@@ -494,6 +506,7 @@ class BucketedGradAllReduce:
     def __init__(self, params: Iterable[torch.nn.Parameter], group=None, bucket_bytes: int = 64 << 20):
         self.group = group
         self.world, _ = _world(group)
+        self.collective = _collective(self.world)
         ps = [p for p in params if p.requires_grad]
         if not ps:
             raise ValueError("no trainable parameters")
@@ -536,7 +549,7 @@ class BucketedGradAllReduce:
 
     def arm(self) -> None:
         """Call before the backward of the mini-batch's last micro-batch."""
-        if self.world == 1:
+        if not self.collective:
             return
         self._armed = True
         self._pending = [len(pl) for _, pl in self.buckets]
@@ -645,6 +658,7 @@ class ShardedModuleOptimizer:
         self.reducer = GradReducer(numel, dev, group=group, bucket_bytes=bucket_bytes)
         lay = self.reducer.layout
         self.world, self.rank = self.reducer.world, self.reducer.rank
+        self.collective = self.reducer.collective
         self.offsets = []
         off = 0
         init = torch.empty(numel, dtype=torch.float32, device=dev)
@@ -654,7 +668,7 @@ class ShardedModuleOptimizer:
             off += p.numel()
         self.opt = ShardedAdamW(self.reducer, init, config, shadow_bf16=True)
         del init
-        if self.world == 1:
+        if not self.collective:
             self.full = self.opt.param
         else:
             self.full = torch.zeros(lay.padded, dtype=torch.float32, device=dev)
@@ -682,7 +696,7 @@ class ShardedModuleOptimizer:
     # ---------------------------------------------------------------- gradient exchange
     def arm(self) -> None:
         """Call before the backward of the mini-batch's last micro-batch."""
-        if self.world == 1:
+        if not self.collective:
             return
         self._armed = True
         self._pending = list(self._bucket_count)
@@ -713,7 +727,7 @@ class ShardedModuleOptimizer:
         self._launch_ready()
 
     def _finish_exchange(self) -> None:
-        if self.world == 1 or not self._armed:
+        if not self.collective or not self._armed:
             return
         while self._next < len(self._ready):  # buckets whose parameters got no gradient
             self.reducer.launch([self._next])
@@ -728,7 +742,7 @@ class ShardedModuleOptimizer:
         self._finish_exchange()
         self._check_grad_views()  # the .grad views must still be the buckets' storage
         gn = self.opt.step(n_micro=n_micro, lr=lr, zero_grad=True)
-        if self.world > 1:
+        if self.collective:
             self._gather_full(sync=False)
             self.opt.sync_weights()
             self.opt.wait_weights()  # the next forward (and the engine) read them
@@ -771,7 +785,7 @@ def allreduce_grads(params: Iterable[torch.Tensor], group=None, bucket_bytes: in
     fsdp_strategy.py:216-226). Returns the number of collectives issued."""
     world, _ = _world(group)
     grads = [p.grad for p in params if p.grad is not None]
-    if world == 1 or not grads:
+    if not _collective(world) or not grads:
         return 0
     n = 0
     bucket: List[torch.Tensor] = []

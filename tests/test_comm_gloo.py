@@ -60,6 +60,35 @@ def test_all_reduce_metrics_single_process_is_identity():
     assert comm.all_reduce_metrics({"a": 2, "b_max": 3}) == {"a": 2.0, "b_max": 3.0}
 
 
+def _forced_solo_case(rank, world):
+    """SKYRL_FORCE_COLLECTIVES=1 on a one-rank group: the exchanges run as collectives (the
+    code path the N > 1 run takes) and give the world-1 result."""
+    os.environ["SKYRL_FORCE_COLLECTIVES"] = "1"
+    try:
+        assert comm._collective(1)
+        m = {"loss": 1.5, "r_min": -2.0, "r_max": 4.0}
+        assert comm.all_reduce_metrics(m, device="cpu") == m
+        red = comm.GradReducer(1000, "cpu", bucket_bytes=256 * 4)
+        assert red.collective and red.grad_shard.data_ptr() != red.grad.data_ptr()
+        red.grad.copy_(torch.arange(red.layout.padded, dtype=torch.float32))
+        red.launch()
+        red.wait()
+        assert torch.equal(red.grad_shard, red.grad)  # one rank: the shard is the whole bucket
+        net = _mlp(0)
+        x = torch.randn(4, 12)
+        net(x).sum().backward()
+        before = [p.grad.clone() for p in net.parameters()]
+        assert comm.allreduce_grads(net.parameters()) > 0
+        assert all(torch.equal(a, p.grad) for a, p in zip(before, net.parameters()))
+    finally:
+        del os.environ["SKYRL_FORCE_COLLECTIVES"]
+    assert not comm._collective(1)
+
+
+def test_forced_collectives_one_rank_gloo():
+    _run(_forced_solo_case, world=1)
+
+
 # --------------------------------------------------------------------------- a12 layout
 def test_flat_layout_pieces_cover_every_index_once():
     for numel, world, bucket in ((1000, 2, 256), (4097, 4, 1024), (64, 1, 1 << 20), (123457, 8, 5000)):

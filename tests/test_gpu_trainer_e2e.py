@@ -82,7 +82,7 @@ def test_data_parallel_trainer_two_ranks_one_gpu():
     assert all(s["logprobs_diff_mean"] < 0.02 for s in res["steps"])
 
 
-def _run_optim_rehearsal(nproc):
+def _run_optim_rehearsal(nproc, rccl_solo=False):
     import json
     import os
     import socket
@@ -91,7 +91,10 @@ def _run_optim_rehearsal(nproc):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = os.path.join(root, "scripts", "rehearse_trainer_optim.py")
-    if nproc == 1:
+    env = dict(os.environ)
+    if rccl_solo:
+        env.update(SKYRL_FORCE_COLLECTIVES="1", REHEARSE_BACKEND="nccl")
+    if nproc == 1 and not rccl_solo:
         cmd = [sys.executable, script]
     else:
         with socket.socket() as s:
@@ -99,7 +102,7 @@ def _run_optim_rehearsal(nproc):
             port = s.getsockname()[1]
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                "--master-addr", "127.0.0.1", "--master-port", str(port), script]
-    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300, env=env)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stderr[-3000:]
     res = json.loads(lines[-1])
@@ -117,6 +120,16 @@ def test_hip_optimizer_trainer_matches_torch_adamw(nproc):
     equal the learner's bf16 cast bit for bit. 1 rank, and 2 ranks on one GPU over gloo."""
     res = _run_optim_rehearsal(nproc)
     assert res["world"] == nproc and len(res["steps"]) == 3
+
+
+def test_hip_optimizer_trainer_over_rccl_one_rank():
+    """The same check with the trainer's exchanges forced through RCCL on a one-rank group
+    (torchrun, nccl backend, SKYRL_FORCE_COLLECTIVES=1): the bucket reduce-scatters fired from
+    the backward hooks, the grad-norm all-reduce and the fp32 / bf16 all-gathers all run as
+    RCCL collectives on the comm stream, as at N > 1 (RCCL refuses two ranks on one GPU)."""
+    res = _run_optim_rehearsal(1, rccl_solo=True)
+    assert res["world"] == 1 and res["backend"] == "nccl" and res["collective_path"]
+    assert res["reduce_scatters_from_backward"] > 0 and len(res["steps"]) == 3
 
 
 def test_fused_policy_pass_matches_chunked_lmhead_path():
