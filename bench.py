@@ -383,6 +383,8 @@ def run(args):
         result["rollout_attention"] = rollout_attention_leg(dev, N)
     if not args.no_lmhead_leg:
         result["rollout_lmhead_sample"] = lmhead_sample_leg(dev, N)
+    if not args.no_filtered_leg:
+        result["sampler_filtered"] = sampler_filtered_leg(dev, N, V)
     if not args.no_vocab_legs:
         result["policy_train_vocabs"] = policy_train_vocab_legs(dev, mb, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -642,6 +644,44 @@ def lmhead_sample_leg(dev, nseq, reps=30):
     return out
 
 
+def sampler_filtered_leg(dev, nseq, V, reps=20):
+    """The §8(d) filter variant of the rollout sampler (top_k = 50 with top_p = 0.9, and top_k =
+    50 alone) at the decode step's shape [nseq, V] bf16, T = 1: the whole skyrl_sample call (the
+    one-pass top_k kernel; rows it hands back run the filter pre-pass + MODE 2 kernels, which
+    also launch and skip the rows it took), against the two-kernel path
+    (skyrl_tune sampler_topk_fast 0). Algorithmic bytes = one read of the logits + 16 B per row."""
+    from skyrl_amd import ops
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = (torch.randn(nseq, V, device=dev, generator=g) * 3).to(torch.bfloat16)
+    ids = torch.arange(nseq, dtype=torch.int64, device=dev)
+    tok = torch.empty(nseq, dtype=torch.int32, device=dev)
+    lp = torch.empty(nseq, dtype=torch.float32, device=dev)
+    nbytes = nseq * V * 2 + nseq * 16
+    out = {"shape": [nseq, V], "dtype": "bf16", "temperature": 1.0, "bytes_per_launch": nbytes}
+    for name, k, p in (("top_k50_top_p0.9", 50, 0.9), ("top_k50", 50, 1.0)):
+        res = {}
+        for fast in (1, 0):
+            ops._ffi.call("skyrl_tune", b"sampler_topk_fast", fast)
+            run = lambda: ops.sample(x, temperature=1.0, top_k=k, top_p=p, seed=3, seq_ids=ids, step=1,  # noqa: E731
+                                     tokens_out=tok, logp_out=lp)
+            run()
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                run()
+            b.record()
+            b.synchronize()
+            us = a.elapsed_time(b) * 1e3 / reps
+            gbs = nbytes / (us * 1e-6) / 1e9
+            res["one_pass" if fast else "two_kernel"] = {"avg_launch_us": round(us, 2), "achieved_GBps": round(gbs, 1),
+                                                         "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        ops._ffi.call("skyrl_tune", b"sampler_topk_fast", 1)
+        out[name] = res
+    return out
+
+
 def rollout_attention_leg(dev, nseq, reps=20):
     """Rollout decode attention (csrc/attention.hip paged_decode_kernel) at the
     headline shape: Qwen2.5-1.5B heads (12 q / 2 kv, D=128), one decode step of all nseq
@@ -779,6 +819,7 @@ def main():
     ap.add_argument("--no-attention-leg", action="store_true", help="skip the rollout paged-attention leg")
     ap.add_argument("--no-lmhead-leg", action="store_true", help="skip the decode lm_head + sampler leg")
     ap.add_argument("--no-vocab-legs", action="store_true", help="skip the per-vocabulary fused training pass legs")
+    ap.add_argument("--no-filtered-leg", action="store_true", help="skip the top_k / top_p sampler leg")
     ap.add_argument("--unfused", action="store_true", help="separate logprob/loss kernels instead of the fused pass")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--params", type=int, default=QWEN_1_5B_PARAMS, help="policy parameter count (0: no optimizer leg)")

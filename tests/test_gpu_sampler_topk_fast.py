@@ -1,0 +1,130 @@
+"""a1 filtered sampling: the one-pass top_k kernel (sample_topk_kernel) against the two-kernel
+path it short-cuts (the filter pre-pass + the MODE 2 sampler, skyrl_tune("sampler_topk_fast", 0))
+and against oracle/sampler_ref.c.
+
+The fast kernel decides every row whose per-thread top-8 lists provably hold the row's top k and
+hands the others back to the two-kernel path (RowFilter.ik = kRowDone marks the rows it took).
+Tokens must be bit-identical either way; logprobs agree to float rounding (the lse is summed in
+another order). Rows are chosen so that both outcomes occur: random rows (taken by the fast
+kernel), tie-heavy rows and mostly -inf rows (handed back), vocabularies smaller than the
+workgroup, top_k at the 128 limit and above it, f32 logits, misaligned row strides.
+"""
+
+import pytest
+import torch
+
+from skyrl_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+_COUNTER_BYTES = 256 * 4  # sampler workspace: per-row counters first, then one 20-B RowFilter per row
+_ROW_DONE = -2
+
+
+def _run(x, fast, **kw):
+    ops._ffi.call("skyrl_tune", b"sampler_topk_fast", int(fast))
+    try:
+        tok, lp = ops.sample(x, **kw)
+        torch.cuda.synchronize()
+        ws = ops.WORKSPACES.get(x.device, "sample", ops._ffi.query("skyrl_sample_workspace_bytes", x.shape[0],
+                                                                       x.shape[1]))
+        n = x.shape[0]
+        filt = ws[_COUNTER_BYTES:_COUNTER_BYTES + 20 * n].view(torch.int32).view(n, 5)
+        done = int((filt[:, 2] == _ROW_DONE).sum()) if fast else 0
+        return tok.cpu(), lp.cpu(), done
+    finally:
+        ops._ffi.call("skyrl_tune", b"sampler_topk_fast", 1)
+
+
+def _ab(x, min_done, **kw):
+    tf, lf, done = _run(x, True, **kw)
+    ts, ls, _ = _run(x, False, **kw)
+    assert torch.equal(tf, ts), (kw, int((tf != ts).sum()))
+    torch.testing.assert_close(lf, ls, atol=2e-5, rtol=1e-5)
+    assert done >= min_done, (kw, done, x.shape[0])
+    return tf, lf, done
+
+
+@pytest.mark.parametrize("cfg", [(1.0, 50, 1.0, 0.0), (1.0, 50, 0.9, 0.0), (0.7, 50, 0.9, 0.05), (1.3, 20, 0.5, 0.0),
+                                 (1.0, 128, 0.95, 0.0), (0.8, 1, 1.0, 0.0), (1.0, 50, 0.0, 0.0)])
+def test_topk_fast_equals_two_kernel_path_bench_shape(dev, cfg):
+    """[512, 151,936] bf16 N(0, 3^2) rows (the bench's decode step): every row is taken by the
+    fast kernel and the tokens equal the two-kernel path's."""
+    temp, k, p, mp = cfg
+    g = torch.Generator().manual_seed(k * 7 + 1)
+    x = (torch.randn(512, 151936, generator=g) * 3).to(torch.bfloat16).to(dev)
+    ids = torch.arange(512, dtype=torch.int64, device=dev) * 5 + 2
+    _ab(x, 500, temperature=temp, top_k=k, top_p=p, min_p=mp, seed=11, seq_ids=ids, step=4)
+
+
+def test_topk_fast_matches_oracle(dev):
+    """Small batches through both row-mode sizes against oracle/sampler_ref.c directly."""
+    from oracle import sampler as osamp
+
+    V = 32000
+    g = torch.Generator().manual_seed(3)
+    for n, (temp, k, p, mp) in ((5, (1.0, 50, 0.9, 0.0)), (300, (0.7, 40, 0.8, 0.02)), (64, (1.0, 3, 1.0, 0.0))):
+        x = (torch.randn(n, V, generator=g) * 2).to(torch.bfloat16)
+        ids = torch.arange(n, dtype=torch.int64) + 100
+        tok, lp, done = _run(x.to(dev), True, temperature=temp, top_k=k, top_p=p, min_p=mp, seed=5,
+                             seq_ids=ids.to(dev), step=7)
+        etok, elp = osamp.sample(x, temp, k, p, mp, 5, ids, 7)
+        assert done >= n - 2
+        assert torch.equal(tok, etok), (n, int((tok != etok).sum()))
+        torch.testing.assert_close(lp, elp, atol=1e-4, rtol=1e-4)
+
+
+def test_topk_fast_hands_back_tie_heavy_and_masked_rows(dev):
+    """Rows the per-thread lists cannot certify go back to the two-kernel path: few distinct
+    values (the k-th value sits in a tie group spread over many threads), and rows that are -inf
+    except for a handful of logits (fewer finite values than k). Tokens still equal."""
+    from oracle import sampler as osamp
+
+    V, n = 151936, 64
+    g = torch.Generator().manual_seed(8)
+    ties = torch.randint(0, 6, (n // 2, V), generator=g).float()
+    masked = torch.full((n // 2, V), float("-inf"))
+    cols = torch.randint(0, V, (n // 2, 20), generator=g)
+    masked.scatter_(1, cols, torch.randn(n // 2, 20, generator=g))
+    x = torch.cat([ties, masked]).to(torch.bfloat16)
+    ids = torch.arange(n, dtype=torch.int64)
+    tf, lf, done = _ab(x.to(dev), 0, temperature=1.0, top_k=50, top_p=0.9, seed=3, seq_ids=ids.to(dev), step=1)
+    assert done < n  # some rows were handed back
+    etok, _ = osamp.sample(x, 1.0, 50, 0.9, 0.0, 3, ids, 1)
+    assert torch.equal(tf, etok)
+
+
+@pytest.mark.parametrize("V,k", [(100, 50), (1000, 3), (4097, 128), (4097, 129), (517, 7)])
+def test_topk_fast_small_and_ragged_vocab(dev, V, k):
+    """Vocabularies with fewer elements than the workgroup has threads, ragged tails, the
+    top_k = 128 limit and one above it (the two-kernel path)."""
+    from oracle import sampler as osamp
+
+    g = torch.Generator().manual_seed(V + k)
+    n = 40
+    width = (V + 7) // 8 * 8 + 8  # row stride a multiple of 8 bf16: 16-B aligned rows
+    base = (torch.randn(n, width, generator=g) * 2).to(torch.bfloat16)
+    x = base.to(dev)[:, :V]
+    ids = torch.arange(n, dtype=torch.int64)
+    tf, lf, _ = _ab(x, 0, temperature=1.0, top_k=k, top_p=0.9, seed=9, seq_ids=ids.to(dev), step=2)
+    etok, elp = osamp.sample(base[:, :V].contiguous(), 1.0, k, 0.9, 0.0, 9, ids, 2)
+    assert torch.equal(tf, etok)
+
+
+def test_topk_fast_f32_and_misaligned_rows(dev):
+    """f32 logits (4 per vector, 32-bit keys: 8 radix steps), and bf16 rows whose stride is not a
+    multiple of 16 B (the two-kernel path)."""
+    from oracle import sampler as osamp
+
+    g = torch.Generator().manual_seed(21)
+    n = 96
+    xf = torch.randn(n, 50256, generator=g) * 3  # row stride 50,256 * 4 B: 16-B aligned
+    ids = torch.arange(n, dtype=torch.int64) * 11
+    tf, _, done = _ab(xf.to(dev), n - 4, temperature=0.9, top_k=50, top_p=0.9, seed=1, seq_ids=ids.to(dev), step=3)
+    etok, _ = osamp.sample(xf, 0.9, 50, 0.9, 0.0, 1, ids, 3)
+    assert torch.equal(tf, etok)
+    xb = torch.cat([xf, xf[:, :1]], dim=1).to(torch.bfloat16)  # stride 50,257 * 2 B: misaligned rows
+    tf, _, done = _ab(xb.to(dev), 0, temperature=0.9, top_k=50, top_p=0.9, seed=1, seq_ids=ids.to(dev), step=3)
+    assert done == 0
+    etok, _ = osamp.sample(xb, 0.9, 50, 0.9, 0.0, 1, ids, 3)
+    assert torch.equal(tf, etok)
