@@ -128,21 +128,21 @@ __device__ __forceinline__ bool in_cut(uint32_t kk, int i, uint32_t kcut, int ic
 // fixed-point masses (top_p) per level. The tie group at either cut is resolved by an
 // index-ordered count: the cut is a (key, last index) pair.
 constexpr int kFT = 1024;
-template <typename T>
-__global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict__ logits, int64_t ld, int V, int top_k,
-                                                            int use_minp, float inv_t, float ln_min_p, float top_p,
-                                                            RowFilter* __restrict__ out, int gate) {
-    if (gate && out[blockIdx.x].ik == -2) return;  // finished by sample_topk_kernel (kRowDone)
-    constexpr int NW = kFT / kWave;
+// One row's cuts with FT threads (the pre-pass kernel: 1024; the top_k fast path's fallback: 512).
+template <typename T, int FT>
+__device__ __forceinline__ void filter_row(const T* __restrict__ logits, int64_t ld, int V, int top_k, int use_minp,
+                                           float inv_t, float ln_min_p, float top_p, RowFilter* __restrict__ dst,
+                                           const int row_i) {
+    constexpr int NW = FT / kWave;
     constexpr int KB = sizeof(T) * 8;
     __shared__ unsigned long long hist[256];
     __shared__ unsigned long long s_red[NW], s_red2[NW];
-    __shared__ unsigned long long s_fine[kFT];
+    __shared__ unsigned long long s_fine[FT];
     __shared__ uint32_t s_u[NW];
     __shared__ uint32_t s_sel[2];               // selected d, found flag
     __shared__ unsigned long long s_below, s_at;
     __shared__ int s_ic;
-    const T* row = logits + (int64_t)blockIdx.x * ld;
+    const T* row = logits + (int64_t)row_i * ld;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
     constexpr int VEC = 16 / sizeof(T);
     // every pass visits the row in 16-B vectors where aligned (VEC elements per thread per
@@ -153,18 +153,18 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
     const int t0 = h0 + nv * VEC;
     auto for_each = [&](auto fn) {
         if ((reinterpret_cast<uintptr_t>(row) & (sizeof(T) - 1)) == 0) {
-            for (int i = threadIdx.x; i < h0; i += kFT) fn(row[i], i);
+            for (int i = threadIdx.x; i < h0; i += FT) fn(row[i], i);
             const uint4* rv = reinterpret_cast<const uint4*>(row + h0);
-            for (int j = threadIdx.x; j < nv; j += kFT) {
+            for (int j = threadIdx.x; j < nv; j += FT) {
                 const uint4 pk = rv[j];
                 T vals[VEC];
                 __builtin_memcpy(vals, &pk, 16);
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) fn(vals[k], h0 + j * VEC + k);
             }
-            for (int i = t0 + threadIdx.x; i < V; i += kFT) fn(row[i], i);
+            for (int i = t0 + threadIdx.x; i < V; i += FT) fn(row[i], i);
         } else {
-            for (int i = threadIdx.x; i < V; i += kFT) fn(row[i], i);
+            for (int i = threadIdx.x; i < V; i += FT) fn(row[i], i);
         }
     };
 
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
         unsigned long long below = 0ull, at = 0ull;
         for (int lvl = 0; lvl < KB / 8; ++lvl) {
             const int shift = KB - 8 * (lvl + 1);
-            for (int j = threadIdx.x; j < 256; j += kFT) hist[j] = 0ull;
+            for (int j = threadIdx.x; j < 256; j += FT) hist[j] = 0ull;
             __syncthreads();
             for_each([&](T raw, int i) {
                 const uint32_t d = kmax - okey<T>(raw);
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
     // within kFine steps of the max has its own bin; the rest is summed in registers), then a
     // block-wide scan of the bins. Falls back to the radix passes when the target is not
     // reached inside the window.
-    constexpr int kFine = kFT;
+    constexpr int kFine = FT;
     struct Sel { bool ok; uint32_t d; unsigned long long below, at, total; };
     auto fine = [&](auto weight, double target, bool want_total) -> Sel {
         unsigned long long* fh = reinterpret_cast<unsigned long long*>(s_fine);
@@ -274,13 +274,13 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
         return r;
     };
 
-    // index of the c-th (1-based) element in index order with pred(raw, i): rounds of kFT
+    // index of the c-th (1-based) element in index order with pred(raw, i): rounds of FT
     // contiguous chunks of CH elements (thread t owns [base + t*CH, base + (t+1)*CH))
     auto nth_index = [&](auto pred, long long c) -> int {
         constexpr int CH = 16;
         if (threadIdx.x == 0) s_ic = 0x7fffffff;
         long long seen = 0;
-        for (int base = 0; base < V; base += kFT * CH) {
+        for (int base = 0; base < V; base += FT * CH) {
             const int i0 = base + threadIdx.x * CH;
             int cntt = 0;
             for (int k = 0; k < CH; ++k) {
@@ -399,350 +399,13 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
                 ic = nth_index([&](T raw, int i) -> bool { return okey<T>(raw) == kc && kept(raw, i); }, c);
         }
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = RowFilter{mx, tk, ik, kc, ic};
+    if (threadIdx.x == 0) *dst = RowFilter{mx, tk, ik, kc, ic};
 }
-
-// ---- top_k fast path: the whole filtered decision in one pass over the row ------------------
-// With top_k set (k <= kFastK) every filter and the decision live in the row's k largest logits.
-// One 512-thread workgroup per row streams the row ONCE:
-//   * B: with the row's first 4 NT vectors in registers (the next 4 NT in flight), the k-th
-//     largest of the threads' maxima over them (4-bit radix select by wave ballots). At least k
-//     elements are >= B, so all of the row's top k are.
-//   * The pass: the raw online (max, sum-exp) for the logprob, and every element >= B appended
-//     to an LDS candidate list (about k V / (4 NT VEC) elements: 464 at k = 50, V = 151,936).
-//   * On chip: the k-th largest candidate key (radix select over LDS bins); the candidates at or
-//     above it ranked in the exact (key desc, index asc) order; top_k = rank < k; min_p = x/T >=
-//     max/T + ln min_p; top_p = the fixed-point masses (mass_q) summed exactly in rank order,
-//     kept while the mass before is < p Z (rank 0 always); the Gumbel-max decision over the
-//     admissible elements (noise_score, lowest index on ties).
-// These are the pre-pass's cut rules and MODE 2's exact scores on the same elements, so tokens
-// are those of the two-kernel path (and of oracle/sampler_ref.c) bit for bit. A row whose lists
-// overflow (tie-heavy rows, mostly -inf rows) is handed back: its RowFilter is marked pending and
-// the filter pre-pass + MODE 2 kernels, which launch after this one, take it (they return at once
-// on rows marked kRowDone).
-constexpr int kFastNT = 512;
-constexpr int kFastK = 128;      // largest top_k served here
-constexpr int kFastCap = 4096;   // candidates >= B
-constexpr int kFastCap2 = 512;   // candidates at or above the k-th largest key
-constexpr int32_t kRowDone = -2;  // RowFilter.ik marker of a row finished by the fast path
-
 template <typename T>
-__global__ __launch_bounds__(kFastNT) void sample_topk_kernel(const T* __restrict__ logits, int64_t ld, int V, int top_k,
-                                                              float inv_t, int use_minp, float ln_min_p, int use_topp,
-                                                              float top_p, uint64_t seed,
-                                                              const int64_t* __restrict__ seq_ids, int64_t step,
-                                                              int32_t* __restrict__ tokens, float* __restrict__ logp_out,
-                                                              RowFilter* __restrict__ filt) {
-    constexpr int NT = kFastNT, NW = NT / kWave, VEC = 16 / sizeof(T), KB = sizeof(T) * 8;
-    constexpr uint32_t KTOP = KB == 16 ? 0xffffu : 0xffffffffu;  // d = KTOP - key: smallest d = largest key
-    __shared__ float s_m[NW], s_s[NW];
-    __shared__ uint32_t s_kmax[NW];
-    __shared__ uint32_t s_rc[2][NW][16];
-    __shared__ uint32_t s_bin[3][16];
-    __shared__ uint32_t s_ckey[kFastCap];
-    __shared__ int32_t s_cidx[kFastCap];
-    __shared__ uint32_t s_fkey[kFastCap2];
-    __shared__ int32_t s_fidx[kFastCap2];
-    __shared__ int32_t s_frank[kFastCap2];
-    __shared__ uint32_t s_mass[kFastK];
-    __shared__ unsigned long long s_before[kFastK];
-    __shared__ unsigned long long s_wsum[NW];
-    __shared__ uint32_t s_cc, s_fc;
-    __shared__ float s_bs[NW];
-    __shared__ int32_t s_bi[NW];
-    const int row_i = blockIdx.x;
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    const T* row = logits + (int64_t)row_i * ld;
-    if (threadIdx.x == 0) {
-        s_cc = 0u;
-        s_fc = 0u;
-    }
-    if (threadIdx.x < 32) s_bin[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
-
-    // ---- prologue: the first 4 NT vectors (the next 4 NT in flight) and their per-thread max
-    const uint4* rv = reinterpret_cast<const uint4*>(row);  // 16-B aligned (host check)
-    const int nvec = V / VEC;
-    constexpr int kStep = 4 * NT;
-    const int nfull = (nvec / kStep) * kStep;
-    uint4 cur[4], nxt[4];
-    if (nfull > 0) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
-        if (kStep < nfull) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + kStep + u * NT + threadIdx.x);
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = u * NT + threadIdx.x;
-            cur[u] = i < nvec ? ld_stream(rv + i) : make_uint4(0u, 0u, 0u, 0u);
-        }
-    }
-    uint32_t km0 = 0u;
-    bool has0 = false;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        if (u * NT + (int)threadIdx.x < nvec) {
-            has0 = true;
-            T raw[VEC];
-            __builtin_memcpy(raw, &cur[u], 16);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) km0 = max(km0, okey<T>(raw[k]));
-        }
-    }
-    // B = the k-th largest of km0 over the threads that hold a vector (radix select on d)
-    const uint32_t d0 = has0 ? KTOP - km0 : 0xffffffffu;
-    uint32_t P = 0u;
-    int below = 0;
-#pragma unroll
-    for (int st = 0; st < KB / 4; ++st) {
-        const int sh = KB - 4 * (st + 1);
-        const bool match = st == 0 ? (KB == 32 ? has0 : d0 <= 0xffffu) : ((d0 >> (sh + 4)) == P);
-        const uint32_t dig = (d0 >> sh) & 15u;
-        uint32_t mine = 0u;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(match && dig == (uint32_t)q));
-            if (lane == q) mine = c;
-        }
-        if (lane < 16) s_rc[st & 1][w][lane] = mine;
-        __syncthreads();
-        uint32_t tq = 0u;  // lane q: the workgroup's count of digit q
-        if (lane < 16) {
-#pragma unroll
-            for (int j = 0; j < NW; ++j) tq += s_rc[st & 1][j][lane];
-        }
-        uint32_t incl = tq;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const uint32_t o = (uint32_t)__shfl_up((int)incl, off, kWave);
-            if (lane >= off) incl += o;
-        }
-        const uint64_t hit = __builtin_amdgcn_ballot_w64(lane < 16 && below + (int)incl >= top_k);
-        const int q = hit ? __builtin_ctzll(hit) : 15;
-        below += (int)__shfl((int)(incl - tq), q, kWave);
-        P = (P << 4) | (uint32_t)q;
-    }
-    // fewer than k threads hold a vector: no bound, every element is a candidate
-    const int n_ne = __syncthreads_count(has0);
-    const float bf = n_ne < top_k ? -INFINITY : from_key<T>(KTOP - P);
-
-    // ---- the pass: lse of the raw logits; every element >= B into the candidate list
-    float m = -1e30f, s = 0.f;
-    uint32_t kmx = 0u;
-    auto append = [&](uint32_t kk, int idx) {
-        const uint32_t pos = atomicAdd(&s_cc, 1u);
-        if (pos < (uint32_t)kFastCap) {
-            s_ckey[pos] = kk;
-            s_cidx[pos] = idx;
-        }
-        kmx = max(kmx, kk);
-    };
-    auto visit = [&](const uint4& pk, int v0) {
-        T raw[VEC];
-        __builtin_memcpy(raw, &pk, 16);
-        float x[VEC];
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) x[k] = to_f<T>(raw[k]);
-        float vmax = x[0];
-#pragma unroll
-        for (int k = 1; k < VEC; ++k) vmax = fmaxf(vmax, x[k]);
-        const float mn = fmaxf(m, vmax);
-        float acc = s * fast_exp2((m - mn) * kLog2e);
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) acc += fast_exp2((x[k] - mn) * kLog2e);
-        s = acc;
-        m = mn;
-        if (vmax >= bf) {  // a float compare admits every key >= key(B) (-0 beside +0 as well)
-#pragma unroll
-            for (int k = 0; k < VEC; ++k)
-                if (x[k] >= bf) append(okey<T>(raw[k]), v0 + k);
-        }
-    };
-    if (nfull > 0) {
-        for (int base = 0; base < nfull; base += kStep) {
-            const bool more = base + kStep < nfull;
-            if (more && base > 0) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) visit(cur[u], (base + u * NT + threadIdx.x) * VEC);
-            if (more) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-            }
-        }
-        for (int i = nfull + threadIdx.x; i < nvec; i += NT) visit(ld_stream(rv + i), i * VEC);
-    } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u * NT + (int)threadIdx.x < nvec) visit(cur[u], (u * NT + threadIdx.x) * VEC);
-    }
-    for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
-        const float x = to_f<T>(row[i]);
-        const float mn = fmaxf(m, x);
-        s = s * fast_exp2((m - mn) * kLog2e) + fast_exp2((x - mn) * kLog2e);
-        m = mn;
-        if (x >= bf) append(okey<T>(row[i]), i);
-    }
-
-    // ---- row lse and max key (the max element is a candidate)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float om = __shfl_xor(m, off, kWave);
-        const float os = __shfl_xor(s, off, kWave);
-        const float mn = fmaxf(m, om);
-        s = s * fast_exp2((m - mn) * kLog2e) + os * fast_exp2((om - mn) * kLog2e);
-        m = mn;
-        kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, off, kWave));
-    }
-    if (lane == 0) {
-        s_m[w] = m;
-        s_s[w] = s;
-        s_kmax[w] = kmx;
-    }
-    __syncthreads();
-    float M = s_m[0], S = s_s[0];
-    uint32_t kmax = s_kmax[0];
-#pragma unroll
-    for (int j = 1; j < NW; ++j) {
-        const float mn = fmaxf(M, s_m[j]);
-        S = S * fast_exp2((M - mn) * kLog2e) + s_s[j] * fast_exp2((s_m[j] - mn) * kLog2e);
-        M = mn;
-        kmax = max(kmax, s_kmax[j]);
-    }
-    const float lse = M + fast_log2(S) * kLn2;
-    const float mx = from_key<T>(kmax);
-    const int C = (int)s_cc;
-    if (C > kFastCap || C < top_k) {
-        if (threadIdx.x == 0) filt[row_i].ik = 0;  // pending: the pre-pass + MODE 2 kernels take this row
-        return;
-    }
-
-    // ---- the k-th largest candidate key: radix select over LDS bins (3 rotating bin sets)
-    uint32_t Pc = 0u;
-    int above = 0;
-#pragma unroll
-    for (int st = 0; st < KB / 4; ++st) {
-        const int sh = KB - 4 * (st + 1);
-        uint32_t* bin = s_bin[st % 3];
-        for (int i = threadIdx.x; i < C; i += NT) {
-            const uint32_t d = KTOP - s_ckey[i];
-            if (st == 0 || (d >> (sh + 4)) == Pc) atomicAdd(&bin[(d >> sh) & 15u], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < 16) s_bin[(st + 2) % 3][threadIdx.x] = 0u;  // last read a step ago, next used in two
-        int cum = above, q = 15;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int c = (int)bin[j];
-            if (cum + c >= top_k) {
-                q = j;
-                break;
-            }
-            cum += c;
-        }
-        above = cum;
-        Pc = (Pc << 4) | (uint32_t)q;
-    }
-    const uint32_t tkey = KTOP - Pc;  // the k-th largest key; `above` candidates are larger
-
-    // ---- candidates at or above it, ranked in (key desc, index asc) order
-    for (int i = threadIdx.x; i < C; i += NT) {
-        const uint32_t kk = s_ckey[i];
-        if (kk >= tkey) {
-            const uint32_t pos = atomicAdd(&s_fc, 1u);
-            if (pos < (uint32_t)kFastCap2) {
-                s_fkey[pos] = kk;
-                s_fidx[pos] = s_cidx[i];
-            }
-        }
-    }
-    for (int r = threadIdx.x; r < top_k; r += NT) s_mass[r] = 0u;
-    __syncthreads();
-    const int F = (int)s_fc;
-    if (F > kFastCap2) {  // a tie group too large for the exact ranking here
-        if (threadIdx.x == 0) filt[row_i].ik = 0;
-        return;
-    }
-    for (int i = threadIdx.x; i < F; i += NT) {
-        const uint32_t ki = s_fkey[i];
-        const int ii = s_fidx[i];
-        int r = 0;
-        for (int j = 0; j < F; ++j) {
-            const uint32_t kj = s_fkey[j];
-            r += (kj > ki || (kj == ki && s_fidx[j] < ii)) ? 1 : 0;
-        }
-        s_frank[i] = r;
-    }
-    __syncthreads();
-
-    // ---- filters on the ranked candidates
-    const float mthr = mx * inv_t + ln_min_p;
-    unsigned long long Z = 0ull;
-    if (use_topp) {
-        for (int i = threadIdx.x; i < F; i += NT) {
-            const int r = s_frank[i];
-            if (r < top_k) {
-                const float x = from_key<T>(s_fkey[i]);
-                if (!use_minp || x * inv_t >= mthr) s_mass[r] = mass_q(x, mx, inv_t);
-            }
-        }
-        __syncthreads();
-        // exclusive scan of the masses in rank order (ranks < k <= NT: one per thread)
-        const unsigned long long mine = (int)threadIdx.x < top_k ? (unsigned long long)s_mass[threadIdx.x] : 0ull;
-        unsigned long long incl = mine;
-#pragma unroll
-        for (int off = 1; off < kWave; off <<= 1) {
-            const unsigned long long o = (unsigned long long)__shfl_up((long long)incl, off, kWave);
-            if (lane >= off) incl += o;
-        }
-        if (lane == kWave - 1) s_wsum[w] = incl;
-        __syncthreads();
-        unsigned long long off_w = 0ull;
-        for (int j = 0; j < NW; ++j) {
-            if (j < w) off_w += s_wsum[j];
-            Z += s_wsum[j];
-        }
-        if ((int)threadIdx.x < top_k) s_before[threadIdx.x] = off_w + incl - mine;
-        __syncthreads();
-    }
-    const double target = (double)top_p * (double)Z;
-    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
-    const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
-    Best best{-INFINITY, 0x7fffffff};
-    for (int i = threadIdx.x; i < F; i += NT) {
-        const int r = s_frank[i];
-        if (r >= top_k) continue;
-        const float x = from_key<T>(s_fkey[i]);
-        if (use_minp && !(x * inv_t >= mthr)) continue;
-        if (use_topp && r != 0 && !((double)s_before[r] < target)) continue;
-        const int v = s_fidx[i];
-        const uint32_t h = ehash(key, keyb, (uint32_t)v >> 3);
-        const float sc = noise_score(x, inv_t, v, h, group_min_e(h), key2);
-        if (better(sc, v, best)) best = Best{sc, v};
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float os = __shfl_xor(best.score, off, kWave);
-        const int oi = __shfl_xor(best.idx, off, kWave);
-        if (better(os, oi, best)) best = Best{os, oi};
-    }
-    if (lane == 0) {
-        s_bs[w] = best.score;
-        s_bi[w] = best.idx;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        Best b{s_bs[0], s_bi[0]};
-        for (int j = 1; j < NW; ++j)
-            if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
-        tokens[row_i] = b.idx;
-        if (logp_out) logp_out[row_i] = to_f<T>(row[b.idx]) - lse;
-        filt[row_i].ik = kRowDone;
-    }
+__global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict__ logits, int64_t ld, int V, int top_k,
+                                                            int use_minp, float inv_t, float ln_min_p, float top_p,
+                                                            RowFilter* __restrict__ out) {
+    filter_row<T, kFT>(logits, ld, V, top_k, use_minp, inv_t, ln_min_p, top_p, out + blockIdx.x, blockIdx.x);
 }
 
 // MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p,
@@ -777,7 +440,7 @@ __device__ __forceinline__ void sample_unit(
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     int use_topp_rt, const RowFilter* __restrict__ filt, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters, const int row_i,
-    const int split, const int nsplit) {
+    const int split, const int nsplit, const int frow) {
     constexpr int NW = NT / kWave;
     SPHASE(0);
     __shared__ Part s_part[NW];
@@ -792,11 +455,11 @@ __device__ __forceinline__ void sample_unit(
     const bool use_topk = MODE == 2 && use_topk_rt;
     const bool use_minp = MODE == 2 && use_minp_rt;
     const bool use_topp = MODE == 2 && use_topp_rt;
-    const uint32_t tk = use_topk ? filt[row_i].tk : 0u;
-    const int ik = use_topk ? filt[row_i].ik : 0;
-    const float mthr = use_minp ? filt[row_i].rmax * inv_t + ln_min_p : 0.f;
-    const uint32_t kc = use_topp ? filt[row_i].kc : 0u;
-    const int ic = use_topp ? filt[row_i].ic : 0;
+    const uint32_t tk = use_topk ? filt[frow].tk : 0u;  // frow: this row's filter (row_i, or 0 of a local copy)
+    const int ik = use_topk ? filt[frow].ik : 0;
+    const float mthr = use_minp ? filt[frow].rmax * inv_t + ln_min_p : 0.f;
+    const uint32_t kc = use_topp ? filt[frow].kc : 0u;
+    const int ic = use_topp ? filt[frow].ic : 0;
     // the filtered distribution's support (MODE 2): top_k, min_p, top_p
     auto admissible = [&](T rawk, float xk, int v) -> bool {
         bool keep = true;
@@ -1259,10 +922,370 @@ __device__ __forceinline__ void sample_unit(
 // Static grid: block (row, split).
 template <typename T, int MODE, int NT, bool PRIO = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(SKYRL_SAMPLE_ARGS) {
-    if constexpr (MODE == 2) {  // use_topk_rt 2: the top_k fast path ran first; skip the rows it finished
-        if (use_topk_rt == 2 && filt[blockIdx.x].ik == kRowDone) return;
+    sample_unit<T, MODE, NT, PRIO>(SKYRL_SAMPLE_PASS, blockIdx.x, blockIdx.y, gridDim.y, blockIdx.x);
+}
+
+// ---- top_k fast path: the whole filtered decision in one pass over the row ------------------
+// With top_k set (k <= kFastK) every filter and the decision live in the row's k largest logits.
+// One 512-thread workgroup per row streams the row ONCE:
+//   * B: with the row's first 4 NT vectors in registers (the next 4 NT in flight), the k-th
+//     largest of the threads' maxima over them (4-bit radix select by wave ballots). At least k
+//     elements are >= B, so all of the row's top k are.
+//   * The pass: the raw online (max, sum-exp) for the logprob, and every element >= B appended
+//     to an LDS candidate list (about k V / (4 NT VEC) elements: 464 at k = 50, V = 151,936).
+//   * On chip: the k-th largest candidate key (radix select over LDS bins); the candidates at or
+//     above it ranked in the exact (key desc, index asc) order; top_k = rank < k; min_p = x/T >=
+//     max/T + ln min_p; top_p = the fixed-point masses (mass_q) summed exactly in rank order,
+//     kept while the mass before is < p Z (rank 0 always); the Gumbel-max decision over the
+//     admissible elements (noise_score, lowest index on ties).
+// These are the pre-pass's cut rules and MODE 2's exact scores on the same elements, so tokens
+// are those of the two-kernel path (and of oracle/sampler_ref.c) bit for bit. A row whose lists
+// overflow (tie-heavy rows, mostly -inf rows) runs the two-kernel path's code in this workgroup
+// (filter_row with 512 threads, then sample_unit MODE 2 on the row).
+constexpr int kFastNT = 512;
+constexpr int kFastK = 128;      // largest top_k served here
+constexpr int kFastCap = 4096;   // candidates >= B
+constexpr int kFastCap2 = 512;   // candidates at or above the k-th largest key
+constexpr int32_t kRowDone = -2;      // RowFilter.ik markers (for tests): the row was decided by the fast path,
+constexpr int32_t kRowFallback = -3;  // or by its in-kernel fallback (the pre-pass's cuts + MODE 2)
+
+template <typename T>
+__device__ __attribute__((noinline)) void topk_fallback(const T* __restrict__ logits, int64_t ld, int V, int top_k,
+                                                        float inv_t, int use_minp, float ln_min_p, int use_topp,
+                                                        float top_p, uint64_t seed, const int64_t* __restrict__ seq_ids,
+                                                        int64_t step, int32_t* __restrict__ tokens,
+                                                        float* __restrict__ logp_out, RowFilter* rf, int row_i) {
+    filter_row<T, kFastNT>(logits, ld, V, top_k, use_minp, inv_t, ln_min_p, use_topp ? top_p : 1.0f, rf, row_i);
+    __syncthreads();
+    sample_unit<T, 2, kFastNT, false>(logits, ld, V, V, inv_t, 1, use_minp, ln_min_p, seed, seq_ids, step, use_topp, rf,
+                                      tokens, logp_out, nullptr, nullptr, row_i, 0, 1, 0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topk_kernel(const T* __restrict__ logits, int64_t ld, int V, int top_k,
+                                                              float inv_t, int use_minp, float ln_min_p, int use_topp,
+                                                              float top_p, uint64_t seed,
+                                                              const int64_t* __restrict__ seq_ids, int64_t step,
+                                                              int32_t* __restrict__ tokens, float* __restrict__ logp_out,
+                                                              RowFilter* __restrict__ filt) {
+    constexpr int NT = kFastNT, NW = NT / kWave, VEC = 16 / sizeof(T), KB = sizeof(T) * 8;
+    constexpr uint32_t KTOP = KB == 16 ? 0xffffu : 0xffffffffu;  // d = KTOP - key: smallest d = largest key
+    __shared__ float s_m[NW], s_s[NW];
+    __shared__ uint32_t s_kmax[NW];
+    __shared__ uint32_t s_rc[2][NW][16];
+    __shared__ uint32_t s_bin[3][16];
+    __shared__ uint32_t s_ckey[kFastCap];
+    __shared__ int32_t s_cidx[kFastCap];
+    __shared__ uint32_t s_fkey[kFastCap2];
+    __shared__ int32_t s_fidx[kFastCap2];
+    __shared__ int32_t s_frank[kFastCap2];
+    __shared__ uint32_t s_mass[kFastK];
+    __shared__ unsigned long long s_before[kFastK];
+    __shared__ unsigned long long s_wsum[NW];
+    __shared__ uint32_t s_cc, s_fc;
+    __shared__ float s_bs[NW];
+    __shared__ int32_t s_bi[NW];
+    __shared__ RowFilter s_rf;
+    const int row_i = blockIdx.x;
+    // a row the candidate lists cannot settle: the pre-pass's cuts and the MODE 2 decision, here
+    // (a call, not inlined: its registers would otherwise crowd the streaming loop)
+    auto fallback = [&]() {
+        topk_fallback<T>(logits, ld, V, top_k, inv_t, use_minp, ln_min_p, use_topp, top_p, seed, seq_ids, step, tokens,
+                         logp_out, &s_rf, row_i);
+        if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
+    };
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const T* row = logits + (int64_t)row_i * ld;
+    if (threadIdx.x == 0) {
+        s_cc = 0u;
+        s_fc = 0u;
     }
-    sample_unit<T, MODE, NT, PRIO>(SKYRL_SAMPLE_PASS, blockIdx.x, blockIdx.y, gridDim.y);
+    if (threadIdx.x < 32) s_bin[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
+
+    // ---- prologue: the first 4 NT vectors (the next 4 NT in flight) and their per-thread max
+    const uint4* rv = reinterpret_cast<const uint4*>(row);  // 16-B aligned (host check)
+    const int nvec = V / VEC;
+    constexpr int kStep = 4 * NT;
+    const int nfull = (nvec / kStep) * kStep;
+    uint4 cur[4], nxt[4];
+    if (nfull > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
+        if (kStep < nfull) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + kStep + u * NT + threadIdx.x);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = u * NT + threadIdx.x;
+            cur[u] = i < nvec ? ld_stream(rv + i) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    uint32_t km0 = 0u;
+    bool has0 = false;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (u * NT + (int)threadIdx.x < nvec) {
+            has0 = true;
+            T raw[VEC];
+            __builtin_memcpy(raw, &cur[u], 16);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) km0 = max(km0, okey<T>(raw[k]));
+        }
+    }
+    // B = the k-th largest of km0 over the threads that hold a vector (radix select on d)
+    const uint32_t d0 = has0 ? KTOP - km0 : 0xffffffffu;
+    uint32_t P = 0u;
+    int below = 0;
+#pragma unroll
+    for (int st = 0; st < KB / 4; ++st) {
+        const int sh = KB - 4 * (st + 1);
+        const bool match = st == 0 ? (KB == 32 ? has0 : d0 <= 0xffffu) : ((d0 >> (sh + 4)) == P);
+        const uint32_t dig = (d0 >> sh) & 15u;
+        uint32_t mine = 0u;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(match && dig == (uint32_t)q));
+            if (lane == q) mine = c;
+        }
+        if (lane < 16) s_rc[st & 1][w][lane] = mine;
+        __syncthreads();
+        uint32_t tq = 0u;  // lane q: the workgroup's count of digit q
+        if (lane < 16) {
+#pragma unroll
+            for (int j = 0; j < NW; ++j) tq += s_rc[st & 1][j][lane];
+        }
+        uint32_t incl = tq;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)incl, off, kWave);
+            if (lane >= off) incl += o;
+        }
+        const uint64_t hit = __builtin_amdgcn_ballot_w64(lane < 16 && below + (int)incl >= top_k);
+        const int q = hit ? __builtin_ctzll(hit) : 15;
+        below += (int)__shfl((int)(incl - tq), q, kWave);
+        P = (P << 4) | (uint32_t)q;
+    }
+    // fewer than k threads hold a vector: no bound, every element is a candidate
+    const int n_ne = __syncthreads_count(has0);
+    const float bf = n_ne < top_k ? -INFINITY : from_key<T>(KTOP - P);
+
+    // ---- the pass: lse of the raw logits; every element >= B into the candidate list
+    float m = -1e30f, s = 0.f;
+    uint32_t kmx = 0u;
+    auto append = [&](uint32_t kk, int idx) {
+        const uint32_t pos = atomicAdd(&s_cc, 1u);
+        if (pos < (uint32_t)kFastCap) {
+            s_ckey[pos] = kk;
+            s_cidx[pos] = idx;
+        }
+        kmx = max(kmx, kk);
+    };
+    auto visit = [&](const uint4& pk, int v0) {
+        T raw[VEC];
+        __builtin_memcpy(raw, &pk, 16);
+        float x[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = to_f<T>(raw[k]);
+        float vmax = x[0];
+#pragma unroll
+        for (int k = 1; k < VEC; ++k) vmax = fmaxf(vmax, x[k]);
+        const float mn = fmaxf(m, vmax);
+        float acc = s * fast_exp2((m - mn) * kLog2e);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc += fast_exp2((x[k] - mn) * kLog2e);
+        s = acc;
+        m = mn;
+        if (vmax >= bf) {  // a float compare admits every key >= key(B) (-0 beside +0 as well)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k)
+                if (x[k] >= bf) append(okey<T>(raw[k]), v0 + k);
+        }
+    };
+    if (nfull > 0) {
+        for (int base = 0; base < nfull; base += kStep) {
+            const bool more = base + kStep < nfull;
+            if (more && base > 0) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) visit(cur[u], (base + u * NT + threadIdx.x) * VEC);
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+            }
+        }
+        for (int i = nfull + threadIdx.x; i < nvec; i += NT) visit(ld_stream(rv + i), i * VEC);
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u * NT + (int)threadIdx.x < nvec) visit(cur[u], (u * NT + threadIdx.x) * VEC);
+    }
+    for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
+        const float x = to_f<T>(row[i]);
+        const float mn = fmaxf(m, x);
+        s = s * fast_exp2((m - mn) * kLog2e) + fast_exp2((x - mn) * kLog2e);
+        m = mn;
+        if (x >= bf) append(okey<T>(row[i]), i);
+    }
+
+    // ---- row lse and max key (the max element is a candidate)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float om = __shfl_xor(m, off, kWave);
+        const float os = __shfl_xor(s, off, kWave);
+        const float mn = fmaxf(m, om);
+        s = s * fast_exp2((m - mn) * kLog2e) + os * fast_exp2((om - mn) * kLog2e);
+        m = mn;
+        kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, off, kWave));
+    }
+    if (lane == 0) {
+        s_m[w] = m;
+        s_s[w] = s;
+        s_kmax[w] = kmx;
+    }
+    __syncthreads();
+    float M = s_m[0], S = s_s[0];
+    uint32_t kmax = s_kmax[0];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) {
+        const float mn = fmaxf(M, s_m[j]);
+        S = S * fast_exp2((M - mn) * kLog2e) + s_s[j] * fast_exp2((s_m[j] - mn) * kLog2e);
+        M = mn;
+        kmax = max(kmax, s_kmax[j]);
+    }
+    const float lse = M + fast_log2(S) * kLn2;
+    const float mx = from_key<T>(kmax);
+    const int C = (int)s_cc;
+    if (C > kFastCap || C < top_k) {
+        fallback();
+        return;
+    }
+
+    // ---- the k-th largest candidate key: radix select over LDS bins (3 rotating bin sets)
+    uint32_t Pc = 0u;
+    int above = 0;
+#pragma unroll
+    for (int st = 0; st < KB / 4; ++st) {
+        const int sh = KB - 4 * (st + 1);
+        uint32_t* bin = s_bin[st % 3];
+        for (int i = threadIdx.x; i < C; i += NT) {
+            const uint32_t d = KTOP - s_ckey[i];
+            if (st == 0 || (d >> (sh + 4)) == Pc) atomicAdd(&bin[(d >> sh) & 15u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 16) s_bin[(st + 2) % 3][threadIdx.x] = 0u;  // last read a step ago, next used in two
+        int cum = above, q = 15;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int c = (int)bin[j];
+            if (cum + c >= top_k) {
+                q = j;
+                break;
+            }
+            cum += c;
+        }
+        above = cum;
+        Pc = (Pc << 4) | (uint32_t)q;
+    }
+    const uint32_t tkey = KTOP - Pc;  // the k-th largest key; `above` candidates are larger
+
+    // ---- candidates at or above it, ranked in (key desc, index asc) order
+    for (int i = threadIdx.x; i < C; i += NT) {
+        const uint32_t kk = s_ckey[i];
+        if (kk >= tkey) {
+            const uint32_t pos = atomicAdd(&s_fc, 1u);
+            if (pos < (uint32_t)kFastCap2) {
+                s_fkey[pos] = kk;
+                s_fidx[pos] = s_cidx[i];
+            }
+        }
+    }
+    for (int r = threadIdx.x; r < top_k; r += NT) s_mass[r] = 0u;
+    __syncthreads();
+    const int F = (int)s_fc;
+    if (F > kFastCap2) {  // a tie group too large for the exact ranking here
+        fallback();
+        return;
+    }
+    for (int i = threadIdx.x; i < F; i += NT) {
+        const uint32_t ki = s_fkey[i];
+        const int ii = s_fidx[i];
+        int r = 0;
+        for (int j = 0; j < F; ++j) {
+            const uint32_t kj = s_fkey[j];
+            r += (kj > ki || (kj == ki && s_fidx[j] < ii)) ? 1 : 0;
+        }
+        s_frank[i] = r;
+    }
+    __syncthreads();
+
+    // ---- filters on the ranked candidates
+    const float mthr = mx * inv_t + ln_min_p;
+    unsigned long long Z = 0ull;
+    if (use_topp) {
+        for (int i = threadIdx.x; i < F; i += NT) {
+            const int r = s_frank[i];
+            if (r < top_k) {
+                const float x = from_key<T>(s_fkey[i]);
+                if (!use_minp || x * inv_t >= mthr) s_mass[r] = mass_q(x, mx, inv_t);
+            }
+        }
+        __syncthreads();
+        // exclusive scan of the masses in rank order (ranks < k <= NT: one per thread)
+        const unsigned long long mine = (int)threadIdx.x < top_k ? (unsigned long long)s_mass[threadIdx.x] : 0ull;
+        unsigned long long incl = mine;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const unsigned long long o = (unsigned long long)__shfl_up((long long)incl, off, kWave);
+            if (lane >= off) incl += o;
+        }
+        if (lane == kWave - 1) s_wsum[w] = incl;
+        __syncthreads();
+        unsigned long long off_w = 0ull;
+        for (int j = 0; j < NW; ++j) {
+            if (j < w) off_w += s_wsum[j];
+            Z += s_wsum[j];
+        }
+        if ((int)threadIdx.x < top_k) s_before[threadIdx.x] = off_w + incl - mine;
+        __syncthreads();
+    }
+    const double target = (double)top_p * (double)Z;
+    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
+    const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
+    Best best{-INFINITY, 0x7fffffff};
+    for (int i = threadIdx.x; i < F; i += NT) {
+        const int r = s_frank[i];
+        if (r >= top_k) continue;
+        const float x = from_key<T>(s_fkey[i]);
+        if (use_minp && !(x * inv_t >= mthr)) continue;
+        if (use_topp && r != 0 && !((double)s_before[r] < target)) continue;
+        const int v = s_fidx[i];
+        const uint32_t h = ehash(key, keyb, (uint32_t)v >> 3);
+        const float sc = noise_score(x, inv_t, v, h, group_min_e(h), key2);
+        if (better(sc, v, best)) best = Best{sc, v};
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(best.score, off, kWave);
+        const int oi = __shfl_xor(best.idx, off, kWave);
+        if (better(os, oi, best)) best = Best{os, oi};
+    }
+    if (lane == 0) {
+        s_bs[w] = best.score;
+        s_bi[w] = best.idx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Best b{s_bs[0], s_bi[0]};
+        for (int j = 1; j < NW; ++j)
+            if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
+        tokens[row_i] = b.idx;
+        if (logp_out) logp_out[row_i] = to_f<T>(row[b.idx]) - lse;
+        filt[row_i].ik = kRowDone;
+    }
 }
 
 int splits_for(int nseq, int V) {
@@ -1313,19 +1336,18 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
     const float ln_min_p = use_minp ? det_ln(min_p) : 0.f;
     const T* lg = reinterpret_cast<const T*>(logits);
-    // top_k <= kFastK on 16-B aligned rows: the one-pass kernel decides every row it can; the
-    // pre-pass and MODE 2 kernels then only run the rows it handed back (usually none)
+    // top_k <= kFastK on 16-B aligned rows: the one-pass kernel alone (rows its candidate lists
+    // cannot settle run the pre-pass's and MODE 2's code inside it)
     const bool fast = g_sampler_topk_fast && use_topk && top_k <= kFastK &&
                       (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && ((ld * (int64_t)sizeof(T)) & 15) == 0;
     if (fast) {
         hipLaunchKernelGGL(sample_topk_kernel<T>, dim3(nseq), dim3(kFastNT), 0, stream, lg, ld, V, top_k, inv_t, use_minp,
                            ln_min_p, use_topp, use_topp ? top_p : 1.0f, seed, seq_ids, step, tokens, logp, filt);
-        int rc = check_launch("sample_topk_kernel");
-        if (rc) return rc;
+        return check_launch("sample_topk_kernel");
     }
     if (use_topk || use_minp || use_topp) {
         hipLaunchKernelGGL(sample_filter_kernel<T>, dim3(nseq), dim3(kFT), 0, stream, lg, ld, V, use_topk ? top_k : 0,
-                           use_minp, inv_t, ln_min_p, use_topp ? top_p : 1.0f, filt, (int)fast);
+                           use_minp, inv_t, ln_min_p, use_topp ? top_p : 1.0f, filt);
         int rc = check_launch("sample_filter_kernel");
         if (rc) return rc;
     }
@@ -1335,8 +1357,8 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         launch_mode<T, 0>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
                           filt, tokens, logp, parts, counters);
     else if (use_topk || use_minp || use_topp)
-        launch_mode<T, 2>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, fast ? 2 : use_topk, use_minp, ln_min_p, seed,
-                          seq_ids, step, use_topp, filt, tokens, logp, parts, counters);
+        launch_mode<T, 2>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, use_topk, use_minp, ln_min_p, seed, seq_ids,
+                          step, use_topp, filt, tokens, logp, parts, counters);
     else if (temperature == 1.0f)
         launch_mode<T, 3>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
                           filt, tokens, logp, parts, counters);

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 _COUNTER_BYTES = 256 * 4  # sampler workspace: per-row counters first, then one 20-B RowFilter per row
 _ROW_DONE = -2
+_ROW_FALLBACK = -3
 
 
 def _run(x, fast, **kw):
@@ -31,6 +32,9 @@ def _run(x, fast, **kw):
         n = x.shape[0]
         filt = ws[_COUNTER_BYTES:_COUNTER_BYTES + 20 * n].view(torch.int32).view(n, 5)
         done = int((filt[:, 2] == _ROW_DONE).sum()) if fast else 0
+        if fast and (x.data_ptr() % 16 == 0 and x.stride(0) * x.element_size() % 16 == 0 and 0 < kw.get("top_k", -1) <= 128
+                     and kw.get("temperature", 1.0) > 0):
+            assert int(((filt[:, 2] == _ROW_DONE) | (filt[:, 2] == _ROW_FALLBACK)).sum()) == n
         return tok.cpu(), lp.cpu(), done
     finally:
         ops._ffi.call("skyrl_tune", b"sampler_topk_fast", 1)
