@@ -59,7 +59,9 @@ int skyrl_abi_version(void);
  * "attn_pf" {0 default (4), 4, 6, 8} (K/V cache blocks in flight per D = 128 decode wave),
  * "train_split" {0, 1} (split-row fused training pass), "train_split_shape" {0 by
  * vocabulary, 1..5: pieces x threads per row 8x128, 4x256, 2x512, 5x256, 6x256}, "grpo_loss_rpb" {1, 2} (row chunks per block of the GRPO+loss launch),
- * "loss_bwd_blocks" [1, 4096] (grid of skyrl_ppo_loss_finish / _bwd).
+ * "loss_bwd_blocks" [1, 4096] (grid of skyrl_ppo_loss_finish / _bwd), "sampler_topk_fast"
+ * {0, 1} (skyrl_sample with top_k <= 128: the filter pre-pass + MODE 2 kernels vs the one-pass
+ * top_k kernel; identical tokens, logprobs to float rounding).
  * Every variant gives identical results except the split-row pass vs the resident one
  * (another fp32 summation order) and the timing probes "finish_mode" 2..4
  * (0 default, 1 = nb loaded first). Not thread-safe.                                    */
