@@ -933,7 +933,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sa
 //     elements are >= B, so all of the row's top k are.
 //   * The pass: the raw online (max, sum-exp) for the logprob, and every element >= B appended
 //     to an LDS candidate list (about k V / (4 NT VEC) elements: 464 at k = 50, V = 151,936).
-//   * On chip: the k-th largest candidate key (radix select over LDS bins); the candidates at or
+//   * On chip: the k-th largest candidate key (a 256-bin histogram of kmax - key, or a radix
+//     select by wave ballots when the candidates span more keys); the candidates at or
 //     above it ranked in the exact (key desc, index asc) order; top_k = rank < k; min_p = x/T >=
 //     max/T + ln min_p; top_p = the fixed-point masses (mass_q) summed exactly in rank order,
 //     kept while the mass before is < p Z (rank 0 always); the Gumbel-max decision over the
@@ -973,11 +974,12 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ float s_m[NW], s_s[NW];
     __shared__ uint32_t s_kmax[NW];
     __shared__ uint32_t s_rc[2][NW][16];
-    __shared__ uint32_t s_bin[3][16];
     __shared__ uint32_t s_ckey[kFastCap];
     __shared__ int32_t s_cidx[kFastCap];
-    __shared__ uint32_t s_fkey[kFastCap2];
-    __shared__ int32_t s_fidx[kFastCap2];
+    __shared__ __attribute__((aligned(16))) uint32_t s_fkey[kFastCap2];
+    __shared__ __attribute__((aligned(16))) int32_t s_fidx[kFastCap2];
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[256];
+    __shared__ uint32_t s_sel;
     __shared__ int32_t s_frank[kFastCap2];
     __shared__ uint32_t s_mass[kFastK];
     __shared__ unsigned long long s_before[kFastK];
@@ -987,6 +989,7 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ int32_t s_bi[NW];
     __shared__ RowFilter s_rf;
     const int row_i = blockIdx.x;
+    SPHASE(0);
     // a row the candidate lists cannot settle: the pre-pass's cuts and the MODE 2 decision, here
     // (a call, not inlined: its registers would otherwise crowd the streaming loop)
     auto fallback = [&]() {
@@ -1000,7 +1003,7 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
         s_cc = 0u;
         s_fc = 0u;
     }
-    if (threadIdx.x < 32) s_bin[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
+    if (threadIdx.x < 256) s_hist[threadIdx.x] = 0u;
 
     // ---- prologue: the first 4 NT vectors (the next 4 NT in flight) and their per-thread max
     const uint4* rv = reinterpret_cast<const uint4*>(row);  // 16-B aligned (host check)
@@ -1034,45 +1037,98 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
             for (int k = 0; k < VEC; ++k) km0 = max(km0, okey<T>(raw[k]));
         }
     }
-    // B = the k-th largest of km0 over the threads that hold a vector (radix select on d)
-    const uint32_t d0 = has0 ? KTOP - km0 : 0xffffffffu;
-    uint32_t P = 0u;
-    int below = 0;
+    // the k-th smallest d among the wave counts' 256 histogram bins (wave 0; s_sel = d, or
+    // 0xffffffff when the k-th is beyond the bins)
+    auto hist_pick = [&](uint32_t k) {
+        if (w == 0) {
+            const uint4 hb = reinterpret_cast<const uint4*>(s_hist)[lane];  // bins 4 lane .. 4 lane + 3
+            const uint32_t tot = hb.x + hb.y + hb.z + hb.w;
+            uint32_t incl = tot;
 #pragma unroll
-    for (int st = 0; st < KB / 4; ++st) {
-        const int sh = KB - 4 * (st + 1);
-        const bool match = st == 0 ? (KB == 32 ? has0 : d0 <= 0xffffu) : ((d0 >> (sh + 4)) == P);
-        const uint32_t dig = (d0 >> sh) & 15u;
-        uint32_t mine = 0u;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(match && dig == (uint32_t)q));
-            if (lane == q) mine = c;
+            for (int off = 1; off < kWave; off <<= 1) {
+                const uint32_t o = (uint32_t)__shfl_up((int)incl, off, kWave);
+                if (lane >= off) incl += o;
+            }
+            const uint64_t hit = __builtin_amdgcn_ballot_w64(incl >= k);
+            if (!hit) {
+                if (lane == 0) s_sel = 0xffffffffu;
+            } else if (lane == __builtin_ctzll(hit)) {
+                uint32_t cum = incl - tot, d = 4u * lane;
+                if (cum + hb.x < k) {
+                    cum += hb.x;
+                    ++d;
+                    if (cum + hb.y < k) {
+                        cum += hb.y;
+                        ++d;
+                        if (cum + hb.z < k) ++d;
+                    }
+                }
+                s_sel = d;
+            }
         }
-        if (lane < 16) s_rc[st & 1][w][lane] = mine;
-        __syncthreads();
-        uint32_t tq = 0u;  // lane q: the workgroup's count of digit q
-        if (lane < 16) {
+    };
+    // B = the k-th largest of km0 over the threads that hold a vector: a 256-bin histogram of
+    // kmax0 - km0 (the last bin saturates), or a radix select by wave ballots when the k-th
+    // lands in the saturated bin. Fewer than k threads holding a vector: no bound.
+    uint32_t kw = has0 ? km0 : 0u;
 #pragma unroll
-            for (int j = 0; j < NW; ++j) tq += s_rc[st & 1][j][lane];
-        }
-        uint32_t incl = tq;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const uint32_t o = (uint32_t)__shfl_up((int)incl, off, kWave);
-            if (lane >= off) incl += o;
-        }
-        const uint64_t hit = __builtin_amdgcn_ballot_w64(lane < 16 && below + (int)incl >= top_k);
-        const int q = hit ? __builtin_ctzll(hit) : 15;
-        below += (int)__shfl((int)(incl - tq), q, kWave);
-        P = (P << 4) | (uint32_t)q;
-    }
-    // fewer than k threads hold a vector: no bound, every element is a candidate
+    for (int off = 32; off > 0; off >>= 1) kw = max(kw, (uint32_t)__shfl_xor((int)kw, off, kWave));
+    if (lane == 0) s_kmax[w] = kw;
     const int n_ne = __syncthreads_count(has0);
-    const float bf = n_ne < top_k ? -INFINITY : from_key<T>(KTOP - P);
+    uint32_t kmax0 = s_kmax[0];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) kmax0 = max(kmax0, s_kmax[j]);
+    uint32_t bkey = 0u;
+    if (n_ne >= top_k) {
+        if (has0) atomicAdd(&s_hist[min(kmax0 - km0, 255u)], 1u);
+        __syncthreads();
+        hist_pick((uint32_t)top_k);
+        __syncthreads();
+        const uint32_t dsel = s_sel;
+        if (threadIdx.x < 256) s_hist[threadIdx.x] = 0u;  // again for the candidates (barriers between)
+        if (dsel < 255u) {
+            bkey = kmax0 - dsel;
+        } else {
+            const uint32_t d0 = has0 ? KTOP - km0 : 0xffffffffu;
+            uint32_t P = 0u;
+            int below = 0;
+#pragma unroll
+            for (int st = 0; st < KB / 4; ++st) {
+                const int sh = KB - 4 * (st + 1);
+                const bool match = st == 0 ? (KB == 32 ? has0 : d0 <= 0xffffu) : ((d0 >> (sh + 4)) == P);
+                const uint32_t dig = (d0 >> sh) & 15u;
+                uint32_t mine = 0u;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(match && dig == (uint32_t)q));
+                    if (lane == q) mine = c;
+                }
+                if (lane < 16) s_rc[st & 1][w][lane] = mine;
+                __syncthreads();
+                uint32_t tq = 0u;  // lane q: the workgroup's count of digit q
+                if (lane < 16) {
+#pragma unroll
+                    for (int j = 0; j < NW; ++j) tq += s_rc[st & 1][j][lane];
+                }
+                uint32_t incl = tq;
+#pragma unroll
+                for (int off = 1; off < 16; off <<= 1) {
+                    const uint32_t o = (uint32_t)__shfl_up((int)incl, off, kWave);
+                    if (lane >= off) incl += o;
+                }
+                const uint64_t hit = __builtin_amdgcn_ballot_w64(lane < 16 && below + (int)incl >= top_k);
+                const int q = hit ? __builtin_ctzll(hit) : 15;
+                below += (int)__shfl((int)(incl - tq), q, kWave);
+                P = (P << 4) | (uint32_t)q;
+            }
+            bkey = KTOP - P;
+        }
+    }
+    const float bf = n_ne < top_k ? -INFINITY : from_key<T>(bkey);
+    SPHASE(1);
 
     // ---- the pass: lse of the raw logits; every element >= B into the candidate list
-    float m = -1e30f, s = 0.f;
+    float m = has0 ? fmaxf(from_key<T>(km0), -1e30f) : -1e30f, s = 0.f;
     uint32_t kmx = 0u;
     auto append = [&](uint32_t kk, int idx) {
         const uint32_t pos = atomicAdd(&s_cc, 1u);
@@ -1091,12 +1147,16 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
         float vmax = x[0];
 #pragma unroll
         for (int k = 1; k < VEC; ++k) vmax = fmaxf(vmax, x[k]);
-        const float mn = fmaxf(m, vmax);
-        float acc = s * fast_exp2((m - mn) * kLog2e);
+        // lagged lse offset (the thread's prologue max): rescaled only when a value rises 64
+        // above it, so the exponentials of one vector never overflow
+        if (vmax > m + 64.f) {
+            s *= fast_exp2((m - vmax) * kLog2e);
+            m = vmax;
+        }
+        float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc += fast_exp2((x[k] - mn) * kLog2e);
-        s = acc;
-        m = mn;
+        for (int k = 0; k < VEC; ++k) acc += fast_exp2((x[k] - m) * kLog2e);
+        s += acc;
         if (vmax >= bf) {  // a float compare admits every key >= key(B) (-0 beside +0 as well)
 #pragma unroll
             for (int k = 0; k < VEC; ++k)
@@ -1106,6 +1166,12 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (nfull > 0) {
         for (int base = 0; base < nfull; base += kStep) {
             const bool more = base + kStep < nfull;
+            switch (((nfull - base) * 4 - 1) / nfull) {  // progress priority, as the row-mode sampler
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
             if (more && base > 0) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
@@ -1131,6 +1197,7 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (x >= bf) append(okey<T>(row[i]), i);
     }
 
+    SPHASE(2);
     // ---- row lse and max key (the max element is a candidate)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1156,6 +1223,7 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
         M = mn;
         kmax = max(kmax, s_kmax[j]);
     }
+    SPHASE(5);
     const float lse = M + fast_log2(S) * kLn2;
     const float mx = from_key<T>(kmax);
     const int C = (int)s_cc;
@@ -1164,39 +1232,70 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
         return;
     }
 
-    // ---- the k-th largest candidate key: radix select over LDS bins (3 rotating bin sets)
+    // ---- the k-th largest candidate key. Candidates lie within kmax - key(B) of the max: when
+    //      that span is under 256 keys (bf16 rows: usually), one histogram of d = kmax - key and
+    //      a scan by one wave; otherwise a radix select by wave ballots over rounds of NT
+    //      candidates (per-wave digit counts summed through LDS)
+    const int rounds = (C + NT - 1) / NT;
+    uint32_t tkey;
+    if (n_ne >= top_k && kmax - bkey < 256u) {
+        for (int i = threadIdx.x; i < C; i += NT) atomicAdd(&s_hist[kmax - s_ckey[i]], 1u);
+        __syncthreads();
+        hist_pick((uint32_t)top_k);
+        __syncthreads();
+        tkey = kmax - s_sel;
+    } else {
     uint32_t Pc = 0u;
     int above = 0;
 #pragma unroll
     for (int st = 0; st < KB / 4; ++st) {
         const int sh = KB - 4 * (st + 1);
-        uint32_t* bin = s_bin[st % 3];
-        for (int i = threadIdx.x; i < C; i += NT) {
-            const uint32_t d = KTOP - s_ckey[i];
-            if (st == 0 || (d >> (sh + 4)) == Pc) atomicAdd(&bin[(d >> sh) & 15u], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < 16) s_bin[(st + 2) % 3][threadIdx.x] = 0u;  // last read a step ago, next used in two
-        int cum = above, q = 15;
+        uint32_t mine = 0u;
+        for (int rd = 0; rd < rounds; ++rd) {
+            const int i = rd * NT + threadIdx.x;
+            const uint32_t d = i < C ? KTOP - s_ckey[i] : 0u;
+            const bool match = i < C && (st == 0 || (d >> (sh + 4)) == Pc);
+            const uint32_t dig = (d >> sh) & 15u;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int c = (int)bin[j];
-            if (cum + c >= top_k) {
-                q = j;
-                break;
+            for (int q = 0; q < 16; ++q) {
+                const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(match && dig == (uint32_t)q));
+                if (lane == q) mine += c;
             }
-            cum += c;
         }
-        above = cum;
+        if (lane < 16) s_rc[st & 1][w][lane] = mine;
+        __syncthreads();
+        uint32_t tq = 0u;
+        if (lane < 16) {
+#pragma unroll
+            for (int j = 0; j < NW; ++j) tq += s_rc[st & 1][j][lane];
+        }
+        uint32_t incl = tq;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)incl, off, kWave);
+            if (lane >= off) incl += o;
+        }
+        const uint64_t hit = __builtin_amdgcn_ballot_w64(lane < 16 && above + (int)incl >= top_k);
+        const int q = hit ? __builtin_ctzll(hit) : 15;
+        above += (int)__shfl((int)(incl - tq), q, kWave);
         Pc = (Pc << 4) | (uint32_t)q;
     }
-    const uint32_t tkey = KTOP - Pc;  // the k-th largest key; `above` candidates are larger
+    tkey = KTOP - Pc;  // the k-th largest key; `above` candidates are larger
+    }
+    SPHASE(3);
 
-    // ---- candidates at or above it, ranked in (key desc, index asc) order
-    for (int i = threadIdx.x; i < C; i += NT) {
-        const uint32_t kk = s_ckey[i];
-        if (kk >= tkey) {
-            const uint32_t pos = atomicAdd(&s_fc, 1u);
+    // ---- candidates at or above it (ballot compaction, one LDS atomic per wave and round),
+    //      ranked in (key desc, index asc) order
+    for (int rd = 0; rd < rounds; ++rd) {
+        const int i = rd * NT + threadIdx.x;
+        const uint32_t kk = i < C ? s_ckey[i] : 0u;
+        const bool keep = i < C && kk >= tkey;
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+        uint32_t wbase = 0u;
+        if (lane == 0 && bal) wbase = atomicAdd(&s_fc, (uint32_t)__builtin_popcountll(bal));
+        wbase = (uint32_t)__shfl((int)wbase, 0, kWave);
+        if (keep) {
+            const uint32_t pos = wbase + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
             if (pos < (uint32_t)kFastCap2) {
                 s_fkey[pos] = kk;
                 s_fidx[pos] = s_cidx[i];
@@ -1206,17 +1305,28 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (int r = threadIdx.x; r < top_k; r += NT) s_mass[r] = 0u;
     __syncthreads();
     const int F = (int)s_fc;
-    if (F > kFastCap2) {  // a tie group too large for the exact ranking here
+    if (F > kFastCap2 - 4) {  // a tie group too large for the exact ranking here
         fallback();
         return;
     }
+    // pad to whole 16-B groups with entries that precede nothing (key 0, the last index)
+    const int F4 = (F + 3) & ~3;
+    if ((int)threadIdx.x < F4 - F) {
+        s_fkey[F + threadIdx.x] = 0u;
+        s_fidx[F + threadIdx.x] = 0x7fffffff;
+    }
+    __syncthreads();
     for (int i = threadIdx.x; i < F; i += NT) {
         const uint32_t ki = s_fkey[i];
         const int ii = s_fidx[i];
         int r = 0;
-        for (int j = 0; j < F; ++j) {
-            const uint32_t kj = s_fkey[j];
-            r += (kj > ki || (kj == ki && s_fidx[j] < ii)) ? 1 : 0;
+        for (int j = 0; j < F4 / 4; ++j) {
+            const uint4 kq = reinterpret_cast<const uint4*>(s_fkey)[j];
+            const int4 iq = reinterpret_cast<const int4*>(s_fidx)[j];
+            r += (kq.x > ki || (kq.x == ki && iq.x < ii)) ? 1 : 0;
+            r += (kq.y > ki || (kq.y == ki && iq.y < ii)) ? 1 : 0;
+            r += (kq.z > ki || (kq.z == ki && iq.z < ii)) ? 1 : 0;
+            r += (kq.w > ki || (kq.w == ki && iq.w < ii)) ? 1 : 0;
         }
         s_frank[i] = r;
     }
@@ -1279,6 +1389,7 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        SPHASE(4);
         Best b{s_bs[0], s_bi[0]};
         for (int j = 1; j < NW; ++j)
             if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
