@@ -44,7 +44,8 @@ const char* skyrl_last_error(void);
  * loss-mask row sums; 4: skyrl_policy_train_fwd takes grad_logits strides; 5: pack emits
  * reward row sums (GRPO scores), skyrl_grpo_advantage / skyrl_grpo_ppo_loss_fwd take them,
  * the loss forwards take flags (SKYRL_LOSS_DEFER_FOLD) and skyrl_ppo_loss_finish; 6:
- * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange). */
+ * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange; 7:
+ * skyrl_comm_* RCCL collectives). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -482,6 +483,37 @@ int skyrl_paged_decode_balanced(const void* q, int64_t q_stride, const void* k_c
 int skyrl_add_rmsnorm(const void* delta, void* hidden, const void* weight, int32_t n, int32_t H, float eps, void* out,
                       void* stream);
 int skyrl_silu_mul(const void* gate_up, int64_t n, int32_t I, void* out, void* stream);
+
+/* ---- a12-a14 collectives over RCCL (xGMI), one communicator per process and GPU ----------
+ * SURVEY §8(b)'s skyrl_comm_{init, allreduce, broadcast}, for hosts that bind this library
+ * directly (the Python host reaches the same RCCL through torch.distributed, skyrl_amd/comm.py).
+ * Reference call sites: all-reduce = metric reduction (distributed/strategy.py:70-95) and the DP
+ * gradient mean (distributed/fsdp_strategy.py:216-226); reduce-scatter = FSDP2's fp32 gradient
+ * reduce-scatter (fsdp_strategy.py:253-271); all-gather = the sharded optimizer's shards;
+ * broadcast = learner -> rollout weights (weight_sync/broadcast_strategy.py:98-191).
+ *   skyrl_comm_get_unique_id  rank 0 writes skyrl_comm_unique_id_bytes() bytes; the caller hands
+ *                             them to every rank (any out-of-band channel)
+ *   skyrl_comm_init           on the current HIP device; *comm_out is caller-owned until
+ *                             skyrl_comm_destroy
+ *   counts are elements of dtype (SKYRL_F32, SKYRL_BF16, SKYRL_I64, SKYRL_I32, SKYRL_U8);
+ *   reduce_scatter: send holds nranks * recv_count, allgather: recv holds nranks * send_count;
+ *   broadcast: send is read on root only (may be NULL elsewhere), recv written everywhere.
+ * Stream-ordered on `stream`, no host synchronization, nothing allocated per call. */
+#define SKYRL_COMM_SUM 0
+#define SKYRL_COMM_MAX 1
+#define SKYRL_COMM_MIN 2
+#define SKYRL_COMM_AVG 3
+size_t skyrl_comm_unique_id_bytes(void);
+int skyrl_comm_get_unique_id(void* id_out);
+int skyrl_comm_init(const void* unique_id, int32_t nranks, int32_t rank, void** comm_out);
+int skyrl_comm_destroy(void* comm);
+int skyrl_comm_size(void* comm, int32_t* nranks_out, int32_t* rank_out);
+int skyrl_comm_allreduce(const void* send, void* recv, int64_t count, int dtype, int op, void* comm, void* stream);
+int skyrl_comm_reduce_scatter(const void* send, void* recv, int64_t recv_count, int dtype, int op, void* comm,
+                              void* stream);
+int skyrl_comm_allgather(const void* send, void* recv, int64_t send_count, int dtype, void* comm, void* stream);
+int skyrl_comm_broadcast(const void* send, void* recv, int64_t count, int dtype, int32_t root, void* comm,
+                         void* stream);
 
 #ifdef __cplusplus
 }

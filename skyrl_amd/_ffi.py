@@ -90,6 +90,15 @@ _INT = ctypes.c_int
 SIGNATURES = {
     "skyrl_last_error": (ctypes.c_char_p, []),
     "skyrl_abi_version": (_INT, []),
+    "skyrl_comm_unique_id_bytes": (_SZ, []),
+    "skyrl_comm_get_unique_id": (_INT, [_P]),
+    "skyrl_comm_init": (_INT, [_P, _I32, _I32, ctypes.POINTER(_P)]),
+    "skyrl_comm_destroy": (_INT, [_P]),
+    "skyrl_comm_size": (_INT, [_P, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "skyrl_comm_allreduce": (_INT, [_P, _P, _I64, _INT, _INT, _P, _P]),
+    "skyrl_comm_reduce_scatter": (_INT, [_P, _P, _I64, _INT, _INT, _P, _P]),
+    "skyrl_comm_allgather": (_INT, [_P, _P, _I64, _INT, _P, _P]),
+    "skyrl_comm_broadcast": (_INT, [_P, _P, _I64, _INT, _I32, _P, _P]),
     "skyrl_tune": (_INT, [ctypes.c_char_p, _INT]),
     "skyrl_grpo_advantage": (_INT, [_P, _P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
     "skyrl_gae_workspace_bytes": (_SZ, [_I32]),

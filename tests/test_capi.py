@@ -34,7 +34,7 @@ def test_ffi_signatures_cover_header():
 
 def test_abi_version_and_error_path():
     lib = _ffi.load()
-    assert lib.skyrl_abi_version() == 6
+    assert lib.skyrl_abi_version() == 7
     # argument validation happens on the host before any launch: no GPU needed
     with pytest.raises(_ffi.SkyrlHipError, match="temperature"):
         _ffi.call("skyrl_logprob_fwd", ctypes.c_void_p(16), _ffi.BF16, 8, 8, 1, 1, 8, ctypes.c_void_p(16), 1, 1,
@@ -105,3 +105,17 @@ def test_ppo_loss_finish_validates_on_host():
         _ffi.call("skyrl_ppo_loss_finish", p, None, None, 4, 4, ctypes.byref(params), p, p, p, None)
     with pytest.raises(_ffi.SkyrlHipError, match="bad sizes"):
         _ffi.call("skyrl_ppo_loss_finish", None, None, None, 0, 4, ctypes.byref(params), p, p, p, None)
+
+
+def test_comm_abi_host_checks():
+    """The RCCL entry points validate on the host (no GPU, no RCCL call)."""
+    assert _ffi.query("skyrl_comm_unique_id_bytes") == 128  # sizeof(ncclUniqueId)
+    with pytest.raises(_ffi.SkyrlHipError, match="null pointer"):
+        _ffi.call("skyrl_comm_init", None, 1, 0, ctypes.byref(ctypes.c_void_p()))
+    with pytest.raises(_ffi.SkyrlHipError, match="rank must be"):
+        _ffi.call("skyrl_comm_init", ctypes.c_void_p(16), 2, 2, ctypes.byref(ctypes.c_void_p()))
+    with pytest.raises(_ffi.SkyrlHipError, match="null communicator"):
+        _ffi.call("skyrl_comm_allreduce", ctypes.c_void_p(16), ctypes.c_void_p(16), 4, _ffi.F32, 0, None, None)
+    with pytest.raises(_ffi.SkyrlHipError, match="dtype"):
+        _ffi.call("skyrl_comm_broadcast", ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 9, 0, ctypes.c_void_p(16), None)
+    assert _ffi.call("skyrl_comm_destroy", None) == 0
