@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--micro", type=int, default=16)
     ap.add_argument("--tunable", action="store_true", help="TunableOp GEMM search in the rollout engine")
     ap.add_argument("--no-packing", action="store_true", help="padded learner batches (no sample packing)")
+    ap.add_argument("--no-grad-ckpt", action="store_true",
+                    help="keep the activations instead of recomputing them (288 GB of HBM affords it)")
     args = ap.parse_args()
     from transformers import AutoModelForCausalLM, Qwen2Config
 
@@ -52,7 +54,8 @@ def main():
     torch.manual_seed(0)
     t0 = time.time()
     policy = AutoModelForCausalLM.from_config(cfg, dtype=torch.float32).to(DEV)
-    policy.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+    if not args.no_grad_ckpt:  # the reference's default (ppo_base_config.yaml gradient_checkpointing: true)
+        policy.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
     policy.config.use_cache = False
     ref = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16).to(DEV).eval()
     ref.load_state_dict(policy.state_dict())
@@ -113,7 +116,7 @@ def main():
                       "config": {"model": "Qwen2.5-1.5B (random init)", "layers": args.layers, "prompts": args.prompts,
                                  "group": args.group, "prompt_len": "U[16,512]",
                                  "response_len": f"U[1,{args.max_response}]", "micro_batch": args.micro,
-                                 "gradient_checkpointing": True, "sample_packing": tcfg.use_sample_packing,
+                                 "gradient_checkpointing": not args.no_grad_ckpt, "sample_packing": tcfg.use_sample_packing,
                                  "learner": "HF transformers fp32 master, autocast bf16"},
                       "generated_tokens": sum(resp_len), "steps": steps}), flush=True)
 
