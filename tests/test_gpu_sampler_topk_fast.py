@@ -79,9 +79,10 @@ def test_topk_fast_matches_oracle(dev):
 
 
 def test_topk_fast_hands_back_tie_heavy_and_masked_rows(dev):
-    """Rows the per-thread lists cannot certify go back to the two-kernel path: few distinct
-    values (the k-th value sits in a tie group spread over many threads), and rows that are -inf
-    except for a handful of logits (fewer finite values than k). Tokens still equal."""
+    """Rows the candidate list cannot settle run the two-kernel path's code in the workgroup: few
+    distinct values (the list overflows), rows that are -inf except for a handful of logits, and
+    a 1000-way tie at the top (the list holds it, the exact ranking does not). Tokens still
+    equal."""
     from oracle import sampler as osamp
 
     V, n = 151936, 64
@@ -90,7 +91,11 @@ def test_topk_fast_hands_back_tie_heavy_and_masked_rows(dev):
     masked = torch.full((n // 2, V), float("-inf"))
     cols = torch.randint(0, V, (n // 2, 20), generator=g)
     masked.scatter_(1, cols, torch.randn(n // 2, 20, generator=g))
-    x = torch.cat([ties, masked]).to(torch.bfloat16)
+    # a tie group of 1000 at the top: few enough candidates for the list, too many to rank
+    tied_top = torch.randn(n // 2, V, generator=g)
+    tied_top.scatter_(1, torch.randint(0, V, (n // 2, 1000), generator=g), 10.0)
+    x = torch.cat([ties, masked, tied_top]).to(torch.bfloat16)
+    n = x.shape[0]
     ids = torch.arange(n, dtype=torch.int64)
     tf, lf, done = _ab(x.to(dev), 0, temperature=1.0, top_k=50, top_p=0.9, seed=3, seq_ids=ids.to(dev), step=1)
     assert done < n  # some rows were handed back
