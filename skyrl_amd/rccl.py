@@ -114,12 +114,8 @@ class RcclComm:
         return t
 
     def close(self) -> None:
+        """Destroy the communicator (collective: every rank calls it). Not done from __del__: at
+        interpreter exit the other ranks may be gone and the destroy would wait for them."""
         if self._h:
             _ffi.call("skyrl_comm_destroy", self._h)
             self._h = ctypes.c_void_p()
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
