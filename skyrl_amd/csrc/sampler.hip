@@ -1239,7 +1239,11 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int rounds = (C + NT - 1) / NT;
     uint32_t tkey;
     if (n_ne >= top_k && kmax - bkey < 256u) {
-        for (int i = threadIdx.x; i < C; i += NT) atomicAdd(&s_hist[kmax - s_ckey[i]], 1u);
+        for (int i = threadIdx.x; i < C; i += NT) {
+            // a -0 admitted beside a bound of +0 lies one key below it: never in the top k
+            const uint32_t dd = kmax - s_ckey[i];
+            if (dd < 256u) atomicAdd(&s_hist[dd], 1u);
+        }
         __syncthreads();
         hist_pick((uint32_t)top_k);
         __syncthreads();
