@@ -137,3 +137,18 @@ def test_topk_fast_f32_and_misaligned_rows(dev):
     assert done == 0
     etok, _ = osamp.sample(xb, 0.9, 50, 0.9, 0.0, 1, ids, 3)
     assert torch.equal(tf, etok)
+
+
+def test_topk_fast_bench_shape_matches_oracle(dev):
+    """The §8(d) variant (top_k 50, top_p 0.9, T = 1) at the bench's V = 151,936 against
+    oracle/sampler_ref.c directly, 512 rows: tokens bit-exact, logprobs 1e-4."""
+    from oracle import sampler as osamp
+
+    g = torch.Generator().manual_seed(77)
+    x = (torch.randn(512, 151936, generator=g) * 3).to(torch.bfloat16)
+    ids = torch.arange(512, dtype=torch.int64) * 3 + 1
+    tok, lp, done = _run(x.to(dev), True, temperature=1.0, top_k=50, top_p=0.9, seed=21, seq_ids=ids.to(dev), step=5)
+    assert done >= 500
+    etok, elp = osamp.sample(x, 1.0, 50, 0.9, 0.0, 21, ids, 5)
+    assert torch.equal(tok, etok), int((tok != etok).sum())
+    torch.testing.assert_close(lp, elp, atol=1e-4, rtol=1e-4)
