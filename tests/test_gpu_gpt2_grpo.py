@@ -9,9 +9,11 @@ aligned) with the lm_head-fused HIP logprob kernels, the HIP pack, GRPO and fuse
 AdamW, and the weight sync back into the engine. A world_size-1 gloo group is the DP group,
 as in config 1.
 
-Checked: the engine's rollout logprobs equal the learner's recomputed old logprobs of the same
-tokens (the sampler, the weight sync and the fused logprob agree), every metric is finite, the
-policy moves away from the reference (KL > 0), with sample packing off and on.
+Checked: every micro-batch's loss from the fused pass equals oracle/cpu_ref's loss assembly
+(PPO clip + k3 KL to ref, token mean) on the same log-probs within 1e-4; the engine's rollout
+logprobs equal the learner's recomputed old logprobs of the same tokens (the sampler, the
+weight sync and the fused logprob agree), every metric is finite, the policy moves away from
+the reference (KL > 0), with sample packing off and on.
 """
 
 import os
@@ -46,8 +48,27 @@ def gloo_world1():
 
 
 @pytest.mark.parametrize("packing", [False, True])
-def test_gpt2_small_grpo_steps(gloo_world1, packing):
+def test_gpt2_small_grpo_steps(gloo_world1, packing, monkeypatch):
     from transformers import AutoModelForCausalLM, GPT2Config
+
+    from oracle import cpu_ref
+    from skyrl_amd import ops
+
+    # every micro-batch's fused pass against the oracle's loss assembly on the same log-probs
+    # (workers/worker.py:801-876: PPO clip + k3 KL to ref, token-mean; cpu_ref.policy_loss_assembly)
+    checked = []
+    orig = ops.policy_train_ragged
+
+    def checked_pass(logits, labels, pos, old, adv, mask, params, **kw):
+        loss, met, lp, ent = orig(logits, labels, pos, old, adv, mask, params, **kw)
+        exp, _ = cpu_ref.policy_loss_assembly(lp.detach().float().cpu(), old.float().cpu(), adv.float().cpu(),
+                                              mask.float().cpu(), kw["ref_log_probs"].float().cpu(),
+                                              ent.detach().float().cpu())
+        got = float(met[0])
+        checked.append(abs(got - float(exp)) <= 1e-5 + 1e-4 * abs(float(exp)))
+        return loss, met, lp, ent
+
+    monkeypatch.setattr(ops, "policy_train_ragged", checked_pass)
 
     cfg = GPT2Config()  # GPT-2-small: 12 layers, 768 wide, 12 heads, V = 50,257
     assert cfg.vocab_size == 50257 and cfg.n_layer == 12
@@ -75,6 +96,7 @@ def test_gpt2_small_grpo_steps(gloo_world1, packing):
         hist.append(m)
         assert all(torch.isfinite(torch.tensor(float(v))) for v in m.values()), m
         assert m["logprobs_diff_mean"] < 0.03, (step, m["logprobs_diff_mean"])
+    assert checked and all(checked), checked  # 3 steps x 4 micro-batches, each within 1e-4 of the oracle
     assert not torch.equal(policy.transformer.h[0].attn.c_attn.weight.detach(), w0)
     assert hist[-1]["policy_kl"] > 0
     # the engine holds the learner's weights (bf16) after the sync
