@@ -70,6 +70,21 @@ def test_gpt2_small_grpo_steps(gloo_world1, packing, monkeypatch):
 
     monkeypatch.setattr(ops, "policy_train_ragged", checked_pass)
 
+    # ... and the GRPO advantages against the oracle (utils/ppo_utils.py:1132-1182), every step
+    from skyrl_amd import trainer_utils
+
+    adv_checked = []
+    orig_adv = trainer_utils.compute_advantages_and_returns
+
+    def checked_adv(data, alg):
+        out = orig_adv(data, alg)
+        exp = cpu_ref.grpo_advantage(out["rewards"].float().cpu(), out["response_mask"].cpu(),
+                                     out.metadata["uids"])
+        adv_checked.append(torch.allclose(out["advantages"].float().cpu(), exp, atol=1e-5, rtol=1e-5))
+        return out
+
+    monkeypatch.setattr(trainer_utils, "compute_advantages_and_returns", checked_adv)
+
     cfg = GPT2Config()  # GPT-2-small: 12 layers, 768 wide, 12 heads, V = 50,257
     assert cfg.vocab_size == 50257 and cfg.n_layer == 12
     torch.manual_seed(0)
@@ -97,6 +112,7 @@ def test_gpt2_small_grpo_steps(gloo_world1, packing, monkeypatch):
         assert all(torch.isfinite(torch.tensor(float(v))) for v in m.values()), m
         assert m["logprobs_diff_mean"] < 0.03, (step, m["logprobs_diff_mean"])
     assert checked and all(checked), checked  # 3 steps x 4 micro-batches, each within 1e-4 of the oracle
+    assert len(adv_checked) == 3 and all(adv_checked), adv_checked
     assert not torch.equal(policy.transformer.h[0].attn.c_attn.weight.detach(), w0)
     assert hist[-1]["policy_kl"] > 0
     # the engine holds the learner's weights (bf16) after the sync
