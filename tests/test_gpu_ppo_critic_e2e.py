@@ -2,8 +2,9 @@
 rollout -> values from a CriticModel (HF base + value_head) -> GAE (lambda 0.95) + whitening on
 the HIP kernel -> HIP clipped value loss update -> HIP PPO policy loss update -> weight sync.
 
-Properties (parity of each kernel is pinned elsewhere against the oracle / golden vectors):
-the critic regresses onto the returns (its loss falls), advantages are whitened (masked mean 0,
+Every step's GAE advantages / returns and every critic micro-batch's value loss are checked
+against the oracle on the step's own batch. Properties: the critic regresses onto the returns
+(its loss falls), advantages are whitened (masked mean 0,
 variance 1 — checked through the GAE registry entry on the step's own batch), rollout and
 learner logprobs agree, and nothing goes non-finite.
 """
@@ -20,8 +21,34 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-def test_ppo_with_critic_and_gae():
+def test_ppo_with_critic_and_gae(monkeypatch):
     from transformers import AutoModelForCausalLM, Qwen2Config
+
+    from oracle import cpu_ref
+    from skyrl_amd import ppo_utils, trainer_utils
+
+    # each step's GAE (+ whitening) and each critic micro-batch's clipped value loss against the
+    # oracle on the same inputs (utils/ppo_utils.py:1101-1129, 148-172, 175-193)
+    checks = {"gae": [], "critic": []}
+    orig_adv, orig_vl = trainer_utils.compute_advantages_and_returns, ppo_utils.ppo_critic_loss
+
+    def checked_adv(data, alg_cfg):
+        out = orig_adv(data, alg_cfg)
+        adv, ret = cpu_ref.gae(out["rewards"].float().cpu(), out["values"].float().cpu(),
+                               out["response_mask"].float().cpu(), alg_cfg.gamma, alg_cfg.lambd)
+        checks["gae"].append(torch.allclose(out["advantages"].cpu(), adv, atol=1e-4, rtol=1e-4)
+                             and torch.allclose(out["returns"].cpu(), ret, atol=1e-5, rtol=1e-5))
+        return out
+
+    def checked_vl(values, old_values, returns, config, loss_mask=None):
+        loss, clipfrac = orig_vl(values, old_values, returns, config, loss_mask=loss_mask)
+        exp, _ = cpu_ref.critic_loss(values.detach().float().cpu(), old_values.float().cpu(), returns.float().cpu(),
+                                     loss_mask.float().cpu(), config.value_clip)
+        checks["critic"].append(abs(float(loss.detach()) - float(exp)) <= 1e-6 + 1e-5 * abs(float(exp)))
+        return loss, clipfrac
+
+    monkeypatch.setattr(trainer_utils, "compute_advantages_and_returns", checked_adv)
+    monkeypatch.setattr(ppo_utils, "ppo_critic_loss", checked_vl)
 
     cfg = Qwen2Config(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
                       num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=256,
@@ -52,3 +79,5 @@ def test_ppo_with_critic_and_gae():
     cl = [h["critic_loss"] for h in hist]
     assert cl[-1] < 0.1 * max(cl) and min(cl[-3:]) < cl[0], cl
     assert "values_clipfrac" in hist[0] and "critic_grad_norm" in hist[0]
+    assert len(checks["gae"]) == 8 and all(checks["gae"]), checks["gae"]
+    assert checks["critic"] and all(checks["critic"]), checks["critic"]
