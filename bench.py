@@ -9,9 +9,12 @@ path over one synthetic batch:
   pack      skyrl_pack_experience: ragged prompts/responses -> padded training tensors
   ref/old   skyrl_logprob_fwd over all 512x1024 response positions (2 passes)
   advantage skyrl_grpo_advantage over [512, 1024] (contiguous groups, pack's reward row sums)
-  update    per micro-batch (16 seqs): skyrl_policy_train_fwd, ONE pass per token computing
-            logprob + entropy + PPO/KL loss and writing dlogits (bf16), each row held in the
-            registers of 8 workgroups; metrics read once per step
+  update    the step form of the fused policy pass (GRPOTrainer's): skyrl_policy_train_plan (every
+            micro-batch's loss scales, one launch), per micro-batch (16 seqs)
+            skyrl_policy_train_micro_fwd, ONE pass per token computing logprob + entropy + PPO/KL
+            loss terms and writing dlogits (bf16), each row held in the registers of 6
+            workgroups, then skyrl_policy_train_fold (every micro-batch's loss + metrics, one
+            launch); metrics read once per step
   optimizer grad norm + clip + AdamW over Qwen2.5-1.5B's 1.54 B fp32 params, writing the bf16
             rollout copy (reduce-scatter / all-gather over RCCL when N > 1)
 
@@ -46,9 +49,11 @@ import torch.distributed as dist  # noqa: E402
 P_MAX, R_MAX, PROMPTS, GROUP, VOCAB = 512, 1024, 64, 8, 151936
 QWEN_1_5B_PARAMS = 1_543_714_304  # Qwen2.5-1.5B, tied embeddings
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# measured on the box by scripts/probe/stream_probe.py (reported beside frac, never instead of it)
-CEILING_READ_GBS = 6100.0    # read-only stream
-CEILING_RW_GBS = 5560.0      # 50/50 read+write copy, best structure (scripts/probe/rw_probe.py, 10 GB)
+# reported beside frac, never instead of it: the guide's measured float4 copy (MI355X_MICROARCH.md,
+# "6.29 TB/s measured") for read+write kernels, and the read-only grid-stride stream our probe
+# measured on the box (7.0-7.1 TB/s, profiles/r03_rw_ceiling_probe2.log) for read-only kernels
+CEILING_READ_GBS = 7100.0
+CEILING_RW_GBS = 6290.0
 
 
 def log(msg):
@@ -147,6 +152,9 @@ def run(args):
             dist.init_process_group("nccl", device_id=dev)
         else:  # rehearsal of the N>1 path with several ranks on one GPU (RCCL refuses duplicate GPUs)
             dist.init_process_group(args.backend)
+        world = dist.get_world_size()  # n_gpus is the communicator's size
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but the launcher started {world} ranks; reporting n_gpus = {world}")
     N = PROMPTS * GROUP
     R, V, mb = R_MAX, VOCAB, args.micro_batch
     data, uids = synth_inputs(dev, N, seed=1234 + rank)
@@ -206,11 +214,18 @@ def run(args):
     lp = torch.empty((mb, R), dtype=torch.float32, device=dev)
     ent = torch.empty_like(lp)
     lse = torch.empty_like(lp)
-    loss_buf = torch.empty((), dtype=torch.float32, device=dev)
-    met_buf = torch.empty(8, dtype=torch.float32, device=dev)
-    train_ws = torch.zeros(ops._ffi.query("skyrl_policy_train_workspace_bytes", mb, R), dtype=torch.uint8,
-                           device=dev)
+    # the step form of the fused pass (GRPOTrainer's): one plan launch (every micro-batch's loss
+    # scales), the micro-batches' passes, one fold launch (every micro-batch's loss + metrics)
+    n_micro = N // mb
+    step_ws = torch.zeros(ops._ffi.query("skyrl_policy_train_step_workspace_bytes", N, R, mb), dtype=torch.uint8,
+                          device=dev)
+    step_loss = torch.empty(n_micro, dtype=torch.float32, device=dev)
+    step_met = torch.empty((n_micro, 8), dtype=torch.float32, device=dev)
+    step_lp = torch.empty((N, R), dtype=torch.float32, device=dev)
+    step_ent = torch.empty((N, R), dtype=torch.float32, device=dev)
     metrics_acc = torch.zeros(8, dtype=torch.float32, device=dev)
+    grpo_timer, plan_timer, fold_timer = KernelTimer(), KernelTimer(), KernelTimer()
+    timers = timers + (grpo_timer, plan_timer, fold_timer)
 
     def step(step_idx):
         # ---- rollout: R decode steps over [N, V] logits (row stride R*V in the resident tensor)
@@ -245,10 +260,13 @@ def run(args):
                     lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None, ops._stream(dev)))
         # ---- GRPO advantage over the whole batch: contiguous groups of G (the rollout layout), the
         #      pack kernel's per-row reward sums as the scores
-        adv = ops.grpo_advantage(rew, rmask, None, None, ng, scores=scores)
+        adv = grpo_timer.wrap(lambda: ops.grpo_advantage(rew, rmask, None, None, ng, scores=scores))
         # ---- update: per micro-batch fused policy pass (logprob/entropy fwd + PPO/KL loss +
         #      logprob bwd -> dlogits); --unfused runs the four separate kernels instead
         metrics_acc.zero_()
+        if not args.unfused:
+            plan_timer.wrap(lambda: ops._ffi.call("skyrl_policy_train_plan", ops._ptr(lmask), N, R, mb,
+                                                  ctypes.byref(params), ops._ptr(step_ws), ops._stream(dev)))
         for s in range(0, N, mb):
             x = lg_rows(s, mb)
             lab = labels[s:s + mb]
@@ -266,12 +284,15 @@ def run(args):
                 metrics_acc.add_(m)
             else:
                 train_timer.wrap(lambda: ops._ffi.call(
-                    "skyrl_policy_train_fwd", ops._ptr(x), ops.BF16, x.stride(0), x.stride(1), mb, R, V,
-                    ops._ptr(lab), lab.stride(0), lab.stride(1), 1.0, ops._ptr(old_lp[s:s + mb]),
-                    ops._ptr(adv[s:s + mb]), ops._ptr(lmask[s:s + mb]), ops._ptr(ref_lp[s:s + mb]),
-                    ctypes.byref(params), ops._ptr(loss_buf), ops._ptr(met_buf), ops._ptr(lp), ops._ptr(ent),
-                    ops._ptr(dlogits), R * V, V, ops._ptr(train_ws), ops._stream(dev)))
-                metrics_acc.add_(met_buf)
+                    "skyrl_policy_train_micro_fwd", ops._ptr(x), ops.BF16, x.stride(1), mb * R, V, ops._ptr(lab),
+                    lab.stride(0), lab.stride(1), None, s // mb, N, R, mb, 1.0, ops._ptr(old_lp), ops._ptr(adv),
+                    ops._ptr(lmask), ops._ptr(ref_lp), ctypes.byref(params), ops._ptr(step_lp), ops._ptr(step_ent),
+                    ops._ptr(dlogits), V, ops._ptr(step_ws), ops._stream(dev)))
+        if not args.unfused:
+            fold_timer.wrap(lambda: ops._ffi.call("skyrl_policy_train_fold", ops._ptr(lmask), N, R, mb,
+                                                  ctypes.byref(params), ops._ptr(step_loss), ops._ptr(step_met),
+                                                  ops._ptr(step_ws), ops._stream(dev)))
+            torch.sum(step_met, 0, out=metrics_acc)
         if dist_on:
             dist.all_reduce(metrics_acc)
         # ---- optimizer step (one mini-batch per step at 64 prompts): DP gradient reduce-scatter on
@@ -320,7 +341,7 @@ def run(args):
          CEILING_READ_GBS),
         ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
          2 * (N // mb) + (N // mb if args.unfused else 0), CEILING_READ_GBS),
-        ("skyrl_policy_train_fwd (policy_train_split_kernel: each row in 6 pieces of 256 threads)", train_timer,
+        ("skyrl_policy_train_micro_fwd (policy_train_split_kernel: each row in 6 pieces of 256 threads)", train_timer,
          rows_per_launch * (V * 4 + 8 + 20 + 8), 0 if args.unfused else N // mb, CEILING_RW_GBS),
         ("skyrl_adamw_step (sumsq + plan + adamw_update_kernel<shadow>)", adam_timer,
          (reducer.layout.shard_numel * (4 + 30)) if reducer is not None else 0, 1, CEILING_RW_GBS),
@@ -334,6 +355,23 @@ def run(args):
                          "ms_per_step": round(ms * launches_per_step, 2), "launches_timed": tm.launches,
                          "ceiling_GBps": ceiling}
     dom_name = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+    # the advantage + loss launches the product issues per step outside the fused logits pass, eager
+    # and event-timed inside the timed steps (GRPOTrainer: compute_advantages_and_returns' GRPO, then
+    # PolicyTrainStep's plan and fold); the per-token loss terms themselves are computed inside
+    # policy_train's pass (their 40 B/token are in its bytes). Algorithmic bytes: GRPO with the pack
+    # scores reads the int64 response mask and writes adv (12 B/token), the plan reads the loss mask
+    # (4), the fold reads the records and the mask (20).
+    product = None
+    if grpo_timer.pairs and plan_timer.pairs:
+        us = {k: round(t.avg_ms() * 1e3, 2) for k, t in (("grpo_us", grpo_timer), ("plan_us", plan_timer),
+                                                       ("fold_us", fold_timer))}
+        tot = sum(us.values())
+        nbytes = N * R * (12 + 4 + 20)
+        product = dict(us, total_us=round(tot, 2), launches_per_step=3, bytes_per_step=nbytes,
+                       achieved_GBps=round(nbytes / (tot * 1e-6) / 1e9, 1),
+                       frac=round(nbytes / (tot * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                       note="eager, event-timed in the timed steps: exactly the launches GRPOTrainer issues per "
+                            "step for GRPO + the loss outside the fused logits pass")
     dom = kernels[dom_name]
     result = {
         "metric": "trained samples/sec (rollout+update), Qwen2.5-1.5B GRPO at 1/2/4/8 MI355X",
@@ -358,6 +396,9 @@ def run(args):
             "optimizer": "sharded AdamW (fp32 master, bf16 rollout copy), reduce-scatter + all-gather over RCCL",
             "collectives": (dist.get_backend() + (" (one-rank group, SKYRL_FORCE_COLLECTIVES)" if world == 1 else ""))
             if dist_on else "none (world size 1)",
+            "launch": ("single process" if world == 1 else
+                       "bench.py --gpus N -> torch.distributed.run child, one rank per GPU"
+                       if os.environ.get("SKYRL_BENCH_SPAWNED") == "1" else "external torch.distributed.run"),
         },
         "roofline": {
             "kernel": dom_name,
@@ -374,18 +415,20 @@ def run(args):
         },
         "kernels": kernels,
         "advantage_loss": None,
+        "advantage_loss_product": product,
         "cpu_baseline": None,
     }
-    if not args.no_adv_loss_leg:
+    legs = rank == 0  # the single-GPU legs after the timed region: rank 0 only; the others wait at the barrier
+    if legs and not args.no_adv_loss_leg:
         result["advantage_loss"] = {"batch": advantage_loss_leg(dev, N, R, variants=args.adv_loss_variants),
                                     "batch_x16": advantage_loss_leg(dev, 16 * N, R, reps=5)}
-    if not args.no_attention_leg:
+    if legs and not args.no_attention_leg:
         result["rollout_attention"] = rollout_attention_leg(dev, N)
-    if not args.no_lmhead_leg:
+    if legs and not args.no_lmhead_leg:
         result["rollout_lmhead_sample"] = lmhead_sample_leg(dev, N)
-    if not args.no_filtered_leg:
+    if legs and not args.no_filtered_leg:
         result["sampler_filtered"] = sampler_filtered_leg(dev, N, V)
-    if not args.no_vocab_legs:
+    if legs and not args.no_vocab_legs:
         result["policy_train_vocabs"] = policy_train_vocab_legs(dev, mb, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
@@ -397,6 +440,7 @@ def run(args):
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist_on:
+        dist.barrier()  # every rank leaves together (rank 0 ran the legs)
         dist.destroy_process_group()
 
 
@@ -405,17 +449,33 @@ def end_to_end_leg(timeout_s=900):
     process): random-init Qwen2.5-1.5B policy + ref, AMDInferenceEngine rollout of 512
     trajectories (responses U[1,1024]), HF learner fwd/bwd with the HIP logprob/loss path, AdamW,
     weight sync. Informational: the headline value above is the hot path (north star)."""
+    import collections
     import subprocess
+    import threading
 
     cmd = [sys.executable, "-u", os.path.join(ROOT, "scripts", "e2e_bench.py"), "--steps", "1", "--warmup", "1"]
+    tail = collections.deque(maxlen=40)  # the child's last stderr lines, kept for the JSON on failure
+
+    def pump(stream):  # forward the child's stderr live (progress) and remember its tail
+        for ln in stream:
+            sys.stderr.write(ln)
+            tail.append(ln.rstrip("\n"))
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    th = threading.Thread(target=pump, args=(p.stderr,), daemon=True)
+    th.start()
     try:
-        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, timeout=timeout_s, text=True)
-        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-        if p.returncode != 0 or not lines:
-            return {"error": f"exit {p.returncode}"}
-        return json.loads(lines[-1])
+        out, _ = p.communicate(timeout=timeout_s)
     except subprocess.TimeoutExpired:
-        return {"error": f"timeout after {timeout_s}s"}
+        p.kill()
+        p.communicate()
+        th.join(5)
+        return {"error": f"timeout after {timeout_s}s", "stderr_tail": list(tail)}
+    th.join(5)
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit {p.returncode}", "stderr_tail": list(tail)}
+    return json.loads(lines[-1])
 
 
 def pmc_traffic(kernel_name, algorithmic_bytes):
@@ -439,8 +499,12 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
     inter-kernel gaps are included. The loss-mask row sums and the GRPO scores (per-row reward
     sums) are the pack kernel's (skyrl_pack_experience emits both with the batch).
 
-    `total_us` is the product path (GRPOTrainer._loss -> ops.grpo_ppo_loss(defer_fold=True,
-    want_advantages=False) and its backward): skyrl_grpo_ppo_loss_fwd with the scores and
+    This leg is the standalone loss kernels (graph-replayed), not the trainer's default: GRPOTrainer
+    computes the loss terms inside the fused logits pass and issues GRPO + plan + fold per step,
+    timed eagerly as `advantage_loss_product`; its unfused path runs GRPO once per step and
+    ops.ppo_loss per micro-batch (`loss_fwd_us` + `loss_bwd_us` here).
+    `total_us` is the one-launch form (ops.grpo_ppo_loss(defer_fold=True, want_advantages=False)
+    and its backward): skyrl_grpo_ppo_loss_fwd with the scores and
     SKYRL_LOSS_DEFER_FOLD (GRPO, loss and gradient in one launch that leaves per-block records;
     no advantages output, so the int64 response mask is not read: the loss mask is 0 outside the
     response) + skyrl_ppo_loss_finish (the backward: folds the records into loss/metrics,
@@ -804,9 +868,60 @@ def cpu_baseline(args):
     }
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) from a plain `python bench.py`: start N ranks, one per GPU, under
+    torch.distributed.run (127.0.0.1 rendezvous) as a CHILD process and return its exit code.
+    Called before anything touches the GPU; the parent never initialises HIP (no exec either).
+    The reference starts one NCCL rank per GPU the same way (workers/worker.py:102-126)."""
+    import subprocess
+
+    if not args.dry_run:
+        n_dev = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if n_dev < args.gpus:
+            log(f"--gpus {args.gpus} but only {n_dev} visible GPUs")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC (the host driver's only mode)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env["SKYRL_BENCH_SPAWNED"] = "1"
+    log(f"launching {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args) -> None:
+    """--dry-run: report this process's rank layout and exercise the rendezvous (a gloo
+    all-reduce of the ranks) without any GPU work; one JSON line per rank."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank_sum = rank
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        rank_sum = int(t.item())
+        world = dist.get_world_size()
+        dist.destroy_process_group()
+    print(json.dumps({"dry_run": True, "rank": rank, "world_size": world, "local_rank": local, "gpus": args.gpus,
+                      "master_addr": os.environ.get("MASTER_ADDR"), "rank_sum": rank_sum,
+                      "collectives": "nccl" if world > 1 else "none (world size 1)"}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU, RCCL); from a plain `python bench.py` N > 1 starts them itself")
+    ap.add_argument("--dry-run", action="store_true", help="print the rank layout and stop before any GPU work")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -827,6 +942,11 @@ def main():
     ap.add_argument("--cpu-sampler-steps", type=int, default=64)
     ap.add_argument("--cpu-logprob-tokens", type=int, default=256)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, sys.argv[1:]))
+    if args.dry_run:
+        dry_run(args)
+        return
     run(args)
 
 

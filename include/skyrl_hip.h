@@ -45,7 +45,8 @@ const char* skyrl_last_error(void);
  * reward row sums (GRPO scores), skyrl_grpo_advantage / skyrl_grpo_ppo_loss_fwd take them,
  * the loss forwards take flags (SKYRL_LOSS_DEFER_FOLD) and skyrl_ppo_loss_finish; 6:
  * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange; 7:
- * skyrl_comm_* RCCL collectives). */
+ * skyrl_comm_* RCCL collectives; 8: the step form of the fused policy pass,
+ * skyrl_policy_train_plan / _micro_fwd / _fold). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -344,6 +345,41 @@ int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int
                                   const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
                                   float* logp_out, float* entropy_out, void* grad_logits, int64_t ld_grad,
                                   void* workspace, void* stream);
+/* Step form: one mini-batch of n_total rows in micro-batches of micro_rows (the last one may be
+ * short), the loss folded once per mini-batch. The reference's micro-batch loop
+ * (workers/worker.py:731-900) reads loss and metrics only after the mini-batch's backward
+ * passes (optim_step, :900-925), and the loss's reduction scales depend on the loss mask only,
+ * so: skyrl_policy_train_plan computes every micro-batch's scales in one launch (one workgroup
+ * per micro-batch); skyrl_policy_train_micro_fwd is the fused pass of micro-batch `micro`
+ * alone (no scales or epilogue launch); skyrl_policy_train_fold folds every micro-batch's
+ * per-token records into loss_out[n_micro] and metrics_out[n_micro * SKYRL_M_COUNT] in one
+ * launch. Per micro-batch the loss and metrics are the bits skyrl_policy_train_fwd /
+ * _ragged_fwd return for it (same code and order; a position with loss mask 0 contributes
+ * nothing). All per-token arrays (old / adv / loss_mask / ref, logp_out / entropy_out) are
+ * the mini-batch's f32 [n_total, R]; loss_mask is required. micro_fwd, dense form
+ * (token_pos NULL): ntok = rows * R, position (b, t) of the micro-batch is logits row b*R + t
+ * (logits + (b*R + t)*ld), labels at labels + b*label_stride_b + t*label_stride_t; packed form:
+ * token q of the launch at logits + q*ld, labels[q*label_stride_t], token_pos[q] its position
+ * within the micro-batch's [rows, R]. Same V / alignment rules as skyrl_policy_train_ragged_fwd.
+ * The plan must precede the micro-batch launches and the fold follow them on one stream; the
+ * workspace (skyrl_policy_train_step_workspace_bytes, zeroed once) must not be shared by two
+ * mini-batches in flight. At most 4096 micro-batches. */
+size_t skyrl_policy_train_step_workspace_bytes(int32_t n_total, int32_t R, int32_t micro_rows);
+int skyrl_policy_train_plan(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
+                            const skyrl_ppo_params* params, void* workspace, void* stream);
+int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
+                                 const int64_t* labels, int64_t label_stride_b, int64_t label_stride_t,
+                                 const int32_t* token_pos, int32_t micro, int32_t n_total, int32_t R,
+                                 int32_t micro_rows, float temperature, const float* old_log_probs,
+                                 const float* advantages, const float* loss_mask, const float* ref_log_probs,
+                                 const skyrl_ppo_params* params, float* logp_out, float* entropy_out,
+                                 void* grad_logits, int64_t ld_grad, void* workspace, void* stream);
+int skyrl_policy_train_fold(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
+                            const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                            void* workspace, void* stream);
+/* 1 if the packed and step forms take vocabulary V (aligned: rows 16-B aligned and V % 8 == 0)
+ * at this temperature, else 0: the same plan their launches make. */
+int skyrl_policy_train_supports(int32_t V, int32_t aligned, float temperature);
 /* x[i] *= g[0] over a bf16 buffer; a no-op kernel when g[0] == 1. */
 int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream);
 

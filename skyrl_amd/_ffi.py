@@ -147,6 +147,15 @@ SIGNATURES = {
         [_P, _INT, _I64, _I32, _I32, _P, _P, _I32, _I32, _F, _P, _P, _P, _P, ctypes.POINTER(PPOParams), _P, _P, _P,
          _P, _P, _I64, _P, _P],
     ),
+    "skyrl_policy_train_step_workspace_bytes": (_SZ, [_I32, _I32, _I32]),
+    "skyrl_policy_train_plan": (_INT, [_P, _I32, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P]),
+    "skyrl_policy_train_micro_fwd": (
+        _INT,
+        [_P, _INT, _I64, _I32, _I32, _P, _I64, _I64, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P,
+         ctypes.POINTER(PPOParams), _P, _P, _P, _I64, _P, _P],
+    ),
+    "skyrl_policy_train_fold": (_INT, [_P, _I32, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P]),
+    "skyrl_policy_train_supports": (_INT, [_I32, _I32, _F]),
     "skyrl_scale_bf16_by_device_scalar": (_INT, [_P, _P, _I64, _P]),
     "skyrl_sample_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_sample": (_INT, [_P, _INT, _I64, _I32, _I32, _F, _I32, _F, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),

@@ -221,7 +221,7 @@ class ShardedAdamW:
     """
 
     def __init__(self, reducer: GradReducer, init_params: torch.Tensor, config: AdamWConfig = AdamWConfig(),
-                 shadow_bf16: bool = True):
+                 shadow_bf16: bool = True, gather_bf16: bool = True):
         from . import _ffi
         from .ops import _require_gpu
 
@@ -244,10 +244,13 @@ class ShardedAdamW:
         self.exp_avg = torch.zeros_like(self.param)
         self.exp_avg_sq = torch.zeros_like(self.param)
         self.weights_bf16 = torch.empty(lay.padded, dtype=torch.bfloat16, device=dev) if shadow_bf16 else None
+        # gather_bf16=False (world > 1): the owner fills weights_bf16 itself (ShardedModuleOptimizer
+        # casts it from the gathered fp32 master), so the update pass writes no bf16 shard
+        self.gather_bf16 = gather_bf16
         if shadow_bf16 and not reducer.collective:
             self.weights_bf16.copy_(flat)
             self.shard_bf16 = self.weights_bf16
-        elif shadow_bf16:
+        elif shadow_bf16 and gather_bf16:
             self.shard_bf16 = self.param.to(torch.bfloat16)
             self._all_gather_weights(sync=True)
         else:
@@ -287,7 +290,7 @@ class ShardedAdamW:
     def sync_weights(self) -> None:
         """Start the learner -> rollout weight all-gather (bf16) on the comm stream; the rollout
         side calls :meth:`wait_weights` before it reads ``weights_bf16``."""
-        if self.weights_bf16 is None or not self.reducer.collective:
+        if self.weights_bf16 is None or not self.reducer.collective or not self.gather_bf16:
             return
         self._all_gather_weights(sync=False)
 
@@ -635,8 +638,8 @@ class ShardedModuleOptimizer:
     as soon as it is complete (buckets strictly in index order, the same collective sequence on
     every rank). :meth:`step` (n_micro) = wait, sharded grad norm + clip + AdamW in one HIP pass
     (non-finite norm: skipped on device), zero grads, re-assemble. Every parameter is updated
-    every step (a parameter that got no gradient in a step sees a zero gradient: AdamW's weight
-    decay and moment decay still apply, where torch.optim.AdamW would skip a None grad).
+    step, except a parameter no rank's backward reached since the last step: like a None grad in
+    torch.optim.AdamW its master weights and moments are left as they were.
     """
 
     def __init__(self, module: torch.nn.Module, config: AdamWConfig, group=None,
@@ -666,8 +669,11 @@ class ShardedModuleOptimizer:
             self.offsets.append(off)
             init[off:off + p.numel()] = p.detach().reshape(-1)
             off += p.numel()
-        self.opt = ShardedAdamW(self.reducer, init, config, shadow_bf16=True)
+        # world > 1: the bf16 engine copy is cast from the gathered fp32 master on every rank
+        # (_gather_full), so ShardedAdamW keeps no bf16 shard of its own to all-gather
+        self.opt = ShardedAdamW(self.reducer, init, config, shadow_bf16=True, gather_bf16=not self.collective)
         del init
+        self._weights_ready = None
         if not self.collective:
             self.full = self.opt.param
         else:
@@ -683,7 +689,10 @@ class ShardedModuleOptimizer:
             for b in range(b0, b1 + 1):
                 self._bucket_count[b] += 1
         self._index = {id(p): i for i, (_, p) in enumerate(self.named)}
+        self._touched = [False] * len(self.named)  # parameters a backward reached since the last step
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p in self.named]
+        # the module's next forward reads the re-assembled master: it waits for the in-flight gather
+        self._fwd_hook = module.register_forward_pre_hook(lambda m, a: self.wait_weights())
         self._armed = False
         self.launched_during_backward = 0
 
@@ -713,9 +722,10 @@ class ShardedModuleOptimizer:
             self.launched_during_backward += 1
 
     def _on_grad(self, p) -> None:
+        i = self._index[id(p)]
+        self._touched[i] = True
         if not self._armed:
             return
-        i = self._index[id(p)]
         if self._fired[i]:
             return
         self._fired[i] = True
@@ -736,17 +746,61 @@ class ShardedModuleOptimizer:
 
     # ---------------------------------------------------------------- step
     def step(self, n_micro: int = 1, lr: Optional[float] = None) -> torch.Tensor:
-        """optim_step: grads * 1/n_micro (and 1/world), clip, AdamW, zero grads; then the updated
-        master is re-assembled on every rank and the bf16 engine copy is all-gathered. Returns
-        the pre-clip grad norm (device scalar)."""
+        """optim_step: grads * 1/n_micro (and 1/world), clip, AdamW, zero grads; then (world > 1)
+        the updated master is re-assembled on every rank by one fp32 all-gather per bucket and the
+        engine's bf16 copy is cast from it on the same comm stream (each rank casts locally: no
+        second, bf16 all-gather over xGMI). Both are left in flight: the module's next forward
+        (a forward pre-hook), :meth:`named_bf16` and :meth:`wait_weights` make the current stream
+        wait for them, so the exchange overlaps whatever the host issues next (the engine's
+        rollout in the fully-async loop, fully_async_trainer.py:415-419). Returns the pre-clip grad
+        norm (device scalar)."""
         self._finish_exchange()
         self._check_grad_views()  # the .grad views must still be the buckets' storage
+        keep = self._untouched_ranges()
+        saved = [(t, o, t[o:o + n].clone()) for o, n in keep
+                 for t in (self.opt.param, self.opt.exp_avg, self.opt.exp_avg_sq)]
         gn = self.opt.step(n_micro=n_micro, lr=lr, zero_grad=True)
+        for t, o, v in saved:  # torch.optim.AdamW skips a parameter whose .grad is None
+            t[o:o + v.numel()].copy_(v)
+        self._touched = [False] * len(self.named)
         if self.collective:
             self._gather_full(sync=False)
-            self.opt.sync_weights()
-            self.opt.wait_weights()  # the next forward (and the engine) read them
         return gn
+
+    def _untouched_ranges(self) -> List[Tuple[int, int]]:
+        """(shard offset, length) of every piece of this rank's shard that belongs to a parameter
+        no rank's backward reached since the last step (one MAX all-reduce of the flags at
+        world > 1). Their master weights and moments are restored after the update, as
+        torch.optim.AdamW and the reference's FSDP2 optimizer skip a None grad (their shared
+        step counter still advances, so a later update of such a parameter uses the global
+        step's bias correction)."""
+        flags = self._touched
+        if self.collective:
+            t = torch.tensor([int(f) for f in flags], dtype=torch.int32, device=self.full.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.reducer.group)
+            flags = [bool(f) for f in t.tolist()]
+        if all(flags):
+            return []
+        lay = self.reducer.layout
+        out = []
+        for i, f in enumerate(flags):
+            if f:
+                continue
+            o, n = self.offsets[i], self.named[i][1].numel()
+            b0, b1 = self._param_buckets[i]
+            for b in range(b0, b1 + 1):
+                ps, pe = lay.piece(b, self.rank) if self.collective else lay.buckets[b]
+                lo, hi = max(o, ps), min(o + n, pe)
+                if hi > lo:
+                    out.append((lay.piece_off[b] + lo - ps if self.collective else lo, hi - lo))
+        return out
+
+    def wait_weights(self) -> None:
+        """Make the current stream wait for the last step's all-gather + bf16 cast (no host sync)."""
+        ev = self._weights_ready
+        if ev is not None:
+            torch.cuda.current_stream(self.full.device).wait_event(ev)
+            self._weights_ready = None
 
     def _check_grad_views(self) -> None:
         base = self.reducer.grad.data_ptr()
@@ -756,6 +810,11 @@ class ShardedModuleOptimizer:
                                    "(set_to_none / reassigned); the exchange would miss it")
 
     def _gather_full(self, sync: bool) -> None:
+        """fp32 all-gather of the updated shards into the full master (one per bucket, comm stream),
+        then the bf16 engine copy cast from it on that stream; records ``_weights_ready``."""
+        from . import _ffi
+        from .ops import _ptr
+
         r = self.reducer
         lay = r.layout
         ready = torch.cuda.Event()
@@ -766,13 +825,18 @@ class ShardedModuleOptimizer:
                 po = lay.piece_off[b]
                 nb = (e - s) // r.world
                 dist.all_gather_into_tensor(self.full[s:e], self.opt.param[po:po + nb], group=r.group)
+            w = self.opt.weights_bf16
+            _ffi.call("skyrl_cast_bf16", _ptr(self.full), _ptr(w), w.numel(), ctypes.c_void_p(r.stream.cuda_stream))
+            self._weights_ready = torch.cuda.Event()
+            self._weights_ready.record(r.stream)
         if sync:
-            torch.cuda.current_stream(self.full.device).wait_stream(r.stream)
+            self.wait_weights()
 
     # ---------------------------------------------------------------- weight sync
     def named_bf16(self) -> List[Tuple[str, torch.Tensor]]:
         """(HF name, bf16 view) of every parameter in the engine copy: the weight update request
         of broadcast_to_inference_engines without a per-parameter cast."""
+        self.wait_weights()
         w = self.opt.weights_bf16
         return [(n, w[o:o + p.numel()].view(p.shape)) for (n, p), o in zip(reversed(self.named),
                                                                           reversed(self.offsets))]

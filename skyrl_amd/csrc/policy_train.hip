@@ -145,9 +145,12 @@ __device__ __forceinline__ void ppo_token(float lp, float old, float A, float lo
 // ---- 1. mask statistics -> gradient scales -------------------------------------------
 // One wave per row (rows strided over the 16 waves); scal[0] = sum m,
 // scal[1] = entropy-gradient scale (-coef/max(sum m,1) or 0), scal[2] = 1/max(sum m,1).
-__global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __restrict__ mask, int n, int R,
-                                                                skyrl_ppo_params p, float* __restrict__ row_scale,
-                                                                float* __restrict__ scal) {
+// Header word 16 is the split kernel's exchange tag for the launch(es) these scales serve:
+// the single-call entries advance it by one per launch; the step plan (skyrl_policy_train_plan)
+// gives micro-batch k the tag (c << 12) | k with c its slot's own counter, so every launch of
+// every step carries a tag no other launch that shares the granules carries.
+__device__ __forceinline__ void scales_body(const float* __restrict__ mask, int n, int R, const skyrl_ppo_params& p,
+                                            float* __restrict__ row_scale, float* __restrict__ scal, int step_k) {
     __shared__ double s_tot[kWaves];
     const int lane = threadIdx.x & 63, w = threadIdx.x / kWave;
     double tot = 0.0;
@@ -174,12 +177,32 @@ __global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __r
         // this launch's tag for the split kernel's exchange granules (header word 16, see
         // skyrl_policy_train_fwd); the previous launch's granules carry the previous tag
         unsigned* epoch = reinterpret_cast<unsigned*>(scal) + 16;
-        epoch[0] = epoch[0] + 1u;
+        epoch[0] = step_k < 0 ? epoch[0] + 1u : ((((epoch[0] >> 12) + 1u) << 12) | (unsigned)step_k);
     }
     if (p.loss_reduction == 0) {
         const float sc = (float)(1.0 / d);
         for (int b = threadIdx.x; b < n; b += kThreads) row_scale[b] = sc;
     }
+}
+
+__global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __restrict__ mask, int n, int R,
+                                                                skyrl_ppo_params p, float* __restrict__ row_scale,
+                                                                float* __restrict__ scal) {
+    scales_body(mask, n, R, p, row_scale, scal, -1);
+}
+
+// The step plan: block k = micro-batch k (rows [k*mb, min(n_total, (k+1)*mb))), the same code
+// and summation order as the per-call kernel above, so its scales are those bits; its scalars
+// sit in micro slot k (kStepSlot bytes each).
+constexpr int kStepSlot = 256;
+__global__ __launch_bounds__(kThreads) void train_plan_kernel(const float* __restrict__ mask, int n_total, int R,
+                                                              int mb, skyrl_ppo_params p,
+                                                              float* __restrict__ row_scale,
+                                                              char* __restrict__ slots) {
+    const int k = blockIdx.x;
+    const int r0 = k * mb;
+    const int n = min(n_total, r0 + mb) - r0;
+    scales_body(mask + (int64_t)r0 * R, n, R, p, row_scale + r0, reinterpret_cast<float*>(slots + k * kStepSlot), k);
 }
 
 // ---- 2. fused sweep pair per token ------------------------------------------------------
@@ -511,7 +534,10 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
 // (metrics[6] = 1 via the epilogue; ops.check_loss_metrics raises) and leaves NaN in that
 // row's terms instead of hanging.
 constexpr int kSplitMaxP = 12;  // most pieces per row of any built shape (split_shapes below)
-constexpr unsigned kSplitMaxPolls = 1u << 20;
+// the exchange's time bound, on the 100 MHz constant clock (s_memrealtime): partners are resident
+// or next to be dispatched, so they arrive within microseconds unless other streams' kernels hold
+// the CUs; 2 s lets any such kernel finish, where an iteration bound (~60 ms) did not
+constexpr uint64_t kSplitTimeoutTicks = 200000000ull;
 
 typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
 typedef __attribute__((address_space(1))) unsigned ptr_gu32;
@@ -638,9 +664,11 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
         }
         if (lane < P * 3 && q != part) {
             unsigned long long x = 0;
-            for (unsigned polls = 0; polls < kSplitMaxPolls; ++polls) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
                 x = __hip_atomic_load((const ptr_gu64*)(g + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((unsigned)(x >> 32) == epoch) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kSplitTimeoutTicks) break;
                 __builtin_amdgcn_s_sleep(2);
             }
             const bool ok = (unsigned)(x >> 32) == epoch;
@@ -719,12 +747,13 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
 // ---- 3. loss scalar + metrics ---------------------------------------------------------
 // One wave per row: row sums of loss*m, kl*m*m, m -> sequence-level terms in fp64;
 // token-level sums (loss*m, clip*m, ent*m) folded over the block; same metric layout as
-// skyrl_ppo_loss_fwd.
-__global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* __restrict__ tok,
-                                                                  const float* __restrict__ mask, int n, int R,
-                                                                  skyrl_ppo_params p, const float* __restrict__ scal,
-                                                                  float* __restrict__ loss_out,
-                                                                  float* __restrict__ metrics) {
+// skyrl_ppo_loss_fwd. MASKED (the step fold): a position whose loss mask is 0 contributes
+// nothing, which lets a packed micro-batch leave the records of positions no token maps to
+// unwritten (every record is premultiplied by m, so for finite terms the sums are the same bits).
+template <bool MASKED>
+__device__ __forceinline__ void epilogue_body(const float* __restrict__ tok, const float* __restrict__ mask, int n,
+                                              int R, const skyrl_ppo_params& p, const float* __restrict__ scal,
+                                              float* __restrict__ loss_out, float* __restrict__ metrics) {
     __shared__ double s_red[kWaves * 5];
     const int lane = threadIdx.x & 63, w = threadIdx.x / kWave;
     // per wave (lane 0): sum l*m, rows_pg, rows_kl; per lane: clip*m, ent*m
@@ -732,12 +761,14 @@ __global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* _
     for (int b = w; b < n; b += kWaves) {
         float a0 = 0.f, a1 = 0.f, am = 0.f;
         for (int t = lane; t < R; t += kWave) {
-            const float4 v = *reinterpret_cast<const float4*>(tok + ((int64_t)b * R + t) * 4);
+            float4 v = *reinterpret_cast<const float4*>(tok + ((int64_t)b * R + t) * 4);
+            const float m = mask ? mask[(int64_t)b * R + t] : 1.f;
+            if (MASKED && m == 0.f) v = make_float4(0.f, 0.f, 0.f, 0.f);
             a0 += v.x;
             a1 += v.z;
             tc += v.y;
             te += v.w;
-            am += mask ? mask[(int64_t)b * R + t] : 1.f;
+            am += m;
         }
         a0 = wave_sum(a0);
         a1 = wave_sum(a1);
@@ -780,6 +811,28 @@ __global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* _
         metrics[7] = 0.f;
         err[0] = 0u;
     }
+}
+
+__global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* __restrict__ tok,
+                                                                  const float* __restrict__ mask, int n, int R,
+                                                                  skyrl_ppo_params p, const float* __restrict__ scal,
+                                                                  float* __restrict__ loss_out,
+                                                                  float* __restrict__ metrics) {
+    epilogue_body<false>(tok, mask, n, R, p, scal, loss_out, metrics);
+}
+
+// The step fold: block k folds micro-batch k's records with the epilogue's code and order, so
+// its loss and metrics are the per-call epilogue's bits (for finite terms, see MASKED).
+__global__ __launch_bounds__(kThreads) void train_fold_kernel(const float* __restrict__ tok,
+                                                              const float* __restrict__ mask, int n_total, int R,
+                                                              int mb, skyrl_ppo_params p, const char* __restrict__ slots,
+                                                              float* __restrict__ loss_out,
+                                                              float* __restrict__ metrics) {
+    const int k = blockIdx.x;
+    const int r0 = k * mb;
+    const int n = min(n_total, r0 + mb) - r0;
+    epilogue_body<true>(tok + (int64_t)r0 * R * 4, mask + (int64_t)r0 * R, n, R, p,
+                        reinterpret_cast<const float*>(slots + k * kStepSlot), loss_out + k, metrics + k * SKYRL_M_COUNT);
 }
 
 // dlogits *= g (skipped when g == 1: the common loss.backward() case)
@@ -1127,4 +1180,117 @@ extern "C" int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_
     hipLaunchKernelGGL(scale_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), g,
                        reinterpret_cast<uint16_t*>(x), n);
     return check_launch("scale_bf16_kernel");
+}
+
+// ---- step form (ABI 8): one plan and one fold per mini-batch instead of two single-workgroup
+// launches per micro-batch. The reference's micro-batch loop (workers/worker.py:731-900) reads
+// loss and metrics only after the mini-batch's backward passes (optim_step, :900-925), so the
+// per-micro-batch fold can wait until then; the scales depend only on the loss mask, so one plan
+// launch computes every micro-batch's before the first pass.
+// Step workspace: [0, 256) header, micro slots (kStepSlot B each: scal[0..2], word 16 the launch's
+// exchange tag, word 32 its timeout flag), row scales (n_total floats), per-token records
+// (n_total * R x 16 B), the exchange granules of one micro-batch (reused by every launch; the
+// tags keep launches apart). Zeroed once at allocation.
+namespace {
+constexpr int kStepMaxMicro = 4096;  // the tag's low 12 bits
+int step_micro_count(int32_t n_total, int32_t mb) { return (n_total + mb - 1) / mb; }
+size_t st_rows_off(int nm) { return 256 + pt_pad((size_t)nm * kStepSlot); }
+size_t st_tok_off(int32_t n_total, int nm) { return st_rows_off(nm) + pt_pad((size_t)n_total * 4); }
+size_t st_gran_off(int32_t n_total, int32_t R, int nm) { return st_tok_off(n_total, nm) + pt_pad((size_t)n_total * R * 16); }
+const char* step_check(int32_t n_total, int32_t R, int32_t mb, const skyrl_ppo_params* params) {
+    if (n_total <= 0 || R <= 0 || mb <= 0) return "bad sizes";
+    if (step_micro_count(n_total, mb) > kStepMaxMicro) return "more than 4096 micro-batches";
+    if (!params) return "null params";
+    if (params->loss_reduction < 0 || params->loss_reduction > 2) return "bad loss_reduction";
+    if (params->loss_reduction == 2 && !(params->max_seq_len > 0.f)) return "seq_mean_token_sum_norm needs max_seq_len";
+    return nullptr;
+}
+}  // namespace
+
+extern "C" size_t skyrl_policy_train_step_workspace_bytes(int32_t n_total, int32_t R, int32_t micro_rows) {
+    if (n_total <= 0 || R <= 0 || micro_rows <= 0) return 256;
+    const int nm = step_micro_count(n_total, micro_rows);
+    return st_gran_off(n_total, R, nm) + (size_t)min(micro_rows, n_total) * R * kSplitMaxP * 3 * 8;
+}
+
+extern "C" int skyrl_policy_train_plan(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
+                                       const skyrl_ppo_params* params, void* workspace, void* stream) {
+    SKYRL_REQUIRE(loss_mask && workspace, "policy_train_plan: null pointer");
+    const char* bad = step_check(n_total, R, micro_rows, params);
+    SKYRL_REQUIRE(bad == nullptr, bad ? bad : "");
+    char* w = reinterpret_cast<char*>(workspace);
+    const int nm = step_micro_count(n_total, micro_rows);
+    hipLaunchKernelGGL(train_plan_kernel, dim3(nm), dim3(kThreads), 0, as_stream(stream), loss_mask, n_total, R,
+                       micro_rows, *params, reinterpret_cast<float*>(w + st_rows_off(nm)), w + 256);
+    return check_launch("train_plan_kernel");
+}
+
+extern "C" int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
+                                            const int64_t* labels, int64_t label_stride_b, int64_t label_stride_t,
+                                            const int32_t* token_pos, int32_t micro, int32_t n_total, int32_t R,
+                                            int32_t micro_rows, float temperature, const float* old_log_probs,
+                                            const float* advantages, const float* loss_mask,
+                                            const float* ref_log_probs, const skyrl_ppo_params* params,
+                                            float* logp_out, float* entropy_out, void* grad_logits, int64_t ld_grad,
+                                            void* workspace, void* stream) {
+    SKYRL_REQUIRE(logits && labels && old_log_probs && advantages && loss_mask && logp_out && grad_logits && workspace,
+                  "policy_train_micro_fwd: null pointer");
+    const char* bad = step_check(n_total, R, micro_rows, params);
+    SKYRL_REQUIRE(bad == nullptr, bad ? bad : "");
+    SKYRL_REQUIRE(dtype == SKYRL_BF16, "policy_train_micro_fwd: logits must be bf16");
+    const int nm = step_micro_count(n_total, micro_rows);
+    SKYRL_REQUIRE(micro >= 0 && micro < nm, "policy_train_micro_fwd: micro-batch index out of range");
+    const int32_t r0 = micro * micro_rows;
+    const int32_t n = min(n_total, r0 + micro_rows) - r0;
+    SKYRL_REQUIRE(ntok > 0 && (int64_t)ntok <= (int64_t)n * R && (token_pos || (int64_t)ntok == (int64_t)n * R),
+                  "policy_train_micro_fwd: bad token count (dense launches cover the micro-batch's n x R positions)");
+    SKYRL_REQUIRE(temperature > 0.f, "policy_train_micro_fwd: temperature must be > 0");
+    SKYRL_REQUIRE(!params->use_kl_loss || ref_log_probs, "policy_train_micro_fwd: use_kl_loss needs ref_log_probs");
+    const auto lgp = reinterpret_cast<uintptr_t>(logits), grp = reinterpret_cast<uintptr_t>(grad_logits);
+    const bool aligned = (V % 8) == 0 && (ld % 8) == 0 && (ld_grad % 8) == 0 && lgp % 16 == 0 && grp % 16 == 0;
+    const SplitPlan sp = split_plan(V, aligned, temperature != 1.0f);
+    SKYRL_REQUIRE(sp.kern != nullptr, "policy_train_micro_fwd: V outside the split kernel's range (V <= 155,648, or "
+                           "114,688 for rows not 16-B aligned)");
+    SKYRL_REQUIRE(ld >= V && ld_grad >= V && lgp % 2 == 0 && (grp - lgp) % 16 == 0 && (ld_grad - ld) % 8 == 0,
+                  "policy_train_micro_fwd: dlogits rows must share the logits rows' offset within 16 B");
+    SKYRL_REQUIRE((int64_t)ntok * sp.parts < (1ll << 31), "policy_train_micro_fwd: too many tokens for one launch");
+    char* w = reinterpret_cast<char*>(workspace);
+    float* scal = reinterpret_cast<float*>(w + 256 + (size_t)micro * kStepSlot);
+    float* row_scale = reinterpret_cast<float*>(w + st_rows_off(nm)) + r0;
+    float* tok = reinterpret_cast<float*>(w + st_tok_off(n_total, nm)) + (int64_t)r0 * R * 4;
+    auto* gran = reinterpret_cast<unsigned long long*>(w + st_gran_off(n_total, R, nm));
+    unsigned* err_word = reinterpret_cast<unsigned*>(scal) + 32;
+    const int64_t o = (int64_t)r0 * R;
+    // dense: position (b, t) of the micro-batch is logits row b * R + t; packed: row q is token q
+    const int64_t sb = token_pos ? 0 : (int64_t)R * ld, gsb = token_pos ? 0 : (int64_t)R * ld_grad;
+    const int64_t lsb = token_pos ? 0 : label_stride_b;
+    hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)ntok * sp.parts)), dim3(sp.threads), 0, as_stream(stream),
+                       reinterpret_cast<const uint16_t*>(logits), sb, ld, R, V, labels, lsb, label_stride_t,
+                       temperature, old_log_probs + o, advantages + o, loss_mask + o,
+                       ref_log_probs ? ref_log_probs + o : nullptr, row_scale, scal, *params, logp_out + o,
+                       entropy_out ? entropy_out + o : nullptr, tok, reinterpret_cast<uint16_t*>(grad_logits), gsb,
+                       ld_grad, g_train_ntstore != 0, gran, err_word, token_pos);
+    return check_launch("policy_train_split_kernel");
+}
+
+extern "C" int skyrl_policy_train_fold(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
+                                       const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                                       void* workspace, void* stream) {
+    SKYRL_REQUIRE(loss_mask && loss_out && metrics_out && workspace, "policy_train_fold: null pointer");
+    const char* bad = step_check(n_total, R, micro_rows, params);
+    SKYRL_REQUIRE(bad == nullptr, bad ? bad : "");
+    char* w = reinterpret_cast<char*>(workspace);
+    const int nm = step_micro_count(n_total, micro_rows);
+    hipLaunchKernelGGL(train_fold_kernel, dim3(nm), dim3(kThreads), 0, as_stream(stream),
+                       reinterpret_cast<const float*>(w + st_tok_off(n_total, nm)), loss_mask, n_total, R,
+                       micro_rows, *params, w + 256, loss_out, metrics_out);
+    return check_launch("train_fold_kernel");
+}
+
+// 1 when the packed / step forms (split kernel) take vocabulary V: rows 16-B aligned with
+// V % 8 == 0 (aligned = 1) or otherwise (the EDGE form), at this temperature; the same plan
+// the launches make, so a host that asks first never gets their range error.
+extern "C" int skyrl_policy_train_supports(int32_t V, int32_t aligned, float temperature) {
+    if (V <= 0 || !(temperature > 0.f)) return 0;
+    return split_plan(V, aligned != 0 && (V % 8) == 0, temperature != 1.0f).kern != nullptr ? 1 : 0;
 }

@@ -727,6 +727,120 @@ def policy_train_ragged(logits, labels, token_pos, old_log_probs, advantages, lo
                                            ref_log_probs, params, temperature)
 
 
+_STEP_LAYOUT: Dict[Tuple, Tuple[int, int, int]] = {}
+
+
+class PolicyTrainStep:
+    """One mini-batch's fused policy passes in the step form (ABI 8, policy_train.hip):
+
+      step = PolicyTrainStep(old, adv, loss_mask, params, micro_rows, ref_log_probs=ref)  # plan: 1 launch
+      for k, (i, j) in enumerate(micro-batches):
+          loss_k = step.micro(k, z_k, labels_k, token_pos_k)   # the fused pass of micro-batch k
+          loss_k.backward()                                    # dlogits were written by the pass
+      losses, metrics = step.fold()                            # every micro-batch's loss: 1 launch
+
+    The reference's micro-batch loop (workers/worker.py:731-900) reads loss and metrics only
+    after the mini-batch's backward passes (optim_step :900-925), so the per-micro-batch fold
+    waits until then; the per-call form (policy_train / policy_train_ragged) pays two
+    single-workgroup launches (scales, epilogue) per micro-batch instead. Per micro-batch the
+    loss and metrics are the per-call form's bits. `micro` returns a 0-d view of `self.loss[k]`,
+    valid after `fold()` (stream-ordered; nothing between reads it). Per-token arrays are the
+    mini-batch's [n_total, R]; `self.logp` / `self.entropy` collect the passes' outputs
+    (positions no packed token maps to stay 0). One mini-batch in flight per device and stream
+    (the workspace is shared)."""
+
+    def __init__(self, old_log_probs, advantages, loss_mask, params, micro_rows: int, ref_log_probs=None,
+                 temperature: float = 1.0):
+        dev = _require_gpu(old_log_probs, advantages, loss_mask, ref_log_probs)
+        self.dev = dev
+        self.old = _f32c(old_log_probs.detach(), "old_log_probs")
+        n_total, R = self.old.shape
+        self.adv = _f32c(advantages.detach(), "advantages")
+        self.mask = loss_mask.detach().to(torch.float32).contiguous()
+        self.ref = None if ref_log_probs is None else _f32c(ref_log_probs.detach(), "ref_log_probs")
+        for name, t in (("advantages", self.adv), ("loss_mask", self.mask), ("ref_log_probs", self.ref)):
+            if t is not None and tuple(t.shape) != (n_total, R):
+                raise ValueError(f"{name} shape {tuple(t.shape)} != {(n_total, R)}")
+        if micro_rows <= 0:
+            raise ValueError("micro_rows must be positive")
+        self.params, self.temperature = params, float(temperature)
+        self.n_total, self.R, self.mb = int(n_total), int(R), int(micro_rows)
+        self.n_micro = -(-self.n_total // self.mb)
+        nbytes = _ffi.query("skyrl_policy_train_step_workspace_bytes", self.n_total, self.R, self.mb)
+        self.ws = WORKSPACES.get(dev, "policy_train_step", nbytes)
+        key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+        layout = (self.n_total, self.R, self.mb)
+        if _STEP_LAYOUT.get(key) != layout:  # regions moved: no stale exchange granules in the new places
+            self.ws.zero_()
+            _STEP_LAYOUT[key] = layout
+        self.loss = torch.empty(self.n_micro, dtype=torch.float32, device=dev)
+        self.metrics = torch.empty((self.n_micro, _ffi.M_COUNT), dtype=torch.float32, device=dev)
+        self.logp = torch.zeros((self.n_total, self.R), dtype=torch.float32, device=dev)
+        self.entropy = torch.zeros((self.n_total, self.R), dtype=torch.float32, device=dev)
+        _ffi.call("skyrl_policy_train_plan", _ptr(self.mask), self.n_total, self.R, self.mb, ctypes.byref(params),
+                  _ptr(self.ws), _stream(dev))
+
+    def rows(self, k: int) -> Tuple[int, int]:
+        return k * self.mb, min(self.n_total, (k + 1) * self.mb)
+
+    def micro(self, k: int, logits, labels, token_pos=None):
+        """Micro-batch k's fused pass. Dense: logits [rows, R, V] (unit vocab stride, rows of
+        one [rows*R, V] matrix) and labels [rows, R]; packed: logits [ntok, V], labels [ntok]
+        and token_pos [ntok] (positions within the micro-batch's [rows, R]). Returns the
+        micro-batch's loss (0-d, differentiable w.r.t. logits; its value is written by fold())."""
+        return _PolicyTrainMicroFunction.apply(logits, labels, token_pos, self, int(k))
+
+    def fold(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        _ffi.call("skyrl_policy_train_fold", _ptr(self.mask), self.n_total, self.R, self.mb,
+                  ctypes.byref(self.params), _ptr(self.loss), _ptr(self.metrics), _ptr(self.ws), _stream(self.dev))
+        return self.loss, self.metrics
+
+
+class _PolicyTrainMicroFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, token_pos, step, k):
+        dev = _require_gpu(logits, labels, token_pos)
+        if not 0 <= k < step.n_micro:
+            raise IndexError(f"micro-batch {k} of {step.n_micro}")
+        r0, r1 = step.rows(k)
+        lg = logits.detach()
+        if lg.dtype != torch.bfloat16 or lg.stride(-1) != 1:
+            raise TypeError("policy pass: logits must be bf16 with unit vocab stride")
+        V = lg.shape[-1]
+        if token_pos is None:  # dense [rows, R, V]: rows of one [rows*R, V] matrix
+            if lg.dim() != 3 or tuple(lg.shape[:2]) != (r1 - r0, step.R) or lg.stride(0) != step.R * lg.stride(1):
+                raise ValueError(f"dense logits must be [{r1 - r0}, {step.R}, V] rows of one matrix")
+            ntok, ld = (r1 - r0) * step.R, lg.stride(1)
+            lab = labels.detach().to(device=dev, dtype=torch.int64)
+            if tuple(lab.shape) != (r1 - r0, step.R):
+                raise ValueError("labels must be [rows, R]")
+            lsb, lst, pos = lab.stride(0), lab.stride(1), None
+        else:
+            if lg.dim() != 2:
+                raise ValueError("packed logits must be [ntok, V]")
+            ntok, ld = lg.shape[0], lg.stride(0)
+            lab = labels.detach().to(device=dev, dtype=torch.int64).contiguous().view(-1)
+            pos = token_pos.detach().to(device=dev, dtype=torch.int32).contiguous().view(-1)
+            if lab.numel() != ntok or pos.numel() != ntok:
+                raise ValueError(f"labels / token_pos need {ntok} entries, got {lab.numel()} / {pos.numel()}")
+            lsb, lst = 0, 1
+        dx = torch.empty(lg.shape, dtype=torch.bfloat16, device=dev)
+        ld_grad = dx.stride(-2)
+        _ffi.call("skyrl_policy_train_micro_fwd", _ptr(lg), BF16, ld, ntok, V, _ptr(lab), lsb, lst, _ptr(pos), k,
+                  step.n_total, step.R, step.mb, step.temperature, _ptr(step.old), _ptr(step.adv), _ptr(step.mask),
+                  _ptr(step.ref), ctypes.byref(step.params), _ptr(step.logp), _ptr(step.entropy), _ptr(dx), ld_grad,
+                  _ptr(step.ws), _stream(dev))
+        ctx.save_for_backward(dx)
+        return step.loss[k]
+
+    @staticmethod
+    def backward(ctx, g_loss):
+        (dx,) = ctx.saved_tensors
+        g = g_loss.detach().to(torch.float32).reshape(1).contiguous()
+        _ffi.call("skyrl_scale_bf16_by_device_scalar", _ptr(g), _ptr(dx), dx.numel(), _stream(dx.device))
+        return dx, None, None, None, None
+
+
 # ---------------------------------------------------------------------------- a1 sampler
 def sample(
     logits: torch.Tensor,

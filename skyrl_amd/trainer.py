@@ -313,39 +313,54 @@ class GRPOTrainer:
 
     def _train_policy(self, data) -> Dict[str, float]:
         """_execute_training_step: mini-batches of policy_mini_batch_size prompts (no shuffle,
-        trainer.py:1067-1081), micro-batches inside, loss scaled by 1/n_micro, grad clip, AdamW."""
+        trainer.py:1067-1081), micro-batches inside, loss scaled by 1/n_micro, grad clip, AdamW.
+        With the fused pass every mini-batch is one ops.PolicyTrainStep: one plan launch (the
+        loss scales of all its micro-batches), the micro-batches' fused passes, one fold launch
+        (every micro-batch's loss and metrics), read once and checked before the optimizer
+        step, so a failed exchange never reaches the weights."""
         from . import ops
 
         self.policy.train()  # worker.py:750
         cfg = self.cfg
-        self._grpo_G = self._fused_grpo_group_size(data)
         n = len(data["sequences"])
         mini = cfg.policy_mini_batch_size * cfg.n_samples_per_prompt
         mb = cfg.micro_train_batch_size_per_gpu
         R = data["response_mask"].shape[1]
+        fused = self._fused_pass_ok()
         acc: Dict[str, List[float]] = {}
         for _ in range(cfg.update_epochs_per_batch):
             for s0, s1 in trainer_utils.mini_batch_slices(n, mini):
                 n_micro = math.ceil((s1 - s0) / mb)
+                step = None
+                if fused:
+                    step = ops.PolicyTrainStep(
+                        data["action_log_probs"][s0:s1], data["advantages"][s0:s1], data["loss_mask"][s0:s1],
+                        self.loss_params, mb,
+                        ref_log_probs=data["base_action_log_probs"][s0:s1] if self.ref is not None else None,
+                        temperature=cfg.temperature)
                 mets = []
-                for i in range(s0, s1, mb):
+                for k, i in enumerate(range(s0, s1, mb)):
                     j = min(i + mb, s1)
-                    ref = data["base_action_log_probs"][i:j] if self.ref is not None else None
-                    if self._fused_pass_ok():
-                        loss, met = self._fused_policy_pass(data, i, j, R, ref)
+                    if step is not None:
+                        loss = self._fused_policy_pass(step, k, data, i, j, R)
                     else:
+                        ref = data["base_action_log_probs"][i:j] if self.ref is not None else None
                         lp, ent = self._logprobs(self.policy, data["sequences"][i:j], data["attention_mask"][i:j],
                                                  R, grad=True)
                         loss, met = self._loss(lp, data, i, j, ref, ent)
+                        mets.append(met)
                     if self.optim is not None:
                         if j == s1:
                             self.optim.arm()  # the last micro-batch: buckets reduce-scatter during its backward
-                        loss.backward()  # 1/n_micro is applied by the optimizer step (worker.py:909-914)
+                        if loss is not None:
+                            loss.backward()  # 1/n_micro is applied by the optimizer step (worker.py:909-914)
                     else:
                         if self.grad_sync is not None and j == s1:
                             self.grad_sync.arm()  # the last micro-batch: buckets all-reduce during its backward
-                        (loss / n_micro).backward()
-                    mets.append(met)
+                        if loss is not None:
+                            (loss / n_micro).backward()
+                allm = (step.fold()[1] if step is not None else torch.stack(mets)).cpu()  # one host read
+                ops.check_loss_metrics(allm)  # before the optimizer step: nothing NaN reaches the weights
                 if self.optim is not None:
                     grad_norm = self.optim.step(n_micro)
                 else:
@@ -357,32 +372,37 @@ class GRPOTrainer:
                         self.grad_sync.zero_grad()
                     else:
                         self.optimizer.zero_grad(set_to_none=True)
-                allm = torch.cat([torch.stack(mets), grad_norm.reshape(1, 1).float().expand(1, len(mets[0]))]).cpu()
-                ops.check_loss_metrics(allm[:-1])  # the one host read of the mini-batch's metrics
-                grad_norm = float(allm[-1, 0])
-                mt = allm[:-1].mean(0).tolist()
+                grad_norm = float(grad_norm)
+                mt = allm.mean(0).tolist()
                 for k, v in (("final_loss", mt[0]), ("policy_loss", mt[1]), ("policy_entropy", mt[2]),
-                             ("policy_kl", mt[3]), ("ppo_clip_ratio", mt[4]), ("grad_norm", float(grad_norm))):
+                             ("policy_kl", mt[3]), ("ppo_clip_ratio", mt[4]), ("grad_norm", grad_norm)):
                     acc.setdefault(k, []).append(v)
         return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
                                        device=next(self.policy.parameters()).device)
 
     def _fused_pass_ok(self) -> bool:
+        """The fused pass takes regular / dual_clip PPO at the vocabularies the split kernel is
+        built for (asked of the library: the same plan the launch makes)."""
+        from . import _ffi
+
         if not self.cfg.fused_policy_pass or self.cfg.algorithm.policy_loss_type not in ("regular", "dual_clip"):
             return False
         V = self.policy.get_output_embeddings().weight.shape[0]
-        return V <= (155648 if V % 8 == 0 else 114688)  # the split kernel's range (policy_train.hip)
+        return bool(_ffi.query("skyrl_policy_train_supports", V, int(V % 8 == 0), float(self.cfg.temperature)))
 
-    def _fused_policy_pass(self, data, i, j, R, ref):
-        """The micro-batch's policy forward + loss with the lm_head logits feeding one fused pass:
+    def _fused_policy_pass(self, step, k, data, i, j, R):
+        """Micro-batch k's policy forward + loss with the lm_head logits feeding one fused pass:
         hidden states of the live response tokens (packed), z = h W^T (bf16, the reference's
-        lm_head under autocast, model_wrapper.py:308-363), then ops.policy_train_ragged computes
-        logprob, entropy, the PPO/KL/entropy loss (worker.py:801-876) and dL/dz in one read of z;
-        autograd's lm_head backward takes dL/dz into the dh / dW GEMMs. Same loss, metrics and
-        gradients as _logprobs + _loss (tests/test_gpu_trainer_e2e.py)."""
-        from . import ops
-
+        lm_head under autocast, model_wrapper.py:308-363), then the step's fused pass computes
+        logprob, entropy, the PPO/KL/entropy loss terms (worker.py:801-876) and dL/dz in one read
+        of z; autograd's lm_head backward takes dL/dz into the dh / dW GEMMs. Same loss, metrics
+        and gradients as _logprobs + _loss (tests/test_gpu_trainer_e2e.py). None when the
+        micro-batch has no response token (nothing to back-propagate; the fold counts it as 0)."""
         seq, att = data["sequences"][i:j], data["attention_mask"][i:j]
+        live = att[:, -R:].bool()
+        pos = torch.nonzero(live.reshape(-1)).reshape(-1).to(torch.int32)
+        if pos.numel() == 0:
+            return None
         model = self.policy
         with torch.autocast("cuda", dtype=torch.bfloat16):
             base = model.base_model
@@ -392,48 +412,18 @@ class GRPOTrainer:
                 hidden = base(input_ids=seq, attention_mask=att, position_ids=_positions(att)).last_hidden_state
                 h = hidden[:, -R - 1:-1].to(torch.bfloat16)
             w = model.get_output_embeddings().weight.to(torch.bfloat16)
-            live = att[:, -R:].bool()
             z = torch.matmul(h[live], w.t())  # [live tokens, V] bf16
-        pos = torch.nonzero(live.reshape(-1)).reshape(-1).to(torch.int32)
-        loss, met, _, _ = ops.policy_train_ragged(z, seq[:, -R:][live], pos, data["action_log_probs"][i:j],
-                                                  data["advantages"][i:j], data["loss_mask"][i:j], self.loss_params,
-                                                  ref_log_probs=ref, temperature=self.cfg.temperature)
-        return loss, met
-
-    def _fused_grpo_group_size(self, data) -> int:
-        """G when the loss may compute GRPO itself (ops.grpo_ppo_loss): the grpo estimator on the
-        pack kernel's scores, contiguous groups of G rows (the rollout layout), no pad rows, no
-        batch-level advantage normalisation or step-wise trajectories; else 0."""
-        alg, G = self.cfg.algorithm, self.cfg.n_samples_per_prompt
-        if (alg.advantage_estimator != "grpo" or alg.advantage_batch_normalize or G > 16
-                or data.get("reward_row_sum") is None or data.get("is_last_step") is not None
-                or data.metadata.get("pad_size", 0)):
-            return 0
-        uids = data.metadata["uids"]
-        if len(uids) % G or any(uids[k] != uids[k - k % G] or (k % G == 0 and k and uids[k] == uids[k - 1])
-                                for k in range(len(uids))):
-            return 0
-        return G
+        return step.micro(k, z, seq[:, -R:][live], pos)
 
     def _loss(self, lp, data, i, j, ref, ent):
-        """The micro-batch's policy loss (worker.py:801-876) on the fused HIP loss, with the pack
-        kernel's loss-mask row sums and the fold deferred to the backward launch (loss and metrics
-        are read after backward, as the reference does). When the micro-batch holds whole GRPO
-        groups the loss computes their advantages itself from the pack kernel's scores (one launch
-        for a4 + a6 + a7, bit-identical to data["advantages"])."""
+        """The micro-batch's policy loss (worker.py:801-876) on the fused HIP loss over the
+        advantages compute_advantages_and_returns wrote (GRPO runs once per step), with the pack
+        kernel's loss-mask row sums and the fold deferred to the backward launch (loss and
+        metrics are read after backward, as the reference does)."""
         from . import ops
 
         rows = data.get("loss_mask_row_sum")
         rows = rows[i:j] if rows is not None else None
-        G = getattr(self, "_grpo_G", 0)
-        if G and i % G == 0 and (j - i) % G == 0:
-            _, loss, met = ops.grpo_ppo_loss(
-                data["rewards"][i:j], data["response_mask"][i:j], (j - i) // G, lp, data["action_log_probs"][i:j],
-                data["loss_mask"][i:j], self.loss_params, ref_log_probs=ref, entropy=ent, loss_mask_row_sum=rows,
-                norm_by_std=self.cfg.algorithm.grpo_norm_by_std, scores=data["reward_row_sum"][i:j],
-                defer_fold=True, want_advantages=False,
-                mask_within_response=bool(data.metadata.get("loss_mask_within_response", False)))
-            return loss, met
         return ops.ppo_loss(lp, data["action_log_probs"][i:j], data["advantages"][i:j], data["loss_mask"][i:j],
                             self.loss_params, ref_log_probs=ref, entropy=ent, loss_mask_row_sum=rows,
                             defer_fold=True)

@@ -201,7 +201,7 @@ def pad_batch(training_input: TrainingInputBatch, dp_size: int) -> TrainingInput
         extra = tuple(t.shape[1:])
         if key == "is_last_step":
             p = torch.ones(pad, *extra, dtype=t.dtype, device=t.device)
-        elif key == "loss_mask":
+        elif key in ("loss_mask", "loss_mask_row_sum"):  # the row sums follow the pads' zero loss mask
             p = torch.zeros(pad, *extra, dtype=t.dtype, device=t.device)
         else:
             p = t[:pad].clone()

@@ -41,3 +41,33 @@ def test_pmc_traffic_lookup_matches_committed_profile():
         table["policy_train_split_kernel"]["hbm_bytes_per_launch"]
     assert bench.pmc_traffic("paged_decode_kernel", 0) == table["paged_decode_kernel"]["hbm_bytes_per_launch"]
     assert bench.pmc_traffic("no_such_kernel", 0) is None
+
+
+def _dry(gpus):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dry-run"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    import re  # ranks share stdout (gloo prints without newlines): pick the records out by pattern
+
+    return [json.loads(m) for m in re.findall(r'\{"dry_run"[^{}]*\}', p.stdout)]
+
+
+def test_gpus_2_spawns_two_ranks():
+    """`python bench.py --gpus 2` (no launcher env) starts two ranks under torch.distributed.run
+    with WORLD_SIZE=2 and a working 127.0.0.1 rendezvous; --dry-run stops before GPU work."""
+    recs = _dry(2)
+    assert sorted(r["rank"] for r in recs) == [0, 1]
+    assert {r["world_size"] for r in recs} == {2} and {r["local_rank"] for r in recs} == {0, 1}
+    assert {r["rank_sum"] for r in recs} == {1}  # the gloo all-reduce across both ranks ran
+    assert {r["master_addr"] for r in recs} == {"127.0.0.1"} and {r["collectives"] for r in recs} == {"nccl"}
+
+
+def test_gpus_1_stays_in_process():
+    recs = _dry(1)
+    assert recs == [{"dry_run": True, "rank": 0, "world_size": 1, "local_rank": 0, "gpus": 1, "master_addr": None,
+                     "rank_sum": 0, "collectives": "none (world size 1)"}]

@@ -96,3 +96,45 @@ def test_cast_bf16_round_to_nearest_even(dev):
     ref = x.cpu().to(torch.bfloat16)
     assert torch.equal(y.cpu().view(torch.int16)[3:], ref.view(torch.int16)[3:])
     assert torch.equal(y.cpu()[:2], ref[:2]) and torch.isnan(y[2].float())
+
+
+def test_module_optimizer_skips_parameters_without_grad(dev):
+    """ShardedModuleOptimizer (the trainer's "hip" optimizer) on a module with a parameter no
+    backward reaches: like torch.optim.AdamW with a None grad, that parameter (and its moments)
+    stay as they were, while the used ones match torch AdamW + clip_grad_norm_ (1e-6). Then the
+    parameter is used and is updated (with the shared step counter's bias correction)."""
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(64, 32)
+            self.unused = torch.nn.Parameter(torch.randn(1000))
+
+        def forward(self, x, use=False):
+            y = self.a(x).square().mean()
+            return y + self.unused.sum() if use else y
+
+    torch.manual_seed(0)
+    m = M().to(dev)
+    ref = M().to(dev)
+    ref.load_state_dict(m.state_dict())
+    cfg = comm.AdamWConfig(lr=1e-2, weight_decay=0.1, max_grad_norm=1.0)
+    opt = comm.ShardedModuleOptimizer(m, cfg)
+    topt = torch.optim.AdamW(ref.parameters(), lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay)
+    u0 = m.unused.detach().clone()
+    for it in range(3):
+        use = it == 2
+        x = torch.randn(8, 64, device=dev)
+        m(x, use).backward()
+        opt.step(1)
+        ref(x, use).backward()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), cfg.max_grad_norm)
+        topt.step()
+        topt.zero_grad(set_to_none=True)
+        if not use:
+            assert torch.equal(m.unused.detach(), u0)
+        for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+            if n == "unused" and use:  # torch counts this parameter's steps from its first grad (1), the
+                continue               # flat optimizer from the shared counter (3): another bias correction
+            torch.testing.assert_close(p.detach(), q.detach(), atol=1e-6, rtol=1e-5, msg=n)
+    assert not torch.equal(m.unused.detach(), u0)

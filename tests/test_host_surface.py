@@ -103,6 +103,18 @@ def test_pad_batch_noop_and_is_last_step():
     assert p.batch_size == 4 and bool(p["is_last_step"][3]) and float(p["loss_mask"][3].sum()) == 0.0
 
 
+def test_pad_batch_keeps_loss_mask_row_sums_consistent():
+    """The pack kernel's loss_mask_row_sum (the fused loss's reduction scales) must follow the
+    pads' zeroed loss mask: every row's sum equals its loss mask's sum after padding."""
+    lm = torch.tensor([[1.0, 1.0, 0.0], [1.0, 0.0, 0.0], [1.0, 1.0, 1.0]])
+    b = TrainingInputBatch({"loss_mask": lm, "loss_mask_row_sum": lm.sum(-1), "reward_row_sum": torch.ones(3)})
+    b.metadata = {"uids": ["a", "b", "c"]}
+    p = tu.pad_batch(b, 5)
+    assert p.batch_size == 5
+    assert torch.equal(p["loss_mask_row_sum"], p["loss_mask"].sum(-1))
+    assert torch.equal(p["reward_row_sum"], torch.ones(5))  # rewards are cloned with their rows
+
+
 def test_flatten_ragged():
     v, o = tu.flatten_ragged([[1, 2], [], [3]], np.int64)
     assert v.tolist() == [1, 2, 3] and o.tolist() == [0, 2, 2, 3]
