@@ -31,6 +31,7 @@
 namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
+int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
 namespace {
 
 constexpr int kThreads = 256;
@@ -434,13 +435,24 @@ __device__ uint64_t g_sphase[4096 * 8];
 // behind is issued first and both finish together (otherwise age priority lets the first-
 // dispatched one finish ~9 us ahead at T = 1 and the other streams its tail alone).
 // One work unit: split `split` of `nsplit` of row row_i (the whole row when nsplit == 1).
-template <typename T, int MODE, int NT, bool PRIO>
+// TieSink (the top_p kernel's pass 2, TIES = true): elements whose key is `kc` are taken out of
+// the decision and appended to an LDS list with their exact scores (the caller ranks them by
+// index: the cut keeps the first c); a kc no key equals (> 0xffff) disables it at run time.
+struct TieSink {
+    int32_t* idx;
+    float* sc;
+    uint32_t* n;
+    int cap;
+    uint32_t kc;
+};
+
+template <typename T, int MODE, int NT, bool PRIO, bool TIES = false>
 __device__ __forceinline__ void sample_unit(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
     int use_minp_rt, float ln_min_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step,
     int use_topp_rt, const RowFilter* __restrict__ filt, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, Part* __restrict__ parts, unsigned* __restrict__ counters, const int row_i,
-    const int split, const int nsplit, const int frow) {
+    const int split, const int nsplit, const int frow, const TieSink* ties = nullptr, Part* result = nullptr) {
     constexpr int NW = NT / kWave;
     SPHASE(0);
     __shared__ Part s_part[NW];
@@ -645,6 +657,28 @@ __device__ __forceinline__ void sample_unit(
             xm = fmaxf(xm, ok[k] ? x[k] : -INFINITY);
         }
         const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+        if constexpr (TIES) {  // the cut key's elements: exact scores into the caller's list
+            bool tie[VEC];
+            bool anyt = false;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                tie[k] = (FULL || k < cnt) && okey<T>(raw[k]) == ties->kc;
+                anyt = anyt || tie[k];
+            }
+            if (__builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {
+                const float Eg = group_e(h);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    if (tie[k]) {
+                        const uint32_t pos = atomicAdd(ties->n, 1u);
+                        if (pos < (uint32_t)ties->cap) {
+                            ties->idx[pos] = v0 + k;
+                            ties->sc[pos] = exact(x[k], v0 + k, h, Eg);
+                        }
+                    }
+                }
+            }
+        }
         if constexpr (!FULL) {
             if (!seeded) seed_vec(x, ok, v0, h);
         }
@@ -898,6 +932,10 @@ __device__ __forceinline__ void sample_unit(
                 p.m = mn;
             }
         }
+    }
+    if (result) {  // the caller decides (the top_p kernel: ties at the cut still to rank)
+        if (threadIdx.x == 0) *result = p;
+        return;
     }
     if (threadIdx.x == 0) {
         SPHASE(4);
@@ -1403,6 +1441,285 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
 }
 
+// ---- top_p / min_p without top_k: the row streamed twice by one workgroup ---------------------
+// (With top_k set, sample_topk_kernel above.) A top_p cut needs the row max before any mass is
+// known, and the kept set can run to thousands of tokens (13k at p = 0.95 on N(0, 3^2) rows), so:
+//  * pass 1 (HBM; cached loads, so that pass 2 finds the row in the Infinity Cache): the row max
+//    and, for top_p, an LDS histogram of COUNTS per exact bf16 key over |x| in [2^-16, 2^16)
+//    (8192 bins: every key of that range has its own), +0 and -0 two more; keys below the window
+//    (0 < |x| < 2^-16) go to a short list; NaN, +inf, x >= 2^16 or a full list send the row to
+//    the fallback.
+//  * on chip: with the max known, a bin's mass is its count x mass_q(value, max) -- the pre-pass's
+//    fixed-point masses, exactly, without a det_exp2 per element; Z is their exact sum (+ the
+//    list's); a block scan over the positive bins in descending key order finds the cut key kc,
+//    and filter_row's tie rule the number c of its elements (index order) that are kept.
+//  * pass 2 (re-read): sample_unit's MODE 2 (group bound, exact noise_score, lse) over the keys
+//    above kc (min_p alone: x/T >= max/T + ln min_p); when the cut splits kc's tie group, kc's
+//    elements go to an LDS list with their exact scores instead, ranked by index afterwards: the
+//    first c are admissible.
+// The pre-pass's cuts and MODE 2's scores on the same elements: the tokens (and the logprobs)
+// of the two-kernel path, and of oracle/sampler_ref.c, bit for bit. Rows outside these bounds
+// (the cut below the positive window, more than kPTieCap ties at the cut) run the two-kernel
+// path's code in this workgroup, as the top_k kernel's fallback does.
+constexpr int kPNT = 512;
+constexpr int kPE0 = 111;       // window: bf16 exponent fields 111..142, |x| in [2^-16, 2^16)
+constexpr int kPHalf = 4096;    // keys per sign in the window
+constexpr int kPSlowCap = 512;  // elements below the window
+constexpr int kPTieCap = 1024;  // elements at a split cut key
+
+template <typename T>
+__global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topp_kernel(
+    const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, int use_topp,
+    float top_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
+    float* __restrict__ logp_out, RowFilter* __restrict__ filt) {
+    static_assert(sizeof(T) == 2, "bf16 rows");
+    constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
+    __shared__ uint32_t s_hist[2 * kPHalf];
+    __shared__ uint16_t s_slow[kPSlowCap];
+    __shared__ uint32_t s_nslow, s_bad, s_nt, s_zero[2];
+    __shared__ float s_vmax[NW];
+    __shared__ unsigned long long s_wpos[NW], s_woth[NW];
+    __shared__ unsigned long long s_cut_a;
+    __shared__ int s_cut_j;
+    __shared__ int32_t s_tidx[kPTieCap];
+    __shared__ float s_tsc[kPTieCap];
+    __shared__ float s_bs[NW];
+    __shared__ int32_t s_bi[NW];
+    __shared__ Part s_p;
+    __shared__ int s_icut;
+    __shared__ RowFilter s_rf;
+    const int row_i = blockIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const T* row = logits + (int64_t)row_i * ld;
+    const uint4* rv = reinterpret_cast<const uint4*>(row);  // 16-B aligned (host check)
+    const int nvec = V / VEC;
+    constexpr int kStep = 4 * NT;
+    const int nfull = (nvec / kStep) * kStep;
+    uint4 cur[4], nxt[4];
+    if (nfull > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = rv[u * NT + threadIdx.x];
+    }
+    if (threadIdx.x == 0) {
+        s_nslow = 0u;
+        s_bad = 0u;
+        s_nt = 0u;
+        s_cut_j = -1;
+        s_zero[0] = s_zero[1] = 0u;
+    }
+    if (use_topp)
+        for (int j = threadIdx.x; j < 2 * kPHalf; j += NT) s_hist[j] = 0u;
+    __syncthreads();
+
+    // ---- pass 1: the row max; for top_p the count histogram
+    float vmx = -INFINITY;
+    bool bad = false;
+    auto elem = [&](uint32_t b) {
+        if (use_topp) {
+            const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
+            if ((unsigned)wi < (unsigned)kPHalf) {
+                atomicAdd(&s_hist[(b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi], 1u);
+            } else if (wi < 0) {
+                if ((b & 0x7fffu) == 0u) {  // +-0: their own counters (exact zeros may be many)
+                    atomicAdd(&s_zero[b >> 15], 1u);
+                } else {
+                    const uint32_t pos = atomicAdd(&s_nslow, 1u);
+                    if (pos < (uint32_t)kPSlowCap) s_slow[pos] = (uint16_t)b;
+                }
+            } else {  // |x| >= 2^16: -inf and large negatives weigh nothing; NaN, +inf, x >= 2^16
+                bad = bad || !(b == 0xff80u || ((b & 0x8000u) && (b & 0x7fffu) < 0x7f80u));
+            }
+        } else {  // min_p alone: the max must be a number (NaN / +inf rows: the fallback)
+            bad = bad || ((b & 0x7f80u) == 0x7f80u && b != 0xff80u);
+        }
+    };
+    auto visit1 = [&](const uint4& pk) {
+        uint16_t raw[VEC];
+        __builtin_memcpy(raw, &pk, 16);
+        float vm = bf16_to_f32(raw[0]);
+#pragma unroll
+        for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, bf16_to_f32(raw[k]));
+        vmx = fmaxf(vmx, vm);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) elem(raw[k]);
+    };
+    if (nfull > 0) {
+        for (int base = 0; base < nfull; base += kStep) {
+            const bool more = base + kStep < nfull;
+            switch (((nfull - base) * 4 - 1) / nfull) {  // progress priority, as the row-mode sampler
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nxt[u] = rv[base + kStep + u * NT + threadIdx.x];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) visit1(cur[u]);
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+            }
+        }
+    }
+    for (int i = nfull + threadIdx.x; i < nvec; i += NT) visit1(rv[i]);
+    for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
+        const uint16_t b = row[i];
+        vmx = fmaxf(vmx, bf16_to_f32(b));
+        elem(b);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    vmx = wave_max(vmx);
+    if (bad) s_bad = 1u;
+    if (lane == 0) s_vmax[w] = vmx;
+    __syncthreads();
+    float mx = s_vmax[0];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) mx = fmaxf(mx, s_vmax[j]);
+    const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
+    const float mthr = mx * inv_t + ln_min_p;
+
+    auto fallback = [&]() {
+        topk_fallback<T>(logits, ld, V, 0, inv_t, use_minp, ln_min_p, use_topp, top_p, seed, seq_ids, step, tokens,
+                         logp_out, &s_rf, row_i);
+        if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
+    };
+    if (s_bad || (use_topp && (s_nslow > (uint32_t)kPSlowCap || !(mx >= 1.52587890625e-05f)))) {
+        fallback();
+        return;
+    }
+
+    // ---- on chip (top_p): bin masses, Z, the cut key and its tie count
+    uint32_t kc = 0u, tie_key = 0x10000u;  // no tie list unless the cut splits kc's group
+    long long c = 0, cnt = 0;
+    int ic = 0x7fffffff;
+    if (use_topp) {
+        // thread t: descending positions j = 8t .. 8t+7 of the positive bins (bin kPHalf + 4095 - j)
+        // and the negative bins 8t .. 8t+7; the list entries t, t + NT, ...
+        auto mass_of = [&](uint32_t bits, uint32_t n) -> unsigned long long {
+            const float x = bf16_to_f32((uint16_t)bits);
+            if (n == 0u || (use_minp && !(x * inv_t >= mthr))) return 0ull;
+            return (unsigned long long)n * (unsigned long long)mass_q(x, mx, inv_t);
+        };
+        unsigned long long pos = 0ull, oth = 0ull;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int wi = kPHalf - 1 - (8 * (int)threadIdx.x + q);
+            pos += mass_of((uint32_t)((kPE0 << 7) + wi), s_hist[kPHalf + wi]);
+            const int wn = 8 * (int)threadIdx.x + q;
+            oth += mass_of(0x8000u | (uint32_t)((kPE0 << 7) + wn), s_hist[kPHalf - 1 - wn]);
+        }
+        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) oth += mass_of(s_slow[i], 1u);
+        if (threadIdx.x < 2) oth += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
+        unsigned long long incl = pos;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const unsigned long long o = (unsigned long long)__shfl_up((long long)incl, off, kWave);
+            if (lane >= off) incl += o;
+        }
+        unsigned long long ow = oth;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) ow += (unsigned long long)__shfl_xor((long long)ow, off, kWave);
+        if (lane == kWave - 1) s_wpos[w] = incl;
+        if (lane == 0) s_woth[w] = ow;
+        __syncthreads();
+        unsigned long long off_w = 0ull, Z = 0ull;
+        for (int j = 0; j < NW; ++j) {
+            if (j < w) off_w += s_wpos[j];
+            Z += s_wpos[j] + s_woth[j];
+        }
+        const double target = (double)top_p * (double)Z;
+        unsigned long long cum = off_w + incl - pos;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int wi = kPHalf - 1 - (8 * (int)threadIdx.x + q);
+            const unsigned long long mq = mass_of((uint32_t)((kPE0 << 7) + wi), s_hist[kPHalf + wi]);
+            // (the first weighted bin also when target <= 0: top_p = 0 keeps the top token, as
+            // filter_row's radix select, whose first bin is the max's)
+            if (mq && (cum == 0ull || (double)cum < target) && (double)(cum + mq) >= target) {
+                s_cut_j = 8 * (int)threadIdx.x + q;
+                s_cut_a = cum;
+            }
+            cum += mq;
+        }
+        __syncthreads();
+        if (s_cut_j < 0) {  // the cut lies below the positive window
+            fallback();
+            return;
+        }
+        const int wi = kPHalf - 1 - s_cut_j;
+        kc = 0x8000u | (uint32_t)((kPE0 << 7) + wi);
+        cnt = (long long)s_hist[kPHalf + wi];
+        const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
+        const unsigned long long A = s_cut_a;
+        // filter_row's rule: c = number of tie ranks j >= 0 with A + j qc < target (the first always
+        // for the top key)
+        const double jd = (target - (double)A) / (double)qc;
+        c = jd > 0.0 ? (long long)jd : 0;
+        while (c > 0 && (double)(A + (unsigned long long)(c - 1) * qc) >= target) --c;
+        while ((double)(A + (unsigned long long)c * qc) < target) ++c;
+        if (kc == kmax && c < 1) c = 1;
+        if (c < cnt) {
+            if (cnt > kPTieCap) {
+                fallback();
+                return;
+            }
+            tie_key = kc;
+            ic = -1;  // pass 2 decides the keys above kc; kc's elements go to the tie list
+        }
+    }
+
+    // ---- pass 2: MODE 2 over the admissible elements (+ the tie list)
+    if (threadIdx.x == 0) s_rf = RowFilter{mx, 0u, 0x7fffffff, kc, ic};
+    __syncthreads();
+    const TieSink sink{s_tidx, s_tsc, &s_nt, kPTieCap, tie_key};
+    sample_unit<T, 2, NT, true, true>(logits, ld, V, V, inv_t, 0, use_minp && !use_topp, ln_min_p, seed, seq_ids,
+                                      step, use_topp, &s_rf, tokens, logp_out, nullptr, nullptr, row_i, 0, 1, 0, &sink,
+                                      &s_p);
+    __syncthreads();
+    Part p = s_p;
+    int icut = ic;
+    if (tie_key <= 0xffffu) {  // rank kc's elements by index: the first c are admissible
+        const int n = (int)min(s_nt, (uint32_t)kPTieCap);
+        Best best{-INFINITY, 0x7fffffff};
+        for (int i = threadIdx.x; i < n; i += NT) {
+            const int ii = s_tidx[i];
+            int r = 0;
+            for (int j = 0; j < n; ++j) r += s_tidx[j] < ii ? 1 : 0;
+            if (r < c && better(s_tsc[i], ii, best)) best = Best{s_tsc[i], ii};
+            if (r == c - 1) s_icut = ii;  // the cut's last kept index (filter_row's ic)
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float os = __shfl_xor(best.score, off, kWave);
+            const int oi = __shfl_xor(best.idx, off, kWave);
+            if (better(os, oi, best)) best = Best{os, oi};
+        }
+        __syncthreads();
+        if (lane == 0) {
+            s_bs[w] = best.score;
+            s_bi[w] = best.idx;
+        }
+        __syncthreads();
+        Best b{p.score, p.idx};
+        for (int j = 0; j < NW; ++j)
+            if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
+        p.score = b.score;
+        p.idx = b.idx;
+        icut = s_icut;
+    }
+    if (threadIdx.x == 0) {
+        tokens[row_i] = p.idx;
+        if (logp_out) {
+            const float lse = p.m + fast_log2(p.s) * kLn2;
+            logp_out[row_i] = (p.idx >= 0 && p.idx < V) ? to_f<T>(row[p.idx]) - lse : __builtin_nanf("");
+        }
+        filt[row_i] = RowFilter{mx, 0u, kRowDone, kc, icut};
+    }
+}
+
 int splits_for(int nseq, int V) {
     if (nseq <= 0 || V <= 0 || nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
     int s = (2048 + nseq - 1) / nseq;
@@ -1459,6 +1776,15 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         hipLaunchKernelGGL(sample_topk_kernel<T>, dim3(nseq), dim3(kFastNT), 0, stream, lg, ld, V, top_k, inv_t, use_minp,
                            ln_min_p, use_topp, use_topp ? top_p : 1.0f, seed, seq_ids, step, tokens, logp, filt);
         return check_launch("sample_topk_kernel");
+    }
+    // top_p / min_p without top_k on 16-B aligned bf16 rows: the two-pass kernel alone
+    if constexpr (sizeof(T) == 2) {
+        if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
+            ((ld * (int64_t)sizeof(T)) & 15) == 0) {
+            hipLaunchKernelGGL(sample_topp_kernel<T>, dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t, use_minp,
+                               ln_min_p, use_topp, use_topp ? top_p : 1.0f, seed, seq_ids, step, tokens, logp, filt);
+            return check_launch("sample_topp_kernel");
+        }
     }
     if (use_topk || use_minp || use_topp) {
         hipLaunchKernelGGL(sample_filter_kernel<T>, dim3(nseq), dim3(kFT), 0, stream, lg, ld, V, use_topk ? top_k : 0,
