@@ -710,10 +710,13 @@ def lmhead_sample_leg(dev, nseq, reps=30):
 
 def sampler_filtered_leg(dev, nseq, V, reps=20):
     """The §8(d) filter variant of the rollout sampler (top_k = 50 with top_p = 0.9, and top_k =
-    50 alone) at the decode step's shape [nseq, V] bf16, T = 1: the whole skyrl_sample call (the
-    one-pass top_k kernel; rows it hands back run the filter pre-pass + MODE 2 kernels, which
-    also launch and skip the rows it took), against the two-kernel path
-    (skyrl_tune sampler_topk_fast 0). Algorithmic bytes = one read of the logits + 16 B per row."""
+    50 alone) and the SkyRL-SQL recipe's top_p = 0.95 alone (examples/text_to_sql/run_skyrl_sql.sh:60)
+    at the decode step's shape [nseq, V] bf16, T = 1: the whole skyrl_sample call (with top_k the
+    one-pass kernel, without it the two-pass top_p kernel; rows either hands back run the
+    pre-pass + MODE 2 code in the same workgroup), against the two-kernel path (skyrl_tune
+    sampler_topk_fast / sampler_topp_fast 0). Algorithmic bytes = one read of the logits + 16 B
+    per row (the top_p kernel reads each row twice; the second read is meant to hit the Infinity
+    Cache)."""
     from skyrl_amd import ops
 
     g = torch.Generator(device=dev).manual_seed(5)
@@ -723,10 +726,11 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
     lp = torch.empty(nseq, dtype=torch.float32, device=dev)
     nbytes = nseq * V * 2 + nseq * 16
     out = {"shape": [nseq, V], "dtype": "bf16", "temperature": 1.0, "bytes_per_launch": nbytes}
-    for name, k, p in (("top_k50_top_p0.9", 50, 0.9), ("top_k50", 50, 1.0)):
+    for name, k, p in (("top_k50_top_p0.9", 50, 0.9), ("top_k50", 50, 1.0), ("top_p0.95", -1, 0.95)):
         res = {}
+        knob = b"sampler_topk_fast" if k > 0 else b"sampler_topp_fast"  # the one-pass / two-pass kernels
         for fast in (1, 0):
-            ops._ffi.call("skyrl_tune", b"sampler_topk_fast", fast)
+            ops._ffi.call("skyrl_tune", knob, fast)
             run = lambda: ops.sample(x, temperature=1.0, top_k=k, top_p=p, seed=3, seq_ids=ids, step=1,  # noqa: E731
                                      tokens_out=tok, logp_out=lp)
             run()
@@ -741,7 +745,7 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
             gbs = nbytes / (us * 1e-6) / 1e9
             res["one_pass" if fast else "two_kernel"] = {"avg_launch_us": round(us, 2), "achieved_GBps": round(gbs, 1),
                                                          "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        ops._ffi.call("skyrl_tune", b"sampler_topk_fast", 1)
+        ops._ffi.call("skyrl_tune", knob, 1)
         out[name] = res
     return out
 
@@ -883,7 +887,7 @@ def spawn_ranks(args, argv) -> int:
     The reference starts one NCCL rank per GPU the same way (workers/worker.py:102-126)."""
     import subprocess
 
-    if not args.dry_run:
+    if not args.dry_run and args.backend == "nccl":  # (gloo rehearsals share one GPU)
         n_dev = torch.cuda.device_count()  # does not initialise the GPU on this image
         if n_dev < args.gpus:
             log(f"--gpus {args.gpus} but only {n_dev} visible GPUs")

@@ -1,0 +1,57 @@
+"""Where the two-pass top_p kernel's time goes at the bench shape [512, 151,936] bf16, T = 1:
+skyrl_tune("topp_probe") 1 = pass 1 alone, 2 = pass 1 + the cut (tokens invalid in both), 0 =
+the whole kernel; beside it the unfiltered T = 1 and greedy samplers (one read of the row) and
+the two-kernel path. One JSON line."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from skyrl_amd import ops  # noqa: E402
+
+
+def timed(fn, reps=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return round(a.elapsed_time(b) * 1e3 / reps, 2)
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(5)
+    n, V = 512, 151936
+    x = (torch.randn(n, V, device=dev, generator=g) * 3).to(torch.bfloat16)
+    ids = torch.arange(n, dtype=torch.int64, device=dev)
+    tok = torch.empty(n, dtype=torch.int32, device=dev)
+    lp = torch.empty(n, dtype=torch.float32, device=dev)
+    out = {}
+    for name, kw in (("top_p0.95", dict(top_p=0.95)), ("top_p0.9", dict(top_p=0.9)), ("min_p0.05", dict(min_p=0.05))):
+        res = {}
+        for probe in (1, 2, 0):
+            ops._ffi.call("skyrl_tune", b"topp_probe", probe)
+            res[f"probe{probe}_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
+                                                               tokens_out=tok, logp_out=lp, **kw))
+        ops._ffi.call("skyrl_tune", b"topp_probe", 0)
+        ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 0)
+        res["two_kernel_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
+                                                        tokens_out=tok, logp_out=lp, **kw), reps=10)
+        ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 1)
+        out[name] = res
+    out["t1_unfiltered_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1, tokens_out=tok,
+                                                       logp_out=lp))
+    out["greedy_us"] = timed(lambda: ops.sample(x, temperature=0.0, seed=3, seq_ids=ids, step=1, tokens_out=tok,
+                                                logp_out=lp))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

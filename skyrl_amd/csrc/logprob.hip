@@ -223,6 +223,7 @@ extern int g_finish_mode;
 extern int g_sampler_row;
 extern int g_sampler_topk_fast;
 extern int g_sampler_topp_fast;
+extern int g_probe_topp;
 extern int g_attn_pf;
 int lmhead_tune(int value);
 int lmhead_group_tune(int value);
@@ -292,6 +293,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "sampler_topk_fast") {
         SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_topk_fast must be 0 or 1");
         g_sampler_topk_fast = value;
+        return SKYRL_OK;
+    }
+    if (k == "topp_probe") {
+        SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: topp_probe must be 0, 1 or 2");
+        g_probe_topp = value;
         return SKYRL_OK;
     }
     if (k == "sampler_topp_fast") {

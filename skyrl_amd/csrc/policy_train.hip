@@ -156,7 +156,8 @@ __device__ __forceinline__ void scales_body(const float* __restrict__ mask, int 
     double tot = 0.0;
     for (int b = w; b < n; b += kWaves) {
         float acc = 0.f;
-        for (int t = lane; t < R; t += kWave) acc += mask ? mask[(int64_t)b * R + t] : 1.f;
+#pragma unroll 8
+        for (int t = lane; t < R; t += kWave) acc += mask ? mask[(int64_t)b * R + t] : 1.f;  // loads in flight, same order
         acc = wave_sum(acc);
         tot += acc;
         if (lane == 0) {
@@ -760,7 +761,8 @@ __device__ __forceinline__ void epilogue_body(const float* __restrict__ tok, con
     double tl = 0.0, rows_pg = 0.0, rows_kl = 0.0, tc = 0.0, te = 0.0;
     for (int b = w; b < n; b += kWaves) {
         float a0 = 0.f, a1 = 0.f, am = 0.f;
-        for (int t = lane; t < R; t += kWave) {
+#pragma unroll 4
+        for (int t = lane; t < R; t += kWave) {  // (unrolled: loads in flight; the sums keep their order)
             float4 v = *reinterpret_cast<const float4*>(tok + ((int64_t)b * R + t) * 4);
             const float m = mask ? mask[(int64_t)b * R + t] : 1.f;
             if (MASKED && m == 0.f) v = make_float4(0.f, 0.f, 0.f, 0.f);

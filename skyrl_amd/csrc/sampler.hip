@@ -32,6 +32,7 @@ namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
 int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
+int g_probe_topp = 0;  // skyrl_tune("topp_probe"): timing only, tokens invalid: 1 pass 1 alone, 2 pass 1 + the cut
 namespace {
 
 constexpr int kThreads = 256;
@@ -1451,16 +1452,17 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
 //    the fallback.
 //  * on chip: with the max known, a bin's mass is its count x mass_q(value, max) -- the pre-pass's
 //    fixed-point masses, exactly, without a det_exp2 per element; Z is their exact sum (+ the
-//    list's); a block scan over the positive bins in descending key order finds the cut key kc,
-//    and filter_row's tie rule the number c of its elements (index order) that are kept.
+//    list's); block scans over the bins in descending key order (positive window, then the
+//    negative one) find the cut key kc, and filter_row's tie rule the number c of its elements
+//    (index order) that are kept.
 //  * pass 2 (re-read): sample_unit's MODE 2 (group bound, exact noise_score, lse) over the keys
 //    above kc (min_p alone: x/T >= max/T + ln min_p); when the cut splits kc's tie group, kc's
 //    elements go to an LDS list with their exact scores instead, ranked by index afterwards: the
 //    first c are admissible.
 // The pre-pass's cuts and MODE 2's scores on the same elements: the tokens (and the logprobs)
 // of the two-kernel path, and of oracle/sampler_ref.c, bit for bit. Rows outside these bounds
-// (the cut below the positive window, more than kPTieCap ties at the cut) run the two-kernel
-// path's code in this workgroup, as the top_k kernel's fallback does.
+// (the cut among the values below 2^-16 or the zeros, more than kPTieCap ties at the cut) run
+// the two-kernel path's code in this workgroup, as the top_k kernel's fallback does.
 constexpr int kPNT = 512;
 constexpr int kPE0 = 111;       // window: bf16 exponent fields 111..142, |x| in [2^-16, 2^16)
 constexpr int kPHalf = 4096;    // keys per sign in the window
@@ -1471,18 +1473,18 @@ template <typename T>
 __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topp_kernel(
     const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, int use_topp,
     float top_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
-    float* __restrict__ logp_out, RowFilter* __restrict__ filt) {
+    float* __restrict__ logp_out, RowFilter* __restrict__ filt, int probe) {
     static_assert(sizeof(T) == 2, "bf16 rows");
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
     __shared__ uint32_t s_hist[2 * kPHalf];
     __shared__ uint16_t s_slow[kPSlowCap];
     __shared__ uint32_t s_nslow, s_bad, s_nt, s_zero[2];
-    __shared__ float s_vmax[NW];
-    __shared__ unsigned long long s_wpos[NW], s_woth[NW];
+    __shared__ float s_vmax[NW], s_lm[NW], s_ls[NW], s_bar;
+    __shared__ double s_wexp[NW];
+    __shared__ unsigned long long s_wpos[NW], s_wneg[NW], s_woth[NW];
     __shared__ unsigned long long s_cut_a;
     __shared__ int s_cut_j;
     __shared__ int32_t s_tidx[kPTieCap];
-    __shared__ float s_tsc[kPTieCap];
     __shared__ float s_bs[NW];
     __shared__ int32_t s_bi[NW];
     __shared__ Part s_p;
@@ -1514,6 +1516,9 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     // ---- pass 1: the row max; for top_p the count histogram
     float vmx = -INFINITY;
     bool bad = false;
+    // min_p alone: the raw online (max, sum-exp) for the logprob here (lagged offset, as the top_k
+    // kernel); top_p takes it from the histogram instead
+    float lm = -1e30f, ls = 0.f;
     auto elem = [&](uint32_t b) {
         if (use_topp) {
             const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
@@ -1540,6 +1545,16 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
 #pragma unroll
         for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, bf16_to_f32(raw[k]));
         vmx = fmaxf(vmx, vm);
+        if (!use_topp) {
+            if (vm > lm + 64.f) {
+                ls *= fast_exp2((lm - vm) * kLog2e);
+                lm = vm;
+            }
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) acc += fast_exp2((bf16_to_f32(raw[k]) - lm) * kLog2e);
+            ls += acc;
+        }
 #pragma unroll
         for (int k = 0; k < VEC; ++k) elem(raw[k]);
     };
@@ -1567,17 +1582,49 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     for (int i = nfull + threadIdx.x; i < nvec; i += NT) visit1(rv[i]);
     for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
         const uint16_t b = row[i];
-        vmx = fmaxf(vmx, bf16_to_f32(b));
+        const float x = bf16_to_f32(b);
+        vmx = fmaxf(vmx, x);
+        if (!use_topp) {
+            const float mn = fmaxf(lm, x);
+            ls = ls * fast_exp2((lm - mn) * kLog2e) + fast_exp2((x - mn) * kLog2e);
+            lm = mn;
+        }
         elem(b);
     }
     __builtin_amdgcn_s_setprio(0);
     vmx = wave_max(vmx);
+    if (!use_topp) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float om = __shfl_xor(lm, off, kWave);
+            const float os = __shfl_xor(ls, off, kWave);
+            const float mn = fmaxf(lm, om);
+            ls = ls * fast_exp2((lm - mn) * kLog2e) + os * fast_exp2((om - mn) * kLog2e);
+            lm = mn;
+        }
+        if (lane == 0) {
+            s_lm[w] = lm;
+            s_ls[w] = ls;
+        }
+    }
     if (bad) s_bad = 1u;
     if (lane == 0) s_vmax[w] = vmx;
     __syncthreads();
     float mx = s_vmax[0];
 #pragma unroll
     for (int j = 1; j < NW; ++j) mx = fmaxf(mx, s_vmax[j]);
+    float lse = 0.f;
+    if (!use_topp) {
+        float M = s_lm[0], S = s_ls[0];
+#pragma unroll
+        for (int j = 1; j < NW; ++j) {
+            const float mn = fmaxf(M, s_lm[j]);
+            S = S * fast_exp2((M - mn) * kLog2e) + s_ls[j] * fast_exp2((s_lm[j] - mn) * kLog2e);
+            M = mn;
+        }
+        lse = M + fast_log2(S) * kLn2;
+    }
+    if (probe == 1) return;  // timing probe (skyrl_tune topp_probe): pass 1 only
     const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
     const float mthr = mx * inv_t + ln_min_p;
 
@@ -1586,7 +1633,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                          logp_out, &s_rf, row_i);
         if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
     };
-    if (s_bad || (use_topp && (s_nslow > (uint32_t)kPSlowCap || !(mx >= 1.52587890625e-05f)))) {
+    if (s_bad || (use_topp && s_nslow > (uint32_t)kPSlowCap)) {
         fallback();
         return;
     }
@@ -1603,55 +1650,105 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             if (n == 0u || (use_minp && !(x * inv_t >= mthr))) return 0ull;
             return (unsigned long long)n * (unsigned long long)mass_q(x, mx, inv_t);
         };
-        unsigned long long pos = 0ull, oth = 0ull;
+        // descending key order: the positive bins (descending value), the list and +-0 (the
+        // middle), the negative bins (ascending |x|); a block scan of each side
+        unsigned long long pos = 0ull, neg = 0ull, mid = 0ull;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int wi = kPHalf - 1 - (8 * (int)threadIdx.x + q);
             pos += mass_of((uint32_t)((kPE0 << 7) + wi), s_hist[kPHalf + wi]);
             const int wn = 8 * (int)threadIdx.x + q;
-            oth += mass_of(0x8000u | (uint32_t)((kPE0 << 7) + wn), s_hist[kPHalf - 1 - wn]);
+            neg += mass_of(0x8000u | (uint32_t)((kPE0 << 7) + wn), s_hist[kPHalf - 1 - wn]);
         }
-        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) oth += mass_of(s_slow[i], 1u);
-        if (threadIdx.x < 2) oth += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
-        unsigned long long incl = pos;
-#pragma unroll
-        for (int off = 1; off < kWave; off <<= 1) {
-            const unsigned long long o = (unsigned long long)__shfl_up((long long)incl, off, kWave);
-            if (lane >= off) incl += o;
-        }
-        unsigned long long ow = oth;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) ow += (unsigned long long)__shfl_xor((long long)ow, off, kWave);
-        if (lane == kWave - 1) s_wpos[w] = incl;
-        if (lane == 0) s_woth[w] = ow;
-        __syncthreads();
-        unsigned long long off_w = 0ull, Z = 0ull;
-        for (int j = 0; j < NW; ++j) {
-            if (j < w) off_w += s_wpos[j];
-            Z += s_wpos[j] + s_woth[j];
-        }
-        const double target = (double)top_p * (double)Z;
-        unsigned long long cum = off_w + incl - pos;
+        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) mid += mass_of(s_slow[i], 1u);
+        if (threadIdx.x < 2) mid += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
+        // the raw logits' sum-exp for the logprob, from the same counts (another summation order
+        // than the streaming lse: equal to float rounding)
+        double se = 0.0;
+        auto sexp = [&](uint32_t bits, uint32_t n) {
+            if (n) se += (double)n * (double)fast_exp2((bf16_to_f32((uint16_t)bits) - mx) * kLog2e);
+        };
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const int wi = kPHalf - 1 - (8 * (int)threadIdx.x + q);
-            const unsigned long long mq = mass_of((uint32_t)((kPE0 << 7) + wi), s_hist[kPHalf + wi]);
-            // (the first weighted bin also when target <= 0: top_p = 0 keeps the top token, as
-            // filter_row's radix select, whose first bin is the max's)
-            if (mq && (cum == 0ull || (double)cum < target) && (double)(cum + mq) >= target) {
-                s_cut_j = 8 * (int)threadIdx.x + q;
-                s_cut_a = cum;
-            }
-            cum += mq;
+            const int p8 = 8 * (int)threadIdx.x + q;
+            sexp((uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf + p8]);
+            sexp(0x8000u | (uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf - 1 - p8]);
         }
+        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) sexp(s_slow[i], 1u);
+        if (threadIdx.x < 2) sexp(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
+        se = wave_sum(se);
+        if (lane == 0) s_wexp[w] = se;
+        unsigned long long ip = pos, in = neg;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const unsigned long long op = (unsigned long long)__shfl_up((long long)ip, off, kWave);
+            const unsigned long long on = (unsigned long long)__shfl_up((long long)in, off, kWave);
+            if (lane >= off) {
+                ip += op;
+                in += on;
+            }
+        }
+        unsigned long long wm = mid;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) wm += (unsigned long long)__shfl_xor((long long)wm, off, kWave);
+        if (lane == kWave - 1) {
+            s_wpos[w] = ip;
+            s_wneg[w] = in;
+        }
+        if (lane == 0) s_woth[w] = wm;
         __syncthreads();
-        if (s_cut_j < 0) {  // the cut lies below the positive window
+        unsigned long long offp = 0ull, offn = 0ull, Zp = 0ull, Zn = 0ull, Zm = 0ull;
+        for (int j = 0; j < NW; ++j) {
+            if (j < w) {
+                offp += s_wpos[j];
+                offn += s_wneg[j];
+            }
+            Zp += s_wpos[j];
+            Zn += s_wneg[j];
+            Zm += s_woth[j];
+        }
+        const unsigned long long Z = Zp + Zm + Zn;
+        double S = 0.0;
+        for (int j = 0; j < NW; ++j) S += s_wexp[j];
+        lse = mx + fast_log2((float)S) * kLn2;
+        const double target = (double)top_p * (double)Z;
+        // the cut: the bin where the mass before it is < p Z and the mass through it reaches it
+        // (the first weighted bin also when target <= 0: top_p = 0 keeps the top token, as
+        // filter_row's radix select, whose first bin is the max's); cut_j < 4096: positive bin
+        // (descending position), >= 4096: negative bin 4096 + wn
+        auto scan8 = [&](unsigned long long cum, bool negative) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int p8 = 8 * (int)threadIdx.x + q;
+                const unsigned long long mq =
+                    negative ? mass_of(0x8000u | (uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf - 1 - p8])
+                             : mass_of((uint32_t)((kPE0 << 7) + kPHalf - 1 - p8), s_hist[2 * kPHalf - 1 - p8]);
+                if (mq && (cum == 0ull || (double)cum < target) && (double)(cum + mq) >= target) {
+                    s_cut_j = negative ? kPHalf + p8 : p8;
+                    s_cut_a = cum;
+                }
+                cum += mq;
+            }
+        };
+        scan8(offp + ip - pos, false);
+        __syncthreads();
+        if (s_cut_j < 0) {
+            if ((double)(Zp + Zm) >= target) {  // the cut among the values below 2^-16 or the zeros
+                fallback();
+                return;
+            }
+            scan8(Zp + Zm + offn + in - neg, true);
+            __syncthreads();
+        }
+        if (s_cut_j < 0) {  // (p Z beyond every weighted bin: not reached for p <= 1)
             fallback();
             return;
         }
-        const int wi = kPHalf - 1 - s_cut_j;
-        kc = 0x8000u | (uint32_t)((kPE0 << 7) + wi);
-        cnt = (long long)s_hist[kPHalf + wi];
+        const bool cut_neg = s_cut_j >= kPHalf;
+        const int cb = cut_neg ? s_cut_j - kPHalf : kPHalf - 1 - s_cut_j;  // window offset of the cut value
+        const uint32_t cbits = (cut_neg ? 0x8000u : 0u) | (uint32_t)((kPE0 << 7) + cb);
+        kc = okey_bf16((uint16_t)cbits);
+        cnt = (long long)s_hist[cut_neg ? kPHalf - 1 - cb : kPHalf + cb];
         const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
         const unsigned long long A = s_cut_a;
         // filter_row's rule: c = number of tie ranks j >= 0 with A + j qc < target (the first always
@@ -1671,51 +1768,196 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
     }
 
-    // ---- pass 2: MODE 2 over the admissible elements (+ the tie list)
-    if (threadIdx.x == 0) s_rf = RowFilter{mx, 0u, 0x7fffffff, kc, ic};
+    if (probe == 2) return;  // timing probe: pass 1 + the cut
+
+    // ---- pass 2: the Gumbel-max decision (MODE 2's noise, bound and exact scores) over the
+    //      admissible elements: top_p x > value(kc) (>= when the cut keeps all of kc's elements;
+    //      float and key order agree off +-0, which no window bin holds), min_p alone x/T >=
+    //      max/T + ln min_p; kc's elements, when the cut splits them, into the tie list
+    const float xc = use_topp ? from_key<T>(kc) : 0.f;
+    const bool split = tie_key <= 0xffffu;
+    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
+    const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
+    const float temp = 1.0f / inv_t;
+    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    float thr = -INFINITY, bar = -INFINITY;
+    float best_s = -INFINITY;
+    int best_i = 0x7fffffff;
+    if (threadIdx.x == 0) s_bar = -INFINITY;
+    auto adm = [&](float x) -> bool { return use_topp ? (split ? x > xc : x >= xc) : x * inv_t >= mthr; };
+    auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
+        const float wb = wave_max_uniform(best_s);
+        if (lane == 0 && wb > -INFINITY)
+            __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const float sb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar)));
+        bar = fmaxf(wb, sb);
+        thr = (bar - kNoiseC) * temp;
+    };
+    // one vector of cnt (<= VEC) elements at v0 (one noise group); a vector without admissible or
+    // tie elements in the whole wave costs no hash
+    auto visit2 = [&](const uint4& pk, int v0, int cnt) {
+        uint16_t raw[VEC];
+        __builtin_memcpy(raw, &pk, 16);
+        float x[VEC];
+        bool ok[VEC], tie[VEC];
+        float xm = -INFINITY;
+        bool anyt = false;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            x[k] = k < cnt ? bf16_to_f32(raw[k]) : -INFINITY;
+            ok[k] = k < cnt && adm(x[k]);
+            xm = fmaxf(xm, ok[k] ? x[k] : -INFINITY);
+            tie[k] = split && k < cnt && x[k] == xc;
+            anyt = anyt || tie[k];
+        }
+        const bool some = xm > -INFINITY;
+        if (__builtin_amdgcn_ballot_w64(some || anyt) == 0) return;
+        if (__builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {  // kc's elements: indices only (their value is xc)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (tie[k]) {
+                    const uint32_t pos = atomicAdd(&s_nt, 1u);
+                    if (pos < (uint32_t)kPTieCap) s_tidx[pos] = v0 + k;
+                }
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(some) == 0) return;
+        const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+        const float bits = noise_bits(h);
+        const bool cand = some && !(fmaf(bits, -kT, xm) - thr < 0.f);
+        if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
+        if (cand) {
+            const float Eg = group_min_e(h);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (ok[k] && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
+                    const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
+                    if (sc > best_s) {  // ascending index within the lane: the lowest wins ties
+                        best_s = sc;
+                        best_i = v0 + k;
+                    }
+                }
+            }
+        }
+        raise_bar();
+    };
+    if (nfull > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
+    }
+    __syncthreads();  // s_bar
+    if (nfull > 0) {
+        // the bar from this lane's first two vectors (one exact score: the best admissible element)
+        float xb = -INFINITY;
+        int vb = -1;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            uint16_t raw[VEC];
+            __builtin_memcpy(raw, &cur[u], 16);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const float x = bf16_to_f32(raw[k]);
+                if (adm(x) && x > xb) {
+                    xb = x;
+                    vb = (u * NT + (int)threadIdx.x) * VEC + k;
+                }
+            }
+        }
+        if (vb >= 0) {
+            const uint32_t h = ehash(key, keyb, (uint32_t)vb >> 3);
+            best_s = noise_score(xb, inv_t, vb, h, group_min_e(h), key2);
+            best_i = vb;
+        }
+        raise_bar();
+        __syncthreads();
+        bar = fmaxf(bar, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar))));
+        thr = (bar - kNoiseC) * temp;
+        for (int base = 0; base < nfull; base += kStep) {
+            const bool more = base + kStep < nfull;
+            switch (((nfull - base) * 4 - 1) / nfull) {
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) visit2(cur[u], (base + u * NT + threadIdx.x) * VEC, VEC);
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+    }
+    // the rest: whole vectors, then the ragged tail's partial group (one thread)
+    for (int i0 = nfull; i0 < nvec; i0 += NT) {  // same trip count in every thread (wave ballots inside)
+        const int i = i0 + (int)threadIdx.x;
+        visit2(i < nvec ? ld_stream(rv + i) : make_uint4(0u, 0u, 0u, 0u), i * VEC, i < nvec ? VEC : 0);
+    }
+    if (nvec * VEC < V) {
+        uint16_t t[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int cnt = V - nvec * VEC;
+        if (threadIdx.x == 0)
+            for (int k = 0; k < cnt; ++k) t[k] = row[nvec * VEC + k];
+        uint4 pk;
+        __builtin_memcpy(&pk, t, 16);
+        visit2(pk, nvec * VEC, threadIdx.x == 0 ? cnt : 0);
+    }
+    // the best admissible element: lanes, waves; then kc's kept ties
+    Best best{best_s, best_i};
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(best.score, off, kWave);
+        const int oi = __shfl_xor(best.idx, off, kWave);
+        if (better(os, oi, best)) best = Best{os, oi};
+    }
+    if (lane == 0) {
+        s_bs[w] = best.score;
+        s_bi[w] = best.idx;
+    }
     __syncthreads();
-    const TieSink sink{s_tidx, s_tsc, &s_nt, kPTieCap, tie_key};
-    sample_unit<T, 2, NT, true, true>(logits, ld, V, V, inv_t, 0, use_minp && !use_topp, ln_min_p, seed, seq_ids,
-                                      step, use_topp, &s_rf, tokens, logp_out, nullptr, nullptr, row_i, 0, 1, 0, &sink,
-                                      &s_p);
-    __syncthreads();
-    Part p = s_p;
+    Best b{s_bs[0], s_bi[0]};
+    for (int j = 1; j < NW; ++j)
+        if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
     int icut = ic;
-    if (tie_key <= 0xffffu) {  // rank kc's elements by index: the first c are admissible
+    if (split) {  // rank kc's elements by index: the first c are admissible
         const int n = (int)min(s_nt, (uint32_t)kPTieCap);
-        Best best{-INFINITY, 0x7fffffff};
+        Best tb{-INFINITY, 0x7fffffff};
         for (int i = threadIdx.x; i < n; i += NT) {
             const int ii = s_tidx[i];
             int r = 0;
             for (int j = 0; j < n; ++j) r += s_tidx[j] < ii ? 1 : 0;
-            if (r < c && better(s_tsc[i], ii, best)) best = Best{s_tsc[i], ii};
+            if (r < c) {  // admissible: its exact score
+                const uint32_t h = ehash(key, keyb, (uint32_t)ii >> 3);
+                const float sc = noise_score(xc, inv_t, ii, h, group_min_e(h), key2);
+                if (better(sc, ii, tb)) tb = Best{sc, ii};
+            }
             if (r == c - 1) s_icut = ii;  // the cut's last kept index (filter_row's ic)
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
-            const float os = __shfl_xor(best.score, off, kWave);
-            const int oi = __shfl_xor(best.idx, off, kWave);
-            if (better(os, oi, best)) best = Best{os, oi};
+            const float os = __shfl_xor(tb.score, off, kWave);
+            const int oi = __shfl_xor(tb.idx, off, kWave);
+            if (better(os, oi, tb)) tb = Best{os, oi};
         }
         __syncthreads();
         if (lane == 0) {
-            s_bs[w] = best.score;
-            s_bi[w] = best.idx;
+            s_bs[w] = tb.score;
+            s_bi[w] = tb.idx;
         }
         __syncthreads();
-        Best b{p.score, p.idx};
         for (int j = 0; j < NW; ++j)
             if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
-        p.score = b.score;
-        p.idx = b.idx;
         icut = s_icut;
     }
     if (threadIdx.x == 0) {
-        tokens[row_i] = p.idx;
-        if (logp_out) {
-            const float lse = p.m + fast_log2(p.s) * kLn2;
-            logp_out[row_i] = (p.idx >= 0 && p.idx < V) ? to_f<T>(row[p.idx]) - lse : __builtin_nanf("");
-        }
+        tokens[row_i] = b.idx;
+        if (logp_out)
+            logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - lse : __builtin_nanf("");
         filt[row_i] = RowFilter{mx, 0u, kRowDone, kc, icut};
     }
 }
@@ -1782,7 +2024,8 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
             hipLaunchKernelGGL(sample_topp_kernel<T>, dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t, use_minp,
-                               ln_min_p, use_topp, use_topp ? top_p : 1.0f, seed, seq_ids, step, tokens, logp, filt);
+                               ln_min_p, use_topp, use_topp ? top_p : 1.0f, seed, seq_ids, step, tokens, logp, filt,
+                               g_probe_topp);
             return check_launch("sample_topp_kernel");
         }
     }

@@ -9,8 +9,11 @@ aligned) with the lm_head-fused HIP logprob kernels, the HIP pack, GRPO and fuse
 AdamW, and the weight sync back into the engine. A world_size-1 gloo group is the DP group,
 as in config 1.
 
-Checked: every micro-batch's loss from the fused pass equals oracle/cpu_ref's loss assembly
-(PPO clip + k3 KL to ref, token mean) on the same log-probs within 1e-4; the engine's rollout
+Rewards: skyrl-gym's strict gsm8k scorer (skyrl_amd/envs/gsm8k.py, utils.py:17-63) on the
+responses through a fixture detokenizer, against answers the test plants per prompt.
+Checked: every micro-batch's fused-pass logprobs and entropies equal oracle/cpu_ref's on the
+micro-batch's own lm_head logits within 1e-4, and its loss equals oracle/cpu_ref's loss assembly
+(PPO clip + k3 KL to ref, token mean) on those oracle log-probs within 1e-4; the engine's rollout
 logprobs equal the learner's recomputed old logprobs of the same tokens (the sampler, the
 weight sync and the fused logprob agree), every metric is finite, the policy moves away from
 the reference (KL > 0), with sample packing off and on.
@@ -32,8 +35,20 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-def _reward(prompt, response, extra):  # gsm8k-style strict-answer stand-in: answer token parity
-    return float(len(response) > 0 and response[-1] % 2 == 0)
+def _detok(ids):
+    """Fixture detokenizer (GPT-2's vocabulary files are not in the image): every 16th token id is
+    the gsm8k answer marker, the others a digit, so the strict scorer sees `#### <digit>` often."""
+    return "".join("#### " if t % 16 == 0 else f"{t % 10} " for t in ids)
+
+
+def _reward_fn(log):
+    from skyrl_amd.envs.gsm8k import compute_score
+
+    def reward(prompt, response, extra):  # skyrl-gym gsm8k strict scorer (utils.py:17-63) on the planted answer
+        r = float(compute_score(_detok(response), extra["ground_truth"]))
+        log.append(r)
+        return r
+    return reward
 
 
 @pytest.fixture
@@ -54,21 +69,40 @@ def test_gpt2_small_grpo_steps(gloo_world1, packing, monkeypatch):
     from oracle import cpu_ref
     from skyrl_amd import ops
 
-    # every micro-batch's fused pass against the oracle's loss assembly on the same log-probs
-    # (workers/worker.py:801-876: PPO clip + k3 KL to ref, token-mean; cpu_ref.policy_loss_assembly)
-    checked = []
-    orig = ops.policy_train_ragged
+    # every micro-batch's fused pass against the oracle: its logprobs / entropies against
+    # cpu_ref.logprobs_from_logits / entropy_from_logits on the micro-batch's own lm_head logits
+    # (1e-4), and its loss against the oracle's loss assembly (workers/worker.py:801-876: PPO clip +
+    # k3 KL to ref, token mean; cpu_ref.policy_loss_assembly) on those ORACLE log-probs (1e-4)
+    checked, lp_checked = [], []
+    orig_micro, orig_fold = ops.PolicyTrainStep.micro, ops.PolicyTrainStep.fold
 
-    def checked_pass(logits, labels, pos, old, adv, mask, params, **kw):
-        loss, met, lp, ent = orig(logits, labels, pos, old, adv, mask, params, **kw)
-        exp, _ = cpu_ref.policy_loss_assembly(lp.detach().float().cpu(), old.float().cpu(), adv.float().cpu(),
-                                              mask.float().cpu(), kw["ref_log_probs"].float().cpu(),
-                                              ent.detach().float().cpu())
-        got = float(met[0])
-        checked.append(abs(got - float(exp)) <= 1e-5 + 1e-4 * abs(float(exp)))
-        return loss, met, lp, ent
+    def micro(self, k, logits, labels, token_pos=None):
+        if not hasattr(self, "_cap"):
+            self._cap = {}
+        self._cap[k] = (logits.detach().cpu(), labels.detach().cpu(), token_pos.detach().cpu().long())
+        return orig_micro(self, k, logits, labels, token_pos)
 
-    monkeypatch.setattr(ops, "policy_train_ragged", checked_pass)
+    def fold(self):
+        loss, met = orig_fold(self)
+        for k, (z, lab, pos) in self._cap.items():
+            i, j = self.rows(k)
+            R = self.R
+            lp_o = cpu_ref.logprobs_from_logits(z, lab)
+            ent_o = cpu_ref.entropy_from_logits(z)
+            lp_k = self.logp[i:j].cpu().reshape(-1)[pos]
+            ent_k = self.entropy[i:j].cpu().reshape(-1)[pos]
+            lp_checked.append(torch.allclose(lp_k, lp_o, atol=1e-4, rtol=1e-4)
+                              and torch.allclose(ent_k, ent_o, atol=1e-4, rtol=1e-4))
+            lp_full = torch.zeros((j - i) * R)
+            ent_full = torch.zeros((j - i) * R)
+            lp_full[pos], ent_full[pos] = lp_o, ent_o
+            exp, _ = cpu_ref.policy_loss_assembly(lp_full.view(j - i, R), self.old[i:j].cpu(), self.adv[i:j].cpu(),
+                                                  self.mask[i:j].cpu(), self.ref[i:j].cpu(), ent_full.view(j - i, R))
+            checked.append(abs(float(met[k][0]) - float(exp)) <= 1e-5 + 1e-4 * abs(float(exp)))
+        return loss, met
+
+    monkeypatch.setattr(ops.PolicyTrainStep, "micro", micro)
+    monkeypatch.setattr(ops.PolicyTrainStep, "fold", fold)
 
     # ... and the GRPO advantages against the oracle (utils/ppo_utils.py:1132-1182), every step
     from skyrl_amd import trainer_utils
@@ -99,19 +133,23 @@ def test_gpt2_small_grpo_steps(gloo_world1, packing, monkeypatch):
                          use_sample_packing=packing,
                          sampling_params={"max_tokens": 24, "min_tokens": 1, "temperature": 1.0},
                          algorithm=AlgorithmConfig(use_kl_loss=True))
-    trainer = GRPOTrainer(tcfg, policy, client, _reward, pad_token_id=0, ref=ref, dp_group=gloo_world1)
+    rewards = []
+    trainer = GRPOTrainer(tcfg, policy, client, _reward_fn(rewards), pad_token_id=0, ref=ref, dp_group=gloo_world1)
     assert trainer.grad_sync is None  # world_size 1: nothing to reduce
     g = torch.Generator().manual_seed(1)
     prompts = [torch.randint(1, 50256, (int(torch.randint(8, 33, (1,), generator=g)),), generator=g).tolist()
                for _ in range(16)]
     w0 = policy.transformer.h[0].attn.c_attn.weight.detach().clone()
     hist = []
+    extras = [{"ground_truth": str(i % 10)} for i in range(16)]  # planted gsm8k answers
     for step in range(3):
-        m = trainer.step(prompts)
+        m = trainer.step(prompts, extras)
         hist.append(m)
         assert all(torch.isfinite(torch.tensor(float(v))) for v in m.values()), m
         assert m["logprobs_diff_mean"] < 0.03, (step, m["logprobs_diff_mean"])
-    assert checked and all(checked), checked  # 3 steps x 4 micro-batches, each within 1e-4 of the oracle
+    assert len(checked) == 12 and all(checked), checked  # 3 steps x 4 micro-batches, each within 1e-4 of the oracle
+    assert len(lp_checked) == 12 and all(lp_checked), lp_checked
+    assert 0 < sum(rewards) < len(rewards), rewards  # the strict scorer's rewards are not degenerate
     assert len(adv_checked) == 3 and all(adv_checked), adv_checked
     assert not torch.equal(policy.transformer.h[0].attn.c_attn.weight.detach(), w0)
     assert hist[-1]["policy_kl"] > 0
