@@ -1,6 +1,6 @@
 """Where the two-pass top_p kernel's time goes at the bench shape [512, 151,936] bf16, T = 1:
-skyrl_tune("topp_probe") 1 = pass 1 alone, 2 = pass 1 + the cut (tokens invalid in both), 0 =
-the whole kernel; beside it the unfiltered T = 1 and greedy samplers (one read of the row) and
+skyrl_tune("topp_probe") 1 = pass 1 alone, 2 = pass 1 + the cut, 3 / 4 = pass 1 + the cut + a bare
+re-read of the row (nontemporal / cached loads) (tokens invalid in 1-4), 0 = the whole kernel; beside it the unfiltered T = 1 and greedy samplers (one read of the row) and
 the two-kernel path. One JSON line."""
 import json
 import os
@@ -36,7 +36,7 @@ def main():
     out = {}
     for name, kw in (("top_p0.95", dict(top_p=0.95)), ("top_p0.9", dict(top_p=0.9)), ("min_p0.05", dict(min_p=0.05))):
         res = {}
-        for probe in (1, 2, 0):
+        for probe in (1, 2, 3, 4, 0):
             ops._ffi.call("skyrl_tune", b"topp_probe", probe)
             res[f"probe{probe}_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
                                                                tokens_out=tok, logp_out=lp, **kw))

@@ -1469,14 +1469,18 @@ constexpr int kPHalf = 4096;    // keys per sign in the window
 constexpr int kPSlowCap = 512;  // elements below the window
 constexpr int kPTieCap = 1024;  // elements at a split cut key
 
-template <typename T>
+// uniform (scalar) copy of a wave-uniform float, so the hot loops keep it in an SGPR
+__device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+
+template <typename T, bool TOPP>
 __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topp_kernel(
-    const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, int use_topp,
-    float top_p, uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
+    const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, float top_p,
+    uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, RowFilter* __restrict__ filt, int probe) {
     static_assert(sizeof(T) == 2, "bf16 rows");
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
-    __shared__ uint32_t s_hist[2 * kPHalf];
+    constexpr int kDummy = 2 * kPHalf;  // 64 words taking the out-of-window elements' increments (no branch)
+    __shared__ uint32_t s_hist[TOPP ? 2 * kPHalf + kWave : 1];
     __shared__ uint16_t s_slow[kPSlowCap];
     __shared__ uint32_t s_nslow, s_bad, s_nt, s_zero[2];
     __shared__ float s_vmax[NW], s_lm[NW], s_ls[NW], s_bar;
@@ -1487,7 +1491,6 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     __shared__ int32_t s_tidx[kPTieCap];
     __shared__ float s_bs[NW];
     __shared__ int32_t s_bi[NW];
-    __shared__ Part s_p;
     __shared__ int s_icut;
     __shared__ RowFilter s_rf;
     const int row_i = blockIdx.x;
@@ -1509,54 +1512,69 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         s_cut_j = -1;
         s_zero[0] = s_zero[1] = 0u;
     }
-    if (use_topp)
-        for (int j = threadIdx.x; j < 2 * kPHalf; j += NT) s_hist[j] = 0u;
+    if constexpr (TOPP)
+        for (int j = threadIdx.x; j < 2 * kPHalf + kWave; j += NT) s_hist[j] = 0u;
     __syncthreads();
 
-    // ---- pass 1: the row max; for top_p the count histogram
+    // ---- pass 1: the row max; top_p: the count histogram (one LDS add per element, no branch;
+    //      elements outside the window take a uniform slow path), min_p: the raw lse
     float vmx = -INFINITY;
     bool bad = false;
-    // min_p alone: the raw online (max, sum-exp) for the logprob here (lagged offset, as the top_k
-    // kernel); top_p takes it from the histogram instead
-    float lm = -1e30f, ls = 0.f;
-    auto elem = [&](uint32_t b) {
-        if (use_topp) {
-            const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
-            if ((unsigned)wi < (unsigned)kPHalf) {
-                atomicAdd(&s_hist[(b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi], 1u);
-            } else if (wi < 0) {
-                if ((b & 0x7fffu) == 0u) {  // +-0: their own counters (exact zeros may be many)
-                    atomicAdd(&s_zero[b >> 15], 1u);
-                } else {
-                    const uint32_t pos = atomicAdd(&s_nslow, 1u);
-                    if (pos < (uint32_t)kPSlowCap) s_slow[pos] = (uint16_t)b;
-                }
-            } else {  // |x| >= 2^16: -inf and large negatives weigh nothing; NaN, +inf, x >= 2^16
-                bad = bad || !(b == 0xff80u || ((b & 0x8000u) && (b & 0x7fffu) < 0x7f80u));
-            }
-        } else {  // min_p alone: the max must be a number (NaN / +inf rows: the fallback)
-            bad = bad || ((b & 0x7f80u) == 0x7f80u && b != 0xff80u);
+    float lm = -1e30f, ls = 0.f;  // (min_p alone) lagged online (max, sum-exp), as the top_k kernel
+    auto rare_elem = [&](uint32_t b) {  // an element outside the window (top_p)
+        const uint32_t a = b & 0x7fffu;
+        if (a == 0u) {
+            atomicAdd(&s_zero[b >> 15], 1u);  // +-0: their own counters (exact zeros may be many)
+        } else if (a < (uint32_t)(kPE0 << 7)) {
+            const uint32_t pos = atomicAdd(&s_nslow, 1u);
+            if (pos < (uint32_t)kPSlowCap) s_slow[pos] = (uint16_t)b;
+        } else {  // |x| >= 2^16: -inf and large negatives weigh nothing; NaN, +inf, x >= 2^16: fallback
+            bad |= !(b == 0xff80u || ((b & 0x8000u) && a < 0x7f80u));
         }
     };
     auto visit1 = [&](const uint4& pk) {
         uint16_t raw[VEC];
         __builtin_memcpy(raw, &pk, 16);
-        float vm = bf16_to_f32(raw[0]);
+        float x[VEC];
 #pragma unroll
-        for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, bf16_to_f32(raw[k]));
+        for (int k = 0; k < VEC; ++k) x[k] = bf16_to_f32(raw[k]);
+        float vm = x[0];
+#pragma unroll
+        for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, x[k]);
         vmx = fmaxf(vmx, vm);
-        if (!use_topp) {
+        if constexpr (TOPP) {
+            bool rare = false;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const uint32_t b = raw[k];
+                const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
+                const bool in = (unsigned)wi < (unsigned)kPHalf;
+                const int bin = (b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi;
+                atomicAdd(&s_hist[in ? bin : kDummy + lane], 1u);
+                rare |= !in;  // (bitwise: a short-circuit || becomes branches)
+            }
+            if (__builtin_amdgcn_ballot_w64(rare) != 0 && rare) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int wi = (int)(raw[k] & 0x7fffu) - (kPE0 << 7);
+                    if (!((unsigned)wi < (unsigned)kPHalf)) rare_elem(raw[k]);
+                }
+            }
+        } else {
             if (vm > lm + 64.f) {
                 ls *= fast_exp2((lm - vm) * kLog2e);
                 lm = vm;
             }
             float acc = 0.f;
+            bool bb = false;
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) acc += fast_exp2((bf16_to_f32(raw[k]) - lm) * kLog2e);
+            for (int k = 0; k < VEC; ++k) {
+                acc += fast_exp2((x[k] - lm) * kLog2e);
+                bb |= ((raw[k] & 0x7f80u) == 0x7f80u) & (raw[k] != 0xff80u);  // NaN, +inf: fallback
+            }
             ls += acc;
+            bad |= bb;
         }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) elem(raw[k]);
     };
     if (nfull > 0) {
         for (int base = 0; base < nfull; base += kStep) {
@@ -1578,22 +1596,26 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
             }
         }
+        __builtin_amdgcn_s_setprio(0);
     }
     for (int i = nfull + threadIdx.x; i < nvec; i += NT) visit1(rv[i]);
     for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
         const uint16_t b = row[i];
         const float x = bf16_to_f32(b);
         vmx = fmaxf(vmx, x);
-        if (!use_topp) {
+        if constexpr (TOPP) {
+            const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
+            if ((unsigned)wi < (unsigned)kPHalf) atomicAdd(&s_hist[(b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi], 1u);
+            else rare_elem(b);
+        } else {
             const float mn = fmaxf(lm, x);
             ls = ls * fast_exp2((lm - mn) * kLog2e) + fast_exp2((x - mn) * kLog2e);
             lm = mn;
+            bad |= ((b & 0x7f80u) == 0x7f80u) & (b != 0xff80u);
         }
-        elem(b);
     }
-    __builtin_amdgcn_s_setprio(0);
     vmx = wave_max(vmx);
-    if (!use_topp) {
+    if constexpr (!TOPP) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const float om = __shfl_xor(lm, off, kWave);
@@ -1613,8 +1635,11 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     float mx = s_vmax[0];
 #pragma unroll
     for (int j = 1; j < NW; ++j) mx = fmaxf(mx, s_vmax[j]);
+    mx = uni(mx);
+    const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
+    const float mthr = uni(mx * inv_t + ln_min_p);
     float lse = 0.f;
-    if (!use_topp) {
+    if constexpr (!TOPP) {
         float M = s_lm[0], S = s_ls[0];
 #pragma unroll
         for (int j = 1; j < NW; ++j) {
@@ -1625,157 +1650,163 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         lse = M + fast_log2(S) * kLn2;
     }
     if (probe == 1) return;  // timing probe (skyrl_tune topp_probe): pass 1 only
-    const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
-    const float mthr = mx * inv_t + ln_min_p;
 
-    auto fallback = [&]() {
-        topk_fallback<T>(logits, ld, V, 0, inv_t, use_minp, ln_min_p, use_topp, top_p, seed, seq_ids, step, tokens,
-                         logp_out, &s_rf, row_i);
-        if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
-    };
-    if (s_bad || (use_topp && s_nslow > (uint32_t)kPSlowCap)) {
-        fallback();
-        return;
-    }
+    bool fb = s_bad != 0u || (TOPP && s_nslow > (uint32_t)kPSlowCap);  // block-uniform
 
-    // ---- on chip (top_p): bin masses, Z, the cut key and its tie count
-    uint32_t kc = 0u, tie_key = 0x10000u;  // no tie list unless the cut splits kc's group
-    long long c = 0, cnt = 0;
+    // ---- on chip (top_p): bin masses (once per bin, kept in registers), Z, the raw lse, the cut
+    //      key and its tie count
+    uint32_t kc = 0u;
+    bool split = false;
+    long long c = 0;
     int ic = 0x7fffffff;
-    if (use_topp) {
-        // thread t: descending positions j = 8t .. 8t+7 of the positive bins (bin kPHalf + 4095 - j)
-        // and the negative bins 8t .. 8t+7; the list entries t, t + NT, ...
-        auto mass_of = [&](uint32_t bits, uint32_t n) -> unsigned long long {
-            const float x = bf16_to_f32((uint16_t)bits);
-            if (n == 0u || (use_minp && !(x * inv_t >= mthr))) return 0ull;
-            return (unsigned long long)n * (unsigned long long)mass_q(x, mx, inv_t);
-        };
-        // descending key order: the positive bins (descending value), the list and +-0 (the
-        // middle), the negative bins (ascending |x|); a block scan of each side
-        unsigned long long pos = 0ull, neg = 0ull, mid = 0ull;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int wi = kPHalf - 1 - (8 * (int)threadIdx.x + q);
-            pos += mass_of((uint32_t)((kPE0 << 7) + wi), s_hist[kPHalf + wi]);
-            const int wn = 8 * (int)threadIdx.x + q;
-            neg += mass_of(0x8000u | (uint32_t)((kPE0 << 7) + wn), s_hist[kPHalf - 1 - wn]);
-        }
-        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) mid += mass_of(s_slow[i], 1u);
-        if (threadIdx.x < 2) mid += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
-        // the raw logits' sum-exp for the logprob, from the same counts (another summation order
-        // than the streaming lse: equal to float rounding)
-        double se = 0.0;
-        auto sexp = [&](uint32_t bits, uint32_t n) {
-            if (n) se += (double)n * (double)fast_exp2((bf16_to_f32((uint16_t)bits) - mx) * kLog2e);
-        };
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int p8 = 8 * (int)threadIdx.x + q;
-            sexp((uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf + p8]);
-            sexp(0x8000u | (uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf - 1 - p8]);
-        }
-        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) sexp(s_slow[i], 1u);
-        if (threadIdx.x < 2) sexp(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
-        se = wave_sum(se);
-        if (lane == 0) s_wexp[w] = se;
-        unsigned long long ip = pos, in = neg;
-#pragma unroll
-        for (int off = 1; off < kWave; off <<= 1) {
-            const unsigned long long op = (unsigned long long)__shfl_up((long long)ip, off, kWave);
-            const unsigned long long on = (unsigned long long)__shfl_up((long long)in, off, kWave);
-            if (lane >= off) {
-                ip += op;
-                in += on;
-            }
-        }
-        unsigned long long wm = mid;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) wm += (unsigned long long)__shfl_xor((long long)wm, off, kWave);
-        if (lane == kWave - 1) {
-            s_wpos[w] = ip;
-            s_wneg[w] = in;
-        }
-        if (lane == 0) s_woth[w] = wm;
-        __syncthreads();
-        unsigned long long offp = 0ull, offn = 0ull, Zp = 0ull, Zn = 0ull, Zm = 0ull;
-        for (int j = 0; j < NW; ++j) {
-            if (j < w) {
-                offp += s_wpos[j];
-                offn += s_wneg[j];
-            }
-            Zp += s_wpos[j];
-            Zn += s_wneg[j];
-            Zm += s_woth[j];
-        }
-        const unsigned long long Z = Zp + Zm + Zn;
-        double S = 0.0;
-        for (int j = 0; j < NW; ++j) S += s_wexp[j];
-        lse = mx + fast_log2((float)S) * kLn2;
-        const double target = (double)top_p * (double)Z;
-        // the cut: the bin where the mass before it is < p Z and the mass through it reaches it
-        // (the first weighted bin also when target <= 0: top_p = 0 keeps the top token, as
-        // filter_row's radix select, whose first bin is the max's); cut_j < 4096: positive bin
-        // (descending position), >= 4096: negative bin 4096 + wn
-        auto scan8 = [&](unsigned long long cum, bool negative) {
+    if constexpr (TOPP) {
+        if (!fb) {
+            // thread t: the positive bins at descending positions p = 8t .. 8t+7 (value offset 4095 - p),
+            // the negative bins at ascending |x| (offset p), the list entries t, t + NT, ...
+            auto mass_of = [&](uint32_t bits, uint32_t n) -> unsigned long long {
+                const float x = bf16_to_f32((uint16_t)bits);
+                if (n == 0u || (use_minp && !(x * inv_t >= mthr))) return 0ull;
+                return (unsigned long long)n * (unsigned long long)mass_q(x, mx, inv_t);
+            };
+            unsigned long long pm[8], nm[8];
+            unsigned long long pos = 0ull, neg = 0ull, mid = 0ull;
+            double se = 0.0;  // the raw logits' sum-exp (the logprob's lse) from the same counts
+            auto sexp = [&](uint32_t bits, uint32_t n) {
+                if (n) se += (double)n * (double)fast_exp2((bf16_to_f32((uint16_t)bits) - mx) * kLog2e);
+            };
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int p8 = 8 * (int)threadIdx.x + q;
-                const unsigned long long mq =
-                    negative ? mass_of(0x8000u | (uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf - 1 - p8])
-                             : mass_of((uint32_t)((kPE0 << 7) + kPHalf - 1 - p8), s_hist[2 * kPHalf - 1 - p8]);
-                if (mq && (cum == 0ull || (double)cum < target) && (double)(cum + mq) >= target) {
-                    s_cut_j = negative ? kPHalf + p8 : p8;
-                    s_cut_a = cum;
+                const uint32_t pb = (uint32_t)((kPE0 << 7) + kPHalf - 1 - p8), nb = 0x8000u | (uint32_t)((kPE0 << 7) + p8);
+                const uint32_t pc = s_hist[2 * kPHalf - 1 - p8], nc = s_hist[kPHalf - 1 - p8];
+                pm[q] = mass_of(pb, pc);
+                nm[q] = mass_of(nb, nc);
+                pos += pm[q];
+                neg += nm[q];
+                sexp(pb, pc);
+                sexp(nb, nc);
+            }
+            for (int i = threadIdx.x; i < (int)s_nslow; i += NT) {
+                mid += mass_of(s_slow[i], 1u);
+                sexp(s_slow[i], 1u);
+            }
+            if (threadIdx.x < 2) {
+                mid += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
+                sexp(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
+            }
+            unsigned long long ip = pos, in = neg;
+#pragma unroll
+            for (int off = 1; off < kWave; off <<= 1) {
+                const unsigned long long op = (unsigned long long)__shfl_up((long long)ip, off, kWave);
+                const unsigned long long on = (unsigned long long)__shfl_up((long long)in, off, kWave);
+                if (lane >= off) {
+                    ip += op;
+                    in += on;
                 }
-                cum += mq;
             }
-        };
-        scan8(offp + ip - pos, false);
-        __syncthreads();
-        if (s_cut_j < 0) {
-            if ((double)(Zp + Zm) >= target) {  // the cut among the values below 2^-16 or the zeros
-                fallback();
-                return;
+            unsigned long long wm = mid;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) wm += (unsigned long long)__shfl_xor((long long)wm, off, kWave);
+            se = wave_sum(se);
+            if (lane == kWave - 1) {
+                s_wpos[w] = ip;
+                s_wneg[w] = in;
             }
-            scan8(Zp + Zm + offn + in - neg, true);
+            if (lane == 0) {
+                s_woth[w] = wm;
+                s_wexp[w] = se;
+            }
             __syncthreads();
-        }
-        if (s_cut_j < 0) {  // (p Z beyond every weighted bin: not reached for p <= 1)
-            fallback();
-            return;
-        }
-        const bool cut_neg = s_cut_j >= kPHalf;
-        const int cb = cut_neg ? s_cut_j - kPHalf : kPHalf - 1 - s_cut_j;  // window offset of the cut value
-        const uint32_t cbits = (cut_neg ? 0x8000u : 0u) | (uint32_t)((kPE0 << 7) + cb);
-        kc = okey_bf16((uint16_t)cbits);
-        cnt = (long long)s_hist[cut_neg ? kPHalf - 1 - cb : kPHalf + cb];
-        const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
-        const unsigned long long A = s_cut_a;
-        // filter_row's rule: c = number of tie ranks j >= 0 with A + j qc < target (the first always
-        // for the top key)
-        const double jd = (target - (double)A) / (double)qc;
-        c = jd > 0.0 ? (long long)jd : 0;
-        while (c > 0 && (double)(A + (unsigned long long)(c - 1) * qc) >= target) --c;
-        while ((double)(A + (unsigned long long)c * qc) < target) ++c;
-        if (kc == kmax && c < 1) c = 1;
-        if (c < cnt) {
-            if (cnt > kPTieCap) {
-                fallback();
-                return;
+            unsigned long long offp = 0ull, offn = 0ull, Zp = 0ull, Zn = 0ull, Zm = 0ull;
+            double S = 0.0;
+            for (int j = 0; j < NW; ++j) {
+                if (j < w) {
+                    offp += s_wpos[j];
+                    offn += s_wneg[j];
+                }
+                Zp += s_wpos[j];
+                Zn += s_wneg[j];
+                Zm += s_woth[j];
+                S += s_wexp[j];
             }
-            tie_key = kc;
-            ic = -1;  // pass 2 decides the keys above kc; kc's elements go to the tie list
+            lse = mx + fast_log2((float)S) * kLn2;
+            const double target = (double)top_p * (double)(Zp + Zm + Zn);
+            // the cut: the bin where the mass before it is < p Z and the mass through it reaches it (the
+            // first weighted bin also when target <= 0: top_p = 0 keeps the top token, as filter_row's
+            // radix select, whose first bin is the max's); cut_j < 4096: positive bin (descending
+            // position), >= 4096: negative bin 4096 + |x| offset
+            auto scan8 = [&](unsigned long long cum, const unsigned long long (&m)[8], int base) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (m[q] && (cum == 0ull || (double)cum < target) && (double)(cum + m[q]) >= target) {
+                        s_cut_j = base + 8 * (int)threadIdx.x + q;
+                        s_cut_a = cum;
+                    }
+                    cum += m[q];
+                }
+            };
+            scan8(offp + ip - pos, pm, 0);
+            __syncthreads();
+            if (s_cut_j < 0 && (double)(Zp + Zm) < target) {  // past the positive window and the middle
+                scan8(Zp + Zm + offn + in - neg, nm, kPHalf);
+                __syncthreads();
+            }
+            if (s_cut_j < 0) {  // the cut among the values below 2^-16 / the zeros (or not reached)
+                fb = true;
+            } else {
+                const int cj = s_cut_j;
+                const bool cut_neg = cj >= kPHalf;
+                const int cb = cut_neg ? cj - kPHalf : kPHalf - 1 - cj;  // window offset of the cut value
+                kc = okey_bf16((uint16_t)((cut_neg ? 0x8000u : 0u) | (uint32_t)((kPE0 << 7) + cb)));
+                const long long cnt = (long long)s_hist[cut_neg ? kPHalf - 1 - cb : kPHalf + cb];
+                const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
+                const unsigned long long A = s_cut_a;
+                // filter_row's rule: c = number of tie ranks j >= 0 with A + j qc < target (the first
+                // always for the top key)
+                const double jd = (target - (double)A) / (double)qc;
+                c = jd > 0.0 ? (long long)jd : 0;
+                while (c > 0 && (double)(A + (unsigned long long)(c - 1) * qc) >= target) --c;
+                while ((double)(A + (unsigned long long)c * qc) < target) ++c;
+                if (kc == kmax && c < 1) c = 1;
+                if (c < cnt) {
+                    if (cnt > kPTieCap) fb = true;
+                    split = true;
+                    ic = -1;
+                }
+            }
         }
     }
-
+    // the cut as wave-uniform scalars (SGPRs through pass 2)
+    kc = (uint32_t)__builtin_amdgcn_readfirstlane((int)kc);
+    split = __builtin_amdgcn_readfirstlane((int)split) != 0;
+    c = (long long)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)c >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c));
+    ic = __builtin_amdgcn_readfirstlane(ic);
+    lse = uni(lse);
+    if (!fb) {  // (the fallback's call site stays after the hot loops: the register allocation of
+                // the passes does not see it)
     if (probe == 2) return;  // timing probe: pass 1 + the cut
 
-    // ---- pass 2: the Gumbel-max decision (MODE 2's noise, bound and exact scores) over the
-    //      admissible elements: top_p x > value(kc) (>= when the cut keeps all of kc's elements;
-    //      float and key order agree off +-0, which no window bin holds), min_p alone x/T >=
-    //      max/T + ln min_p; kc's elements, when the cut splits them, into the tie list
-    const float xc = use_topp ? from_key<T>(kc) : 0.f;
-    const bool split = tie_key <= 0xffffu;
+    // ---- pass 2: the Gumbel-max decision (MODE 2's noise, group bound and exact scores) over the
+    //      admissible elements x >= xlo: top_p, the value above the cut key when the cut splits its
+    //      tie group, else the cut key's value (value and key order agree off +-0, which no window
+    //      bin holds); min_p alone, the smallest bf16 value with x/T >= max/T + ln min_p; the cut
+    //      key's elements, when split, into the tie list (indices: their value is xc)
+    const float xc = uni(TOPP ? from_key<T>(kc) : 0.f);
+    float xlo;
+    if constexpr (TOPP) {
+        xlo = uni(split ? from_key<T>(kc + 1u) : xc);
+    } else {
+        // min_p as a value bound: the smallest bf16 x with x/T >= mthr (x * inv_t is monotone in x),
+        // by bisection over the keys between -inf (never) and +inf (always)
+        uint32_t lo = 0x007fu, hi = 0xff80u;
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (from_key<T>(mid) * inv_t >= mthr) hi = mid;
+            else lo = mid;
+        }
+        xlo = uni(from_key<T>(hi));
+    }
     const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
     const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
     const float temp = 1.0f / inv_t;
@@ -1784,53 +1815,49 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     float best_s = -INFINITY;
     int best_i = 0x7fffffff;
     if (threadIdx.x == 0) s_bar = -INFINITY;
-    auto adm = [&](float x) -> bool { return use_topp ? (split ? x > xc : x >= xc) : x * inv_t >= mthr; };
+    auto adm = [&](float x) -> bool { return x >= xlo; };
     auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
         const float wb = wave_max_uniform(best_s);
         if (lane == 0 && wb > -INFINITY)
             __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const float sb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar)));
-        bar = fmaxf(wb, sb);
+        bar = fmaxf(wb, uni(s_bar));
         thr = (bar - kNoiseC) * temp;
     };
-    // one vector of cnt (<= VEC) elements at v0 (one noise group); a vector without admissible or
-    // tie elements in the whole wave costs no hash
-    auto visit2 = [&](const uint4& pk, int v0, int cnt) {
+    // one vector of up to VEC elements at v0 (one noise group; padding slots are -inf); a vector
+    // without admissible elements in the whole wave costs no hash
+    auto visit2 = [&](const uint4& pk, int v0) {
         uint16_t raw[VEC];
         __builtin_memcpy(raw, &pk, 16);
         float x[VEC];
-        bool ok[VEC], tie[VEC];
         float xm = -INFINITY;
         bool anyt = false;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            x[k] = k < cnt ? bf16_to_f32(raw[k]) : -INFINITY;
-            ok[k] = k < cnt && adm(x[k]);
-            xm = fmaxf(xm, ok[k] ? x[k] : -INFINITY);
-            tie[k] = split && k < cnt && x[k] == xc;
-            anyt = anyt || tie[k];
+            x[k] = bf16_to_f32(raw[k]);
+            xm = fmaxf(xm, adm(x[k]) ? x[k] : -INFINITY);
+            if constexpr (TOPP) anyt |= x[k] == xc;  // (gated by split at the ballot)
         }
-        const bool some = xm > -INFINITY;
-        if (__builtin_amdgcn_ballot_w64(some || anyt) == 0) return;
-        if (__builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {  // kc's elements: indices only (their value is xc)
+        if constexpr (TOPP) {
+            if (split && __builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                if (tie[k]) {
-                    const uint32_t pos = atomicAdd(&s_nt, 1u);
-                    if (pos < (uint32_t)kPTieCap) s_tidx[pos] = v0 + k;
+                for (int k = 0; k < VEC; ++k) {
+                    if (x[k] == xc) {
+                        const uint32_t p = atomicAdd(&s_nt, 1u);
+                        if (p < (uint32_t)kPTieCap) s_tidx[p] = v0 + k;
+                    }
                 }
             }
         }
-        if (__builtin_amdgcn_ballot_w64(some) == 0) return;
+        if (__builtin_amdgcn_ballot_w64(xm > -INFINITY) == 0) return;
         const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
         const float bits = noise_bits(h);
-        const bool cand = some && !(fmaf(bits, -kT, xm) - thr < 0.f);
+        const bool cand = !(fmaf(bits, -kT, xm) - thr < 0.f);
         if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
         if (cand) {
             const float Eg = group_min_e(h);
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
-                if (ok[k] && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
+                if (adm(x[k]) && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
                     const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
                     if (sc > best_s) {  // ascending index within the lane: the lowest wins ties
                         best_s = sc;
@@ -1841,6 +1868,25 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         raise_bar();
     };
+    constexpr uint32_t kPadNinf = 0xff80ff80u;  // -inf bf16 pairs: never admissible, never a tie
+    if (probe == 3) {  // timing probe: pass 2's re-read alone (loads consumed by an xor)
+        uint32_t acc = 0u;
+        for (int i = threadIdx.x; i < nvec; i += NT) {
+            const uint4 v = ld_stream(rv + i);
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        if (acc == 0x12345678u) tokens[row_i] = -7;
+        return;
+    }
+    if (probe == 4) {  // timing probe: the same re-read with cached loads
+        uint32_t acc = 0u;
+        for (int i = threadIdx.x; i < nvec; i += NT) {
+            const uint4 v = rv[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        if (acc == 0x12345678u) tokens[row_i] = -7;
+        return;
+    }
     if (nfull > 0) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) cur[u] = ld_stream(rv + u * NT + threadIdx.x);
@@ -1870,7 +1916,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         raise_bar();
         __syncthreads();
-        bar = fmaxf(bar, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar))));
+        bar = fmaxf(bar, uni(s_bar));
         thr = (bar - kNoiseC) * temp;
         for (int base = 0; base < nfull; base += kStep) {
             const bool more = base + kStep < nfull;
@@ -1885,7 +1931,10 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) visit2(cur[u], (base + u * NT + threadIdx.x) * VEC, VEC);
+            for (int u = 0; u < 4; ++u) {
+                visit2(cur[u], (base + u * NT + threadIdx.x) * VEC);
+                __builtin_amdgcn_sched_barrier(0);  // one vector's temporaries at a time (no spills)
+            }
             if (more) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
@@ -1893,21 +1942,22 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         __builtin_amdgcn_s_setprio(0);
     }
-    // the rest: whole vectors, then the ragged tail's partial group (one thread)
-    for (int i0 = nfull; i0 < nvec; i0 += NT) {  // same trip count in every thread (wave ballots inside)
+    // the rest: whole vectors (same trip count in every thread: the wave ballots inside), then the
+    // ragged tail's partial group, read element-wise by thread 0
+    for (int i0 = nfull; i0 < nvec; i0 += NT) {
         const int i = i0 + (int)threadIdx.x;
-        visit2(i < nvec ? ld_stream(rv + i) : make_uint4(0u, 0u, 0u, 0u), i * VEC, i < nvec ? VEC : 0);
+        visit2(i < nvec ? ld_stream(rv + i) : make_uint4(kPadNinf, kPadNinf, kPadNinf, kPadNinf), i * VEC);
     }
     if (nvec * VEC < V) {
-        uint16_t t[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
-        const int cnt = V - nvec * VEC;
-        if (threadIdx.x == 0)
-            for (int k = 0; k < cnt; ++k) t[k] = row[nvec * VEC + k];
+        const int t0 = nvec * VEC, cnt = V - t0;
+        uint16_t t[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) t[k] = (threadIdx.x == 0 && k < cnt) ? row[t0 + k] : (uint16_t)0xff80u;
         uint4 pk;
         __builtin_memcpy(&pk, t, 16);
-        visit2(pk, nvec * VEC, threadIdx.x == 0 ? cnt : 0);
+        visit2(pk, t0);
     }
-    // the best admissible element: lanes, waves; then kc's kept ties
+    // the best admissible element: lanes, waves; then the cut key's kept ties
     Best best{best_s, best_i};
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1924,14 +1974,14 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     for (int j = 1; j < NW; ++j)
         if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
     int icut = ic;
-    if (split) {  // rank kc's elements by index: the first c are admissible
+    if (TOPP && split) {  // rank kc's elements by index: the first c are admissible, scored exactly here
         const int n = (int)min(s_nt, (uint32_t)kPTieCap);
         Best tb{-INFINITY, 0x7fffffff};
         for (int i = threadIdx.x; i < n; i += NT) {
             const int ii = s_tidx[i];
             int r = 0;
             for (int j = 0; j < n; ++j) r += s_tidx[j] < ii ? 1 : 0;
-            if (r < c) {  // admissible: its exact score
+            if (r < c) {
                 const uint32_t h = ehash(key, keyb, (uint32_t)ii >> 3);
                 const float sc = noise_score(xc, inv_t, ii, h, group_min_e(h), key2);
                 if (better(sc, ii, tb)) tb = Best{sc, ii};
@@ -1960,6 +2010,12 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - lse : __builtin_nanf("");
         filt[row_i] = RowFilter{mx, 0u, kRowDone, kc, icut};
     }
+    return;
+    }
+    // the two-kernel path's code in this workgroup (one call site)
+    topk_fallback<T>(logits, ld, V, 0, inv_t, use_minp, ln_min_p, TOPP ? 1 : 0, top_p, seed, seq_ids, step, tokens,
+                     logp_out, &s_rf, row_i);
+    if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
 }
 
 int splits_for(int nseq, int V) {
@@ -2023,9 +2079,12 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     if constexpr (sizeof(T) == 2) {
         if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
-            hipLaunchKernelGGL(sample_topp_kernel<T>, dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t, use_minp,
-                               ln_min_p, use_topp, use_topp ? top_p : 1.0f, seed, seq_ids, step, tokens, logp, filt,
-                               g_probe_topp);
+            if (use_topp)
+                hipLaunchKernelGGL((sample_topp_kernel<T, true>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
+                                   use_minp, ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, g_probe_topp);
+            else
+                hipLaunchKernelGGL((sample_topp_kernel<T, false>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
+                                   use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, g_probe_topp);
             return check_launch("sample_topp_kernel");
         }
     }
