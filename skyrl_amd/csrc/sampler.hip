@@ -1446,7 +1446,7 @@ __global__ __launch_bounds__(kFastNT) __attribute__((amdgpu_waves_per_eu(4))) vo
 // (With top_k set, sample_topk_kernel above.) A top_p cut needs the row max before any mass is
 // known, and the kept set can run to thousands of tokens (13k at p = 0.95 on N(0, 3^2) rows), so:
 //  * pass 1 (HBM; cached loads, so that pass 2 finds the row in the Infinity Cache): the row max
-//    and, for top_p, an LDS histogram of COUNTS per exact bf16 key over |x| in [2^-16, 2^16)
+//    and an LDS histogram of COUNTS per exact bf16 key over |x| in [2^-16, 2^16)
 //    (8192 bins: every key of that range has its own), +0 and -0 two more; keys below the window
 //    (0 < |x| < 2^-16) go to a short list; NaN, +inf, x >= 2^16 or a full list send the row to
 //    the fallback.
@@ -1468,6 +1468,7 @@ constexpr int kPE0 = 111;       // window: bf16 exponent fields 111..142, |x| in
 constexpr int kPHalf = 4096;    // keys per sign in the window
 constexpr int kPSlowCap = 512;  // elements below the window
 constexpr int kPTieCap = 1024;  // elements at a split cut key
+constexpr int kPCandCap = 2048; // pass 1's exactly scored elements (seeds + bound survivors)
 
 // uniform (scalar) copy of a wave-uniform float, so the hot loops keep it in an SGPR
 __device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
@@ -1480,15 +1481,20 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     static_assert(sizeof(T) == 2, "bf16 rows");
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
     constexpr int kDummy = 2 * kPHalf;  // 64 words taking the out-of-window elements' increments (no branch)
-    __shared__ uint32_t s_hist[TOPP ? 2 * kPHalf + kWave : 1];
+    __shared__ uint32_t s_hist[2 * kPHalf + kWave];
     __shared__ uint16_t s_slow[kPSlowCap];
     __shared__ uint32_t s_nslow, s_bad, s_nt, s_zero[2];
-    __shared__ float s_vmax[NW], s_lm[NW], s_ls[NW], s_bar;
+    __shared__ float s_vmax[NW], s_bar;
     __shared__ double s_wexp[NW];
     __shared__ unsigned long long s_wpos[NW], s_wneg[NW], s_woth[NW];
     __shared__ unsigned long long s_cut_a;
     __shared__ int s_cut_j;
     __shared__ int32_t s_tidx[kPTieCap];
+    __shared__ float s_cs[kPCandCap];     // pass 1's exactly scored elements: score, index, key
+    __shared__ int32_t s_ci[kPCandCap];
+    __shared__ uint16_t s_ck[kPCandCap];
+    __shared__ uint32_t s_nc, s_nbad, s_ntie;
+    __shared__ float s_bar1;
     __shared__ float s_bs[NW];
     __shared__ int32_t s_bi[NW];
     __shared__ int s_icut;
@@ -1499,6 +1505,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     const uint4* rv = reinterpret_cast<const uint4*>(row);  // 16-B aligned (host check)
     const int nvec = V / VEC;
     constexpr int kStep = 4 * NT;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();  // (probes 5 / 6: per-row phase times)
     const int nfull = (nvec / kStep) * kStep;
     uint4 cur[4], nxt[4];
     if (nfull > 0) {
@@ -1511,16 +1518,66 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         s_nt = 0u;
         s_cut_j = -1;
         s_zero[0] = s_zero[1] = 0u;
+        s_nc = 0u;
+        s_nbad = 0u;
+        s_ntie = 0u;
+        s_bar1 = -INFINITY;  // the workgroup's best exact score so far
     }
-    if constexpr (TOPP)
-        for (int j = threadIdx.x; j < 2 * kPHalf + kWave; j += NT) s_hist[j] = 0u;
+    for (int j = threadIdx.x; j < 2 * kPHalf + kWave; j += NT) s_hist[j] = 0u;
     __syncthreads();
 
     // ---- pass 1: the row max; top_p: the count histogram (one LDS add per element, no branch;
     //      elements outside the window take a uniform slow path), min_p: the raw lse
     float vmx = -INFINITY;
     bool bad = false;
-    float lm = -1e30f, ls = 0.f;  // (min_p alone) lagged online (max, sum-exp), as the top_k kernel
+    // The decision in the same pass: MODE 2's noise (group hash, group bound, exact noise_score)
+    // against the workgroup's bar = the best exact score computed so far (the unfiltered sampler's
+    // race over the whole row). Admissibility is unknown until the cut, so every element the bound
+    // lets through is scored exactly and recorded (s_cs / s_ci / s_ck); an element the bound skips
+    // scored below a record. After the cut, the best record is the row's decision when it is
+    // admissible (the unfiltered winner lies in the kept set: the filtered race's winner too) --
+    // the certificate, which holds with probability about the kept mass (>= top_p); rows without
+    // one take pass 2 (the re-read).
+    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
+    const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
+    const float temp = 1.0f / inv_t;
+    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    float thr1 = -INFINITY;  // (bar - C) T, wave-uniform
+    int seed_v = -1;         // this lane's seed element (scored once: no duplicate record)
+    auto record = [&](float sc, int v, uint32_t b) {
+        const uint32_t p = atomicAdd(&s_nc, 1u);
+        if (p < (uint32_t)kPCandCap) {
+            s_cs[p] = sc;
+            s_ci[p] = v;
+            s_ck[p] = (uint16_t)b;
+        }
+    };
+    auto bar_merge = [&](float best_new) {  // publish the wave's best new score, read the workgroup's
+        const float wb = wave_max_uniform(best_new);
+        if (lane == 0 && wb > -INFINITY)
+            __hip_atomic_fetch_max(&s_bar1, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        thr1 = (fmaxf(wb, uni(s_bar1)) - kNoiseC) * temp;
+    };
+    // the group bound and the exact scores of one group's elements (x[k] at v0 + k, raw bits b[k])
+    auto gumbel = [&](const float (&x)[VEC], const uint16_t (&b)[VEC], float vm, int v0, int cnt) {
+        const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+        const float bits = noise_bits(h);
+        const bool cand = !(fmaf(bits, -kT, vm) - thr1 < 0.f);
+        if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
+        float bn = -INFINITY;
+        if (cand) {
+            const float Eg = group_min_e(h);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (k < cnt && v0 + k != seed_v && !(fmaf(bits, -kT, x[k]) - thr1 < 0.f)) {
+                    const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
+                    record(sc, v0 + k, b[k]);
+                    bn = fmaxf(bn, sc);
+                }
+            }
+        }
+        bar_merge(bn);
+    };
     auto rare_elem = [&](uint32_t b) {  // an element outside the window (top_p)
         const uint32_t a = b & 0x7fffu;
         if (a == 0u) {
@@ -1532,7 +1589,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             bad |= !(b == 0xff80u || ((b & 0x8000u) && a < 0x7f80u));
         }
     };
-    auto visit1 = [&](const uint4& pk) {
+    auto visit1 = [&](const uint4& pk, int v0) {
         uint16_t raw[VEC];
         __builtin_memcpy(raw, &pk, 16);
         float x[VEC];
@@ -1542,7 +1599,8 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
 #pragma unroll
         for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, x[k]);
         vmx = fmaxf(vmx, vm);
-        if constexpr (TOPP) {
+        gumbel(x, raw, vm, v0, VEC);
+        {
             bool rare = false;
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
@@ -1560,23 +1618,31 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                     if (!((unsigned)wi < (unsigned)kPHalf)) rare_elem(raw[k]);
                 }
             }
-        } else {
-            if (vm > lm + 64.f) {
-                ls *= fast_exp2((lm - vm) * kLog2e);
-                lm = vm;
-            }
-            float acc = 0.f;
-            bool bb = false;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                acc += fast_exp2((x[k] - lm) * kLog2e);
-                bb |= ((raw[k] & 0x7f80u) == 0x7f80u) & (raw[k] != 0xff80u);  // NaN, +inf: fallback
-            }
-            ls += acc;
-            bad |= bb;
         }
     };
     if (nfull > 0) {
+        // the wave's first bar: each lane's exact score of the largest element of its first vector
+        {
+            uint16_t raw[VEC];
+            __builtin_memcpy(raw, &cur[0], 16);
+            float xb = bf16_to_f32(raw[0]);
+            int kb = 0;
+#pragma unroll
+            for (int k = 1; k < VEC; ++k) {
+                const float xk = bf16_to_f32(raw[k]);
+                kb = xk > xb ? k : kb;
+                xb = fmaxf(xb, xk);
+            }
+            const int vb = (int)threadIdx.x * VEC + kb;
+            const uint32_t h = ehash(key, keyb, (uint32_t)vb >> 3);
+            const float sc = noise_score(xb, inv_t, vb, h, group_min_e(h), key2);
+            uint16_t bb = raw[0];
+#pragma unroll
+            for (int k = 1; k < VEC; ++k) bb = k == kb ? raw[k] : bb;
+            record(sc, vb, bb);
+            seed_v = vb;
+            bar_merge(sc);
+        }
         for (int base = 0; base < nfull; base += kStep) {
             const bool more = base + kStep < nfull;
             switch (((nfull - base) * 4 - 1) / nfull) {  // progress priority, as the row-mode sampler
@@ -1590,7 +1656,10 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 for (int u = 0; u < 4; ++u) nxt[u] = rv[base + kStep + u * NT + threadIdx.x];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) visit1(cur[u]);
+            for (int u = 0; u < 4; ++u) {
+                visit1(cur[u], (base + u * NT + (int)threadIdx.x) * VEC);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             if (more) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
@@ -1598,37 +1667,39 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         __builtin_amdgcn_s_setprio(0);
     }
-    for (int i = nfull + threadIdx.x; i < nvec; i += NT) visit1(rv[i]);
+    for (int i0 = nfull; i0 < nvec; i0 += NT) {  // same trip count in every thread (wave ballots inside)
+        const int i = i0 + (int)threadIdx.x;
+        if (i < nvec) {
+            visit1(rv[i], i * VEC);
+        } else {  // an idle lane joins the ballots with nothing to score
+            const uint16_t nb[VEC] = {0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u};
+            const float nx[VEC] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            gumbel(nx, nb, -INFINITY, 0, 0);
+        }
+    }
+    if (nvec * VEC < V) {  // the ragged tail: one partial group, lanes 0 .. cnt-1 one element each
+        const int t0 = nvec * VEC, cnt = V - t0;
+        uint16_t tb[VEC];
+        float tx[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            tb[k] = threadIdx.x == 0 && k < cnt ? row[t0 + k] : (uint16_t)0xff80u;
+            tx[k] = bf16_to_f32(tb[k]);
+        }
+        float tm = tx[0];
+#pragma unroll
+        for (int k = 1; k < VEC; ++k) tm = fmaxf(tm, tx[k]);
+        gumbel(tx, tb, tm, t0, threadIdx.x == 0 ? cnt : 0);
+    }
     for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
         const uint16_t b = row[i];
         const float x = bf16_to_f32(b);
         vmx = fmaxf(vmx, x);
-        if constexpr (TOPP) {
-            const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
-            if ((unsigned)wi < (unsigned)kPHalf) atomicAdd(&s_hist[(b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi], 1u);
-            else rare_elem(b);
-        } else {
-            const float mn = fmaxf(lm, x);
-            ls = ls * fast_exp2((lm - mn) * kLog2e) + fast_exp2((x - mn) * kLog2e);
-            lm = mn;
-            bad |= ((b & 0x7f80u) == 0x7f80u) & (b != 0xff80u);
-        }
+        const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
+        if ((unsigned)wi < (unsigned)kPHalf) atomicAdd(&s_hist[(b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi], 1u);
+        else rare_elem(b);
     }
     vmx = wave_max(vmx);
-    if constexpr (!TOPP) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const float om = __shfl_xor(lm, off, kWave);
-            const float os = __shfl_xor(ls, off, kWave);
-            const float mn = fmaxf(lm, om);
-            ls = ls * fast_exp2((lm - mn) * kLog2e) + os * fast_exp2((om - mn) * kLog2e);
-            lm = mn;
-        }
-        if (lane == 0) {
-            s_lm[w] = lm;
-            s_ls[w] = ls;
-        }
-    }
     if (bad) s_bad = 1u;
     if (lane == 0) s_vmax[w] = vmx;
     __syncthreads();
@@ -1638,20 +1709,32 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     mx = uni(mx);
     const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
     const float mthr = uni(mx * inv_t + ln_min_p);
-    float lse = 0.f;
-    if constexpr (!TOPP) {
-        float M = s_lm[0], S = s_ls[0];
-#pragma unroll
-        for (int j = 1; j < NW; ++j) {
-            const float mn = fmaxf(M, s_lm[j]);
-            S = S * fast_exp2((M - mn) * kLog2e) + s_ls[j] * fast_exp2((s_lm[j] - mn) * kLog2e);
-            M = mn;
-        }
-        lse = M + fast_log2(S) * kLn2;
-    }
     if (probe == 1) return;  // timing probe (skyrl_tune topp_probe): pass 1 only
 
-    bool fb = s_bad != 0u || (TOPP && s_nslow > (uint32_t)kPSlowCap);  // block-uniform
+    bool fb = s_bad != 0u || s_nslow > (uint32_t)kPSlowCap;  // block-uniform
+    // the raw logits' sum-exp for the logprob, from the counts (another summation order than a
+    // streaming lse: equal to float rounding)
+    float lse = 0.f;
+    if (!fb) {
+        double se = 0.0;
+        auto sexp = [&](uint32_t bits, uint32_t n) {
+            if (n) se += (double)n * (double)fast_exp2((bf16_to_f32((uint16_t)bits) - mx) * kLog2e);
+        };
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int p8 = 8 * (int)threadIdx.x + q;
+            sexp((uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf + p8]);
+            sexp(0x8000u | (uint32_t)((kPE0 << 7) + p8), s_hist[kPHalf - 1 - p8]);
+        }
+        for (int i = threadIdx.x; i < (int)s_nslow; i += NT) sexp(s_slow[i], 1u);
+        if (threadIdx.x < 2) sexp(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
+        se = wave_sum(se);
+        if (lane == 0) s_wexp[w] = se;
+        __syncthreads();
+        double S = 0.0;
+        for (int j = 0; j < NW; ++j) S += s_wexp[j];
+        lse = mx + fast_log2((float)S) * kLn2;
+    }
 
     // ---- on chip (top_p): bin masses (once per bin, kept in registers), Z, the raw lse, the cut
     //      key and its tie count
@@ -1670,10 +1753,6 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             };
             unsigned long long pm[8], nm[8];
             unsigned long long pos = 0ull, neg = 0ull, mid = 0ull;
-            double se = 0.0;  // the raw logits' sum-exp (the logprob's lse) from the same counts
-            auto sexp = [&](uint32_t bits, uint32_t n) {
-                if (n) se += (double)n * (double)fast_exp2((bf16_to_f32((uint16_t)bits) - mx) * kLog2e);
-            };
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int p8 = 8 * (int)threadIdx.x + q;
@@ -1683,17 +1762,9 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 nm[q] = mass_of(nb, nc);
                 pos += pm[q];
                 neg += nm[q];
-                sexp(pb, pc);
-                sexp(nb, nc);
             }
-            for (int i = threadIdx.x; i < (int)s_nslow; i += NT) {
-                mid += mass_of(s_slow[i], 1u);
-                sexp(s_slow[i], 1u);
-            }
-            if (threadIdx.x < 2) {
-                mid += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
-                sexp(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
-            }
+            for (int i = threadIdx.x; i < (int)s_nslow; i += NT) mid += mass_of(s_slow[i], 1u);
+            if (threadIdx.x < 2) mid += mass_of(threadIdx.x ? 0x8000u : 0u, s_zero[threadIdx.x]);
             unsigned long long ip = pos, in = neg;
 #pragma unroll
             for (int off = 1; off < kWave; off <<= 1) {
@@ -1707,18 +1778,13 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             unsigned long long wm = mid;
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) wm += (unsigned long long)__shfl_xor((long long)wm, off, kWave);
-            se = wave_sum(se);
             if (lane == kWave - 1) {
                 s_wpos[w] = ip;
                 s_wneg[w] = in;
             }
-            if (lane == 0) {
-                s_woth[w] = wm;
-                s_wexp[w] = se;
-            }
+            if (lane == 0) s_woth[w] = wm;
             __syncthreads();
             unsigned long long offp = 0ull, offn = 0ull, Zp = 0ull, Zn = 0ull, Zm = 0ull;
-            double S = 0.0;
             for (int j = 0; j < NW; ++j) {
                 if (j < w) {
                     offp += s_wpos[j];
@@ -1727,9 +1793,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 Zp += s_wpos[j];
                 Zn += s_wneg[j];
                 Zm += s_woth[j];
-                S += s_wexp[j];
             }
-            lse = mx + fast_log2((float)S) * kLn2;
             const double target = (double)top_p * (double)(Zp + Zm + Zn);
             // the cut: the bin where the mass before it is < p Z and the mass through it reaches it (the
             // first weighted bin also when target <= 0: top_p = 0 keeps the top token, as filter_row's
@@ -1807,10 +1871,62 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         xlo = uni(from_key<T>(hi));
     }
-    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
-    const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
-    const float temp = 1.0f / inv_t;
-    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    // ---- pass 1's decision: the best admissible record e*, certified when no record beats it (no
+    //      inadmissible one, no unranked element of a split cut key): an element the bound skipped
+    //      scored below a record, so below e*; otherwise pass 2 decides
+    {
+        const int nc = (int)min(s_nc, (uint32_t)kPCandCap);
+        const bool complete = s_nc <= (uint32_t)kPCandCap;
+        auto cls = [&](int i) -> int {  // 1 admissible, 0 inadmissible, 2 an element of the split cut key
+            const uint32_t kk = okey_bf16(s_ck[i]);
+            if constexpr (TOPP) {
+                if (kk > kc || (!split && kk == kc)) return 1;
+                return (split && kk == kc) ? 2 : 0;
+            } else {
+                return bf16_to_f32(s_ck[i]) >= xlo ? 1 : 0;
+            }
+        };
+        Best e{-INFINITY, 0x7fffffff};
+        for (int i = threadIdx.x; i < nc; i += NT)
+            if (cls(i) == 1 && better(s_cs[i], s_ci[i], e)) e = Best{s_cs[i], s_ci[i]};
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float os = __shfl_xor(e.score, off, kWave);
+            const int oi = __shfl_xor(e.idx, off, kWave);
+            if (better(os, oi, e)) e = Best{os, oi};
+        }
+        if (lane == 0) {
+            s_bs[w] = e.score;
+            s_bi[w] = e.idx;
+        }
+        __syncthreads();
+        Best es{s_bs[0], s_bi[0]};
+        for (int j = 1; j < NW; ++j)
+            if (better(s_bs[j], s_bi[j], es)) es = Best{s_bs[j], s_bi[j]};
+        uint32_t nbad = 0u, ntie = 0u;
+        for (int i = threadIdx.x; i < nc; i += NT) {
+            if (better(s_cs[i], s_ci[i], es)) {
+                const int cl = cls(i);
+                nbad += cl == 0 ? 1u : 0u;
+                ntie += cl == 2 ? 1u : 0u;
+            }
+        }
+        if (nbad) atomicAdd(&s_nbad, nbad);
+        if (ntie) atomicAdd(&s_ntie, ntie);
+        __syncthreads();
+        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && s_ntie == 0u && s_nbad == 0u;
+        if (certified) {
+            if (threadIdx.x == 0) {
+                tokens[row_i] = es.idx;
+                if (logp_out) logp_out[row_i] = to_f<T>(row[es.idx]) - lse;
+                // (tk = 1: decided in pass 1; ic unresolved: not needed)
+                filt[row_i] = RowFilter{mx, 1u, kRowDone, kc, split ? -1 : ic};
+            }
+            return;
+        }
+        __syncthreads();  // s_bs reused below
+    }
+    const uint64_t t_p2 = __builtin_amdgcn_s_memrealtime();
     float thr = -INFINITY, bar = -INFINITY;
     float best_s = -INFINITY;
     int best_i = 0x7fffffff;
@@ -2009,6 +2125,10 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         if (logp_out)
             logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - lse : __builtin_nanf("");
         filt[row_i] = RowFilter{mx, 0u, kRowDone, kc, icut};
+        if (probe >= 5) {  // timing probes: pass 2's and the row's time before it, 10-ns ticks
+            tokens[row_i] = (int)(__builtin_amdgcn_s_memrealtime() - t_p2);
+            if (logp_out) logp_out[row_i] = (float)(t_p2 - t_start);
+        }
     }
     return;
     }

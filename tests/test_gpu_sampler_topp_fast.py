@@ -2,9 +2,11 @@
 against the two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
 skyrl_tune("sampler_topp_fast", 0)) and against oracle/sampler_ref.c.
 
-The kernel takes the row max in pass 1 with a count histogram per exact bf16 key, finds the top_p
-cut on chip, and decides in pass 2 (MODE 2 over the keys above the cut, the cut key's elements
-ranked by index). Tokens, logprobs and the recorded cut (key, last kept index) must be the
+The kernel takes the row max in pass 1 with a count histogram per exact bf16 key and scores every
+element MODE 2's group bound lets through against a per-wave bar (the 8th best score); it finds the
+top_p cut on chip and decides from those records when a certificate holds (fewer than 8
+inadmissible records beat the best admissible one, none of them an unranked element of a split cut
+key), else in pass 2 (MODE 2 over the keys above the cut, the cut key's elements ranked by index). Tokens, logprobs and the recorded cut (key, last kept index) must be the
 two-kernel path's bit for bit. Rows outside its bounds (the cut among the values below 2^-16 or the
 zeros, a tie group over 1024 at the cut, NaN / +inf, values >= 2^16, over 512 nonzero values below
 2^-16) run the
@@ -48,8 +50,11 @@ def _ab(x, min_done, **kw):
     assert torch.allclose(lf, ls, atol=2e-5, rtol=1e-5, equal_nan=True), (kw, (lf - ls).abs().max())
     done = ff[:, 2] == _ROW_DONE
     assert bool(((ff[:, 2] == _ROW_DONE) | (ff[:, 2] == _ROW_FALLBACK)).all())
-    if kw.get("top_p", 1.0) < 1.0:  # the cut (key, last kept index) of every row the kernel decided
-        assert torch.equal(ff[done][:, 3], fs[done][:, 3]) and torch.equal(ff[done][:, 4], fs[done][:, 4])
+    if kw.get("top_p", 1.0) < 1.0:  # the cut (key, and the last kept index where the kernel resolved it:
+        # -1 = a split tie group that pass 1's certified decision did not need to rank) of every row
+        assert torch.equal(ff[done][:, 3], fs[done][:, 3])
+        rk = done & (ff[:, 4] != -1)
+        assert torch.equal(ff[rk][:, 4], fs[rk][:, 4])
     assert int(done.sum()) >= min_done, (kw, int(done.sum()), x.shape[0])
     return tf, lf, int(done.sum())
 
