@@ -43,24 +43,28 @@ def main():
         ops._ffi.call("skyrl_tune", b"topp_probe", 0)
         ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1, tokens_out=tok, logp_out=lp, **kw)
         ws = ops.WORKSPACES.get(dev, "sample", ops._ffi.query("skyrl_sample_workspace_bytes", n, V))
-        ff = ws[1280:1280 + 20 * n].view(torch.int32).view(n, 5).cpu()
+        ff = ws[1024:1024 + 20 * n].view(torch.int32).view(n, 5).cpu()
         res["pass1_decided"] = int((ff[:, 1] == 1).sum())  # RowFilter.tk = 1: certified in pass 1
-        res["chunked_pass2"] = int((ff[:, 1] == 2).sum())  # RowFilter.tk = 2: decided by the chunked pass 2
-        ops._ffi.call("skyrl_tune", b"topp_probe", 5)  # every row through the chunked pass 2
-        res["all_chunked_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
-                                                         tokens_out=tok, logp_out=lp, **kw))
+        for probe in (5, 6):  # per-row pass-2 time (5: every row takes pass 2; 6: the rows that do)
+            ops._ffi.call("skyrl_tune", b"topp_probe", probe)
+            tok.fill_(-1)
+            ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1, tokens_out=tok, logp_out=lp, **kw)
+            ff = ws[1024:1024 + 20 * n].view(torch.int32).view(n, 5).cpu()
+            p2 = tok.cpu()[ff[:, 1] != 1].float() / 100.0  # us
+            pre = lp.cpu()[ff[:, 1] != 1].float() / 100.0
+            if p2.numel():
+                res[f"probe{probe}_rows"] = int(p2.numel())
+                res[f"probe{probe}_pass2_us"] = [round(float(p2.min()), 2), round(float(p2.median()), 2), round(float(p2.max()), 2)]
+                res[f"probe{probe}_before_us"] = [round(float(pre.min()), 2), round(float(pre.median()), 2), round(float(pre.max()), 2)]
         ops._ffi.call("skyrl_tune", b"topp_probe", 0)
-        for hp in (0, 64):
-            ops._ffi.call("skyrl_tune", b"topp_helpers", hp)
-            res[f"helpers{hp}_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
-                                                             tokens_out=tok, logp_out=lp, **kw))
-        ops._ffi.call("skyrl_tune", b"topp_helpers", 256)
-        steps = []
-        for st in range(2, 12):  # fresh noise per decode step (the rows pass 1 cannot decide vary)
+        steps, dec = [], []
+        for st in range(2, 22):  # fresh noise per decode step: how many rows pass 1 leaves varies
             steps.append(timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=st, tokens_out=tok,
                                                   logp_out=lp, **kw), reps=5))
-        res["steps_2_11_us"] = [min(steps), round(sum(steps) / len(steps), 2), max(steps)]
-        ops._ffi.call("skyrl_tune", b"topp_probe", 0)
+            ws = ops.WORKSPACES.get(dev, "sample", ops._ffi.query("skyrl_sample_workspace_bytes", n, V))
+            dec.append(int((ws[1024:1024 + 20 * n].view(torch.int32).view(n, 5)[:, 1] == 1).sum()))
+        res["steps_2_21_us"] = [min(steps), round(sum(steps) / len(steps), 2), max(steps)]
+        res["steps_2_21_rows_left"] = [n - d for d in dec]
         ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 0)
         res["two_kernel_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
                                                         tokens_out=tok, logp_out=lp, **kw), reps=10)

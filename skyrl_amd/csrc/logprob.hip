@@ -224,7 +224,6 @@ extern int g_sampler_row;
 extern int g_sampler_topk_fast;
 extern int g_sampler_topp_fast;
 extern int g_probe_topp;
-extern int g_topp_helpers;
 extern int g_attn_pf;
 int lmhead_tune(int value);
 int lmhead_group_tune(int value);
@@ -297,13 +296,8 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "topp_probe") {
-        SKYRL_REQUIRE(value >= 0 && value <= 5, "skyrl_tune: topp_probe must be 0 .. 5");
+        SKYRL_REQUIRE(value >= 0 && value <= 6, "skyrl_tune: topp_probe must be 0 .. 6");
         g_probe_topp = value;
-        return SKYRL_OK;
-    }
-    if (k == "topp_helpers") {
-        SKYRL_REQUIRE(value >= 0 && value <= 4096, "skyrl_tune: topp_helpers must be 0 .. 4096");
-        g_topp_helpers = value;
         return SKYRL_OK;
     }
     if (k == "sampler_topp_fast") {

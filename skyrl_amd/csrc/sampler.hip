@@ -32,9 +32,7 @@ namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
 int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
-int g_probe_topp = 0;  // skyrl_tune("topp_probe"): timing only, tokens invalid: 1 pass 1 alone, 2 pass 1 + the cut,
-                       // 3 / 4 + a bare re-read; 5: valid tokens, every row through the chunked pass 2
-int g_topp_helpers = 256;  // skyrl_tune("topp_helpers"): extra workgroups of the top_p kernel's chunked pass 2
+int g_probe_topp = 0;  // skyrl_tune("topp_probe"): timing only, tokens invalid: 1 pass 1 alone, 2 pass 1 + the cut
 namespace {
 
 constexpr int kThreads = 256;
@@ -44,7 +42,7 @@ constexpr int kRowModeMinSeqs = 256;  // enough rows to fill the chip with one w
 // batch size and never overlap another call's row filters or partials in a reused workspace (a
 // split-mode call after one with fewer rows would otherwise read that call's partials as
 // counters): every counter is zero at allocation and re-armed by its user.
-constexpr size_t kCounterBytes = (size_t)kRowModeMinSeqs * 4 + 256;  // + the top_p kernel's ToppCtl
+constexpr size_t kCounterBytes = (size_t)kRowModeMinSeqs * 4;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -1471,63 +1469,16 @@ constexpr int kPHalf = 4096;    // keys per sign in the window
 constexpr int kPSlowCap = 512;  // elements below the window
 constexpr int kPTieCap = 1024;  // elements at a split cut key
 constexpr int kPCandCap = 2048; // pass 1's exactly scored elements (seeds + bound survivors)
+constexpr float kCertDelta = 5.f;  // pass 1's recording margin below the bar (score units)
 
 // uniform (scalar) copy of a wave-uniform float, so the hot loops keep it in an SGPR
 __device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-
-// Pass 2 of the rows pass 1 does not decide runs in chunks of the row that any workgroup of the
-// launch may take (the row's own after publishing it, rows' workgroups done with their own,
-// and kPHelpers extra workgroups the dispatcher starts as slots free up), so that a few such rows
-// cost a few microseconds of the whole chip, not one CU's latency-bound re-read of the row. The
-// workgroup that completes a row's last chunk merges the chunks' bests and ranks the cut key's
-// ties. No workgroup waits for another to start: a row's owner takes its own chunks, helpers only
-// take chunks already published, and the last arriver (not a waiting owner) decides.
-constexpr int kPChunks = 32;  // (<= kWave: the merge reads one part per lane)
-constexpr int kPHelpers = 256;
-constexpr uint64_t kHelpIdleTicks = 2000;  // 20 us (100 MHz clock) with no row deciding: helpers leave
-struct ToppRowState {  // what the chunked pass 2 needs of a published row
-    float xlo, xc, lse, mx;  // admissibility bound, the cut key's value, the raw lse, the raw max
-    float e_s;               // e*: the best admissible element pass 1 scored (a lower bound)
-    int e_i;
-    uint32_t kc;
-    int split;
-    long long c;             // the split cut key's kept tie ranks
-    int nch, pad;
-};
-static_assert(sizeof(ToppRowState) % 4 == 0, "word copies");
-struct ToppRowWs {
-    ToppRowState st;
-    uint32_t claim, done, nt, pad;
-    Best part[kPChunks];  // (parts and ties: agent-scope stores and loads)
-    int32_t tidx[kPTieCap];
-};
-struct ToppCtl {  // launch-wide words at a fixed workspace offset: zero at allocation, re-armed by
-                  // the launch's last workgroup
-    uint32_t qn, decided, finished, head;  // head: queue entries below it have no chunk left to claim
-};
-__device__ __forceinline__ int topp_nchunks(int nvec) { return max(1, min(kPChunks, (nvec + 1023) / 1024)); }
-__device__ __forceinline__ uint32_t g_add(uint32_t* p, uint32_t v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t g_ld(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void g_st(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t g_ld64(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void g_st64(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <typename T, bool TOPP>
 __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topp_kernel(
     const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, float top_p,
     uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
-    float* __restrict__ logp_out, RowFilter* __restrict__ filt, int probe, int nseq, ToppCtl* __restrict__ ctl,
-    uint64_t* __restrict__ queue, ToppRowWs* __restrict__ rws, uint32_t epoch) {
+    float* __restrict__ logp_out, RowFilter* __restrict__ filt, int probe) {
     static_assert(sizeof(T) == 2, "bf16 rows");
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
     constexpr int kDummy = 2 * kPHalf;  // 64 words taking the out-of-window elements' increments (no branch)
@@ -1543,28 +1494,20 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     __shared__ float s_cs[kPCandCap];     // pass 1's exactly scored elements: score, index, key
     __shared__ int32_t s_ci[kPCandCap];
     __shared__ uint16_t s_ck[kPCandCap];
-    __shared__ uint32_t s_nc, s_nbad, s_ntie;
+    __shared__ uint32_t s_nc, s_ntie;
+    __shared__ float s_dmin;
     __shared__ float s_bar1;
     __shared__ float s_bs[NW];
     __shared__ int32_t s_bi[NW];
     __shared__ int s_icut;
     __shared__ RowFilter s_rf;
-    // (the chunked pass 2's block-uniform words reuse the cut's per-wave sums: LDS stays under 64 KB)
-    static_assert(sizeof(ToppRowState) <= sizeof(s_wpos) && 4 * sizeof(uint32_t) <= sizeof(s_woth), "LDS reuse");
-    uint32_t* const s_q = reinterpret_cast<uint32_t*>(s_woth);
-    ToppRowState& s_st = *reinterpret_cast<ToppRowState*>(s_wpos);
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    const int nvec = V / VEC;
-    const float temp = 1.0f / inv_t;
-    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-
-    // ---- a row's workgroup: pass 1, the cut, the decision when pass 1 certifies it; returns 1 when
-    //      the row is published for the chunked pass 2 below
-    auto row_part = [&]() -> int {
     const int row_i = blockIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
     const T* row = logits + (int64_t)row_i * ld;
     const uint4* rv = reinterpret_cast<const uint4*>(row);  // 16-B aligned (host check)
+    const int nvec = V / VEC;
     constexpr int kStep = 4 * NT;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();  // (probes 5 / 6: per-row phase times)
     const int nfull = (nvec / kStep) * kStep;
     uint4 cur[4], nxt[4];
     if (nfull > 0) {
@@ -1578,7 +1521,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         s_cut_j = -1;
         s_zero[0] = s_zero[1] = 0u;
         s_nc = 0u;
-        s_nbad = 0u;
+        s_dmin = kCertDelta;
         s_ntie = 0u;
         s_bar1 = -INFINITY;  // the workgroup's best exact score so far
     }
@@ -1591,15 +1534,21 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     bool bad = false;
     // The decision in the same pass: MODE 2's noise (group hash, group bound, exact noise_score)
     // against the workgroup's bar = the best exact score computed so far (the unfiltered sampler's
-    // race over the whole row). Admissibility is unknown until the cut, so every element the bound
-    // lets through is scored exactly and recorded (s_cs / s_ci / s_ck); an element the bound skips
-    // scored below a record. After the cut, the best record is the row's decision when it is
-    // admissible (the unfiltered winner lies in the kept set: the filtered race's winner too) --
-    // the certificate, which holds with probability about the kept mass (>= top_p); rows without
-    // one take pass 2 (the re-read).
+    // race over the whole row), lowered by a margin delta. Admissibility is unknown until the cut,
+    // so every element the bound lets through is scored exactly and recorded (s_cs / s_ci / s_ck);
+    // an element the bound skips scored below (bar - delta) at its visit, so below (final bar -
+    // final delta): the margin only shrinks (5 while the record list is under half full, then 3,
+    // 1.5, 0), per wave. After the cut, the best admissible record e* is the row's decision when its
+    // score is at least (final bar - the smallest final delta) and no unranked element of a split
+    // cut key beats it -- the certificate. It fails when the filtered race's winner trails the
+    // unfiltered one by more than delta: probability about (1 - kept mass) e^-delta (under 4e-4 of
+    // the rows at top_p 0.95); those rows take pass 2 (the re-read).
     const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
     const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
-    float thr1 = -INFINITY;  // (bar - C) T, wave-uniform
+    const float temp = 1.0f / inv_t;
+    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    float thr1 = -INFINITY;  // (bar - delta - C) T, wave-uniform
+    float delta = kCertDelta;
     int seed_v = -1;         // this lane's seed element (scored once: no duplicate record)
     auto record = [&](float sc, int v, uint32_t b) {
         const uint32_t p = atomicAdd(&s_nc, 1u);
@@ -1613,7 +1562,10 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         const float wb = wave_max_uniform(best_new);
         if (lane == 0 && wb > -INFINITY)
             __hip_atomic_fetch_max(&s_bar1, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        thr1 = (fmaxf(wb, uni(s_bar1)) - kNoiseC) * temp;
+        const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_nc);
+        delta = fminf(delta, n < (uint32_t)kPCandCap / 2 ? kCertDelta : n < (uint32_t)kPCandCap * 3 / 4 ? 3.f
+                                                        : n < (uint32_t)kPCandCap * 15 / 16 ? 1.5f : 0.f);
+        thr1 = (fmaxf(wb, uni(s_bar1)) - delta - kNoiseC) * temp;
     };
     // the group bound and the exact scores of one group's elements (x[k] at v0 + k, raw bits b[k])
     auto gumbel = [&](const float (&x)[VEC], const uint16_t (&b)[VEC], float vm, int v0, int cnt) {
@@ -1758,6 +1710,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     vmx = wave_max(vmx);
     if (bad) s_bad = 1u;
+    if (lane == 0) __hip_atomic_fetch_min(&s_dmin, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (lane == 0) s_vmax[w] = vmx;
     __syncthreads();
     float mx = s_vmax[0];
@@ -1766,7 +1719,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     mx = uni(mx);
     const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
     const float mthr = uni(mx * inv_t + ln_min_p);
-    if (probe == 1) return 0;  // timing probe (skyrl_tune topp_probe): pass 1 only
+    if (probe == 1) return;  // timing probe (skyrl_tune topp_probe): pass 1 only
 
     bool fb = s_bad != 0u || s_nslow > (uint32_t)kPSlowCap;  // block-uniform
     // the raw logits' sum-exp for the logprob, from the counts (another summation order than a
@@ -1906,25 +1859,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     lse = uni(lse);
     if (!fb) {  // (the fallback's call site stays after the hot loops: the register allocation of
                 // the passes does not see it)
-    if (probe == 2) return 0;  // timing probe: pass 1 + the cut
-    if (probe == 3) {  // timing probe: pass 2's re-read alone (loads consumed by an xor)
-        uint32_t acc = 0u;
-        for (int i = threadIdx.x; i < nvec; i += NT) {
-            const uint4 v = ld_stream(rv + i);
-            acc ^= v.x ^ v.y ^ v.z ^ v.w;
-        }
-        if (acc == 0x12345678u) tokens[row_i] = -7;
-        return 0;
-    }
-    if (probe == 4) {  // timing probe: the same re-read with cached loads
-        uint32_t acc = 0u;
-        for (int i = threadIdx.x; i < nvec; i += NT) {
-            const uint4 v = rv[i];
-            acc ^= v.x ^ v.y ^ v.z ^ v.w;
-        }
-        if (acc == 0x12345678u) tokens[row_i] = -7;
-        return 0;
-    }
+    if (probe == 2) return;  // timing probe: pass 1 + the cut
 
     // ---- pass 2: the Gumbel-max decision (MODE 2's noise, group bound and exact scores) over the
     //      admissible elements x >= xlo: top_p, the value above the cut key when the cut splits its
@@ -1946,9 +1881,9 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         xlo = uni(from_key<T>(hi));
     }
-    // ---- pass 1's decision: the best admissible record e*, certified when no record beats it (no
-    //      inadmissible one, no unranked element of a split cut key): an element the bound skipped
-    //      scored below a record, so below e*; otherwise pass 2 decides
+    // ---- pass 1's decision: the best admissible record e*, certified when its score is at least
+    //      (final bar - smallest final delta) and no unranked element of a split cut key beats it:
+    //      an element the bound skipped scored below that, so below e*; otherwise pass 2 decides
     {
         const int nc = (int)min(s_nc, (uint32_t)kPCandCap);
         const bool complete = s_nc <= (uint32_t)kPCandCap;
@@ -1978,18 +1913,13 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         Best es{s_bs[0], s_bi[0]};
         for (int j = 1; j < NW; ++j)
             if (better(s_bs[j], s_bi[j], es)) es = Best{s_bs[j], s_bi[j]};
-        uint32_t nbad = 0u, ntie = 0u;
-        for (int i = threadIdx.x; i < nc; i += NT) {
-            if (better(s_cs[i], s_ci[i], es)) {
-                const int cl = cls(i);
-                nbad += cl == 0 ? 1u : 0u;
-                ntie += cl == 2 ? 1u : 0u;
-            }
-        }
-        if (nbad) atomicAdd(&s_nbad, nbad);
+        uint32_t ntie = 0u;
+        if (TOPP && split)
+            for (int i = threadIdx.x; i < nc; i += NT) ntie += (better(s_cs[i], s_ci[i], es) && cls(i) == 2) ? 1u : 0u;
         if (ntie) atomicAdd(&s_ntie, ntie);
         __syncthreads();
-        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && s_ntie == 0u && s_nbad == 0u;
+        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && s_ntie == 0u &&
+                               es.score >= s_bar1 - s_dmin;
         if (certified) {
             if (threadIdx.x == 0) {
                 tokens[row_i] = es.idx;
@@ -1997,294 +1927,229 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 // (tk = 1: decided in pass 1; ic unresolved: not needed)
                 filt[row_i] = RowFilter{mx, 1u, kRowDone, kc, split ? -1 : ic};
             }
-            return 0;
+            return;
         }
-        // not decided: publish the row for the chunked pass 2 (any workgroup of the launch takes
-        // chunks; the one that completes the last decides)
-        if (threadIdx.x == 0) {  // (agent-scope stores and loads throughout: the L2s of the XCDs are
-                                 // not coherent with each other for plain accesses)
-            ToppRowWs* q = rws + row_i;
-            const ToppRowState st{xlo, xc, lse, mx, es.score, es.idx, kc, split ? 1 : 0, c, topp_nchunks(nvec), 0};
-            uint32_t wd[sizeof(ToppRowState) / 4];
-            __builtin_memcpy(wd, &st, sizeof(st));
-            for (int j = 0; j < (int)(sizeof(ToppRowState) / 4); ++j) g_st(reinterpret_cast<uint32_t*>(&q->st) + j, wd[j]);
-            g_st(&q->claim, 0u);
-            g_st(&q->done, 0u);
-            g_st(&q->nt, 0u);
-            __threadfence();  // (release: the state before the queue entry)
-            const uint32_t slot = g_add(&ctl->qn, 1u);
-            g_st64(queue + slot, ((uint64_t)epoch << 32) | (uint32_t)row_i);
-        }
-        return 1;
+        __syncthreads();  // s_bs reused below
     }
+    const uint64_t t_p2 = __builtin_amdgcn_s_memrealtime();
+    float thr = -INFINITY, bar = -INFINITY;
+    float best_s = -INFINITY;
+    int best_i = 0x7fffffff;
+    if (threadIdx.x == 0) s_bar = -INFINITY;
+    auto adm = [&](float x) -> bool { return x >= xlo; };
+    auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
+        const float wb = wave_max_uniform(best_s);
+        if (lane == 0 && wb > -INFINITY)
+            __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bar = fmaxf(wb, uni(s_bar));
+        thr = (bar - kNoiseC) * temp;
+    };
+    // one vector of up to VEC elements at v0 (one noise group; padding slots are -inf); a vector
+    // without admissible elements in the whole wave costs no hash
+    auto visit2 = [&](const uint4& pk, int v0) {
+        uint16_t raw[VEC];
+        __builtin_memcpy(raw, &pk, 16);
+        float x[VEC];
+        float xm = -INFINITY;
+        bool anyt = false;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            x[k] = bf16_to_f32(raw[k]);
+            xm = fmaxf(xm, adm(x[k]) ? x[k] : -INFINITY);
+            if constexpr (TOPP) anyt |= x[k] == xc;  // (gated by split at the ballot)
+        }
+        if constexpr (TOPP) {
+            if (split && __builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    if (x[k] == xc) {
+                        const uint32_t p = atomicAdd(&s_nt, 1u);
+                        if (p < (uint32_t)kPTieCap) s_tidx[p] = v0 + k;
+                    }
+                }
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(xm > -INFINITY) == 0) return;
+        const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+        const float bits = noise_bits(h);
+        const bool cand = !(fmaf(bits, -kT, xm) - thr < 0.f);
+        if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
+        if (cand) {
+            const float Eg = group_min_e(h);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (adm(x[k]) && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
+                    const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
+                    if (sc > best_s) {  // ascending index within the lane: the lowest wins ties
+                        best_s = sc;
+                        best_i = v0 + k;
+                    }
+                }
+            }
+        }
+        raise_bar();
+    };
+    constexpr uint32_t kPadNinf = 0xff80ff80u;  // -inf bf16 pairs: never admissible, never a tie
+    if (probe == 3) {  // timing probe: pass 2's re-read alone (loads consumed by an xor)
+        uint32_t acc = 0u;
+        for (int i = threadIdx.x; i < nvec; i += NT) {
+            const uint4 v = ld_stream(rv + i);
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        if (acc == 0x12345678u) tokens[row_i] = -7;
+        return;
+    }
+    if (probe == 4) {  // timing probe: the same re-read with cached loads
+        uint32_t acc = 0u;
+        for (int i = threadIdx.x; i < nvec; i += NT) {
+            const uint4 v = rv[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        if (acc == 0x12345678u) tokens[row_i] = -7;
+        return;
+    }
+    // pass 2's stream: kP2Depth stages of 4 NT vectors, each refilled right after it is visited, so
+    // that (kP2Depth - 1) x 4 loads per lane stay in flight (a row re-read alone on its CU at the end
+    // of the launch is latency-bound; cached loads: the row is in the Infinity Cache)
+    constexpr int kP2Depth = 4;
+    const int nit = nfull / kStep;
+    uint4 stg[kP2Depth][4];
+#pragma unroll
+    for (int d = 0; d < kP2Depth; ++d)
+        if (d < nit) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) stg[d][u] = rv[d * kStep + u * NT + threadIdx.x];
+        }
+    __syncthreads();  // s_bar
+    if (nfull > 0) {
+        // the bar from this lane's first two vectors (one exact score: the best admissible element)
+        float xb = -INFINITY;
+        int vb = -1;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            uint16_t raw[VEC];
+            __builtin_memcpy(raw, &stg[0][u], 16);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const float x = bf16_to_f32(raw[k]);
+                if (adm(x) && x > xb) {
+                    xb = x;
+                    vb = (u * NT + (int)threadIdx.x) * VEC + k;
+                }
+            }
+        }
+        if (vb >= 0) {
+            const uint32_t h = ehash(key, keyb, (uint32_t)vb >> 3);
+            best_s = noise_score(xb, inv_t, vb, h, group_min_e(h), key2);
+            best_i = vb;
+        }
+        raise_bar();
+        __syncthreads();
+        bar = fmaxf(bar, uni(s_bar));
+        thr = (bar - kNoiseC) * temp;
+        for (int it0 = 0; it0 < nit; it0 += kP2Depth) {
+            switch (((nit - it0) * 4 - 1) / nit) {
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+#pragma unroll
+            for (int d = 0; d < kP2Depth; ++d) {  // stage d in place (no register rotation: a move
+                const int it = it0 + d;           // would wait for the loads in flight)
+                if (it < nit) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        visit2(stg[d][u], (it * kStep + u * NT + (int)threadIdx.x) * VEC);
+                        __builtin_amdgcn_sched_barrier(0);  // one vector's temporaries at a time
+                    }
+                    if (it + kP2Depth < nit) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) stg[d][u] = rv[(it + kP2Depth) * kStep + u * NT + threadIdx.x];
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+    }
+    // the rest: whole vectors (same trip count in every thread: the wave ballots inside), then the
+    // ragged tail's partial group, read element-wise by thread 0
+    for (int i0 = nfull; i0 < nvec; i0 += NT) {
+        const int i = i0 + (int)threadIdx.x;
+        visit2(i < nvec ? rv[i] : make_uint4(kPadNinf, kPadNinf, kPadNinf, kPadNinf), i * VEC);
+    }
+    if (nvec * VEC < V) {
+        const int t0 = nvec * VEC, cnt = V - t0;
+        uint16_t t[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) t[k] = (threadIdx.x == 0 && k < cnt) ? row[t0 + k] : (uint16_t)0xff80u;
+        uint4 pk;
+        __builtin_memcpy(&pk, t, 16);
+        visit2(pk, t0);
+    }
+    // the best admissible element: lanes, waves; then the cut key's kept ties
+    Best best{best_s, best_i};
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(best.score, off, kWave);
+        const int oi = __shfl_xor(best.idx, off, kWave);
+        if (better(os, oi, best)) best = Best{os, oi};
+    }
+    if (lane == 0) {
+        s_bs[w] = best.score;
+        s_bi[w] = best.idx;
+    }
+    __syncthreads();
+    Best b{s_bs[0], s_bi[0]};
+    for (int j = 1; j < NW; ++j)
+        if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
+    int icut = ic;
+    if (TOPP && split) {  // rank kc's elements by index: the first c are admissible, scored exactly here
+        const int n = (int)min(s_nt, (uint32_t)kPTieCap);
+        Best tb{-INFINITY, 0x7fffffff};
+        for (int i = threadIdx.x; i < n; i += NT) {
+            const int ii = s_tidx[i];
+            int r = 0;
+            for (int j = 0; j < n; ++j) r += s_tidx[j] < ii ? 1 : 0;
+            if (r < c) {
+                const uint32_t h = ehash(key, keyb, (uint32_t)ii >> 3);
+                const float sc = noise_score(xc, inv_t, ii, h, group_min_e(h), key2);
+                if (better(sc, ii, tb)) tb = Best{sc, ii};
+            }
+            if (r == c - 1) s_icut = ii;  // the cut's last kept index (filter_row's ic)
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float os = __shfl_xor(tb.score, off, kWave);
+            const int oi = __shfl_xor(tb.idx, off, kWave);
+            if (better(os, oi, tb)) tb = Best{os, oi};
+        }
+        __syncthreads();
+        if (lane == 0) {
+            s_bs[w] = tb.score;
+            s_bi[w] = tb.idx;
+        }
+        __syncthreads();
+        for (int j = 0; j < NW; ++j)
+            if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
+        icut = s_icut;
+    }
+    if (threadIdx.x == 0) {
+        tokens[row_i] = b.idx;
+        if (logp_out)
+            logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - lse : __builtin_nanf("");
+        filt[row_i] = RowFilter{mx, 0u, kRowDone, kc, icut};
+        if (probe >= 5) {  // timing probes: pass 2's and the row's time before it, 10-ns ticks
+            tokens[row_i] = (int)(__builtin_amdgcn_s_memrealtime() - t_p2);
+            if (logp_out) logp_out[row_i] = (float)(t_p2 - t_start);
+        }
+    }
+    return;
     }
     // the two-kernel path's code in this workgroup (one call site)
     topk_fallback<T>(logits, ld, V, 0, inv_t, use_minp, ln_min_p, TOPP ? 1 : 0, top_p, seed, seq_ids, step, tokens,
                      logp_out, &s_rf, row_i);
     if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
-    return 0;
-    };  // row_part
-
-    const bool is_row = (int)blockIdx.x < nseq;
-    int pub = 0;
-    if (is_row) {
-        pub = row_part();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            g_add(&ctl->decided, 1u);
-        }
-    }
-
-    // ---- the chunked pass 2 of published rows: sample_unit's MODE 2 over the admissible elements
-    //      x >= xlo of a chunk of vectors, bar and best starting from e*; the split cut key's
-    //      elements (value xc) into the row's tie list (indices)
-    auto merge = [&](int r, ToppRowWs* q, const ToppRowState& st, uint32_t rkey, uint32_t rkeyb, uint32_t rkey2) {
-        if (threadIdx.x == 0) {
-            __threadfence();  // (acquire: every chunk's part and ties)
-            s_q[2] = min(g_ld(&q->nt), (uint32_t)kPTieCap);
-        }
-        __syncthreads();
-        Best b{-INFINITY, 0x7fffffff};
-        if (w == 0) {  // the chunks' bests, one lane each (kPChunks <= kWave)
-            if (lane < st.nch)
-                b = Best{__uint_as_float(g_ld(reinterpret_cast<const uint32_t*>(&q->part[lane].score))),
-                         (int)g_ld(reinterpret_cast<const uint32_t*>(&q->part[lane].idx))};
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const float os = __shfl_xor(b.score, off, kWave);
-                const int oi = __shfl_xor(b.idx, off, kWave);
-                if (better(os, oi, b)) b = Best{os, oi};
-            }
-        }
-        int icut = st.split ? -1 : 0x7fffffff;
-        if (st.split) {  // rank kc's elements by index: the first c are admissible, scored exactly here
-            const int n = (int)s_q[2];
-            for (int i = threadIdx.x; i < n; i += NT) s_tidx[i] = (int32_t)g_ld(reinterpret_cast<const uint32_t*>(q->tidx + i));
-            if (threadIdx.x == 0) s_icut = -1;
-            __syncthreads();
-            Best tb{-INFINITY, 0x7fffffff};
-            for (int i = threadIdx.x; i < n; i += NT) {
-                const int ii = s_tidx[i];
-                int rk = 0;
-                for (int j = 0; j < n; ++j) rk += s_tidx[j] < ii ? 1 : 0;
-                if (rk < st.c) {
-                    const uint32_t h = ehash(rkey, rkeyb, (uint32_t)ii >> 3);
-                    const float sc = noise_score(st.xc, inv_t, ii, h, group_min_e(h), rkey2);
-                    if (better(sc, ii, tb)) tb = Best{sc, ii};
-                }
-                if (rk == st.c - 1) s_icut = ii;  // the cut's last kept index (filter_row's ic)
-            }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const float os = __shfl_xor(tb.score, off, kWave);
-                const int oi = __shfl_xor(tb.idx, off, kWave);
-                if (better(os, oi, tb)) tb = Best{os, oi};
-            }
-            if (lane == 0) {
-                s_bs[w] = tb.score;
-                s_bi[w] = tb.idx;
-            }
-            __syncthreads();
-            if (threadIdx.x == 0)
-                for (int j = 0; j < NW; ++j)
-                    if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
-            icut = s_icut;
-        }
-        if (threadIdx.x == 0) {
-            const T* rrow = logits + (int64_t)r * ld;
-            tokens[r] = b.idx;
-            if (logp_out) logp_out[r] = (b.idx >= 0 && b.idx < V) ? to_f<T>(rrow[b.idx]) - st.lse : __builtin_nanf("");
-            filt[r] = RowFilter{st.mx, 2u, kRowDone, st.kc, icut};  // (tk = 2: decided by the chunked pass 2)
-        }
-    };
-    auto take_row = [&](int r) {  // chunks of row r until none is left to claim
-        ToppRowWs* q = rws + r;
-        const int nch = topp_nchunks(nvec), cs = (nvec + nch - 1) / nch;
-        __syncthreads();
-        if (threadIdx.x == 0) s_q[0] = g_add(&q->claim, 1u);
-        __syncthreads();
-        if ((int)s_q[0] >= nch) return;
-        if (threadIdx.x < (int)(sizeof(ToppRowState) / 4)) {  // (acquire: published before the queue entry)
-            __threadfence();
-            reinterpret_cast<uint32_t*>(&s_st)[threadIdx.x] = g_ld(reinterpret_cast<const uint32_t*>(&q->st) + threadIdx.x);
-        }
-        __syncthreads();
-        const ToppRowState st = s_st;
-        const uint4* rrv = reinterpret_cast<const uint4*>(logits + (int64_t)r * ld);
-        const uint32_t rkey = row_key(seed, seq_ids ? seq_ids[r] : (int64_t)r, step);
-        const uint32_t rkey2 = noise_key2(rkey), rkeyb = noise_keyb(rkey);
-        const float xlo = uni(st.xlo), xc = uni(st.xc);
-        const bool split = st.split != 0;
-        int ck = (int)s_q[0];
-        while (ck < nch) {
-            // the next claim in flight under this chunk's loads (a claimed chunk is always taken)
-            uint32_t next = 0u;
-            if (threadIdx.x == 0) next = g_add(&q->claim, 1u);
-            const int c0 = ck * cs, c1 = min(nvec, c0 + cs);
-            if (threadIdx.x == 0) s_bar = st.e_s;
-            float best_s = st.e_s, bar = uni(st.e_s);
-            int best_i = st.e_i;
-            float thr = (bar - kNoiseC) * temp;
-            auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
-                const float wb = wave_max_uniform(best_s);
-                if (lane == 0 && wb > bar)
-                    __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                bar = fmaxf(wb, uni(s_bar));
-                thr = (bar - kNoiseC) * temp;
-            };
-            // one vector of up to VEC elements at v0 (one noise group; padding slots are -inf); a
-            // vector without admissible elements in the whole wave costs no hash
-            auto visit2 = [&](const uint4& pk, int v0) {
-                uint16_t raw[VEC];
-                __builtin_memcpy(raw, &pk, 16);
-                float x[VEC];
-                float xm = -INFINITY;
-                int nt = 0;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    x[k] = bf16_to_f32(raw[k]);
-                    xm = fmaxf(xm, x[k] >= xlo ? x[k] : -INFINITY);
-                    if constexpr (TOPP) nt += x[k] == xc ? 1 : 0;  // (gated by split at the ballot)
-                }
-                if constexpr (TOPP) {
-                    if (split && __builtin_amdgcn_ballot_w64(nt != 0) != 0 && nt != 0) {
-                        uint32_t p = g_add(&q->nt, (uint32_t)nt);
-#pragma unroll
-                        for (int k = 0; k < VEC; ++k) {
-                            if (x[k] == xc) {
-                                if (p < (uint32_t)kPTieCap) g_st(reinterpret_cast<uint32_t*>(q->tidx + p), (uint32_t)(v0 + k));
-                                ++p;
-                            }
-                        }
-                    }
-                }
-                if (__builtin_amdgcn_ballot_w64(xm > -INFINITY) == 0) return;
-                const uint32_t h = ehash(rkey, rkeyb, (uint32_t)v0 >> 3);
-                const float bits = noise_bits(h);
-                const bool cand = !(fmaf(bits, -kT, xm) - thr < 0.f);
-                if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
-                if (cand) {
-                    const float Eg = group_min_e(h);
-#pragma unroll
-                    for (int k = 0; k < VEC; ++k) {
-                        if (x[k] >= xlo && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
-                            const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, rkey2);
-                            if (better(sc, v0 + k, Best{best_s, best_i})) {
-                                best_s = sc;
-                                best_i = v0 + k;
-                            }
-                        }
-                    }
-                }
-                raise_bar();
-            };
-            __syncthreads();  // s_bar
-            constexpr uint32_t kPadNinf = 0xff80ff80u;  // -inf bf16 pairs: never admissible, never a tie
-            for (int b0 = c0; b0 < c1; b0 += 4 * NT) {
-                uint4 v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = b0 + u * NT + (int)threadIdx.x;
-                    v[u] = i < c1 ? rrv[i] : make_uint4(kPadNinf, kPadNinf, kPadNinf, kPadNinf);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (b0 + u * NT < c1) visit2(v[u], (b0 + u * NT + (int)threadIdx.x) * VEC);
-            }
-            if (ck == nch - 1 && nvec * VEC < V) {  // the ragged tail's partial group, read by thread 0
-                const T* rrow = logits + (int64_t)r * ld;
-                const int t0 = nvec * VEC, cnt = V - t0;
-                uint16_t t[VEC];
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) t[k] = (threadIdx.x == 0 && k < cnt) ? rrow[t0 + k] : (uint16_t)0xff80u;
-                uint4 pk;
-                __builtin_memcpy(&pk, t, 16);
-                visit2(pk, t0);
-            }
-            Best best{best_s, best_i};
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const float os = __shfl_xor(best.score, off, kWave);
-                const int oi = __shfl_xor(best.idx, off, kWave);
-                if (better(os, oi, best)) best = Best{os, oi};
-            }
-            if (lane == 0) {
-                s_bs[w] = best.score;
-                s_bi[w] = best.idx;
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                Best b{s_bs[0], s_bi[0]};
-                for (int j = 1; j < NW; ++j)
-                    if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
-                g_st(reinterpret_cast<uint32_t*>(&q->part[ck].score), __float_as_uint(b.score));
-                g_st(reinterpret_cast<uint32_t*>(&q->part[ck].idx), (uint32_t)b.idx);
-                __threadfence();  // (release: the part and the ties before the arrival)
-                s_q[1] = g_add(&q->done, 1u) == (uint32_t)(nch - 1) ? 1u : 0u;
-                s_q[0] = next;
-            }
-            __syncthreads();
-            if (s_q[1]) merge(r, q, st, rkey, rkeyb, rkey2);
-            ck = (int)s_q[0];
-            __syncthreads();
-        }
-    };
-    // published rows in queue order from the head; a helper (wait) stays while rows are still deciding
-    auto help = [&](bool wait) {
-        uint32_t i = 0u, last_dec = 0xffffffffu;
-        uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
-        while (true) {
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                s_q[2] = __hip_atomic_load(&ctl->decided, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                s_q[3] = g_ld(&ctl->qn);  // (after decided: all rows decided means the queue is final)
-                s_q[1] = g_ld(&ctl->head);
-            }
-            __syncthreads();
-            const uint32_t dec = s_q[2], qn = min(s_q[3], (uint32_t)nseq);
-            i = max(i, s_q[1]);
-            if (i < qn) {
-                if (threadIdx.x == 0) {  // the entry follows its slot's claim at once: a short wait
-                    uint32_t r = 0xffffffffu;
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    do {
-                        const uint64_t e = g_ld64(queue + i);
-                        if ((uint32_t)(e >> 32) == epoch) r = (uint32_t)e;
-                    } while (r == 0xffffffffu && __builtin_amdgcn_s_memrealtime() - t0 < kHelpIdleTicks);
-                    s_q[0] = r;
-                }
-                __syncthreads();
-                const uint32_t r = s_q[0];
-                if (r < (uint32_t)nseq) take_row((int)r);
-                ++i;
-                if (threadIdx.x == 0)
-                    __hip_atomic_fetch_max(&ctl->head, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                continue;
-            }
-            if (!wait || dec >= (uint32_t)nseq) break;
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (dec != last_dec) {
-                last_dec = dec;
-                t_idle = now;
-            } else if (now - t_idle > kHelpIdleTicks) {
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    };
-    if (pub) take_row((int)blockIdx.x);
-    help(!is_row);
-    // the launch's last workgroup re-arms the launch-wide words
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (g_add(&ctl->finished, 1u) == gridDim.x - 1) {
-            __threadfence();
-            g_st(&ctl->qn, 0u);
-            g_st(&ctl->decided, 0u);
-            g_st(&ctl->head, 0u);
-            g_st(&ctl->finished, 0u);
-        }
-    }
 }
 
 int splits_for(int nseq, int V) {
@@ -2328,11 +2193,6 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     RowFilter* filt = reinterpret_cast<RowFilter*>(w + off);
     off += ws_align((size_t)nseq * sizeof(RowFilter));
     Part* parts = reinterpret_cast<Part*>(w + off);
-    off += ws_align((size_t)nseq * nsplit * sizeof(Part));
-    ToppCtl* ctl = reinterpret_cast<ToppCtl*>(w + (size_t)kRowModeMinSeqs * 4);
-    uint64_t* queue = reinterpret_cast<uint64_t*>(w + off);
-    off += ws_align((size_t)nseq * sizeof(uint64_t));
-    ToppRowWs* rws = reinterpret_cast<ToppRowWs*>(w + off);
     const int greedy = temperature == 0.f;
     const int use_topk = !greedy && top_k > 0 && top_k < V;
     const int use_minp = !greedy && min_p > 0.f;
@@ -2353,17 +2213,12 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     if constexpr (sizeof(T) == 2) {
         if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
-            static uint32_t epoch = 0u;  // tags the launch's queue entries (never 0: zeroed memory)
-            if (++epoch == 0u) epoch = 1u;
-            const dim3 grid(nseq + g_topp_helpers);
             if (use_topp)
-                hipLaunchKernelGGL((sample_topp_kernel<T, true>), grid, dim3(kPNT), 0, stream, lg, ld, V, inv_t, use_minp,
-                                   ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, g_probe_topp, nseq, ctl,
-                                   queue, rws, epoch);
+                hipLaunchKernelGGL((sample_topp_kernel<T, true>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
+                                   use_minp, ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, g_probe_topp);
             else
-                hipLaunchKernelGGL((sample_topp_kernel<T, false>), grid, dim3(kPNT), 0, stream, lg, ld, V, inv_t,
-                                   use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, g_probe_topp, nseq,
-                                   ctl, queue, rws, epoch);
+                hipLaunchKernelGGL((sample_topp_kernel<T, false>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
+                                   use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, g_probe_topp);
             return check_launch("sample_topp_kernel");
         }
     }
@@ -2397,8 +2252,7 @@ using namespace skyrl;
 
 extern "C" size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V) {
     return kCounterBytes + ws_align((size_t)nseq * sizeof(RowFilter)) +
-           ws_align((size_t)nseq * splits_for(nseq, V) * sizeof(Part)) + ws_align((size_t)nseq * sizeof(uint64_t)) +
-           (size_t)nseq * sizeof(ToppRowWs) + 256;
+           (size_t)nseq * splits_for(nseq, V) * sizeof(Part) + 256;
 }
 
 extern "C" int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V, float temperature,

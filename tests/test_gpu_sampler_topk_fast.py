@@ -17,8 +17,7 @@ from skyrl_amd import ops
 
 pytestmark = pytest.mark.gpu
 
-_COUNTER_BYTES = 256 * 4 + 256  # sampler workspace: per-row counters and the top_p kernel's control words
-# first, then one 20-B RowFilter per row
+_COUNTER_BYTES = 256 * 4  # sampler workspace: per-row counters first, then one 20-B RowFilter per row
 _ROW_DONE = -2
 _ROW_FALLBACK = -3
 

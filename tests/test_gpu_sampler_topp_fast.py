@@ -1,18 +1,16 @@
-"""a1 filtered sampling without top_k: the top_p / min_p kernel (sample_topp_kernel) against the
-two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
+"""a1 filtered sampling without top_k: the two-pass top_p / min_p kernel (sample_topp_kernel)
+against the two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
 skyrl_tune("sampler_topp_fast", 0)) and against oracle/sampler_ref.c.
 
-Pass 1 takes the row max, a count histogram per exact bf16 key and MODE 2's race over the whole
-row (group bound, exact scores against the workgroup's best, every scored element recorded); the
-top_p cut is found on chip. A row is decided there when the race's best record is admissible
-(RowFilter.tk = 1); else the row is published and its pass 2 (MODE 2 over the keys above the
-cut, the cut key's elements ranked by index) runs in chunks that any workgroup of the launch
-takes, the last one merging (tk = 2). Tokens, logprobs and the recorded cut (key, last kept index)
-must be the two-kernel path's bit for bit. Rows outside its bounds (the cut among the values below
-2^-16 or the zeros, a tie group over 1024 at the cut, NaN / +inf, values >= 2^16, over 512 nonzero
-values below 2^-16) run the two-kernel path's code in the workgroup (RowFilter.ik =
-kRowFallback); the rest are kRowDone. skyrl_tune("topp_probe", 5) sends every row through the
-chunked pass 2, skyrl_tune("topp_helpers", n) sets the extra workgroups.
+The kernel takes the row max in pass 1 with a count histogram per exact bf16 key and scores every
+element MODE 2's group bound lets through against a per-wave bar (the 8th best score); it finds the
+top_p cut on chip and decides from those records when a certificate holds (fewer than 8
+inadmissible records beat the best admissible one, none of them an unranked element of a split cut
+key), else in pass 2 (MODE 2 over the keys above the cut, the cut key's elements ranked by index). Tokens, logprobs and the recorded cut (key, last kept index) must be the
+two-kernel path's bit for bit. Rows outside its bounds (the cut among the values below 2^-16 or the
+zeros, a tie group over 1024 at the cut, NaN / +inf, values >= 2^16, over 512 nonzero values below
+2^-16) run the
+two-kernel path's code in the workgroup (RowFilter.ik = kRowFallback); the rest are kRowDone.
 The recipe this serves: top_p = 0.95 alone (examples/text_to_sql/run_skyrl_sql.sh:60 and eight
 more example scripts), semantics skyrl-tx/tx/utils/generator.py:423-449.
 """
@@ -24,8 +22,7 @@ from skyrl_amd import ops
 
 pytestmark = pytest.mark.gpu
 
-_COUNTER_BYTES = 256 * 4 + 256  # sampler workspace: per-row counters and the top_p kernel's control words
-# first, then one 20-B RowFilter per row
+_COUNTER_BYTES = 256 * 4  # sampler workspace: per-row counters first, then one 20-B RowFilter per row
 _ROW_DONE = -2
 _ROW_FALLBACK = -3
 
@@ -36,31 +33,25 @@ def _filters(x):
     return ws[_COUNTER_BYTES:_COUNTER_BYTES + 20 * n].view(torch.int32).view(n, 5).cpu().clone()
 
 
-def _run(x, fast, chunked=False, helpers=256, **kw):
+def _run(x, fast, **kw):
     ops._ffi.call("skyrl_tune", b"sampler_topp_fast", int(fast))
-    ops._ffi.call("skyrl_tune", b"topp_probe", 5 if chunked else 0)
-    ops._ffi.call("skyrl_tune", b"topp_helpers", helpers)
     try:
         tok, lp = ops.sample(x, **kw)
         torch.cuda.synchronize()
         return tok.cpu(), lp.cpu(), _filters(x)
     finally:
         ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 1)
-        ops._ffi.call("skyrl_tune", b"topp_probe", 0)
-        ops._ffi.call("skyrl_tune", b"topp_helpers", 256)
 
 
-def _ab(x, min_done, chunked=False, helpers=256, **kw):
-    tf, lf, ff = _run(x, True, chunked, helpers, **kw)
+def _ab(x, min_done, **kw):
+    tf, lf, ff = _run(x, True, **kw)
     ts, ls, fs = _run(x, False, **kw)
     assert torch.equal(tf, ts), (kw, int((tf != ts).sum()))
     assert torch.allclose(lf, ls, atol=2e-5, rtol=1e-5, equal_nan=True), (kw, (lf - ls).abs().max())
     done = ff[:, 2] == _ROW_DONE
     assert bool(((ff[:, 2] == _ROW_DONE) | (ff[:, 2] == _ROW_FALLBACK)).all())
-    if chunked:  # every taken row through the chunked pass 2
-        assert bool((ff[done][:, 1] == 2).all())
     if kw.get("top_p", 1.0) < 1.0:  # the cut (key, and the last kept index where the kernel resolved it:
-        # -1 = a split tie group that pass 1's decision did not need to rank) of every row
+        # -1 = a split tie group that pass 1's certified decision did not need to rank) of every row
         assert torch.equal(ff[done][:, 3], fs[done][:, 3])
         rk = done & (ff[:, 4] != -1)
         assert torch.equal(ff[rk][:, 4], fs[rk][:, 4])
@@ -166,49 +157,3 @@ def test_topp_fast_small_and_ragged_vocab(dev, V):
         etok, elp = osamp.sample(base[:, :V].contiguous(), 1.0, -1, p, mp, 9, ids, 2)
         assert torch.equal(tf, etok)
         torch.testing.assert_close(lf, elp, atol=1e-4, rtol=1e-4)
-
-
-@pytest.mark.parametrize("helpers", [256, 0, 7])
-@pytest.mark.parametrize("cfg", [(1.0, 0.95, 0.0), (0.7, 0.9, 0.05), (1.0, 1.0, 0.1), (1.0, 0.0, 0.0)])
-def test_chunked_pass2_equals_two_kernel_path(dev, cfg, helpers):
-    """Every row through the chunked pass 2 (skyrl_tune topp_probe 5), with the default extra
-    workgroups, none (each row's own workgroup takes all its chunks) and a few: tokens, logprobs
-    and cuts equal the two-kernel path's at the bench shape."""
-    temp, p, mp = cfg
-    g = torch.Generator().manual_seed(int(p * 100) + int(mp * 1000) + 17)
-    x = (torch.randn(512, 151936, generator=g) * 3).to(torch.bfloat16).to(dev)
-    ids = torch.arange(512, dtype=torch.int64, device=dev) * 7 + 1
-    _ab(x, 512, chunked=True, helpers=helpers, temperature=temp, top_p=p, min_p=mp, seed=19, seq_ids=ids, step=3)
-
-
-def test_chunked_pass2_ties_ragged_and_few_rows(dev):
-    """The chunked pass 2 on rows whose cut splits a tie group, small and ragged vocabularies
-    (one chunk, the partial group in the last chunk), and a batch of 3 rows (the extra workgroups
-    start at once and wait for rows to publish), against the two-kernel path and the oracle."""
-    from oracle import sampler as osamp
-
-    g = torch.Generator().manual_seed(77)
-    V = 151936
-    ties = torch.randint(0, 80, (24, V), generator=g).float() / 16
-    ties[:, :V // 2] = -5.0  # ~950-element key groups: the cut splits one within the tie list's bound
-    x = ties.to(torch.bfloat16)
-    ids = torch.arange(24, dtype=torch.int64)
-    for p in (0.5, 0.93):
-        tf, lf, done = _ab(x.to(dev), 24, chunked=True, temperature=1.0, top_p=p, seed=3, seq_ids=ids.to(dev), step=1)
-        etok, _ = osamp.sample(x, 1.0, -1, p, 0.0, 3, ids, 1)
-        assert torch.equal(tf, etok)
-    for V in (100, 517, 4097, 50257):
-        base = (torch.randn(9, (V + 7) // 8 * 8 + 8, generator=g) * 2).to(torch.bfloat16)
-        x = base.to(dev)[:, :V]
-        ids = torch.arange(9, dtype=torch.int64)
-        for helpers in (256, 0):
-            tf, lf, _ = _ab(x, 9, chunked=True, helpers=helpers, temperature=0.9, top_p=0.8, seed=2,
-                            seq_ids=ids.to(dev), step=6)
-            etok, elp = osamp.sample(base[:, :V].contiguous(), 0.9, -1, 0.8, 0.0, 2, ids, 6)
-            assert torch.equal(tf, etok)
-            torch.testing.assert_close(lf, elp, atol=1e-4, rtol=1e-4)
-    x = (torch.randn(3, 151936, generator=g) * 3).to(torch.bfloat16)
-    ids = torch.arange(3, dtype=torch.int64)
-    tf, lf, _ = _ab(x.to(dev), 3, chunked=True, temperature=1.0, top_p=0.95, seed=8, seq_ids=ids.to(dev), step=2)
-    etok, _ = osamp.sample(x, 1.0, -1, 0.95, 0.0, 8, ids, 2)
-    assert torch.equal(tf, etok)
