@@ -8,4 +8,4 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 500 python bench.py > gpurun_out/r04e_bench.json 2> gpurun_out/r04e_bench.err; rc=$?
 echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/r04e_bench.err; exit $rc; }
 python -c "import json;d=json.loads(open('gpurun_out/r04e_bench.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']['frac'])"
-PMC=1 PMC_REGEX="logprob|grpo|ppo_loss|sample_kernel|sample_topk|pack|policy_train|paged_decode|lmhead_gemm" bash scripts/profile.sh > gpurun_out/r04e_profile.log 2>&1; rc=$?; tail -3 gpurun_out/r04e_profile.log; exit $rc
+PMC=1 PMC_REGEX="logprob|grpo|ppo_loss|sample_kernel|sample_topk|sample_topp|pack|policy_train|paged_decode|lmhead_gemm" bash scripts/profile.sh > gpurun_out/r04e_profile.log 2>&1; rc=$?; tail -3 gpurun_out/r04e_profile.log; exit $rc

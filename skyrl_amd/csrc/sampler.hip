@@ -1469,7 +1469,6 @@ constexpr int kPHalf = 4096;    // keys per sign in the window
 constexpr int kPSlowCap = 512;  // elements below the window
 constexpr int kPTieCap = 1024;  // elements at a split cut key
 constexpr int kPCandCap = 2048; // pass 1's exactly scored elements (seeds + bound survivors)
-constexpr float kCertDelta = 5.f;  // pass 1's recording margin below the bar (score units)
 
 // uniform (scalar) copy of a wave-uniform float, so the hot loops keep it in an SGPR
 __device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
@@ -1495,7 +1494,6 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     __shared__ int32_t s_ci[kPCandCap];
     __shared__ uint16_t s_ck[kPCandCap];
     __shared__ uint32_t s_nc, s_ntie;
-    __shared__ float s_dmin;
     __shared__ float s_bar1;
     __shared__ float s_bs[NW];
     __shared__ int32_t s_bi[NW];
@@ -1521,7 +1519,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         s_cut_j = -1;
         s_zero[0] = s_zero[1] = 0u;
         s_nc = 0u;
-        s_dmin = kCertDelta;
+
         s_ntie = 0u;
         s_bar1 = -INFINITY;  // the workgroup's best exact score so far
     }
@@ -1534,21 +1532,19 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     bool bad = false;
     // The decision in the same pass: MODE 2's noise (group hash, group bound, exact noise_score)
     // against the workgroup's bar = the best exact score computed so far (the unfiltered sampler's
-    // race over the whole row), lowered by a margin delta. Admissibility is unknown until the cut,
-    // so every element the bound lets through is scored exactly and recorded (s_cs / s_ci / s_ck);
-    // an element the bound skips scored below (bar - delta) at its visit, so below (final bar -
-    // final delta): the margin only shrinks (5 while the record list is under half full, then 3,
-    // 1.5, 0), per wave. After the cut, the best admissible record e* is the row's decision when its
-    // score is at least (final bar - the smallest final delta) and no unranked element of a split
-    // cut key beats it -- the certificate. It fails when the filtered race's winner trails the
-    // unfiltered one by more than delta: probability about (1 - kept mass) e^-delta (under 4e-4 of
-    // the rows at top_p 0.95); those rows take pass 2 (the re-read).
+    // race over the whole row). Admissibility is unknown until the cut, so every element the bound
+    // lets through is scored exactly and recorded (s_cs / s_ci / s_ck); an element the bound skips
+    // scored below the bar at its visit, so below the final bar. After the cut, the best admissible
+    // record e* is the row's decision when it is the best record (the unfiltered winner lies in the
+    // kept set, so it wins the filtered race too) and no unranked element of a split cut key beats
+    // it -- the certificate, which holds with probability about the kept mass (>= top_p); the other
+    // rows take pass 2 (the re-read), with e* as its starting bar. (A margin below the bar, which
+    // certifies more rows, made pass 1 slower than the re-reads it saved: DESIGN §3 "Filters".)
     const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
     const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
     const float temp = 1.0f / inv_t;
     const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-    float thr1 = -INFINITY;  // (bar - delta - C) T, wave-uniform
-    float delta = kCertDelta;
+    float thr1 = -INFINITY;  // (bar - C) T, wave-uniform
     int seed_v = -1;         // this lane's seed element (scored once: no duplicate record)
     auto record = [&](float sc, int v, uint32_t b) {
         const uint32_t p = atomicAdd(&s_nc, 1u);
@@ -1562,10 +1558,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         const float wb = wave_max_uniform(best_new);
         if (lane == 0 && wb > -INFINITY)
             __hip_atomic_fetch_max(&s_bar1, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_nc);
-        delta = fminf(delta, n < (uint32_t)kPCandCap / 2 ? kCertDelta : n < (uint32_t)kPCandCap * 3 / 4 ? 3.f
-                                                        : n < (uint32_t)kPCandCap * 15 / 16 ? 1.5f : 0.f);
-        thr1 = (fmaxf(wb, uni(s_bar1)) - delta - kNoiseC) * temp;
+        thr1 = (fmaxf(wb, uni(s_bar1)) - kNoiseC) * temp;
     };
     // the group bound and the exact scores of one group's elements (x[k] at v0 + k, raw bits b[k])
     auto gumbel = [&](const float (&x)[VEC], const uint16_t (&b)[VEC], float vm, int v0, int cnt) {
@@ -1710,7 +1703,6 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     vmx = wave_max(vmx);
     if (bad) s_bad = 1u;
-    if (lane == 0) __hip_atomic_fetch_min(&s_dmin, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (lane == 0) s_vmax[w] = vmx;
     __syncthreads();
     float mx = s_vmax[0];
@@ -1881,9 +1873,10 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         xlo = uni(from_key<T>(hi));
     }
-    // ---- pass 1's decision: the best admissible record e*, certified when its score is at least
-    //      (final bar - smallest final delta) and no unranked element of a split cut key beats it:
-    //      an element the bound skipped scored below that, so below e*; otherwise pass 2 decides
+    // ---- pass 1's decision: the best admissible record e*, certified when it is the best record
+    //      (the final bar) and no unranked element of a split cut key beats it: an element the bound
+    //      skipped scored below the bar, so below e*; otherwise pass 2 decides, starting from e*
+    Best e0{-INFINITY, 0x7fffffff};
     {
         const int nc = (int)min(s_nc, (uint32_t)kPCandCap);
         const bool complete = s_nc <= (uint32_t)kPCandCap;
@@ -1913,13 +1906,13 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         Best es{s_bs[0], s_bi[0]};
         for (int j = 1; j < NW; ++j)
             if (better(s_bs[j], s_bi[j], es)) es = Best{s_bs[j], s_bi[j]};
+        e0 = es;
         uint32_t ntie = 0u;
         if (TOPP && split)
             for (int i = threadIdx.x; i < nc; i += NT) ntie += (better(s_cs[i], s_ci[i], es) && cls(i) == 2) ? 1u : 0u;
         if (ntie) atomicAdd(&s_ntie, ntie);
         __syncthreads();
-        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && s_ntie == 0u &&
-                               es.score >= s_bar1 - s_dmin;
+        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && s_ntie == 0u && es.score >= s_bar1;
         if (certified) {
             if (threadIdx.x == 0) {
                 tokens[row_i] = es.idx;
@@ -1932,10 +1925,13 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         __syncthreads();  // s_bs reused below
     }
     const uint64_t t_p2 = __builtin_amdgcn_s_memrealtime();
-    float thr = -INFINITY, bar = -INFINITY;
-    float best_s = -INFINITY;
-    int best_i = 0x7fffffff;
-    if (threadIdx.x == 0) s_bar = -INFINITY;
+    // e* (admissible, exactly scored) is the starting best and bar: only elements that beat it
+    // are scored exactly
+    float bar = uni(e0.score);
+    float thr = (bar - kNoiseC) * temp;
+    float best_s = e0.score;
+    int best_i = e0.idx;
+    if (threadIdx.x == 0) s_bar = e0.score;
     auto adm = [&](float x) -> bool { return x >= xlo; };
     auto raise_bar = [&]() {  // publish the wave's best, read the workgroup's
         const float wb = wave_max_uniform(best_s);
@@ -1980,9 +1976,79 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             for (int k = 0; k < VEC; ++k) {
                 if (adm(x[k]) && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) {
                     const float sc = noise_score(x[k], inv_t, v0 + k, h, Eg, key2);
-                    if (sc > best_s) {  // ascending index within the lane: the lowest wins ties
+                    if (better(sc, v0 + k, Best{best_s, best_i})) {
                         best_s = sc;
                         best_i = v0 + k;
+                    }
+                }
+            }
+        }
+        raise_bar();
+    };
+    // four vectors (a stage) at once: one ballot per decision instead of one per vector, and the
+    // four group hashes independent of each other (a row left to pass 2 runs alone on its CU at the
+    // end of the launch, bound by its waves' dependent chains, not by bandwidth)
+    auto visit2x4 = [&](const uint4 (&pk)[4], int vbase) {  // vector u at (vbase + u NT) VEC
+        float xm[4];
+        bool anyt = false, anya = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint16_t raw[VEC];
+            __builtin_memcpy(raw, &pk[u], 16);
+            xm[u] = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const float x = bf16_to_f32(raw[k]);
+                xm[u] = fmaxf(xm[u], adm(x) ? x : -INFINITY);
+                if constexpr (TOPP) anyt |= x == xc;  // (gated by split at the ballot)
+            }
+            anya |= xm[u] > -INFINITY;
+        }
+        if constexpr (TOPP) {
+            if (split && __builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    uint16_t raw[VEC];
+                    __builtin_memcpy(raw, &pk[u], 16);
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) {
+                        if (bf16_to_f32(raw[k]) == xc) {
+                            const uint32_t p = atomicAdd(&s_nt, 1u);
+                            if (p < (uint32_t)kPTieCap) s_tidx[p] = (vbase + u * NT) * VEC + k;
+                        }
+                    }
+                }
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(anya) == 0) return;
+        uint32_t h[4];
+        bool cand[4], anyc = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            h[u] = ehash(key, keyb, (uint32_t)(vbase + u * NT));  // (the group index: vector index)
+            cand[u] = !(fmaf(noise_bits(h[u]), -kT, xm[u]) - thr < 0.f);
+            anyc |= cand[u];
+        }
+        if (__builtin_amdgcn_ballot_w64(anyc) == 0) return;
+        if (anyc) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (cand[u]) {
+                    uint16_t raw[VEC];
+                    __builtin_memcpy(raw, &pk[u], 16);
+                    const float bits = noise_bits(h[u]);
+                    const float Eg = group_min_e(h[u]);
+                    const int v0 = (vbase + u * NT) * VEC;
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) {
+                        const float x = bf16_to_f32(raw[k]);
+                        if (adm(x) && !(fmaf(bits, -kT, x) - thr < 0.f)) {
+                            const float sc = noise_score(x, inv_t, v0 + k, h[u], Eg, key2);
+                            if (better(sc, v0 + k, Best{best_s, best_i})) {
+                                best_s = sc;
+                                best_i = v0 + k;
+                            }
+                        }
                     }
                 }
             }
@@ -2011,7 +2077,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     // pass 2's stream: kP2Depth stages of 4 NT vectors, each refilled right after it is visited, so
     // that (kP2Depth - 1) x 4 loads per lane stay in flight (a row re-read alone on its CU at the end
     // of the launch is latency-bound; cached loads: the row is in the Infinity Cache)
-    constexpr int kP2Depth = 4;
+    constexpr int kP2Depth = 3;
     const int nit = nfull / kStep;
     uint4 stg[kP2Depth][4];
 #pragma unroll
@@ -2040,8 +2106,11 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         if (vb >= 0) {
             const uint32_t h = ehash(key, keyb, (uint32_t)vb >> 3);
-            best_s = noise_score(xb, inv_t, vb, h, group_min_e(h), key2);
-            best_i = vb;
+            const float sc = noise_score(xb, inv_t, vb, h, group_min_e(h), key2);
+            if (better(sc, vb, Best{best_s, best_i})) {
+                best_s = sc;
+                best_i = vb;
+            }
         }
         raise_bar();
         __syncthreads();
@@ -2058,11 +2127,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             for (int d = 0; d < kP2Depth; ++d) {  // stage d in place (no register rotation: a move
                 const int it = it0 + d;           // would wait for the loads in flight)
                 if (it < nit) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        visit2(stg[d][u], (it * kStep + u * NT + (int)threadIdx.x) * VEC);
-                        __builtin_amdgcn_sched_barrier(0);  // one vector's temporaries at a time
-                    }
+                    visit2x4(stg[d], it * kStep + (int)threadIdx.x);
                     if (it + kP2Depth < nit) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) stg[d][u] = rv[(it + kP2Depth) * kStep + u * NT + threadIdx.x];
