@@ -1956,11 +1956,15 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         if constexpr (TOPP) {
             if (split && __builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {
+                uint32_t nt = 0u;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) nt += x[k] == xc ? 1u : 0u;
+                uint32_t p = atomicAdd(&s_nt, nt);
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
                     if (x[k] == xc) {
-                        const uint32_t p = atomicAdd(&s_nt, 1u);
                         if (p < (uint32_t)kPTieCap) s_tidx[p] = v0 + k;
+                        ++p;
                     }
                 }
             }
@@ -2005,16 +2009,30 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             anya |= xm[u] > -INFINITY;
         }
         if constexpr (TOPP) {
-            if (split && __builtin_amdgcn_ballot_w64(anyt) != 0 && anyt) {
+            // the cut key's elements into the tie list: ONE LDS add per lane for all its ties (an
+            // add per element would wait on its return in each of the 32 slots, exec-masked or not:
+            // 2/3 of the pass's time before this)
+            if (split && __builtin_amdgcn_ballot_w64(anyt) != 0) {
+                uint32_t nt = 0u;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     uint16_t raw[VEC];
                     __builtin_memcpy(raw, &pk[u], 16);
 #pragma unroll
-                    for (int k = 0; k < VEC; ++k) {
-                        if (bf16_to_f32(raw[k]) == xc) {
-                            const uint32_t p = atomicAdd(&s_nt, 1u);
-                            if (p < (uint32_t)kPTieCap) s_tidx[p] = (vbase + u * NT) * VEC + k;
+                    for (int k = 0; k < VEC; ++k) nt += bf16_to_f32(raw[k]) == xc ? 1u : 0u;
+                }
+                if (nt) {
+                    uint32_t p = atomicAdd(&s_nt, nt);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        uint16_t raw[VEC];
+                        __builtin_memcpy(raw, &pk[u], 16);
+#pragma unroll
+                        for (int k = 0; k < VEC; ++k) {
+                            if (bf16_to_f32(raw[k]) == xc) {
+                                if (p < (uint32_t)kPTieCap) s_tidx[p] = (vbase + u * NT) * VEC + k;
+                                ++p;
+                            }
                         }
                     }
                 }
