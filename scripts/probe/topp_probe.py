@@ -45,7 +45,8 @@ def main():
         ws = ops.WORKSPACES.get(dev, "sample", ops._ffi.query("skyrl_sample_workspace_bytes", n, V))
         ff = ws[1024:1024 + 20 * n].view(torch.int32).view(n, 5).cpu()
         res["pass1_decided"] = int((ff[:, 1] == 1).sum())  # RowFilter.tk = 1: certified in pass 1
-        for probe in (5, 6):  # per-row pass-2 time (5: every row takes pass 2; 6: the rows that do)
+        for probe in (5, 6, 7):  # per-row pass-2 time (5: every row takes pass 2; 6: the rows that do;
+            # 7: as 6 with the stage loop's visits replaced by an xor of the loaded words)
             ops._ffi.call("skyrl_tune", b"topp_probe", probe)
             tok.fill_(-1)
             ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1, tokens_out=tok, logp_out=lp, **kw)

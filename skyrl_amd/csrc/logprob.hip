@@ -296,7 +296,7 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "topp_probe") {
-        SKYRL_REQUIRE(value >= 0 && value <= 6, "skyrl_tune: topp_probe must be 0 .. 6");
+        SKYRL_REQUIRE(value >= 0 && value <= 7, "skyrl_tune: topp_probe must be 0 .. 7");
         g_probe_topp = value;
         return SKYRL_OK;
     }

@@ -2145,7 +2145,14 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             for (int d = 0; d < kP2Depth; ++d) {  // stage d in place (no register rotation: a move
                 const int it = it0 + d;           // would wait for the loads in flight)
                 if (it < nit) {
-                    visit2x4(stg[d], it * kStep + (int)threadIdx.x);
+                    if (probe == 7) {  // timing probe: the stage loop's loads without the visits
+                        uint32_t acc = 0u;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) acc ^= stg[d][u].x ^ stg[d][u].y ^ stg[d][u].z ^ stg[d][u].w;
+                        if (acc == 0x12345678u) s_nt = acc;
+                    } else {
+                        visit2x4(stg[d], it * kStep + (int)threadIdx.x);
+                    }
                     if (it + kP2Depth < nit) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) stg[d][u] = rv[(it + kP2Depth) * kStep + u * NT + threadIdx.x];
