@@ -45,8 +45,9 @@ def main():
         ws = ops.WORKSPACES.get(dev, "sample", ops._ffi.query("skyrl_sample_workspace_bytes", n, V))
         ff = ws[1024:1024 + 20 * n].view(torch.int32).view(n, 5).cpu()
         res["pass1_decided"] = int((ff[:, 1] == 1).sum())  # RowFilter.tk = 1: certified in pass 1
-        for probe in (5, 6, 7):  # per-row pass-2 time (5: every row takes pass 2; 6: the rows that do;
-            # 7: as 6 with the stage loop's visits replaced by an xor of the loaded words)
+        # per-row in-row pass-2 time (min_p alone; top_p's left rows go to the pass-2 kernel): 5 every
+        # row takes pass 2, 6 the rows that do, 7 as 6 with the stage loop's visits replaced by an xor
+        for probe in ((5, 6, 7) if name.startswith("min_p") else ()):
             ops._ffi.call("skyrl_tune", b"topp_probe", probe)
             tok.fill_(-1)
             ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1, tokens_out=tok, logp_out=lp, **kw)
@@ -58,6 +59,11 @@ def main():
                 res[f"probe{probe}_pass2_us"] = [round(float(p2.min()), 2), round(float(p2.median()), 2), round(float(p2.max()), 2)]
                 res[f"probe{probe}_before_us"] = [round(float(pre.min()), 2), round(float(pre.median()), 2), round(float(pre.max()), 2)]
         ops._ffi.call("skyrl_tune", b"topp_probe", 0)
+        if name.startswith("top_p"):
+            ops._ffi.call("skyrl_tune", b"topp_probe", 5)  # every row through the pass-2 kernel
+            res["all_pass2_kernel_us"] = timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1,
+                                                              tokens_out=tok, logp_out=lp, **kw))
+            ops._ffi.call("skyrl_tune", b"topp_probe", 0)
         steps, dec = [], []
         for st in range(2, 22):  # fresh noise per decode step: how many rows pass 1 leaves varies
             steps.append(timed(lambda: ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=st, tokens_out=tok,

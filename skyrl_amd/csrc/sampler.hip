@@ -1469,6 +1469,16 @@ constexpr int kPHalf = 4096;    // keys per sign in the window
 constexpr int kPSlowCap = 512;  // elements below the window
 constexpr int kPTieCap = 1024;  // elements at a split cut key
 constexpr int kPCandCap = 2048; // pass 1's exactly scored elements (seeds + bound survivors)
+constexpr int32_t kRowPending = -4;  // RowFilter.ik between the two top_p kernels: pass 2 to run
+constexpr int kP2Splits = 8;         // workgroups per left row in sample_topp_pass2_kernel
+struct ToppPending {  // a row pass 1 did not decide, for sample_topp_pass2_kernel
+    float xlo, xc, lse, mx;  // admissibility bound, the cut key's value, the raw lse, the raw max
+    float e_s;               // e*: pass 1's best admissible record (score, index)
+    int e_i;
+    int split;
+    uint32_t kc;
+    long long c;             // the split cut key's kept tie ranks
+};
 
 // uniform (scalar) copy of a wave-uniform float, so the hot loops keep it in an SGPR
 __device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
@@ -1477,7 +1487,8 @@ template <typename T, bool TOPP>
 __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topp_kernel(
     const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, float top_p,
     uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
-    float* __restrict__ logp_out, RowFilter* __restrict__ filt, int probe) {
+    float* __restrict__ logp_out, RowFilter* __restrict__ filt, ToppPending* __restrict__ pend,
+    unsigned* __restrict__ pend_nt, int probe) {
     static_assert(sizeof(T) == 2, "bf16 rows");
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
     constexpr int kDummy = 2 * kPHalf;  // 64 words taking the out-of-window elements' increments (no branch)
@@ -1924,6 +1935,21 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         __syncthreads();  // s_bs reused below
     }
+    if constexpr (TOPP) {
+        // top_p: a row pass 1 did not decide goes to sample_topp_pass2_kernel (launched next), cut
+        // into kP2Splits workgroups: few rows are left (~5 %), and one alone on this workgroup's CU
+        // spends ~20 us in the visits' VALU. min_p alone leaves most rows (~70 %): the in-row pass 2
+        // below, at full occupancy, is the better form there.
+        if (probe < 3 || probe > 4) {
+            if (threadIdx.x == 0) {
+                pend[row_i] = ToppPending{xlo, xc, lse, mx, e0.score, e0.idx, split ? 1 : 0, kc, c};
+                pend_nt[2 * row_i] = 0u;      // the row's tie count and its pieces' arrival counter (the
+                pend_nt[2 * row_i + 1] = 0u;  // workspace layout moves with the batch size: not left re-armed)
+                filt[row_i] = RowFilter{mx, 0u, kRowPending, kc, ic};
+            }
+            return;
+        }
+    }
     const uint64_t t_p2 = __builtin_amdgcn_s_memrealtime();
     // e* (admissible, exactly scored) is the starting best and bar: only elements that beat it
     // are scored exactly
@@ -2242,6 +2268,231 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
 }
 
+// Pass 2 of the rows sample_topp_kernel left pending (RowFilter.ik = kRowPending), each row cut into
+// kP2Splits workgroups of contiguous vectors (a fixed partition: the split-mode sampler's pattern):
+// MODE 2 over the admissible elements x >= xlo of the piece, bar and best starting from e*; the
+// split cut key's indices appended to the row's tie list (one agent-scope add per lane). The last
+// arriving piece (arrive_last) merges the pieces' bests, ranks the ties by index (the first c are
+// admissible, scored exactly) and writes token, logprob and cut. The other rows' workgroups exit.
+template <typename T, bool TOPP>
+__global__ __launch_bounds__(kPNT) void sample_topp_pass2_kernel(
+    const T* __restrict__ logits, int64_t ld, int V, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
+    int64_t step, int32_t* __restrict__ tokens, float* __restrict__ logp_out, RowFilter* __restrict__ filt,
+    const ToppPending* __restrict__ pend, unsigned* __restrict__ pend_nt, int32_t* __restrict__ ties,
+    Best* __restrict__ parts) {
+    constexpr int NT = kPNT, NW = NT / kWave, VEC = 8, kPer = 8;  // up to kPer vectors per lane
+    const int row_i = blockIdx.x, piece = blockIdx.y;
+    if (filt[row_i].ik != kRowPending) return;  // (workgroup-uniform)
+    __shared__ float s_bar, s_bs[NW];
+    __shared__ int32_t s_bi[NW];
+    __shared__ int s_last, s_icut;
+    __shared__ int32_t s_tidx[kPTieCap];
+    const ToppPending st = pend[row_i];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const T* row = logits + (int64_t)row_i * ld;
+    const uint4* rv = reinterpret_cast<const uint4*>(row);
+    const int nvec = V / VEC;
+    const int cs = (nvec + kP2Splits - 1) / kP2Splits;  // host check: cs <= kPer NT
+    const int c0 = min(nvec, piece * cs), c1 = min(nvec, c0 + cs);
+    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
+    const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
+    const float temp = 1.0f / inv_t;
+    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    const float xlo = uni(st.xlo), xc = uni(st.xc);
+    const bool split = st.split != 0;
+    // the piece's vectors, all loads in flight at once
+    constexpr uint32_t kPadNinf = 0xff80ff80u;  // -inf bf16 pairs: never admissible, never a tie
+    uint4 v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int i = c0 + u * NT + (int)threadIdx.x;
+        v[u] = i < c1 ? rv[i] : make_uint4(kPadNinf, kPadNinf, kPadNinf, kPadNinf);
+    }
+    if (threadIdx.x == 0) s_bar = st.e_s;
+    __syncthreads();
+    float bar = uni(st.e_s);
+    float thr = (bar - kNoiseC) * temp;
+    float best_s = st.e_s;
+    int best_i = st.e_i;
+    uint32_t nt = 0u;
+    // ties first (one add per lane), then MODE 2 per vector
+    if constexpr (TOPP) {
+        if (split) {
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                uint16_t raw[VEC];
+                __builtin_memcpy(raw, &v[u], 16);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) nt += bf16_to_f32(raw[k]) == xc ? 1u : 0u;
+            }
+            if (nt) {
+                uint32_t p = __hip_atomic_fetch_add(pend_nt + 2 * row_i, nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int u = 0; u < kPer; ++u) {
+                    uint16_t raw[VEC];
+                    __builtin_memcpy(raw, &v[u], 16);
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) {
+                        if (bf16_to_f32(raw[k]) == xc) {
+                            if (p < (uint32_t)kPTieCap)
+                                st_wt(ties + (int64_t)row_i * kPTieCap + p, (c0 + u * NT + (int)threadIdx.x) * VEC + k);
+                            ++p;
+                        }
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        if (c0 + u * NT >= c1) break;  // (uniform)
+        const int v0 = (c0 + u * NT + (int)threadIdx.x) * VEC;
+        uint16_t raw[VEC];
+        __builtin_memcpy(raw, &v[u], 16);
+        float xm = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const float x = bf16_to_f32(raw[k]);
+            xm = fmaxf(xm, x >= xlo ? x : -INFINITY);
+        }
+        if (__builtin_amdgcn_ballot_w64(xm > -INFINITY) == 0) continue;
+        const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
+        const float bits = noise_bits(h);
+        const bool cand = !(fmaf(bits, -kT, xm) - thr < 0.f);
+        if (__builtin_amdgcn_ballot_w64(cand) == 0) continue;
+        if (cand) {
+            const float Eg = group_min_e(h);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const float x = bf16_to_f32(raw[k]);
+                if (x >= xlo && !(fmaf(bits, -kT, x) - thr < 0.f)) {
+                    const float sc = noise_score(x, inv_t, v0 + k, h, Eg, key2);
+                    if (better(sc, v0 + k, Best{best_s, best_i})) {
+                        best_s = sc;
+                        best_i = v0 + k;
+                    }
+                }
+            }
+        }
+        const float wb = wave_max_uniform(best_s);
+        if (lane == 0 && wb > bar) __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bar = fmaxf(wb, uni(s_bar));
+        thr = (bar - kNoiseC) * temp;
+    }
+    if (piece == kP2Splits - 1 && nvec * VEC < V) {  // the ragged tail's partial group, by thread 0
+        const int t0 = nvec * VEC, cnt = V - t0;
+        if (threadIdx.x == 0) {
+            float xs[VEC];
+            float xm = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                xs[k] = k < cnt ? to_f<T>(row[t0 + k]) : -INFINITY;
+                xm = fmaxf(xm, xs[k] >= xlo ? xs[k] : -INFINITY);
+            }
+            const uint32_t h = ehash(key, keyb, (uint32_t)t0 >> 3);
+            if constexpr (TOPP) {
+                if (split) {
+                    uint32_t n2 = 0u;
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) n2 += xs[k] == xc ? 1u : 0u;
+                    if (n2) {
+                        uint32_t p = __hip_atomic_fetch_add(pend_nt + 2 * row_i, n2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                        for (int k = 0; k < VEC; ++k)
+                            if (xs[k] == xc) {
+                                if (p < (uint32_t)kPTieCap) st_wt(ties + (int64_t)row_i * kPTieCap + p, t0 + k);
+                                ++p;
+                            }
+                    }
+                }
+            }
+            if (xm > -INFINITY) {
+                const float Eg = group_min_e(h);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    if (xs[k] >= xlo) {
+                        const float sc = noise_score(xs[k], inv_t, t0 + k, h, Eg, key2);
+                        if (better(sc, t0 + k, Best{best_s, best_i})) {
+                            best_s = sc;
+                            best_i = t0 + k;
+                        }
+                    }
+            }
+        }
+    }
+    // the piece's best: lanes, waves; stored write-through, every storing wave drained, then the
+    // arrival (the last piece merges)
+    Best best{best_s, best_i};
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(best.score, off, kWave);
+        const int oi = __shfl_xor(best.idx, off, kWave);
+        if (better(os, oi, best)) best = Best{os, oi};
+    }
+    if (lane == 0) {
+        s_bs[w] = best.score;
+        s_bi[w] = best.idx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Best b{s_bs[0], s_bi[0]};
+        for (int j = 1; j < NW; ++j)
+            if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
+        Best* dst = parts + (int64_t)row_i * kP2Splits + piece;
+        st_wt(&dst->score, b.score);
+        st_wt(&dst->idx, b.idx);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every wave that stored ties)
+    __syncthreads();
+    if (!arrive_last(pend_nt + 2 * row_i + 1, (unsigned)kP2Splits, &s_last)) return;
+    Best b{-INFINITY, 0x7fffffff};
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < kP2Splits; ++j) {
+            const Best q = parts[(int64_t)row_i * kP2Splits + j];
+            if (better(q.score, q.idx, b)) b = q;
+        }
+    }
+    int icut = split ? -1 : 0x7fffffff;
+    if (TOPP && split) {  // rank kc's elements by index: the first c are admissible, scored exactly here
+        const int n = (int)min(pend_nt[2 * row_i], (uint32_t)kPTieCap);
+        for (int i = threadIdx.x; i < n; i += NT) s_tidx[i] = ties[(int64_t)row_i * kPTieCap + i];
+        if (threadIdx.x == 0) s_icut = -1;
+        __syncthreads();
+        Best tb{-INFINITY, 0x7fffffff};
+        for (int i = threadIdx.x; i < n; i += NT) {
+            const int ii = s_tidx[i];
+            int r = 0;
+            for (int j = 0; j < n; ++j) r += s_tidx[j] < ii ? 1 : 0;
+            if (r < st.c) {
+                const uint32_t h = ehash(key, keyb, (uint32_t)ii >> 3);
+                const float sc = noise_score(xc, inv_t, ii, h, group_min_e(h), key2);
+                if (better(sc, ii, tb)) tb = Best{sc, ii};
+            }
+            if (r == st.c - 1) s_icut = ii;  // the cut's last kept index (filter_row's ic)
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float os = __shfl_xor(tb.score, off, kWave);
+            const int oi = __shfl_xor(tb.idx, off, kWave);
+            if (better(os, oi, tb)) tb = Best{os, oi};
+        }
+        if (lane == 0) {
+            s_bs[w] = tb.score;
+            s_bi[w] = tb.idx;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int j = 0; j < NW; ++j)
+                if (better(s_bs[j], s_bi[j], b)) b = Best{s_bs[j], s_bi[j]};
+        icut = s_icut;
+    }
+    if (threadIdx.x == 0) {
+        tokens[row_i] = b.idx;
+        if (logp_out) logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - st.lse : __builtin_nanf("");
+        filt[row_i] = RowFilter{st.mx, 0u, kRowDone, st.kc, icut};
+    }
+}
+
 int splits_for(int nseq, int V) {
     if (nseq <= 0 || V <= 0 || nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
     int s = (2048 + nseq - 1) / nseq;
@@ -2301,15 +2552,31 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     }
     // top_p / min_p without top_k on 16-B aligned bf16 rows: the two-pass kernel alone
     if constexpr (sizeof(T) == 2) {
-        if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
+        if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && V <= kP2Splits * 8 * kPNT * 8 &&
+            (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
+            // the pass-2 kernel's per-row state after the split sampler's parts (never used by this path)
+            char* pw = w + off + ws_align((size_t)nseq * nsplit * sizeof(Part));
+            ToppPending* pend = reinterpret_cast<ToppPending*>(pw);
+            pw += ws_align((size_t)nseq * sizeof(ToppPending));
+            unsigned* pend_nt = reinterpret_cast<unsigned*>(pw);  // per row: tie count, arrival counter
+            pw += ws_align((size_t)nseq * 2 * sizeof(unsigned));
+            Best* pparts = reinterpret_cast<Best*>(pw);
+            pw += ws_align((size_t)nseq * kP2Splits * sizeof(Best));
+            int32_t* pties = reinterpret_cast<int32_t*>(pw);
             if (use_topp)
                 hipLaunchKernelGGL((sample_topp_kernel<T, true>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
-                                   use_minp, ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, g_probe_topp);
+                                   use_minp, ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt,
+                                   g_probe_topp);
             else
                 hipLaunchKernelGGL((sample_topp_kernel<T, false>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
-                                   use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, g_probe_topp);
-            return check_launch("sample_topp_kernel");
+                                   use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt,
+                                   g_probe_topp);
+            int rc = check_launch("sample_topp_kernel");
+            if (rc || !use_topp || (g_probe_topp >= 1 && g_probe_topp <= 4)) return rc;  // (probes 1-4: pass 1 only)
+            hipLaunchKernelGGL((sample_topp_pass2_kernel<T, true>), dim3(nseq, kP2Splits), dim3(kPNT), 0, stream, lg, ld,
+                               V, inv_t, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt, pties, pparts);
+            return check_launch("sample_topp_pass2_kernel");
         }
     }
     if (use_topk || use_minp || use_topp) {
@@ -2342,7 +2609,9 @@ using namespace skyrl;
 
 extern "C" size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V) {
     return kCounterBytes + ws_align((size_t)nseq * sizeof(RowFilter)) +
-           (size_t)nseq * splits_for(nseq, V) * sizeof(Part) + 256;
+           ws_align((size_t)nseq * splits_for(nseq, V) * sizeof(Part)) + ws_align((size_t)nseq * sizeof(ToppPending)) +
+           ws_align((size_t)nseq * 2 * sizeof(unsigned)) + ws_align((size_t)nseq * kP2Splits * sizeof(Best)) +
+           (size_t)nseq * kPTieCap * sizeof(int32_t) + 256;
 }
 
 extern "C" int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V, float temperature,
