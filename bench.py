@@ -712,11 +712,12 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
     """The §8(d) filter variant of the rollout sampler (top_k = 50 with top_p = 0.9, and top_k =
     50 alone) and the SkyRL-SQL recipe's top_p = 0.95 alone (examples/text_to_sql/run_skyrl_sql.sh:60)
     at the decode step's shape [nseq, V] bf16, T = 1: the whole skyrl_sample call (with top_k the
-    one-pass kernel, without it the two-pass top_p kernel; rows either hands back run the
-    pre-pass + MODE 2 code in the same workgroup), against the two-kernel path (skyrl_tune
-    sampler_topk_fast / sampler_topp_fast 0). Algorithmic bytes = one read of the logits + 16 B
-    per row (the top_p kernel reads each row twice; the second read is meant to hit the Infinity
-    Cache)."""
+    one-pass kernel; without it the top_p kernel, which decides most rows in one pass and hands
+    the rest to a second launch that re-reads each of them in 8 pieces; rows either kernel cannot
+    take run the pre-pass + MODE 2 code in the same workgroup), against the two-kernel path
+    (skyrl_tune sampler_topk_fast / sampler_topp_fast 0). "one_pass" is the fast path's whole call
+    (for top_p both launches). Algorithmic bytes = one read of the logits + 16 B per row (the
+    left rows' re-read, ~6 % at top_p 0.95, is meant to hit the Infinity Cache)."""
     from skyrl_amd import ops
 
     g = torch.Generator(device=dev).manual_seed(5)
