@@ -47,7 +47,7 @@ def main():
         res["pass1_decided"] = int((ff[:, 1] == 1).sum())  # RowFilter.tk = 1: certified in pass 1
         # per-row in-row pass-2 time (min_p alone; top_p's left rows go to the pass-2 kernel): 5 every
         # row takes pass 2, 6 the rows that do, 7 as 6 with the stage loop's visits replaced by an xor
-        for probe in ((5, 6, 7) if name.startswith("min_p") else ()):
+        for probe in ((6, 7) if name.startswith("min_p") else ()):
             ops._ffi.call("skyrl_tune", b"topp_probe", probe)
             tok.fill_(-1)
             ops.sample(x, temperature=1.0, seed=3, seq_ids=ids, step=1, tokens_out=tok, logp_out=lp, **kw)

@@ -32,7 +32,9 @@ namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
 int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
-int g_probe_topp = 0;  // skyrl_tune("topp_probe"): timing only, tokens invalid: 1 pass 1 alone, 2 pass 1 + the cut
+int g_probe_topp = 0;  // skyrl_tune("topp_probe"): 1 pass 1 alone, 2 pass 1 + the cut, 3 / 4 + a bare re-read
+                       // (timing only, tokens invalid); 5: every row through pass 2 (valid tokens); 6 / 7:
+                       // min_p's in-row pass 2 timed per row (tokens = ticks; 7 without the visits)
 namespace {
 
 constexpr int kThreads = 256;
@@ -2255,7 +2257,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         if (logp_out)
             logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - lse : __builtin_nanf("");
         filt[row_i] = RowFilter{mx, 0u, kRowDone, kc, icut};
-        if (probe >= 5) {  // timing probes: pass 2's and the row's time before it, 10-ns ticks
+        if (probe >= 6) {  // timing probes (6, 7): pass 2's and the row's time before it, 10-ns ticks
             tokens[row_i] = (int)(__builtin_amdgcn_s_memrealtime() - t_p2);
             if (logp_out) logp_out[row_i] = (float)(t_p2 - t_start);
         }

@@ -1,16 +1,17 @@
-"""a1 filtered sampling without top_k: the two-pass top_p / min_p kernel (sample_topp_kernel)
-against the two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
+"""a1 filtered sampling without top_k: the top_p / min_p kernel (sample_topp_kernel) against the
+two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
 skyrl_tune("sampler_topp_fast", 0)) and against oracle/sampler_ref.c.
 
-The kernel takes the row max in pass 1 with a count histogram per exact bf16 key and scores every
-element MODE 2's group bound lets through against a per-wave bar (the 8th best score); it finds the
-top_p cut on chip and decides from those records when a certificate holds (fewer than 8
-inadmissible records beat the best admissible one, none of them an unranked element of a split cut
-key), else in pass 2 (MODE 2 over the keys above the cut, the cut key's elements ranked by index). Tokens, logprobs and the recorded cut (key, last kept index) must be the
-two-kernel path's bit for bit. Rows outside its bounds (the cut among the values below 2^-16 or the
-zeros, a tie group over 1024 at the cut, NaN / +inf, values >= 2^16, over 512 nonzero values below
-2^-16) run the
-two-kernel path's code in the workgroup (RowFilter.ik = kRowFallback); the rest are kRowDone.
+Pass 1 takes the row max, a count histogram per exact bf16 key and MODE 2's race over the whole
+row (every scored element recorded); the top_p cut is found on chip and the race's best record
+decides the row when it is admissible (RowFilter.tk = 1). The other rows run pass 2 (MODE 2 over
+the keys above the cut, the cut key's elements ranked by index): for top_p in a second launch,
+sample_topp_pass2_kernel, each left row cut into 8 pieces with the last piece merging; for min_p
+alone in the same workgroup. Tokens, logprobs and the recorded cut (key, last kept index) must be
+the two-kernel path's bit for bit. Rows outside its bounds (the cut among the values below 2^-16
+or the zeros, a tie group over 1024 at the cut, NaN / +inf, values >= 2^16, over 512 nonzero
+values below 2^-16) run the two-kernel path's code in the workgroup (RowFilter.ik =
+kRowFallback); the rest are kRowDone. skyrl_tune("topp_probe", 5) sends every row through pass 2.
 The recipe this serves: top_p = 0.95 alone (examples/text_to_sql/run_skyrl_sql.sh:60 and eight
 more example scripts), semantics skyrl-tx/tx/utils/generator.py:423-449.
 """
@@ -155,5 +156,35 @@ def test_topp_fast_small_and_ragged_vocab(dev, V):
     for p, mp in ((0.9, 0.0), (1.0, 0.05), (0.7, 0.01)):
         tf, lf, _ = _ab(x, n, temperature=1.0, top_p=p, min_p=mp, seed=9, seq_ids=ids.to(dev), step=2)
         etok, elp = osamp.sample(base[:, :V].contiguous(), 1.0, -1, p, mp, 9, ids, 2)
+        assert torch.equal(tf, etok)
+        torch.testing.assert_close(lf, elp, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("V", [517, 4097, 50257, 151936])
+def test_every_row_through_pass2(dev, V):
+    """skyrl_tune("topp_probe", 5): no row decided in pass 1, so every row runs pass 2 (top_p: the
+    second launch's 8 pieces, the ragged tail in the last piece; min_p: in the workgroup), against
+    the two-kernel path and the oracle."""
+    from oracle import sampler as osamp
+
+    g = torch.Generator().manual_seed(V + 1)
+    n = 24
+    width = (V + 7) // 8 * 8 + 8
+    base = (torch.randn(n, width, generator=g) * 3).to(torch.bfloat16)
+    x = base.to(dev)[:, :V]
+    ids = torch.arange(n, dtype=torch.int64)
+    for p, mp in ((0.95, 0.0), (0.5, 0.0), (1.0, 0.05)):
+        ops._ffi.call("skyrl_tune", b"topp_probe", 5)
+        try:
+            tf, lf, ff = _run(x, True, temperature=1.0, top_p=p, min_p=mp, seed=4, seq_ids=ids.to(dev), step=9)
+        finally:
+            ops._ffi.call("skyrl_tune", b"topp_probe", 0)
+        ts, ls, fs = _run(x, False, temperature=1.0, top_p=p, min_p=mp, seed=4, seq_ids=ids.to(dev), step=9)
+        assert torch.equal(tf, ts), (V, p, mp, int((tf != ts).sum()))
+        assert torch.allclose(lf, ls, atol=2e-5, rtol=1e-5)
+        assert bool((ff[:, 2] == _ROW_DONE).all()) and bool((ff[:, 1] == 0).all())
+        if p < 1.0:
+            assert torch.equal(ff[:, 3], fs[:, 3]) and torch.equal(ff[:, 4], fs[:, 4])
+        etok, elp = osamp.sample(base[:, :V].contiguous(), 1.0, -1, p, mp, 4, ids, 9)
         assert torch.equal(tf, etok)
         torch.testing.assert_close(lf, elp, atol=1e-4, rtol=1e-4)
