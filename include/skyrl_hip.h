@@ -46,7 +46,8 @@ const char* skyrl_last_error(void);
  * the loss forwards take flags (SKYRL_LOSS_DEFER_FOLD) and skyrl_ppo_loss_finish; 6:
  * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange; 7:
  * skyrl_comm_* RCCL collectives; 8: the step form of the fused policy pass,
- * skyrl_policy_train_plan / _micro_fwd / _fold). */
+ * skyrl_policy_train_plan / _micro_fwd / _fold; 9: per-parameter AdamW,
+ * skyrl_adamw_seg_plan / _seg_update / _seg_tile). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -468,6 +469,27 @@ int skyrl_adamw_plan(const float* sumsq, const skyrl_adamw_params* hp, int32_t* 
                      float* grad_norm_out, void* stream);
 int skyrl_adamw_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_bf16,
                        int64_t n, const float* plan, float beta1, float beta2, void* stream);
+/* Per-parameter form for a module's parameters in one flat shard (torch.optim.AdamW over
+ * named parameters, fsdp_strategy.py:284-296: a parameter whose .grad is None is skipped and
+ * its own `step` is not advanced). touched i32[nparams]: 1 = some DP rank's backward reached
+ * the parameter since the last step (the caller MAX-all-reduces it on device). No host sync.
+ *   skyrl_adamw_seg_plan    as skyrl_adamw_plan, plus per parameter p: if touched[p],
+ *                           ++param_step[p] and coef f32[2*nparams] = (-lr/bc1, sqrt(bc2)) of
+ *                           its own count, else (0, 0). One launch of one workgroup.
+ *   skyrl_adamw_seg_update  as skyrl_adamw_update; shard element e belongs to segment s with
+ *                           seg_start[s] <= e < seg_start[s+1] (i64[nseg+1], seg_start[0] = 0,
+ *                           seg_start[nseg] = n) of parameter seg_owner[s] (i32[nseg]);
+ *                           tile_seg[t] (i32[ceil(n / skyrl_adamw_seg_tile())]) = the segment
+ *                           holding element t * tile. Untouched parameters' elements (param,
+ *                           moments, bf16 copy) are left as they are. When every parameter is
+ *                           touched at one common count it runs skyrl_adamw_update's loop. */
+int skyrl_adamw_seg_plan(const float* sumsq, const skyrl_adamw_params* hp, const int32_t* touched, int32_t nparams,
+                         int32_t* param_step, float* plan, float* coef, float* grad_norm_out, void* stream);
+int skyrl_adamw_seg_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_bf16,
+                           int64_t n, const float* plan, const float* coef, const int64_t* seg_start,
+                           const int32_t* seg_owner, int32_t nseg, const int32_t* tile_seg, float beta1, float beta2,
+                           void* stream);
+size_t skyrl_adamw_seg_tile(void);
 /* y = bf16(x), round-to-nearest-even: the learner -> rollout weight copy when the
  * optimizer ran without a bf16 shadow (FSDPWeightExtractor, fsdp_worker.py:30-87). */
 int skyrl_cast_bf16(const float* x, void* y, int64_t n, void* stream);

@@ -110,6 +110,36 @@ def main():
         return gn
 
     opt.step = checked_step
+    # REHEARSE_DELAY_GATHER=1 (one-rank RCCL): the comm stream sleeps before each in-flight
+    # re-assembly of the master, and every read of the policy's weights by the trainer's passes
+    # (base_model forward, the lm_head weight) checks on the reading stream that the weights it
+    # sees are the optimizer's updated shard: a pass that did not wait for the gather reads the
+    # previous step's weights (2 mini-batches per train_on)
+    weight_reads = {"checked": 0, "stale": 0}
+    if os.environ.get("REHEARSE_DELAY_GATHER") == "1" and opt.collective and world == 1:
+        orig_gather = opt._gather_full
+
+        def delayed_gather(sync):
+            with torch.cuda.stream(opt.reducer.stream):
+                torch.cuda._sleep(100_000_000)  # ~40 ms of spinning before the all-gather
+            return orig_gather(sync)
+
+        opt._gather_full = delayed_gather
+
+        def check_weights(*_):
+            n = opt.reducer.layout.numel  # one rank: the shard is the whole master in flat order
+            weight_reads["checked"] += 1
+            if not torch.equal(opt.full[:n], opt.opt.param[:n]):  # (syncs the reading stream only)
+                weight_reads["stale"] += 1
+
+        policy.base_model.register_forward_pre_hook(check_weights)
+        orig_emb = policy.get_output_embeddings
+
+        def checked_emb():
+            check_weights()
+            return orig_emb()
+
+        policy.get_output_embeddings = checked_emb
     init = torch.cat([p.detach().reshape(-1) for p in policy.parameters()]).clone()
     out = []
     ok_all = True
@@ -135,11 +165,12 @@ def main():
               and all(c["param_max_diff"] < 1e-6 and c["grad_norm_rel"] < 1e-5 for c in checks[-2:]))
         ok_all = ok_all and ok
         out.append(rec)
+    ok_all = ok_all and weight_reads["stale"] == 0
     if rank == 0:
         print(json.dumps({"world": world, "backend": dist.get_backend() if dist_on else None,
                           "collective_path": bool(opt.collective),
                           "reduce_scatters_from_backward": opt.launched_during_backward,
-                          "ok": ok_all, "steps": out}), flush=True)
+                          "weight_reads": weight_reads, "ok": ok_all, "steps": out}), flush=True)
     if dist_on:
         dist.destroy_process_group()
     if not ok_all:

@@ -170,6 +170,9 @@ SIGNATURES = {
     "skyrl_adamw_plan_floats": (_SZ, []),
     "skyrl_adamw_plan": (_INT, [_P, ctypes.POINTER(AdamWParams), _P, _P, _P, _P]),
     "skyrl_adamw_update": (_INT, [_P, _P, _P, _P, _P, _I64, _P, _F, _F, _P]),
+    "skyrl_adamw_seg_plan": (_INT, [_P, ctypes.POINTER(AdamWParams), _P, _I32, _P, _P, _P, _P, _P]),
+    "skyrl_adamw_seg_update": (_INT, [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _I32, _P, _F, _F, _P]),
+    "skyrl_adamw_seg_tile": (_SZ, []),
     "skyrl_cast_bf16": (_INT, [_P, _P, _I64, _P]),
     "skyrl_rope_kv_write": (_INT, [_P, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "skyrl_paged_decode_workspace_bytes": (_SZ, [_I32, _I32, _I32, _I32]),

@@ -265,7 +265,11 @@ class ShardedAdamW:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self._dev).cuda_stream)
 
-    def step(self, n_micro: int = 1, lr: Optional[float] = None, zero_grad: bool = True) -> torch.Tensor:
+    def step(self, n_micro: int = 1, lr: Optional[float] = None, zero_grad: bool = True,
+             seg: Optional["ParamSegments"] = None) -> torch.Tensor:
+        """With ``seg`` (a module's parameters) the update is per parameter: ``seg.touched``
+        (device, already reduced over ranks) selects the parameters to update, each with its own
+        step count, as torch.optim.AdamW does for named parameters (skyrl_adamw_seg_*)."""
         from .ops import _ptr
 
         cfg = self.cfg
@@ -278,11 +282,20 @@ class ShardedAdamW:
         hp = self._ffi.AdamWParams(float(cfg.lr if lr is None else lr), float(cfg.betas[0]), float(cfg.betas[1]),
                                    float(cfg.eps), float(cfg.weight_decay), float(cfg.max_grad_norm),
                                    1.0 / (max(1, n_micro) * r.world))
-        self._ffi.call("skyrl_adamw_plan", _ptr(self.sumsq), ctypes.byref(hp), _ptr(self.step_count), _ptr(self.plan),
-                       _ptr(self.grad_norm), self._stream())
-        self._ffi.call("skyrl_adamw_update", _ptr(self.param), _ptr(g), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
-                       _ptr(self.shard_bf16), self.param.numel(), _ptr(self.plan), float(cfg.betas[0]),
-                       float(cfg.betas[1]), self._stream())
+        if seg is None:
+            self._ffi.call("skyrl_adamw_plan", _ptr(self.sumsq), ctypes.byref(hp), _ptr(self.step_count),
+                           _ptr(self.plan), _ptr(self.grad_norm), self._stream())
+            self._ffi.call("skyrl_adamw_update", _ptr(self.param), _ptr(g), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
+                           _ptr(self.shard_bf16), self.param.numel(), _ptr(self.plan), float(cfg.betas[0]),
+                           float(cfg.betas[1]), self._stream())
+        else:
+            self._ffi.call("skyrl_adamw_seg_plan", _ptr(self.sumsq), ctypes.byref(hp), _ptr(seg.touched),
+                           seg.nparams, _ptr(seg.param_step), _ptr(self.plan), _ptr(seg.coef), _ptr(self.grad_norm),
+                           self._stream())
+            self._ffi.call("skyrl_adamw_seg_update", _ptr(self.param), _ptr(g), _ptr(self.exp_avg),
+                           _ptr(self.exp_avg_sq), _ptr(self.shard_bf16), self.param.numel(), _ptr(self.plan),
+                           _ptr(seg.coef), _ptr(seg.start), _ptr(seg.owner), seg.nseg, _ptr(seg.tile_seg),
+                           float(cfg.betas[0]), float(cfg.betas[1]), self._stream())
         if zero_grad:  # strategy.optimizer_step ends with optimizer.zero_grad()
             r.zero_grad()
         return self.grad_norm
@@ -620,6 +633,68 @@ class BucketedGradAllReduce:
 
 
 
+class ParamSegments:
+    """The per-parameter map of one rank's optimizer shard (skyrl_adamw_seg_update): segment s
+    covers shard elements [start[s], start[s+1]) of parameter owner[s]; the shard's padding
+    belongs to a pseudo-parameter (index nparams - 1) that is always updated (zeros stay zeros).
+    ``touched`` i32[nparams] is written per step from the host flags (pinned, non-blocking) and
+    MAX-reduced over the DP group on the device; ``param_step`` holds each parameter's AdamW
+    step count (torch.optim.AdamW's per-parameter ``state["step"]``)."""
+
+    def __init__(self, pieces: Sequence[Tuple[int, int, int]], n_real: int, shard_numel: int, device):
+        import numpy as np
+
+        from . import _ffi
+
+        pad = n_real  # the padding's pseudo-parameter
+        starts, owners = [], []
+        pos = 0
+        for off, n, i in sorted(pieces):
+            if n <= 0:
+                continue
+            if off > pos:
+                starts.append(pos)
+                owners.append(pad)
+            starts.append(off)
+            owners.append(i)
+            pos = off + n
+        if pos < shard_numel or not starts:
+            starts.append(pos)
+            owners.append(pad)
+        start = np.asarray(starts + [shard_numel], dtype=np.int64)
+        tile = int(_ffi.query("skyrl_adamw_seg_tile"))
+        tiles = np.arange(0, max(1, -(-shard_numel // tile)), dtype=np.int64) * tile
+        tile_seg = np.searchsorted(start, tiles, side="right") - 1
+        self.nparams = n_real + 1
+        self.nseg = len(owners)
+        self.start = torch.from_numpy(start).to(device)
+        self.owner = torch.tensor(owners, dtype=torch.int32, device=device)
+        self.tile_seg = torch.from_numpy(tile_seg.astype(np.int32)).to(device)
+        self.touched = torch.ones(self.nparams, dtype=torch.int32, device=device)
+        self.param_step = torch.zeros(self.nparams, dtype=torch.int32, device=device)
+        self.coef = torch.zeros(2 * self.nparams, dtype=torch.float32, device=device)
+        # two pinned staging buffers for the host flags: a buffer is rewritten only after the
+        # copy that read it two steps ago has completed (its event)
+        self._host = [torch.ones(self.nparams, dtype=torch.int32).pin_memory() for _ in range(2)]
+        self._ev: List[Optional[torch.cuda.Event]] = [None, None]
+        self._k = 0
+
+    def upload(self, flags: Sequence[bool], group=None, collective: bool = False) -> None:
+        """Stage this rank's flags and (collective) MAX-reduce them over the group: no host sync."""
+        k = self._k
+        self._k ^= 1
+        if self._ev[k] is not None:
+            self._ev[k].synchronize()  # the copy of two steps ago
+        h = self._host[k]
+        h[:-1] = torch.tensor([bool(f) for f in flags], dtype=torch.int32)
+        self.touched.copy_(h, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.touched.device))
+        self._ev[k] = ev
+        if collective:
+            dist.all_reduce(self.touched, op=dist.ReduceOp.MAX, group=group)
+
+
 class ShardedModuleOptimizer:
     """The HIP a12/a14 path for a module's parameters (the HF learner of GRPOTrainer): the
     reference's FSDP2 reduce-scatter + clip + AdamW (fsdp_strategy.py:155-191, 216-271) with
@@ -691,8 +766,24 @@ class ShardedModuleOptimizer:
         self._index = {id(p): i for i, (_, p) in enumerate(self.named)}
         self._touched = [False] * len(self.named)  # parameters a backward reached since the last step
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p in self.named]
+        # every piece of this rank's shard that belongs to a parameter: the per-parameter update
+        # (skip untouched parameters, per-parameter step counts) runs on this map on the device
+        pieces = []
+        for i, ((_, p), o) in enumerate(zip(self.named, self.offsets)):
+            b0, b1 = self._param_buckets[i]
+            for b in range(b0, b1 + 1):
+                ps, pe = lay.piece(b, self.rank) if self.collective else lay.buckets[b]
+                lo, hi = max(o, ps), min(o + p.numel(), pe)
+                if hi > lo:
+                    pieces.append(((lay.piece_off[b] + lo - ps) if self.collective else lo, hi - lo, i))
+        self.segments = ParamSegments(pieces, len(self.named), lay.shard_numel, dev)
         # the module's next forward reads the re-assembled master: it waits for the in-flight gather
-        self._fwd_hook = module.register_forward_pre_hook(lambda m, a: self.wait_weights())
+        # (callers that read the weights without calling the module -- the trainer's base_model /
+        # lm_head passes -- call wait_weights() themselves; base_model gets the same hook)
+        self._fwd_hooks = [module.register_forward_pre_hook(lambda m, a: self.wait_weights())]
+        base = getattr(module, "base_model", None)
+        if isinstance(base, torch.nn.Module) and base is not module:
+            self._fwd_hooks.append(base.register_forward_pre_hook(lambda m, a: self.wait_weights()))
         self._armed = False
         self.launched_during_backward = 0
 
@@ -756,44 +847,16 @@ class ShardedModuleOptimizer:
         norm (device scalar)."""
         self._finish_exchange()
         self._check_grad_views()  # the .grad views must still be the buckets' storage
-        keep = self._untouched_ranges()
-        saved = [(t, o, t[o:o + n].clone()) for o, n in keep
-                 for t in (self.opt.param, self.opt.exp_avg, self.opt.exp_avg_sq)]
-        gn = self.opt.step(n_micro=n_micro, lr=lr, zero_grad=True)
-        for t, o, v in saved:  # torch.optim.AdamW skips a parameter whose .grad is None
-            t[o:o + v.numel()].copy_(v)
+        # which parameters some rank's backward reached: this rank's flags staged from pinned host
+        # memory and MAX-reduced on the device (no host read). torch.optim.AdamW skips a parameter
+        # whose .grad is None and keeps a step count per parameter: the update pass does the same
+        # per shard segment (master, moments and bf16 copy of a skipped parameter untouched)
+        self.segments.upload(self._touched, group=self.reducer.group, collective=self.collective)
+        gn = self.opt.step(n_micro=n_micro, lr=lr, zero_grad=True, seg=self.segments)
         self._touched = [False] * len(self.named)
         if self.collective:
             self._gather_full(sync=False)
         return gn
-
-    def _untouched_ranges(self) -> List[Tuple[int, int]]:
-        """(shard offset, length) of every piece of this rank's shard that belongs to a parameter
-        no rank's backward reached since the last step (one MAX all-reduce of the flags at
-        world > 1). Their master weights and moments are restored after the update, as
-        torch.optim.AdamW and the reference's FSDP2 optimizer skip a None grad (their shared
-        step counter still advances, so a later update of such a parameter uses the global
-        step's bias correction)."""
-        flags = self._touched
-        if self.collective:
-            t = torch.tensor([int(f) for f in flags], dtype=torch.int32, device=self.full.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.reducer.group)
-            flags = [bool(f) for f in t.tolist()]
-        if all(flags):
-            return []
-        lay = self.reducer.layout
-        out = []
-        for i, f in enumerate(flags):
-            if f:
-                continue
-            o, n = self.offsets[i], self.named[i][1].numel()
-            b0, b1 = self._param_buckets[i]
-            for b in range(b0, b1 + 1):
-                ps, pe = lay.piece(b, self.rank) if self.collective else lay.buckets[b]
-                lo, hi = max(o, ps), min(o + n, pe)
-                if hi > lo:
-                    out.append((lay.piece_off[b] + lo - ps if self.collective else lo, hi - lo))
-        return out
 
     def wait_weights(self) -> None:
         """Make the current stream wait for the last step's all-gather + bf16 cast (no host sync)."""

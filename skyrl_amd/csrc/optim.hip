@@ -31,7 +31,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kThreads = 256;
 constexpr int kMaxPartials = 2048;
 
-enum { PLAN_SKIP = 0, PLAN_GMUL, PLAN_DECAY, PLAN_STEP, PLAN_BC2SQRT, PLAN_EPS, PLAN_N };
+// PLAN_UNIFORM (per-parameter form only): every parameter is updated this step and all share one
+// step count, so the update pass runs the plain loop on PLAN_STEP / PLAN_BC2SQRT
+enum { PLAN_SKIP = 0, PLAN_GMUL, PLAN_DECAY, PLAN_STEP, PLAN_BC2SQRT, PLAN_EPS, PLAN_UNIFORM, PLAN_N };
+constexpr int kSegTile = kThreads * 4;  // elements per tile of the per-parameter segment map
 
 __host__ __device__ inline int sumsq_blocks(int64_t n) {
     const int64_t per_block = (int64_t)kThreads * 4 * 8;  // 8 float4 per thread at least
@@ -112,6 +115,65 @@ __global__ void adamw_plan_kernel(const float* __restrict__ sumsq, skyrl_adamw_p
     plan[PLAN_STEP] = (float)(-((double)hp.lr / bc1));
     plan[PLAN_BC2SQRT] = (float)sqrt(bc2);
     plan[PLAN_EPS] = hp.eps;
+    plan[PLAN_UNIFORM] = 1.f;
+}
+
+// Per-parameter plan (torch.optim.AdamW over a module: a parameter whose .grad is None is
+// skipped and its own `step` state is not advanced, so its bias corrections follow its own count).
+// One workgroup: the global clip / finiteness as adamw_plan_kernel, then per parameter p
+// (touched[p] = some rank's backward reached it since the last step): step[p] += 1 and
+// coef[2p..2p+1] = (-lr / bc1(step[p]), sqrt(bc2(step[p]))), or (0, 0) = leave p untouched.
+// PLAN_UNIFORM = every parameter touched and all counts equal (the update then runs the plain
+// loop on coef[0..1] as PLAN_STEP / PLAN_BC2SQRT).
+__global__ __launch_bounds__(kThreads) void adamw_seg_plan_kernel(const float* __restrict__ sumsq,
+                                                                   skyrl_adamw_params hp,
+                                                                   const int32_t* __restrict__ touched, int nparams,
+                                                                   int32_t* __restrict__ pstep, float* __restrict__ plan,
+                                                                   float* __restrict__ coef,
+                                                                   float* __restrict__ grad_norm_out) {
+    const float norm = sqrtf(fmaxf(sumsq[0], 0.f)) * hp.grad_scale;
+    float clip = 1.f;
+    if (hp.max_grad_norm > 0.f) clip = fminf(hp.max_grad_norm / (norm + 1e-6f), 1.f);
+    const bool finite = isfinite(norm) || hp.max_grad_norm <= 0.f;
+    if (threadIdx.x == 0 && grad_norm_out) grad_norm_out[0] = norm;
+    if (!finite) {  // fsdp_strategy.py:178-186: no step, no count advanced
+        if (threadIdx.x == 0) plan[PLAN_SKIP] = 1.f;
+        return;
+    }
+    __shared__ int s_first;
+    if (threadIdx.x == 0) s_first = touched[0] ? pstep[0] + 1 : -1;
+    __syncthreads();
+    const int first = s_first;
+    int uniform = 1;
+    for (int p = threadIdx.x; p < nparams; p += kThreads) {
+        if (touched[p]) {
+            const int step = pstep[p] + 1;
+            pstep[p] = step;
+            const double bc1 = 1.0 - pow((double)hp.beta1, (double)step);
+            const double bc2 = 1.0 - pow((double)hp.beta2, (double)step);
+            coef[2 * p] = (float)(-((double)hp.lr / bc1));
+            coef[2 * p + 1] = (float)sqrt(bc2);
+            uniform &= step == first;
+        } else {
+            coef[2 * p] = 0.f;
+            coef[2 * p + 1] = 0.f;
+            uniform = 0;
+        }
+    }
+    uniform = __syncthreads_and(uniform);
+    if (threadIdx.x == 0) {
+        plan[PLAN_SKIP] = 0.f;
+        plan[PLAN_GMUL] = hp.grad_scale * clip;
+        plan[PLAN_DECAY] = 1.f - hp.lr * hp.weight_decay;
+        plan[PLAN_EPS] = hp.eps;
+        plan[PLAN_UNIFORM] = uniform ? 1.f : 0.f;
+        if (uniform) {  // the plain loop's constants: every parameter's (equal) step
+            const double bc1 = 1.0 - pow((double)hp.beta1, (double)first);
+            const double bc2 = 1.0 - pow((double)hp.beta2, (double)first);
+            plan[PLAN_STEP] = (float)(-((double)hp.lr / bc1));
+            plan[PLAN_BC2SQRT] = (float)sqrt(bc2);
+        }
+    }
 }
 
 struct AdamPlan {
@@ -127,11 +189,88 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     p = p + a.step * (m / denom);           // addcdiv_(m, denom, value=-lr/bc1)
 }
 
+// The per-parameter segment map of a shard: segment s covers shard elements [start[s], start[s+1])
+// of parameter owner[s] (segments cover the shard, padding included); tile_seg[t] = the segment
+// holding element t * kSegTile. Elements of an untouched parameter (coef (0, 0)) are left as they
+// are; a vector none of whose elements is updated is not stored.
+struct SegMap {
+    const int64_t* start;
+    const int32_t* owner;
+    const int32_t* tile_seg;
+    const float* coef;
+};
+
+__device__ __forceinline__ int seg_of(const SegMap& sm, int s, int64_t e) {
+    while (sm.start[s + 1] <= e) ++s;
+    return s;
+}
+
+template <bool SHADOW>
+__device__ void adamw_seg_loop(float* __restrict__ param, const float* __restrict__ grad, float* __restrict__ exp_avg,
+                               float* __restrict__ exp_avg_sq, uint16_t* __restrict__ shadow, int64_t n, AdamPlan a,
+                               const SegMap& sm) {
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    f32x4* p4 = reinterpret_cast<f32x4*>(param);
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(grad);
+    f32x4* m4 = reinterpret_cast<f32x4*>(exp_avg);
+    f32x4* v4 = reinterpret_cast<f32x4*>(exp_avg_sq);
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += stride) {
+        int s = seg_of(sm, sm.tile_seg[(i << 2) / kSegTile], i << 2);
+        const f32x4 pv = p4[i];
+        const f32x4 gv = __builtin_nontemporal_load(g4 + i);
+        const f32x4 mv = m4[i];
+        const f32x4 vv = v4[i];
+        float p[4] = {pv.x, pv.y, pv.z, pv.w}, m[4] = {mv.x, mv.y, mv.z, mv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+        const float g[4] = {gv.x, gv.y, gv.z, gv.w};
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s = seg_of(sm, s, (i << 2) + k);
+            const int o = sm.owner[s];
+            const float st = sm.coef[2 * o], b2s = sm.coef[2 * o + 1];
+            if (b2s != 0.f) {
+                AdamPlan b = a;
+                b.step = st;
+                b.bc2s = b2s;
+                adam_elem(p[k], g[k], m[k], v[k], b);
+                any = true;
+            }
+        }
+        if (!any) continue;
+        p4[i] = f32x4{p[0], p[1], p[2], p[3]};
+        __builtin_nontemporal_store(f32x4{m[0], m[1], m[2], m[3]}, m4 + i);
+        __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, v4 + i);
+        if (SHADOW) {
+            uint2 sh;
+            sh.x = pack_bf16x2(p[0], p[1]);
+            sh.y = pack_bf16x2(p[2], p[3]);
+            reinterpret_cast<uint2*>(shadow)[i] = sh;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const int64_t k = (n4 << 2) + threadIdx.x;
+        const int s = seg_of(sm, sm.tile_seg[k / kSegTile], k);
+        const int o = sm.owner[s];
+        if (sm.coef[2 * o + 1] == 0.f) return;
+        AdamPlan b = a;
+        b.step = sm.coef[2 * o];
+        b.bc2s = sm.coef[2 * o + 1];
+        float pk = param[k], mk = exp_avg[k], vk = exp_avg_sq[k];
+        adam_elem(pk, grad[k], mk, vk, b);
+        param[k] = pk;
+        exp_avg[k] = mk;
+        exp_avg_sq[k] = vk;
+        if (SHADOW) shadow[k] = f32_to_bf16(pk);
+    }
+}
+
 template <bool SHADOW>
 __global__ __launch_bounds__(kThreads) void adamw_update_kernel(float* __restrict__ param, const float* __restrict__ grad,
                                                                  float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
                                                                  uint16_t* __restrict__ shadow, int64_t n,
-                                                                 const float* __restrict__ plan, float beta1, float beta2) {
+                                                                 const float* __restrict__ plan, float beta1, float beta2,
+                                                                 SegMap sm) {
     if (plan[PLAN_SKIP] != 0.f) return;
     AdamPlan a;
     a.gmul = plan[PLAN_GMUL];
@@ -142,6 +281,10 @@ __global__ __launch_bounds__(kThreads) void adamw_update_kernel(float* __restric
     a.omb1 = 1.f - beta1;
     a.b2 = beta2;
     a.omb2 = 1.f - beta2;
+    if (sm.start && plan[PLAN_UNIFORM] == 0.f) {  // some parameter skipped or behind: per-parameter loop
+        adamw_seg_loop<SHADOW>(param, grad, exp_avg, exp_avg_sq, shadow, n, a, sm);
+        return;
+    }
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * kThreads;
     f32x4* p4 = reinterpret_cast<f32x4*>(param);
@@ -252,12 +395,54 @@ extern "C" int skyrl_adamw_update(float* param, const float* grad, float* exp_av
                   "adamw_update: bf16 copy must be 8-byte aligned");
     const unsigned nb = stream_blocks(n);
     hipStream_t s = as_stream(stream);
+    const SegMap none{nullptr, nullptr, nullptr, nullptr};
     if (param_bf16) {
         hipLaunchKernelGGL(adamw_update_kernel<true>, dim3(nb), dim3(kThreads), 0, s, param, grad, exp_avg, exp_avg_sq,
-                           reinterpret_cast<uint16_t*>(param_bf16), n, plan, beta1, beta2);
+                           reinterpret_cast<uint16_t*>(param_bf16), n, plan, beta1, beta2, none);
     } else {
         hipLaunchKernelGGL(adamw_update_kernel<false>, dim3(nb), dim3(kThreads), 0, s, param, grad, exp_avg,
-                           exp_avg_sq, nullptr, n, plan, beta1, beta2);
+                           exp_avg_sq, nullptr, n, plan, beta1, beta2, none);
+    }
+    return check_launch("adamw_update_kernel");
+}
+
+extern "C" size_t skyrl_adamw_seg_tile(void) { return kSegTile; }
+
+extern "C" int skyrl_adamw_seg_plan(const float* sumsq, const skyrl_adamw_params* hp, const int32_t* touched,
+                                    int32_t nparams, int32_t* param_step, float* plan, float* coef,
+                                    float* grad_norm_out, void* stream) {
+    SKYRL_REQUIRE(sumsq && hp && touched && param_step && plan && coef, "adamw_seg_plan: null pointer");
+    SKYRL_REQUIRE(nparams >= 1, "adamw_seg_plan: nparams < 1");
+    SKYRL_REQUIRE(hp->lr >= 0.f && hp->eps >= 0.f && hp->beta1 >= 0.f && hp->beta1 < 1.f && hp->beta2 >= 0.f &&
+                      hp->beta2 < 1.f,
+                  "adamw_seg_plan: invalid hyper-parameters");
+    hipLaunchKernelGGL(adamw_seg_plan_kernel, dim3(1), dim3(kThreads), 0, as_stream(stream), sumsq, *hp, touched,
+                       nparams, param_step, plan, coef, grad_norm_out);
+    return check_launch("adamw_seg_plan_kernel");
+}
+
+extern "C" int skyrl_adamw_seg_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                                      void* param_bf16, int64_t n, const float* plan, const float* coef,
+                                      const int64_t* seg_start, const int32_t* seg_owner, int32_t nseg,
+                                      const int32_t* tile_seg, float beta1, float beta2, void* stream) {
+    SKYRL_REQUIRE(n >= 0, "adamw_seg_update: n < 0");
+    if (n == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(param && grad && exp_avg && exp_avg_sq && plan && coef && seg_start && seg_owner && tile_seg,
+                  "adamw_seg_update: null pointer");
+    SKYRL_REQUIRE(nseg >= 1, "adamw_seg_update: nseg < 1");
+    SKYRL_REQUIRE(aligned16(param) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq),
+                  "adamw_seg_update: fp32 buffers must be 16-byte aligned");
+    SKYRL_REQUIRE(!param_bf16 || (reinterpret_cast<uintptr_t>(param_bf16) & 7) == 0,
+                  "adamw_seg_update: bf16 copy must be 8-byte aligned");
+    const unsigned nb = stream_blocks(n);
+    hipStream_t s = as_stream(stream);
+    const SegMap sm{seg_start, seg_owner, tile_seg, coef};
+    if (param_bf16) {
+        hipLaunchKernelGGL(adamw_update_kernel<true>, dim3(nb), dim3(kThreads), 0, s, param, grad, exp_avg, exp_avg_sq,
+                           reinterpret_cast<uint16_t*>(param_bf16), n, plan, beta1, beta2, sm);
+    } else {
+        hipLaunchKernelGGL(adamw_update_kernel<false>, dim3(nb), dim3(kThreads), 0, s, param, grad, exp_avg,
+                           exp_avg_sq, nullptr, n, plan, beta1, beta2, sm);
     }
     return check_launch("adamw_update_kernel");
 }

@@ -160,9 +160,18 @@ class GRPOTrainer:
                 "loss_masks": [[1] * len(r) for r in out["response_ids"]]}
 
     # ---------------------------------------------------------------- model passes
+    def _wait_weights(self, model) -> None:
+        """The policy's parameters are views of the HIP optimizer's master, which the previous
+        optimizer step re-assembles on the comm stream (world > 1, left in flight): a pass that
+        reads them -- base_model and the lm_head weight, not through the module's own forward --
+        makes the current stream wait for that all-gather first (no host sync)."""
+        if self.optim is not None and model is self.policy:
+            self.optim.wait_weights()
+
     def _logprobs(self, model, seq, att, R, grad: bool):
         """action log-probs (and entropy) of the last R positions: HFModelWrapper.forward
         (model_wrapper.py:261-375) with the lm_head-fused HIP logprob/entropy."""
+        self._wait_weights(model)
         with torch.autocast("cuda", dtype=torch.bfloat16), torch.set_grad_enabled(grad):
             base = model.base_model  # model.model (Qwen2/Llama), model.transformer (GPT-2)
             if self.cfg.use_sample_packing:
@@ -404,6 +413,7 @@ class GRPOTrainer:
         if pos.numel() == 0:
             return None
         model = self.policy
+        self._wait_weights(model)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             base = model.base_model
             if self.cfg.use_sample_packing:

@@ -59,15 +59,47 @@ def _dry(gpus):
 
 def test_gpus_2_spawns_two_ranks():
     """`python bench.py --gpus 2` (no launcher env) starts two ranks under torch.distributed.run
-    with WORLD_SIZE=2 and a working 127.0.0.1 rendezvous; --dry-run stops before GPU work."""
-    recs = _dry(2)
-    assert sorted(r["rank"] for r in recs) == [0, 1]
+    with WORLD_SIZE=2 and a working 127.0.0.1 rendezvous; --dry-run stops before GPU work. The
+    ranks split ONE 512-trajectory batch by whole prompt groups (SURVEY §8(e), strong scaling)."""
+    recs = sorted(_dry(2), key=lambda r: r["rank"])
+    assert [r["rank"] for r in recs] == [0, 1]
     assert {r["world_size"] for r in recs} == {2} and {r["local_rank"] for r in recs} == {0, 1}
     assert {r["rank_sum"] for r in recs} == {1}  # the gloo all-reduce across both ranks ran
     assert {r["master_addr"] for r in recs} == {"127.0.0.1"} and {r["collectives"] for r in recs} == {"nccl"}
+    assert [r["rows"] for r in recs] == [[0, 256], [256, 512]]
+    assert [r["prompt_groups"] for r in recs] == [[0, 32], [32, 64]]
+    assert {r["global_batch"] for r in recs} == {512} and {r["scaling"] for r in recs} == {"strong"}
+
+
+def test_gpus_4_row_ranges():
+    recs = sorted(_dry(4), key=lambda r: r["rank"])
+    assert [r["rows"] for r in recs] == [[0, 128], [128, 256], [256, 384], [384, 512]]
 
 
 def test_gpus_1_stays_in_process():
     recs = _dry(1)
     assert recs == [{"dry_run": True, "rank": 0, "world_size": 1, "local_rank": 0, "gpus": 1, "master_addr": None,
-                     "rank_sum": 0, "collectives": "none (world size 1)"}]
+                     "rank_sum": 0, "collectives": "none (world size 1)", "scaling": "strong", "global_batch": 512,
+                     "rows": [0, 512], "prompt_groups": [0, 64]}]
+
+
+def test_rank_rows_partition_the_global_batch():
+    """The 8 ranks' inputs are the N = 1 batch cut into contiguous whole-group chunks
+    (dispatch.py:122-141): concatenated, they are the global batch element for element."""
+    import torch
+
+    full, uids = bench.synth_inputs("cpu", 512)
+    for world in (2, 4, 8):
+        parts = [bench.synth_inputs("cpu", 512, row0=r * 512 // world, rows=512 // world) for r in range(world)]
+        assert [u for _, us in parts for u in us] == uids
+        for k in ("plens", "rlens", "ptok", "rtok", "rew", "lmask", "rlp"):
+            assert torch.equal(torch.cat([p[k] for p, _ in parts]), full[k]), (world, k)
+        for p, _ in parts:
+            assert int(p["poff"][0]) == 0 and int(p["roff"][-1]) == len(p["rtok"])
+            assert int(p["poff"][-1]) == len(p["ptok"])
+        assert [bench.rank_rows(512, world, r) for r in range(world)] == [(r * 512 // world, 512 // world)
+                                                                           for r in range(world)]
+    import pytest
+
+    with pytest.raises(ValueError):
+        bench.rank_rows(512, 128, 0)  # 4 rows per rank would cut prompt groups of 8

@@ -100,18 +100,20 @@ def test_cast_bf16_round_to_nearest_even(dev):
 
 def test_module_optimizer_skips_parameters_without_grad(dev):
     """ShardedModuleOptimizer (the trainer's "hip" optimizer) on a module with a parameter no
-    backward reaches: like torch.optim.AdamW with a None grad, that parameter (and its moments)
-    stay as they were, while the used ones match torch AdamW + clip_grad_norm_ (1e-6). Then the
-    parameter is used and is updated (with the shared step counter's bias correction)."""
+    backward reaches: like torch.optim.AdamW with a None grad, that parameter, its moments and
+    its bf16 engine copy stay as they were, while the used ones match torch AdamW +
+    clip_grad_norm_ (1e-6). Then the parameter is used and is updated with its OWN step count's
+    bias correction (torch's per-parameter state["step"]), on the device (no host read)."""
 
     class M(torch.nn.Module):
         def __init__(self):
             super().__init__()
             self.a = torch.nn.Linear(64, 32)
             self.unused = torch.nn.Parameter(torch.randn(1000))
+            self.b = torch.nn.Linear(16, 3)  # odd sizes: segments that do not start on a 16-B vector
 
         def forward(self, x, use=False):
-            y = self.a(x).square().mean()
+            y = self.a(x).square().mean() + self.b(x[:, :16]).sum()
             return y + self.unused.sum() if use else y
 
     torch.manual_seed(0)
@@ -122,8 +124,10 @@ def test_module_optimizer_skips_parameters_without_grad(dev):
     opt = comm.ShardedModuleOptimizer(m, cfg)
     topt = torch.optim.AdamW(ref.parameters(), lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay)
     u0 = m.unused.detach().clone()
-    for it in range(3):
-        use = it == 2
+    named_bf16 = dict(opt.named_bf16())
+    ub0 = named_bf16["unused"].clone()
+    for it in range(5):
+        use = it in (2, 4)
         x = torch.randn(8, 64, device=dev)
         m(x, use).backward()
         opt.step(1)
@@ -131,10 +135,13 @@ def test_module_optimizer_skips_parameters_without_grad(dev):
         torch.nn.utils.clip_grad_norm_(ref.parameters(), cfg.max_grad_norm)
         topt.step()
         topt.zero_grad(set_to_none=True)
-        if not use:
+        if it < 2:
             assert torch.equal(m.unused.detach(), u0)
+            assert torch.equal(dict(opt.named_bf16())["unused"], ub0)  # the engine copy too (world 1)
         for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
-            if n == "unused" and use:  # torch counts this parameter's steps from its first grad (1), the
-                continue               # flat optimizer from the shared counter (3): another bias correction
-            torch.testing.assert_close(p.detach(), q.detach(), atol=1e-6, rtol=1e-5, msg=n)
+            torch.testing.assert_close(p.detach(), q.detach(), atol=1e-6, rtol=1e-5, msg=f"{n} step {it}")
+        for n, w in opt.named_bf16():
+            assert torch.equal(w, dict(m.named_parameters())[n].detach().to(torch.bfloat16)), n
     assert not torch.equal(m.unused.detach(), u0)
+    steps = opt.segments.param_step.tolist()
+    assert steps[opt._index[id(m.unused)]] == 2 and max(steps) == 5  # per-parameter counts

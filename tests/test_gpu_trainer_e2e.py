@@ -82,7 +82,7 @@ def test_data_parallel_trainer_two_ranks_one_gpu():
     assert all(s["logprobs_diff_mean"] < 0.02 for s in res["steps"])
 
 
-def _run_optim_rehearsal(nproc, rccl_solo=False):
+def _run_optim_rehearsal(nproc, rccl_solo=False, extra_env=None):
     import json
     import os
     import socket
@@ -92,6 +92,7 @@ def _run_optim_rehearsal(nproc, rccl_solo=False):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = os.path.join(root, "scripts", "rehearse_trainer_optim.py")
     env = dict(os.environ)
+    env.update(extra_env or {})
     if rccl_solo:
         env.update(SKYRL_FORCE_COLLECTIVES="1", REHEARSE_BACKEND="nccl")
     if nproc == 1 and not rccl_solo:
@@ -130,6 +131,16 @@ def test_hip_optimizer_trainer_over_rccl_one_rank():
     res = _run_optim_rehearsal(1, rccl_solo=True)
     assert res["world"] == 1 and res["backend"] == "nccl" and res["collective_path"]
     assert res["reduce_scatters_from_backward"] > 0 and len(res["steps"]) == 3
+
+
+def test_trainer_passes_wait_for_the_in_flight_weight_gather():
+    """the optimizer's fp32 re-assembly of the master is left in flight on the
+    comm stream, and the trainer's passes read the weights through base_model and the lm_head
+    weight, not the module's forward. With the comm stream held back ~40 ms before each gather
+    and 2 mini-batches (2 optimizer steps) per train_on, every weight read of the trainer's passes
+    must see the updated master (checked on the reading stream), over one-rank RCCL."""
+    res = _run_optim_rehearsal(1, rccl_solo=True, extra_env={"REHEARSE_DELAY_GATHER": "1"})
+    assert res["weight_reads"]["checked"] >= 12 and res["weight_reads"]["stale"] == 0, res["weight_reads"]
 
 
 def test_fused_policy_pass_matches_chunked_lmhead_path():
