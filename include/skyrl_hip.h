@@ -47,7 +47,7 @@ const char* skyrl_last_error(void);
  * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange; 7:
  * skyrl_comm_* RCCL collectives; 8: the step form of the fused policy pass,
  * skyrl_policy_train_plan / _micro_fwd / _fold; 9: per-parameter AdamW,
- * skyrl_adamw_seg_plan / _seg_update / _seg_tile). */
+ * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -381,6 +381,12 @@ int skyrl_policy_train_fold(const float* loss_mask, int32_t n_total, int32_t R, 
 /* 1 if the packed and step forms take vocabulary V (aligned: rows 16-B aligned and V % 8 == 0)
  * at this temperature, else 0: the same plan their launches make. */
 int skyrl_policy_train_supports(int32_t V, int32_t aligned, float temperature);
+/* Test infrastructure (never on the hot path): `blocks` workgroups of `threads` threads that each
+ * spin on the 100 MHz constant clock for base_ticks + (block % 64) * step_ticks, holding their
+ * CU slots: the co-residency test runs the split training pass beside it on another stream (its
+ * pieces then arrive spread over time; a piece whose partner is late computes that partner's state
+ * itself, header word 33 of the policy_train workspace counts those states). */
+int skyrl_debug_occupy(int32_t blocks, int32_t threads, int64_t base_ticks, int64_t step_ticks, void* stream);
 /* x[i] *= g[0] over a bf16 buffer; a no-op kernel when g[0] == 1. */
 int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream);
 

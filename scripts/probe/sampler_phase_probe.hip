@@ -10,3 +10,8 @@ extern "C" int probe_read(void* host, size_t bytes) {
 }
 
 extern "C" void probe_set_row(int v) { skyrl::g_sampler_row = v; }
+
+extern "C" int probe_clear() {
+    static uint64_t zeros[4096 * 8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sphase), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+}

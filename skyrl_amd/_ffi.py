@@ -156,6 +156,7 @@ SIGNATURES = {
     ),
     "skyrl_policy_train_fold": (_INT, [_P, _I32, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P]),
     "skyrl_policy_train_supports": (_INT, [_I32, _I32, _F]),
+    "skyrl_debug_occupy": (_INT, [_I32, _I32, _I64, _I64, _P]),
     "skyrl_scale_bf16_by_device_scalar": (_INT, [_P, _P, _I64, _P]),
     "skyrl_sample_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_sample": (_INT, [_P, _INT, _I64, _I32, _I32, _F, _I32, _F, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),

@@ -215,12 +215,16 @@ extern int g_train_resident_nt;
 extern int g_train_ntstore;
 extern int g_train_split;
 extern int g_train_split_shape;
+extern unsigned g_train_split_wait;
 extern int g_grpo_slices;
 extern int g_loss_units;
 extern int g_loss_bwd_blocks;
 extern int g_grpo_loss_rpb;
 extern int g_finish_mode;
 extern int g_sampler_row;
+extern int g_sampler_split_rows;
+extern int g_sampler_split_wgs;
+extern int g_sampler_split_gran;
 extern int g_sampler_topk_fast;
 extern int g_sampler_topp_fast;
 extern int g_probe_topp;
@@ -239,6 +243,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "train_split_shape") {
         SKYRL_REQUIRE(value >= 0 && value <= 5, "skyrl_tune: train_split_shape must be 0..5");
         g_train_split_shape = value;
+        return SKYRL_OK;
+    }
+    if (k == "train_split_wait") {  // 0: a piece computes every partner state not yet published (tests)
+        SKYRL_REQUIRE(value >= 0 && value <= 100000000, "skyrl_tune: train_split_wait must be in [0, 1e8] ticks");
+        g_train_split_wait = (unsigned)value;
         return SKYRL_OK;
     }
     if (k == "train_split") {
@@ -288,6 +297,22 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "sampler_row") {
         SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_row must be 0 or 1");
         g_sampler_row = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_split_rows") {
+        SKYRL_REQUIRE(value >= 1 && value <= 1024, "skyrl_tune: sampler_split_rows must be in [1, 1024]");
+        g_sampler_split_rows = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_split_wgs") {
+        SKYRL_REQUIRE(value >= 64 && value <= 16384, "skyrl_tune: sampler_split_wgs must be in [64, 16384]");
+        g_sampler_split_wgs = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_split_gran") {
+        SKYRL_REQUIRE(value >= 2048 && value <= 65536 && value % 2048 == 0,
+                      "skyrl_tune: sampler_split_gran must be a multiple of 2048 in [2048, 65536]");
+        g_sampler_split_gran = value;
         return SKYRL_OK;
     }
     if (k == "sampler_topk_fast") {

@@ -535,10 +535,12 @@ __global__ __launch_bounds__(NT) void policy_train_resident_kernel(
 // (metrics[6] = 1 via the epilogue; ops.check_loss_metrics raises) and leaves NaN in that
 // row's terms instead of hanging.
 constexpr int kSplitMaxP = 12;  // most pieces per row of any built shape (split_shapes below)
-// the exchange's time bound, on the 100 MHz constant clock (s_memrealtime): partners are resident
-// or next to be dispatched, so they arrive within microseconds unless other streams' kernels hold
-// the CUs; 2 s lets any such kernel finish, where an iteration bound (~60 ms) did not
-constexpr uint64_t kSplitTimeoutTicks = 200000000ull;
+// how long a piece waits for a partner's published state, on the 100 MHz constant clock
+// (s_memrealtime): partners are consecutive blocks, resident or next to be dispatched, and
+// publish within microseconds; past this bound (other streams' kernels holding the CUs, a grid
+// larger than what is resident) the piece computes the partner's state itself (no deadlock, no
+// error path, the same bits)
+constexpr unsigned kSplitWaitTicks = 5000u;  // 50 us (skyrl_tune("train_split_wait", ticks) for tests)
 
 typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
 typedef __attribute__((address_space(1))) unsigned ptr_gu32;
@@ -550,11 +552,13 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
     const float* __restrict__ mask, const float* __restrict__ ref, const float* __restrict__ row_scale,
     const float* __restrict__ scal, skyrl_ppo_params p, float* __restrict__ logp_out, float* __restrict__ ent_out,
     float* __restrict__ tok, uint16_t* __restrict__ dx, int64_t gsb, int64_t gst, bool nts,
-    unsigned long long* __restrict__ gran, unsigned* __restrict__ err_word, const int32_t* __restrict__ tpos) {
+    unsigned long long* __restrict__ gran, unsigned* __restrict__ err_word, const int32_t* __restrict__ tpos,
+    unsigned wait_ticks) {
     static_assert(P <= 16 && NT % 64 == 0 && NT <= 1024, "split shape");
     __shared__ St s_st[NT / 64];
     __shared__ float s_g[4];
     __shared__ float s_part[P * 3];
+    __shared__ unsigned s_missing;  // partners whose state this piece computes itself
     // block -> (row, piece): consecutive blocks. (Placing a row's pieces on one XCD, so the
     // exchange stays in that XCD's L2, measured slower: 2.05 vs 1.71 ms per 16 x 1024 tokens,
     // profiles/r03_kbench_split.json; so did longer sleeps between polls, no change.)
@@ -637,24 +641,35 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
         st_add8(st, x);
         __builtin_amdgcn_sched_barrier(0);
     }
+    // a piece's state from its threads' states: the xor butterfly in each wave, then (wave 0) an
+    // xor tree over the NT/64 wave states, at least 4 lanes wide so lanes 0..2, which publish
+    // m, s, w, all hold it. Shared by this piece's own state and a partner state recomputed
+    // below, so both give the same bits.
+    auto wave_fold = [&](St x) -> St {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        St o{__shfl_xor(st.m, off, kWave), __shfl_xor(st.s, off, kWave), __shfl_xor(st.w, off, kWave)};
-        st_merge(st, o);
-    }
-    if (lane == 0) s_st[threadIdx.x / kWave] = st;
-    __syncthreads();
-    if (threadIdx.x < kWave) {
-        // this piece's state: an xor tree over the NT/64 wave states (lanes beyond them hold the
-        // empty state), at least 4 lanes wide so lanes 0..2, which publish m, s, w, all hold it
+        for (int off = 32; off > 0; off >>= 1) {
+            St o{__shfl_xor(x.m, off, kWave), __shfl_xor(x.s, off, kWave), __shfl_xor(x.w, off, kWave)};
+            st_merge(x, o);
+        }
+        return x;
+    };
+    auto piece_tree = [&]() -> St {  // wave 0, after the barrier that follows the s_st writes
         St a = threadIdx.x < NT / 64 ? s_st[threadIdx.x] : St{-3.402823466e38f, 0.f, 0.f};
 #pragma unroll
         for (int off = (NT / 128 > 2 ? NT / 128 : 2); off > 0; off >>= 1) {
             St o{__shfl_xor(a.m, off, kWave), __shfl_xor(a.s, off, kWave), __shfl_xor(a.w, off, kWave)};
             st_merge(a, o);
         }
+        return a;
+    };
+    st = wave_fold(st);
+    if (lane == 0) s_st[threadIdx.x / kWave] = st;
+    if (threadIdx.x == 0) s_missing = 0u;
+    __syncthreads();
+    if (threadIdx.x < kWave) {
+        const St a = piece_tree();
         unsigned long long* g = gran + r * (P * 3);
-        // lanes 0..2 publish (m, s, w) of this quarter; lanes 3q..3q+2 of the other quarters poll
+        // lanes 0..2 publish (m, s, w) of this piece; lanes 3q..3q+2 of the other pieces poll
         const int q = lane / 3, f = lane % 3;
         const float mine = f == 0 ? a.m : (f == 1 ? a.s : a.w);
         if (lane < 3) {
@@ -669,14 +684,75 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
             for (;;) {
                 x = __hip_atomic_load((const ptr_gu64*)(g + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((unsigned)(x >> 32) == epoch) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kSplitTimeoutTicks) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > wait_ticks) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            const bool ok = (unsigned)(x >> 32) == epoch;
-            s_part[lane] = ok ? __uint_as_float((unsigned)x) : __builtin_nanf("");
-            if (!ok) __hip_atomic_store((ptr_gu32*)err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(x >> 32) == epoch) s_part[lane] = __uint_as_float((unsigned)x);
+            else atomicOr(&s_missing, 1u << q);  // LDS
         }
-        __builtin_amdgcn_wave_barrier();  // wave 0's LDS writes above precede its reads below
+    }
+    __syncthreads();
+    const unsigned missing = s_missing;  // workgroup-uniform
+    if (missing != 0u) {
+        // A partner not published within the bound (not resident: other streams' kernels hold
+        // the CUs, or the grid outgrew what is resident at once): this workgroup computes that
+        // partner's state itself from the partner's slice of the row, with the partner's own
+        // loads, masking, summation order and trees, so the bits are the ones the partner
+        // publishes (or already did). No piece ever waits on a partner being dispatched.
+        for (int pp = 0; pp < P; ++pp) {
+            if (!((missing >> pp) & 1u)) continue;
+            const int plo = pp * per;
+            const int pnq = min(nvec, plo + per) - plo;
+            const uint4* prv = reinterpret_cast<const uint4*>(row - h) + plo;
+            St ps{-3.402823466e38f, 0.f, 0.f};
+#pragma unroll 1
+            for (int k = 0; k < NV; ++k) {
+                const int idx = threadIdx.x + k * NT;
+                const bool ok = idx < pnq;
+                uint4 w4;
+                if (!EDGE && k < NV - 1) {
+                    w4 = ld_nt(prv + idx);
+                } else {
+                    const uint4 t4 = ld_nt(prv + (ok ? idx : (EDGE ? 0 : pnq - 1)));
+                    w4 = make_uint4(ok ? t4.x : kNinf2, ok ? t4.y : kNinf2, ok ? t4.z : kNinf2, ok ? t4.w : kNinf2);
+                }
+                if constexpr (EDGE) {
+                    const int sl = h - 8 * (plo + idx), sh = V + h - 8 * (plo + idx);
+                    if (ok && (sl > 0 || sh < 8)) {
+                        uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            if (j < sl || j >= sh) {
+                                const uint32_t keep = (j & 1) ? 0x0000ffffu : 0xffff0000u;
+                                wv[j >> 1] = (wv[j >> 1] & keep) | (kNinf2 & ~keep);
+                            }
+                        }
+                        w4 = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                    }
+                }
+                float x[8];
+                unpack8(w4, x);
+                if constexpr (HAS_T) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) x[j] = tval(x[j]);
+                }
+                st_add8(ps, x);
+            }
+            ps = wave_fold(ps);
+            __syncthreads();  // s_st is free again (the previous tree has been read)
+            if (lane == 0) s_st[threadIdx.x / kWave] = ps;
+            __syncthreads();
+            if (threadIdx.x < kWave) {
+                const St a = piece_tree();
+                if (lane < 3) s_part[pp * 3 + lane] = lane == 0 ? a.m : (lane == 1 ? a.s : a.w);
+            }
+        }
+        if (threadIdx.x == 0)  // diagnostics (tests): partner states recomputed, header word 33
+            __hip_atomic_fetch_add((ptr_gu32*)(err_word + 1), (unsigned)__popc(missing), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+    if (threadIdx.x < kWave) {
         // the row's state: a fixed xor tree over lanes 0..P-1 (lane j holds piece j), the same
         // operations on the same values in every piece, so all pieces get the same bits (a
         // serial fold in lane 0 held 3P more VGPRs across the exchange)
@@ -860,6 +936,7 @@ int g_train_resident_nt = 1024;  // skyrl_tune("train_resident_nt", 768/1024)
 int g_train_ntstore = 1;   // skyrl_tune("train_ntstore", 0/1): non-temporal dlogits stores
 int g_train_split = 1;     // skyrl_tune("train_split", 0/1): split-row kernel where it applies
 int g_train_split_shape = 0;  // skyrl_tune("train_split_shape", 0 = by vocabulary, 1..7: kSplitShapes)
+unsigned g_train_split_wait = kSplitWaitTicks;  // skyrl_tune("train_split_wait"): partner wait bound (ticks)
 
 }  // namespace skyrl
 
@@ -908,7 +985,7 @@ TrainKernel resident_edge_for(int nv, bool has_t) {
 using SplitKernel = void (*)(const uint16_t*, int64_t, int64_t, int, int, const int64_t*, int64_t, int64_t, float,
                              const float*, const float*, const float*, const float*, const float*, const float*,
                              skyrl_ppo_params, float*, float*, float*, uint16_t*, int64_t, int64_t, bool,
-                             unsigned long long*, unsigned*, const int32_t*);
+                             unsigned long long*, unsigned*, const int32_t*, unsigned);
 // Split shapes: P pieces per row of NT threads each, W waves per SIMD (the __launch_bounds__
 // occupancy target, i.e. the VGPR cap 512 / W in granules of 8 the compiler schedules the
 // piece's registers under). skyrl_tune("train_split_shape", i) picks one; 0 = by vocabulary.
@@ -1089,7 +1166,7 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
         hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)n * R * sp.parts)), dim3(sp.threads), 0, s, in,
                            stride_b, stride_t, R, V, labels, lstride_b, lstride_t, temperature, old_log_probs,
                            advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok,
-                           out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word, nullptr);
+                           out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word, nullptr, g_train_split_wait);
     } else if (g_train_resident && use768 && aligned) {
         auto kern = has_t ? policy_train_resident_kernel<768, 25, true, false>
                           : policy_train_resident_kernel<768, 25, false, false>;
@@ -1165,7 +1242,7 @@ extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int6
     hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)ntok * sp.parts)), dim3(sp.threads), 0, s, reinterpret_cast<const uint16_t*>(logits), (int64_t)0, ld, R, V,
                        labels, (int64_t)0, (int64_t)1, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
                        row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
-                       (int64_t)0, ld_grad, g_train_ntstore != 0, gran, err_word, token_pos);
+                       (int64_t)0, ld_grad, g_train_ntstore != 0, gran, err_word, token_pos, g_train_split_wait);
     rc = check_launch("policy_train_split_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
@@ -1271,7 +1348,7 @@ extern "C" int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64
                        temperature, old_log_probs + o, advantages + o, loss_mask + o,
                        ref_log_probs ? ref_log_probs + o : nullptr, row_scale, scal, *params, logp_out + o,
                        entropy_out ? entropy_out + o : nullptr, tok, reinterpret_cast<uint16_t*>(grad_logits), gsb,
-                       ld_grad, g_train_ntstore != 0, gran, err_word, token_pos);
+                       ld_grad, g_train_ntstore != 0, gran, err_word, token_pos, g_train_split_wait);
     return check_launch("policy_train_split_kernel");
 }
 
@@ -1296,3 +1373,23 @@ extern "C" int skyrl_policy_train_supports(int32_t V, int32_t aligned, float tem
     if (V <= 0 || !(temperature > 0.f)) return 0;
     return split_plan(V, aligned != 0 && (V % 8) == 0, temperature != 1.0f).kern != nullptr ? 1 : 0;
 }
+
+namespace skyrl {
+namespace {
+__global__ void debug_occupy_kernel(int64_t base, int64_t step) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t until = (uint64_t)(base + (int64_t)(blockIdx.x % 64) * step);
+    while (__builtin_amdgcn_s_memrealtime() - t0 < until) __builtin_amdgcn_s_sleep(8);
+}
+}  // namespace
+}  // namespace skyrl
+
+extern "C" int skyrl_debug_occupy(int32_t blocks, int32_t threads, int64_t base_ticks, int64_t step_ticks, void* stream) {
+    SKYRL_REQUIRE(blocks >= 1 && blocks <= 65536 && threads >= 64 && threads <= 1024 && threads % 64 == 0,
+                  "debug_occupy: bad grid");
+    SKYRL_REQUIRE(base_ticks >= 0 && step_ticks >= 0 && base_ticks + 64 * step_ticks <= 100000000,
+                  "debug_occupy: at most 1 s of spinning");
+    hipLaunchKernelGGL(debug_occupy_kernel, dim3(blocks), dim3(threads), 0, as_stream(stream), base_ticks, step_ticks);
+    return check_launch("debug_occupy_kernel");
+}
+

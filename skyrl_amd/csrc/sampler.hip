@@ -30,6 +30,9 @@
 
 namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
+int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows split over workgroups below this
+int g_sampler_split_wgs = 2048;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at
+int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
 int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
 int g_probe_topp = 0;  // skyrl_tune("topp_probe"): 1 pass 1 alone, 2 pass 1 + the cut, 3 / 4 + a bare re-read
@@ -38,13 +41,13 @@ int g_probe_topp = 0;  // skyrl_tune("topp_probe"): 1 pass 1 alone, 2 pass 1 + t
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kRowModeMinSeqs = 256;  // enough rows to fill the chip with one workgroup each
-// Workspace: a fixed-size region of per-row arrival counters first (only split mode, i.e. fewer
-// than kRowModeMinSeqs rows, uses them), so that the counters sit at the same place for every
-// batch size and never overlap another call's row filters or partials in a reused workspace (a
-// split-mode call after one with fewer rows would otherwise read that call's partials as
-// counters): every counter is zero at allocation and re-armed by its user.
-constexpr size_t kCounterBytes = (size_t)kRowModeMinSeqs * 4;
+constexpr int kMaxSplitRows = 1024;  // split mode is never used at or above this many rows
+// Workspace: a fixed-size region of per-row arrival counters first (only split mode uses them),
+// so that the counters sit at the same place for every batch size and never overlap another
+// call's row filters or partials in a reused workspace (a split-mode call after one with fewer
+// rows would otherwise read that call's partials as counters): every counter is zero at
+// allocation and re-armed by its user.
+constexpr size_t kCounterBytes = (size_t)kMaxSplitRows * 4;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -66,7 +69,46 @@ struct Part {  // per (row, split) partial
     int idx;
     float m;
     float s;
+    float xb;  // raw logit of idx (the logprob needs no re-load of the winner)
 };
+
+// Fold partial b into a: best (score desc, index asc) with its raw logit, and the raw online
+// (max, sum-exp). Every fold below runs in a fixed order, so the result is deterministic.
+__device__ __forceinline__ void part_merge(Part& a, const Part& b) {
+    const Best ab{a.score, a.idx};
+    if (better(b.score, b.idx, ab)) {
+        a.score = b.score;
+        a.idx = b.idx;
+        a.xb = b.xb;
+    }
+    const float mn = fmaxf(a.m, b.m);
+    a.s = a.s * fast_exp2((a.m - mn) * kLog2e) + b.s * fast_exp2((b.m - mn) * kLog2e);
+    a.m = mn;
+}
+template <int CTRL>
+__device__ __forceinline__ void part_dpp_step(Part& p) {
+    auto mv = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false)); };
+    const Part o{mv(p.score), __builtin_amdgcn_update_dpp(0, p.idx, CTRL, 0xF, 0xF, false), mv(p.m), mv(p.s), mv(p.xb)};
+    part_merge(p, o);
+}
+__device__ __forceinline__ Part part_readlane(const Part& p, int l) {
+    auto rl = [l](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); };
+    return Part{rl(p.score), __builtin_amdgcn_readlane(p.idx, l), rl(p.m), rl(p.s), rl(p.xb)};
+}
+// Wave-wide fold on DPP (quad_perm xor 1 / xor 2, row_ror 4 / 8 inside each 16-lane row) and the
+// four row results read with v_readlane, no LDS round trips; the result is wave-uniform.
+// Requires all 64 lanes active.
+__device__ __forceinline__ Part wave_reduce_part(Part p) {
+    part_dpp_step<0xB1>(p);
+    part_dpp_step<0x4E>(p);
+    part_dpp_step<0x124>(p);
+    part_dpp_step<0x128>(p);
+    Part r0 = part_readlane(p, 0), r2 = part_readlane(p, 32);
+    part_merge(r0, part_readlane(p, 16));
+    part_merge(r2, part_readlane(p, 48));
+    part_merge(r0, r2);
+    return r0;
+}
 
 template <typename T>
 __device__ __forceinline__ float to_f(T v);
@@ -421,10 +463,11 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
 __device__ uint64_t g_sphase[4096 * 8];
 #define SPHASE(k)                                                                              \
     do {                                                                                       \
-        if (threadIdx.x == 0 && blockIdx.x < 4096 && blockIdx.y == 0) {                        \
-            g_sphase[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                 \
-            if ((k) == 0) g_sphase[blockIdx.x * 8 + 7] = (uint64_t)__smid();                   \
-            if ((k) == 0) g_sphase[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg(20 | (3 << 11)); \
+        const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;                             \
+        if (threadIdx.x == 0 && lin_ < 4096) {                                                 \
+            g_sphase[lin_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                       \
+            if ((k) == 0) g_sphase[lin_ * 8 + 7] = (uint64_t)__smid();                         \
+            if ((k) == 0) g_sphase[lin_ * 8 + 6] = __builtin_amdgcn_s_getreg(20 | (3 << 11));  \
         }                                                                                      \
     } while (0)
 #else
@@ -464,7 +507,7 @@ __device__ __forceinline__ void sample_unit(
     const int lane = threadIdx.x & (kWave - 1);
     const T* row = logits + (int64_t)row_i * ld;
     const int v_beg = split * chunk;
-    const int v_end = min(V, v_beg + chunk);
+    const int v_end = max(v_beg, min(V, v_beg + chunk));  // (an empty split contributes the identity)
     const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);  // per (seed, seq, step)
     constexpr bool greedy = MODE == 0;
     const bool use_topk = MODE == 2 && use_topk_rt;
@@ -493,6 +536,7 @@ __device__ __forceinline__ void sample_unit(
     // (so a strict '>' keeps the lowest index on ties) and the raw online (max, sum-exp).
     float best_s = -INFINITY;
     int best_i = 0x7fffffff;
+    float best_x = 0.f;  // raw logit of best_i
     const uint32_t key2 = noise_key2(key);  // per-element uniforms (candidates only)
     const uint32_t keyb = noise_keyb(key);  // second-round key of ehash
     // raw online (max, sum-exp) for the sampled token's logprob; finite start so that an
@@ -545,6 +589,7 @@ __device__ __forceinline__ void sample_unit(
                 if (sc > best_s) {  // ascending k within the lane's ascending visit order
                     best_s = sc;
                     best_i = v0 + k;
+                    best_x = x[k];
                 }
             }
         }
@@ -604,6 +649,7 @@ __device__ __forceinline__ void sample_unit(
             if (sc > best_s) {
                 best_s = sc;
                 best_i = v0 + kb;
+                best_x = xb;
             }
         }
         raise_bar();
@@ -648,6 +694,7 @@ __device__ __forceinline__ void sample_unit(
                 for (int k = VEC - 2; k >= 0; --k) kk = (x[k] == vmax) ? k : kk;
                 best_s = vmax;
                 best_i = v0 + kk;
+                best_x = vmax;
             }
             return;
         }
@@ -879,62 +926,48 @@ __device__ __forceinline__ void sample_unit(
         for (int k = 0; k < VEC; ++k) vals[k] = k < cnt ? row[g0 + k] : row[v_beg];
         visit_vec(vals, g0, cnt, kPart);
     }
-    Best best{best_s, best_i};
     SPHASE(2);
 
-    // wave reduce: best (score desc, idx asc) and (m, s)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float os = __shfl_xor(best.score, off, kWave);
-        const int oi = __shfl_xor(best.idx, off, kWave);
-        if (better(os, oi, best)) best = Best{os, oi};
-        const float om = __shfl_xor(m, off, kWave);
-        const float oss = __shfl_xor(s, off, kWave);
-        const float mn = fmaxf(m, om);
-        s = s * fast_exp2((m - mn) * kLog2e) + oss * fast_exp2((om - mn) * kLog2e);
-        m = mn;
-    }
-    if (lane == 0) s_part[threadIdx.x / kWave] = Part{best.score, best.idx, m, s};
+    // wave fold on DPP: best (score desc, idx asc) with its raw logit, and (m, s)
+    const Part wp = wave_reduce_part(Part{best_s, best_i, m, s, best_x});
+    if (lane == 0) s_part[threadIdx.x / kWave] = wp;
     __syncthreads();
     SPHASE(3);
     Part p;
     if (threadIdx.x == 0) {
         p = s_part[0];
-        for (int j = 1; j < NW; ++j) {
-            const Part q = s_part[j];
-            Best b{p.score, p.idx};
-            if (better(q.score, q.idx, b)) {
-                p.score = q.score;
-                p.idx = q.idx;
-            }
-            const float mn = fmaxf(p.m, q.m);
-            p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
-            p.m = mn;
-        }
+        for (int j = 1; j < NW; ++j) part_merge(p, s_part[j]);
     }
     if (nsplit > 1) {
+        // Hand-off without an acquire (MI355X_MICROARCH.md, the valid sc1 form: one lane stores
+        // the whole record write-through, drains, adds to the row's counter; the workgroup whose
+        // add returned last reads every record with sc1 loads after the barrier its adding wave
+        // joins): the last split's wave 0 loads the nsplit records in parallel, one per lane,
+        // and folds them on DPP in a fixed tree.
         if (threadIdx.x == 0) {
             float* dst = reinterpret_cast<float*>(parts + (int64_t)row_i * nsplit + split);
             st_wt(dst + 0, p.score);
             st_wt(reinterpret_cast<int*>(dst) + 1, p.idx);
             st_wt(dst + 2, p.m);
             st_wt(dst + 3, p.s);
+            st_wt(dst + 4, p.xb);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned prev = __hip_atomic_fetch_add(counters + row_i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev == (unsigned)nsplit - 1u;
+            SPHASE(5);
         }
-        if (!arrive_last(counters + row_i, (unsigned)nsplit, &s_last)) return;
-        if (threadIdx.x == 0) {
-            p = parts[(int64_t)row_i * nsplit];
-            for (int j = 1; j < nsplit; ++j) {
-                const Part q = parts[(int64_t)row_i * nsplit + j];
-                Best b{p.score, p.idx};
-                if (better(q.score, q.idx, b)) {
-                    p.score = q.score;
-                    p.idx = q.idx;
-                }
-                const float mn = fmaxf(p.m, q.m);
-                p.s = p.s * fast_exp2((p.m - mn) * kLog2e) + q.s * fast_exp2((q.m - mn) * kLog2e);
-                p.m = mn;
-            }
+        __syncthreads();
+        if (!s_last || threadIdx.x >= kWave) return;
+        Part q{-INFINITY, 0x7fffffff, -1e30f, 0.f, 0.f};  // identity for lanes past nsplit
+        if (lane < nsplit) {
+            const float* src = reinterpret_cast<const float*>(parts + (int64_t)row_i * nsplit + lane);
+            q.score = __hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q.idx = __hip_atomic_load(reinterpret_cast<const int*>(src) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q.m = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q.s = __hip_atomic_load(src + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q.xb = __hip_atomic_load(src + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        p = wave_reduce_part(q);
     }
     if (result) {  // the caller decides (the top_p kernel: ties at the cut still to rank)
         if (threadIdx.x == 0) *result = p;
@@ -945,10 +978,10 @@ __device__ __forceinline__ void sample_unit(
         tokens[row_i] = p.idx;
         if (logp_out) {
             const float lse = p.m + fast_log2(p.s) * kLn2;
-            logp_out[row_i] = (p.idx >= 0 && p.idx < V) ? to_f<T>(row[p.idx]) - lse : __builtin_nanf("");
+            logp_out[row_i] = (p.idx >= 0 && p.idx < V) ? p.xb - lse : __builtin_nanf("");
         }
+        if (nsplit > 1) rearm(counters + row_i);
     }
-    if (nsplit > 1) rearm(counters + row_i);
 }
 
 #define SKYRL_SAMPLE_ARGS                                                                                     \
@@ -2495,14 +2528,26 @@ __global__ __launch_bounds__(kPNT) void sample_topp_pass2_kernel(
     }
 }
 
+constexpr int kMaxSplits = 64;
+
+// Splits per row: below g_sampler_split_rows rows the row is cut into chunks of a multiple of
+// g_sampler_split_gran elements (default 8192 = one full streaming iteration of a 256-thread
+// split, so every split runs the pipelined main loop, not the ragged-tail path) for about
+// g_sampler_split_wgs workgroups in all; at or above it one 512-thread workgroup owns a row.
 int splits_for(int nseq, int V) {
-    if (nseq <= 0 || V <= 0 || nseq >= kRowModeMinSeqs) return 1;  // one 512-thread workgroup per row
-    int s = (2048 + nseq - 1) / nseq;
-    const int max_s = (V + 4095) / 4096;  // at least 4096 elements per split
-    if (s > max_s) s = max_s;
-    if (s > 64) s = 64;
+    if (nseq <= 0 || V <= 0 || nseq >= g_sampler_split_rows || nseq >= kMaxSplitRows) return 1;
+    const int s0 = (g_sampler_split_wgs + nseq - 1) / nseq;
+    const int64_t g = g_sampler_split_gran;
+    int64_t chunk = ((int64_t)(V + s0 - 1) / s0 + g - 1) / g * g;
+    if ((V + chunk - 1) / chunk > kMaxSplits) chunk = ((int64_t)(V + kMaxSplits - 1) / kMaxSplits + g - 1) / g * g;
+    const int s = (int)((V + chunk - 1) / chunk);  // every split non-empty (launch_sample's chunk is <= this one)
     return s < 1 ? 1 : s;
 }
+
+size_t ws_align(size_t b) { return (b + 255) / 256 * 256; }
+// the split partials' region: sized for the most splits any setting gives, so a workspace
+// allocated once stays valid under every skyrl_tune choice
+size_t parts_bytes(int nseq) { return ws_align((size_t)nseq * kMaxSplits * sizeof(Part)); }
 
 template <typename T, int MODE>
 void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int64_t ld, int V, int chunk, float inv_t,
@@ -2521,15 +2566,14 @@ void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int6
                            counters);
 }
 
-size_t ws_align(size_t b) { return (b + 255) / 256 * 256; }
-
 template <typename T>
 int launch_sample(const void* logits, int64_t ld, int nseq, int V, float temperature, int top_k, float top_p,
                   float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens, float* logp,
                   void* ws, hipStream_t stream) {
     const int nsplit = splits_for(nseq, V);
     int chunk = (V + nsplit - 1) / nsplit;
-    chunk = (chunk + 15) & ~15;
+    chunk = nsplit > 1 ? (chunk + g_sampler_split_gran - 1) / g_sampler_split_gran * g_sampler_split_gran
+                       : (chunk + 15) & ~15;
     char* w = reinterpret_cast<char*>(ws);
     unsigned* counters = reinterpret_cast<unsigned*>(w);
     size_t off = kCounterBytes;
@@ -2558,7 +2602,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
             (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
             // the pass-2 kernel's per-row state after the split sampler's parts (never used by this path)
-            char* pw = w + off + ws_align((size_t)nseq * nsplit * sizeof(Part));
+            char* pw = w + off + parts_bytes(nseq);
             ToppPending* pend = reinterpret_cast<ToppPending*>(pw);
             pw += ws_align((size_t)nseq * sizeof(ToppPending));
             unsigned* pend_nt = reinterpret_cast<unsigned*>(pw);  // per row: tie count, arrival counter
@@ -2588,7 +2632,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         if (rc) return rc;
     }
     const dim3 grid(nseq, nsplit);
-    const bool row_mode = nsplit == 1 && nseq >= kRowModeMinSeqs;
+    const bool row_mode = nsplit == 1 && nseq >= g_sampler_split_rows;
     if (greedy)
         launch_mode<T, 0>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
                           filt, tokens, logp, parts, counters);
@@ -2611,7 +2655,7 @@ using namespace skyrl;
 
 extern "C" size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V) {
     return kCounterBytes + ws_align((size_t)nseq * sizeof(RowFilter)) +
-           ws_align((size_t)nseq * splits_for(nseq, V) * sizeof(Part)) + ws_align((size_t)nseq * sizeof(ToppPending)) +
+           parts_bytes(nseq) + ws_align((size_t)nseq * sizeof(ToppPending)) +
            ws_align((size_t)nseq * 2 * sizeof(unsigned)) + ws_align((size_t)nseq * kP2Splits * sizeof(Best)) +
            (size_t)nseq * kPTieCap * sizeof(int32_t) + 256;
 }

@@ -173,3 +173,50 @@ def test_split_edge_rows_match_resident(dev, V, shape):
     assert torch.count_nonzero(grad[:, :S - R - 1]) == 0 and torch.count_nonzero(grad[:, -1]) == 0
     live = grad[:, -R - 1:-1][mask.bool()]  # masked tokens have zero dlogits
     assert torch.count_nonzero(live) > 0.9 * live.numel()
+
+
+def _recomputed(dev, n, R):
+    """Header word 33 of the per-call workspace: partner states a piece computed itself."""
+    ws = ops.WORKSPACES.get(dev, "policy_train", ops._ffi.query("skyrl_policy_train_workspace_bytes", n, R))
+    return int(ws[132:136].view(torch.int32).item())
+
+
+def test_partner_states_computed_in_place_give_the_same_bits(dev):
+    """skyrl_tune("train_split_wait", 0): a piece does not wait for any partner that has not
+    published at its first poll and computes that partner's state from the partner's slice
+    (the path a piece takes when its partners are not resident). The pieces' states are the
+    same bits either way, so loss, metrics, logp, entropy and dlogits equal the default run's
+    bit for bit, at the metric's V and an EDGE vocabulary (GPT-2's 50,257)."""
+    params = _params()
+    for V in (151936, 50257):  # (odd V: rows of a contiguous [n, R, V] tensor are not 16-B aligned)
+        inp = _inputs(21, 4, 64, V, dev)
+        base = _run(inp, params)
+        n, R = inp[1].shape
+        c0 = _recomputed(dev, n, R)
+        ops._ffi.call("skyrl_tune", b"train_split_wait", 0)
+        try:
+            forced = _run(inp, params)
+        finally:
+            ops._ffi.call("skyrl_tune", b"train_split_wait", 5000)
+        assert _recomputed(dev, n, R) > c0, V  # the in-place path ran
+        for a, b in zip(base, forced):
+            assert torch.equal(a, b), V
+
+
+def test_split_pass_beside_a_kernel_holding_the_cus(dev):
+    """the split pass on one stream while another stream's kernel holds every
+    CU slot and releases them a few at a time (64 groups of workgroups ending 20 us apart), so the
+    pieces of a row are dispatched far apart. No piece may wait on a partner's residency: no
+    timeout flag, and the same bits as the uncontended run."""
+    params = _params()
+    inp = _inputs(5, 8, 256, 151936, dev)
+    base = _run(inp, params)
+    side = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(side):
+        ops._ffi.call("skyrl_debug_occupy", 512, 1024, 100_000, 2_000, ops._stream(dev))
+    out = _run(inp, params)  # current stream: runs beside the occupier
+    torch.cuda.synchronize(dev)
+    assert float(out[1][6]) == 0.0  # no split-exchange error
+    for a, b in zip(base, out):
+        assert torch.equal(a, b)

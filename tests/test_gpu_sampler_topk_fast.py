@@ -17,7 +17,7 @@ from skyrl_amd import ops
 
 pytestmark = pytest.mark.gpu
 
-_COUNTER_BYTES = 256 * 4  # sampler workspace: per-row counters first, then one 20-B RowFilter per row
+_COUNTER_BYTES = 1024 * 4  # sampler workspace: 1024 per-row split counters first, then one 20-B RowFilter per row
 _ROW_DONE = -2
 _ROW_FALLBACK = -3
 
