@@ -10,8 +10,8 @@ One step is one pass of the hot path over one synthetic batch (per rank, its row
   rollout   R decode steps of skyrl_sample over [512, V] logits (T=1, top_p=1, top_k=-1)
   pack      skyrl_pack_experience: ragged prompts/responses -> padded training tensors
   ref/old   skyrl_logprob_fwd over all 512x1024 response positions (2 passes)
-  advantage skyrl_grpo_advantage over [512, 1024] (contiguous groups, pack's reward row sums)
-  update    the step form of the fused policy pass (GRPOTrainer's): skyrl_policy_train_plan (every
+  update    the step form of the fused policy pass (GRPOTrainer's): skyrl_policy_train_plan_grpo
+            (GRPO advantages over contiguous groups from pack's reward row sums + every
             micro-batch's loss scales, one launch), per micro-batch (16 seqs)
             skyrl_policy_train_micro_fwd, ONE pass per token computing logprob + entropy + PPO/KL
             loss terms and writing dlogits (bf16), each row held in the registers of 6
@@ -275,6 +275,7 @@ def run(args):
     step_met = torch.empty((n_micro, 8), dtype=torch.float32, device=dev)
     step_lp = torch.empty((N, R), dtype=torch.float32, device=dev)
     step_ent = torch.empty((N, R), dtype=torch.float32, device=dev)
+    step_adv = torch.empty((N, R), dtype=torch.float32, device=dev)
     metrics_acc = torch.zeros(8, dtype=torch.float32, device=dev)
     grpo_timer, plan_timer, fold_timer = KernelTimer(), KernelTimer(), KernelTimer()
     timers = timers + (grpo_timer, plan_timer, fold_timer)
@@ -296,7 +297,7 @@ def run(args):
         # ---- pack ragged rollout output into the padded training tensors
         rtok = sampler.tokens[tok_t, tok_n]
         rlp_sampled = sampler.logprobs[tok_t, tok_n]
-        seqs, att, rmask, rew, lmask, rlp, _, scores = ops.pack_experience(
+        seqs, att, rmask, rew, lmask, rlp, lrows, scores = ops.pack_experience(
             data["ptok"], data["poff"], rtok, roff, data["rew"], roff, data["lmask"],
             roff, rlp_sampled, roff, N=N, P=P_MAX, R=R, pad=0, pad_token_id=0, return_row_sums=True)
         labels = seqs[:, P_MAX:]  # the sampled response tokens (int64 view, row stride P+R)
@@ -318,13 +319,19 @@ def run(args):
                     lab.stride(0), lab.stride(1), 1.0, ops._ptr(out[s:s + mb]), None, None, ops._stream(dev)))
         # ---- GRPO advantage over the whole batch: contiguous groups of G (the rollout layout), the
         #      pack kernel's per-row reward sums as the scores
-        adv = grpo_timer.wrap(lambda: ops.grpo_advantage(rew, rmask, None, None, ng, scores=scores))
         # ---- update: per micro-batch fused policy pass (logprob/entropy fwd + PPO/KL loss +
-        #      logprob bwd -> dlogits); --unfused runs the four separate kernels instead
+        #      logprob bwd -> dlogits); --unfused runs the four separate kernels instead. The step
+        #      plan computes GRPO (pack's reward row sums, contiguous groups of G) into `adv` in the
+        #      same launch as every micro-batch's loss scales (skyrl_policy_train_plan_grpo)
         metrics_acc.zero_()
-        if not args.unfused:
-            plan_timer.wrap(lambda: ops._ffi.call("skyrl_policy_train_plan", ops._ptr(lmask), N, R, mb,
-                                                  ctypes.byref(params), ops._ptr(step_ws), ops._stream(dev)))
+        if args.unfused:
+            adv = grpo_timer.wrap(lambda: ops.grpo_advantage(rew, rmask, None, None, ng, scores=scores))
+        else:
+            adv = step_adv
+            plan_timer.wrap(lambda: ops._ffi.call(
+                "skyrl_policy_train_plan_grpo", ops._ptr(lmask), N, R, mb, ctypes.byref(params), ops._ptr(scores),
+                ops._ptr(rmask), ops.I64, GROUP, 1e-6, 1, ops._ptr(adv), ops._ptr(lrows), ops._ptr(step_ws),
+                ops._stream(dev)))
         for s in range(0, N, mb):
             x = lg_rows(s, mb)
             lab = labels[s:s + mb]
@@ -428,16 +435,17 @@ def run(args):
     # scores reads the int64 response mask and writes adv (12 B/token), the plan reads the loss mask
     # (4), the fold reads the records and the mask (20).
     product = None
-    if grpo_timer.pairs and plan_timer.pairs:
-        us = {k: round(t.avg_ms() * 1e3, 2) for k, t in (("grpo_us", grpo_timer), ("plan_us", plan_timer),
-                                                       ("fold_us", fold_timer))}
+    if plan_timer.pairs and fold_timer.pairs:
+        us = {k: round(t.avg_ms() * 1e3, 2) for k, t in (("plan_grpo_us", plan_timer), ("fold_us", fold_timer))}
         tot = sum(us.values())
-        nbytes = N * R * (12 + 4 + 20)
-        product = dict(us, total_us=round(tot, 2), launches_per_step=3, bytes_per_step=nbytes,
+        # plan + GRPO: int64 response mask 8 read, advantages 4 written (pack's loss-mask row sums and
+        # reward row sums: 8 B per row); fold: records 16 + loss mask 4 read
+        nbytes = N * R * (12 + 20) + N * 8
+        product = dict(us, total_us=round(tot, 2), launches_per_step=2, bytes_per_step=nbytes,
                        achieved_GBps=round(nbytes / (tot * 1e-6) / 1e9, 1),
                        frac=round(nbytes / (tot * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                        note="eager, event-timed in the timed steps: exactly the launches GRPOTrainer issues per "
-                            "step for GRPO + the loss outside the fused logits pass")
+                            "step for GRPO + the loss outside the fused logits pass (GRPO inside the plan launch)")
     dom = kernels[dom_name]
     result = {
         "metric": "trained samples/sec (rollout+update), Qwen2.5-1.5B GRPO at 1/2/4/8 MI355X",
@@ -791,8 +799,9 @@ def lmhead_sample_leg(dev, nseq, reps=30):
 
 def sampler_filtered_leg(dev, nseq, V, reps=20):
     """The §8(d) filter variant of the rollout sampler (top_k = 50 with top_p = 0.9, and top_k =
-    50 alone) and the SkyRL-SQL recipe's top_p = 0.95 alone (examples/text_to_sql/run_skyrl_sql.sh:60)
-    at the decode step's shape [nseq, V] bf16, T = 1: the whole skyrl_sample call (with top_k the
+    50 alone), the SkyRL-SQL recipe's top_p = 0.95 alone at T = 1 and at its T = 0.6
+    (examples/text_to_sql/run_skyrl_sql.sh:59-60), and min_p = 0.05 (skyrl-tx generator.py:423-449)
+    at the decode step's shape [nseq, V] bf16: the whole skyrl_sample call (with top_k the
     one-pass kernel; without it the top_p kernel, which decides most rows in one pass and hands
     the rest to a second launch that re-reads each of them in 8 pieces; rows either kernel cannot
     take run the pre-pass + MODE 2 code in the same workgroup), against the two-kernel path
@@ -808,13 +817,15 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
     lp = torch.empty(nseq, dtype=torch.float32, device=dev)
     nbytes = nseq * V * 2 + nseq * 16
     out = {"shape": [nseq, V], "dtype": "bf16", "temperature": 1.0, "bytes_per_launch": nbytes}
-    for name, k, p in (("top_k50_top_p0.9", 50, 0.9), ("top_k50", 50, 1.0), ("top_p0.95", -1, 0.95)):
+    for name, k, p, t, mp in (("top_k50_top_p0.9", 50, 0.9, 1.0, 0.0), ("top_k50", 50, 1.0, 1.0, 0.0),
+                              ("top_p0.95", -1, 0.95, 1.0, 0.0), ("top_p0.95_T0.6", -1, 0.95, 0.6, 0.0),
+                              ("min_p0.05", -1, 1.0, 1.0, 0.05), ("min_p0.05_T0.6", -1, 1.0, 0.6, 0.05)):
         res = {}
         knob = b"sampler_topk_fast" if k > 0 else b"sampler_topp_fast"  # the one-pass / two-pass kernels
         for fast in (1, 0):
             ops._ffi.call("skyrl_tune", knob, fast)
-            run = lambda: ops.sample(x, temperature=1.0, top_k=k, top_p=p, seed=3, seq_ids=ids, step=1,  # noqa: E731
-                                     tokens_out=tok, logp_out=lp)
+            run = lambda: ops.sample(x, temperature=t, top_k=k, top_p=p, min_p=mp, seed=3, seq_ids=ids,  # noqa: E731
+                                     step=1, tokens_out=tok, logp_out=lp)
             run()
             torch.cuda.synchronize(dev)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -47,7 +47,7 @@ const char* skyrl_last_error(void);
  * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange; 7:
  * skyrl_comm_* RCCL collectives; 8: the step form of the fused policy pass,
  * skyrl_policy_train_plan / _micro_fwd / _fold; 9: per-parameter AdamW,
- * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy). */
+ * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy, skyrl_policy_train_plan_grpo). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -350,11 +350,19 @@ int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int
  * short), the loss folded once per mini-batch. The reference's micro-batch loop
  * (workers/worker.py:731-900) reads loss and metrics only after the mini-batch's backward
  * passes (optim_step, :900-925), and the loss's reduction scales depend on the loss mask only,
- * so: skyrl_policy_train_plan computes every micro-batch's scales in one launch (one workgroup
- * per micro-batch); skyrl_policy_train_micro_fwd is the fused pass of micro-batch `micro`
- * alone (no scales or epilogue launch); skyrl_policy_train_fold folds every micro-batch's
- * per-token records into loss_out[n_micro] and metrics_out[n_micro * SKYRL_M_COUNT] in one
- * launch. Per micro-batch the loss and metrics are the bits skyrl_policy_train_fwd /
+ * so: skyrl_policy_train_plan computes every micro-batch's scales in one launch (one wave
+ * per row, the last row of each micro-batch totalling it); skyrl_policy_train_plan_grpo does
+ * the same and, in the same launch, writes the mini-batch's GRPO advantages
+ * (compute_grpo_outcome_advantage, utils/ppo_utils.py:1132-1182, bit-identical to
+ * skyrl_grpo_advantage) from the per-row scores (skyrl_pack_experience's reward_row_sum) over
+ * contiguous groups of group_size rows times the response mask (with loss_mask_row_sum, pack's
+ * loss-mask row sums, it reads neither the loss mask nor hands rows over: each row's wave totals
+ * its micro-batch from them; same scales for masks whose row sums are exact, e.g. 0/1);
+ * skyrl_policy_train_micro_fwd is
+ * the fused pass of micro-batch `micro` alone (no scales or epilogue launch);
+ * skyrl_policy_train_fold folds every micro-batch's per-token records into loss_out[n_micro]
+ * and metrics_out[n_micro * SKYRL_M_COUNT] in one launch (one wave per row, the last row of each
+ * micro-batch folding its rows' records in row order). Per micro-batch the loss and metrics are the bits skyrl_policy_train_fwd /
  * _ragged_fwd return for it (same code and order; a position with loss mask 0 contributes
  * nothing). All per-token arrays (old / adv / loss_mask / ref, logp_out / entropy_out) are
  * the mini-batch's f32 [n_total, R]; loss_mask is required. micro_fwd, dense form
@@ -368,6 +376,11 @@ int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int
 size_t skyrl_policy_train_step_workspace_bytes(int32_t n_total, int32_t R, int32_t micro_rows);
 int skyrl_policy_train_plan(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
                             const skyrl_ppo_params* params, void* workspace, void* stream);
+int skyrl_policy_train_plan_grpo(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
+                                 const skyrl_ppo_params* params, const float* scores, const void* response_mask,
+                                 int mask_dtype, int32_t group_size, float epsilon, int32_t norm_by_std,
+                                 float* advantages, const float* loss_mask_row_sum /* [n_total] or NULL */,
+                                 void* workspace, void* stream);
 int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
                                  const int64_t* labels, int64_t label_stride_b, int64_t label_stride_t,
                                  const int32_t* token_pos, int32_t micro, int32_t n_total, int32_t R,

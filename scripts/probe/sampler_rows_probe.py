@@ -66,6 +66,6 @@ for nseq in rows_list:
             out[f"{nseq}_{name}_rows{rows_thr}_wgs{wgs}_g{gran}"] = rec
             del g
 _ffi.call("skyrl_tune", b"sampler_split_rows", 256)
-_ffi.call("skyrl_tune", b"sampler_split_wgs", 2048)
+_ffi.call("skyrl_tune", b"sampler_split_wgs", 1024)
 _ffi.call("skyrl_tune", b"sampler_split_gran", 8192)
 print(json.dumps(out), flush=True)

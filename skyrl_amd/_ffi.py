@@ -149,6 +149,8 @@ SIGNATURES = {
     ),
     "skyrl_policy_train_step_workspace_bytes": (_SZ, [_I32, _I32, _I32]),
     "skyrl_policy_train_plan": (_INT, [_P, _I32, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P]),
+    "skyrl_policy_train_plan_grpo": (_INT, [_P, _I32, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _I32, _I32, _F, _I32, _P,
+                                           _P, _P, _P]),
     "skyrl_policy_train_micro_fwd": (
         _INT,
         [_P, _INT, _I64, _I32, _I32, _P, _I64, _I64, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P,

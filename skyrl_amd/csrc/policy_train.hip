@@ -143,47 +143,72 @@ __device__ __forceinline__ void ppo_token(float lp, float old, float A, float lo
 }
 
 // ---- 1. mask statistics -> gradient scales -------------------------------------------
-// One wave per row (rows strided over the 16 waves); scal[0] = sum m,
-// scal[1] = entropy-gradient scale (-coef/max(sum m,1) or 0), scal[2] = 1/max(sum m,1).
+// Sum of one loss-mask row by one wave: lane l takes the 16-B vectors l, l + 64, ... as
+// (x + y) + (z + w) in vector order (scalars t = l, l + 64, ... when the row is not 16-B aligned
+// or R % 4 != 0), then the wave's xor-butterfly sum; a NULL mask counts R. The per-call scales and
+// the step plan both sum rows this way, and total a micro-batch's rows in row order (fp64), so
+// they derive the same bits.
+__device__ __forceinline__ float mask_row_sum(const float* __restrict__ row, int R) {
+    const int lane = threadIdx.x & 63;
+    if (!row) return (float)R;
+    float acc = 0.f;
+    if ((R & 3) == 0 && (reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+        const float4* r4 = reinterpret_cast<const float4*>(row);
+#pragma unroll 4
+        for (int i = lane; i < (R >> 2); i += kWave) {
+            const float4 v = r4[i];
+            acc += (v.x + v.y) + (v.z + v.w);
+        }
+    } else {
+#pragma unroll 8
+        for (int t = lane; t < R; t += kWave) acc += row[t];
+    }
+    return wave_sum(acc);
+}
+__device__ __forceinline__ float row_scale_of(const skyrl_ppo_params& p, float acc, int n) {
+    const double mrow = acc > 1.f ? acc : 1.0;
+    if (p.loss_reduction == 1) return (float)(1.0 / ((double)n * mrow));
+    return (float)(1.0 / ((double)n * (double)p.max_seq_len));  // (reduction 2; token_mean is set from D)
+}
+// scal[0] = sum m, scal[1] = entropy-gradient scale (-coef / D or 0), scal[2] = 1 / D with
+// D = max(sum m, 1); row_scale[b] = 1 / D (token_mean) or the per-row scale.
+__device__ __forceinline__ void write_scales(const skyrl_ppo_params& p, double all, float* __restrict__ scal) {
+    const double d = all > 1.0 ? all : 1.0;
+    scal[0] = (float)all;
+    scal[1] = p.use_entropy_loss ? (float)(-(double)p.entropy_loss_coef / d) : 0.f;
+    scal[2] = (float)(1.0 / d);
+}
+
+// One block: rows strided over the 16 waves; the row sums staged in row_scale, totalled by
+// thread 0 in row order, then every row's scale.
 // Header word 16 is the split kernel's exchange tag for the launch(es) these scales serve:
 // the single-call entries advance it by one per launch; the step plan (skyrl_policy_train_plan)
 // gives micro-batch k the tag (c << 12) | k with c its slot's own counter, so every launch of
 // every step carries a tag no other launch that shares the granules carries.
 __device__ __forceinline__ void scales_body(const float* __restrict__ mask, int n, int R, const skyrl_ppo_params& p,
                                             float* __restrict__ row_scale, float* __restrict__ scal, int step_k) {
-    __shared__ double s_tot[kWaves];
+    __shared__ double s_all;
     const int lane = threadIdx.x & 63, w = threadIdx.x / kWave;
-    double tot = 0.0;
     for (int b = w; b < n; b += kWaves) {
-        float acc = 0.f;
-#pragma unroll 8
-        for (int t = lane; t < R; t += kWave) acc += mask ? mask[(int64_t)b * R + t] : 1.f;  // loads in flight, same order
-        acc = wave_sum(acc);
-        tot += acc;
-        if (lane == 0) {
-            const double mrow = acc > 1.f ? acc : 1.0;
-            if (p.loss_reduction == 1) row_scale[b] = (float)(1.0 / ((double)n * mrow));
-            else if (p.loss_reduction == 2) row_scale[b] = (float)(1.0 / ((double)n * (double)p.max_seq_len));
-        }
+        const float acc = mask_row_sum(mask ? mask + (int64_t)b * R : nullptr, R);
+        if (lane == 0) row_scale[b] = acc;
     }
-    if (lane == 0) s_tot[w] = tot;
+    __threadfence_block();
     __syncthreads();
-    double all = 0.0;
-    for (int j = 0; j < kWaves; ++j) all += s_tot[j];
-    const double d = all > 1.0 ? all : 1.0;
     if (threadIdx.x == 0) {
-        scal[0] = (float)all;
-        scal[1] = p.use_entropy_loss ? (float)(-(double)p.entropy_loss_coef / d) : 0.f;
-        scal[2] = (float)(1.0 / d);
+        double all = 0.0;
+        for (int b = 0; b < n; ++b) all += (double)row_scale[b];
+        s_all = all;
+        write_scales(p, all, scal);
         // this launch's tag for the split kernel's exchange granules (header word 16, see
         // skyrl_policy_train_fwd); the previous launch's granules carry the previous tag
         unsigned* epoch = reinterpret_cast<unsigned*>(scal) + 16;
         epoch[0] = step_k < 0 ? epoch[0] + 1u : ((((epoch[0] >> 12) + 1u) << 12) | (unsigned)step_k);
     }
-    if (p.loss_reduction == 0) {
-        const float sc = (float)(1.0 / d);
-        for (int b = threadIdx.x; b < n; b += kThreads) row_scale[b] = sc;
-    }
+    __syncthreads();
+    const double d = s_all > 1.0 ? s_all : 1.0;
+    for (int b = threadIdx.x; b < n; b += kThreads)
+        row_scale[b] = p.loss_reduction == 0 ? (float)(1.0 / d) : row_scale_of(p, row_scale[b], n);
 }
 
 __global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __restrict__ mask, int n, int R,
@@ -192,18 +217,117 @@ __global__ __launch_bounds__(kThreads) void train_scales_kernel(const float* __r
     scales_body(mask, n, R, p, row_scale, scal, -1);
 }
 
-// The step plan: block k = micro-batch k (rows [k*mb, min(n_total, (k+1)*mb))), the same code
-// and summation order as the per-call kernel above, so its scales are those bits; its scalars
-// sit in micro slot k (kStepSlot bytes each).
 constexpr int kStepSlot = 256;
-__global__ __launch_bounds__(kThreads) void train_plan_kernel(const float* __restrict__ mask, int n_total, int R,
-                                                              int mb, skyrl_ppo_params p,
-                                                              float* __restrict__ row_scale,
-                                                              char* __restrict__ slots) {
-    const int k = blockIdx.x;
+// micro slot words (kStepSlot bytes each): 0..2 scal floats, 16 the exchange tag, 32 the error
+// flag, 33 recomputed partner states (diagnostics), 40 / 41 the plan's / fold's arrival counters
+constexpr int kSlotPlanCtr = 40, kSlotFoldCtr = 41;
+constexpr int kStepRows = 2;  // rows (one wave each) per block of the step plan and fold
+
+// The step plan: one wave per row of the mini-batch (2 rows per block: n_total / 2 blocks). A row's
+// wave sums its loss mask (mask_row_sum), stores it write-through and adds to its micro-batch's
+// counter; the wave whose add comes last totals the micro-batch's rows in row order (fp64, the
+// per-call scales' order and bits), writes the micro slot's scalars and tag and every row scale.
+// Hand-off without an acquire (MI355X_MICROARCH.md's valid sc1 form: sc1 stores by the adding
+// lane, drained; the last adder's wave reads them with sc1 loads).
+// With GRPO (scores != NULL, contiguous groups of G rows): the wave also writes its row's advantages,
+// adv = (score - mean) / (std + eps) (fp64 group stats in j order, compute_grpo_outcome_advantage,
+// ppo_utils.py:1132-1182, the same arithmetic as grpo_adv_contig_kernel) times the response mask.
+template <int MDT>
+__global__ __launch_bounds__(kStepRows * kWave) void train_plan_kernel(
+    const float* __restrict__ mask, int n_total, int R, int mb, skyrl_ppo_params p, float* __restrict__ row_scale,
+    float* __restrict__ rsum, char* __restrict__ slots, const float* __restrict__ scores,
+    const void* __restrict__ rmask, int G, float eps, int norm_by_std, float* __restrict__ adv,
+    const float* __restrict__ pack_rsum) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * kStepRows + threadIdx.x / kWave;
+    if (b >= n_total) return;
+    const int k = b / mb;
     const int r0 = k * mb;
     const int n = min(n_total, r0 + mb) - r0;
-    scales_body(mask + (int64_t)r0 * R, n, R, p, row_scale + r0, reinterpret_cast<float*>(slots + k * kStepSlot), k);
+    float* scal = reinterpret_cast<float*>(slots + (size_t)k * kStepSlot);
+    unsigned* ctr = reinterpret_cast<unsigned*>(scal) + kSlotPlanCtr;
+    // pack_rsum (skyrl_pack_experience's loss-mask row sums): every wave totals its micro-batch's
+    // rows itself (row order, fp64): no mask read and no arrival; else the row's own sum here
+    const float acc = pack_rsum ? pack_rsum[b] : mask_row_sum(mask + (int64_t)b * R, R);
+    unsigned prev = 0;
+    if (pack_rsum) {
+        if (lane == 0 && p.loss_reduction != 0) row_scale[b] = row_scale_of(p, acc, n);
+    } else if (lane == 0) {
+        if (p.loss_reduction != 0) row_scale[b] = row_scale_of(p, acc, n);
+        st_wt(rsum + b, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (scores) {  // GRPO: this row's advantages (overlaps the arrival's round trip)
+        const int g0 = b - b % G;
+        const float sj = lane < G ? scores[g0 + lane] : 0.f;
+        float mean_f, denom_f;
+        if (G <= 1) {
+            mean_f = 0.f;  // singleton group: mean 0, std 1 (ppo_utils.py:1167-1169)
+            denom_f = norm_by_std ? (1.f + eps) : 1.f;
+        } else {  // fp64 like torch.std on CPU, j in order
+            double sum = 0.0;
+            for (int j = 0; j < G; ++j) sum += (double)__shfl(sj, j, kWave);
+            const double mean = sum / (double)G;
+            double m2 = 0.0;
+            for (int j = 0; j < G; ++j) {
+                const double d = (double)__shfl(sj, j, kWave) - mean;
+                m2 += d * d;
+            }
+            mean_f = (float)mean;
+            const float std_f = (float)sqrt(m2 / (double)(G - 1));
+            denom_f = norm_by_std ? (std_f + eps) : 1.f;
+        }
+        const float sc = __shfl(sj, b - g0, kWave);
+        const float a = norm_by_std ? (sc - mean_f) / denom_f : (sc - mean_f);
+        float* orow = adv + (int64_t)b * R;
+        if ((R & 3) == 0) {
+            float4* o4 = reinterpret_cast<float4*>(orow);
+#pragma unroll 4
+            for (int i = lane; i < (R >> 2); i += kWave) {
+                float mm[4];
+                load_mask4(rmask, MDT, (int64_t)b * R + 4 * i, mm);
+                o4[i] = make_float4(a * mm[0], a * mm[1], a * mm[2], a * mm[3]);
+            }
+        } else {
+            for (int t = lane; t < R; t += kWave) orow[t] = a * load_mask(rmask, MDT, (int64_t)b * R + t);
+        }
+    }
+    double all = 0.0;
+    if (pack_rsum) {  // every wave: the micro-batch's total; the wave of its first row writes the slot
+        for (int j0 = 0; j0 < n; j0 += kWave) {
+            const float v = j0 + lane < n ? pack_rsum[r0 + j0 + lane] : 0.f;
+            for (int j = 0; j < kWave && j0 + j < n; ++j)
+                all += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+        }
+        if (p.loss_reduction == 0 && lane == 0) row_scale[b] = (float)(1.0 / (all > 1.0 ? all : 1.0));
+        if (b != r0) return;
+        if (lane == 0) {
+            write_scales(p, all, scal);
+            unsigned* epoch = reinterpret_cast<unsigned*>(scal) + 16;
+            epoch[0] = (((epoch[0] >> 12) + 1u) << 12) | (unsigned)k;
+        }
+        return;
+    }
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev != (unsigned)n - 1u) return;
+    // the micro-batch's last row: total in row order, scalars, tag, token_mean scales
+    for (int j0 = 0; j0 < n; j0 += kWave) {
+        const float v = j0 + lane < n ? __hip_atomic_load(rsum + r0 + j0 + lane, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        for (int j = 0; j < kWave && j0 + j < n; ++j)
+            all += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+    }
+    if (lane == 0) {
+        write_scales(p, all, scal);
+        unsigned* epoch = reinterpret_cast<unsigned*>(scal) + 16;
+        epoch[0] = (((epoch[0] >> 12) + 1u) << 12) | (unsigned)k;
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    if (p.loss_reduction == 0) {
+        const double d = all > 1.0 ? all : 1.0;
+        for (int j = lane; j < n; j += kWave) row_scale[r0 + j] = (float)(1.0 / d);
+    }
 }
 
 // ---- 2. fused sweep pair per token ------------------------------------------------------
@@ -822,73 +946,108 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
 }
 
 // ---- 3. loss scalar + metrics ---------------------------------------------------------
-// One wave per row: row sums of loss*m, kl*m*m, m -> sequence-level terms in fp64;
-// token-level sums (loss*m, clip*m, ent*m) folded over the block; same metric layout as
-// skyrl_ppo_loss_fwd. MASKED (the step fold): a position whose loss mask is 0 contributes
-// nothing, which lets a packed micro-batch leave the records of positions no token maps to
-// unwritten (every record is premultiplied by m, so for finite terms the sums are the same bits).
+// Per row (one wave): a0 = sum l*m, a1 = sum kl*m*m, am = sum m (fp32, lane order then the
+// butterfly), clip*m and ent*m per lane in fp64 then the butterfly; the row's record is
+// (a0, a0 / mrow | a0 / max_seq_len, a1 / mrow, clip, ent) in fp64. A micro-batch's terms are its
+// rows' records summed in row order (the per-call epilogue and the step fold alike, so their
+// loss and metrics are the same bits); same metric layout as skyrl_ppo_loss_fwd. MASKED (the step
+// fold): a position whose loss mask is 0 contributes nothing, which lets a packed micro-batch leave
+// the records of positions no token maps to unwritten (every record is premultiplied by m, so for
+// finite terms the sums are the same bits).
+struct RowRec {
+    double tl, pg, kl, tc, te;
+};
+template <bool MASKED>
+__device__ __forceinline__ RowRec row_record(const float* __restrict__ tok, const float* __restrict__ mask, int R,
+                                             const skyrl_ppo_params& p) {
+    const int lane = threadIdx.x & 63;
+    float a0 = 0.f, a1 = 0.f, am = 0.f;
+    double tc = 0.0, te = 0.0;
+    constexpr int kU = 16;  // a lane's positions per batch: every load of the batch in flight at once
+    for (int t0 = 0; t0 < R; t0 += kU * kWave) {
+        float4 v[kU];
+        float mm[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {  // clamped addresses: the loads are unconditional
+            const int t = min(t0 + u * kWave + lane, R - 1);
+            v[u] = *reinterpret_cast<const float4*>(tok + (int64_t)t * 4);
+            mm[u] = mask ? mask[t] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {  // in position order, as one position at a time would
+            if (t0 + u * kWave + lane >= R) continue;
+            float4 x = v[u];
+            const float m = mm[u];
+            if (MASKED && m == 0.f) x = make_float4(0.f, 0.f, 0.f, 0.f);
+            a0 += x.x;
+            a1 += x.z;
+            tc += x.y;
+            te += x.w;
+            am += m;
+        }
+    }
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    am = wave_sum(am);
+    tc = wave_sum(tc);
+    te = wave_sum(te);
+    const double mrow = am > 1.f ? am : 1.0;
+    RowRec r{a0, 0.0, a1 / mrow, tc, te};
+    if (p.loss_reduction == 1) r.pg = a0 / mrow;
+    else if (p.loss_reduction == 2) r.pg = a0 / (double)p.max_seq_len;
+    return r;
+}
+__device__ __forceinline__ void rec_add(RowRec& a, const RowRec& b) {
+    a.tl += b.tl;
+    a.pg += b.pg;
+    a.kl += b.kl;
+    a.tc += b.tc;
+    a.te += b.te;
+}
+// the micro-batch's loss and metrics from its summed records (n rows)
+__device__ __forceinline__ void finish_metrics(const RowRec& v, int n, const skyrl_ppo_params& p,
+                                               const float* __restrict__ scal, float* __restrict__ loss_out,
+                                               float* __restrict__ metrics) {
+    const double msum = scal[0] > 1.f ? (double)scal[0] : 1.0;
+    const float pg = p.loss_reduction == 0 ? (float)(v.tl / msum) : (float)(v.pg / (double)n);
+    const float kl = p.use_kl_loss ? (float)(v.kl / (double)n) : 0.f;
+    const float entropy = (float)(v.te / msum);
+    float final_loss = pg + kl * p.kl_loss_coef;
+    if (p.use_entropy_loss) final_loss = final_loss - entropy * p.entropy_loss_coef;
+    loss_out[0] = final_loss;
+    metrics[SKYRL_M_FINAL_LOSS] = final_loss;
+    metrics[SKYRL_M_POLICY_LOSS] = pg;
+    metrics[SKYRL_M_ENTROPY] = entropy;
+    metrics[SKYRL_M_KL] = kl;
+    metrics[SKYRL_M_CLIP_RATIO] = (float)(v.tc / msum);
+    metrics[SKYRL_M_MASK_SUM] = scal[0];
+    unsigned* err = reinterpret_cast<unsigned*>(const_cast<float*>(scal)) + 32;  // header word 32
+    metrics[6] = err[0] ? 1.f : 0.f;  // split-row exchange failure (not produced since r05)
+    metrics[7] = 0.f;
+    err[0] = 0u;
+}
+
+// One block over n rows: 16 rows (one per wave) at a time, their records summed by thread 0 in
+// row order.
 template <bool MASKED>
 __device__ __forceinline__ void epilogue_body(const float* __restrict__ tok, const float* __restrict__ mask, int n,
                                               int R, const skyrl_ppo_params& p, const float* __restrict__ scal,
                                               float* __restrict__ loss_out, float* __restrict__ metrics) {
-    __shared__ double s_red[kWaves * 5];
+    __shared__ RowRec s_rec[kWaves];
     const int lane = threadIdx.x & 63, w = threadIdx.x / kWave;
-    // per wave (lane 0): sum l*m, rows_pg, rows_kl; per lane: clip*m, ent*m
-    double tl = 0.0, rows_pg = 0.0, rows_kl = 0.0, tc = 0.0, te = 0.0;
-    for (int b = w; b < n; b += kWaves) {
-        float a0 = 0.f, a1 = 0.f, am = 0.f;
-#pragma unroll 4
-        for (int t = lane; t < R; t += kWave) {  // (unrolled: loads in flight; the sums keep their order)
-            float4 v = *reinterpret_cast<const float4*>(tok + ((int64_t)b * R + t) * 4);
-            const float m = mask ? mask[(int64_t)b * R + t] : 1.f;
-            if (MASKED && m == 0.f) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            a0 += v.x;
-            a1 += v.z;
-            tc += v.y;
-            te += v.w;
-            am += m;
+    RowRec tot{0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int b0 = 0; b0 < n; b0 += kWaves) {
+        const int b = b0 + w;
+        if (b < n) {
+            const RowRec r = row_record<MASKED>(tok + (int64_t)b * R * 4, mask ? mask + (int64_t)b * R : nullptr, R, p);
+            if (lane == 0) s_rec[w] = r;
         }
-        a0 = wave_sum(a0);
-        a1 = wave_sum(a1);
-        am = wave_sum(am);
-        const double mrow = am > 1.f ? am : 1.0;
-        tl += a0;
-        if (p.loss_reduction == 1) rows_pg += a0 / mrow;
-        else if (p.loss_reduction == 2) rows_pg += a0 / (double)p.max_seq_len;
-        rows_kl += a1 / mrow;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int j = 0; j < kWaves && b0 + j < n; ++j) rec_add(tot, s_rec[j]);
+        __syncthreads();
     }
-    tc = wave_sum(tc);
-    te = wave_sum(te);
-    if (lane == 0) {
-        s_red[w * 5 + 0] = tl;
-        s_red[w * 5 + 1] = rows_pg;
-        s_red[w * 5 + 2] = rows_kl;
-        s_red[w * 5 + 3] = tc;
-        s_red[w * 5 + 4] = te;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double v[5] = {0, 0, 0, 0, 0};
-        for (int j = 0; j < kWaves; ++j)
-            for (int k = 0; k < 5; ++k) v[k] += s_red[j * 5 + k];
-        const double msum = scal[0] > 1.f ? (double)scal[0] : 1.0;
-        const float pg = p.loss_reduction == 0 ? (float)(v[0] / msum) : (float)(v[1] / (double)n);
-        const float kl = p.use_kl_loss ? (float)(v[2] / (double)n) : 0.f;
-        const float entropy = (float)(v[4] / msum);
-        float final_loss = pg + kl * p.kl_loss_coef;
-        if (p.use_entropy_loss) final_loss = final_loss - entropy * p.entropy_loss_coef;
-        loss_out[0] = final_loss;
-        metrics[SKYRL_M_FINAL_LOSS] = final_loss;
-        metrics[SKYRL_M_POLICY_LOSS] = pg;
-        metrics[SKYRL_M_ENTROPY] = entropy;
-        metrics[SKYRL_M_KL] = kl;
-        metrics[SKYRL_M_CLIP_RATIO] = (float)(v[3] / msum);
-        metrics[SKYRL_M_MASK_SUM] = scal[0];
-        unsigned* err = reinterpret_cast<unsigned*>(const_cast<float*>(scal)) + 32;  // header word 32
-        metrics[6] = err[0] ? 1.f : 0.f;  // split-row exchange timed out (never expected)
-        metrics[7] = 0.f;
-        err[0] = 0u;
-    }
+    if (threadIdx.x == 0) finish_metrics(tot, n, p, scal, loss_out, metrics);
 }
 
 __global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* __restrict__ tok,
@@ -899,18 +1058,51 @@ __global__ __launch_bounds__(kThreads) void train_epilogue_kernel(const float* _
     epilogue_body<false>(tok, mask, n, R, p, scal, loss_out, metrics);
 }
 
-// The step fold: block k folds micro-batch k's records with the epilogue's code and order, so
-// its loss and metrics are the per-call epilogue's bits (for finite terms, see MASKED).
-__global__ __launch_bounds__(kThreads) void train_fold_kernel(const float* __restrict__ tok,
-                                                              const float* __restrict__ mask, int n_total, int R,
-                                                              int mb, skyrl_ppo_params p, const char* __restrict__ slots,
-                                                              float* __restrict__ loss_out,
-                                                              float* __restrict__ metrics) {
-    const int k = blockIdx.x;
+// The step fold: one wave per row (2 rows per block), the row's record (row_record, MASKED) stored
+// write-through, one arrival per row on the micro-batch's counter; the last row's wave sums the
+// micro-batch's records in row order (the per-call epilogue's order and bits, for finite terms)
+// and writes its loss and metrics (the plan's hand-off form).
+__global__ __launch_bounds__(kStepRows * kWave) void train_fold_kernel(
+    const float* __restrict__ tok, const float* __restrict__ mask, int n_total, int R, int mb, skyrl_ppo_params p,
+    char* __restrict__ slots, double* __restrict__ recs, float* __restrict__ loss_out, float* __restrict__ metrics) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * kStepRows + threadIdx.x / kWave;
+    if (b >= n_total) return;
+    const int k = b / mb;
     const int r0 = k * mb;
     const int n = min(n_total, r0 + mb) - r0;
-    epilogue_body<true>(tok + (int64_t)r0 * R * 4, mask + (int64_t)r0 * R, n, R, p,
-                        reinterpret_cast<const float*>(slots + k * kStepSlot), loss_out + k, metrics + k * SKYRL_M_COUNT);
+    float* scal = reinterpret_cast<float*>(slots + (size_t)k * kStepSlot);
+    unsigned* ctr = reinterpret_cast<unsigned*>(scal) + kSlotFoldCtr;
+    const RowRec r = row_record<true>(tok + (int64_t)b * R * 4, mask + (int64_t)b * R, R, p);
+    unsigned prev = 0;
+    if (lane == 0) {
+        double* d = recs + (size_t)b * 5;
+        st_wt(d + 0, r.tl);
+        st_wt(d + 1, r.pg);
+        st_wt(d + 2, r.kl);
+        st_wt(d + 3, r.tc);
+        st_wt(d + 4, r.te);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev != (unsigned)n - 1u) return;
+    RowRec tot{0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int j0 = 0; j0 < n; j0 += kWave) {
+        double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        if (j0 + lane < n) {
+            const double* d = recs + (size_t)(r0 + j0 + lane) * 5;
+#pragma unroll
+            for (int f = 0; f < 5; ++f) v[f] = __hip_atomic_load(d + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int j = 0; j < kWave && j0 + j < n; ++j)
+            rec_add(tot, RowRec{readlane_f64(v[0], j), readlane_f64(v[1], j), readlane_f64(v[2], j),
+                                readlane_f64(v[3], j), readlane_f64(v[4], j)});
+    }
+    if (lane == 0) {
+        finish_metrics(tot, n, p, scal, loss_out + k, metrics + (size_t)k * SKYRL_M_COUNT);
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
 }
 
 // dlogits *= g (skipped when g == 1: the common loss.backward() case)
@@ -1274,7 +1466,9 @@ namespace {
 constexpr int kStepMaxMicro = 4096;  // the tag's low 12 bits
 int step_micro_count(int32_t n_total, int32_t mb) { return (n_total + mb - 1) / mb; }
 size_t st_rows_off(int nm) { return 256 + pt_pad((size_t)nm * kStepSlot); }
-size_t st_tok_off(int32_t n_total, int nm) { return st_rows_off(nm) + pt_pad((size_t)n_total * 4); }
+size_t st_rsum_off(int32_t n_total, int nm) { return st_rows_off(nm) + pt_pad((size_t)n_total * 4); }
+size_t st_recs_off(int32_t n_total, int nm) { return st_rsum_off(n_total, nm) + pt_pad((size_t)n_total * 4); }
+size_t st_tok_off(int32_t n_total, int nm) { return st_recs_off(n_total, nm) + pt_pad((size_t)n_total * 5 * 8); }
 size_t st_gran_off(int32_t n_total, int32_t R, int nm) { return st_tok_off(n_total, nm) + pt_pad((size_t)n_total * R * 16); }
 const char* step_check(int32_t n_total, int32_t R, int32_t mb, const skyrl_ppo_params* params) {
     if (n_total <= 0 || R <= 0 || mb <= 0) return "bad sizes";
@@ -1292,16 +1486,52 @@ extern "C" size_t skyrl_policy_train_step_workspace_bytes(int32_t n_total, int32
     return st_gran_off(n_total, R, nm) + (size_t)min(micro_rows, n_total) * R * kSplitMaxP * 3 * 8;
 }
 
+namespace {
+int launch_plan(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows, const skyrl_ppo_params* params,
+                const float* scores, const void* rmask, int mask_dtype, int32_t G, float eps, int32_t norm_by_std,
+                float* adv, const float* pack_rsum, void* workspace, hipStream_t stream) {
+    char* w = reinterpret_cast<char*>(workspace);
+    const int nm = step_micro_count(n_total, micro_rows);
+    float* rows = reinterpret_cast<float*>(w + st_rows_off(nm));
+    float* rsum = reinterpret_cast<float*>(w + st_rsum_off(n_total, nm));
+    const dim3 grid((unsigned)((n_total + kStepRows - 1) / kStepRows));
+    auto k = mask_dtype == SKYRL_I64   ? train_plan_kernel<SKYRL_I64>
+             : mask_dtype == SKYRL_F32 ? train_plan_kernel<SKYRL_F32>
+             : mask_dtype == SKYRL_I32 ? train_plan_kernel<SKYRL_I32>
+                                       : train_plan_kernel<SKYRL_U8>;
+    hipLaunchKernelGGL(k, grid, dim3(kStepRows * kWave), 0, stream, loss_mask, n_total, R, micro_rows, *params, rows,
+                       rsum, w + 256, scores, rmask, G, eps, norm_by_std, adv, pack_rsum);
+    return check_launch("train_plan_kernel");
+}
+}  // namespace
+
 extern "C" int skyrl_policy_train_plan(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
                                        const skyrl_ppo_params* params, void* workspace, void* stream) {
     SKYRL_REQUIRE(loss_mask && workspace, "policy_train_plan: null pointer");
     const char* bad = step_check(n_total, R, micro_rows, params);
     SKYRL_REQUIRE(bad == nullptr, bad ? bad : "");
-    char* w = reinterpret_cast<char*>(workspace);
-    const int nm = step_micro_count(n_total, micro_rows);
-    hipLaunchKernelGGL(train_plan_kernel, dim3(nm), dim3(kThreads), 0, as_stream(stream), loss_mask, n_total, R,
-                       micro_rows, *params, reinterpret_cast<float*>(w + st_rows_off(nm)), w + 256);
-    return check_launch("train_plan_kernel");
+    return launch_plan(loss_mask, n_total, R, micro_rows, params, nullptr, nullptr, SKYRL_F32, 1, 0.f, 0, nullptr,
+                       nullptr, workspace, as_stream(stream));
+}
+
+extern "C" int skyrl_policy_train_plan_grpo(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
+                                            const skyrl_ppo_params* params, const float* scores,
+                                            const void* response_mask, int mask_dtype, int32_t group_size,
+                                            float epsilon, int32_t norm_by_std, float* advantages,
+                                            const float* loss_mask_row_sum, void* workspace, void* stream) {
+    SKYRL_REQUIRE(loss_mask && workspace && scores && response_mask && advantages,
+                  "policy_train_plan_grpo: null pointer");
+    const char* bad = step_check(n_total, R, micro_rows, params);
+    SKYRL_REQUIRE(bad == nullptr, bad ? bad : "");
+    SKYRL_REQUIRE(group_size >= 1 && group_size <= kWave && n_total % group_size == 0,
+                  "policy_train_plan_grpo: contiguous groups of 1..64 rows dividing the rows");
+    SKYRL_REQUIRE(mask_dtype == SKYRL_F32 || mask_dtype == SKYRL_I64 || mask_dtype == SKYRL_I32 ||
+                      mask_dtype == SKYRL_U8,
+                  "policy_train_plan_grpo: unsupported mask dtype");
+    SKYRL_REQUIRE((R % 4) != 0 || ((reinterpret_cast<uintptr_t>(advantages) | reinterpret_cast<uintptr_t>(response_mask)) % 16) == 0,
+                  "policy_train_plan_grpo: advantages / response mask must be 16-B aligned");
+    return launch_plan(loss_mask, n_total, R, micro_rows, params, scores, response_mask, mask_dtype, group_size,
+                       epsilon, norm_by_std, advantages, loss_mask_row_sum, workspace, as_stream(stream));
 }
 
 extern "C" int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
@@ -1360,9 +1590,11 @@ extern "C" int skyrl_policy_train_fold(const float* loss_mask, int32_t n_total, 
     SKYRL_REQUIRE(bad == nullptr, bad ? bad : "");
     char* w = reinterpret_cast<char*>(workspace);
     const int nm = step_micro_count(n_total, micro_rows);
-    hipLaunchKernelGGL(train_fold_kernel, dim3(nm), dim3(kThreads), 0, as_stream(stream),
+    hipLaunchKernelGGL(train_fold_kernel, dim3((unsigned)((n_total + kStepRows - 1) / kStepRows)),
+                       dim3(kStepRows * kWave), 0, as_stream(stream),
                        reinterpret_cast<const float*>(w + st_tok_off(n_total, nm)), loss_mask, n_total, R,
-                       micro_rows, *params, w + 256, loss_out, metrics_out);
+                       micro_rows, *params, w + 256, reinterpret_cast<double*>(w + st_recs_off(n_total, nm)), loss_out,
+                       metrics_out);
     return check_launch("train_fold_kernel");
 }
 

@@ -750,12 +750,19 @@ class PolicyTrainStep:
     (the workspace is shared)."""
 
     def __init__(self, old_log_probs, advantages, loss_mask, params, micro_rows: int, ref_log_probs=None,
-                 temperature: float = 1.0):
+                 temperature: float = 1.0, grpo=None):
+        """grpo (optional): dict(scores=[n_total] per-row reward sums, response_mask=[n_total, R],
+        group_size=G, epsilon=1e-6, norm_by_std=True, loss_mask_row_sum=None (pack's row sums: no
+        loss-mask read in the plan)): the plan launch also computes the
+        mini-batch's GRPO advantages (contiguous groups of G rows) INTO `advantages`
+        (skyrl_policy_train_plan_grpo), so GRPO costs no launch of its own."""
         dev = _require_gpu(old_log_probs, advantages, loss_mask, ref_log_probs)
         self.dev = dev
         self.old = _f32c(old_log_probs.detach(), "old_log_probs")
         n_total, R = self.old.shape
         self.adv = _f32c(advantages.detach(), "advantages")
+        if grpo is not None and self.adv.data_ptr() != advantages.data_ptr():
+            raise ValueError("grpo: advantages must be a contiguous f32 tensor (written in place)")
         self.mask = loss_mask.detach().to(torch.float32).contiguous()
         self.ref = None if ref_log_probs is None else _f32c(ref_log_probs.detach(), "ref_log_probs")
         for name, t in (("advantages", self.adv), ("loss_mask", self.mask), ("ref_log_probs", self.ref)):
@@ -777,8 +784,25 @@ class PolicyTrainStep:
         self.metrics = torch.empty((self.n_micro, _ffi.M_COUNT), dtype=torch.float32, device=dev)
         self.logp = torch.zeros((self.n_total, self.R), dtype=torch.float32, device=dev)
         self.entropy = torch.zeros((self.n_total, self.R), dtype=torch.float32, device=dev)
-        _ffi.call("skyrl_policy_train_plan", _ptr(self.mask), self.n_total, self.R, self.mb, ctypes.byref(params),
-                  _ptr(self.ws), _stream(dev))
+        if grpo is None:
+            _ffi.call("skyrl_policy_train_plan", _ptr(self.mask), self.n_total, self.R, self.mb, ctypes.byref(params),
+                      _ptr(self.ws), _stream(dev))
+        else:
+            scores = _f32c(grpo["scores"].detach(), "scores").view(-1)
+            rmask = grpo["response_mask"].detach().contiguous()
+            if scores.numel() != self.n_total or tuple(rmask.shape) != (self.n_total, self.R):
+                raise ValueError("grpo: scores [n_total] and response_mask [n_total, R] expected")
+            if rmask.dtype not in _MASK_DTYPES:
+                raise TypeError(f"grpo: response_mask dtype {rmask.dtype} unsupported")
+            rsum = grpo.get("loss_mask_row_sum")  # pack's: the plan then reads no loss mask
+            if rsum is not None:
+                rsum = _f32c(rsum.detach(), "loss_mask_row_sum").view(-1)
+                if rsum.numel() != self.n_total:
+                    raise ValueError("grpo: loss_mask_row_sum [n_total] expected")
+            _ffi.call("skyrl_policy_train_plan_grpo", _ptr(self.mask), self.n_total, self.R, self.mb,
+                      ctypes.byref(params), _ptr(scores), _ptr(rmask), _MASK_DTYPES[rmask.dtype],
+                      int(grpo["group_size"]), float(grpo.get("epsilon", 1e-6)), int(bool(grpo.get("norm_by_std", True))),
+                      _ptr(self.adv), _ptr(rsum), _ptr(self.ws), _stream(dev))
 
     def rows(self, k: int) -> Tuple[int, int]:
         return k * self.mb, min(self.n_total, (k + 1) * self.mb)

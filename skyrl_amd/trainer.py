@@ -269,7 +269,15 @@ class GRPOTrainer:
         if self.critic is not None:
             data["values"] = self._fwd_values(data)
         self._mark("fwd_logprobs")
-        data = trainer_utils.compute_advantages_and_returns(data, alg)
+        # GRPO inside the policy step's plan launch (skyrl_policy_train_plan_grpo) when the built-in
+        # estimator would run on contiguous groups with pack's reward row sums: the same advantages
+        # (bit for bit), no launch of their own; the estimator's metrics follow the update
+        plan_grpo = self._plan_grpo_ok(data, step_wise)
+        if plan_grpo:
+            data["advantages"] = torch.empty_like(data["rewards"])
+            data["returns"] = data["advantages"]  # compute_grpo_outcome_advantage returns (adv, adv)
+        else:
+            data = trainer_utils.compute_advantages_and_returns(data, alg)
         self._mark("advantages")
         metrics.update(data.metadata.get("metrics", {}))
         m = data["loss_mask"]
@@ -278,7 +286,10 @@ class GRPOTrainer:
             metrics["logprobs_diff_mean"] = float(((rl - data["action_log_probs"]).abs() * m).sum() / m.sum().clamp(min=1))
         if self.critic is not None:  # train_critic_and_policy: the critic steps first (trainer.py:1085-1120)
             metrics.update(self._train_critic(data))
-        metrics.update(self._train_policy(data))
+        metrics.update(self._train_policy(data, plan_grpo=plan_grpo))
+        if plan_grpo:
+            trainer_utils.advantage_metrics(data)
+            metrics.update(data.metadata["metrics"])
         self._mark("train")
         self.global_step += 1
         return metrics
@@ -320,7 +331,20 @@ class GRPOTrainer:
         return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
                                        device=next(self.critic.parameters()).device)
 
-    def _train_policy(self, data) -> Dict[str, float]:
+    def _plan_grpo_ok(self, data, step_wise: bool) -> bool:
+        """GRPO can run inside the policy step's plan launch: the built-in GRPO estimator (not a
+        plugin registered under its name), no critic, the fused policy pass, pack's reward row sums
+        (absent once a reward KL penalty changed the rewards), contiguous groups of G rows that the
+        mini-batches do not cut (no DP pad rows), and every row inside a trained mini-batch (the
+        reference estimates the dropped tail rows too)."""
+        alg, G = self.cfg.algorithm, self.cfg.n_samples_per_prompt
+        n = len(data["rewards"])
+        return (not step_wise and self.critic is None and alg.advantage_estimator == "grpo"
+                and ppo_utils.AdvantageEstimatorRegistry.get("grpo") is ppo_utils.compute_grpo_outcome_advantage
+                and data.get("reward_row_sum") is not None and data.metadata.get("pad_size", 0) == 0
+                and 1 <= G <= 64 and n % (self.cfg.policy_mini_batch_size * G) == 0 and self._fused_pass_ok())
+
+    def _train_policy(self, data, plan_grpo: bool = False) -> Dict[str, float]:
         """_execute_training_step: mini-batches of policy_mini_batch_size prompts (no shuffle,
         trainer.py:1067-1081), micro-batches inside, loss scaled by 1/n_micro, grad clip, AdamW.
         With the fused pass every mini-batch is one ops.PolicyTrainStep: one plan launch (the
@@ -337,16 +361,22 @@ class GRPOTrainer:
         R = data["response_mask"].shape[1]
         fused = self._fused_pass_ok()
         acc: Dict[str, List[float]] = {}
-        for _ in range(cfg.update_epochs_per_batch):
+        for epoch in range(cfg.update_epochs_per_batch):
             for s0, s1 in trainer_utils.mini_batch_slices(n, mini):
                 n_micro = math.ceil((s1 - s0) / mb)
                 step = None
                 if fused:
+                    grpo = None
+                    if plan_grpo and epoch == 0:  # this mini-batch's advantages, in the plan launch
+                        grpo = dict(scores=data["reward_row_sum"][s0:s1], response_mask=data["response_mask"][s0:s1],
+                                    group_size=cfg.n_samples_per_prompt, epsilon=1e-6,
+                                    norm_by_std=cfg.algorithm.grpo_norm_by_std,
+                                    loss_mask_row_sum=data.get("loss_mask_row_sum", None))
                     step = ops.PolicyTrainStep(
                         data["action_log_probs"][s0:s1], data["advantages"][s0:s1], data["loss_mask"][s0:s1],
                         self.loss_params, mb,
                         ref_log_probs=data["base_action_log_probs"][s0:s1] if self.ref is not None else None,
-                        temperature=cfg.temperature)
+                        temperature=cfg.temperature, grpo=grpo)
                 mets = []
                 for k, i in enumerate(range(s0, s1, mb)):
                     j = min(i + mb, s1)

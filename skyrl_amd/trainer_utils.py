@@ -294,6 +294,15 @@ def compute_advantages_and_returns(data: TrainingInputBatch, algorithm_cfg) -> T
             values=values, **kw)
     data["returns"] = ret
     data["advantages"] = adv
+    advantage_metrics(data, step_wise)
+    return data
+
+
+def advantage_metrics(data: TrainingInputBatch, step_wise: bool = False) -> None:
+    """trainer.py:838-860's metrics of compute_advantages_and_returns: avg_final_rewards /
+    avg_response_length / avg_advantages / avg_advantages_abs over the non-pad rows (device
+    reductions, one host read)."""
+    rewards, adv = data["rewards"], data["advantages"]
     pad = data.metadata.get("pad_size", 0)
     n = len(rewards) - pad
     m = data["response_mask"][:n].to(torch.float32)
@@ -308,7 +317,6 @@ def compute_advantages_and_returns(data: TrainingInputBatch, algorithm_cfg) -> T
         "avg_advantages": stats[1],
         "avg_advantages_abs": stats[2],
     })
-    return data
 
 
 @torch.no_grad()

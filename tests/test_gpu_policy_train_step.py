@@ -134,3 +134,93 @@ def test_step_micro_without_tokens_and_errors(dev):
         step.micro(2, logits[0:2], labels[0:2])
     with pytest.raises(ValueError):
         step.micro(0, logits[0:1], labels[0:1])
+
+
+@pytest.mark.parametrize("G,norm,mdt", [(8, True, torch.int64), (4, False, torch.int64), (1, True, torch.float32),
+                                        (16, True, torch.int32), (5, True, torch.bool)])
+def test_plan_grpo_advantages_equal_grpo_kernel(dev, G, norm, mdt):
+    """skyrl_policy_train_plan_grpo: the plan launch also writes the mini-batch's GRPO advantages
+    (pack's reward row sums as scores, contiguous groups of G). They must be skyrl_grpo_advantage's
+    bits (ops.grpo_advantage on the same scores), and the plan's loss scales those of the plain
+    plan (the micro-batches' losses unchanged), for every mask dtype, singleton groups and
+    zero-variance groups."""
+    n, R, mb = 8 * G if G > 1 else 24, 1024 if G != 5 else 130, 4
+    g = torch.Generator().manual_seed(G * 10 + int(norm))
+    lens = torch.randint(1, R + 1, (n,), generator=g)
+    live = torch.arange(R)[None] < lens[:, None]
+    rew = torch.zeros(n, R)
+    rew[torch.arange(n), lens - 1] = (torch.rand(n, generator=g) < 0.4).float()
+    rew[:G, :] = 0.0  # a zero-variance group (all scores 0)
+    rmask = live.to(mdt).to(dev)
+    lmask = (live & (torch.rand(n, R, generator=g) < 0.9)).float().to(dev)
+    scores = rew.sum(-1).to(dev)
+    params = _params(0, R)
+    ref_adv = ops.grpo_advantage(rew.to(dev), rmask, None, None, n // G, epsilon=1e-6, norm_by_std=norm, scores=scores)
+    old = torch.zeros(n, R, device=dev)
+    adv = torch.full((n, R), float("nan"), device=dev)
+    step = ops.PolicyTrainStep(old, adv, lmask, params, mb,
+                               grpo=dict(scores=scores, response_mask=rmask, group_size=G, norm_by_std=norm))
+    torch.cuda.synchronize()
+    assert torch.equal(adv, ref_adv)
+    ws_g = step.ws[:4096].clone()  # header + micro slots: scales and tags
+    step2 = ops.PolicyTrainStep(old, adv, lmask, params, mb)  # the plain plan
+    torch.cuda.synchronize()
+    ws_p = step2.ws[:4096].clone()
+    for k in range(step.n_micro):  # scal[0..2] of every micro slot are the same bits
+        o = 256 + 256 * k
+        assert torch.equal(ws_g[o:o + 12], ws_p[o:o + 12]), k
+
+
+def test_plan_and_fold_wide_grids_at_bench_shape(dev):
+    """The wide plan / fold (one wave per row, last arriver per micro-batch) at the bench's
+    512 x 1024 with 32 micro-batches of 16: the step's per-micro-batch loss and metrics equal
+    the per-call epilogue's (ops.policy_train on each micro-batch's logits) bit for bit, and the
+    plan's GRPO advantages feed the passes."""
+    n, R, mb, V = 64, 256, 16, 4096
+    live, logits, labels, old, adv, ref, mask = _batch(dev, n, R, V, 3)
+    params = _params(0, R)
+    step = ops.PolicyTrainStep(old, adv, mask, params, mb, ref_log_probs=ref)
+    for k in range(step.n_micro):
+        i, j = step.rows(k)
+        z = logits[i:j].contiguous().requires_grad_(True)
+        step.micro(k, z, labels[i:j]).backward()
+    losses, mets = step.fold()
+    for k in range(step.n_micro):
+        i, j = step.rows(k)
+        zc = logits[i:j].contiguous().requires_grad_(True)
+        l_c, m_c, _, _ = ops.policy_train(zc, labels[i:j], old[i:j], adv[i:j], mask[i:j], params, ref_log_probs=ref[i:j])
+        assert torch.equal(losses[k], l_c.detach()), k
+        assert torch.equal(mets[k], m_c), k
+
+
+@pytest.mark.parametrize("red", [0, 1, 2])
+def test_plan_with_pack_row_sums_equals_mask_plan(dev, red):
+    """The plan given pack's loss-mask row sums (no loss-mask read, no hand-over between rows) writes
+    the same slot scalars, epoch tags and row scales as the plan that sums the loss mask itself,
+    for every loss reduction, with GRPO advantages and a ragged last micro-batch."""
+    n, R, mb, G = 40, 300, 16, 4
+    g = torch.Generator().manual_seed(red + 77)
+    lens = torch.randint(1, R + 1, (n,), generator=g)
+    live = torch.arange(R)[None] < lens[:, None]
+    lmask = (live & (torch.rand(n, R, generator=g) < 0.8)).float().to(dev)
+    scores = (torch.rand(n, generator=g) < 0.5).float().to(dev)
+    rmask = live.to(torch.int64).to(dev)
+    params = _params(red, R)
+    old = torch.zeros(n, R, device=dev)
+    outs = []
+    for rows in (None, lmask.sum(-1)):
+        adv = torch.full((n, R), float("nan"), device=dev)
+        step = ops.PolicyTrainStep(old, adv, lmask, params, mb,
+                                   grpo=dict(scores=scores, response_mask=rmask, group_size=G, loss_mask_row_sum=rows))
+        torch.cuda.synchronize()
+        nm = step.n_micro
+        pad = lambda x: (x + 255) // 256 * 256  # noqa: E731
+        rows_end = 256 + pad(nm * 256) + pad(n * 4)  # header, micro slots, row scales
+        outs.append((adv.clone(), step.ws[:rows_end].clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    w0, w1 = (o[1].view(torch.int32) for o in outs)  # one cached workspace: the tags advance by one plan
+    for k in range(nm):
+        e = (256 + 256 * k) // 4 + 16
+        assert int(w1[e]) == int(w0[e]) + (1 << 12), k
+        w1[e] = w0[e]
+    assert torch.equal(w0, w1)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 V = 151936
 
 
-def _knobs(rows=256, wgs=2048, gran=8192):
+def _knobs(rows=256, wgs=1024, gran=8192):
     ops._ffi.call("skyrl_tune", b"sampler_split_rows", rows)
     ops._ffi.call("skyrl_tune", b"sampler_split_wgs", wgs)
     ops._ffi.call("skyrl_tune", b"sampler_split_gran", gran)
