@@ -55,6 +55,14 @@ import torch.distributed as dist  # noqa: E402
 P_MAX, R_MAX, PROMPTS, GROUP, VOCAB = 512, 1024, 64, 8, 151936
 QWEN_1_5B_PARAMS = 1_543_714_304  # Qwen2.5-1.5B, tied embeddings
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def SAMPLER_LABEL(nrows):
+    """The T = 1 sampler kernel the library picks at this row count (csrc/sampler.hip splits_for:
+    below 256 rows a row is split over workgroups, at or above one 512-thread workgroup per row)."""
+    if nrows >= 256:
+        return "skyrl_sample (sample_kernel<bf16,3,512>: T=1, one workgroup per row)"
+    return "skyrl_sample (sample_kernel<bf16,3,256>: T=1, split mode: each row over several workgroups, last arriver merges)"
 # reported beside frac, never instead of it: the guide's measured float4 copy (MI355X_MICROARCH.md,
 # "6.29 TB/s measured") for read+write kernels, and the read-only grid-stride stream our probe
 # measured on the box (7.0-7.1 TB/s, profiles/r03_rw_ceiling_probe2.log) for read-only kernels
@@ -410,7 +418,7 @@ def run(args):
     rows_per_launch = mb * R
     kernels = {}
     for name, tm, nbytes, launches_per_step, ceiling in (
-        ("skyrl_sample (sample_kernel<bf16,3,512>: T=1, one workgroup per row)", sample_timer, N * V * 2 + N * 16, R,
+        (SAMPLER_LABEL(N), sample_timer, N * V * 2 + N * 16, R,
          CEILING_READ_GBS),
         ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
          2 * (N // mb) + (N // mb if args.unfused else 0), CEILING_READ_GBS),

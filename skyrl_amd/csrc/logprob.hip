@@ -226,6 +226,7 @@ extern int g_sampler_split_rows;
 extern int g_sampler_split_wgs;
 extern int g_sampler_split_gran;
 extern int g_sampler_topk_fast;
+extern int g_topp_p2_slots;
 extern int g_sampler_topp_fast;
 extern int g_probe_topp;
 extern int g_attn_pf;
@@ -313,6 +314,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
         SKYRL_REQUIRE(value >= 2048 && value <= 65536 && value % 2048 == 0,
                       "skyrl_tune: sampler_split_gran must be a multiple of 2048 in [2048, 65536]");
         g_sampler_split_gran = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_topp_p2_slots") {
+        SKYRL_REQUIRE(value >= 1 && value <= 65536, "skyrl_tune: sampler_topp_p2_slots must be in [1, 65536]");
+        g_topp_p2_slots = value;
         return SKYRL_OK;
     }
     if (k == "sampler_topk_fast") {

@@ -188,3 +188,30 @@ def test_every_row_through_pass2(dev, V):
         etok, elp = osamp.sample(base[:, :V].contiguous(), 1.0, -1, p, mp, 4, ids, 9)
         assert torch.equal(tf, etok)
         torch.testing.assert_close(lf, elp, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("n", [300, 700])
+def test_pass2_slots_take_every_left_row(dev, n):
+    """Pass 2's grid is row slots x 8 pieces, each slot taking the left rows of rank s, s + slots,
+    ... from pass 1's flags: every row left (topp_probe 5) with the fewest slots the host allows
+    (ceil(n / 64): 64 rows per slot) and with 64, against the oracle and the two-kernel path."""
+    from oracle import sampler as osamp
+
+    V = 4097
+    g = torch.Generator().manual_seed(n + 3)
+    width = (V + 7) // 8 * 8 + 8
+    base = (torch.randn(n, width, generator=g) * 3).to(torch.bfloat16)
+    x = base.to(dev)[:, :V]
+    ids = torch.arange(n, dtype=torch.int64)
+    etok, elp = osamp.sample(base[:, :V].contiguous(), 1.0, -1, 0.9, 0.0, 6, ids, 3)
+    for slots in (1, 3, 64):
+        ops._ffi.call("skyrl_tune", b"sampler_topp_p2_slots", slots)
+        ops._ffi.call("skyrl_tune", b"topp_probe", 5)
+        try:
+            tf, lf, ff = _run(x, True, temperature=1.0, top_p=0.9, seed=6, seq_ids=ids.to(dev), step=3)
+        finally:
+            ops._ffi.call("skyrl_tune", b"topp_probe", 0)
+            ops._ffi.call("skyrl_tune", b"sampler_topp_p2_slots", 64)
+        assert bool((ff[:, 2] == _ROW_DONE).all()), slots
+        assert torch.equal(tf, etok), (slots, int((tf != etok).sum()))
+        torch.testing.assert_close(lf, elp, atol=1e-4, rtol=1e-4)
