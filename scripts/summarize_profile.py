@@ -1,4 +1,5 @@
-"""Turn a scripts/profile.sh run (gpurun_out/prof) into committed evidence under profiles/.
+"""Turn a scripts/profile.sh run (gpurun_out/prof, or the directory given after the tag) into
+committed evidence under profiles/.
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_kernel_stats.md    per-kernel table with short names
@@ -25,7 +26,10 @@ def short(name):
     return m.group(0) if m else name.split("(")[0][:60]
 
 
-def main(tag):
+def main(tag, src=None):
+    global SRC
+    if src:
+        SRC = src
     os.makedirs(DST, exist_ok=True)
     stats = os.path.join(SRC, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
@@ -66,4 +70,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else None)
