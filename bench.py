@@ -435,6 +435,8 @@ def run(args):
                          "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "ms_per_step": round(ms * launches_per_step, 2), "launches_timed": tm.launches,
                          "ceiling_GBps": ceiling}
+        if launches_per_step == 1:  # one launch (block) per step: each step's time, for the spread
+            kernels[name]["per_step_ms"] = [round(pr[0].elapsed_time(pr[1]), 3) for pr in tm.pairs]
     dom_name = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     # the advantage + loss launches the product issues per step outside the fused logits pass, eager
     # and event-timed inside the timed steps (GRPOTrainer: compute_advantages_and_returns' GRPO, then

@@ -90,4 +90,15 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
+// fp32 wave sum, the same DPP tree (quad_perm xor 1, xor 2, row_ror 4, 8, then the four row sums
+// read with v_readlane as (r0 + r1) + (r2 + r3)); wave-uniform. Requires all 64 lanes active.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+    auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+    return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+
 }  // namespace skyrl

@@ -226,7 +226,6 @@ extern int g_sampler_split_rows;
 extern int g_sampler_split_wgs;
 extern int g_sampler_split_gran;
 extern int g_sampler_topk_fast;
-extern int g_topp_p2_slots;
 extern int g_sampler_topp_fast;
 extern int g_probe_topp;
 extern int g_attn_pf;
@@ -316,18 +315,13 @@ extern "C" int skyrl_tune(const char* key, int value) {
         g_sampler_split_gran = value;
         return SKYRL_OK;
     }
-    if (k == "sampler_topp_p2_slots") {
-        SKYRL_REQUIRE(value >= 1 && value <= 65536, "skyrl_tune: sampler_topp_p2_slots must be in [1, 65536]");
-        g_topp_p2_slots = value;
-        return SKYRL_OK;
-    }
     if (k == "sampler_topk_fast") {
         SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_topk_fast must be 0 or 1");
         g_sampler_topk_fast = value;
         return SKYRL_OK;
     }
     if (k == "topp_probe") {
-        SKYRL_REQUIRE(value >= 0 && value <= 7, "skyrl_tune: topp_probe must be 0 .. 7");
+        SKYRL_REQUIRE((value >= 0 && value <= 7) || value == 11, "skyrl_tune: topp_probe must be 0 .. 7 or 11");
         g_probe_topp = value;
         return SKYRL_OK;
     }

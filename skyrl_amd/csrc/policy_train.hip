@@ -248,7 +248,11 @@ __global__ __launch_bounds__(kStepRows * kWave) void train_plan_kernel(
     unsigned* ctr = reinterpret_cast<unsigned*>(scal) + kSlotPlanCtr;
     // pack_rsum (skyrl_pack_experience's loss-mask row sums): every wave totals its micro-batch's
     // rows itself (row order, fp64): no mask read and no arrival; else the row's own sum here
-    const float acc = pack_rsum ? pack_rsum[b] : mask_row_sum(mask + (int64_t)b * R, R);
+    // (micro-batches of up to 64 rows: one load of all its row sums, first)
+    const float vrow = pack_rsum && n <= kWave ? pack_rsum[r0 + min(lane, n - 1)] : 0.f;
+    const float acc = pack_rsum ? (n <= kWave ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vrow), b - r0))
+                                              : pack_rsum[b])
+                                : mask_row_sum(mask + (int64_t)b * R, R);
     unsigned prev = 0;
     if (pack_rsum) {
         if (lane == 0 && p.loss_reduction != 0) row_scale[b] = row_scale_of(p, acc, n);
@@ -261,27 +265,43 @@ __global__ __launch_bounds__(kStepRows * kWave) void train_plan_kernel(
     if (scores) {  // GRPO: this row's advantages (overlaps the arrival's round trip)
         const int g0 = b - b % G;
         const float sj = lane < G ? scores[g0 + lane] : 0.f;
+        // the response mask's loads (up to R = 1024) issued with the scores', before the group
+        // statistics they do not depend on (clamped indices: unconditional loads)
+        constexpr int kPre = 4;
+        const int nq = R >> 2;
+        const bool pre = (R & 3) == 0 && nq <= kPre * kWave;
+        float mm[kPre][4];
+        if (pre) {
+#pragma unroll
+            for (int u = 0; u < kPre; ++u) load_mask4(rmask, MDT, (int64_t)b * R + 4 * min(lane + u * kWave, nq - 1), mm[u]);
+        }
+        auto lane_score = [&](int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sj), j)); };
         float mean_f, denom_f;
         if (G <= 1) {
             mean_f = 0.f;  // singleton group: mean 0, std 1 (ppo_utils.py:1167-1169)
             denom_f = norm_by_std ? (1.f + eps) : 1.f;
         } else {  // fp64 like torch.std on CPU, j in order
             double sum = 0.0;
-            for (int j = 0; j < G; ++j) sum += (double)__shfl(sj, j, kWave);
+            for (int j = 0; j < G; ++j) sum += (double)lane_score(j);
             const double mean = sum / (double)G;
             double m2 = 0.0;
             for (int j = 0; j < G; ++j) {
-                const double d = (double)__shfl(sj, j, kWave) - mean;
+                const double d = (double)lane_score(j) - mean;
                 m2 += d * d;
             }
             mean_f = (float)mean;
             const float std_f = (float)sqrt(m2 / (double)(G - 1));
             denom_f = norm_by_std ? (std_f + eps) : 1.f;
         }
-        const float sc = __shfl(sj, b - g0, kWave);
+        const float sc = lane_score(b - g0);
         const float a = norm_by_std ? (sc - mean_f) / denom_f : (sc - mean_f);
         float* orow = adv + (int64_t)b * R;
-        if ((R & 3) == 0) {
+        if (pre) {
+            float4* o4 = reinterpret_cast<float4*>(orow);
+#pragma unroll
+            for (int u = 0; u < kPre; ++u)
+                if (lane + u * kWave < nq) o4[lane + u * kWave] = make_float4(a * mm[u][0], a * mm[u][1], a * mm[u][2], a * mm[u][3]);
+        } else if ((R & 3) == 0) {
             float4* o4 = reinterpret_cast<float4*>(orow);
 #pragma unroll 4
             for (int i = lane; i < (R >> 2); i += kWave) {
@@ -295,10 +315,14 @@ __global__ __launch_bounds__(kStepRows * kWave) void train_plan_kernel(
     }
     double all = 0.0;
     if (pack_rsum) {  // every wave: the micro-batch's total; the wave of its first row writes the slot
-        for (int j0 = 0; j0 < n; j0 += kWave) {
-            const float v = j0 + lane < n ? pack_rsum[r0 + j0 + lane] : 0.f;
-            for (int j = 0; j < kWave && j0 + j < n; ++j)
-                all += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+        if (n <= kWave) {
+            for (int j = 0; j < n; ++j) all += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(vrow), j));
+        } else {
+            for (int j0 = 0; j0 < n; j0 += kWave) {
+                const float v = j0 + lane < n ? pack_rsum[r0 + j0 + lane] : 0.f;
+                for (int j = 0; j < kWave && j0 + j < n; ++j)
+                    all += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+            }
         }
         if (p.loss_reduction == 0 && lane == 0) row_scale[b] = (float)(1.0 / (all > 1.0 ? all : 1.0));
         if (b != r0) return;
@@ -986,11 +1010,11 @@ __device__ __forceinline__ RowRec row_record(const float* __restrict__ tok, cons
             am += m;
         }
     }
-    a0 = wave_sum(a0);
-    a1 = wave_sum(a1);
-    am = wave_sum(am);
-    tc = wave_sum(tc);
-    te = wave_sum(te);
+    a0 = wave_sum_dpp(a0);  // (DPP trees, no LDS round trips: the fold's wave is latency-bound)
+    a1 = wave_sum_dpp(a1);
+    am = wave_sum_dpp(am);
+    tc = wave_sum_dpp(tc);
+    te = wave_sum_dpp(te);
     const double mrow = am > 1.f ? am : 1.0;
     RowRec r{a0, 0.0, a1 / mrow, tc, te};
     if (p.loss_reduction == 1) r.pg = a0 / mrow;

@@ -35,8 +35,10 @@ int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups
 int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
 int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
-int g_topp_p2_slots = 64;  // skyrl_tune("sampler_topp_p2_slots"): pass-2 row slots (>= ceil(rows / 64))
-int g_probe_topp = 0;  // skyrl_tune("topp_probe"): 1 pass 1 alone, 2 pass 1 + the cut, 3 / 4 + a bare re-read
+#ifndef SKYRL_TP_PROBE0  // scripts/probe/topp_variants.py builds with another default; the product: 0
+#define SKYRL_TP_PROBE0 0
+#endif
+int g_probe_topp = SKYRL_TP_PROBE0;  // (11: per row, the cut's and pass 1's times in the outputs)  // skyrl_tune("topp_probe"): 1 pass 1 alone, 2 pass 1 + the cut, 3 / 4 + a bare re-read
                        // (timing only, tokens invalid); 5: every row through pass 2 (valid tokens); 6 / 7:
                        // min_p's in-row pass 2 timed per row (tokens = ticks; 7 without the visits)
 namespace {
@@ -1507,7 +1509,6 @@ constexpr int kPTieCap = 1024;  // elements at a split cut key
 constexpr int kPCandCap = 2048; // pass 1's exactly scored elements (seeds + bound survivors)
 constexpr int32_t kRowPending = -4;  // RowFilter.ik between the two top_p kernels: pass 2 to run
 constexpr int kP2Splits = 8;         // workgroups per left row in sample_topp_pass2_kernel
-constexpr int kP2RowsPerSlot = 64;   // left rows one pass-2 slot takes at most (slots = ceil(nseq / 64), >= 64)
 struct ToppPending {  // a row pass 1 did not decide, for sample_topp_pass2_kernel
     float xlo, xc, lse, mx;  // admissibility bound, the cut key's value, the raw lse, the raw max
     float e_s;               // e*: pass 1's best admissible record (score, index)
@@ -1525,7 +1526,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     const T* __restrict__ logits, int64_t ld, int V, float inv_t, int use_minp, float ln_min_p, float top_p,
     uint64_t seed, const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens,
     float* __restrict__ logp_out, RowFilter* __restrict__ filt, ToppPending* __restrict__ pend,
-    unsigned* __restrict__ pend_nt, int32_t* __restrict__ pflag, int probe) {
+    unsigned* __restrict__ pend_nt, int probe) {
     static_assert(sizeof(T) == 2, "bf16 rows");
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8;
     constexpr int kDummy = 2 * kPHalf;  // 64 words taking the out-of-window elements' increments (no branch)
@@ -1561,7 +1562,6 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         for (int u = 0; u < 4; ++u) cur[u] = rv[u * NT + threadIdx.x];
     }
     if (threadIdx.x == 0) {
-        pflag[row_i] = 0;  // (1 below when the row is left to pass 2: same thread, program order)
         s_nslow = 0u;
         s_bad = 0u;
         s_nt = 0u;
@@ -1596,6 +1596,10 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     float thr1 = -INFINITY;  // (bar - C) T, wave-uniform
     int seed_v = -1;         // this lane's seed element (scored once: no duplicate record)
     auto record = [&](float sc, int v, uint32_t b) {
+#ifdef SKYRL_TP_NOREC  // (probe builds only)
+        asm volatile("" ::"v"(sc), "v"(v), "v"(b));
+        return;
+#endif
         const uint32_t p = atomicAdd(&s_nc, 1u);
         if (p < (uint32_t)kPCandCap) {
             s_cs[p] = sc;
@@ -1650,7 +1654,9 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
 #pragma unroll
         for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, x[k]);
         vmx = fmaxf(vmx, vm);
+#ifndef SKYRL_TP_NORACE  // (probe builds only: timing attribution, tokens invalid)
         gumbel(x, raw, vm, v0, VEC);
+#endif
         {
             bool rare = false;
 #pragma unroll
@@ -1659,7 +1665,11 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 const int wi = (int)(b & 0x7fffu) - (kPE0 << 7);
                 const bool in = (unsigned)wi < (unsigned)kPHalf;
                 const int bin = (b & 0x8000u) ? kPHalf - 1 - wi : kPHalf + wi;
+#ifndef SKYRL_TP_NOHIST  // (probe builds only)
                 atomicAdd(&s_hist[in ? bin : kDummy + lane], 1u);
+#else
+                asm volatile("" ::"v"(bin), "v"(in));
+#endif
                 rare |= !in;  // (bitwise: a short-circuit || becomes branches)
             }
             if (__builtin_amdgcn_ballot_w64(rare) != 0 && rare) {
@@ -1761,6 +1771,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
     const float mthr = uni(mx * inv_t + ln_min_p);
     if (probe == 1) return;  // timing probe (skyrl_tune topp_probe): pass 1 only
+    const uint64_t t_p1 = __builtin_amdgcn_s_memrealtime();  // (probe 11: the cut's time per row)
 
     bool fb = s_bad != 0u || s_nslow > (uint32_t)kPSlowCap;  // block-uniform
     // the raw logits' sum-exp for the logprob, from the counts (another summation order than a
@@ -1901,6 +1912,13 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     if (!fb) {  // (the fallback's call site stays after the hot loops: the register allocation of
                 // the passes does not see it)
     if (probe == 2) return;  // timing probe: pass 1 + the cut
+    if (probe == 11) {  // timing probe: per row, the cut's and pass 1's times (10-ns ticks; tokens invalid)
+        if (threadIdx.x == 0) {
+            tokens[row_i] = (int)(__builtin_amdgcn_s_memrealtime() - t_p1);
+            if (logp_out) logp_out[row_i] = (float)(t_p1 - t_start);
+        }
+        return;
+    }
 
     // ---- pass 2: the Gumbel-max decision (MODE 2's noise, group bound and exact scores) over the
     //      admissible elements x >= xlo: top_p, the value above the cut key when the cut splits its
@@ -1984,7 +2002,6 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 pend_nt[2 * row_i] = 0u;      // the row's tie count and its pieces' arrival counter (the
                 pend_nt[2 * row_i + 1] = 0u;  // workspace layout moves with the batch size: not left re-armed)
                 filt[row_i] = RowFilter{mx, 0u, kRowPending, kc, ic};
-                pflag[row_i] = 1;
             }
             return;
         }
@@ -2307,15 +2324,25 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     if (threadIdx.x == 0) filt[row_i].ik = kRowFallback;
 }
 
-// one left row's piece (a call, not inlined: inside the kernel's row loop the inlined body
-// took 256 VGPRs against 53 alone; called: 120, two workgroups per CU)
+// Pass 2 of the rows sample_topp_kernel left pending (RowFilter.ik = kRowPending), each row cut into
+// kP2Splits workgroups of contiguous vectors (a fixed partition: the split-mode sampler's pattern).
+// (Measured and dropped in r05: a (slots x 8) grid over the left rows only, 25.6 vs 24 us; pass 2
+// inside pass 1's launch with the left rows' pieces claimed by the workgroups that finished -- a
+// CAS-claimed queue head ~1.4 ms, a row-by-row walk ~120 us, tickets ~88-91 vs 80-82 us a launch:
+// a piece claimed after the row's cut waits out the same latency chain as a launch, plus the claim.)
+// MODE 2 over the admissible elements x >= xlo of the piece, bar and best starting from e*; the
+// split cut key's indices appended to the row's tie list (one agent-scope add per lane). The last
+// arriving piece (arrive_last) merges the pieces' bests, ranks the ties by index (the first c are
+// admissible, scored exactly) and writes token, logprob and cut. The other rows' workgroups exit.
 template <typename T, bool TOPP>
-__device__ __attribute__((noinline)) void topp_pass2_row(
+__global__ __launch_bounds__(kPNT) void sample_topp_pass2_kernel(
     const T* __restrict__ logits, int64_t ld, int V, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
     int64_t step, int32_t* __restrict__ tokens, float* __restrict__ logp_out, RowFilter* __restrict__ filt,
     const ToppPending* __restrict__ pend, unsigned* __restrict__ pend_nt, int32_t* __restrict__ ties,
-    Best* __restrict__ parts, const int row_i, const int piece) {
+    Best* __restrict__ parts) {
     constexpr int NT = kPNT, NW = NT / kWave, VEC = 8, kPer = 8;  // up to kPer vectors per lane
+    const int row_i = blockIdx.x, piece = blockIdx.y;
+    if (filt[row_i].ik != kRowPending) return;  // (workgroup-uniform)
     __shared__ float s_bar, s_bs[NW];
     __shared__ int32_t s_bi[NW];
     __shared__ int s_last, s_icut;
@@ -2526,57 +2553,6 @@ __device__ __attribute__((noinline)) void topp_pass2_row(
     }
 }
 
-// Pass 2 of the rows sample_topp_kernel left pending (RowFilter.ik = kRowPending; pflag[row] = 1),
-// each row cut into kP2Splits workgroups of contiguous vectors (a fixed partition: the split-mode
-// sampler's pattern). The grid is (slots, kP2Splits), not (rows, kP2Splits): slot s takes the left
-// rows of rank s, s + slots, ... (each workgroup ranks pass 1's flags itself: no counter to re-arm),
-// so only the few left rows' pieces are launched, not rows x 8 mostly idle workgroups:
-// MODE 2 over the admissible elements x >= xlo of the piece, bar and best starting from e*; the
-// split cut key's indices appended to the row's tie list (one agent-scope add per lane). The last
-// arriving piece (arrive_last) merges the pieces' bests, ranks the ties by index (the first c are
-// admissible, scored exactly) and writes token, logprob and cut. The other rows' workgroups exit.
-template <typename T, bool TOPP>
-__global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_topp_pass2_kernel(
-    const T* __restrict__ logits, int64_t ld, int V, float inv_t, uint64_t seed, const int64_t* __restrict__ seq_ids,
-    int64_t step, int32_t* __restrict__ tokens, float* __restrict__ logp_out, RowFilter* __restrict__ filt,
-    const ToppPending* __restrict__ pend, unsigned* __restrict__ pend_nt, int32_t* __restrict__ ties,
-    Best* __restrict__ parts, const int32_t* __restrict__ pflag, int nseq) {
-    constexpr int NT = kPNT, NW = NT / kWave;
-    const int piece = blockIdx.y, slot = blockIdx.x, nslot = gridDim.x;
-    __shared__ int32_t s_mine[kP2RowsPerSlot];
-    __shared__ int s_wc[NW], s_nmine, s_base;
-    // the left rows in row order (pass 1's flags), this slot's share: ranks slot, slot + nslot, ...
-    if (threadIdx.x == 0) {
-        s_nmine = 0;
-        s_base = 0;
-    }
-    const int lane0 = threadIdx.x & (kWave - 1), w0 = threadIdx.x / kWave;
-    for (int r0 = 0; r0 < nseq; r0 += NT) {
-        const int r = r0 + (int)threadIdx.x;
-        const bool left = r < nseq && pflag[r] != 0;
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(left);
-        if (lane0 == 0) s_wc[w0] = __builtin_popcountll(bal);
-        __syncthreads();
-        int before = s_base;
-        for (int j = 0; j < w0; ++j) before += s_wc[j];
-        const int rank = before + __builtin_popcountll(bal & ((1ull << lane0) - 1ull));
-        if (left && rank % nslot == slot) s_mine[rank / nslot] = r;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int j = 0; j < NW; ++j) s_base += s_wc[j];
-        }
-        __syncthreads();
-    }
-    const int nmine = (s_base - slot + nslot - 1) / nslot;  // host: nslot * kP2RowsPerSlot >= nseq
-#pragma nounroll
-    for (int mi = 0; mi < nmine; ++mi) {
-        const int row_i = __builtin_amdgcn_readfirstlane(s_mine[mi]);  // (uniform: scalar addressing)
-        __syncthreads();  // the previous row's LDS reads before this row's writes
-        topp_pass2_row<T, TOPP>(logits, ld, V, inv_t, seed, seq_ids, step, tokens, logp_out, filt, pend, pend_nt, ties,
-                                parts, row_i, piece);
-    }
-}
-
 constexpr int kMaxSplits = 64;
 
 // Splits per row: below g_sampler_split_rows rows the row is cut into chunks of a multiple of
@@ -2659,22 +2635,18 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
             Best* pparts = reinterpret_cast<Best*>(pw);
             pw += ws_align((size_t)nseq * kP2Splits * sizeof(Best));
             int32_t* pties = reinterpret_cast<int32_t*>(pw);
-            pw += (size_t)nseq * kPTieCap * sizeof(int32_t);
-            int32_t* pflag = reinterpret_cast<int32_t*>(pw);  // per row: left to pass 2
             if (use_topp)
                 hipLaunchKernelGGL((sample_topp_kernel<T, true>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
                                    use_minp, ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt,
-                                   pflag, g_probe_topp);
+                                   g_probe_topp);
             else
                 hipLaunchKernelGGL((sample_topp_kernel<T, false>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
                                    use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt,
-                                   pflag, g_probe_topp);
+                                   g_probe_topp);
             int rc = check_launch("sample_topp_kernel");
-            if (rc || !use_topp || (g_probe_topp >= 1 && g_probe_topp <= 4)) return rc;  // (probes 1-4: pass 1 only)
-            const int slots = std::min(nseq, std::max(g_topp_p2_slots, (nseq + kP2RowsPerSlot - 1) / kP2RowsPerSlot));
-            hipLaunchKernelGGL((sample_topp_pass2_kernel<T, true>), dim3(slots, kP2Splits), dim3(kPNT), 0, stream, lg,
-                               ld, V, inv_t, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt, pties, pparts,
-                               pflag, nseq);
+            if (rc || !use_topp || (g_probe_topp >= 1 && g_probe_topp <= 4) || g_probe_topp == 11) return rc;  // (probes 1-4, 11)
+            hipLaunchKernelGGL((sample_topp_pass2_kernel<T, true>), dim3(nseq, kP2Splits), dim3(kPNT), 0, stream, lg, ld,
+                               V, inv_t, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt, pties, pparts);
             return check_launch("sample_topp_pass2_kernel");
         }
     }
@@ -2710,7 +2682,7 @@ extern "C" size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V) {
     return kCounterBytes + ws_align((size_t)nseq * sizeof(RowFilter)) +
            parts_bytes(nseq) + ws_align((size_t)nseq * sizeof(ToppPending)) +
            ws_align((size_t)nseq * 2 * sizeof(unsigned)) + ws_align((size_t)nseq * kP2Splits * sizeof(Best)) +
-           ws_align((size_t)nseq * kPTieCap * sizeof(int32_t)) + ws_align((size_t)nseq * sizeof(int32_t)) + 256;
+           (size_t)nseq * kPTieCap * sizeof(int32_t) + 256;
 }
 
 extern "C" int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V, float temperature,
