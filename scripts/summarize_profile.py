@@ -64,6 +64,15 @@ def main(tag, src=None):
             if key not in out["kernels"]:
                 out["kernels"][key] = dict(rec, instance=k, instances={})
             out["kernels"][key]["instances"][k] = rec
+        # kernels the new passes did not profile keep their earlier entries (with their round)
+        path = os.path.join(DST, "pmc_traffic.json")
+        if os.path.exists(path):
+            prev = json.load(open(path))
+            for k, v in prev.get("kernels", {}).items():
+                if k not in out["kernels"]:
+                    out["kernels"][k] = dict(v, round=v.get("round", "earlier"))
+        for v in out["kernels"].values():
+            v.setdefault("round", tag)
         with open(os.path.join(DST, "pmc_traffic.json"), "w") as fh:
             json.dump(out, fh, indent=1)
     print("profiles written for", tag)
