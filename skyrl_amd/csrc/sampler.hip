@@ -997,8 +997,11 @@ __device__ __forceinline__ void sample_unit(
         tokens, logp_out, parts, counters
 
 // Static grid: block (row, split).
+#ifndef SKYRL_SPLIT_WPE  // waves per SIMD the split (256-thread) instances are built for; probe builds vary it
+#define SKYRL_SPLIT_WPE 4
+#endif
 template <typename T, int MODE, int NT, bool PRIO = false>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel(SKYRL_SAMPLE_ARGS) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? SKYRL_SPLIT_WPE : 4))) void sample_kernel(SKYRL_SAMPLE_ARGS) {
     sample_unit<T, MODE, NT, PRIO>(SKYRL_SAMPLE_PASS, blockIdx.x, blockIdx.y, gridDim.y, blockIdx.x);
 }
 

@@ -371,7 +371,8 @@ class GRPOTrainer:
                         grpo = dict(scores=data["reward_row_sum"][s0:s1], response_mask=data["response_mask"][s0:s1],
                                     group_size=cfg.n_samples_per_prompt, epsilon=1e-6,
                                     norm_by_std=cfg.algorithm.grpo_norm_by_std,
-                                    loss_mask_row_sum=data.get("loss_mask_row_sum", None))
+                                    loss_mask_row_sum=(data["loss_mask_row_sum"][s0:s1]
+                                                       if data.get("loss_mask_row_sum") is not None else None))
                     step = ops.PolicyTrainStep(
                         data["action_log_probs"][s0:s1], data["advantages"][s0:s1], data["loss_mask"][s0:s1],
                         self.loss_params, mb,
@@ -435,15 +436,21 @@ class GRPOTrainer:
         lm_head under autocast, model_wrapper.py:308-363), then the step's fused pass computes
         logprob, entropy, the PPO/KL/entropy loss terms (worker.py:801-876) and dL/dz in one read
         of z; autograd's lm_head backward takes dL/dz into the dh / dW GEMMs. Same loss, metrics
-        and gradients as _logprobs + _loss (tests/test_gpu_trainer_e2e.py). None when the
-        micro-batch has no response token (nothing to back-propagate; the fold counts it as 0)."""
+        and gradients as _logprobs + _loss (tests/test_gpu_trainer_e2e.py). A micro-batch with no
+        response token contributes a zero loss through the same forward (the fold counts it as 0):
+        its backward still reaches every parameter, so the optimizer's per-bucket reduce-scatters
+        fire from the backward hooks in the same order on every rank."""
         seq, att = data["sequences"][i:j], data["attention_mask"][i:j]
         live = att[:, -R:].bool()
         pos = torch.nonzero(live.reshape(-1)).reshape(-1).to(torch.int32)
-        if pos.numel() == 0:
-            return None
         model = self.policy
         self._wait_weights(model)
+        if pos.numel() == 0:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                hidden = model.base_model(input_ids=seq, attention_mask=att,
+                                          position_ids=_positions(att)).last_hidden_state
+                w = model.get_output_embeddings().weight
+            return (hidden.float().sum() + w.float().sum()) * 0.0
         with torch.autocast("cuda", dtype=torch.bfloat16):
             base = model.base_model
             if self.cfg.use_sample_packing:

@@ -118,6 +118,17 @@ def test_gpt2_small_grpo_steps(gloo_world1, packing, monkeypatch):
         return out
 
     monkeypatch.setattr(trainer_utils, "compute_advantages_and_returns", checked_adv)
+    # with the built-in GRPO estimator the advantages come from the step plan's launch
+    # (skyrl_policy_train_plan_grpo) and are complete when the metrics are taken after training
+    orig_metrics = trainer_utils.advantage_metrics
+
+    def checked_metrics(data, step_wise=False):
+        exp = cpu_ref.grpo_advantage(data["rewards"].float().cpu(), data["response_mask"].cpu(),
+                                     data.metadata["uids"])
+        adv_checked.append(torch.allclose(data["advantages"].float().cpu(), exp, atol=1e-5, rtol=1e-5))
+        return orig_metrics(data, step_wise)
+
+    monkeypatch.setattr(trainer_utils, "advantage_metrics", checked_metrics)
 
     cfg = GPT2Config()  # GPT-2-small: 12 layers, 768 wide, 12 heads, V = 50,257
     assert cfg.vocab_size == 50257 and cfg.n_layer == 12
