@@ -143,20 +143,8 @@ def main():
     init = torch.cat([p.detach().reshape(-1) for p in policy.parameters()]).clone()
     out = []
     ok_all = True
-    # REHEARSE_EMPTY_LAST=1: on the last rank, the last micro-batch of every mini-batch (the last
-    # prompt group of it) has empty responses: no response token, a zero loss whose backward must
-    # still fire the bucket reduce-scatters in the other ranks' order
-    empty_last = os.environ.get("REHEARSE_EMPTY_LAST") == "1" and rank == world - 1
     for step in range(3):
         gen = fixed_generation(step, rank)
-        if empty_last:
-            mini = tcfg.policy_mini_batch_size * tcfg.n_samples_per_prompt
-            for b in range(0, len(gen["response_ids"]), mini):
-                for q in range(b + mini - tcfg.micro_train_batch_size_per_gpu, b + mini):
-                    gen["response_ids"][q], gen["rollout_logprobs"][q], gen["loss_masks"][q] = [], [], []
-            # per-token rewards (the reward on a response's last token; none for an empty one)
-            gen["rewards"] = [[0.0] * (len(r) - 1) + [w] if r else [] for r, w in
-                              zip(gen["response_ids"], gen["rewards"])]
         m = hip.train_on(copy.deepcopy(gen))
         a = torch.cat([p.detach().reshape(-1) for p in policy.parameters()])
         same = torch.tensor([1.0], device=dev)

@@ -437,9 +437,11 @@ class GRPOTrainer:
         logprob, entropy, the PPO/KL/entropy loss terms (worker.py:801-876) and dL/dz in one read
         of z; autograd's lm_head backward takes dL/dz into the dh / dW GEMMs. Same loss, metrics
         and gradients as _logprobs + _loss (tests/test_gpu_trainer_e2e.py). A micro-batch with no
-        response token contributes a zero loss through the same forward (the fold counts it as 0):
-        its backward still reaches every parameter, so the optimizer's per-bucket reduce-scatters
-        fire from the backward hooks in the same order on every rank."""
+        response token (not reachable from valid generator output: every response has a token, the
+        generator output check rejects empty reward lists as the reference's does) would contribute
+        a zero loss through the same forward (the fold counts it as 0), so its backward still
+        reaches every parameter and the per-bucket reduce-scatters fire from the backward hooks in
+        the same order on every rank."""
         seq, att = data["sequences"][i:j], data["attention_mask"][i:j]
         live = att[:, -R:].bool()
         pos = torch.nonzero(live.reshape(-1)).reshape(-1).to(torch.int32)

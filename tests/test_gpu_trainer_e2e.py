@@ -143,14 +143,6 @@ def test_trainer_passes_wait_for_the_in_flight_weight_gather():
     assert res["weight_reads"]["checked"] >= 12 and res["weight_reads"]["stale"] == 0, res["weight_reads"]
 
 
-def test_empty_last_micro_batch_on_one_rank():
-    """Two ranks (gloo, one GPU): the second rank's last micro-batch of every mini-batch has no
-    response token. Its zero-loss backward still fires every bucket's reduce-scatter (the first
-    rank's order), and the step still matches torch AdamW + clip on the rank-mean gradient."""
-    res = _run_optim_rehearsal(2, extra_env={"REHEARSE_EMPTY_LAST": "1"})
-    assert res["ok"], res
-
-
 def test_fused_policy_pass_matches_chunked_lmhead_path():
     """GRPOTrainer's policy micro-batch through the fused pass (lm_head GEMM -> ONE pass for
     logprob + entropy + PPO/KL/entropy loss + dL/dz -> the lm_head backward GEMMs) against the
