@@ -31,9 +31,6 @@
 namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows split over workgroups below this
-#ifndef SKYRL_SEED_IN_LOOP  // probe builds A/B the seed's placement (sampler_seed.py)
-#define SKYRL_SEED_IN_LOOP 1
-#endif
 int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: MODE 3 holds 4 waves per SIMD)
 int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
@@ -834,7 +831,6 @@ __device__ __forceinline__ void sample_unit(
             // puts vmcnt(2)/(1)/(0) before cur[1..3] in EVERY iteration: those counts then wait for
             // the next iteration's prefetch, and the last vector is processed with nothing in flight.
             __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-#if !SKYRL_SEED_IN_LOOP
             if constexpr (!greedy) {  // seed from this lane's first two vectors
                 float x[2][VEC];
                 bool ok[2][VEC];
@@ -867,7 +863,6 @@ __device__ __forceinline__ void sample_unit(
                 __syncthreads();
                 refresh_bar();
             }
-#endif
             SPHASE(1);
         }
         for (int base = 0; base < nfull; base += kStep) {
@@ -884,44 +879,6 @@ __device__ __forceinline__ void sample_unit(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) nxt[u] = ld_stream(rv + base + kStep + u * NT + threadIdx.x);
             }
-#if SKYRL_SEED_IN_LOOP
-            // the seed (first two vectors' exact scores, the workgroup's best as the bar) while the
-            // next iteration's loads are already in flight, instead of before them
-            if (base == 0) {
-                if constexpr (!greedy) {  // seed from this lane's first two vectors
-                    float x[2][VEC];
-                    bool ok[2][VEC];
-                    float xb[2] = {-INFINITY, -INFINITY};
-    #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        T vals[VEC];
-                        __builtin_memcpy(vals, &cur[u], 16);
-                        const int v0s = v_beg + (u * NT + threadIdx.x) * VEC;
-    #pragma unroll
-                        for (int k = 0; k < VEC; ++k) {
-                            x[u][k] = to_f<T>(vals[k]);
-                            ok[u][k] = true;
-                            if constexpr (MODE == 2) ok[u][k] = admissible(vals[k], x[u][k], v0s + k);
-                            xb[u] = fmaxf(xb[u], ok[u][k] ? x[u][k] : -INFINITY);
-                        }
-                    }
-                    if constexpr (MODE == 3) m = fmaxf(xb[0], xb[1]);  // lagged lse offset: this lane's first max
-                    const bool us = xb[1] > xb[0];
-                    float xs[VEC];
-                    bool oks[VEC];
-    #pragma unroll
-                    for (int k = 0; k < VEC; ++k) {  // selects, not a dynamically indexed array (scratch)
-                        xs[k] = us ? x[1][k] : x[0][k];
-                        oks[k] = us ? ok[1][k] : ok[0][k];
-                    }
-                    const int v0s = v_beg + ((us ? NT : 0) + threadIdx.x) * VEC;
-                    seed_vec(xs, oks, v0s, ehash(key, keyb, (uint32_t)v0s >> 3));
-                    // every wave starts from the best of the workgroup's 2 x NT seeds
-                    __syncthreads();
-                    refresh_bar();
-                }
-            }
-#endif
             if constexpr (MODE == 3) {
                 f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
