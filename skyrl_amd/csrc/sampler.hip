@@ -31,9 +31,6 @@
 namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows split over workgroups below this
-#ifndef SKYRL_SEED_BARRIER  // probe builds A/B the seeding barrier (scripts/probe/sampler_ab.py)
-#define SKYRL_SEED_BARRIER 1
-#endif
 int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: MODE 3 holds 4 waves per SIMD)
 int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
@@ -863,9 +860,7 @@ __device__ __forceinline__ void sample_unit(
                 const int v0s = v_beg + ((us ? NT : 0) + threadIdx.x) * VEC;
                 seed_vec(xs, oks, v0s, ehash(key, keyb, (uint32_t)v0s >> 3));
                 // every wave starts from the best of the workgroup's 2 x NT seeds
-#if SKYRL_SEED_BARRIER
                 __syncthreads();
-#endif
                 refresh_bar();
             }
             SPHASE(1);
