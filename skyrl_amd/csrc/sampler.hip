@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kFT) void sample_filter_kernel(const T* __restrict_
 }
 
 // MODE: 0 greedy (T == 0), 1 Gumbel-max without filters, 2 Gumbel-max with top_k / min_p,
-// 3 Gumbel-max without filters at T == 1 (the bound test reuses the lse exponentials).
+// 3 Gumbel-max without filters at T == 1 in row mode (the bound test reuses the lse exponentials).
 // NT threads per workgroup. Grid (row, split): with one split the workgroup owns the whole
 // row and finishes it alone; with several, the last-arriving split folds the partials.
 // Phase timestamps for scripts/probe/sampler_phase_probe (compiled only there, never in the product).
@@ -2594,6 +2594,14 @@ void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int6
                            counters);
 }
 
+// T = 1 in row mode takes the multiplicative bound on the lse exponentials (MODE 3); split
+// launches take the additive form (MODE 1), which measured faster there (64 / 128 rows: 14.85 /
+// 18.31 vs 15.14 / 18.64 us; 512 rows in row mode: 35.67 vs 33.35 us, same tokens;
+// profiles/r05_sampler_t1mode_ab.json). Probe builds set SKYRL_T1_MODE to 1 to time row mode
+// through the additive form.
+#ifndef SKYRL_T1_MODE
+#define SKYRL_T1_MODE 3
+#endif
 template <typename T>
 int launch_sample(const void* logits, int64_t ld, int nseq, int V, float temperature, int top_k, float top_p,
                   float min_p, uint64_t seed, const int64_t* seq_ids, int64_t step, int32_t* tokens, float* logp,
@@ -2667,8 +2675,8 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     else if (use_topk || use_minp || use_topp)
         launch_mode<T, 2>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, use_topk, use_minp, ln_min_p, seed, seq_ids,
                           step, use_topp, filt, tokens, logp, parts, counters);
-    else if (temperature == 1.0f)
-        launch_mode<T, 3>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
+    else if (temperature == 1.0f && row_mode)
+        launch_mode<T, SKYRL_T1_MODE>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
                           filt, tokens, logp, parts, counters);
     else
         launch_mode<T, 1>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
