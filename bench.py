@@ -62,7 +62,8 @@ def SAMPLER_LABEL(nrows):
     below 256 rows a row is split over workgroups, at or above one 512-thread workgroup per row)."""
     if nrows >= 256:
         return "skyrl_sample (sample_kernel<bf16,3,512>: T=1, one workgroup per row)"
-    return "skyrl_sample (sample_kernel<bf16,3,256>: T=1, split mode: each row over several workgroups, last arriver merges)"
+    return ("skyrl_sample (sample_kernel<bf16,1,256>: T=1 through the additive bound, split mode: each row over "
+            "several workgroups, last arriver merges)")
 # reported beside frac, never instead of it: the guide's measured float4 copy (MI355X_MICROARCH.md,
 # "6.29 TB/s measured") for read+write kernels, and the read-only grid-stride stream our probe
 # measured on the box (7.0-7.1 TB/s, profiles/r03_rw_ceiling_probe2.log) for read-only kernels
