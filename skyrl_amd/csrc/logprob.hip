@@ -326,7 +326,7 @@ extern "C" int skyrl_tune(const char* key, int value) {
         return SKYRL_OK;
     }
     if (k == "sampler_topp_fast") {
-        SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_topp_fast must be 0 or 1");
+        SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: sampler_topp_fast must be 0, 1 or 2");
         g_sampler_topp_fast = value;
         return SKYRL_OK;
     }

@@ -34,7 +34,11 @@ int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows spli
 int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: MODE 3 holds 4 waves per SIMD)
 int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
-int g_sampler_topp_fast = 1;  // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels
+// skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels; 1 (default)
+// = the one-pass kernel, except min_p without top_p below the row-mode batch, where the pre-pass and
+// the split MODE 2 sampler measured faster (32 / 64 / 128 rows: 26.2 / 33.0 / 43.2 vs 43.8 / 44.8 /
+// 47.4 us; 256 rows: 68.1 vs 49.6; same tokens; profiles/r05_topp_rows.json); 2 = always the one-pass kernel
+int g_sampler_topp_fast = 1;
 #ifndef SKYRL_TP_PROBE0  // scripts/probe/topp_variants.py builds with another default; the product: 0
 #define SKYRL_TP_PROBE0 0
 #endif
@@ -2634,7 +2638,9 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     }
     // top_p / min_p without top_k on 16-B aligned bf16 rows: the two-pass kernel alone
     if constexpr (sizeof(T) == 2) {
-        if (g_sampler_topp_fast && !use_topk && (use_topp || use_minp) && V <= kP2Splits * 8 * kPNT * 8 &&
+        if (g_sampler_topp_fast && !use_topk &&
+            (use_topp || (use_minp && (g_sampler_topp_fast == 2 || nseq >= g_sampler_split_rows))) &&
+            V <= kP2Splits * 8 * kPNT * 8 &&
             (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
             // the pass-2 kernel's per-row state after the split sampler's parts (never used by this path)

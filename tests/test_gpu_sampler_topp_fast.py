@@ -1,6 +1,8 @@
 """a1 filtered sampling without top_k: the top_p / min_p kernel (sample_topp_kernel) against the
 two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
-skyrl_tune("sampler_topp_fast", 0)) and against oracle/sampler_ref.c.
+skyrl_tune("sampler_topp_fast", 0)) and against oracle/sampler_ref.c. The tests force the kernel
+with skyrl_tune("sampler_topp_fast", 2); the default (1) sends min_p without top_p below 256 rows
+to the two-kernel path, which is faster there.
 
 Pass 1 takes the row max, a count histogram per exact bf16 key and MODE 2's race over the whole
 row (every scored element recorded); the top_p cut is found on chip and the race's best record
@@ -35,7 +37,7 @@ def _filters(x):
 
 
 def _run(x, fast, **kw):
-    ops._ffi.call("skyrl_tune", b"sampler_topp_fast", int(fast))
+    ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 2 if fast else 0)  # 2: the one-pass kernel at any row count
     try:
         tok, lp = ops.sample(x, **kw)
         torch.cuda.synchronize()
@@ -139,6 +141,26 @@ def test_topp_fast_split_ties_and_fallback_rows(dev):
     assert bool((ff[k:3 * k, 2] == _ROW_DONE).all()) and bool((ff[4 * k:, 2] == _ROW_DONE).all())
     assert bool((ff[3 * k:3 * k + 3, 2] == _ROW_FALLBACK).all()) and bool((ff[3 * k + 3:3 * k + 6, 2] == _ROW_DONE).all())
     assert int(ff[3 * k + 6, 2]) == _ROW_FALLBACK and bool((ff[3 * k + 7:4 * k, 2] == _ROW_DONE).all())
+
+
+def test_minp_default_route_by_row_count(dev):
+    """Default routing (sampler_topp_fast 1): min_p alone at 64 rows takes the two-kernel path
+    (the RowFilter's state is the pre-pass's, not the one-pass kernel's done mark), at 256 rows the
+    one-pass kernel; both give oracle/sampler_ref.c's tokens."""
+    from oracle import sampler as osamp
+
+    V = 32000
+    g = torch.Generator().manual_seed(12)
+    for n, one_pass in ((64, False), (256, True)):
+        x = (torch.randn(n, V, generator=g) * 2).to(torch.bfloat16)
+        ids = torch.arange(n, dtype=torch.int64) + 7
+        tok, lp = ops.sample(x.to(dev), temperature=1.0, min_p=0.05, seed=3, seq_ids=ids.to(dev), step=5)
+        torch.cuda.synchronize()
+        ff = _filters(x.to(dev))
+        assert bool((ff[:, 2] == _ROW_DONE).all()) == one_pass, n
+        etok, elp = osamp.sample(x, 1.0, -1, 1.0, 0.05, 3, ids, 5)
+        assert torch.equal(tok.cpu(), etok), (n, int((tok.cpu() != etok).sum()))
+        torch.testing.assert_close(lp.cpu(), elp, atol=1e-4, rtol=1e-4)
 
 
 @pytest.mark.parametrize("V", [100, 517, 1000, 4097, 50257])
