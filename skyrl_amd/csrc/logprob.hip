@@ -225,6 +225,7 @@ extern int g_sampler_row;
 extern int g_sampler_split_rows;
 extern int g_sampler_split_wgs;
 extern int g_sampler_split_gran;
+extern int g_sampler_split_nt;
 extern int g_sampler_topk_fast;
 extern int g_sampler_topp_fast;
 extern int g_probe_topp;
@@ -313,6 +314,11 @@ extern "C" int skyrl_tune(const char* key, int value) {
         SKYRL_REQUIRE(value >= 2048 && value <= 65536 && value % 2048 == 0,
                       "skyrl_tune: sampler_split_gran must be a multiple of 2048 in [2048, 65536]");
         g_sampler_split_gran = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_split_nt") {
+        SKYRL_REQUIRE(value == 256 || value == 512, "skyrl_tune: sampler_split_nt must be 256 or 512");
+        g_sampler_split_nt = value;
         return SKYRL_OK;
     }
     if (k == "sampler_topk_fast") {

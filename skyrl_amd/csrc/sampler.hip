@@ -32,6 +32,7 @@ namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows split over workgroups below this
 int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: MODE 3 holds 4 waves per SIMD)
+int g_sampler_split_nt = 256;    // skyrl_tune("sampler_split_nt"): threads per split-mode workgroup (256 or 512)
 int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
 // skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels; 1 (default)
@@ -2589,7 +2590,7 @@ void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int6
         hipLaunchKernelGGL((sample_kernel<T, MODE, 512, true>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t,
                            use_topk, use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts,
                            counters);
-    else if (row_mode)
+    else if (row_mode || g_sampler_split_nt == 512)
         hipLaunchKernelGGL((sample_kernel<T, MODE, 512>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
                            use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts, counters);
     else
