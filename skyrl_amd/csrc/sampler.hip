@@ -31,7 +31,7 @@
 namespace skyrl {
 int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
 int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows split over workgroups below this
-int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: MODE 3 holds 4 waves per SIMD)
+int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: 4 waves per SIMD at 256 threads)
 int g_sampler_split_nt = 256;    // skyrl_tune("sampler_split_nt"): threads per split-mode workgroup (256 or 512)
 int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
 int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels

@@ -4,7 +4,8 @@ arriver folds the partials (no acquire: sc1 records, MI355X_MICROARCH.md's valid
 against oracle/sampler_ref.c (tokens bit-exact, logprobs 1e-4) and against the same rows decided
 by one workgroup per row (tokens identical: every split decides with exact scores, the lowest
 index on ties). The split count follows skyrl_tune("sampler_split_wgs") and the row threshold
-"sampler_split_rows"; every setting must give the same tokens."""
+"sampler_split_rows", the split workgroup size "sampler_split_nt"; every setting must give the same
+tokens (T = 1 runs the multiplicative bound in row mode and the additive one in split mode)."""
 
 import pytest
 import torch
@@ -16,7 +17,8 @@ pytestmark = pytest.mark.gpu
 V = 151936
 
 
-def _knobs(rows=256, wgs=1024, gran=8192):
+def _knobs(rows=256, wgs=1024, gran=8192, nt=256):
+    ops._ffi.call("skyrl_tune", b"sampler_split_nt", nt)
     ops._ffi.call("skyrl_tune", b"sampler_split_rows", rows)
     ops._ffi.call("skyrl_tune", b"sampler_split_wgs", wgs)
     ops._ffi.call("skyrl_tune", b"sampler_split_gran", gran)
@@ -30,8 +32,11 @@ def _restore():
 
 @pytest.mark.parametrize("n", [64, 128])
 @pytest.mark.parametrize("temp", [1.0, 0.7, 0.0])
-def test_split_rows_match_oracle(dev, n, temp):
+@pytest.mark.parametrize("nt", [256, 512])
+def test_split_rows_match_oracle(dev, n, temp, nt):
     from oracle import sampler as osamp
+
+    _knobs(nt=nt)
 
     g = torch.Generator().manual_seed(n * 10 + int(temp * 10))
     x = (torch.randn(n, V, generator=g) * 3).to(torch.bfloat16)
@@ -51,9 +56,11 @@ def test_split_settings_give_identical_tokens(dev, n):
     x = big[:, 1]  # row stride 3 V
     ids = torch.arange(n, dtype=torch.int64, device=dev) + 1000
     outs = {}
-    for rows, wgs, gran in ((1, 2048, 8192), (256, 2048, 8192), (1024, 2048, 8192), (1024, 512, 8192),
-                            (1024, 8192, 8192), (1024, 1024, 2048), (1024, 8192, 2048), (1024, 960, 4096)):
-        _knobs(rows, wgs, gran)
+    for rows, wgs, gran, nt in ((1, 2048, 8192, 256), (256, 2048, 8192, 256), (1024, 2048, 8192, 256),
+                                (1024, 512, 8192, 256), (1024, 8192, 8192, 256), (1024, 1024, 2048, 256),
+                                (1024, 8192, 2048, 256), (1024, 960, 4096, 256), (1024, 256, 16384, 512),
+                                (1024, 2048, 2048, 512)):
+        _knobs(rows, wgs, gran, nt)
         for temp in (1.0, 0.0, 1.3):
             tok, lp = ops.sample(x, temperature=temp, seed=2, seq_ids=ids, step=5)
             outs.setdefault(temp, []).append((tok.clone(), lp.clone()))
