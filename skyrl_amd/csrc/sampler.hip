@@ -634,6 +634,14 @@ __device__ __forceinline__ void sample_unit(
             if constexpr (MODE == 3) recompute_q();
         }
     };
+    // after a candidate vector: publish the wave's best and read the workgroup's when some lane
+    // improved on the bar, else only read the workgroup's (the wave max and the LDS max skipped:
+    // 512 / 128 / 64 rows at T = 1 33.28 / 17.78 / 14.22 vs 34.44 / 18.59 / 14.80 us, same tokens;
+    // profiles/r05_sampler_eval_form_ab.json, form 1)
+    auto after_eval = [&]() {
+        if (__builtin_amdgcn_ballot_w64(best_s > bar) != 0) raise_bar();
+        else refresh_bar();
+    };
     // additive bound test of a vector whose largest admissible logit is xm
     auto cand_add = [&](float xm, uint32_t h) -> bool {
         const float bits = (float)(int)__float_as_uint((float)(h >> 16));
@@ -743,7 +751,7 @@ __device__ __forceinline__ void sample_unit(
         const bool cand = xm > -INFINITY && cand_add(xm, h);
         if (__builtin_amdgcn_ballot_w64(cand) == 0) return;  // wave-uniform: rare once the bar is up
         if (cand) eval_vec(x, ok, v0, h);
-        raise_bar();
+        after_eval();
     };
     // MODE 3 full vector, lagged lse offset m (exps accumulate into acc2; the caller checks
     // for overflow once per iteration)
@@ -785,6 +793,10 @@ __device__ __forceinline__ void sample_unit(
 #ifdef SKYRL_SV_NOCAND
         cand = false;
 #endif
+#if defined(SKYRL_SV_NOCAND_LIVE) && SKYRL_SV_NOCAND_LIVE  // probe: the bound test computed, nothing evaluated
+        asm volatile("" ::"v"((int)cand));
+        cand = false;
+#endif
         if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
         if (cand) {
             bool ok[VEC];
@@ -792,7 +804,7 @@ __device__ __forceinline__ void sample_unit(
             for (int k = 0; k < VEC; ++k) ok[k] = true;
             eval_vec(x, ok, v0, h);
         }
-        raise_bar();
+        after_eval();
     };
     // lse of one iteration redone with a fresh offset after an overflow of the lagged one
     auto lse_refresh = [&](const uint4 (&dw)[4]) {
