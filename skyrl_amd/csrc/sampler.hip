@@ -492,6 +492,11 @@ __device__ uint64_t g_sphase[4096 * 8];
 // TieSink (the top_p kernel's pass 2, TIES = true): elements whose key is `kc` are taken out of
 // the decision and appended to an LDS list with their exact scores (the caller ranks them by
 // index: the cut keeps the first c); a kc no key equals (> 0xffff) disables it at run time.
+// the top_p kernel's pass-1 bar: 1 publishes only when a lane improved (product), 0 after every
+// candidate vector (probe builds, scripts/probe/sampler_ab.py)
+#ifndef SKYRL_TP_BAR_FORM
+#define SKYRL_TP_BAR_FORM 1
+#endif
 struct TieSink {
     int32_t* idx;
     float* sc;
@@ -1627,12 +1632,30 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             s_ck[p] = (uint16_t)b;
         }
     };
+#if SKYRL_TP_BAR_FORM
+    // publish the wave's best new score and read the workgroup's when a lane beat the wave's bar,
+    // else only read the workgroup's (as the unfiltered sampler's after_eval). s_bar1 stays the
+    // best record: an unpublished score is <= bar1 <= s_bar1.
+    float bar1 = -INFINITY;
+    auto bar_merge = [&](float best_new) {
+        if (__builtin_amdgcn_ballot_w64(best_new > bar1) != 0) {
+            const float wb = wave_max_uniform(best_new);
+            if (lane == 0 && wb > -INFINITY)
+                __hip_atomic_fetch_max(&s_bar1, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            bar1 = fmaxf(wb, uni(s_bar1));
+        } else {
+            bar1 = fmaxf(bar1, uni(s_bar1));
+        }
+        thr1 = (bar1 - kNoiseC) * temp;
+    };
+#else
     auto bar_merge = [&](float best_new) {  // publish the wave's best new score, read the workgroup's
         const float wb = wave_max_uniform(best_new);
         if (lane == 0 && wb > -INFINITY)
             __hip_atomic_fetch_max(&s_bar1, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         thr1 = (fmaxf(wb, uni(s_bar1)) - kNoiseC) * temp;
     };
+#endif
     // the group bound and the exact scores of one group's elements (x[k] at v0 + k, raw bits b[k])
     auto gumbel = [&](const float (&x)[VEC], const uint16_t (&b)[VEC], float vm, int v0, int cnt) {
         const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
