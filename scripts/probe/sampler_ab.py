@@ -1,5 +1,5 @@
 """A/B of a compile-time switch of the T > 0 sampler (sampler.hip), at 512 rows (row mode, the
-bench's decode step) and 64 / 128 rows (split mode) x V = 151,936 bf16, T = 1 and T = 0.7, and top_p 0.95 at T = 1 and 0.6: one
+bench's decode step) and 64 / 128 rows (split mode) x V = 151,936 bf16, T = 1 and T = 0.7, top_p 0.95 at T = 1 and 0.6, and min_p 0.05: one
 capi.hip + sampler.hip library per value of AB_DEFINE (default SKYRL_LAZY_BAR) in AB_VALUES
 (default 0,1), interleaved rounds of 200 back-to-back launches, medians; the tokens of every
 value must be equal (the switches change speed only).
@@ -47,24 +47,24 @@ def run():
             lib.skyrl_sample_workspace_bytes.restype = ctypes.c_size_t
             for n in (64, 128, 512):
                 ws = torch.zeros(lib.skyrl_sample_workspace_bytes(n, V), dtype=torch.uint8, device=dev)
-                for temp, top_p in ((1.0, 1.0), (0.7, 1.0), (1.0, 0.95), (0.6, 0.95)):
+                for temp, top_p, min_p in ((1.0, 1.0, 0.0), (0.7, 1.0, 0.0), (1.0, 0.95, 0.0), (0.6, 0.95, 0.0), (1.0, 1.0, 0.05)):
                     def call(t):
                         rc = lib.skyrl_sample(ctypes.c_void_p(big.data_ptr()), 1, ctypes.c_int64(V), n, V,
-                                              ctypes.c_float(temp), -1, ctypes.c_float(top_p), ctypes.c_float(0.0),
+                                              ctypes.c_float(temp), -1, ctypes.c_float(top_p), ctypes.c_float(min_p),
                                               ctypes.c_uint64(1), ctypes.c_void_p(ids.data_ptr()), ctypes.c_int64(t),
                                               ctypes.c_void_p(tok.data_ptr()), ctypes.c_void_p(lp.data_ptr()),
                                               ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(s.cuda_stream))
                         assert rc == 0
                     call(3)
                     torch.cuda.synchronize()
-                    toks.setdefault(f"n{n}_T{temp}_p{top_p}", {})[v] = tok[:n].cpu().clone()
+                    toks.setdefault(f"n{n}_T{temp}_p{top_p}_m{min_p}", {})[v] = tok[:n].cpu().clone()
                     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     a.record(s)
                     for t in range(200):
                         call(t)
                     b.record(s)
                     b.synchronize()
-                    out.setdefault(f"n{n}_T{temp}_p{top_p}_{DEF}{v}", []).append(a.elapsed_time(b) / 200 * 1e3)
+                    out.setdefault(f"n{n}_T{temp}_p{top_p}_m{min_p}_{DEF}{v}", []).append(a.elapsed_time(b) / 200 * 1e3)
     res = {k: round(sorted(x)[len(x) // 2], 2) for k, x in out.items()}
     res["tokens_equal"] = all(all(torch.equal(d[VALS[0]], d[v]) for v in VALS) for d in toks.values())
     print(json.dumps(res), flush=True)

@@ -497,6 +497,12 @@ __device__ uint64_t g_sphase[4096 * 8];
 #ifndef SKYRL_TP_BAR_FORM
 #define SKYRL_TP_BAR_FORM 1
 #endif
+// the same for the top_p pass-2 kernel's pieces (1, product; the form measured 65 -> 80 us in the
+// in-row min_p pass 2, which keeps publishing after every candidate vector:
+// profiles/r05_topp2_bar_form_ab.json)
+#ifndef SKYRL_TP2_BAR_FORM
+#define SKYRL_TP2_BAR_FORM 1
+#endif
 struct TieSink {
     int32_t* idx;
     float* sc;
@@ -2477,9 +2483,19 @@ __global__ __launch_bounds__(kPNT) void sample_topp_pass2_kernel(
                 }
             }
         }
+#if SKYRL_TP2_BAR_FORM
+        if (__builtin_amdgcn_ballot_w64(best_s > bar) != 0) {  // publish only when a lane improved
+            const float wb = wave_max_uniform(best_s);
+            if (lane == 0 && wb > bar) __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            bar = fmaxf(wb, uni(s_bar));
+        } else {
+            bar = fmaxf(bar, uni(s_bar));
+        }
+#else
         const float wb = wave_max_uniform(best_s);
         if (lane == 0 && wb > bar) __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         bar = fmaxf(wb, uni(s_bar));
+#endif
         thr = (bar - kNoiseC) * temp;
     }
     if (piece == kP2Splits - 1 && nvec * VEC < V) {  // the ragged tail's partial group, by thread 0
