@@ -47,7 +47,8 @@ const char* skyrl_last_error(void);
  * skyrl_policy_train_ragged_fwd, the policy_train workspace holds the split-row exchange; 7:
  * skyrl_comm_* RCCL collectives; 8: the step form of the fused policy pass,
  * skyrl_policy_train_plan / _micro_fwd / _fold; 9: per-parameter AdamW,
- * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy, skyrl_policy_train_plan_grpo). */
+ * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy, skyrl_policy_train_plan_grpo;
+ * 10: skyrl_adv_norm_stats / _apply). */
 int skyrl_abi_version(void);
 /* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
  * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
@@ -88,6 +89,22 @@ int skyrl_grpo_advantage(const float* rewards, const float* scores_in /* [N] or 
                          const int32_t* group_off, const int32_t* group_rows, int32_t num_groups,
                          int32_t N, int32_t R, float epsilon, int32_t norm_by_std,
                          float* advantages, float* scores_out /* [N] or NULL */, void* stream);
+
+/* ---- a4 (cont.): advantage_batch_normalize --------------------------------
+ * Replaces normalize_advantages_dict (utils/ppo_utils.py:127-145) as applied after the
+ * advantages when trainer.algorithm.advantage_batch_normalize is set (trainer.py:275-276,
+ * fully_async_trainer.py:514-515): mean over EVERY element (unmasked), ss = sum((adv -
+ * mean)^2 * mask), rstd = rsqrt(clamp(ss / sum(mask), 1e-8)), out = (adv - mean) * rstd
+ * (not re-masked). Two launches so a data-parallel caller can SUM-all-reduce the sums between
+ * them (one all-reduce of 5 fp64 scalars):
+ *   skyrl_adv_norm_stats  sums_out f64[5] (device) = (sum adv, sum mask, sum adv*mask,
+ *                         sum adv^2*mask, n); workspace: skyrl_adv_norm_workspace_bytes(),
+ *                         16-B aligned, zeroed once at allocation (the kernel re-arms it).
+ *   skyrl_adv_norm_apply  out f32[n] from the (reduced) sums; out may equal advantages.   */
+size_t skyrl_adv_norm_workspace_bytes(void);
+int skyrl_adv_norm_stats(const float* advantages, const void* response_mask, int mask_dtype, int64_t n,
+                         double* sums_out, void* workspace, void* stream);
+int skyrl_adv_norm_apply(const float* advantages, int64_t n, const double* sums, float* out, void* stream);
 
 /* ---- a5: GAE + masked whitening ----------------------------------------
  * Replaces compute_gae_advantage_return (ppo_utils.py:1101-1129) and

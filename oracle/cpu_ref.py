@@ -75,6 +75,17 @@ def grpo_advantage(rewards: torch.Tensor, mask: torch.Tensor, index: Sequence, e
     return out.unsqueeze(-1) * mask
 
 
+def normalize_advantages(adv: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """utils/ppo_utils.py:127-145 (advantage_batch_normalize, trainer.py:275-276): the mean is
+    over EVERY element (unmasked), the squared deviations are masked and divided by the mask
+    sum, rstd = clamp(., 1e-8).rsqrt(); the result is not re-masked."""
+    num = mask.sum()
+    mean = adv.mean()
+    ss = ((adv - mean).pow(2) * mask).sum()
+    rstd = (ss / num).clamp(min=1e-8).rsqrt()
+    return (adv - mean) * rstd
+
+
 # --------------------------------------------------------------------------- a5 GAE
 def masked_whiten(values: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     """utils/ppo_utils.py:148-172 (unbiased masked variance)"""

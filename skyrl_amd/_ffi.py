@@ -101,6 +101,9 @@ SIGNATURES = {
     "skyrl_comm_broadcast": (_INT, [_P, _P, _I64, _INT, _I32, _P, _P]),
     "skyrl_tune": (_INT, [ctypes.c_char_p, _INT]),
     "skyrl_grpo_advantage": (_INT, [_P, _P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
+    "skyrl_adv_norm_workspace_bytes": (_SZ, []),
+    "skyrl_adv_norm_stats": (_INT, [_P, _P, _INT, _I64, _P, _P, _P]),
+    "skyrl_adv_norm_apply": (_INT, [_P, _I64, _P, _P, _P]),
     "skyrl_gae_workspace_bytes": (_SZ, [_I32]),
     "skyrl_gae_advantage_return": (_INT, [_P, _P, _P, _INT, _I32, _I32, _F, _F, _P, _P, _P, _P, _P]),
     "skyrl_approx_kl": (_INT, [_P, _P, _P, _INT, _I64, _I32, _P, _P]),

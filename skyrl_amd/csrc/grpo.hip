@@ -10,7 +10,7 @@
 // so every slice sees bit-identical scores. Group stats in fp64 (torch.std on
 // CPU accumulates in double), the normalisation itself in fp32 as the
 // reference does.
-#include "common.h"
+#include "arrive.h"
 
 namespace skyrl {
 namespace {
@@ -295,10 +295,154 @@ __global__ __launch_bounds__(kMaxFastG * kWave) void grpo_adv_sliced_kernel(
     }
 }
 
+// ---- advantage_batch_normalize (ppo_utils.py:127-145, called at trainer.py:275-276) -----------
+// mean over EVERY element (unmasked), masked sum of squared deviations / mask sum, rstd =
+// rsqrt(clamp(., 1e-8)), out = (adv - mean) * rstd (not re-masked). Two launches so that a DP
+// caller can all-reduce the five fp64 sums in between (one all-reduce of scalars):
+//   stats: per block fp64 (sum a, sum m, sum a m, sum a^2 m) over a contiguous range, the last
+//          arriving block folds the block records in block order (deterministic) and appends
+//          the element count; sum (a - mu)^2 m = sum a^2 m - 2 mu sum a m + mu^2 sum m in fp64
+//   apply: mean / rstd from the sums (every block, scalar loads), one streaming pass.
+constexpr int kNormThreads = 256;
+constexpr int kNormMaxBlocks = 512;
+
+template <int MDT>
+__global__ __launch_bounds__(kNormThreads) void adv_norm_stats_kernel(const float* __restrict__ adv,
+                                                                     const void* __restrict__ mask, int64_t n,
+                                                                     int64_t per_block, bool vec4,
+                                                                     double* __restrict__ parts,
+                                                                     unsigned* __restrict__ counter,
+                                                                     double* __restrict__ sums_out) {
+    __shared__ double s_red[(kNormThreads / kWave) * 4];
+    __shared__ int s_last;
+    const int64_t b0 = (int64_t)blockIdx.x * per_block;
+    const int64_t b1 = min(n, b0 + per_block);
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    auto add = [&](float a, float m) {
+        const double ad = a, md = m;
+        v[0] += ad;
+        v[1] += md;
+        v[2] += ad * md;
+        v[3] += ad * ad * md;
+    };
+    if (vec4) {  // b0, b1 multiples of 4 (per_block is), n % 4 == 0
+        for (int64_t i = b0 + 4 * (int64_t)threadIdx.x; i < b1; i += 4 * kNormThreads) {
+            const float4 a = *reinterpret_cast<const float4*>(adv + i);
+            float m[4];
+            mask4_to_float<MDT>(load_mask4_raw<MDT>(mask, i), m);
+            add(a.x, m[0]);
+            add(a.y, m[1]);
+            add(a.z, m[2]);
+            add(a.w, m[3]);
+        }
+    } else {
+        for (int64_t i = b0 + threadIdx.x; i < b1; i += kNormThreads) add(adv[i], load_mask(mask, MDT, i));
+    }
+    block_sum_d<kNormThreads / kWave, 4>(v, s_red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st_wt(parts + (int64_t)blockIdx.x * 4 + k, v[k]);
+    }
+    if (!arrive_last(counter, gridDim.x, &s_last)) return;
+    if (threadIdx.x < kWave) {  // wave 0: lane l folds blocks l, l+64, ... in order, then a fixed tree
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = threadIdx.x; j < (int)gridDim.x; j += kWave) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) t[k] += __hip_atomic_load(parts + (int64_t)j * 4 + k, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = wave_sum_dpp(t[k]);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sums_out[k] = t[k];
+            sums_out[4] = (double)n;
+            rearm(counter);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kNormThreads) void adv_norm_apply_kernel(const float* __restrict__ adv, int64_t n,
+                                                                      const double* __restrict__ sums, bool vec4,
+                                                                      float* __restrict__ out) {
+    // torch: mean = adv.mean() (f32), ss = ((adv - mean)^2 * m).sum(), rstd = (ss / m.sum()).clamp(1e-8).rsqrt()
+    const double cnt = sums[4];
+    const float mean_f = (float)(sums[0] / cnt);
+    const double mu = (double)mean_f;
+    const double ss = sums[3] - 2.0 * mu * sums[2] + mu * mu * sums[1];
+    double var = ss / sums[1];      // mask sum 0: nan (0/0) or inf, as the reference's
+    if (var < 1e-8) var = 1e-8;     // clamp(min=1e-8); a NaN stays NaN (torch.clamp propagates it)
+    const float rstd = (float)(1.0 / sqrt(var));
+    const int64_t stride = (int64_t)gridDim.x * kNormThreads;
+    if (vec4) {
+        const int64_t n4 = n >> 2;
+        for (int64_t i = (int64_t)blockIdx.x * kNormThreads + threadIdx.x; i < n4; i += stride) {
+            float4 a = reinterpret_cast<const float4*>(adv)[i];
+            a.x = (a.x - mean_f) * rstd;
+            a.y = (a.y - mean_f) * rstd;
+            a.z = (a.z - mean_f) * rstd;
+            a.w = (a.w - mean_f) * rstd;
+            reinterpret_cast<float4*>(out)[i] = a;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNormThreads + threadIdx.x; i < n; i += stride)
+            out[i] = (adv[i] - mean_f) * rstd;
+    }
+}
+
 }  // namespace
 int g_grpo_slices = 4;  // skyrl_tune("grpo_slices", 1/2/4): column slices per group (contiguous form)
 
 }  // namespace skyrl
+
+extern "C" size_t skyrl_adv_norm_workspace_bytes(void) {
+    using namespace skyrl;
+    return 256 + (size_t)kNormMaxBlocks * 4 * sizeof(double);
+}
+
+extern "C" int skyrl_adv_norm_stats(const float* advantages, const void* response_mask, int mask_dtype, int64_t n,
+                                    double* sums_out, void* workspace, void* stream) {
+    using namespace skyrl;
+    SKYRL_REQUIRE(n >= 0, "adv_norm: negative size");
+    SKYRL_REQUIRE(advantages && response_mask && sums_out && workspace, "adv_norm: null pointer");
+    SKYRL_REQUIRE(mask_dtype == SKYRL_F32 || mask_dtype == SKYRL_I64 || mask_dtype == SKYRL_I32 ||
+                      mask_dtype == SKYRL_U8,
+                  "adv_norm: unsupported mask dtype");
+    SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "adv_norm: workspace must be 16-B aligned");
+    const size_t mbytes = mask_dtype == SKYRL_I64 ? 8 : mask_dtype == SKYRL_U8 ? 1 : 4;
+    const bool vec4 = (n % 4) == 0 && (reinterpret_cast<uintptr_t>(advantages) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(response_mask) % (4 * mbytes < 16 ? 4 * mbytes : 16)) == 0;
+    // blocks of >= 8 float4 per thread, at most kNormMaxBlocks; a multiple of 4 elements each
+    int64_t per = (n + kNormMaxBlocks - 1) / kNormMaxBlocks;
+    const int64_t minper = (int64_t)kNormThreads * 32;
+    per = per < minper ? minper : per;
+    per = (per + 3) / 4 * 4;
+    const int blocks = n == 0 ? 1 : (int)((n + per - 1) / per);
+    unsigned* counter = reinterpret_cast<unsigned*>(workspace);
+    double* parts = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + 256);
+    auto k = mask_dtype == SKYRL_I64   ? adv_norm_stats_kernel<SKYRL_I64>
+             : mask_dtype == SKYRL_F32 ? adv_norm_stats_kernel<SKYRL_F32>
+             : mask_dtype == SKYRL_I32 ? adv_norm_stats_kernel<SKYRL_I32>
+                                       : adv_norm_stats_kernel<SKYRL_U8>;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kNormThreads), 0, as_stream(stream), advantages, response_mask, n, per,
+                       vec4, parts, counter, sums_out);
+    return check_launch("adv_norm_stats_kernel");
+}
+
+extern "C" int skyrl_adv_norm_apply(const float* advantages, int64_t n, const double* sums, float* out, void* stream) {
+    using namespace skyrl;
+    SKYRL_REQUIRE(n >= 0, "adv_norm: negative size");
+    if (n == 0) return SKYRL_OK;
+    SKYRL_REQUIRE(advantages && sums && out, "adv_norm: null pointer");
+    const bool vec4 = (n % 4) == 0 && (reinterpret_cast<uintptr_t>(advantages) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(out) % 16) == 0;
+    const int64_t work = vec4 ? n / 4 : n;
+    int64_t blocks = (work + kNormThreads - 1) / kNormThreads;
+    blocks = blocks > 2048 ? 2048 : blocks;
+    hipLaunchKernelGGL(adv_norm_apply_kernel, dim3((unsigned)blocks), dim3(kNormThreads), 0, as_stream(stream),
+                       advantages, n, sums, vec4, out);
+    return check_launch("adv_norm_apply_kernel");
+}
 
 extern "C" int skyrl_grpo_advantage(const float* rewards, const float* scores_in, const void* response_mask,
                                     int mask_dtype,

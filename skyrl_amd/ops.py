@@ -164,6 +164,32 @@ def grpo_advantage(
     return out
 
 
+def normalize_advantages(advantages: torch.Tensor, response_mask: torch.Tensor, group=None) -> torch.Tensor:
+    """advantage_batch_normalize (ppo_utils.py:127-145, trainer.py:275-276): (adv - mean) * rstd
+    with the unmasked mean over every element and rstd = rsqrt(clamp(sum((adv - mean)^2 * mask) /
+    sum(mask), 1e-8)), returned as a new tensor (the reference does not re-mask). Two launches:
+    the five fp64 sums (sum a, sum m, sum a m, sum a^2 m, count), then the apply pass. With a
+    data-parallel `group` (each rank holding its rows of one global batch, as the reference
+    normalizes the whole batch on the driver) the sums are SUM-all-reduced between them: one
+    collective of 5 fp64 scalars, no host sync."""
+    dev = _require_gpu(advantages, response_mask)
+    adv = _f32c(advantages.detach(), "advantages")
+    mask = response_mask.contiguous()
+    if mask.dtype not in _MASK_DTYPES:
+        raise TypeError(f"unsupported response_mask dtype {mask.dtype}")
+    if mask.shape != adv.shape:
+        raise ValueError(f"advantages {tuple(adv.shape)} and response_mask {tuple(mask.shape)} must match")
+    sums = torch.empty(5, dtype=torch.float64, device=dev)
+    ws = WORKSPACES.get(dev, "adv_norm", _ffi.query("skyrl_adv_norm_workspace_bytes"))
+    _ffi.call("skyrl_adv_norm_stats", _ptr(adv), _ptr(mask), _MASK_DTYPES[mask.dtype], adv.numel(), _ptr(sums),
+              _ptr(ws), _stream(dev))
+    if group is not None and torch.distributed.get_world_size(group) > 1:
+        torch.distributed.all_reduce(sums, group=group)
+    out = torch.empty_like(adv)
+    _ffi.call("skyrl_adv_norm_apply", _ptr(adv), adv.numel(), _ptr(sums), _ptr(out), _stream(dev))
+    return out
+
+
 # ---------------------------------------------------------------------------- a5 GAE
 def gae_advantage_return(
     token_level_rewards: torch.Tensor,

@@ -225,14 +225,12 @@ def masked_whiten(values, mask, shift_mean=True):
 
 
 @torch.no_grad()
-def normalize_advantages_dict(data):
-    """ppo_utils.py:127-145 (advantage_batch_normalize): note the unmasked mean."""
-    adv = data["advantages"]
-    m = data["response_mask"]
-    mean = adv.mean()
-    var = ((adv - mean).pow(2) * m).sum()
-    rstd = (var / m.sum()).clamp(min=1e-8).rsqrt()
-    data["advantages"] = (adv - mean) * rstd
+def normalize_advantages_dict(data, group=None):
+    """ppo_utils.py:127-145 (advantage_batch_normalize) on the HIP kernels (ops.normalize_advantages):
+    the unmasked mean, the masked squared deviations; a new advantages tensor (returns keep the
+    old one, as in the reference). `group`: the data-parallel group whose ranks hold the rows of
+    one global batch (the sums are all-reduced once)."""
+    data["advantages"] = ops.normalize_advantages(data["advantages"], data["response_mask"], group=group)
     return data
 
 

@@ -278,6 +278,8 @@ class GRPOTrainer:
             data["returns"] = data["advantages"]  # compute_grpo_outcome_advantage returns (adv, adv)
         else:
             data = trainer_utils.compute_advantages_and_returns(data, alg)
+            if alg.advantage_batch_normalize:  # trainer.py:275-276 / fully_async_trainer.py:514-515
+                data = ppo_utils.normalize_advantages_dict(data, group=self._dp_group_if_dist())
         self._mark("advantages")
         metrics.update(data.metadata.get("metrics", {}))
         m = data["loss_mask"]
@@ -331,15 +333,23 @@ class GRPOTrainer:
         return comm.all_reduce_metrics(trainer_utils.reduce_metrics(acc), group=self.dp_group,
                                        device=next(self.critic.parameters()).device)
 
+    def _dp_group_if_dist(self):
+        """The data-parallel group when torch.distributed is up (the ranks' rows form one batch)."""
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            return self.dp_group if self.dp_group is not None else torch.distributed.group.WORLD
+        return None
+
     def _plan_grpo_ok(self, data, step_wise: bool) -> bool:
         """GRPO can run inside the policy step's plan launch: the built-in GRPO estimator (not a
-        plugin registered under its name), no critic, the fused policy pass, pack's reward row sums
-        (absent once a reward KL penalty changed the rewards), contiguous groups of G rows that the
-        mini-batches do not cut (no DP pad rows), and every row inside a trained mini-batch (the
-        reference estimates the dropped tail rows too)."""
+        plugin registered under its name), no critic, no advantage_batch_normalize (whose batch
+        statistics need every advantage before the first micro-batch), the fused policy pass,
+        pack's reward row sums (absent once a reward KL penalty changed the rewards), contiguous
+        groups of G rows that the mini-batches do not cut (no DP pad rows), and every row inside a
+        trained mini-batch (the reference estimates the dropped tail rows too)."""
         alg, G = self.cfg.algorithm, self.cfg.n_samples_per_prompt
         n = len(data["rewards"])
         return (not step_wise and self.critic is None and alg.advantage_estimator == "grpo"
+                and not alg.advantage_batch_normalize
                 and ppo_utils.AdvantageEstimatorRegistry.get("grpo") is ppo_utils.compute_grpo_outcome_advantage
                 and data.get("reward_row_sum") is not None and data.metadata.get("pad_size", 0) == 0
                 and 1 <= G <= 64 and n % (self.cfg.policy_mini_batch_size * G) == 0 and self._fused_pass_ok())
@@ -452,7 +462,10 @@ class GRPOTrainer:
                 hidden = model.base_model(input_ids=seq, attention_mask=att,
                                           position_ids=_positions(att)).last_hidden_state
                 w = model.get_output_embeddings().weight
-            return (hidden.float().sum() + w.float().sum()) * 0.0
+            # one element of each, native dtype (no fp32 copy of the [V, H] weight, no overflow to
+            # inf * 0): the slice's backward still reaches every parameter with a dense zero
+            # gradient, so every grad hook fires
+            return (hidden[..., :1].sum() + w.view(-1)[:1].sum()).float() * 0.0
         with torch.autocast("cuda", dtype=torch.bfloat16):
             base = model.base_model
             if self.cfg.use_sample_packing:

@@ -197,3 +197,30 @@ def test_fused_policy_pass_matches_chunked_lmhead_path():
         assert abs(mf[k] - mc[k]) <= 1e-4 * max(1.0, abs(mc[k])), (k, mf[k], mc[k])
     rel = float((gf - gc).norm() / gc.norm())
     assert rel < 2e-2, rel
+
+
+def test_empty_last_micro_batch_on_one_rank():
+    """scripts/rehearse_empty_micro.py under torch.distributed.run
+    (2 ranks, gloo, one GPU) runs GRPOTrainer._fused_policy_pass directly on a mini-batch whose
+    last micro-batch has no response token on rank 1 only (the generator check rejects such
+    output, so it is made empty after packing). Its loss is 0, both ranks fire the same
+    bucket reduce-scatter sequence from the backward hooks, and the weights stay bit-identical."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "scripts", "rehearse_empty_micro.py")]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, p.stderr[-3000:]
+    res = json.loads(lines[-1])
+    assert p.returncode == 0 and res["ok"], json.dumps(res) + p.stderr[-2000:]
+    assert res["launch_sequences_equal"] and res["empty_micro_loss"] == 0.0
+    assert res["weights_identical_across_ranks"]

@@ -69,6 +69,14 @@ def test_grpo_golden(golden, name):
         close(out, d[f"adv_norm{nbs}"], atol=1e-6, rtol=1e-6)
 
 
+@pytest.mark.parametrize("case", ["grpo", "dense", "const"])
+def test_advnorm_golden(golden, case):
+    """advantage_batch_normalize: normalize_advantages_dict (ppo_utils.py:127-145)."""
+    d = golden("advnorm")
+    out = cpu_ref.normalize_advantages(d[f"{case}_in"], d[f"{case}_mask"])
+    close(out, d[f"{case}_out"], atol=1e-6, rtol=1e-6)
+
+
 def test_gae_golden(golden):
     d = golden("gae")
     for tag, g, l in (("g1_l1", 1.0, 1.0), ("g099_l095", 0.99, 0.95), ("g05_l1", 0.5, 1.0)):

@@ -181,6 +181,35 @@ def gen_grpo(pu):
         save(name, rewards=rew, response_mask=mask, uids=np.array(uids), **out)
 
 
+def gen_advnorm(pu):
+    """advantage_batch_normalize (trainer.py:275-276 -> normalize_advantages_dict,
+    ppo_utils.py:127-145): the unmasked mean, the masked sum of squared deviations."""
+    g = torch.Generator().manual_seed(99)
+    out = {}
+    # GRPO advantages of a synthetic batch (16 prompts x 8, int64 response mask)
+    N, R = 128, 96
+    lens = torch.randint(1, R + 1, (N,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64)
+    rew = torch.zeros(N, R)
+    rew[torch.arange(N), lens - 1] = (torch.rand(N, generator=g) < 0.3).float()
+    adv, _ = pu.compute_grpo_outcome_advantage(token_level_rewards=rew, response_mask=mask,
+                                               index=np.array([str(i // 8) for i in range(N)]))
+    d = {"advantages": adv.clone(), "response_mask": mask}
+    out["grpo_in"], out["grpo_mask"], out["grpo_out"] = adv, mask, pu.normalize_advantages_dict(d)["advantages"]
+    # dense float advantages with an offset (mean far from 0), f32 mask, odd width
+    N, R = 37, 131
+    a = torch.randn(N, R, generator=g) * 0.7 + 2.5
+    m = (torch.rand(N, R, generator=g) < 0.6).float()
+    d = {"advantages": a.clone(), "response_mask": m}
+    out["dense_in"], out["dense_mask"], out["dense_out"] = a, m, pu.normalize_advantages_dict(d)["advantages"]
+    # constant advantages: zero variance, the clamp at 1e-8 decides rstd
+    a = torch.full((4, 10), 0.25)
+    m = torch.ones(4, 10, dtype=torch.int64)
+    d = {"advantages": a.clone(), "response_mask": m}
+    out["const_in"], out["const_mask"], out["const_out"] = a, m, pu.normalize_advantages_dict(d)["advantages"]
+    save("advnorm", **out)
+
+
 def gen_gae(pu):
     g = torch.Generator().manual_seed(7)
     N, R = 6, 40
@@ -585,6 +614,7 @@ def main():
     assert not tu.FLASH_ATTN_CROSS_ENTROPY_LOSS_AVAILABLE
     jobs = {
         "grpo": lambda: gen_grpo(pu),
+        "advnorm": lambda: gen_advnorm(pu),
         "gae": lambda: gen_gae(pu),
         "kl": lambda: gen_kl(pu),
         "ppo": lambda: gen_ppo(pu, cfgmod),
