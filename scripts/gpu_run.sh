@@ -65,7 +65,7 @@ for S in "$@"; do
     pmc_emu8|pmc)
       EXTRA=""
       [ $name = pmc_emu8 ] && EXTRA="--emulate-world 8"
-      timeout -s KILL 400 rocprofv3 --pmc ${arg//,/ } --kernel-trace --output-format csv -d $O -o run -- python3 bench.py \
+      timeout -s KILL 400 rocprofv3 --pmc ${arg//,/ } --kernel-trace --kernel-include-regex "${PMC_REGEX:-policy_train|sample_kernel|logprob}" --output-format csv -d $O -o run -- python3 bench.py \
         --steps 1 --warmup 1 $EXTRA $NOLEGS > $O.log 2>&1
       rc=$?; step_rc $name $rc $O.log ;;
     py)
