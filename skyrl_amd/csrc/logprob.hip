@@ -228,6 +228,8 @@ extern int g_sampler_split_gran;
 extern int g_sampler_split_nt;
 extern int g_sampler_topk_fast;
 extern int g_sampler_topp_fast;
+extern int g_sampler_wide_rows;
+extern int g_sampler_wide_wgs;
 extern int g_probe_topp;
 extern int g_attn_pf;
 int lmhead_tune(int value);
@@ -324,6 +326,16 @@ extern "C" int skyrl_tune(const char* key, int value) {
     if (k == "sampler_topk_fast") {
         SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_topk_fast must be 0 or 1");
         g_sampler_topk_fast = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_wide_rows") {
+        SKYRL_REQUIRE(value >= 0 && value <= 1024, "skyrl_tune: sampler_wide_rows must be in [0, 1024]");
+        g_sampler_wide_rows = value;
+        return SKYRL_OK;
+    }
+    if (k == "sampler_wide_wgs") {
+        SKYRL_REQUIRE(value >= 1 && value <= 8192, "skyrl_tune: sampler_wide_wgs must be in [1, 8192]");
+        g_sampler_wide_wgs = value;
         return SKYRL_OK;
     }
     if (k == "topp_probe") {

@@ -5,7 +5,10 @@ against oracle/sampler_ref.c (tokens bit-exact, logprobs 1e-4) and against the s
 by one workgroup per row (tokens identical: every split decides with exact scores, the lowest
 index on ties). The split count follows skyrl_tune("sampler_split_wgs") and the row threshold
 "sampler_split_rows", the split workgroup size "sampler_split_nt"; every setting must give the same
-tokens (T = 1 runs the multiplicative bound in row mode and the additive one in split mode)."""
+tokens (T = 1 runs the multiplicative bound in row mode and the additive one in split mode).
+Since r06 unfiltered bf16 batches below "sampler_wide_rows" (256) take the wide split kernel
+(sample_wide_kernel: every load of a workgroup in flight at once, "sampler_wide_wgs" workgroups
+per launch); "sampler_wide_rows" 0 selects the streaming split kernel, and both must agree."""
 
 import pytest
 import torch
@@ -17,7 +20,9 @@ pytestmark = pytest.mark.gpu
 V = 151936
 
 
-def _knobs(rows=256, wgs=1024, gran=8192, nt=256):
+def _knobs(rows=256, wgs=1024, gran=8192, nt=256, wide=256, wide_wgs=512):
+    ops._ffi.call("skyrl_tune", b"sampler_wide_rows", wide)
+    ops._ffi.call("skyrl_tune", b"sampler_wide_wgs", wide_wgs)
     ops._ffi.call("skyrl_tune", b"sampler_split_nt", nt)
     ops._ffi.call("skyrl_tune", b"sampler_split_rows", rows)
     ops._ffi.call("skyrl_tune", b"sampler_split_wgs", wgs)
@@ -30,13 +35,16 @@ def _restore():
     _knobs()
 
 
-@pytest.mark.parametrize("n", [64, 128])
+@pytest.mark.parametrize("n", [1, 13, 64, 128, 255])
 @pytest.mark.parametrize("temp", [1.0, 0.7, 0.0])
-@pytest.mark.parametrize("nt", [256, 512])
-def test_split_rows_match_oracle(dev, n, temp, nt):
+@pytest.mark.parametrize("kernel", ["wide", "split256", "split512"])
+def test_split_rows_match_oracle(dev, n, temp, kernel):
     from oracle import sampler as osamp
 
-    _knobs(nt=nt)
+    if kernel == "wide":
+        _knobs()
+    else:
+        _knobs(nt=int(kernel[5:]), wide=0)
 
     g = torch.Generator().manual_seed(n * 10 + int(temp * 10))
     x = (torch.randn(n, V, generator=g) * 3).to(torch.bfloat16)
@@ -56,11 +64,13 @@ def test_split_settings_give_identical_tokens(dev, n):
     x = big[:, 1]  # row stride 3 V
     ids = torch.arange(n, dtype=torch.int64, device=dev) + 1000
     outs = {}
-    for rows, wgs, gran, nt in ((1, 2048, 8192, 256), (256, 2048, 8192, 256), (1024, 2048, 8192, 256),
-                                (1024, 512, 8192, 256), (1024, 8192, 8192, 256), (1024, 1024, 2048, 256),
-                                (1024, 8192, 2048, 256), (1024, 960, 4096, 256), (1024, 256, 16384, 512),
-                                (1024, 2048, 2048, 512)):
-        _knobs(rows, wgs, gran, nt)
+    for rows, wgs, gran, nt, wide, wwgs in (
+            (1, 2048, 8192, 256, 0, 512), (256, 2048, 8192, 256, 0, 512), (1024, 2048, 8192, 256, 0, 512),
+            (1024, 512, 8192, 256, 0, 512), (1024, 8192, 8192, 256, 0, 512), (1024, 1024, 2048, 256, 0, 512),
+            (1024, 8192, 2048, 256, 0, 512), (1024, 960, 4096, 256, 0, 512), (1024, 256, 16384, 512, 0, 512),
+            (1024, 2048, 2048, 512, 0, 512), (256, 1024, 8192, 256, 1024, 512), (256, 1024, 8192, 256, 1024, 64),
+            (256, 1024, 8192, 256, 1024, 2048), (256, 1024, 8192, 256, 1024, 8192)):
+        _knobs(rows, wgs, gran, nt, wide, wwgs)
         for temp in (1.0, 0.0, 1.3):
             tok, lp = ops.sample(x, temperature=temp, seed=2, seq_ids=ids, step=5)
             outs.setdefault(temp, []).append((tok.clone(), lp.clone()))
@@ -76,10 +86,11 @@ def test_split_workspace_reused_across_sizes_and_settings(dev):
     g = torch.Generator(device=dev).manual_seed(5)
     x = torch.empty((300, V), dtype=torch.bfloat16, device=dev).normal_(0, 3, generator=g)
     ids = torch.arange(300, dtype=torch.int64, device=dev)
-    seq = [(64, 2048), (200, 2048), (7, 512), (300, 2048), (128, 8192), (64, 1024), (255, 2048)]
-    for k, (n, wgs) in enumerate(seq):
-        _knobs(1024, wgs)
+    seq = [(64, 2048, 0), (200, 2048, 256), (7, 512, 0), (300, 2048, 1024), (128, 8192, 256), (64, 1024, 0),
+           (255, 2048, 256), (33, 2048, 256), (300, 512, 0)]
+    for k, (n, wgs, wide) in enumerate(seq):
+        _knobs(1024, wgs, wide=wide, wide_wgs=wgs)
         tok, _ = ops.sample(x[:n], temperature=1.0, seed=3, seq_ids=ids[:n], step=k)
-        _knobs(1, 2048)  # one workgroup per row: no counters
+        _knobs(1, 2048, wide=0)  # one workgroup per row: no counters
         ref, _ = ops.sample(x[:n], temperature=1.0, seed=3, seq_ids=ids[:n], step=k)
         assert torch.equal(tok, ref), (n, wgs)
