@@ -704,13 +704,11 @@ def advantage_loss_leg(dev, N, R, reps=20, variants=False):
         out["variants"] = {"total_without_row_sums_us": timed((grpo, lambda s: fwd(s, False), bwd)),
                            "grpo_adv_loss_no_bwd_us": timed((grpo, fwd))}
         for sl in (1, 2, 4):
-            _ffi.call("skyrl_tune", b"grpo_slices", sl)
-            out["variants"][f"grpo_slices{sl}_us"] = timed((grpo,))
-        _ffi.call("skyrl_tune", b"grpo_slices", 4)
+            with _ffi.variant(grpo_slices=sl):
+                out["variants"][f"grpo_slices{sl}_us"] = timed((grpo,))
         for u in (1, 2, 4):
-            _ffi.call("skyrl_tune", b"loss_units", u)
-            out["variants"][f"loss_units{u}_us"] = timed((fwd,))
-        _ffi.call("skyrl_tune", b"loss_units", 0)
+            with _ffi.variant(loss_units=u):
+                out["variants"][f"loss_units{u}_us"] = timed((fwd,))
     nbytes = 56 * N * R
     gbs = nbytes / (out["total_us"] * 1e-6) / 1e9
     out.update({"rows": N, "R": R, "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
@@ -816,7 +814,7 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
     one-pass kernel; without it the top_p kernel, which decides most rows in one pass and hands
     the rest to a second launch that re-reads each of them in 8 pieces; rows either kernel cannot
     take run the pre-pass + MODE 2 code in the same workgroup), against the two-kernel path
-    (skyrl_tune sampler_topk_fast / sampler_topp_fast 0). "one_pass" is the fast path's whole call
+    (skyrl_variant sampler_topk_fast / sampler_topp_fast 0). "one_pass" is the fast path's whole call
     (for top_p both launches). Algorithmic bytes = one read of the logits + 16 B per row (the
     left rows' re-read, ~6 % at top_p 0.95, is meant to hit the Infinity Cache)."""
     from skyrl_amd import ops
@@ -832,9 +830,10 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
                               ("top_p0.95", -1, 0.95, 1.0, 0.0), ("top_p0.95_T0.6", -1, 0.95, 0.6, 0.0),
                               ("min_p0.05", -1, 1.0, 1.0, 0.05), ("min_p0.05_T0.6", -1, 1.0, 0.6, 0.05)):
         res = {}
-        knob = b"sampler_topk_fast" if k > 0 else b"sampler_topp_fast"  # the one-pass / two-pass kernels
+        knob = "sampler_topk_fast" if k > 0 else "sampler_topp_fast"  # the one-pass / two-pass kernels
         for fast in (1, 0):
-            ops._ffi.call("skyrl_tune", knob, fast)
+            vscope = ops.variant(**{knob: fast})
+            vscope.__enter__()
             run = lambda: ops.sample(x, temperature=t, top_k=k, top_p=p, min_p=mp, seed=3, seq_ids=ids,  # noqa: E731
                                      step=1, tokens_out=tok, logp_out=lp)
             run()
@@ -847,9 +846,9 @@ def sampler_filtered_leg(dev, nseq, V, reps=20):
             b.synchronize()
             us = a.elapsed_time(b) * 1e3 / reps
             gbs = nbytes / (us * 1e-6) / 1e9
+            vscope.__exit__(None, None, None)
             res["one_pass" if fast else "two_kernel"] = {"avg_launch_us": round(us, 2), "achieved_GBps": round(gbs, 1),
                                                          "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        ops._ffi.call("skyrl_tune", knob, 1)
         out[name] = res
     return out
 

@@ -48,28 +48,50 @@ const char* skyrl_last_error(void);
  * skyrl_comm_* RCCL collectives; 8: the step form of the fused policy pass,
  * skyrl_policy_train_plan / _micro_fwd / _fold; 9: per-parameter AdamW,
  * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy, skyrl_policy_train_plan_grpo;
- * 10: skyrl_adv_norm_stats / _apply). */
+ * 10: skyrl_adv_norm_stats / _apply; 11: skyrl_tune and skyrl_debug_occupy removed, per-call
+ * kernel variants through skyrl_variant and the *_ex entry points). */
 int skyrl_abi_version(void);
-/* Process-wide kernel variant selection for A/B measurement (defaults are the tuned
- * ones): "logprob_unroll" in {4, 8} (16-B loads in flight per lane), "logprob_nt"
- * {0, 1} (non-temporal streaming loads of the logits), "train_resident" {0, 1} (fused
- * training pass keeps the vocab row in registers vs re-reading it), "train_ntstore"
- * {0, 1} (non-temporal dlogits stores), "train_resident_nt" {768, 1024} (threads per
- * register-resident row at Qwen2.5's vocabulary), "grpo_slices" {1, 2, 4} (column slices
- * per group of the contiguous-group GRPO kernel), "loss_units" {0 auto, 1, 2, 4} (row chunks
- * per block of the fused PPO loss), "sampler_row" {0, 1} (row-mode sampler without / with
- * the progress-based wave priority), "lmhead_pipe" {-1 default, 0..14} (K pipeline of the
- * lm_head MFMA GEMM), "lmhead_group" {0 all, n} (M tiles per group of its tile order),
- * "attn_pf" {0 default (4), 4, 6, 8} (K/V cache blocks in flight per D = 128 decode wave),
- * "train_split" {0, 1} (split-row fused training pass), "train_split_shape" {0 by
- * vocabulary, 1..5: pieces x threads per row 8x128, 4x256, 2x512, 5x256, 6x256}, "grpo_loss_rpb" {1, 2} (row chunks per block of the GRPO+loss launch),
- * "loss_bwd_blocks" [1, 4096] (grid of skyrl_ppo_loss_finish / _bwd), "sampler_topk_fast"
- * {0, 1} (skyrl_sample with top_k <= 128: the filter pre-pass + MODE 2 kernels vs the one-pass
- * top_k kernel; identical tokens, logprobs to float rounding).
- * Every variant gives identical results except the split-row pass vs the resident one
- * (another fp32 summation order) and the timing probes "finish_mode" 2..4
- * (0 default, 1 = nb loaded first). Not thread-safe.                                    */
-int skyrl_tune(const char* key, int value);
+/* ---- kernel variants, per call ---------------------------------------------------------------
+ * Every entry point runs the tuned kernels. The *_ex forms (declared after each family) take a
+ * caller-owned skyrl_variant as their LAST argument and run another variant of the same
+ * computation for that call only: A/B measurement, and the tests that pin the alternatives
+ * against each other. NULL means the tuned defaults, and so does every field left at
+ * SKYRL_VARIANT_DEFAULT. The library keeps no mutable state between calls: a variant is read only
+ * while its _ex call runs (a bad field value fails that call with SKYRL_ERR_INVALID before any
+ * launch). Every variant gives identical results except the split-row fused training pass vs the
+ * resident one (another fp32 summation order) and the timing probes topp_probe 1..4 /
+ * 6 / 7 / 11 and finish_mode 2..4 (deliberately wrong values). */
+#define SKYRL_VARIANT_DEFAULT INT32_MIN
+typedef struct skyrl_variant {
+    int32_t logprob_unroll;      /* {4, 8}: 16-B loads in flight per lane (logprob fwd / bwd) */
+    int32_t logprob_nt;          /* {0, 1}: non-temporal streaming loads of the logits */
+    int32_t train_resident;      /* {0, 1}: the fused training pass keeps the row in registers */
+    int32_t train_resident_nt;   /* {768, 1024}: threads per register-resident row at V ~ 152K */
+    int32_t train_ntstore;       /* {0, 1}: non-temporal dlogits stores */
+    int32_t train_split;         /* {0, 1}: split-row fused training pass where it applies */
+    int32_t train_split_shape;   /* 0 by vocabulary, 1..5: pieces x threads 8x128, 4x256, 2x512, 5x256, 6x256 */
+    int32_t train_split_wait;    /* [0, 1e8] ticks a piece waits for a partner before recomputing it */
+    int32_t grpo_slices;         /* {1, 2, 4}: column slices per group (contiguous-group GRPO) */
+    int32_t loss_units;          /* {0 auto, 1, 2, 4}: row chunks per block of the fused PPO loss */
+    int32_t loss_bwd_blocks;     /* [1, 4096]: grid of skyrl_ppo_loss_finish / _bwd */
+    int32_t grpo_loss_rpb;       /* {1, 2}: row chunks per block of the GRPO + loss launch */
+    int32_t finish_mode;         /* [0, 4]: 0 block tree, 1 nb first; 2..4 timing probes */
+    int32_t sampler_row;         /* {0, 1}: row-mode sampler without / with progress priority */
+    int32_t sampler_split_rows;  /* [1, 1024]: rows split over workgroups below this */
+    int32_t sampler_split_wgs;   /* [64, 16384]: workgroups a split launch aims at */
+    int32_t sampler_split_nt;    /* {256, 512}: threads per split-mode workgroup */
+    int32_t sampler_split_gran;  /* multiple of 2048 in [2048, 65536]: split chunk granule (elements) */
+    int32_t sampler_topk_fast;   /* {0, 1}: top_k <= 128 through the one-pass kernel */
+    int32_t sampler_topp_fast;   /* {0, 1, 2}: top_p / min_p through the one-pass kernel (2: always) */
+    int32_t sampler_wide_rows;   /* [0, 1024]: unfiltered bf16 batches below this take the wide split kernel */
+    int32_t sampler_wide_wgs;    /* [1, 8192]: workgroups a wide launch aims at */
+    int32_t topp_probe;          /* {0 .. 7, 11}: top_p timing probes (0 = product) */
+    int32_t lmhead_pipe;         /* -1 default or 0..14: K pipeline of the lm_head MFMA GEMM */
+    int32_t lmhead_group;        /* [0, 4096): M tiles per group of its tile order (0 = all) */
+    int32_t attn_pf;             /* {0 default, 4, 6, 8}: K/V blocks in flight per D = 128 decode wave */
+} skyrl_variant;
+/* Fills every field with SKYRL_VARIANT_DEFAULT (a pure function of its argument). */
+void skyrl_variant_init(skyrl_variant* v);
 
 /* ---- a4: GRPO outcome advantage ----------------------------------------
  * Replaces compute_grpo_outcome_advantage (utils/ppo_utils.py:1132-1182) as
@@ -89,6 +111,12 @@ int skyrl_grpo_advantage(const float* rewards, const float* scores_in /* [N] or 
                          const int32_t* group_off, const int32_t* group_rows, int32_t num_groups,
                          int32_t N, int32_t R, float epsilon, int32_t norm_by_std,
                          float* advantages, float* scores_out /* [N] or NULL */, void* stream);
+int skyrl_grpo_advantage_ex(const float* rewards, const float* scores_in /* [N] or NULL */,
+                         const void* response_mask, int mask_dtype,
+                         const int32_t* group_off, const int32_t* group_rows, int32_t num_groups,
+                         int32_t N, int32_t R, float epsilon, int32_t norm_by_std,
+                         float* advantages, float* scores_out /* [N] or NULL */, void* stream,
+        const skyrl_variant* variant);
 
 /* ---- a4 (cont.): advantage_batch_normalize --------------------------------
  * Replaces normalize_advantages_dict (utils/ppo_utils.py:127-145) as applied after the
@@ -194,6 +222,14 @@ int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_probs, const
                        float* loss_out /* [1] */, float* metrics_out /* [SKYRL_M_COUNT] */,
                        float* grad_logp /* [n,R] */, float* grad_entropy /* [n,R] or NULL */,
                        int32_t flags, void* workspace, void* stream);
+int skyrl_ppo_loss_fwd_ex(const float* log_probs, const float* old_log_probs, const float* advantages,
+                       const float* loss_mask /* NULL = all ones */, const float* ref_log_probs,
+                       const float* entropy, const float* row_mask_sum /* [n] or NULL */,
+                       int32_t n, int32_t R, const skyrl_ppo_params* params,
+                       float* loss_out /* [1] */, float* metrics_out /* [SKYRL_M_COUNT] */,
+                       float* grad_logp /* [n,R] */, float* grad_entropy /* [n,R] or NULL */,
+                       int32_t flags, void* workspace, void* stream,
+        const skyrl_variant* variant);
 /* a4 + a7 for a batch that is one micro-batch: skyrl_grpo_advantage (contiguous groups of
  * G = n/num_groups rows; its contiguous-form conditions apply: G <= 16, R % 4 == 0, 16-B
  * aligned rewards/mask/advantages) followed by skyrl_ppo_loss_fwd on its advantages. ONE
@@ -219,10 +255,25 @@ int skyrl_grpo_ppo_loss_fwd(const float* rewards, const float* scores /* [n] or 
                             float* metrics_out /* [SKYRL_M_COUNT] */, float* grad_logp /* [n,R] */,
                             float* grad_entropy /* [n,R] or NULL */, int32_t flags, void* workspace,
                             void* stream);
+int skyrl_grpo_ppo_loss_fwd_ex(const float* rewards, const float* scores /* [n] or NULL */,
+                            const void* response_mask, int mask_dtype,
+                            int32_t num_groups, float epsilon, int32_t norm_by_std,
+                            const float* log_probs, const float* old_log_probs,
+                            const float* loss_mask /* NULL = all ones */, const float* ref_log_probs,
+                            const float* entropy, const float* row_mask_sum /* [n] or NULL */,
+                            int32_t n, int32_t R, const skyrl_ppo_params* params,
+                            float* advantages /* [n,R] */, float* loss_out /* [1] */,
+                            float* metrics_out /* [SKYRL_M_COUNT] */, float* grad_logp /* [n,R] */,
+                            float* grad_entropy /* [n,R] or NULL */, int32_t flags, void* workspace,
+                            void* stream,
+        const skyrl_variant* variant);
 /* Autograd backward of the loss: grad_logp (and grad_entropy, if given) *= grad_out[0] in
  * place; no memory is touched when grad_out[0] == 1 (loss.backward()).                    */
 int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, int64_t numel, float* grad_logp,
                        float* grad_entropy /* or NULL */, void* stream);
+int skyrl_ppo_loss_bwd_ex(const float* grad_out /* [1] device */, int64_t numel, float* grad_logp,
+                       float* grad_entropy /* or NULL */, void* stream,
+        const skyrl_variant* variant);
 /* The backward of a forward run with SKYRL_LOSS_DEFER_FOLD (same workspace, same stream):
  * folds its per-block records into loss_out and metrics_out (bit-identical to the in-launch
  * fold; stream-ordered, no polling) and, when grad_out is given and grad_out[0] != 1,
@@ -232,6 +283,10 @@ int skyrl_ppo_loss_bwd(const float* grad_out /* [1] device */, int64_t numel, fl
 int skyrl_ppo_loss_finish(const float* grad_out /* [1] device or NULL */, float* grad_logp,
                           float* grad_entropy /* or NULL */, int32_t n, int32_t R, const skyrl_ppo_params* params,
                           float* loss_out, float* metrics_out, void* workspace, void* stream);
+int skyrl_ppo_loss_finish_ex(const float* grad_out /* [1] device or NULL */, float* grad_logp,
+                          float* grad_entropy /* or NULL */, int32_t n, int32_t R, const skyrl_ppo_params* params,
+                          float* loss_out, float* metrics_out, void* workspace, void* stream,
+        const skyrl_variant* variant);
 
 /* ---- a8: clipped value loss ---------------------------------------------
  * Replaces ppo_critic_loss (ppo_utils.py:175-193): 0.5*mean_rows(masked_mean(
@@ -256,6 +311,11 @@ int skyrl_logprob_fwd(const void* logits, int dtype, int64_t stride_b, int64_t s
                       int32_t nb, int32_t nt, int32_t V, const int64_t* labels,
                       int64_t lstride_b, int64_t lstride_t, float temperature, float* logp_out,
                       float* entropy_out, float* lse_out, void* stream);
+int skyrl_logprob_fwd_ex(const void* logits, int dtype, int64_t stride_b, int64_t stride_t,
+                      int32_t nb, int32_t nt, int32_t V, const int64_t* labels,
+                      int64_t lstride_b, int64_t lstride_t, float temperature, float* logp_out,
+                      float* entropy_out, float* lse_out, void* stream,
+        const skyrl_variant* variant);
 /* d logits (same dtype, dense [nb,nt,V]) = (g_lp*(onehot-p) + g_ent*(-p*(logp_v+H)))/T.
  * grad_entropy may be NULL; entropy must be given if grad_entropy is.          */
 int skyrl_logprob_bwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t,
@@ -263,6 +323,12 @@ int skyrl_logprob_bwd(const void* logits, int dtype, int64_t stride_b, int64_t s
                       int64_t lstride_b, int64_t lstride_t, float temperature, const float* lse,
                       const float* entropy, const float* grad_logp, const float* grad_entropy,
                       void* grad_logits, void* stream);
+int skyrl_logprob_bwd_ex(const void* logits, int dtype, int64_t stride_b, int64_t stride_t,
+                      int32_t nb, int32_t nt, int32_t V, const int64_t* labels,
+                      int64_t lstride_b, int64_t lstride_t, float temperature, const float* lse,
+                      const float* entropy, const float* grad_logp, const float* grad_entropy,
+                      void* grad_logits, void* stream,
+        const skyrl_variant* variant);
 
 /* ---- §8(f)1: lm_head-fused logprob + entropy (logits never materialized) ----
  * Replaces the lm_head output -> logits.div_(T) -> logprobs_from_logits +
@@ -312,6 +378,9 @@ int skyrl_lmhead_chunk_bwd(const void* z, int64_t ldz, int32_t T, int32_t vc, in
  *                        skyrl_lmhead_sample_workspace_bytes(M, V), 16-B aligned.            */
 int skyrl_lmhead_gemm(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
                       int32_t N, int32_t K, void* out, int64_t ld_out, void* stream);
+int skyrl_lmhead_gemm_ex(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
+                      int32_t N, int32_t K, void* out, int64_t ld_out, void* stream,
+        const skyrl_variant* variant);
 size_t skyrl_lmhead_sample_workspace_bytes(int32_t M, int32_t V);
 /* Learner side (old / ref log-probs, no grad): logp/entropy/lse f32 [T] of log_softmax(bf16(h W^T) / T)
  * at labels (int64, token r at labels[r*label_stride]) with the same kernel's online-softmax
@@ -322,9 +391,17 @@ size_t skyrl_lmhead_logprob_workspace_bytes(int32_t T, int32_t V);
 int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t T,
                              int32_t V, int32_t K, const int64_t* labels, int64_t label_stride, float temperature,
                              float* logp_out, float* entropy_out, float* lse_out, void* workspace, void* stream);
+int skyrl_lmhead_logprob_fwd_ex(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t T,
+                             int32_t V, int32_t K, const int64_t* labels, int64_t label_stride, float temperature,
+                             float* logp_out, float* entropy_out, float* lse_out, void* workspace, void* stream,
+        const skyrl_variant* variant);
 int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
                         int32_t V, int32_t K, float temperature, uint64_t seed, const int64_t* seq_ids, int64_t step,
                         int32_t* tokens_out, float* logp_out, void* workspace, void* stream);
+int skyrl_lmhead_sample_ex(const void* hidden, int64_t ld_hidden, const void* weight, int64_t ld_weight, int32_t M,
+                        int32_t V, int32_t K, float temperature, uint64_t seed, const int64_t* seq_ids, int64_t step,
+                        int32_t* tokens_out, float* logp_out, void* workspace, void* stream,
+        const skyrl_variant* variant);
 
 /* ---- a2+a3+a6+a7 fused: the policy training pass ------------------------------
  * One call per micro-batch replaces logprob fwd + fused loss fwd + loss bwd +
@@ -347,6 +424,15 @@ int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t stride_b, int6
                            float* logp_out, float* entropy_out, void* grad_logits, int64_t gstride_b,
                            int64_t gstride_t, void* workspace,
                            void* stream);
+int skyrl_policy_train_fwd_ex(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t n,
+                           int32_t R, int32_t V, const int64_t* labels, int64_t lstride_b,
+                           int64_t lstride_t, float temperature, const float* old_log_probs,
+                           const float* advantages, const float* loss_mask, const float* ref_log_probs,
+                           const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                           float* logp_out, float* entropy_out, void* grad_logits, int64_t gstride_b,
+                           int64_t gstride_t, void* workspace,
+                           void* stream,
+        const skyrl_variant* variant);
 /* The same pass over a sample-packed batch (the learner's padding-free layout,
  * model_wrapper.py:272-330 with the lm_head of :308-363): ntok tokens with dense logits rows
  * (row q at logits + q*ld, bf16; V <= 155,648, or <= 114,688 when V % 8 != 0 or rows are not
@@ -363,6 +449,14 @@ int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int64_t ld, int
                                   const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
                                   float* logp_out, float* entropy_out, void* grad_logits, int64_t ld_grad,
                                   void* workspace, void* stream);
+int skyrl_policy_train_ragged_fwd_ex(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
+                                  const int64_t* labels, const int32_t* token_pos, int32_t n, int32_t R,
+                                  float temperature, const float* old_log_probs, const float* advantages,
+                                  const float* loss_mask, const float* ref_log_probs,
+                                  const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
+                                  float* logp_out, float* entropy_out, void* grad_logits, int64_t ld_grad,
+                                  void* workspace, void* stream,
+        const skyrl_variant* variant);
 /* Step form: one mini-batch of n_total rows in micro-batches of micro_rows (the last one may be
  * short), the loss folded once per mini-batch. The reference's micro-batch loop
  * (workers/worker.py:731-900) reads loss and metrics only after the mini-batch's backward
@@ -405,18 +499,22 @@ int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64_t ld, int3
                                  const float* advantages, const float* loss_mask, const float* ref_log_probs,
                                  const skyrl_ppo_params* params, float* logp_out, float* entropy_out,
                                  void* grad_logits, int64_t ld_grad, void* workspace, void* stream);
+int skyrl_policy_train_micro_fwd_ex(const void* logits, int dtype, int64_t ld, int32_t ntok, int32_t V,
+                                 const int64_t* labels, int64_t label_stride_b, int64_t label_stride_t,
+                                 const int32_t* token_pos, int32_t micro, int32_t n_total, int32_t R,
+                                 int32_t micro_rows, float temperature, const float* old_log_probs,
+                                 const float* advantages, const float* loss_mask, const float* ref_log_probs,
+                                 const skyrl_ppo_params* params, float* logp_out, float* entropy_out,
+                                 void* grad_logits, int64_t ld_grad, void* workspace, void* stream,
+        const skyrl_variant* variant);
 int skyrl_policy_train_fold(const float* loss_mask, int32_t n_total, int32_t R, int32_t micro_rows,
                             const skyrl_ppo_params* params, float* loss_out, float* metrics_out,
                             void* workspace, void* stream);
 /* 1 if the packed and step forms take vocabulary V (aligned: rows 16-B aligned and V % 8 == 0)
  * at this temperature, else 0: the same plan their launches make. */
 int skyrl_policy_train_supports(int32_t V, int32_t aligned, float temperature);
-/* Test infrastructure (never on the hot path): `blocks` workgroups of `threads` threads that each
- * spin on the 100 MHz constant clock for base_ticks + (block % 64) * step_ticks, holding their
- * CU slots: the co-residency test runs the split training pass beside it on another stream (its
- * pieces then arrive spread over time; a piece whose partner is late computes that partner's state
- * itself, header word 33 of the policy_train workspace counts those states). */
-int skyrl_debug_occupy(int32_t blocks, int32_t threads, int64_t base_ticks, int64_t step_ticks, void* stream);
+int skyrl_policy_train_supports_ex(int32_t V, int32_t aligned, float temperature,
+        const skyrl_variant* variant);
 /* x[i] *= g[0] over a bf16 buffer; a no-op kernel when g[0] == 1. */
 int skyrl_scale_bf16_by_device_scalar(const float* g, void* x, int64_t n, void* stream);
 
@@ -440,6 +538,11 @@ int skyrl_sample(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_
                  float temperature, int32_t top_k, float top_p, float min_p, uint64_t seed,
                  const int64_t* seq_ids, int64_t step, int32_t* tokens_out, float* logp_out,
                  void* workspace, void* stream);
+int skyrl_sample_ex(const void* logits, int dtype, int64_t ld, int32_t nseq, int32_t V,
+                 float temperature, int32_t top_k, float top_p, float min_p, uint64_t seed,
+                 const int64_t* seq_ids, int64_t step, int32_t* tokens_out, float* logp_out,
+                 void* workspace, void* stream,
+        const skyrl_variant* variant);
 size_t skyrl_sample_workspace_bytes(int32_t nseq, int32_t V);
 
 /* ---- a9: experience pack --------------------------------------------------
@@ -557,6 +660,11 @@ int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, con
                        const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens, int32_t nseq,
                        int32_t nh, int32_t nkv, int32_t head_dim, float scale, int32_t part_tokens, int32_t nparts,
                        void* out, int64_t out_stride, void* workspace, void* stream);
+int skyrl_paged_decode_ex(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                       const int32_t* block_tables, int64_t bt_stride, const int32_t* context_lens, int32_t nseq,
+                       int32_t nh, int32_t nkv, int32_t head_dim, float scale, int32_t part_tokens, int32_t nparts,
+                       void* out, int64_t out_stride, void* workspace, void* stream,
+        const skyrl_variant* variant);
 /* skyrl_paged_decode_balanced: the same attention with the work split by blocks instead of by
  *                        sequence: the cache blocks of all sequences (per kv head) are laid end
  *                        to end and each of `waves` waves streams an equal share, so a ragged

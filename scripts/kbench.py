@@ -81,16 +81,16 @@ def main():
         times = {v: {"fwd": [], "bwd": []} for v in variants}
         for r in range(args.rounds):
             for (u, nt) in variants:
-                _ffi.call("skyrl_tune", b"logprob_unroll", u)
-                _ffi.call("skyrl_tune", b"logprob_nt", nt)
+                _ffi.set_default_variant(logprob_unroll=u)
+                _ffi.set_default_variant(logprob_nt=nt)
                 times[(u, nt)]["fwd"].append(timeit(lambda: (fwd(x0), fwd(x1))) / 2)
                 times[(u, nt)]["bwd"].append(timeit(lambda: (bwd(x0), bwd(x1))) / 2)
         for (u, nt), t in times.items():
             f, b = statistics.median(t["fwd"]), statistics.median(t["bwd"])
             res[f"logprob_fwd_u{u}_nt{nt}"] = {"ms": f, "GBps": fwd_bytes / f / 1e6}
             res[f"logprob_bwd_u{u}_nt{nt}"] = {"ms": b, "GBps": bwd_bytes / b / 1e6}
-        _ffi.call("skyrl_tune", b"logprob_unroll", 4)
-        _ffi.call("skyrl_tune", b"logprob_nt", 1)
+        _ffi.set_default_variant(logprob_unroll=4)
+        _ffi.set_default_variant(logprob_nt=1)
 
     if on("fused"):
         from skyrl_amd import ppo_utils as pu
@@ -112,28 +112,28 @@ def main():
                       ops._ptr(ent), ops._ptr(dlog), R * V, V, ops._ptr(ws), st)
         # (split, resident, nt stores, resident threads)
         # (split, resident, nt stores, resident threads, 100 * split parts)
-        # (split, resident, nt stores, resident threads, split shape: skyrl_tune "train_split_shape")
+        # (split, resident, nt stores, resident threads, split shape: skyrl_variant "train_split_shape")
         variants = [(1, 1, 1, 1024, 0), (1, 1, 1, 1024, 1), (1, 1, 0, 1024, 0), (0, 1, 1, 1024, 0)]
         times = {v: [] for v in variants}
         for _ in range(args.rounds):  # interleaved rounds
             for v in variants:
                 split, resident, nts, nt, sm = v
-                _ffi.call("skyrl_tune", b"train_split_shape", sm)
-                _ffi.call("skyrl_tune", b"train_split", split)
-                _ffi.call("skyrl_tune", b"train_resident", resident)
-                _ffi.call("skyrl_tune", b"train_ntstore", nts)
-                _ffi.call("skyrl_tune", b"train_resident_nt", nt)
+                _ffi.set_default_variant(train_split_shape=sm)
+                _ffi.set_default_variant(train_split=split)
+                _ffi.set_default_variant(train_resident=resident)
+                _ffi.set_default_variant(train_ntstore=nts)
+                _ffi.set_default_variant(train_resident_nt=nt)
                 times[v].append(timeit(lambda: (fused(x0), fused(x1))) / 2)
-        _ffi.call("skyrl_tune", b"train_split", 1)
-        _ffi.call("skyrl_tune", b"train_split_shape", 0)
+        _ffi.set_default_variant(train_split=1)
+        _ffi.set_default_variant(train_split_shape=0)
         for (split, resident, nts, nt, sm), t in times.items():
             ms = statistics.median(t)
             res[f"policy_train_fused_split{split}_shape{sm}_resident{resident}_nts{nts}_nt{nt}"] = {
                 "ms": ms, "GBps_hbm_algorithmic": rows * (V * 4 + 40) / ms / 1e6,
                 "vs_unfused_bytes": rows * (V * 6) / ms / 1e6}
-        _ffi.call("skyrl_tune", b"train_resident", 1)
-        _ffi.call("skyrl_tune", b"train_ntstore", 1)
-        _ffi.call("skyrl_tune", b"train_resident_nt", 1024)
+        _ffi.set_default_variant(train_resident=1)
+        _ffi.set_default_variant(train_ntstore=1)
+        _ffi.set_default_variant(train_resident_nt=1024)
 
     if on("fused_mb"):  # the fused pass at smaller micro-batches (bytes per launch vs rate)
         from skyrl_amd import ppo_utils as pu
@@ -190,16 +190,16 @@ def main():
                           ops._ptr(lab2), lab2.stride(0), lab2.stride(1), 1.0, ops._ptr(old), ops._ptr(adv),
                           ops._ptr(msk), ops._ptr(ref), ctypes.byref(params), ops._ptr(loss), ops._ptr(met),
                           ops._ptr(lp), ops._ptr(ent), ops._ptr(d2), R * V2, V2, ops._ptr(ws), st)
-            # (split, shape: skyrl_tune "train_split_shape"); split 0 = the resident kernel
+            # (split, shape: skyrl_variant "train_split_shape"); split 0 = the resident kernel
             variants = [(1, sh) for sh in range(0, 6)] + [(0, 0)]  # shape 0: the default by vocabulary
             times = {v: [] for v in variants}
             for _ in range(args.rounds):
                 for v in variants:
-                    _ffi.call("skyrl_tune", b"train_split", v[0])
-                    _ffi.call("skyrl_tune", b"train_split_shape", v[1])
+                    _ffi.set_default_variant(train_split=v[0])
+                    _ffi.set_default_variant(train_split_shape=v[1])
                     times[v].append(timeit(lambda: (fused2(g2[0]), fused2(g2[1]))) / 2)
-            _ffi.call("skyrl_tune", b"train_split", 1)
-            _ffi.call("skyrl_tune", b"train_split_shape", 0)
+            _ffi.set_default_variant(train_split=1)
+            _ffi.set_default_variant(train_split_shape=0)
             for (split, shape), t in times.items():
                 ms = statistics.median(t)
                 res[f"policy_train_V{V2}_split{split}_shape{shape}"] = {

@@ -1,4 +1,4 @@
-"""A/B of the advantage+loss leg's finish launch (skyrl_tune "finish_mode", "loss_bwd_blocks"):
+"""A/B of the advantage+loss leg's finish launch (skyrl_variant "finish_mode", "loss_bwd_blocks"):
 replays bench.advantage_loss_leg at the metric's batch for each setting, twice interleaved."""
 import json
 import os
@@ -17,21 +17,21 @@ if len(sys.argv) > 1 and sys.argv[1] == "nt":  # non-temporal dlogp stores x fin
     for rep in range(2):
         for nt in (0, 1):
             for blocks in (256, 8):
-                _ffi.call("skyrl_tune", b"loss_ntstore", nt)
-                _ffi.call("skyrl_tune", b"loss_bwd_blocks", blocks)
+                _ffi.set_default_variant(loss_ntstore=nt)
+                _ffi.set_default_variant(loss_bwd_blocks=blocks)
                 r = bench.advantage_loss_leg(dev, 512, 1024)
                 print(f"nt {nt} blocks {blocks}:", {k: r[k] for k in keys}, flush=True)
-    _ffi.call("skyrl_tune", b"loss_ntstore", 0)
-    _ffi.call("skyrl_tune", b"loss_bwd_blocks", 256)
+    _ffi.set_default_variant(loss_ntstore=0)
+    _ffi.set_default_variant(loss_bwd_blocks=256)
     sys.exit(0)
 for rep in range(2):
     for mode in (0, 2, 3, 4):
         for blocks in (256,):
-            _ffi.call("skyrl_tune", b"finish_mode", mode)
-            _ffi.call("skyrl_tune", b"loss_bwd_blocks", blocks)
+            _ffi.set_default_variant(finish_mode=mode)
+            _ffi.set_default_variant(loss_bwd_blocks=blocks)
             r = bench.advantage_loss_leg(dev, 512, 1024)
             out.setdefault(f"mode{mode}_blocks{blocks}", []).append({k: r[k] for k in keys})
             print(f"mode {mode} blocks {blocks}:", {k: r[k] for k in keys}, flush=True)
-_ffi.call("skyrl_tune", b"finish_mode", 0)
-_ffi.call("skyrl_tune", b"loss_bwd_blocks", 256)
+_ffi.set_default_variant(finish_mode=0)
+_ffi.set_default_variant(loss_bwd_blocks=256)
 print(json.dumps(out))

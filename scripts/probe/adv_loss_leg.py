@@ -14,8 +14,8 @@ out = {"batch": bench.advantage_loss_leg(dev, 512, 1024, variants=True),
 from skyrl_amd import _ffi  # noqa: E402
 
 for rpb in (1, 2):  # row chunks per fused GRPO+loss block
-    _ffi.call("skyrl_tune", b"grpo_loss_rpb", rpb)
+    _ffi.set_default_variant(grpo_loss_rpb=rpb)
     out[f"rpb{rpb}"] = {k: v for k, v in bench.advantage_loss_leg(dev, 512, 1024).items()
                         if k in ("grpo_loss_fused_us", "total_us")}
-_ffi.call("skyrl_tune", b"grpo_loss_rpb", 1)
+_ffi.set_default_variant(grpo_loss_rpb=1)
 print(json.dumps(out))

@@ -1,4 +1,4 @@
-"""A/B of the paged decode kernel's K/V prefetch depth (skyrl_tune "attn_pf": blocks in flight per wave).
+"""A/B of the paged decode kernel's K/V prefetch depth (skyrl_variant "attn_pf": blocks in flight per wave).
 
 Times the decode kernel (Qwen2.5-1.5B heads: 12 q / 2 kv, D = 128) with the knob
 interleaved over depths, on ragged U[17,1536] and uniform contexts, and checks every depth gives
@@ -34,7 +34,7 @@ def same_outputs(dev):
     q = torch.randn(nseq, nh, D, device=dev, generator=g).to(torch.bfloat16)
     outs = []
     for p in PFS:
-        _ffi.call("skyrl_tune", b"attn_pf", p)
+        _ffi.set_default_variant(attn_pf=p)
         ws = kernels.DecodeWorkspace(dev)
         o = kernels.paged_decode(q, kc, vc, bt, ctx, int(ctx.max()), 1 / math.sqrt(D), workspace=ws,
                                  nparts=kernels.choose_nparts(nseq, nkv, int(ctx.max())))
@@ -53,11 +53,11 @@ def main():
         nparts = kernels.choose_nparts(nseq, 2, args[5])
         for rep in range(2):
             for p in PFS:
-                _ffi.call("skyrl_tune", b"attn_pf", p)
+                _ffi.set_default_variant(attn_pf=p)
                 us, gbs, _ = time_it(dev, args, nparts, kernels.MIN_PARTITION, reps=50)
                 print(json.dumps({"nseq": nseq, "ctx": f"U[{lo},{hi}]", "nparts": nparts, "attn_pf": p, "rep": rep,
                                   "us": round(us, 2), "GBps": round(gbs, 1)}), flush=True)
-    _ffi.call("skyrl_tune", b"attn_pf", 0)
+    _ffi.set_default_variant(attn_pf=0)
 
 
 if __name__ == "__main__":

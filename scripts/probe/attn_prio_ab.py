@@ -1,4 +1,4 @@
-"""A/B of the paged decode kernel's remaining-work priority variant (skyrl_tune "attn_prio").
+"""A/B of the paged decode kernel's remaining-work priority variant (skyrl_variant "attn_prio").
 
 Times bench.rollout_attention_leg (ragged U[17,1536] contexts, Qwen2.5-1.5B heads) with the knob
 off/on interleaved, and checks the two variants give bit-identical outputs (only wave issue
@@ -32,7 +32,7 @@ def same_outputs(dev):
     q = torch.randn(nseq, nh, D, device=dev, generator=g).to(torch.bfloat16)
     outs = []
     for p in (0, 1):
-        _ffi.call("skyrl_tune", b"attn_prio", p)
+        _ffi.set_default_variant(attn_prio=p)
         ws = kernels.DecodeWorkspace(dev)
         o = kernels.paged_decode(q, kc, vc, bt, ctx, int(ctx.max()), 1 / math.sqrt(D), workspace=ws,
                                  nparts=kernels.choose_nparts(nseq, nkv, int(ctx.max())))
@@ -47,11 +47,11 @@ def main():
     for nseq in (512, 256, 1024):
         for rep in range(3):
             for p in (0, 1):
-                _ffi.call("skyrl_tune", b"attn_prio", p)
+                _ffi.set_default_variant(attn_prio=p)
                 r = bench.rollout_attention_leg(dev, nseq, reps=50)
                 r.update({"nseq": nseq, "attn_prio": p, "rep": rep})
                 print(json.dumps(r), flush=True)
-    _ffi.call("skyrl_tune", b"attn_prio", 0)
+    _ffi.set_default_variant(attn_prio=0)
 
 
 if __name__ == "__main__":

@@ -1,4 +1,4 @@
-"""Times the lm_head GEMM loop structures (skyrl_tune lmhead_pipe 4 vs 11) with and without
+"""Times the lm_head GEMM loop structures (skyrl_variant lmhead_pipe 4 vs 11) with and without
 operand copies: the probe library is built with -DSKYRL_GEMM_NOLOAD (the K loop re-reads the
 prologue's LDS tiles; results are garbage, timing is the loop's compute/LDS/barrier cost).
 

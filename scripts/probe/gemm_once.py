@@ -13,7 +13,7 @@ H, V = 1536, 151936
 w = (torch.randn(V, H, device=dev) * 0.08).to(torch.bfloat16)
 h = torch.randn(M, H, device=dev).to(torch.bfloat16)
 z = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
-_ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
+_ffi.set_default_variant(lmhead_pipe=pipe)
 for _ in range(20):
     ops.lmhead_gemm(h, w, out=z)
 torch.cuda.synchronize()

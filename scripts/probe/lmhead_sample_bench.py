@@ -39,14 +39,14 @@ def main():
     ap.add_argument("--V", type=int, default=151936)
     ap.add_argument("--T", type=float, nargs="+", default=[1.0])
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--pipes", type=int, nargs="+", default=[-1], help="skyrl_tune lmhead_pipe variants (-1: default)")
+    ap.add_argument("--pipes", type=int, nargs="+", default=[-1], help="skyrl_variant lmhead_pipe variants (-1: default)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     H, V = args.H, args.V
     w = (torch.randn(V, H, device=dev) * (3.0 / H ** 0.5)).to(torch.bfloat16)
     from skyrl_amd import _ffi
     for M, pipe in [(m, p) for m in args.M for p in args.pipes]:
-        _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
+        _ffi.set_default_variant(lmhead_pipe=pipe)
         h = torch.randn(M, H, device=dev).to(torch.bfloat16)
         ids = torch.arange(M, device=dev)
         z = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
@@ -113,20 +113,20 @@ def gemm_sweep(shapes=((512, 151936), (8192, 151936))):
         for rep in range(2):
             res = {"M": M, "V": V, "rep": rep, "torch_us": round(timeit(lambda: torch.matmul(h, w.T, out=z), it), 1)}
             for pipe in PIPES:
-                _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
+                _ffi.set_default_variant(lmhead_pipe=pipe)
                 res[f"pipe{pipe}_us"] = round(timeit(lambda: ops.lmhead_gemm(h, w, out=z), it), 1)
             zs = []
             for pipe in PIPES:
-                _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
+                _ffi.set_default_variant(lmhead_pipe=pipe)
                 zs.append(ops.lmhead_gemm(h, w).clone())
             res["all_equal"] = all(bool(torch.equal(zs[0], z)) for z in zs[1:])
-            _ffi.call("skyrl_tune", b"lmhead_pipe", -1)
+            _ffi.set_default_variant(lmhead_pipe=-1)
             res["best_TFs"] = round(flops / (min(v for k, v in res.items() if k.startswith("pipe") and k.endswith("_us")) * 1e-6) / 1e12, 1)
             print(json.dumps(res), flush=True)
 
 
 def gemm_group_sweep():
-    """Tile order (skyrl_tune lmhead_group: M tiles per group, 0 = all) x pipeline, learner and
+    """Tile order (skyrl_variant lmhead_group: M tiles per group, 0 = all) x pipeline, learner and
     decode shapes; every configuration's Z must equal the default's bit for bit."""
     from skyrl_amd import _ffi
 
@@ -144,14 +144,14 @@ def gemm_group_sweep():
         for rep in range(2):
             for pipe in (4, 12):
                 for grp in (0, 4, 8):
-                    _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
-                    _ffi.call("skyrl_tune", b"lmhead_group", grp)
+                    _ffi.set_default_variant(lmhead_pipe=pipe)
+                    _ffi.set_default_variant(lmhead_group=grp)
                     t = round(timeit(lambda: ops.lmhead_gemm(h, w, out=z), it), 1)
                     res.setdefault(f"p{pipe}_g{grp}_us", []).append(t)
                     if rep == 0:
                         same = same and bool(torch.equal(ops.lmhead_gemm(h, w), ref))
-        _ffi.call("skyrl_tune", b"lmhead_pipe", -1)
-        _ffi.call("skyrl_tune", b"lmhead_group", 0)
+        _ffi.set_default_variant(lmhead_pipe=-1)
+        _ffi.set_default_variant(lmhead_group=0)
         best = min(min(v) for k, v in res.items() if k.endswith("_us") and k != "torch_us")
         res.update({"all_equal": same, "best_TFs": round(flops / (best * 1e-6) / 1e12, 1)})
         print(json.dumps(res), flush=True)

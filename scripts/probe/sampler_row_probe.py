@@ -1,4 +1,4 @@
-"""Row-mode sampler A/B (skyrl_tune "sampler_row" 0 / 1) at the bench shape (512 x 151,936 bf16):
+"""Row-mode sampler A/B (skyrl_variant "sampler_row" 0 / 1) at the bench shape (512 x 151,936 bf16):
 interleaved passes of 64 launches, plus token/logprob equality against variant 0."""
 import json
 import sys
@@ -21,14 +21,14 @@ def main():
     for T in (1.0, 0.0):
         ref = None
         for var in variants:
-            _ffi.call("skyrl_tune", b"sampler_row", var)
+            _ffi.set_default_variant(sampler_row=var)
             ops.sample(logits[0], temperature=T, seed=1, seq_ids=ids, step=3, tokens_out=tok, logp_out=lp)
             got = (tok.clone(), lp.clone())
             ref = got if ref is None else ref
             res[f"T{T}_v{var}_same"] = bool(torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]))
         for rep in range(4):
             for var in variants:
-                _ffi.call("skyrl_tune", b"sampler_row", var)
+                _ffi.set_default_variant(sampler_row=var)
                 for i in range(3):
                     ops.sample(logits[i], temperature=T, seed=1, seq_ids=ids, step=i, tokens_out=tok, logp_out=lp)
                 torch.cuda.synchronize()
@@ -39,7 +39,7 @@ def main():
                 b.record()
                 b.synchronize()
                 res.setdefault(f"T{T}_v{var}_us", []).append(round(a.elapsed_time(b) / 64 * 1e3, 2))
-    _ffi.call("skyrl_tune", b"sampler_row", 1)
+    _ffi.set_default_variant(sampler_row=1)
     print(json.dumps(res), flush=True)
 
 

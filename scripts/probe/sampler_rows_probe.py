@@ -1,6 +1,6 @@
 """Sampler per launch at the per-rank row counts of a strong-scaling job (512 / N rows x V =
 151,936 bf16, rows R*V apart as in the bench's resident logits, T = 1 and greedy), for each
-split setting (skyrl_tune sampler_split_rows / sampler_split_wgs): 200 launches replayed from a
+split setting (skyrl_variant sampler_split_rows / sampler_split_wgs): 200 launches replayed from a
 HIP graph (the kernels alone; EAGER=1 also times them host-issued through
 TokenSampler.step_ptr). Run under rocprofv3 --kernel-trace --stats for the kernels' own
 durations. Prints one JSON line."""
@@ -29,9 +29,9 @@ for nseq in rows_list:
     for rows_thr, wgs, gran in settings:
         if rows_thr <= nseq and (rows_thr, wgs, gran) != settings[0]:
             continue  # row mode: the same kernel as the first setting's
-        _ffi.call("skyrl_tune", b"sampler_split_rows", rows_thr)
-        _ffi.call("skyrl_tune", b"sampler_split_wgs", wgs)
-        _ffi.call("skyrl_tune", b"sampler_split_gran", gran)
+        _ffi.set_default_variant(sampler_split_rows=rows_thr)
+        _ffi.set_default_variant(sampler_split_wgs=wgs)
+        _ffi.set_default_variant(sampler_split_gran=gran)
         for name, sp in (("t1", SamplingParams()), ("greedy", SamplingParams(temperature=0.0))):
             smp = TokenSampler(nseq, V, R, dev, sp, seed=1)
 
@@ -65,7 +65,7 @@ for nseq in rows_list:
             rec.update(graph_us=round(us, 2), TBps=round(nseq * V * 2 / (us * 1e-6) / 1e12, 2))
             out[f"{nseq}_{name}_rows{rows_thr}_wgs{wgs}_g{gran}"] = rec
             del g
-_ffi.call("skyrl_tune", b"sampler_split_rows", 256)
-_ffi.call("skyrl_tune", b"sampler_split_wgs", 1024)
-_ffi.call("skyrl_tune", b"sampler_split_gran", 8192)
+_ffi.set_default_variant(sampler_split_rows=256)
+_ffi.set_default_variant(sampler_split_wgs=1024)
+_ffi.set_default_variant(sampler_split_gran=8192)
 print(json.dumps(out), flush=True)

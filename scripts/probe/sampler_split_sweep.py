@@ -1,5 +1,5 @@
-"""Split-mode sampler shape sweep on the product library: skyrl_tune("sampler_split_wgs") x
-skyrl_tune("sampler_split_gran") (x skyrl_tune("sampler_split_nt") with SWEEP_NT) at 64 and 128 rows x V = 151,936 bf16 (normal(0, 3) logits),
+"""Split-mode sampler shape sweep on the product library: skyrl_variant ("sampler_split_wgs") x
+skyrl_variant ("sampler_split_gran") (x skyrl_variant ("sampler_split_nt") with SWEEP_NT) at 64 and 128 rows x V = 151,936 bf16 (normal(0, 3) logits),
 T = 1 and greedy. Interleaved rounds of 200 back-to-back launches through TokenSampler.step_ptr
 (one foreign call per launch: ops.sample's Python checks cost ~15 us a call, more than a 64-row
 launch), medians (us); tokens must not depend on the shape (the split partials fold exactly).
@@ -31,9 +31,9 @@ def main():
     out, toks = {}, {}
     for rnd in range(5):
         for nt, wgs, gran in [(a, b, c) for a in NTS for b in WGS for c in GRAN]:
-            _ffi.call("skyrl_tune", b"sampler_split_nt", nt)
-            _ffi.call("skyrl_tune", b"sampler_split_wgs", wgs)
-            _ffi.call("skyrl_tune", b"sampler_split_gran", gran)
+            _ffi.set_default_variant(sampler_split_nt=nt)
+            _ffi.set_default_variant(sampler_split_wgs=wgs)
+            _ffi.set_default_variant(sampler_split_gran=gran)
             for (n, temp), smp in samplers.items():
                 key = f"n{n}_T{temp}_nt{nt}_wgs{wgs}_gran{gran}"
                 smp.step_ptr(big.data_ptr(), V, 3, sh)
@@ -46,9 +46,9 @@ def main():
                 b.record()
                 b.synchronize()
                 out.setdefault(key, []).append(a.elapsed_time(b) / 200 * 1e3)
-    _ffi.call("skyrl_tune", b"sampler_split_nt", 256)  # the defaults
-    _ffi.call("skyrl_tune", b"sampler_split_wgs", 1024)
-    _ffi.call("skyrl_tune", b"sampler_split_gran", 8192)
+    _ffi.set_default_variant(sampler_split_nt=256)  # the defaults
+    _ffi.set_default_variant(sampler_split_wgs=1024)
+    _ffi.set_default_variant(sampler_split_gran=8192)
     res = {k: round(sorted(x)[len(x) // 2], 2) for k, x in out.items()}
     res["tokens_equal"] = all(all(torch.equal(v[0], w) for w in v) for v in toks.values())
     print(json.dumps(res), flush=True)

@@ -1,6 +1,6 @@
 """Wide split sampler (r06, sample_wide_kernel: every load of a workgroup in flight at once) vs the
 streaming split kernel (sample_kernel in split mode) on the product library, selected with
-skyrl_tune("sampler_wide_rows", 0 | 256). Rows in ROWS (default 1,8,16,32,64,96,128,192) x V =
+skyrl_variant ("sampler_wide_rows", 0 | 256). Rows in ROWS (default 1,8,16,32,64,96,128,192) x V =
 151,936 bf16 N(0, 3) logits, T = 1, 0.7 and greedy; interleaved rounds of 200 back-to-back
 launches through TokenSampler.step_ptr, medians (us). The tokens of both kernels must be equal
 (both take the exact-score argmax) and the logprobs within 1e-5. Prints one JSON line.
@@ -31,8 +31,8 @@ def main():
     out, toks, lps = {}, {}, {}
     for rnd in range(5):
         for name, rows_knob, wgs in variants:
-            _ffi.call("skyrl_tune", b"sampler_wide_rows", rows_knob)
-            _ffi.call("skyrl_tune", b"sampler_wide_wgs", wgs)
+            _ffi.set_default_variant(sampler_wide_rows=rows_knob)
+            _ffi.set_default_variant(sampler_wide_wgs=wgs)
             for (n, temp), smp in samplers.items():
                 key = f"n{n}_T{temp}_{name}"
                 for t in range(4):
@@ -48,8 +48,8 @@ def main():
                 b.record()
                 b.synchronize()
                 out.setdefault(key, []).append(a.elapsed_time(b) / 200 * 1e3)
-    _ffi.call("skyrl_tune", b"sampler_wide_rows", 256)  # the defaults
-    _ffi.call("skyrl_tune", b"sampler_wide_wgs", 512)
+    _ffi.set_default_variant(sampler_wide_rows=256)  # the defaults
+    _ffi.set_default_variant(sampler_wide_wgs=512)
     res = {k: round(sorted(x)[len(x) // 2], 2) for k, x in out.items()}
     res["tokens_equal"] = all(all(torch.equal(v[0], w) for w in v) for v in toks.values())
     res["logprob_maxdiff"] = max(float((w - v[0]).abs().max()) for v in lps.values() for w in v)

@@ -1,5 +1,5 @@
 """top_p / min_p below the row-mode batch: the one-pass kernel (one workgroup per row,
-skyrl_tune("sampler_topp_fast") = 1, the default) against the two-kernel path (filter pre-pass +
+skyrl_variant ("sampler_topp_fast") = 1, the default) against the two-kernel path (filter pre-pass +
 MODE 2 sampler in split mode, = 0) at 32 / 64 / 128 / 256 / 512 rows x V = 151,936 bf16
 (normal(0, 3) logits). Interleaved rounds of 100 back-to-back launches through TokenSampler.step_ptr,
 medians (us); the two
@@ -29,7 +29,7 @@ def main():
     out, toks = {}, {}
     for rnd in range(5):
         for fast in (1, 0):
-            _ffi.call("skyrl_tune", b"sampler_topp_fast", fast)
+            _ffi.set_default_variant(sampler_topp_fast=fast)
             for (n, (temp, top_p, min_p)), smp in samplers.items():
                 case = f"n{n}_T{temp}_p{top_p}_minp{min_p}"
                 smp.step_ptr(big.data_ptr(), V, 3, sh)
@@ -42,7 +42,7 @@ def main():
                 b.record()
                 b.synchronize()
                 out.setdefault(f"{case}_fast{fast}", []).append(a.elapsed_time(b) / 100 * 1e3)
-    _ffi.call("skyrl_tune", b"sampler_topp_fast", 1)
+    _ffi.set_default_variant(sampler_topp_fast=1)
     res = {k: round(sorted(x)[len(x) // 2], 2) for k, x in out.items()}
     res["tokens_equal"] = all(torch.equal(d[0], d[1]) for d in toks.values())
     print(json.dumps(res), flush=True)

@@ -1,6 +1,6 @@
 """Attributes pass 1 of the one-pass top_p kernel (sample_topp_kernel) at the bench shape
 [512, 151,936] bf16, T = 1, top_p = 0.95: probe-only builds of capi.hip + sampler.hip with
-compile-time switches (never set in the product) and skyrl_tune's topp_probe = 1 as the default
+compile-time switches (never set in the product) and skyrl_variant's topp_probe = 1 as the default
 (pass 1 alone): the LDS count histogram removed (nohist), the recorded race removed (norace),
 both (neither), the race without its LDS records (norec), against the unchanged pass 1 (base) and the unfiltered T = 1 kernel (one read of
 the row). Interleaved rounds in one process; medians.

@@ -11,6 +11,8 @@ inside our kernels.
 
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import ctypes
 import os
 import threading
@@ -79,6 +81,28 @@ class PackInputs(ctypes.Structure):
     ]
 
 
+VARIANT_FIELDS = (
+    "logprob_unroll", "logprob_nt", "train_resident", "train_resident_nt", "train_ntstore", "train_split",
+    "train_split_shape", "train_split_wait", "grpo_slices", "loss_units", "loss_bwd_blocks", "grpo_loss_rpb",
+    "finish_mode", "sampler_row", "sampler_split_rows", "sampler_split_wgs", "sampler_split_nt", "sampler_split_gran",
+    "sampler_topk_fast", "sampler_topp_fast", "sampler_wide_rows", "sampler_wide_wgs", "topp_probe", "lmhead_pipe",
+    "lmhead_group", "attn_pf")
+VARIANT_DEFAULT = -(2 ** 31)  # SKYRL_VARIANT_DEFAULT
+
+
+class Variant(ctypes.Structure):
+    """Mirror of ``skyrl_variant`` (include/skyrl_hip.h): per-call kernel variant selection."""
+
+    _fields_ = [(f, ctypes.c_int32) for f in VARIANT_FIELDS]
+
+    def __init__(self, **kw):
+        super().__init__(*([VARIANT_DEFAULT] * len(VARIANT_FIELDS)))
+        for k, v in kw.items():
+            if k not in VARIANT_FIELDS:
+                raise KeyError(f"unknown kernel variant field {k!r}")
+            setattr(self, k, int(v))
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -99,7 +123,7 @@ SIGNATURES = {
     "skyrl_comm_reduce_scatter": (_INT, [_P, _P, _I64, _INT, _INT, _P, _P]),
     "skyrl_comm_allgather": (_INT, [_P, _P, _I64, _INT, _P, _P]),
     "skyrl_comm_broadcast": (_INT, [_P, _P, _I64, _INT, _I32, _P, _P]),
-    "skyrl_tune": (_INT, [ctypes.c_char_p, _INT]),
+    "skyrl_variant_init": (None, [ctypes.POINTER(Variant)]),
     "skyrl_grpo_advantage": (_INT, [_P, _P, _P, _INT, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P, _P]),
     "skyrl_adv_norm_workspace_bytes": (_SZ, []),
     "skyrl_adv_norm_stats": (_INT, [_P, _P, _INT, _I64, _P, _P, _P]),
@@ -161,7 +185,6 @@ SIGNATURES = {
     ),
     "skyrl_policy_train_fold": (_INT, [_P, _I32, _I32, _I32, ctypes.POINTER(PPOParams), _P, _P, _P, _P]),
     "skyrl_policy_train_supports": (_INT, [_I32, _I32, _F]),
-    "skyrl_debug_occupy": (_INT, [_I32, _I32, _I64, _I64, _P]),
     "skyrl_scale_bf16_by_device_scalar": (_INT, [_P, _P, _I64, _P]),
     "skyrl_sample_workspace_bytes": (_SZ, [_I32, _I32]),
     "skyrl_sample": (_INT, [_P, _INT, _I64, _I32, _I32, _F, _I32, _F, _F, ctypes.c_uint64, _P, _I64, _P, _P, _P, _P]),
@@ -190,6 +213,51 @@ SIGNATURES = {
     "skyrl_add_rmsnorm": (_INT, [_P, _P, _P, _I32, _I32, _F, _P, _P]),
     "skyrl_silu_mul": (_INT, [_P, _I64, _I32, _P, _P]),
 }
+
+# entry points with a per-call variant form (name + "_ex": the same arguments, then the variant)
+EX_FORMS = ("skyrl_grpo_advantage", "skyrl_ppo_loss_fwd", "skyrl_grpo_ppo_loss_fwd", "skyrl_ppo_loss_bwd",
+            "skyrl_ppo_loss_finish", "skyrl_logprob_fwd", "skyrl_logprob_bwd", "skyrl_lmhead_gemm",
+            "skyrl_lmhead_logprob_fwd", "skyrl_lmhead_sample", "skyrl_policy_train_fwd", "skyrl_policy_train_ragged_fwd",
+            "skyrl_policy_train_micro_fwd", "skyrl_policy_train_supports", "skyrl_sample", "skyrl_paged_decode")
+for _n in EX_FORMS:
+    _r, _a = SIGNATURES[_n]
+    SIGNATURES[_n + "_ex"] = (_r, _a + [ctypes.POINTER(Variant)])
+
+# The host's kernel-variant selection: a context variable (per thread / task), never library
+# state. ``variant(**fields)`` scopes it; ``set_default_variant`` (probes) sets it until reset.
+_VARIANT: contextvars.ContextVar = contextvars.ContextVar("skyrl_variant", default=None)
+
+
+def _merged(fields):
+    """The enclosing variant (if any) with `fields` overridden."""
+    base = _VARIANT.get()
+    out = Variant(**{f: getattr(base, f) for f in VARIANT_FIELDS}) if base is not None else Variant()
+    for k, v in fields.items():
+        if k not in VARIANT_FIELDS:
+            raise KeyError(f"unknown kernel variant field {k!r}")
+        setattr(out, k, int(v))
+    return out
+
+
+@contextlib.contextmanager
+def variant(**fields):
+    """Run the enclosed calls with another variant of the kernels (skyrl_variant, A/B and tests);
+    nested scopes override the enclosing one's fields."""
+    tok = _VARIANT.set(_merged(fields) if fields else _VARIANT.get())
+    try:
+        yield
+    finally:
+        _VARIANT.reset(tok)
+
+
+def set_default_variant(**fields) -> None:
+    """Probe scripts: keep this variant for the following calls of this thread (no args: the defaults)."""
+    _VARIANT.set(_merged(fields) if fields else None)
+
+
+def current_variant():
+    return _VARIANT.get()
+
 
 _lock = threading.Lock()
 _lib = None
@@ -222,9 +290,14 @@ def load() -> ctypes.CDLL:
 
 
 def call(name: str, *args) -> int:
-    """Invoke a status-returning entry point; raise SkyrlHipError on a non-zero status."""
+    """Invoke a status-returning entry point; raise SkyrlHipError on a non-zero status. Under an
+    active ``variant(...)`` an entry point with an _ex form runs that form with the variant."""
     lib = load()
-    rc = getattr(lib, name)(*args)
+    v = _VARIANT.get()
+    if v is not None and name in EX_FORMS:
+        rc = getattr(lib, name + "_ex")(*args, ctypes.byref(v))
+    else:
+        rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.skyrl_last_error().decode(errors="replace")
         raise SkyrlHipError(f"{name} failed (status {rc}): {msg}")
@@ -232,5 +305,8 @@ def call(name: str, *args) -> int:
 
 
 def query(name: str, *args):
-    """Invoke a non-status entry point (workspace sizes, version)."""
+    """Invoke a non-status entry point (workspace sizes, version, support queries)."""
+    v = _VARIANT.get()
+    if v is not None and name in EX_FORMS:
+        return getattr(load(), name + "_ex")(*args, ctypes.byref(v))
     return getattr(load(), name)(*args)

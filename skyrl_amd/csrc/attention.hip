@@ -22,6 +22,7 @@
 // HBM into VGPRs (guide: decode attention, M <= 16 rows per kv head). Partitions are
 // merged by a small reduce kernel when a sequence spans more than one.
 #include "common.h"
+#include "variant.h"
 
 namespace skyrl {
 namespace {
@@ -505,7 +506,6 @@ extern "C" size_t skyrl_paged_decode_workspace_bytes(int32_t nseq, int32_t nh, i
 }
 
 namespace skyrl {
-int g_attn_pf = 0;  // skyrl_tune("attn_pf", 0 default / 4 / 6 / 8): K/V blocks in flight per D = 128 decode wave
 }
 
 extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
@@ -538,7 +538,7 @@ extern "C" int skyrl_paged_decode(const void* q, int64_t q_stride, const void* k
     // D = 128: 4 blocks in flight (205 VGPRs, 2 waves / SIMD). Measured on the ragged rollout mix
     // (512 x U[17,1536]): 92 us vs 101 for the earlier 3-deep loop; 6 and 8 deep (1 wave / SIMD,
     // ring partly in AGPRs) 94-96 us; 3 deep in this unrolled form spills at 3 waves / SIMD.
-    const int pf = g_attn_pf > 0 ? g_attn_pf : 4;
+    const int pf = knobs().attn_pf > 0 ? knobs().attn_pf : 4;
 #define SKYRL_PD_LAUNCH(DD, PF, MINW)                                                                          \
     hipLaunchKernelGGL((paged_decode_kernel<DD, PF, MINW>), grid, dim3(64), 0, as_stream(stream), qp, q_stride, kp, \
                        vp, block_tables, bt_stride, context_lens, nh, nkv, qpk, scale_log2, part_tokens, nparts, op, \

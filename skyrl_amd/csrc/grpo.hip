@@ -11,6 +11,7 @@
 // CPU accumulates in double), the normalisation itself in fp32 as the
 // reference does.
 #include "arrive.h"
+#include "variant.h"
 
 namespace skyrl {
 namespace {
@@ -391,7 +392,6 @@ __global__ __launch_bounds__(kNormThreads) void adv_norm_apply_kernel(const floa
 }
 
 }  // namespace
-int g_grpo_slices = 4;  // skyrl_tune("grpo_slices", 1/2/4): column slices per group (contiguous form)
 
 }  // namespace skyrl
 
@@ -464,8 +464,8 @@ extern "C" int skyrl_grpo_advantage(const float* rewards, const float* scores_in
     if (!group_off && !group_rows) {  // contiguous uniform groups of N / num_groups rows
         SKYRL_REQUIRE(N % num_groups == 0, "grpo: contiguous groups need N % num_groups == 0");
         const int G = N / num_groups;
-        if (vec4 && G <= kMaxFastG && g_grpo_slices > 1) {
-            const int S = g_grpo_slices;
+        if (vec4 && G <= kMaxFastG && knobs().grpo_slices > 1) {
+            const int S = knobs().grpo_slices;
             auto pick = [&](auto k2, auto k4) { return S == 2 ? k2 : k4; };
             auto k = mask_dtype == SKYRL_I64   ? pick(grpo_adv_sliced_kernel<SKYRL_I64, 2>, grpo_adv_sliced_kernel<SKYRL_I64, 4>)
                      : mask_dtype == SKYRL_F32 ? pick(grpo_adv_sliced_kernel<SKYRL_F32, 2>, grpo_adv_sliced_kernel<SKYRL_F32, 4>)

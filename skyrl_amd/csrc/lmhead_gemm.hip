@@ -30,6 +30,7 @@
 // oracle/sampler_ref.c's on the bf16 logits this GEMM produces (STORE), bit for bit.
 #include "noise.h"
 #include "softmax.h"
+#include "variant.h"
 
 namespace skyrl {
 namespace {
@@ -91,14 +92,13 @@ __device__ __forceinline__ float hw_ln(float x) { return __builtin_amdgcn_logf(x
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// skyrl_tune("lmhead_pipe") selects the K pipeline (pick_kernel): 0 = 256 x 256 tiles, BK 64, 2
+// the variant field lmhead_pipe selects the K pipeline (pick_kernel): 0 = 256 x 256 tiles, BK 64, 2
 // stages, one 512-thread workgroup per CU; 1 = 256 x 128 tiles, BK 32, 3 stages, two workgroups
 // per CU; 2 = 256 x 256, BK 32, 4 stages; 3-10 = staggered copies / fragment double buffer /
 // spread copies; 11 = ping-pong wave groups (4 phases per K step); 12 (default) = the fragment
 // double buffer of 4 with three W stages and two H stages. All produce identical Z. Measured
 // (profiles/r02_gemm_*): 12 is the fastest at 512, 2048 and 8192 rows; 11 is slower
 // even without copies (8 barriers per K step).
-int g_lmhead_pipe = 12;
 
 // scripts/probe/gemm_noload.py only (never in the product build): the K loop re-reads the
 // prologue's tiles instead of copying new ones, to time the loop structure without memory.
@@ -1006,13 +1006,12 @@ inline int tiles(int n, int b) { return (n + b - 1) / b; }
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
                             float, uint64_t, const int64_t*, int64_t, float4*, float*, int, const int64_t*, int64_t,
                             unsigned*);
-int g_lmhead_group = 8;  // skyrl_tune("lmhead_group"): M tiles per group of the tile order (0: all)
-int group_for(int mt) { return g_lmhead_group > 0 && g_lmhead_group < mt ? g_lmhead_group : 0; }
+int group_for(int mt) { return knobs().lmhead_group > 0 && knobs().lmhead_group < mt ? knobs().lmhead_group : 0; }
 int tile_threads(int pipe) { return pipe == 13 ? 256 : 2 * (pipe == 1 ? 128 : 256); }
 // the pipeline for these operands: pipe 13 addresses them with 32-bit element offsets
 int pipe_for(int64_t M, int64_t ldh, int64_t N, int64_t ldw) {
-    if (g_lmhead_pipe == 13 && (M * ldh >= (int64_t(1) << 31) || N * ldw >= (int64_t(1) << 31))) return 12;
-    return g_lmhead_pipe;
+    if (knobs().lmhead_pipe == 13 && (M * ldh >= (int64_t(1) << 31) || N * ldw >= (int64_t(1) << 31))) return 12;
+    return knobs().lmhead_pipe;
 }
 int tile_n(int pipe) { return pipe == 1 ? 128 : 256; }  // pipe 3: 256, staggered copies
 template <int EPI>
@@ -1048,17 +1047,6 @@ int check_operands(const void* h, int64_t ldh, const void* w, int64_t ldw, int M
 
 }  // namespace
 
-int lmhead_group_tune(int value) {
-    SKYRL_REQUIRE(value >= 0 && value < 4096, "skyrl_tune: lmhead_group must be in [0, 4096)");
-    g_lmhead_group = value;
-    return SKYRL_OK;
-}
-
-int lmhead_tune(int value) {
-    SKYRL_REQUIRE(value >= -1 && value <= 14, "skyrl_tune: lmhead_pipe must be -1 (default) or 0..14");
-    g_lmhead_pipe = value < 0 ? 12 : value;
-    return SKYRL_OK;
-}
 }  // namespace skyrl
 
 using namespace skyrl;

@@ -17,6 +17,7 @@
 // Backward streams the row again and writes dlogits (2 B/element):
 //   d/dx_v = (g_lp*(1[v=label] - p_v) - g_ent*p_v*(logp_v + H)) / T.
 #include "softmax.h"
+#include "variant.h"
 
 namespace skyrl {
 namespace {
@@ -151,11 +152,6 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(
     }
 }
 
-struct Tuning {
-    int unroll = 4;
-    int nt = 1;
-};
-Tuning g_tune;
 
 template <typename T, int U, bool NT>
 int launch_fwd_v(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
@@ -185,8 +181,8 @@ int launch_bwd_v(const void* logits, int64_t sb, int64_t st, int nb, int nt, int
 template <typename T>
 int launch_fwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
                int64_t lst, float temp, float* logp, float* ent, float* lse, hipStream_t s) {
-    const bool nt_ = g_tune.nt != 0;
-    if (g_tune.unroll == 8)
+    const bool nt_ = knobs().logprob_nt != 0;
+    if (knobs().logprob_unroll == 8)
         return nt_ ? launch_fwd_v<T, 8, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s)
                    : launch_fwd_v<T, 8, false>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s);
     return nt_ ? launch_fwd_v<T, 4, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, logp, ent, lse, s)
@@ -197,8 +193,8 @@ template <typename T>
 int launch_bwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V, const int64_t* labels, int64_t lsb,
                int64_t lst, float temp, const float* lse, const float* ent, const float* glp, const float* gent,
                void* dx, hipStream_t s) {
-    const bool nt_ = g_tune.nt != 0;
-    if (g_tune.unroll == 8)
+    const bool nt_ = knobs().logprob_nt != 0;
+    if (knobs().logprob_unroll == 8)
         return nt_ ? launch_bwd_v<T, 8, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s)
                    : launch_bwd_v<T, 8, false>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s);
     return nt_ ? launch_bwd_v<T, 4, true>(logits, sb, st, nb, nt, V, labels, lsb, lst, temp, lse, ent, glp, gent, dx, s)
@@ -209,157 +205,6 @@ int launch_bwd(const void* logits, int64_t sb, int64_t st, int nb, int nt, int V
 }  // namespace skyrl
 
 using namespace skyrl;
-namespace skyrl {
-extern int g_train_resident;
-extern int g_train_resident_nt;
-extern int g_train_ntstore;
-extern int g_train_split;
-extern int g_train_split_shape;
-extern unsigned g_train_split_wait;
-extern int g_grpo_slices;
-extern int g_loss_units;
-extern int g_loss_bwd_blocks;
-extern int g_grpo_loss_rpb;
-extern int g_finish_mode;
-extern int g_sampler_row;
-extern int g_sampler_split_rows;
-extern int g_sampler_split_wgs;
-extern int g_sampler_split_gran;
-extern int g_sampler_split_nt;
-extern int g_sampler_topk_fast;
-extern int g_sampler_topp_fast;
-extern int g_sampler_wide_rows;
-extern int g_sampler_wide_wgs;
-extern int g_probe_topp;
-extern int g_attn_pf;
-int lmhead_tune(int value);
-int lmhead_group_tune(int value);
-}
-
-extern "C" int skyrl_tune(const char* key, int value) {
-    const std::string k = key ? key : "";
-    if (k == "logprob_unroll") {
-        SKYRL_REQUIRE(value == 4 || value == 8, "skyrl_tune: logprob_unroll must be 4 or 8");
-        g_tune.unroll = value;
-        return SKYRL_OK;
-    }
-    if (k == "train_split_shape") {
-        SKYRL_REQUIRE(value >= 0 && value <= 5, "skyrl_tune: train_split_shape must be 0..5");
-        g_train_split_shape = value;
-        return SKYRL_OK;
-    }
-    if (k == "train_split_wait") {  // 0: a piece computes every partner state not yet published (tests)
-        SKYRL_REQUIRE(value >= 0 && value <= 100000000, "skyrl_tune: train_split_wait must be in [0, 1e8] ticks");
-        g_train_split_wait = (unsigned)value;
-        return SKYRL_OK;
-    }
-    if (k == "train_split") {
-        SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: train_split must be 0 or 1");
-        g_train_split = value;
-        return SKYRL_OK;
-    }
-    if (k == "train_ntstore") {
-        g_train_ntstore = value != 0;
-        return SKYRL_OK;
-    }
-    if (k == "train_resident") {
-        g_train_resident = value != 0;
-        return SKYRL_OK;
-    }
-    if (k == "train_resident_nt") {
-        SKYRL_REQUIRE(value == 768 || value == 1024, "skyrl_tune: train_resident_nt must be 768 or 1024");
-        g_train_resident_nt = value;
-        return SKYRL_OK;
-    }
-    if (k == "grpo_slices") {
-        SKYRL_REQUIRE(value == 1 || value == 2 || value == 4, "skyrl_tune: grpo_slices must be 1, 2 or 4");
-        g_grpo_slices = value;
-        return SKYRL_OK;
-    }
-    if (k == "loss_units") {
-        SKYRL_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "skyrl_tune: loss_units must be 0, 1, 2 or 4");
-        g_loss_units = value;
-        return SKYRL_OK;
-    }
-    if (k == "grpo_loss_rpb") {
-        SKYRL_REQUIRE(value == 1 || value == 2, "skyrl_tune: grpo_loss_rpb must be 1 or 2");
-        g_grpo_loss_rpb = value;
-        return SKYRL_OK;
-    }
-    if (k == "loss_bwd_blocks") {
-        SKYRL_REQUIRE(value >= 1 && value <= 4096, "skyrl_tune: loss_bwd_blocks must be in [1, 4096]");
-        g_loss_bwd_blocks = value;
-        return SKYRL_OK;
-    }
-    if (k == "finish_mode") {
-        SKYRL_REQUIRE(value >= 0 && value <= 4, "skyrl_tune: finish_mode must be in [0, 4]");
-        g_finish_mode = value;
-        return SKYRL_OK;
-    }
-    if (k == "lmhead_pipe") return lmhead_tune(value);
-    if (k == "sampler_row") {
-        SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_row must be 0 or 1");
-        g_sampler_row = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_split_rows") {
-        SKYRL_REQUIRE(value >= 1 && value <= 1024, "skyrl_tune: sampler_split_rows must be in [1, 1024]");
-        g_sampler_split_rows = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_split_wgs") {
-        SKYRL_REQUIRE(value >= 64 && value <= 16384, "skyrl_tune: sampler_split_wgs must be in [64, 16384]");
-        g_sampler_split_wgs = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_split_gran") {
-        SKYRL_REQUIRE(value >= 2048 && value <= 65536 && value % 2048 == 0,
-                      "skyrl_tune: sampler_split_gran must be a multiple of 2048 in [2048, 65536]");
-        g_sampler_split_gran = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_split_nt") {
-        SKYRL_REQUIRE(value == 256 || value == 512, "skyrl_tune: sampler_split_nt must be 256 or 512");
-        g_sampler_split_nt = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_topk_fast") {
-        SKYRL_REQUIRE(value == 0 || value == 1, "skyrl_tune: sampler_topk_fast must be 0 or 1");
-        g_sampler_topk_fast = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_wide_rows") {
-        SKYRL_REQUIRE(value >= 0 && value <= 1024, "skyrl_tune: sampler_wide_rows must be in [0, 1024]");
-        g_sampler_wide_rows = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_wide_wgs") {
-        SKYRL_REQUIRE(value >= 1 && value <= 8192, "skyrl_tune: sampler_wide_wgs must be in [1, 8192]");
-        g_sampler_wide_wgs = value;
-        return SKYRL_OK;
-    }
-    if (k == "topp_probe") {
-        SKYRL_REQUIRE((value >= 0 && value <= 7) || value == 11, "skyrl_tune: topp_probe must be 0 .. 7 or 11");
-        g_probe_topp = value;
-        return SKYRL_OK;
-    }
-    if (k == "sampler_topp_fast") {
-        SKYRL_REQUIRE(value >= 0 && value <= 2, "skyrl_tune: sampler_topp_fast must be 0, 1 or 2");
-        g_sampler_topp_fast = value;
-        return SKYRL_OK;
-    }
-    if (k == "lmhead_group") return lmhead_group_tune(value);
-    if (k == "attn_pf") {
-        SKYRL_REQUIRE(value == 0 || value == 4 || value == 6 || value == 8, "skyrl_tune: attn_pf must be 0, 4, 6 or 8");
-        g_attn_pf = value;
-        return SKYRL_OK;
-    }
-    if (k == "logprob_nt") {
-        g_tune.nt = value != 0;
-        return SKYRL_OK;
-    }
-    return fail(SKYRL_ERR_INVALID, "skyrl_tune: unknown key " + k);
-}
 
 extern "C" int skyrl_logprob_fwd(const void* logits, int dtype, int64_t stride_b, int64_t stride_t, int32_t nb,
                                  int32_t nt, int32_t V, const int64_t* labels, int64_t lstride_b, int64_t lstride_t,

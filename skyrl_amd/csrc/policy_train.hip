@@ -25,6 +25,7 @@
 #include <utility>
 
 #include "arrive.h"
+#include "variant.h"
 
 // Phase timestamps for scripts/probe/train_phase_probe (compiled only there, never in the product).
 #ifdef SKYRL_TRAIN_PHASE_PROBE
@@ -59,7 +60,7 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// dlogits are written once and not re-read here: optionally non-temporal (skyrl_tune("train_ntstore"))
+// dlogits are written once and not re-read here: optionally non-temporal (the variant field train_ntstore)
 __device__ __forceinline__ void st_out(uint4* p, uint4 v, bool nts) {
     if (nts) __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(p));
     else *p = v;
@@ -688,7 +689,7 @@ constexpr int kSplitMaxP = 12;  // most pieces per row of any built shape (split
 // publish within microseconds; past this bound (other streams' kernels holding the CUs, a grid
 // larger than what is resident) the piece computes the partner's state itself (no deadlock, no
 // error path, the same bits)
-constexpr unsigned kSplitWaitTicks = 5000u;  // 50 us (skyrl_tune("train_split_wait", ticks) for tests)
+constexpr unsigned kSplitWaitTicks = 5000u;  // 50 us (the variant field train_split_wait = ticks for tests)
 
 typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
 typedef __attribute__((address_space(1))) unsigned ptr_gu32;
@@ -1147,12 +1148,6 @@ __global__ void scale_bf16_kernel(const float* __restrict__ g, uint16_t* __restr
 
 }  // namespace
 
-int g_train_resident = 1;  // skyrl_tune("train_resident", 0/1)
-int g_train_resident_nt = 1024;  // skyrl_tune("train_resident_nt", 768/1024)
-int g_train_ntstore = 1;   // skyrl_tune("train_ntstore", 0/1): non-temporal dlogits stores
-int g_train_split = 1;     // skyrl_tune("train_split", 0/1): split-row kernel where it applies
-int g_train_split_shape = 0;  // skyrl_tune("train_split_shape", 0 = by vocabulary, 1..7: kSplitShapes)
-unsigned g_train_split_wait = kSplitWaitTicks;  // skyrl_tune("train_split_wait"): partner wait bound (ticks)
 
 }  // namespace skyrl
 
@@ -1204,7 +1199,7 @@ using SplitKernel = void (*)(const uint16_t*, int64_t, int64_t, int, int, const 
                              unsigned long long*, unsigned*, const int32_t*, unsigned);
 // Split shapes: P pieces per row of NT threads each, W waves per SIMD (the __launch_bounds__
 // occupancy target, i.e. the VGPR cap 512 / W in granules of 8 the compiler schedules the
-// piece's registers under). skyrl_tune("train_split_shape", i) picks one; 0 = by vocabulary.
+// piece's registers under). the variant field train_split_shape = i picks one; 0 = by vocabulary.
 template <int P, bool EDGE, int W, int NT, int NV>
 SplitKernel pick_split(bool has_t) {
     return has_t ? policy_train_split_kernel<NV, true, P, EDGE, W, NT>
@@ -1278,7 +1273,7 @@ int split_nv(int nvec, int parts, int nt) {
     if (nv < 1 || nv > 19 || last <= (nv - 1) * nt) return 0;
     return nv;
 }
-// the split launch for a vocabulary: skyrl_tune("train_split_shape") if set, else by V
+// the split launch for a vocabulary: the variant field train_split_shape if set, else by V
 struct SplitPlan {
     SplitKernel kern = nullptr;
     int parts = 0, threads = 0;
@@ -1289,7 +1284,7 @@ SplitPlan split_plan(int V, bool aligned, bool has_t) {
     // 128 KB in six 256-thread pieces (13 vectors per thread at V = 151,936: 79 VGPRs, so 6
     // waves per SIMD and 6 pieces per CU in flight), shorter rows and rows with partial
     // vectors (GPT-2) in four
-    const int shape = g_train_split_shape ? g_train_split_shape : (aligned && V > 65536 ? 5 : 2);
+    const int shape = knobs().train_split_shape ? knobs().train_split_shape : (aligned && V > 65536 ? 5 : 2);
     const SplitShape& sh = kSplitShapes[shape];
     const int nv = aligned ? split_nv(V / 8, sh.parts, sh.threads) : split_nv_edge(V, sh.parts, sh.threads);
     if (nv > 0) sp.kern = split_for(nv, has_t, shape, !aligned);
@@ -1361,8 +1356,8 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
     const bool same_align = ((reinterpret_cast<uintptr_t>(out) - reinterpret_cast<uintptr_t>(in)) % 16) == 0 &&
                             ((gstride_b - stride_b) % 8) == 0 && ((gstride_t - stride_t) % 8) == 0 &&
                             (reinterpret_cast<uintptr_t>(in) % 2) == 0;
-    // Qwen2.5's V = 151,936 at 768 threads x 25 vectors (skyrl_tune("train_resident_nt", 768))
-    const bool use768 = g_train_resident_nt == 768 && nvec <= 25 * 768 && nvec > 24 * 768;
+    // Qwen2.5's V = 151,936 at 768 threads x 25 vectors (the variant field train_resident_nt = 768)
+    const bool use768 = knobs().train_resident_nt == 768 && nvec <= 25 * 768 && nvec > 24 * 768;
     // rows without partial vectors: 16-B-aligned logits and dlogits rows, V % 8 == 0
     const bool aligned = (V % 8) == 0 && (reinterpret_cast<uintptr_t>(in) % 16) == 0 && (stride_b % 8) == 0 &&
                          (stride_t % 8) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0 &&
@@ -1376,31 +1371,31 @@ extern "C" int skyrl_policy_train_fwd(const void* logits, int dtype, int64_t str
         for (int cand : kEdgeNV)
             if (span <= cand * 1024) { nv = cand; break; }
     }
-    const bool resident_ok = g_train_resident && same_align && nv > 0;
+    const bool resident_ok = knobs().train_resident && same_align && nv > 0;
     const SplitPlan sp = split_plan(V, aligned, has_t);
-    if (g_train_split && g_train_resident && same_align && sp.kern && (int64_t)n * R * sp.parts < (1ll << 31)) {
+    if (knobs().train_split && knobs().train_resident && same_align && sp.kern && (int64_t)n * R * sp.parts < (1ll << 31)) {
         hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)n * R * sp.parts)), dim3(sp.threads), 0, s, in,
                            stride_b, stride_t, R, V, labels, lstride_b, lstride_t, temperature, old_log_probs,
                            advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok,
-                           out, gstride_b, gstride_t, g_train_ntstore != 0, gran, err_word, nullptr, g_train_split_wait);
-    } else if (g_train_resident && use768 && aligned) {
+                           out, gstride_b, gstride_t, knobs().train_ntstore != 0, gran, err_word, nullptr, (unsigned)knobs().train_split_wait);
+    } else if (knobs().train_resident && use768 && aligned) {
         auto kern = has_t ? policy_train_resident_kernel<768, 25, true, false>
                           : policy_train_resident_kernel<768, 25, false, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)n * R)), dim3(768), 0, s, in, stride_b, stride_t, R, V, labels,
                            lstride_b, lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
                            row_scale, scal, *params, logp_out, entropy_out, tok, out, gstride_b, gstride_t,
-                           g_train_ntstore != 0);
+                           knobs().train_ntstore != 0);
     } else if (resident_ok) {
         hipLaunchKernelGGL(aligned ? resident_aligned_for(nv, has_t) : resident_edge_for(nv, has_t),
                            dim3((unsigned)((int64_t)n * R)), dim3(1024), 0, s, in, stride_b, stride_t, R, V, labels,
                            lstride_b, lstride_t, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
                            row_scale, scal, *params, logp_out, entropy_out, tok, out, gstride_b, gstride_t,
-                           g_train_ntstore != 0);
+                           knobs().train_ntstore != 0);
     } else
     hipLaunchKernelGGL(policy_train_kernel, dim3((unsigned)((int64_t)n * R)), dim3(kThreads), 0, s, in, stride_b,
                        stride_t, R, (int64_t)n * R, V, labels, lstride_b, lstride_t, temperature, has_t, old_log_probs,
                        advantages, loss_mask, ref_log_probs, row_scale, scal, *params, logp_out, entropy_out, tok, out,
-                       gstride_b, gstride_t, g_train_ntstore != 0);
+                       gstride_b, gstride_t, knobs().train_ntstore != 0);
     rc = check_launch("policy_train_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
@@ -1458,7 +1453,7 @@ extern "C" int skyrl_policy_train_ragged_fwd(const void* logits, int dtype, int6
     hipLaunchKernelGGL(sp.kern, dim3((unsigned)((int64_t)ntok * sp.parts)), dim3(sp.threads), 0, s, reinterpret_cast<const uint16_t*>(logits), (int64_t)0, ld, R, V,
                        labels, (int64_t)0, (int64_t)1, temperature, old_log_probs, advantages, loss_mask, ref_log_probs,
                        row_scale, scal, *params, logp_out, entropy_out, tok, reinterpret_cast<uint16_t*>(grad_logits),
-                       (int64_t)0, ld_grad, g_train_ntstore != 0, gran, err_word, token_pos, g_train_split_wait);
+                       (int64_t)0, ld_grad, knobs().train_ntstore != 0, gran, err_word, token_pos, (unsigned)knobs().train_split_wait);
     rc = check_launch("policy_train_split_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(train_epilogue_kernel, dim3(1), dim3(kThreads), 0, s, tok, loss_mask, n, R, *params, scal,
@@ -1602,7 +1597,7 @@ extern "C" int skyrl_policy_train_micro_fwd(const void* logits, int dtype, int64
                        temperature, old_log_probs + o, advantages + o, loss_mask + o,
                        ref_log_probs ? ref_log_probs + o : nullptr, row_scale, scal, *params, logp_out + o,
                        entropy_out ? entropy_out + o : nullptr, tok, reinterpret_cast<uint16_t*>(grad_logits), gsb,
-                       ld_grad, g_train_ntstore != 0, gran, err_word, token_pos, g_train_split_wait);
+                       ld_grad, knobs().train_ntstore != 0, gran, err_word, token_pos, (unsigned)knobs().train_split_wait);
     return check_launch("policy_train_split_kernel");
 }
 
@@ -1630,22 +1625,4 @@ extern "C" int skyrl_policy_train_supports(int32_t V, int32_t aligned, float tem
     return split_plan(V, aligned != 0 && (V % 8) == 0, temperature != 1.0f).kern != nullptr ? 1 : 0;
 }
 
-namespace skyrl {
-namespace {
-__global__ void debug_occupy_kernel(int64_t base, int64_t step) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t until = (uint64_t)(base + (int64_t)(blockIdx.x % 64) * step);
-    while (__builtin_amdgcn_s_memrealtime() - t0 < until) __builtin_amdgcn_s_sleep(8);
-}
-}  // namespace
-}  // namespace skyrl
-
-extern "C" int skyrl_debug_occupy(int32_t blocks, int32_t threads, int64_t base_ticks, int64_t step_ticks, void* stream) {
-    SKYRL_REQUIRE(blocks >= 1 && blocks <= 65536 && threads >= 64 && threads <= 1024 && threads % 64 == 0,
-                  "debug_occupy: bad grid");
-    SKYRL_REQUIRE(base_ticks >= 0 && step_ticks >= 0 && base_ticks + 64 * step_ticks <= 100000000,
-                  "debug_occupy: at most 1 s of spinning");
-    hipLaunchKernelGGL(debug_occupy_kernel, dim3(blocks), dim3(threads), 0, as_stream(stream), base_ticks, step_ticks);
-    return check_launch("debug_occupy_kernel");
-}
 

@@ -19,6 +19,7 @@
 // backward launch (skyrl_ppo_loss_finish) folds them stream-ordered -- no polling -- and
 // rescales; loss and metrics are valid once that launch has run.
 #include "arrive.h"
+#include "variant.h"
 
 // Phase timestamps for scripts/probe/phase_probe (compiled only there, never in the product).
 #ifdef SKYRL_PHASE_PROBE
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void loss_finish_kernel(const float* __re
                                                                float* __restrict__ gent, int64_t numel, int mode) {
     if (blockIdx.x == 0) {
         __shared__ double s_redd[kFW * kNP];
-        if (mode == 2) return;  // timing probe only (skyrl_tune "finish_mode" 2): no fold
+        if (mode == 2) return;  // timing probe only (the variant field finish_mode = 2): no fold
         double tot[kNP] = {0, 0, 0, 0, 0};
         if (mode == 0) {  // two records per thread in flight per pass (512 units: one pass); clamped
             // indices, no branch around a load (its end would wait for every load before it)
@@ -909,16 +910,11 @@ inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<
 
 using namespace skyrl;
 
-namespace skyrl {
-int g_loss_units = 0;  // skyrl_tune("loss_units", 0 auto / 1 / 2 / 4): row chunks per loss block
-int g_loss_bwd_blocks = 256;
-int g_finish_mode = 0;  // skyrl_tune("finish_mode"): 0 block tree, 1 nb first; timing probes (wrong values):
-                        // 2 no fold, 3 no block reduction, 4 no divisions. A one-wave
-                        // fold standing for the 256 threads (no LDS / barrier) measured slower: 4.02 vs
-                        // 3.05 us (profiles/r03_adv_leg_finish_one_wave.log)
-int g_grpo_loss_rpb = 1;  // skyrl_tune("grpo_loss_rpb", 1 / 2): row chunks per fused GRPO+loss block (2 measured slower: 12.1 vs 11.0 us)
-  // skyrl_tune("loss_bwd_blocks"): grid cap of the backward rescale
-}
+// Loss variants (skyrl_variant, per call): loss_units (row chunks per loss block, 0 auto), grpo_loss_rpb
+// (row chunks per fused GRPO+loss block; 2 measured slower: 12.1 vs 11.0 us), loss_bwd_blocks (grid cap
+// of the backward rescale), finish_mode (0 block tree, 1 nb first; timing probes with wrong values: 2 no
+// fold, 3 no block reduction, 4 no divisions; a one-wave fold standing for the 256 threads (no LDS /
+// barrier) measured slower: 4.02 vs 3.05 us, profiles/r03_adv_leg_finish_one_wave.log).
 
 extern "C" size_t skyrl_ppo_loss_workspace_bytes(int32_t n, int32_t R) {
     const size_t nchunks = (size_t)((R + kFT - 1) / kFT);
@@ -985,7 +981,7 @@ extern "C" int skyrl_ppo_loss_fwd(const float* log_probs, const float* old_log_p
                       aligned16(loss_mask) && aligned16(ref_log_probs) && aligned16(entropy) && aligned16(grad_logp) &&
                       aligned16(grad_entropy);
     const int units = n * nchunks;
-    int U = g_loss_units > 0 ? g_loss_units : (units > 2048 ? 4 : 1);
+    int U = knobs().loss_units > 0 ? knobs().loss_units : (units > 2048 ? 4 : 1);
     if (!vec4) U = 1;
     const int nb = (units + U - 1) / U;
     auto pick = [&](auto kd, auto kf) { return defer ? kd : kf; };
@@ -1047,7 +1043,7 @@ extern "C" int skyrl_grpo_ppo_loss_fwd(const float* rewards, const float* scores
     unsigned* epoch_word = reinterpret_cast<unsigned*>(w);
     unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + 256);
     const int xcd_map = (num_groups % 8) == 0 ? 1 : 0;  // grid stays n * nchunks blocks either way
-    const int rpb = (g_grpo_loss_rpb == 2 && (G * nchunks) % 2 == 0) ? 2 : 1;
+    const int rpb = (knobs().grpo_loss_rpb == 2 && (G * nchunks) % 2 == 0) ? 2 : 1;
     using KT = decltype(&grpo_loss_grad_kernel<SKYRL_I64, 1, false>);
     KT k = nullptr;
 #define SKYRL_GL_PICK(MDT)                                                                              \
@@ -1074,11 +1070,11 @@ extern "C" int skyrl_ppo_loss_finish(const float* grad_out, float* grad_logp, fl
     const int64_t numel = (int64_t)n * R;
     const int units = n * ((R + kFT - 1) / kFT);
     int64_t blocks = grad_out ? (numel + kThreads - 1) / kThreads : 0;
-    if (blocks > g_loss_bwd_blocks) blocks = g_loss_bwd_blocks;
+    if (blocks > knobs().loss_bwd_blocks) blocks = knobs().loss_bwd_blocks;
     const float* parts = reinterpret_cast<const float*>(reinterpret_cast<char*>(workspace) + 256);
     hipLaunchKernelGGL(loss_finish_kernel, dim3((unsigned)(1 + blocks)), dim3(kThreads), 0, as_stream(stream), grad_out,
                        parts, nb_word_of(workspace), n, units, *params, loss_out, metrics_out, grad_logp, grad_entropy,
-                       numel, g_finish_mode);
+                       numel, knobs().finish_mode);
     return check_launch("loss_finish_kernel");
 }
 
@@ -1089,7 +1085,7 @@ extern "C" int skyrl_ppo_loss_bwd(const float* grad_out, int64_t numel, float* g
     if (numel == 0) return SKYRL_OK;
     // a small grid: at unit upstream gradient (the common case) the launch only dispatches
     int64_t blocks = (numel + kThreads - 1) / kThreads;
-    if (blocks > g_loss_bwd_blocks) blocks = g_loss_bwd_blocks;
+    if (blocks > knobs().loss_bwd_blocks) blocks = knobs().loss_bwd_blocks;
     hipLaunchKernelGGL(rescale_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, as_stream(stream), grad_out,
                        grad_logp, grad_entropy, numel);
     return check_launch("rescale_kernel");

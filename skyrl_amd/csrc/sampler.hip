@@ -23,32 +23,30 @@
 // partials in split order (lowest index wins ties).
 #include "arrive.h"
 #include "noise.h"
+#include "variant.h"
 
 #include <type_traits>
 
 #pragma clang fp contract(off)
 
 namespace skyrl {
-int g_sampler_row = 1;  // skyrl_tune("sampler_row"): 1 = progress-priority row kernel (default), 0 = plain
-int g_sampler_split_rows = 256;   // skyrl_tune("sampler_split_rows"): rows split over workgroups below this
-int g_sampler_split_wgs = 1024;   // skyrl_tune("sampler_split_wgs"): workgroups a split launch aims at (4 per CU: 4 waves per SIMD at 256 threads)
-int g_sampler_split_nt = 256;    // skyrl_tune("sampler_split_nt"): threads per split-mode workgroup (256 or 512)
-int g_sampler_split_gran = 8192;  // skyrl_tune("sampler_split_gran"): split chunks are multiples of this (elements)
-int g_sampler_topk_fast = 1;  // skyrl_tune("sampler_topk_fast"): 0 = always the pre-pass + MODE 2 kernels
-int g_sampler_wide_rows = 256;  // skyrl_tune("sampler_wide_rows"): unfiltered bf16 batches below this many rows take
-                                // the wide split kernel (0: never)
-int g_sampler_wide_wgs = 512;   // skyrl_tune("sampler_wide_wgs"): workgroups a wide launch aims at
-// skyrl_tune("sampler_topp_fast"): 0 = top_p / min_p alone on the pre-pass + MODE 2 kernels; 1 (default)
-// = the one-pass kernel, except min_p without top_p below the row-mode batch, where the pre-pass and
-// the split MODE 2 sampler measured faster (32 / 64 / 128 rows: 26.2 / 33.0 / 43.2 vs 43.8 / 44.8 /
-// 47.4 us; 256 rows: 68.1 vs 49.6; same tokens; profiles/r05_topp_rows.json); 2 = always the one-pass kernel
-int g_sampler_topp_fast = 1;
+// Sampler variants (skyrl_variant, per call; the defaults are the tuned choices): sampler_row (1 =
+// progress-priority row kernel, 0 = plain), sampler_split_rows (rows split over workgroups below
+// this), sampler_split_wgs (workgroups a split launch aims at: 4 per CU at 256 threads),
+// sampler_split_nt (threads per split workgroup), sampler_split_gran (split chunks are multiples of
+// this many elements), sampler_topk_fast (0 = top_k on the pre-pass + MODE 2 kernels),
+// sampler_wide_rows / sampler_wide_wgs (unfiltered bf16 batches below this many rows take the wide
+// split kernel, aiming at this many workgroups; 0 rows: never), sampler_topp_fast (0 = top_p / min_p
+// alone on the pre-pass + MODE 2 kernels; 1 = the one-pass kernel, except min_p without top_p below
+// the row-mode batch, where the pre-pass and the split MODE 2 sampler measured faster (32 / 64 / 128
+// rows: 26.2 / 33.0 / 43.2 vs 43.8 / 44.8 / 47.4 us; 256 rows: 68.1 vs 49.6; same tokens;
+// profiles/r05_topp_rows.json); 2 = always the one-pass kernel), topp_probe (timing probes: 1 pass 1
+// alone, 2 pass 1 + the cut, 3 / 4 + a bare re-read (tokens invalid); 5 every row through pass 2
+// (valid tokens); 6 / 7 min_p's in-row pass 2 timed per row (tokens = ticks; 7 without the visits);
+// 11 per row, the cut's and pass 1's times in the outputs).
 #ifndef SKYRL_TP_PROBE0  // scripts/probe/topp_variants.py builds with another default; the product: 0
 #define SKYRL_TP_PROBE0 0
 #endif
-int g_probe_topp = SKYRL_TP_PROBE0;  // (11: per row, the cut's and pass 1's times in the outputs)  // skyrl_tune("topp_probe"): 1 pass 1 alone, 2 pass 1 + the cut, 3 / 4 + a bare re-read
-                       // (timing only, tokens invalid); 5: every row through pass 2 (valid tokens); 6 / 7:
-                       // min_p's in-row pass 2 timed per row (tokens = ticks; 7 without the visits)
 namespace {
 
 constexpr int kThreads = 256;
@@ -1822,7 +1820,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     mx = uni(mx);
     const uint32_t kmax = okey_bf16(f32_to_bf16(mx));  // the max is a bf16 value: exact
     const float mthr = uni(mx * inv_t + ln_min_p);
-    if (probe == 1) return;  // timing probe (skyrl_tune topp_probe): pass 1 only
+    if (probe == 1) return;  // timing probe (variant field topp_probe): pass 1 only
     const uint64_t t_p1 = __builtin_amdgcn_s_memrealtime();  // (probe 11: the cut's time per row)
 
     bool fb = s_bad != 0u || s_nslow > (uint32_t)kPSlowCap;  // block-uniform
@@ -2807,14 +2805,14 @@ __global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
 }
 
-// Splits per row: below g_sampler_split_rows rows the row is cut into chunks of a multiple of
-// g_sampler_split_gran elements (default 8192 = one full streaming iteration of a 256-thread
+// Splits per row: below knobs().sampler_split_rows rows the row is cut into chunks of a multiple of
+// knobs().sampler_split_gran elements (default 8192 = one full streaming iteration of a 256-thread
 // split, so every split runs the pipelined main loop, not the ragged-tail path) for about
-// g_sampler_split_wgs workgroups in all; at or above it one 512-thread workgroup owns a row.
+// knobs().sampler_split_wgs workgroups in all; at or above it one 512-thread workgroup owns a row.
 int splits_for(int nseq, int V) {
-    if (nseq <= 0 || V <= 0 || nseq >= g_sampler_split_rows || nseq >= kMaxSplitRows) return 1;
-    const int s0 = (g_sampler_split_wgs + nseq - 1) / nseq;
-    const int64_t g = g_sampler_split_gran;
+    if (nseq <= 0 || V <= 0 || nseq >= knobs().sampler_split_rows || nseq >= kMaxSplitRows) return 1;
+    const int s0 = (knobs().sampler_split_wgs + nseq - 1) / nseq;
+    const int64_t g = knobs().sampler_split_gran;
     int64_t chunk = ((int64_t)(V + s0 - 1) / s0 + g - 1) / g * g;
     if ((V + chunk - 1) / chunk > kMaxSplits) chunk = ((int64_t)(V + kMaxSplits - 1) / kMaxSplits + g - 1) / g * g;
     const int s = (int)((V + chunk - 1) / chunk);  // every split non-empty (launch_sample's chunk is <= this one)
@@ -2823,18 +2821,18 @@ int splits_for(int nseq, int V) {
 
 size_t ws_align(size_t b) { return (b + 255) / 256 * 256; }
 // the split partials' region: sized for the most splits any setting gives, so a workspace
-// allocated once stays valid under every skyrl_tune choice
+// allocated once stays valid under every variant
 size_t parts_bytes(int nseq) { return ws_align((size_t)nseq * kMaxSplits * sizeof(Part)); }
 
 template <typename T, int MODE>
 void launch_mode(dim3 grid, bool row_mode, hipStream_t stream, const T* lg, int64_t ld, int V, int chunk, float inv_t,
                  int use_topk, int use_minp, float ln_min_p, uint64_t seed, const int64_t* seq_ids, int64_t step,
                  int use_topp, const RowFilter* filt, int32_t* tokens, float* logp, Part* parts, unsigned* counters) {
-    if (row_mode && g_sampler_row == 1)
+    if (row_mode && knobs().sampler_row == 1)
         hipLaunchKernelGGL((sample_kernel<T, MODE, 512, true>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t,
                            use_topk, use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts,
                            counters);
-    else if (row_mode || g_sampler_split_nt == 512)
+    else if (row_mode || knobs().sampler_split_nt == 512)
         hipLaunchKernelGGL((sample_kernel<T, MODE, 512>), grid, dim3(512), 0, stream, lg, ld, V, chunk, inv_t, use_topk,
                            use_minp, ln_min_p, seed, seq_ids, step, use_topp, filt, tokens, logp, parts, counters);
     else
@@ -2857,7 +2855,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
                   void* ws, hipStream_t stream) {
     const int nsplit = splits_for(nseq, V);
     int chunk = (V + nsplit - 1) / nsplit;
-    chunk = nsplit > 1 ? (chunk + g_sampler_split_gran - 1) / g_sampler_split_gran * g_sampler_split_gran
+    chunk = nsplit > 1 ? (chunk + knobs().sampler_split_gran - 1) / knobs().sampler_split_gran * knobs().sampler_split_gran
                        : (chunk + 15) & ~15;
     char* w = reinterpret_cast<char*>(ws);
     unsigned* counters = reinterpret_cast<unsigned*>(w);
@@ -2874,7 +2872,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     const T* lg = reinterpret_cast<const T*>(logits);
     // top_k <= kFastK on 16-B aligned rows: the one-pass kernel alone (rows its candidate lists
     // cannot settle run the pre-pass's and MODE 2's code inside it)
-    const bool fast = g_sampler_topk_fast && use_topk && top_k <= kFastK &&
+    const bool fast = knobs().sampler_topk_fast && use_topk && top_k <= kFastK &&
                       (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && ((ld * (int64_t)sizeof(T)) & 15) == 0;
     if (fast) {
         hipLaunchKernelGGL(sample_topk_kernel<T>, dim3(nseq), dim3(kFastNT), 0, stream, lg, ld, V, top_k, inv_t, use_minp,
@@ -2883,8 +2881,9 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     }
     // top_p / min_p without top_k on 16-B aligned bf16 rows: the two-pass kernel alone
     if constexpr (sizeof(T) == 2) {
-        if (g_sampler_topp_fast && !use_topk &&
-            (use_topp || (use_minp && (g_sampler_topp_fast == 2 || nseq >= g_sampler_split_rows))) &&
+        const int probe = knobs().topp_probe ? knobs().topp_probe : SKYRL_TP_PROBE0;
+        if (knobs().sampler_topp_fast && !use_topk &&
+            (use_topp || (use_minp && (knobs().sampler_topp_fast == 2 || nseq >= knobs().sampler_split_rows))) &&
             V <= kP2Splits * 8 * kPNT * 8 &&
             (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
             ((ld * (int64_t)sizeof(T)) & 15) == 0) {
@@ -2900,13 +2899,13 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
             if (use_topp)
                 hipLaunchKernelGGL((sample_topp_kernel<T, true>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
                                    use_minp, ln_min_p, top_p, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt,
-                                   g_probe_topp);
+                                   probe);
             else
                 hipLaunchKernelGGL((sample_topp_kernel<T, false>), dim3(nseq), dim3(kPNT), 0, stream, lg, ld, V, inv_t,
                                    use_minp, ln_min_p, 1.0f, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt,
-                                   g_probe_topp);
+                                   probe);
             int rc = check_launch("sample_topp_kernel");
-            if (rc || !use_topp || (g_probe_topp >= 1 && g_probe_topp <= 4) || g_probe_topp == 11) return rc;  // (probes 1-4, 11)
+            if (rc || !use_topp || (probe >= 1 && probe <= 4) || probe == 11) return rc;  // (probes 1-4, 11)
             hipLaunchKernelGGL((sample_topp_pass2_kernel<T, true>), dim3(nseq, kP2Splits), dim3(kPNT), 0, stream, lg, ld,
                                V, inv_t, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt, pties, pparts);
             return check_launch("sample_topp_pass2_kernel");
@@ -2916,10 +2915,10 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
     if constexpr (sizeof(T) == 2) {
         const int nvec = V / 8;
         const int cap = kWideNT * kWideVPT;
-        if (!use_topk && !use_minp && !use_topp && nseq < g_sampler_wide_rows && nseq < kMaxSplitRows &&
+        if (!use_topk && !use_minp && !use_topp && nseq < knobs().sampler_wide_rows && nseq < kMaxSplitRows &&
             V % 8 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && ((ld * (int64_t)sizeof(T)) & 15) == 0 &&
             (nvec + cap - 1) / cap <= kMaxSplits) {
-            int ns = (g_sampler_wide_wgs + nseq - 1) / nseq;
+            int ns = (knobs().sampler_wide_wgs + nseq - 1) / nseq;
             ns = max(ns, (nvec + cap - 1) / cap);
             ns = min(ns, min(kMaxSplits, nvec));
             const int per_wg = (nvec + ns - 1) / ns;
@@ -2947,7 +2946,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
         if (rc) return rc;
     }
     const dim3 grid(nseq, nsplit);
-    const bool row_mode = nsplit == 1 && nseq >= g_sampler_split_rows;
+    const bool row_mode = nsplit == 1 && nseq >= knobs().sampler_split_rows;
     if (greedy)
         launch_mode<T, 0>(grid, row_mode, stream, lg, ld, V, chunk, inv_t, 0, 0, ln_min_p, seed, seq_ids, step, 0,
                           filt, tokens, logp, parts, counters);

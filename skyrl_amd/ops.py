@@ -14,6 +14,7 @@ import torch
 
 from . import _ffi
 from ._ffi import BF16, F32, I32, I64, U8
+from ._ffi import set_default_variant, variant  # noqa: F401  (per-call kernel variants, skyrl_variant)
 
 _MASK_DTYPES = {torch.float32: F32, torch.int64: I64, torch.int32: I32, torch.bool: U8, torch.uint8: U8}
 KL_TYPES = {"k1": 0, "abs": 1, "k2": 2, "k3": 3}

@@ -40,6 +40,7 @@ class TokenSampler:
         self.workspace = torch.zeros(_ffi.query("skyrl_sample_workspace_bytes", nseq, vocab), dtype=torch.uint8,
                                      device=self.device)
         self._fn = _ffi.load().skyrl_sample
+        self._fn_ex = _ffi.load().skyrl_sample_ex  # under an active _ffi.variant(...)
         self._ids_ptr, self._ws_ptr = self.seq_ids.data_ptr(), self.workspace.data_ptr()
         self._tok_ptr, self._lp_ptr = self.tokens.data_ptr(), self.logprobs.data_ptr()
         self._err = _ffi.load().skyrl_last_error
@@ -48,11 +49,12 @@ class TokenSampler:
         """Lowest-overhead form for decode loops: raw device address of row 0 of step t's
         [nseq, V] logits, row stride in elements, and the hipStream_t handle."""
         p = self.params
-        rc = self._fn(logits_ptr, self.dtype_code, row_stride, self.nseq, self.vocab, float(p.temperature),
-                      int(p.top_k if p.top_k is not None else -1), _top_p(p), float(p.min_p or 0.0),
-                      ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self._ids_ptr, int(t),
-                      self._tok_ptr + 4 * self.nseq * t, self._lp_ptr + 4 * self.nseq * t, self._ws_ptr,
-                      stream_handle)
+        args = (logits_ptr, self.dtype_code, row_stride, self.nseq, self.vocab, float(p.temperature),
+                int(p.top_k if p.top_k is not None else -1), _top_p(p), float(p.min_p or 0.0),
+                ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self._ids_ptr, int(t),
+                self._tok_ptr + 4 * self.nseq * t, self._lp_ptr + 4 * self.nseq * t, self._ws_ptr, stream_handle)
+        v = _ffi.current_variant()
+        rc = self._fn(*args) if v is None else self._fn_ex(*args, ctypes.byref(v))
         if rc != 0:
             raise _ffi.SkyrlHipError(f"skyrl_sample failed: {self._err().decode()}")
 
@@ -62,11 +64,12 @@ class TokenSampler:
             raise ValueError(f"logits must be [{self.nseq}, {self.vocab}] with unit vocab stride")
         s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         p = self.params
-        rc = self._fn(logits.data_ptr(), self.dtype_code, logits.stride(0), self.nseq, self.vocab,
-                      float(p.temperature), int(p.top_k if p.top_k is not None else -1), _top_p(p),
-                      float(p.min_p or 0.0),
-                      ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self.seq_ids.data_ptr(), int(t),
-                      self.tokens[t].data_ptr(), self.logprobs[t].data_ptr(), self.workspace.data_ptr(), s)
+        args = (logits.data_ptr(), self.dtype_code, logits.stride(0), self.nseq, self.vocab, float(p.temperature),
+                int(p.top_k if p.top_k is not None else -1), _top_p(p), float(p.min_p or 0.0),
+                ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self.seq_ids.data_ptr(), int(t),
+                self.tokens[t].data_ptr(), self.logprobs[t].data_ptr(), self.workspace.data_ptr(), s)
+        v = _ffi.current_variant()
+        rc = self._fn(*args) if v is None else self._fn_ex(*args, ctypes.byref(v))
         if rc != 0:
             raise _ffi.SkyrlHipError(f"skyrl_sample failed: {self._err().decode()}")
         return self.tokens[t], self.logprobs[t]

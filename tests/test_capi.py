@@ -34,7 +34,7 @@ def test_ffi_signatures_cover_header():
 
 def test_abi_version_and_error_path():
     lib = _ffi.load()
-    assert lib.skyrl_abi_version() == 10
+    assert lib.skyrl_abi_version() == 11
     # argument validation happens on the host before any launch: no GPU needed
     with pytest.raises(_ffi.SkyrlHipError, match="temperature"):
         _ffi.call("skyrl_logprob_fwd", ctypes.c_void_p(16), _ffi.BF16, 8, 8, 1, 1, 8, ctypes.c_void_p(16), 1, 1,
@@ -119,3 +119,50 @@ def test_comm_abi_host_checks():
     with pytest.raises(_ffi.SkyrlHipError, match="dtype"):
         _ffi.call("skyrl_comm_broadcast", ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 9, 0, ctypes.c_void_p(16), None)
     assert _ffi.call("skyrl_comm_destroy", None) == 0
+
+
+def _exported_symbols():
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _ffi.LIB_PATH], stdout=subprocess.PIPE, text=True, check=True)
+    return sorted({ln.split()[-1] for ln in out.stdout.splitlines() if " T " in ln and ln.split()[-1].startswith("skyrl_")})
+
+
+def test_no_process_state_setters_exported():
+    """reentrant entry points, no global mutable state. The A/B
+    knobs are a caller-owned skyrl_variant passed to one *_ex call; nothing exported stores state:
+    no skyrl_tune, no test hook, and every exported C symbol is an entry point of skyrl_hip.h."""
+    syms = _exported_symbols()
+    assert syms == header_functions(), set(syms) ^ set(header_functions())
+    assert not [s for s in syms if "tune" in s or "occupy" in s or s.startswith("skyrl_set")]
+    assert all(n + "_ex" in syms for n in _ffi.EX_FORMS)
+
+
+def test_variant_applies_to_its_call_only():
+    """A variant changes the decision of the call it is passed to and of no other call: the
+    fused-pass support query (host-only, no GPU) with the 4 x 256 split shape at V = 200,000 says
+    no; the plain call before and after, and an _ex call with NULL or an all-default variant, say
+    yes. A bad field fails that call alone."""
+    lib = _ffi.load()
+    V = 200_000
+    v = _ffi.Variant(train_split_shape=2)
+    d = _ffi.Variant()
+    lib.skyrl_variant_init(ctypes.byref(d))
+    assert all(getattr(d, f) == _ffi.VARIANT_DEFAULT for f in _ffi.VARIANT_FIELDS)
+    assert lib.skyrl_policy_train_supports(V, 1, 1.0) == 1
+    assert lib.skyrl_policy_train_supports_ex(V, 1, 1.0, ctypes.byref(v)) == 0
+    assert lib.skyrl_policy_train_supports(V, 1, 1.0) == 1
+    assert lib.skyrl_policy_train_supports_ex(V, 1, 1.0, None) == 1
+    assert lib.skyrl_policy_train_supports_ex(V, 1, 1.0, ctypes.byref(d)) == 1
+    bad = _ffi.Variant(sampler_split_nt=300)
+    assert lib.skyrl_policy_train_supports_ex(V, 1, 1.0, ctypes.byref(bad)) == -1
+    with pytest.raises(_ffi.SkyrlHipError, match="bad value for sampler_split_nt"):
+        _ffi.call("skyrl_sample_ex", ctypes.c_void_p(16), _ffi.BF16, 8, 1, 8, 1.0, -1, 1.0, 0.0, 0, None, 0,
+                  ctypes.c_void_p(16), None, ctypes.c_void_p(16), None, ctypes.byref(bad))
+    # the host-side scope: nested scopes override fields, leaving restores the enclosing one
+    with _ffi.variant(train_split_shape=2):
+        assert _ffi.query("skyrl_policy_train_supports", V, 1, 1.0) == 0
+        with _ffi.variant(train_split_shape=5):
+            assert _ffi.query("skyrl_policy_train_supports", V, 1, 1.0) == 1
+        assert _ffi.query("skyrl_policy_train_supports", V, 1, 1.0) == 0
+    assert _ffi.query("skyrl_policy_train_supports", V, 1, 1.0) == 1 and _ffi.current_variant() is None

@@ -113,7 +113,7 @@ def test_paged_decode_matches_fp32_reference(nh, nkv, D, nparts, part_min):
 
 @pytest.mark.parametrize("pf", [4, 6, 8])
 def test_paged_decode_prefetch_depths(pf):
-    """Every K/V prefetch depth of the D = 128 kernel (skyrl_tune attn_pf: blocks in flight per
+    """Every K/V prefetch depth of the D = 128 kernel (skyrl_variant attn_pf: blocks in flight per
     wave, a register ring unrolled by the depth) matches the fp32 reference and the default
     bit for bit: ragged contexts that end mid-ring and past the 64-entry block-table window
     (2051 tokens = 129 blocks in one wave), unsplit and split."""
@@ -126,11 +126,8 @@ def test_paged_decode_prefetch_depths(pf):
     ref = attn_ref(q, dense, scale)
     for nparts in (1, 3):
         base = kernels.paged_decode(q, kc, vc, bt, cl, max(ctx), scale, nparts=nparts)
-        kernels._ffi.call("skyrl_tune", b"attn_pf", pf)
-        try:
+        with kernels._ffi.variant(attn_pf=pf):
             out = kernels.paged_decode(q, kc, vc, bt, cl, max(ctx), scale, nparts=nparts)
-        finally:
-            kernels._ffi.call("skyrl_tune", b"attn_pf", 0)
         torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
         assert torch.equal(out, base)
 

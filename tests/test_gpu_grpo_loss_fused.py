@@ -202,16 +202,13 @@ def test_deferred_fold_graph_replay_and_no_grad(dev):
 
 @pytest.mark.parametrize("rpb", [1, 2])
 def test_rows_per_block_variants(dev, rpb):
-    """Both block shapes of the one-launch kernel (skyrl_tune "grpo_loss_rpb") give the two
+    """Both block shapes of the one-launch kernel (skyrl_variant grpo_loss_rpb) give the two
     calls' outputs bit for bit."""
     from skyrl_amd import _ffi
 
-    _ffi.call("skyrl_tune", b"grpo_loss_rpb", rpb)
-    try:
+    with _ffi.variant(grpo_loss_rpb=rpb):
         test_fused_matches_two_calls_bit_exact(dev, CASES[0])
         test_fused_matches_two_calls_bit_exact(dev, CASES[2])
-    finally:
-        _ffi.call("skyrl_tune", b"grpo_loss_rpb", 1)
 
 
 @pytest.mark.parametrize("n", [4096, 777])

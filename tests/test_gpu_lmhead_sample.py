@@ -43,12 +43,9 @@ def test_gemm_pipeline_variants_exact(dev, pipe, K):
     g = torch.Generator().manual_seed(K + pipe)
     M, V = 300, 700
     h, w = _ints((M, K), g, -2, 3), _ints((V, K), g, -2, 3)
-    _ffi.call("skyrl_tune", b"lmhead_pipe", pipe)
-    try:
+    with _ffi.variant(lmhead_pipe=pipe):
         z = ops.lmhead_gemm(h.to(dev), w.to(dev))
         tf, _ = ops.lmhead_sample(h.to(dev), w.to(dev), seed=3, step=1)
-    finally:
-        _ffi.call("skyrl_tune", b"lmhead_pipe", -1)
     assert torch.equal(z.cpu(), (h.float() @ w.float().T).to(torch.bfloat16))
     tu, _ = ops.sample(z, seed=3, step=1)
     assert torch.equal(tf, tu)
@@ -216,7 +213,7 @@ def test_lmhead_logprob_fwd_matches_oracle_and_chunked(dev, V, K, temp):
 
 @pytest.mark.parametrize("group", [8, 4, 3, 0])
 def test_gemm_grouped_tile_order_exact(dev, group):
-    """The grouped tile order (skyrl_tune lmhead_group: M tiles per group, M fastest inside a group)
+    """The grouped tile order (skyrl_variant lmhead_group: M tiles per group, M fastest inside a group)
     with a partial last group (M = 2600 -> 11 M tiles), exact on small-integer operands; the fused
     sampler and the learner logprob epilogue give the same results under every order."""
     from skyrl_amd import _ffi
@@ -227,13 +224,10 @@ def test_gemm_grouped_tile_order_exact(dev, group):
     w[:, 0] += torch.arange(V).remainder(5).to(torch.bfloat16)
     hd, wd = h.to(dev), w.to(dev)
     lab = torch.randint(0, V, (M,), generator=g).to(dev)
-    _ffi.call("skyrl_tune", b"lmhead_group", group)
-    try:
+    with _ffi.variant(lmhead_group=group):
         z = ops.lmhead_gemm(hd, wd)
         tok, lp = ops.lmhead_sample(hd, wd, temperature=1.0, seed=9, step=2)
         lpf, entf = ops.lmhead_logprob_fwd(hd, wd, lab)
-    finally:
-        _ffi.call("skyrl_tune", b"lmhead_group", 8)
     assert torch.equal(z.cpu(), (h.float() @ w.float().T).to(torch.bfloat16))
     tok_u, lp_u = ops.sample(z, temperature=1.0, seed=9, step=2)
     assert torch.equal(tok, tok_u)

@@ -592,12 +592,11 @@ def test_policy_train_resident_qwen_vocab(dev, temp):
                                               use_entropy_loss=True, has_entropy=True)
     outs = []
     for resident in (1, 0):
-        ops._ffi.call("skyrl_tune", b"train_resident", resident)
-        x = logits.clone().requires_grad_(True)
-        loss, m, lp, ent = ops.policy_train(x, labels, old, adv, mask, params, ref_log_probs=ref, temperature=temp)
-        loss.backward()
+        with ops.variant(train_resident=resident):
+            x = logits.clone().requires_grad_(True)
+            loss, m, lp, ent = ops.policy_train(x, labels, old, adv, mask, params, ref_log_probs=ref, temperature=temp)
+            loss.backward()
         outs.append((loss.detach(), m.clone(), lp, ent, x.grad))
-    ops._ffi.call("skyrl_tune", b"train_resident", 1)
     for a, b in zip(outs[0], outs[1]):
         close(a, b, atol=1e-6, rtol=1e-5)
     lpc = cpu_ref.logprobs_from_logits(logits.cpu(), labels.cpu(), temperature=temp)

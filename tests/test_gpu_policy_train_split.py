@@ -55,8 +55,7 @@ def test_split_fresh_granules_every_launch(dev, V, R, shape):
     params = _params()
     n = 3
     A, B = _inputs(1, n, R, V, dev), _inputs(2, n, R, V, dev)
-    ops._ffi.call("skyrl_tune", b"train_split_shape", shape)
-    try:
+    with ops.variant(train_split_shape=shape):
         ops.WORKSPACES._bufs.clear()
         ref_b = _run(B, params)  # B on a fresh workspace
         ops.WORKSPACES._bufs.clear()
@@ -64,8 +63,6 @@ def test_split_fresh_granules_every_launch(dev, V, R, shape):
         got = _run(B, params)  # B after A on the same workspace
         _same(got, ref_b)
         _same(_run(B, params), ref_b)  # replay
-    finally:
-        ops._ffi.call("skyrl_tune", b"train_split_shape", 0)
     assert float(ref_b[1][6]) == 0.0
     if shape != 5:  # vs the default shape: another fp32 summation order only
         q = _run(B, params)
@@ -79,11 +76,8 @@ def test_split_matches_resident_at_metric_vocab(dev, temp):
     params = _params()
     inp = _inputs(3, 16, 128, 151936, dev)
     split = _run(inp, params, temp)
-    ops._ffi.call("skyrl_tune", b"train_split", 0)
-    try:
+    with ops.variant(train_split=0):
         res = _run(inp, params, temp)
-    finally:
-        ops._ffi.call("skyrl_tune", b"train_split", 1)
     for a, b in zip(split[:4], res[:4]):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(split[4].float(), res[4].float(), atol=2e-6, rtol=1e-2)
@@ -153,18 +147,13 @@ def test_split_edge_rows_match_resident(dev, V, shape):
     mask = (torch.rand(n, R, generator=g) < 0.9).float().to(dev)
     ref = (-6 + torch.randn(n, R, generator=g)).to(dev)
     outs = []
-    ops._ffi.call("skyrl_tune", b"train_split_shape", shape)
-    try:
-        for split in (1, 0):
-            ops._ffi.call("skyrl_tune", b"train_split", split)
+    for split in (1, 0):
+        with ops.variant(train_split_shape=shape, train_split=split):
             full = logits.clone().requires_grad_(True)
             loss, m, lp, ent = ops.policy_train(full[:, -R - 1:-1], labels, old, adv, mask, params, ref_log_probs=ref,
                                                 temperature=0.8)
             loss.backward()
-            outs.append((loss.detach(), m.clone(), lp, ent, full.grad))
-    finally:
-        ops._ffi.call("skyrl_tune", b"train_split", 1)
-        ops._ffi.call("skyrl_tune", b"train_split_shape", 0)
+        outs.append((loss.detach(), m.clone(), lp, ent, full.grad))
     for a, b in zip(outs[0][:4], outs[1][:4]):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(outs[0][4].float(), outs[1][4].float(), atol=2e-6, rtol=1e-2)
@@ -182,7 +171,7 @@ def _recomputed(dev, n, R):
 
 
 def test_partner_states_computed_in_place_give_the_same_bits(dev):
-    """skyrl_tune("train_split_wait", 0): a piece does not wait for any partner that has not
+    """skyrl_variant train_split_wait = 0: a piece does not wait for any partner that has not
     published at its first poll and computes that partner's state from the partner's slice
     (the path a piece takes when its partners are not resident). The pieces' states are the
     same bits either way, so loss, metrics, logp, entropy and dlogits equal the default run's
@@ -193,14 +182,22 @@ def test_partner_states_computed_in_place_give_the_same_bits(dev):
         base = _run(inp, params)
         n, R = inp[1].shape
         c0 = _recomputed(dev, n, R)
-        ops._ffi.call("skyrl_tune", b"train_split_wait", 0)
-        try:
+        with ops.variant(train_split_wait=0):
             forced = _run(inp, params)
-        finally:
-            ops._ffi.call("skyrl_tune", b"train_split_wait", 5000)
         assert _recomputed(dev, n, R) > c0, V  # the in-place path ran
         for a, b in zip(base, forced):
             assert torch.equal(a, b), V
+
+
+def occupy(*args):
+    """tests/csrc/occupy.hip (a test hook library, not part of libskyrl_hip.so)."""
+    import ctypes
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libskyrl_testhooks.so")
+    fn = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL).skyrl_test_occupy
+    fn.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+    assert fn(*args) == 0
 
 
 def test_split_pass_beside_a_kernel_holding_the_cus(dev):
@@ -214,7 +211,7 @@ def test_split_pass_beside_a_kernel_holding_the_cus(dev):
     side = torch.cuda.Stream(dev)
     torch.cuda.synchronize(dev)
     with torch.cuda.stream(side):
-        ops._ffi.call("skyrl_debug_occupy", 512, 1024, 100_000, 2_000, ops._stream(dev))
+        occupy(512, 1024, 100_000, 2_000, ops._stream(dev))
     out = _run(inp, params)  # current stream: runs beside the occupier
     torch.cuda.synchronize(dev)
     assert float(out[1][6]) == 0.0  # no split-exchange error

@@ -3,8 +3,8 @@ N = 2, 4, 8; the engine's shrinking decode batches too): rows split over workgro
 arriver folds the partials (no acquire: sc1 records, MI355X_MICROARCH.md's valid hand-off form),
 against oracle/sampler_ref.c (tokens bit-exact, logprobs 1e-4) and against the same rows decided
 by one workgroup per row (tokens identical: every split decides with exact scores, the lowest
-index on ties). The split count follows skyrl_tune("sampler_split_wgs") and the row threshold
-"sampler_split_rows", the split workgroup size "sampler_split_nt"; every setting must give the same
+index on ties). The split count follows the variant field sampler_split_wgs and the row threshold
+sampler_split_rows, the split workgroup size sampler_split_nt; every setting must give the same
 tokens (T = 1 runs the multiplicative bound in row mode and the additive one in split mode).
 Since r06 unfiltered bf16 batches below "sampler_wide_rows" (256) take the wide split kernel
 (sample_wide_kernel: every load of a workgroup in flight at once, "sampler_wide_wgs" workgroups
@@ -21,18 +21,9 @@ V = 151936
 
 
 def _knobs(rows=256, wgs=1024, gran=8192, nt=256, wide=256, wide_wgs=512):
-    ops._ffi.call("skyrl_tune", b"sampler_wide_rows", wide)
-    ops._ffi.call("skyrl_tune", b"sampler_wide_wgs", wide_wgs)
-    ops._ffi.call("skyrl_tune", b"sampler_split_nt", nt)
-    ops._ffi.call("skyrl_tune", b"sampler_split_rows", rows)
-    ops._ffi.call("skyrl_tune", b"sampler_split_wgs", wgs)
-    ops._ffi.call("skyrl_tune", b"sampler_split_gran", gran)
-
-
-@pytest.fixture(autouse=True)
-def _restore():
-    yield
-    _knobs()
+    """The calls' kernel variant (skyrl_variant through ops.variant, per call)."""
+    return ops.variant(sampler_wide_rows=wide, sampler_wide_wgs=wide_wgs, sampler_split_nt=nt, sampler_split_rows=rows,
+                       sampler_split_wgs=wgs, sampler_split_gran=gran)
 
 
 @pytest.mark.parametrize("n", [1, 13, 64, 128, 255])
@@ -41,15 +32,11 @@ def _restore():
 def test_split_rows_match_oracle(dev, n, temp, kernel):
     from oracle import sampler as osamp
 
-    if kernel == "wide":
-        _knobs()
-    else:
-        _knobs(nt=int(kernel[5:]), wide=0)
-
     g = torch.Generator().manual_seed(n * 10 + int(temp * 10))
     x = (torch.randn(n, V, generator=g) * 3).to(torch.bfloat16)
     ids = torch.arange(n, dtype=torch.int64) * 7 + 3
-    tok, lp = ops.sample(x.to(dev), temperature=temp, seed=9, seq_ids=ids.to(dev), step=11)
+    with _knobs() if kernel == "wide" else _knobs(nt=int(kernel[5:]), wide=0):
+        tok, lp = ops.sample(x.to(dev), temperature=temp, seed=9, seq_ids=ids.to(dev), step=11)
     etok, elp = osamp.sample(x, temp, -1, 1.0, 0.0, 9, ids, 11)
     assert torch.equal(tok.cpu(), etok), int((tok.cpu() != etok).sum())
     torch.testing.assert_close(lp.cpu(), elp, atol=1e-4, rtol=1e-4)
@@ -70,10 +57,10 @@ def test_split_settings_give_identical_tokens(dev, n):
             (1024, 8192, 2048, 256, 0, 512), (1024, 960, 4096, 256, 0, 512), (1024, 256, 16384, 512, 0, 512),
             (1024, 2048, 2048, 512, 0, 512), (256, 1024, 8192, 256, 1024, 512), (256, 1024, 8192, 256, 1024, 64),
             (256, 1024, 8192, 256, 1024, 2048), (256, 1024, 8192, 256, 1024, 8192)):
-        _knobs(rows, wgs, gran, nt, wide, wwgs)
-        for temp in (1.0, 0.0, 1.3):
-            tok, lp = ops.sample(x, temperature=temp, seed=2, seq_ids=ids, step=5)
-            outs.setdefault(temp, []).append((tok.clone(), lp.clone()))
+        with _knobs(rows, wgs, gran, nt, wide, wwgs):
+            for temp in (1.0, 0.0, 1.3):
+                tok, lp = ops.sample(x, temperature=temp, seed=2, seq_ids=ids, step=5)
+                outs.setdefault(temp, []).append((tok.clone(), lp.clone()))
     for temp, res in outs.items():
         for tok, lp in res[1:]:
             assert torch.equal(tok, res[0][0]), (n, temp)
@@ -89,8 +76,8 @@ def test_split_workspace_reused_across_sizes_and_settings(dev):
     seq = [(64, 2048, 0), (200, 2048, 256), (7, 512, 0), (300, 2048, 1024), (128, 8192, 256), (64, 1024, 0),
            (255, 2048, 256), (33, 2048, 256), (300, 512, 0)]
     for k, (n, wgs, wide) in enumerate(seq):
-        _knobs(1024, wgs, wide=wide, wide_wgs=wgs)
-        tok, _ = ops.sample(x[:n], temperature=1.0, seed=3, seq_ids=ids[:n], step=k)
-        _knobs(1, 2048, wide=0)  # one workgroup per row: no counters
-        ref, _ = ops.sample(x[:n], temperature=1.0, seed=3, seq_ids=ids[:n], step=k)
+        with _knobs(1024, wgs, wide=wide, wide_wgs=wgs):
+            tok, _ = ops.sample(x[:n], temperature=1.0, seed=3, seq_ids=ids[:n], step=k)
+        with _knobs(1, 2048, wide=0):  # one workgroup per row: no counters
+            ref, _ = ops.sample(x[:n], temperature=1.0, seed=3, seq_ids=ids[:n], step=k)
         assert torch.equal(tok, ref), (n, wgs)

@@ -1,5 +1,5 @@
 """a1 filtered sampling: the one-pass top_k kernel (sample_topk_kernel) against the two-kernel
-path it short-cuts (the filter pre-pass + the MODE 2 sampler, skyrl_tune("sampler_topk_fast", 0))
+path it short-cuts (the filter pre-pass + the MODE 2 sampler, skyrl_variant sampler_topk_fast = 0)
 and against oracle/sampler_ref.c.
 
 The fast kernel decides every row whose per-thread top-8 lists provably hold the row's top k and
@@ -23,8 +23,7 @@ _ROW_FALLBACK = -3
 
 
 def _run(x, fast, **kw):
-    ops._ffi.call("skyrl_tune", b"sampler_topk_fast", int(fast))
-    try:
+    with ops.variant(sampler_topk_fast=int(fast)):
         tok, lp = ops.sample(x, **kw)
         torch.cuda.synchronize()
         ws = ops.WORKSPACES.get(x.device, "sample", ops._ffi.query("skyrl_sample_workspace_bytes", x.shape[0],
@@ -36,8 +35,6 @@ def _run(x, fast, **kw):
                      and kw.get("temperature", 1.0) > 0):
             assert int(((filt[:, 2] == _ROW_DONE) | (filt[:, 2] == _ROW_FALLBACK)).sum()) == n
         return tok.cpu(), lp.cpu(), done
-    finally:
-        ops._ffi.call("skyrl_tune", b"sampler_topk_fast", 1)
 
 
 def _ab(x, min_done, **kw):

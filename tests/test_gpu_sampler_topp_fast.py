@@ -1,7 +1,7 @@
 """a1 filtered sampling without top_k: the top_p / min_p kernel (sample_topp_kernel) against the
 two-kernel path it replaces (the filter pre-pass + the MODE 2 sampler,
-skyrl_tune("sampler_topp_fast", 0)) and against oracle/sampler_ref.c. The tests force the kernel
-with skyrl_tune("sampler_topp_fast", 2); the default (1) sends min_p without top_p below 256 rows
+skyrl_variant sampler_topp_fast = 0) and against oracle/sampler_ref.c. The tests force the kernel
+with sampler_topp_fast = 2 (ops.variant, per call); the default (1) sends min_p without top_p below 256 rows
 to the two-kernel path, which is faster there.
 
 Pass 1 takes the row max, a count histogram per exact bf16 key and MODE 2's race over the whole
@@ -13,7 +13,7 @@ alone in the same workgroup. Tokens, logprobs and the recorded cut (key, last ke
 the two-kernel path's bit for bit. Rows outside its bounds (the cut among the values below 2^-16
 or the zeros, a tie group over 1024 at the cut, NaN / +inf, values >= 2^16, over 512 nonzero
 values below 2^-16) run the two-kernel path's code in the workgroup (RowFilter.ik =
-kRowFallback); the rest are kRowDone. skyrl_tune("topp_probe", 5) sends every row through pass 2.
+kRowFallback); the rest are kRowDone. The variant topp_probe = 5 sends every row through pass 2.
 The recipe this serves: top_p = 0.95 alone (examples/text_to_sql/run_skyrl_sql.sh:60 and eight
 more example scripts), semantics skyrl-tx/tx/utils/generator.py:423-449.
 """
@@ -37,13 +37,10 @@ def _filters(x):
 
 
 def _run(x, fast, **kw):
-    ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 2 if fast else 0)  # 2: the one-pass kernel at any row count
-    try:
+    with ops.variant(sampler_topp_fast=2 if fast else 0):  # 2: the one-pass kernel at any row count
         tok, lp = ops.sample(x, **kw)
         torch.cuda.synchronize()
         return tok.cpu(), lp.cpu(), _filters(x)
-    finally:
-        ops._ffi.call("skyrl_tune", b"sampler_topp_fast", 1)
 
 
 def _ab(x, min_done, **kw):
@@ -184,7 +181,7 @@ def test_topp_fast_small_and_ragged_vocab(dev, V):
 
 @pytest.mark.parametrize("V", [517, 4097, 50257, 151936])
 def test_every_row_through_pass2(dev, V):
-    """skyrl_tune("topp_probe", 5): no row decided in pass 1, so every row runs pass 2 (top_p: the
+    """variant topp_probe = 5: no row decided in pass 1, so every row runs pass 2 (top_p: the
     second launch's 8 pieces, the ragged tail in the last piece; min_p: in the workgroup), against
     the two-kernel path and the oracle."""
     from oracle import sampler as osamp
@@ -196,11 +193,8 @@ def test_every_row_through_pass2(dev, V):
     x = base.to(dev)[:, :V]
     ids = torch.arange(n, dtype=torch.int64)
     for p, mp in ((0.95, 0.0), (0.5, 0.0), (1.0, 0.05)):
-        ops._ffi.call("skyrl_tune", b"topp_probe", 5)
-        try:
+        with ops.variant(topp_probe=5):
             tf, lf, ff = _run(x, True, temperature=1.0, top_p=p, min_p=mp, seed=4, seq_ids=ids.to(dev), step=9)
-        finally:
-            ops._ffi.call("skyrl_tune", b"topp_probe", 0)
         ts, ls, fs = _run(x, False, temperature=1.0, top_p=p, min_p=mp, seed=4, seq_ids=ids.to(dev), step=9)
         assert torch.equal(tf, ts), (V, p, mp, int((tf != ts).sum()))
         assert torch.allclose(lf, ls, atol=2e-5, rtol=1e-5)
@@ -222,11 +216,8 @@ def test_pass2_state_across_batch_sizes(dev):
     x = torch.empty((512, V), dtype=torch.bfloat16, device=dev).normal_(0, 3, generator=g)
     ids = torch.arange(512, dtype=torch.int64, device=dev)
     for k, (n, probe) in enumerate(((512, 5), (300, 0), (5, 5), (512, 0), (64, 5), (300, 5), (7, 0))):
-        ops._ffi.call("skyrl_tune", b"topp_probe", probe)
-        try:
+        with ops.variant(topp_probe=probe):
             tf, lf, ff = _run(x[:n], True, temperature=1.0, top_p=0.9, seed=8, seq_ids=ids[:n], step=k)
-        finally:
-            ops._ffi.call("skyrl_tune", b"topp_probe", 0)
         ts, ls, _ = _run(x[:n], False, temperature=1.0, top_p=0.9, seed=8, seq_ids=ids[:n], step=k)
         assert torch.equal(tf, ts), (n, probe, int((tf != ts).sum()))
         assert bool((ff[:, 2] == _ROW_DONE).all()), (n, probe)

@@ -107,17 +107,12 @@ def test_policy_train_per_vocab(dev, V, temp):
     params = ppo_utils.ppo_params_from_config(cfg, use_kl_loss=True, use_entropy_loss=True, has_entropy=True)
     outs = []
     for split, resident in ((1, 1), (0, 1), (0, 0)):
-        ops._ffi.call("skyrl_tune", b"train_split", split)
-        ops._ffi.call("skyrl_tune", b"train_resident", resident)
-        try:
+        with ops.variant(train_split=split, train_resident=resident):
             full = logits.to(dev).requires_grad_(True)
             x = full[:, -R - 1:-1]
             loss, m, lp, ent = ops.policy_train(x, labels.to(dev), old.to(dev), adv.to(dev), mask.to(dev), params,
                                                 ref_log_probs=ref.to(dev), temperature=temp)
             (loss * 1.5).backward()
-        finally:
-            ops._ffi.call("skyrl_tune", b"train_resident", 1)
-            ops._ffi.call("skyrl_tune", b"train_split", 1)
         outs.append((loss.detach(), m.clone(), lp, ent, full.grad))
     for a, b in zip(outs[1], outs[2]):  # resident vs two-sweep: the same per-thread order
         close(a, b, atol=1e-6, rtol=1e-5)
