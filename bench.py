@@ -57,13 +57,16 @@ QWEN_1_5B_PARAMS = 1_543_714_304  # Qwen2.5-1.5B, tied embeddings
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def SAMPLER_LABEL(nrows):
-    """The T = 1 sampler kernel the library picks at this row count (csrc/sampler.hip splits_for:
-    below 256 rows a row is split over workgroups, at or above one 512-thread workgroup per row)."""
+def SAMPLER_LABEL(nrows, rollout="live"):
+    """The T = 1 sampler kernel(s) the library picks (csrc/sampler.hip launch_sample: at or above
+    256 rows one 512-thread workgroup per row, below it the wide split kernel)."""
+    if rollout == "live":
+        return ("skyrl_sample over the live decode batch (sample_kernel<bf16,3,512> one workgroup per row at >= 256 "
+                "live rows, sample_wide_kernel below: rows split over workgroups, every load in flight at once)")
     if nrows >= 256:
         return "skyrl_sample (sample_kernel<bf16,3,512>: T=1, one workgroup per row)"
-    return ("skyrl_sample (sample_kernel<bf16,1,256>: T=1 through the additive bound, split mode: each row over "
-            "several workgroups, last arriver merges)")
+    return ("skyrl_sample (sample_wide_kernel<false,6>: T=1, each row over several workgroups with every load in "
+            "flight at once, last arriver merges)")
 # reported beside frac, never instead of it: the guide's measured float4 copy (MI355X_MICROARCH.md,
 # "6.29 TB/s measured") for read+write kernels, and the read-only grid-stride stream our probe
 # measured on the box (7.0-7.1 TB/s, profiles/r03_rw_ceiling_probe2.log) for read-only kernels
@@ -252,13 +255,25 @@ def run(args):
         return logits[blk * mb * R:(blk + 1) * mb * R].view(mb, R, V)[: nseq] if not full else \
             logits[seq0 * R:(seq0 + nseq) * R].view(nseq, R, V)
 
-    # the rollout's sampled tokens / logprobs ([R, N] per decode step) become the ragged response
-    # CSR that pack consumes: token j of sequence n was sampled at decode step j - roff[n]
+    # decode slots. The rollout's decode batch holds the LIVE sequences (logits
+    # [num_live_seqs, V]): a sequence leaves after its last token, as vLLM's continuous batching
+    # does. Slot s holds trajectory order[s], longest response first, so decode step t samples
+    # slots [0, live[t]); --rollout all keeps every sequence in the batch for all R steps (the
+    # r01-r05 bench). The resident logits are indexed by slot for the rollout (synthetic values).
     roff = data["roff"]
+    rl_cpu = data["rlens"].cpu()
+    order = (torch.argsort(-rl_cpu, stable=True) if args.rollout == "live" else torch.arange(N)).to(dev)
+    slot_of = torch.empty_like(order)
+    slot_of[order] = torch.arange(N, device=dev)
+    srt = torch.sort(rl_cpu, descending=True).values
+    live = [int((srt > t).sum()) if args.rollout == "live" else N for t in range(R)]
+    # the rollout's sampled tokens / logprobs ([R, N] per decode step, by slot) become the ragged
+    # response CSR that pack consumes: token j of sequence n was sampled at decode step j - roff[n]
     tok_n = torch.repeat_interleave(torch.arange(N, device=dev), data["rlens"])
     tok_t = torch.arange(int(roff[-1]), device=dev) - roff[:-1][tok_n]
+    tok_s = slot_of[tok_n]
     # sampler keys are the global trajectory ids: a trajectory's tokens do not depend on the world size
-    seq_ids = torch.arange(N, device=dev, dtype=torch.int64) + (row0 if args.scaling == "strong" else rank * N)
+    seq_ids = (torch.arange(N, device=dev, dtype=torch.int64) + (row0 if args.scaling == "strong" else rank * N))[order]
     from skyrl_amd.config import SamplingParams
     from skyrl_amd.sampler import TokenSampler
 
@@ -298,14 +313,14 @@ def run(args):
             ptr, ld = (base_ptr + 2 * V * t, R * V) if full else (base_ptr + 2 * V * ((t * N) % (rows - N + 1)), V)
             if t % 64 == 0:  # event-timed in blocks of 64 back-to-back decode-step launches
                 sample_timer.begin()
-            sampler.step_ptr(ptr, ld, t, sh)
+            sampler.step_ptr(ptr, ld, t, sh, nseq=live[t])
             if t % 64 == 63 or t == R - 1:
                 sample_timer.end(t % 64 + 1)
         if opt is not None and not inflight:  # the previous step's all-gather overlapped the rollout
             opt.wait_weights()
         # ---- pack ragged rollout output into the padded training tensors
-        rtok = sampler.tokens[tok_t, tok_n]
-        rlp_sampled = sampler.logprobs[tok_t, tok_n]
+        rtok = sampler.tokens[tok_t, tok_s]
+        rlp_sampled = sampler.logprobs[tok_t, tok_s]
         seqs, att, rmask, rew, lmask, rlp, lrows, scores = ops.pack_experience(
             data["ptok"], data["poff"], rtok, roff, data["rew"], roff, data["lmask"],
             roff, rlp_sampled, roff, N=N, P=P_MAX, R=R, pad=0, pad_token_id=0, return_row_sums=True)
@@ -418,8 +433,9 @@ def run(args):
     # per-kernel roofline: algorithmic bytes per launch / average event-timed launch duration
     rows_per_launch = mb * R
     kernels = {}
+    sampled_rows = sum(live)  # per step: the live sequences of every decode step
     for name, tm, nbytes, launches_per_step, ceiling in (
-        (SAMPLER_LABEL(N), sample_timer, N * V * 2 + N * 16, R,
+        (SAMPLER_LABEL(N, args.rollout), sample_timer, sampled_rows * (V * 2 + 16) // R, R,
          CEILING_READ_GBS),
         ("skyrl_logprob_fwd (logprob_fwd_kernel<bf16>)", fwd_timer, rows_per_launch * (V * 2 + 8 + 4),
          2 * (N // mb) + (N // mb if args.unfused else 0), CEILING_READ_GBS),
@@ -476,6 +492,11 @@ def run(args):
             "prompts": N_GLOBAL // GROUP, "group": GROUP, "global_batch": N_GLOBAL, "seq_len": R,
             "prompt_len": P_MAX, "vocab": V, "micro_batch": mb, "parallelism": f"dp{world}",
             "rows_per_rank": N, "rank0_rows": [row0, row0 + N],
+            "rollout": ({"form": "live decode batch (continuous batching: a sequence leaves after its last token)",
+                         "sampled_rows_per_step": sampled_rows, "decode_steps": R, "first_live": live[0],
+                         "last_live": live[-1]} if args.rollout == "live" else
+                        {"form": "every sequence at every decode step", "sampled_rows_per_step": sampled_rows,
+                         "decode_steps": R}),
             "work_split": ("strong: one global batch of 512 trajectories, rank r takes rows [r*512/N, (r+1)*512/N) "
                            "(whole prompt groups; dispatch.py:122-141)" if args.scaling == "strong" else
                            "weak: every rank its own 512-trajectory batch"),
@@ -1044,6 +1065,9 @@ def main():
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--weight-sync", choices=("auto", "sync", "inflight"), default="auto",
                     help="auto: sync at 1 rank (config 2), inflight over DP ranks (configs 3/5)")
+    ap.add_argument("--rollout", choices=("live", "all"), default="all",
+                    help="live: each decode step samples the sequences still generating (continuous batching); "
+                         "all (default, the r01-r05 workload): every sequence at every one of the R steps")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--micro-batch", type=int, default=16)

@@ -2631,6 +2631,29 @@ constexpr int kMaxSplits = 64;
 constexpr int kWideNT = 512;
 constexpr int kWideVPT = 6;  // 16-B vectors per lane at most (24 VGPRs of packed logits)
 
+struct WideBest {
+    float s;
+    int i;
+    float x;
+};
+// Every element of a candidate vector (16-B bf16 logits w, elements v0..v0+7, group hash h) whose
+// additive bound reaches thr gets its exact score; the best (score desc, index asc) is kept.
+__device__ __attribute__((noinline)) WideBest wide_eval_vec(uint4 w, int v0, uint32_t h, float thr, float kT,
+                                                           float inv_t, uint32_t key2, WideBest b) {
+    uint16_t raw[8];
+    __builtin_memcpy(raw, &w, 16);
+    const float bits = noise_bits(h);
+    const float Eg = group_min_e(h);
+    for (int k = 0; k < 8; ++k) {
+        const float x = bf16_to_f32(raw[k]);
+        if (!(fmaf(bits, -kT, x) - thr < 0.f)) {
+            const float sc = noise_score(x, inv_t, v0 + k, h, Eg, key2);
+            if (better(sc, v0 + k, Best{b.s, b.i})) b = WideBest{sc, v0 + k, x};
+        }
+    }
+    return b;
+}
+
 template <bool GREEDY, int VPT>
 __global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_wide_kernel(
     const uint16_t* __restrict__ logits, int64_t ld, int V, int per_wg, float inv_t, uint64_t seed,
@@ -2714,50 +2737,50 @@ __global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(4))) vo
                 us = u;
             }
         }
-        auto consider = [&](float sc, int v, float x) {
-            if (better(sc, v, Best{best_s, best_i})) {
-                best_s = sc;
-                best_i = v;
-                best_x = x;
-            }
-        };
-        // seed: the exact score of the largest element of this lane's best-bounded vector
+        // seed: the exact score of the largest element of this lane's best-bounded vector (the
+        // vector selected first, so the exact score is one copy of the code)
+        uint4 ds = d[0];
+        uint32_t hs = h[0];
+        int v0s = vb + (int)threadIdx.x;
 #pragma unroll
-        for (int u = 0; u < VPT; ++u) {
-            if (u == us) {
-                float x[VEC];
-                unpack(d[u], x);
-                int kb = 0;
+        for (int u = 1; u < VPT; ++u) {
+            ds = u == us ? d[u] : ds;
+            hs = u == us ? h[u] : hs;
+            v0s = u == us ? vb + u * kWideNT + (int)threadIdx.x : v0s;
+        }
+        if (us >= 0) {
+            float x[VEC];
+            unpack(ds, x);
+            int kb = 0;
 #pragma unroll
-                for (int k = 1; k < VEC; ++k) kb = x[k] > x[kb] ? k : kb;
-                float xs = x[0];
+            for (int k = 1; k < VEC; ++k) kb = x[k] > x[kb] ? k : kb;
+            float xs = x[0];
 #pragma unroll
-                for (int k = 1; k < VEC; ++k) xs = k == kb ? x[k] : xs;
-                const int v = (vb + u * kWideNT + (int)threadIdx.x) * VEC + kb;
-                consider(noise_score(xs, inv_t, v, h[u], group_min_e(h[u]), key2), v, xs);
-            }
+            for (int k = 1; k < VEC; ++k) xs = k == kb ? x[k] : xs;
+            best_s = noise_score(xs, inv_t, v0s * VEC + kb, hs, group_min_e(hs), key2);
+            best_i = v0s * VEC + kb;
+            best_x = xs;
         }
         // the workgroup's best seed is the bar every wave filters against
-        const float wb = wave_max_uniform(best_s);
+        float bar = wave_max_uniform(best_s);
         __syncthreads();  // s_bar initialised
-        if (lane == 0 && wb > -INFINITY) __hip_atomic_fetch_max(&s_bar, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0 && bar > -INFINITY) __hip_atomic_fetch_max(&s_bar, bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __syncthreads();
-        const float bar = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar)));
-        const float thr = (bar - kNoiseC) * temp;
+        bar = fmaxf(bar, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar))));
+        float thr = (bar - kNoiseC) * temp;
 #pragma unroll
         for (int u = 0; u < VPT; ++u) {
             const bool cand = !(bnd[u] - thr < 0.f);  // (bnd = -inf for an empty slot: never)
             if (__builtin_amdgcn_ballot_w64(cand) == 0) continue;
-            if (cand) {
-                float x[VEC];
-                unpack(d[u], x);
-                const float bits = noise_bits(h[u]);
-                const float Eg = group_min_e(h[u]);
-                const int v0 = (vb + u * kWideNT + (int)threadIdx.x) * VEC;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k)
-                    if (!(fmaf(bits, -kT, x[k]) - thr < 0.f)) consider(noise_score(x[k], inv_t, v0 + k, h[u], Eg, key2), v0 + k, x[k]);
+            if (cand) {  // out of line: a rare path, one copy of the exact scoring
+                const WideBest r = wide_eval_vec(d[u], (vb + u * kWideNT + (int)threadIdx.x) * VEC, h[u], thr, kT, inv_t,
+                                                 key2, WideBest{best_s, best_i, best_x});
+                best_s = r.s;
+                best_i = r.i;
+                best_x = r.x;
             }
+            bar = fmaxf(bar, wave_max_uniform(best_s));  // the wave's own finds raise its filter
+            thr = (bar - kNoiseC) * temp;
         }
     }
     // wave fold on DPP, then the workgroup's waves in order
@@ -2920,7 +2943,7 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
             (nvec + cap - 1) / cap <= kMaxSplits) {
             int ns = (knobs().sampler_wide_wgs + nseq - 1) / nseq;
             ns = max(ns, (nvec + cap - 1) / cap);
-            ns = min(ns, min(kMaxSplits, nvec));
+            ns = min(ns, min(kMaxSplits, (nvec + 2 * kWideNT - 1) / (2 * kWideNT)));  // >= 2 vectors per lane
             const int per_wg = (nvec + ns - 1) / ns;
             ns = (nvec + per_wg - 1) / per_wg;  // every split non-empty
             const dim3 grid(nseq, ns);

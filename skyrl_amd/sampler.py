@@ -45,11 +45,16 @@ class TokenSampler:
         self._tok_ptr, self._lp_ptr = self.tokens.data_ptr(), self.logprobs.data_ptr()
         self._err = _ffi.load().skyrl_last_error
 
-    def step_ptr(self, logits_ptr: int, row_stride: int, t: int, stream_handle: int):
+    def step_ptr(self, logits_ptr: int, row_stride: int, t: int, stream_handle: int, nseq: Optional[int] = None):
         """Lowest-overhead form for decode loops: raw device address of row 0 of step t's
-        [nseq, V] logits, row stride in elements, and the hipStream_t handle."""
+        [nseq, V] logits, row stride in elements, and the hipStream_t handle. `nseq` (default all):
+        the live sequences of this step, the first nseq of the sampler's (a continuous batch whose
+        finished sequences have left; their slots keep their earlier outputs)."""
         p = self.params
-        args = (logits_ptr, self.dtype_code, row_stride, self.nseq, self.vocab, float(p.temperature),
+        n = self.nseq if nseq is None else int(nseq)
+        if not 0 <= n <= self.nseq:
+            raise ValueError(f"nseq {n} outside [0, {self.nseq}]")
+        args = (logits_ptr, self.dtype_code, row_stride, n, self.vocab, float(p.temperature),
                 int(p.top_k if p.top_k is not None else -1), _top_p(p), float(p.min_p or 0.0),
                 ctypes.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), self._ids_ptr, int(t),
                 self._tok_ptr + 4 * self.nseq * t, self._lp_ptr + 4 * self.nseq * t, self._ws_ptr, stream_handle)
