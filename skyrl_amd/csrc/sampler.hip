@@ -512,6 +512,29 @@ struct TieSink {
     uint32_t kc;
 };
 
+// Exact scores of the slots in `needm` of one vector (elements v0 + k, group hash h): the best
+// (score desc; ascending k, so a strict '>' keeps the lowest index, as the caller's ascending visit
+// order requires) starting from b. Out of line: one copy of the exact scoring per kernel.
+struct Slots8 {
+    float v[8];
+};
+struct SlotBest {
+    float s;
+    int i;
+    float x;
+};
+__device__ __attribute__((noinline)) SlotBest eval_slots(Slots8 xs, unsigned needm, int v0, uint32_t h, float inv_t,
+                                                        uint32_t key2, SlotBest b) {
+    const float Eg = group_min_e(h);
+    for (int k = 0; k < 8; ++k) {
+        if ((needm >> k) & 1u) {
+            const float sc = noise_score(xs.v[k], inv_t, v0 + k, h, Eg, key2);
+            if (sc > b.s) b = SlotBest{sc, v0 + k, xs.v[k]};
+        }
+    }
+    return b;
+}
+
 template <typename T, int MODE, int NT, bool PRIO, bool TIES = false>
 __device__ __forceinline__ void sample_unit(
     const T* __restrict__ logits, int64_t ld, int V, int chunk, float inv_t, int use_topk_rt,
@@ -591,28 +614,23 @@ __device__ __forceinline__ void sample_unit(
     // Every element of a candidate vector that can still reach the bar through the group bound
     // (the additive form per element; a tie with the bar is evaluated). Unrolled over the slots:
     // a slot's block runs only when some lane needs it (usually one or two per candidate vector).
+    // The exact scoring runs out of line (eval_slots, one copy): inlined at every visit site it
+    // made the T > 0 kernels 51-53 KB of code against greedy's 9 KB, and a split-mode workgroup
+    // lives ~9 us, so instruction fetch was part of the race's fixed cost.
     auto eval_vec = [&](const float (&x)[VEC], const bool (&ok)[VEC], int v0, uint32_t h) {
         const float bits = (float)(int)__float_as_uint((float)(h >> 16));
-        bool need[VEC];
-        bool any = false;
+        unsigned needm = 0u;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            need[k] = ok[k] && !(fmaf(bits, -kT, x[k]) - thr < 0.f);
-            any = any || need[k];
-        }
-        if (!any) return;
-        const float Eg = group_e(h);
+        for (int k = 0; k < VEC; ++k)
+            if (ok[k] && !(fmaf(bits, -kT, x[k]) - thr < 0.f)) needm |= 1u << k;
+        if (!needm) return;
+        Slots8 xs;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            if (need[k]) {
-                const float sc = exact(x[k], v0 + k, h, Eg);
-                if (sc > best_s) {  // ascending k within the lane's ascending visit order
-                    best_s = sc;
-                    best_i = v0 + k;
-                    best_x = x[k];
-                }
-            }
-        }
+        for (int k = 0; k < 8; ++k) xs.v[k] = k < VEC ? x[k] : 0.f;
+        const SlotBest r = eval_slots(xs, needm, v0, h, inv_t, key2, SlotBest{best_s, best_i, best_x});
+        best_s = r.s;
+        best_i = r.i;
+        best_x = r.x;
     };
     // MODE 3 (T == 1) bound in multiplicative form, reusing the lse exponentials ex = e^(x - m):
     // h16 <= 2^19 e^(xmax - bar + 0.01) <=> h16 <= exmax * Q, Q = 2^19 e^(m - bar + 0.01) per lane.
@@ -673,12 +691,13 @@ __device__ __forceinline__ void sample_unit(
             }
         }
         if (kb >= 0) {
-            const float sc = exact(xb, v0 + kb, h, group_e(h));
-            if (sc > best_s) {
-                best_s = sc;
-                best_i = v0 + kb;
-                best_x = xb;
-            }
+            Slots8 xs;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) xs.v[k] = k < VEC ? x[k] : 0.f;
+            const SlotBest r = eval_slots(xs, 1u << kb, v0, h, inv_t, key2, SlotBest{best_s, best_i, best_x});
+            best_s = r.s;
+            best_i = r.i;
+            best_x = r.x;
         }
         raise_bar();
     };
