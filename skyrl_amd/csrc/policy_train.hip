@@ -936,9 +936,17 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
     __syncthreads();
     const float L = s_g[0], glp = s_g[1], gent = s_g[2], H = s_g[3];
     const int lab_s = (lab >= 0 && lab < V) ? (int)lab + h - 8 * lo : -1;  // label's slot in this piece
+    const int lab_v = lab_s >= 0 ? lab_s >> 3 : -1, lab_j = lab_s & 7;
 #pragma unroll
     for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
     const float inv_t = HAS_T ? 1.f / temp : 1.f;
+    // dL/dz = glp (onehot - p) - gent p (logp + H) with logp = z - L and p = 2^((z - L) log2e):
+    //   gg = p (ca z + cb), ca = -gent, cb = -glp - gent (H - L); the label's element adds glp.
+    // Two packed fma, one exp2 and one multiply per element (the per-element label compare and the
+    // separate subtract / scale are gone): the sweep is less VALU per byte, which matters when the
+    // chip's clock drops under sustained HBM load (policy_train)
+    const float cy = -L * kLog2e;
+    const float ca = -gent, cb = -glp - gent * (H - L);
     uint4* ov = reinterpret_cast<uint4*>(out - h) + lo;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -946,14 +954,26 @@ __global__ __launch_bounds__(NT, W) void policy_train_split_kernel(
         if ((!EDGE && k < NV - 1) || idx < nq) {
             float x[8];
             unpack8(v[k], x);
-            const int v0 = idx * 8;
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 l2 = {kLog2e, kLog2e}, c2 = {cy, cy}, a2 = {ca, ca}, b2 = {cb, cb};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float lpv = tval(x[j]) - L;
-                const float pv = fast_exp2(lpv * kLog2e);
-                float gg = -glp * pv - gent * pv * (lpv + H);
-                if (v0 + j == lab_s) gg += glp;
-                x[j] = HAS_T ? gg * inv_t : gg;
+            for (int j = 0; j < 8; j += 2) {  // packed fma pairs (v_pk_fma_f32)
+                const f2 z = {tval(x[j]), tval(x[j + 1])};
+                const f2 y = __builtin_elementwise_fma(z, l2, c2);
+                const f2 t = __builtin_elementwise_fma(a2, z, b2);
+                const f2 pv = {fast_exp2(y.x), fast_exp2(y.y)};
+                const f2 g = pv * t;
+                x[j] = g.x;
+                x[j + 1] = g.y;
+            }
+            if (idx == lab_v) {  // one lane of the row
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j == lab_j) x[j] += glp;
+            }
+            if constexpr (HAS_T) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] *= inv_t;
             }
             const int sl = h - 8 * (lo + idx), sh = V + h - 8 * (lo + idx);
             if (!EDGE || (sl <= 0 && sh >= 8)) {
