@@ -71,7 +71,11 @@ __host__ __device__ __forceinline__ float group_min_e(uint32_t h) {
     const float ug = (float)(((t16 << 8) | ((h >> 8) & 0xffu)) | 1u) * kNoiseU24;
     return -det_ln(ug) * 0.125f;
 }
-__host__ __device__ __forceinline__ float noise_score(float xk, float inv_t, int v, uint32_t h, float Eg, uint32_t key2) {
+// Out of line: the exact score is needed for few elements (the bound filters the rest), and at
+// every call site inlined it made the T > 0 sampler kernels 2-5x the greedy kernel's code (51-108 KB:
+// instruction fetch in a ~10 us workgroup's life). The same instructions either way.
+inline __host__ __device__ __attribute__((noinline)) float noise_score(float xk, float inv_t, int v, uint32_t h, float Eg,
+                                                              uint32_t key2) {
     float E = Eg;
     if (((uint32_t)v & 7u) != (h & 7u)) {
         const uint32_t hu = hash32(key2 ^ ((uint32_t)v * 0x9e3779b1u));

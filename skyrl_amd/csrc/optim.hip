@@ -124,7 +124,9 @@ __global__ void adamw_plan_kernel(const float* __restrict__ sumsq, skyrl_adamw_p
 // (touched[p] = some rank's backward reached it since the last step): step[p] += 1 and
 // coef[2p..2p+1] = (-lr / bc1(step[p]), sqrt(bc2(step[p]))), or (0, 0) = leave p untouched.
 // PLAN_UNIFORM = every parameter touched and all counts equal (the update then runs the plain
-// loop on coef[0..1] as PLAN_STEP / PLAN_BC2SQRT).
+// loop on coef[0..1] as PLAN_STEP / PLAN_BC2SQRT). Otherwise (a parameter skipped once, or never
+// touched) the update reads one coefficient pair per 16-B vector and skips untouched vectors
+// without loading them; only vectors that straddle a parameter boundary go element by element.
 __global__ __launch_bounds__(kThreads) void adamw_seg_plan_kernel(const float* __restrict__ sumsq,
                                                                    skyrl_adamw_params hp,
                                                                    const int32_t* __restrict__ touched, int nparams,
@@ -217,6 +219,35 @@ __device__ void adamw_seg_loop(float* __restrict__ param, const float* __restric
     f32x4* v4 = reinterpret_cast<f32x4*>(exp_avg_sq);
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += stride) {
         int s = seg_of(sm, sm.tile_seg[(i << 2) / kSegTile], i << 2);
+        if (sm.start[s + 1] >= (i << 2) + 4) {
+            // the whole vector in one segment (all but the vectors that straddle a parameter
+            // boundary): one coefficient lookup; an untouched parameter's vector is neither loaded
+            // nor stored, so a step that skipped some parameters costs what the plain loop does
+            const int o = sm.owner[s];
+            const float st = sm.coef[2 * o], b2s = sm.coef[2 * o + 1];
+            if (b2s == 0.f) continue;
+            AdamPlan b = a;
+            b.step = st;
+            b.bc2s = b2s;
+            const f32x4 pv = p4[i];
+            const f32x4 gv = __builtin_nontemporal_load(g4 + i);
+            const f32x4 mv = m4[i];
+            const f32x4 vv = v4[i];
+            float p[4] = {pv.x, pv.y, pv.z, pv.w}, m[4] = {mv.x, mv.y, mv.z, mv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+            const float g[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) adam_elem(p[k], g[k], m[k], v[k], b);
+            p4[i] = f32x4{p[0], p[1], p[2], p[3]};
+            __builtin_nontemporal_store(f32x4{m[0], m[1], m[2], m[3]}, m4 + i);
+            __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, v4 + i);
+            if (SHADOW) {
+                uint2 sh;
+                sh.x = pack_bf16x2(p[0], p[1]);
+                sh.y = pack_bf16x2(p[2], p[3]);
+                reinterpret_cast<uint2*>(shadow)[i] = sh;
+            }
+            continue;
+        }
         const f32x4 pv = p4[i];
         const f32x4 gv = __builtin_nontemporal_load(g4 + i);
         const f32x4 mv = m4[i];
