@@ -13,17 +13,6 @@ from skyrl_amd import _ffi  # noqa: E402
 dev = torch.device("cuda", 0)
 keys = ("loss_bwd_us", "grpo_loss_deferred_us", "finish_us", "total_us", "in_launch_fold_total_us")
 out = {}
-if len(sys.argv) > 1 and sys.argv[1] == "nt":  # non-temporal dlogp stores x finish grid size (r03: no gain, knob removed)
-    for rep in range(2):
-        for nt in (0, 1):
-            for blocks in (256, 8):
-                _ffi.set_default_variant(loss_ntstore=nt)
-                _ffi.set_default_variant(loss_bwd_blocks=blocks)
-                r = bench.advantage_loss_leg(dev, 512, 1024)
-                print(f"nt {nt} blocks {blocks}:", {k: r[k] for k in keys}, flush=True)
-    _ffi.set_default_variant(loss_ntstore=0)
-    _ffi.set_default_variant(loss_bwd_blocks=256)
-    sys.exit(0)
 for rep in range(2):
     for mode in (0, 2, 3, 4):
         for blocks in (256,):

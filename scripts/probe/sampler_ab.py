@@ -1,8 +1,9 @@
 """A/B of a compile-time switch of the T > 0 sampler (sampler.hip), at 512 rows (row mode, the
 bench's decode step) and 64 / 128 rows (split mode) x V = 151,936 bf16, T = 1 and T = 0.7, top_p 0.95 at T = 1 and 0.6, and min_p 0.05: one
 capi.hip + sampler.hip library per value of AB_DEFINE (default SKYRL_LAZY_BAR) in AB_VALUES
-(default 0,1), interleaved rounds of 200 back-to-back launches, medians; the tokens of every
-value must be equal (the switches change speed only).
+(default 0,1), or one library per set of AB_SETS ("name:DEF=v,DEF2=w|name2:..."), interleaved
+rounds of 200 back-to-back launches, medians; the tokens of every value must be equal (the
+switches change speed only). Rows in AB_ROWS (default 64,128,512).
 Build: python scripts/probe/sampler_ab.py build; run (GPU): python scripts/probe/sampler_ab.py run"""
 import ctypes
 import json
@@ -14,18 +15,26 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(ROOT, "skyrl_amd", "csrc")
 DEF = os.environ.get("AB_DEFINE", "SKYRL_LAZY_BAR")
-VALS = [int(v) for v in os.environ.get("AB_VALUES", "0,1").split(",")]
+ROWS = [int(v) for v in os.environ.get("AB_ROWS", "64,128,512").split(",")]
+if os.environ.get("AB_SETS"):  # name:DEF=v,DEF2=w|name2:...
+    SETS = {}
+    for item in os.environ["AB_SETS"].split("|"):
+        name, defs = item.split(":")
+        SETS[name] = [f"-D{d}" for d in defs.split(",") if d]
+else:
+    SETS = {f"{DEF}{v}": [f"-D{DEF}={v}"] for v in os.environ.get("AB_VALUES", "0,1").split(",")}
+VALS = list(SETS)
 
 
 def lib_path(v):
-    return os.path.join(HERE, f"libab_{DEF}_{v}.so")
+    return os.path.join(HERE, f"libab_{v}.so")
 
 
 def build():
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-shared", "-Wno-unused-function",
              "-Wno-unused-parameter"]
     for v in VALS:
-        subprocess.run(["/opt/rocm/bin/hipcc", *flags, f"-D{DEF}={v}", os.path.join(CSRC, "capi.hip"),
+        subprocess.run(["/opt/rocm/bin/hipcc", *flags, *SETS[v], os.path.join(CSRC, "capi.hip"),
                         os.path.join(CSRC, "sampler.hip"), "-o", lib_path(v)], check=True)
         print("built", lib_path(v))
 
@@ -45,7 +54,7 @@ def run():
     for rnd in range(5):
         for v, lib in libs.items():
             lib.skyrl_sample_workspace_bytes.restype = ctypes.c_size_t
-            for n in (64, 128, 512):
+            for n in ROWS:
                 ws = torch.zeros(lib.skyrl_sample_workspace_bytes(n, V), dtype=torch.uint8, device=dev)
                 for temp, top_p, min_p in ((1.0, 1.0, 0.0), (0.7, 1.0, 0.0), (1.0, 0.95, 0.0), (0.6, 0.95, 0.0), (1.0, 1.0, 0.05)):
                     def call(t):
@@ -64,7 +73,7 @@ def run():
                         call(t)
                     b.record(s)
                     b.synchronize()
-                    out.setdefault(f"n{n}_T{temp}_p{top_p}_m{min_p}_{DEF}{v}", []).append(a.elapsed_time(b) / 200 * 1e3)
+                    out.setdefault(f"n{n}_T{temp}_p{top_p}_m{min_p}_{v}", []).append(a.elapsed_time(b) / 200 * 1e3)
     res = {k: round(sorted(x)[len(x) // 2], 2) for k, x in out.items()}
     res["tokens_equal"] = all(all(torch.equal(d[VALS[0]], d[v]) for v in VALS) for d in toks.values())
     print(json.dumps(res), flush=True)

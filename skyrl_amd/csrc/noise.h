@@ -71,11 +71,10 @@ __host__ __device__ __forceinline__ float group_min_e(uint32_t h) {
     const float ug = (float)(((t16 << 8) | ((h >> 8) & 0xffu)) | 1u) * kNoiseU24;
     return -det_ln(ug) * 0.125f;
 }
-// Out of line: the exact score is needed for few elements (the bound filters the rest), and at
-// every call site inlined it made the T > 0 sampler kernels 2-5x the greedy kernel's code (51-108 KB:
-// instruction fetch in a ~10 us workgroup's life). The same instructions either way.
-inline __host__ __device__ __attribute__((noinline)) float noise_score(float xk, float inv_t, int v, uint32_t h, float Eg,
-                                                              uint32_t key2) {
+// score = x/T - ln E_v of element v (group hash h, group minimum Eg); the body, for a caller that
+// keeps ONE inlined site (a loop over candidates) instead of a call
+__host__ __device__ __forceinline__ float noise_score_inl(float xk, float inv_t, int v, uint32_t h, float Eg,
+                                                          uint32_t key2) {
     float E = Eg;
     if (((uint32_t)v & 7u) != (h & 7u)) {
         const uint32_t hu = hash32(key2 ^ ((uint32_t)v * 0x9e3779b1u));
@@ -83,6 +82,23 @@ inline __host__ __device__ __attribute__((noinline)) float noise_score(float xk,
         E = Eg + (-det_ln(U));
     }
     return xk * inv_t + (-det_ln(E));
+}
+// Out of line: the exact score is needed for few elements (the bound filters the rest), and at
+// every call site inlined it made the T > 0 sampler kernels 2-5x the greedy kernel's code (51-108 KB:
+// instruction fetch in a ~10 us workgroup's life). The same instructions either way. (A call
+// saves the caller's live VGPRs to scratch, so a kernel with many values in registers keeps one
+// inlined site of noise_score_inl instead.)
+#ifndef SKYRL_NOISE_INLINE  // probe builds (scripts/probe/sampler_ab.py) A/B the inlining
+#define SKYRL_NOISE_INLINE 0
+#endif
+#if SKYRL_NOISE_INLINE
+#define SKYRL_NOISE_ATTR __attribute__((always_inline))
+#else
+#define SKYRL_NOISE_ATTR __attribute__((noinline))
+#endif
+inline __host__ __device__ SKYRL_NOISE_ATTR float noise_score(float xk, float inv_t, int v, uint32_t h, float Eg,
+                                                              uint32_t key2) {
+    return noise_score_inl(xk, inv_t, v, h, Eg, key2);
 }
 // Group bound: an element of group hash h can reach an exact score `bar` only if
 //   xmax - (T ln2 2^-23) bits(float(h >> 16)) >= (bar - kNoiseC) T     (see sample_kernel)

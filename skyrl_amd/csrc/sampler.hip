@@ -523,15 +523,27 @@ struct SlotBest {
     int i;
     float x;
 };
-__device__ __attribute__((noinline)) SlotBest eval_slots(Slots8 xs, unsigned needm, int v0, uint32_t h, float inv_t,
-                                                        uint32_t key2, SlotBest b) {
+__device__ SKYRL_NOISE_ATTR SlotBest eval_slots(Slots8 xs, unsigned needm, int v0, uint32_t h, float inv_t,
+                                                uint32_t key2, SlotBest b) {
     const float Eg = group_min_e(h);
+#if SKYRL_NOISE_INLINE == 2  // one copy of the scoring per site: a loop over the needed slots
+    for (unsigned m = needm; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        const float x01 = (k & 1) ? xs.v[1] : xs.v[0], x23 = (k & 1) ? xs.v[3] : xs.v[2];
+        const float x45 = (k & 1) ? xs.v[5] : xs.v[4], x67 = (k & 1) ? xs.v[7] : xs.v[6];
+        const float x03 = (k & 2) ? x23 : x01, x47 = (k & 2) ? x67 : x45;
+        const float x = (k & 4) ? x47 : x03;
+        const float sc = noise_score_inl(x, inv_t, v0 + k, h, Eg, key2);
+        if (sc > b.s) b = SlotBest{sc, v0 + k, x};  // ascending k: a strict '>' keeps the lowest index
+    }
+#else
     for (int k = 0; k < 8; ++k) {
         if ((needm >> k) & 1u) {
             const float sc = noise_score(xs.v[k], inv_t, v0 + k, h, Eg, key2);
             if (sc > b.s) b = SlotBest{sc, v0 + k, xs.v[k]};
         }
     }
+#endif
     return b;
 }
 
@@ -2648,33 +2660,19 @@ constexpr int kMaxSplits = 64;
 // sample_kernel / oracle/sampler_ref.c; the filter only skips elements whose exact score is
 // provably below one already found. bf16, V % 8 == 0, 16-B aligned rows, no filters.
 constexpr int kWideNT = 512;
-constexpr int kWideVPT = 6;  // 16-B vectors per lane at most (24 VGPRs of packed logits)
+constexpr int kWideVPT = 12;  // 16-B vectors per lane at most (48 VGPRs of packed logits; 20 spills)
 
-struct WideBest {
-    float s;
-    int i;
-    float x;
-};
-// Every element of a candidate vector (16-B bf16 logits w, elements v0..v0+7, group hash h) whose
-// additive bound reaches thr gets its exact score; the best (score desc, index asc) is kept.
-__device__ __attribute__((noinline)) WideBest wide_eval_vec(uint4 w, int v0, uint32_t h, float thr, float kT,
-                                                           float inv_t, uint32_t key2, WideBest b) {
-    uint16_t raw[8];
-    __builtin_memcpy(raw, &w, 16);
-    const float bits = noise_bits(h);
-    const float Eg = group_min_e(h);
-    for (int k = 0; k < 8; ++k) {
-        const float x = bf16_to_f32(raw[k]);
-        if (!(fmaf(bits, -kT, x) - thr < 0.f)) {
-            const float sc = noise_score(x, inv_t, v0 + k, h, Eg, key2);
-            if (better(sc, v0 + k, Best{b.s, b.i})) b = WideBest{sc, v0 + k, x};
-        }
-    }
-    return b;
+// a = this lane's bit of m set ? a : b, as one v_cndmask the compiler cannot fold: a chain of
+// `t == u ? d[t] : w` selects over a register array is otherwise turned back into a dynamically
+// indexed load, which puts the whole array in scratch
+__device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
 }
 
 template <bool GREEDY, int VPT>
-__global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(4))) void sample_wide_kernel(
+__global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(VPT > 6 ? 2 : 4))) void sample_wide_kernel(
     const uint16_t* __restrict__ logits, int64_t ld, int V, int per_wg, float inv_t, uint64_t seed,
     const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens, float* __restrict__ logp_out,
     Part* __restrict__ parts, unsigned* __restrict__ counters) {
@@ -2756,29 +2754,55 @@ __global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(4))) vo
                 us = u;
             }
         }
-        // seed: the exact score of the largest element of this lane's best-bounded vector (the
-        // vector selected first, so the exact score is one copy of the code)
-        uint4 ds = d[0];
-        uint32_t hs = h[0];
-        int v0s = vb + (int)threadIdx.x;
+        // One inlined site of the exact score (noise_score_inl) for the seed and every candidate: a
+        // call would save the VPT packed vectors to scratch around it. Work item j of a lane is a
+        // vector u (selected, not indexed: a dynamic index would put d[] in scratch) and its
+        // slots in `need`; item 0 is the seed (the largest element of the best-bounded vector).
+        auto pick = [&](int u, uint4& w, uint32_t& hu, int& v0) {
+            w = d[0];
+            hu = h[0];
 #pragma unroll
-        for (int u = 1; u < VPT; ++u) {
-            ds = u == us ? d[u] : ds;
-            hs = u == us ? h[u] : hs;
-            v0s = u == us ? vb + u * kWideNT + (int)threadIdx.x : v0s;
-        }
+            for (int t = 1; t < VPT; ++t) {
+                const uint64_t mk = __builtin_amdgcn_ballot_w64(t == u);
+                w.x = lane_sel(mk, d[t].x, w.x);
+                w.y = lane_sel(mk, d[t].y, w.y);
+                w.z = lane_sel(mk, d[t].z, w.z);
+                w.w = lane_sel(mk, d[t].w, w.w);
+                hu = lane_sel(mk, h[t], hu);
+            }
+            v0 = (vb + u * kWideNT + (int)threadIdx.x) * VEC;
+        };
+        auto slot = [](const uint4& w, int k) -> float {  // bf16 k of a packed vector, k dynamic
+            const uint32_t lo = (k & 2) ? ((k & 4) ? w.w : w.y) : ((k & 4) ? w.z : w.x);
+            return __uint_as_float((k & 1) ? (lo & 0xffff0000u) : (lo << 16));
+        };
+        auto eval = [&](const uint4& w, uint32_t hu, int v0, unsigned need) {
+            const float Eg = group_min_e(hu);
+            for (unsigned m = need; m; m &= m - 1) {
+                const int k = __builtin_ctz(m);
+                const float x = slot(w, k);
+                const float sc = noise_score_inl(x, inv_t, v0 + k, hu, Eg, key2);
+                if (better(sc, v0 + k, Best{best_s, best_i})) {
+                    best_s = sc;
+                    best_i = v0 + k;
+                    best_x = x;
+                }
+            }
+        };
         if (us >= 0) {
-            float x[VEC];
-            unpack(ds, x);
+            uint4 w;
+            uint32_t hu;
+            int v0;
+            pick(us, w, hu, v0);
             int kb = 0;
+            float xb = slot(w, 0);
 #pragma unroll
-            for (int k = 1; k < VEC; ++k) kb = x[k] > x[kb] ? k : kb;
-            float xs = x[0];
-#pragma unroll
-            for (int k = 1; k < VEC; ++k) xs = k == kb ? x[k] : xs;
-            best_s = noise_score(xs, inv_t, v0s * VEC + kb, hs, group_min_e(hs), key2);
-            best_i = v0s * VEC + kb;
-            best_x = xs;
+            for (int k = 1; k < VEC; ++k) {
+                const float x = slot(w, k);
+                kb = x > xb ? k : kb;
+                xb = fmaxf(xb, x);
+            }
+            eval(w, hu, v0, 1u << kb);
         }
         // the workgroup's best seed is the bar every wave filters against
         float bar = wave_max_uniform(best_s);
@@ -2787,19 +2811,30 @@ __global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(4))) vo
         __syncthreads();
         bar = fmaxf(bar, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar))));
         float thr = (bar - kNoiseC) * temp;
+        auto cands = [&]() {  // vectors whose bound reaches thr (bnd = -inf for an empty slot: never)
+            unsigned c = 0u;
 #pragma unroll
-        for (int u = 0; u < VPT; ++u) {
-            const bool cand = !(bnd[u] - thr < 0.f);  // (bnd = -inf for an empty slot: never)
-            if (__builtin_amdgcn_ballot_w64(cand) == 0) continue;
-            if (cand) {  // out of line: a rare path, one copy of the exact scoring
-                const WideBest r = wide_eval_vec(d[u], (vb + u * kWideNT + (int)threadIdx.x) * VEC, h[u], thr, kT, inv_t,
-                                                 key2, WideBest{best_s, best_i, best_x});
-                best_s = r.s;
-                best_i = r.i;
-                best_x = r.x;
+            for (int u = 0; u < VPT; ++u) c |= (!(bnd[u] - thr < 0.f) ? 1u : 0u) << u;
+            return c;
+        };
+        unsigned cm = cands();
+        while (__builtin_amdgcn_ballot_w64(cm != 0u) != 0) {
+            if (cm) {
+                const int u = __builtin_ctz(cm);
+                cm &= cm - 1;
+                uint4 w;
+                uint32_t hu;
+                int v0;
+                pick(u, w, hu, v0);
+                const float bits = noise_bits(hu);
+                unsigned need = 0u;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) need |= (!(fmaf(bits, -kT, slot(w, k)) - thr < 0.f) ? 1u : 0u) << k;
+                eval(w, hu, v0, need);
             }
             bar = fmaxf(bar, wave_max_uniform(best_s));  // the wave's own finds raise its filter
             thr = (bar - kNoiseC) * temp;
+            cm &= cands();
         }
     }
     // wave fold on DPP, then the workgroup's waves in order
@@ -2974,7 +3009,9 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
                 if (greedy) SKYRL_WIDE(true, 2); else SKYRL_WIDE(false, 2);
             } else if (per_wg <= 4 * kWideNT) {
                 if (greedy) SKYRL_WIDE(true, 4); else SKYRL_WIDE(false, 4);
-            } else {
+            } else if (per_wg <= 6 * kWideNT) {
+                if (greedy) SKYRL_WIDE(true, 6); else SKYRL_WIDE(false, 6);
+            } else {  // fewer, longer workgroups (sampler_wide_wgs < 512)
                 if (greedy) SKYRL_WIDE(true, kWideVPT); else SKYRL_WIDE(false, kWideVPT);
             }
 #undef SKYRL_WIDE

@@ -3,6 +3,13 @@
 #pragma once
 #include "common.h"
 
+#ifndef SKYRL_WIDE_ROWS_DEFAULT  // probe builds (scripts/probe/sampler_ab.py) A/B the routing
+#define SKYRL_WIDE_ROWS_DEFAULT 256
+#endif
+#ifndef SKYRL_WIDE_WGS_DEFAULT
+#define SKYRL_WIDE_WGS_DEFAULT 512
+#endif
+
 namespace skyrl {
 
 struct Knobs {
@@ -26,8 +33,8 @@ struct Knobs {
     int sampler_split_gran = 8192;
     int sampler_topk_fast = 1;
     int sampler_topp_fast = 1;
-    int sampler_wide_rows = 256;
-    int sampler_wide_wgs = 512;
+    int sampler_wide_rows = SKYRL_WIDE_ROWS_DEFAULT;
+    int sampler_wide_wgs = SKYRL_WIDE_WGS_DEFAULT;
     int topp_probe = 0;
     int lmhead_pipe = 12;
     int lmhead_group = 8;
@@ -35,8 +42,12 @@ struct Knobs {
 };
 inline constexpr Knobs kDefaultKnobs{};
 
-// the variant of the running call (the defaults outside *_ex calls)
-const Knobs& knobs();
+// the variant of the running call (the defaults outside *_ex calls); header-inline so that a
+// probe build of one kernel file links without variant.hip
+namespace detail {
+inline thread_local const Knobs* tl_knobs = nullptr;
+}  // namespace detail
+inline const Knobs& knobs() { return detail::tl_knobs ? *detail::tl_knobs : kDefaultKnobs; }
 
 // installs a validated variant for the lifetime of one *_ex call
 class VariantScope {

@@ -9,11 +9,7 @@
 #include <string>
 
 namespace skyrl {
-namespace {
-thread_local const Knobs* tl_knobs = nullptr;
-}  // namespace
-
-const Knobs& knobs() { return tl_knobs ? *tl_knobs : kDefaultKnobs; }
+using detail::tl_knobs;
 
 int VariantScope::enter(const skyrl_variant* v) {
     prev_ = tl_knobs;
