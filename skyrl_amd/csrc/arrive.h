@@ -1,13 +1,25 @@
-// Last-arriver election for in-launch reductions (gfx950, 8 XCDs with private L2s).
+// Last-arriver hand-offs for in-launch reductions (gfx950, 8 XCDs with private L2s).
 //
-// Producer side (guide: split-K seam, write-through form): the block's partial record is
-// stored WRITE-THROUGH with agent-scope relaxed atomic stores (global_store ... sc1) by
-// the single storing thread, which then drains (s_waitcnt vmcnt(0)) and draws a ticket
-// with a relaxed agent-scope fetch_add. No release fence: a per-block buffer_wbl2 over
-// thousands of workgroups was the dominant cost (SQ_WAIT_ANY 82% of wave cycles in the
-// sampler). The block drawing the last ticket does one agent-scope ACQUIRE (invalidates
-// this CU's L1) before a block barrier, then reads every partial, and re-arms the counter.
-// The counter lives in caller-owned workspace zeroed once at allocation.
+// Producer side, every form (MI355X_MICROARCH.md, "Valid forms", split-K seam, write-through):
+// the block's (or wave's) partial record is stored WRITE-THROUGH with agent-scope relaxed atomic
+// stores (global_store ... sc1, st_wt below) by ONE lane, which then drains them
+// (s_waitcnt vmcnt(0)) and draws a ticket with a relaxed agent-scope fetch_add on one counter.
+// No release fence: a per-block buffer_wbl2 over thousands of workgroups was the dominant cost
+// (SQ_WAIT_ANY 82 % of wave cycles in the sampler). The counter lives in caller-owned workspace
+// zeroed once at allocation; the consumer re-arms it (rearm).
+//
+// Consumer side: the workgroup (or wave) whose add returned total - 1 reads every record with
+// agent-scope relaxed loads (global_load ... sc1) after ONE agent acquire (buffer_inv sc1 +
+// vmcnt(0)): arrive_last() for block-level records, handoff_acquire() where the merging wave
+// tested the ticket itself (the sampler's split merge, the fused pass's plan and fold). The
+// guide's row 1 would allow the sc1 loads without the acquire, but it was measured at one
+// workgroup per CU; these launches put several on a CU, so the acquire stays. The
+// sc1 form alone is still what the tests exercise hardest: tests/test_gpu_sampler_splits.py runs
+// every split shape for many decode steps against the oracle's tokens (a stale record would show
+// as a wrong token or logprob), and the fold / plan tests compare every micro-batch's loss.
+#ifndef SKYRL_HANDOFF_ACQUIRE  // probe builds A/B its cost
+#define SKYRL_HANDOFF_ACQUIRE 1
+#endif
 #pragma once
 #include "common.h"
 
@@ -32,6 +44,14 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total, i
     }
     __syncthreads();
     return *lds_flag != 0;
+}
+
+// the merging wave's acquire before it loads the other producers' records (see the header)
+__device__ __forceinline__ void handoff_acquire() {
+#if SKYRL_HANDOFF_ACQUIRE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 
 __device__ __forceinline__ void rearm(unsigned* counter) {

@@ -83,13 +83,14 @@ __host__ __device__ __forceinline__ float noise_score_inl(float xk, float inv_t,
     }
     return xk * inv_t + (-det_ln(E));
 }
-// Out of line: the exact score is needed for few elements (the bound filters the rest), and at
-// every call site inlined it made the T > 0 sampler kernels 2-5x the greedy kernel's code (51-108 KB:
-// instruction fetch in a ~10 us workgroup's life). The same instructions either way. (A call
-// saves the caller's live VGPRs to scratch, so a kernel with many values in registers keeps one
-// inlined site of noise_score_inl instead.)
+// Inlined (SKYRL_NOISE_INLINE 2, the product): r06 tried the exact score out of line to shrink
+// the T > 0 kernels' code (51-108 KB vs greedy's 9 KB), and every T > 0 launch got slower (512 /
+// 64 / 1 rows at T = 1: 32.5 -> 39.7, 14.5 -> 20.4, 8.9 -> 13.8 us; profiles/r06_sampler_inline_ab.json):
+// a callee starts with s_waitcnt vmcnt(0), so each call drained the loads the streaming loop had
+// in flight. The callers keep the code small instead with one inlined copy of the scoring per
+// visit site (a loop over the slots that need it; eval_slots in sampler.hip).
 #ifndef SKYRL_NOISE_INLINE  // probe builds (scripts/probe/sampler_ab.py) A/B the inlining
-#define SKYRL_NOISE_INLINE 0
+#define SKYRL_NOISE_INLINE 2
 #endif
 #if SKYRL_NOISE_INLINE
 #define SKYRL_NOISE_ATTR __attribute__((always_inline))

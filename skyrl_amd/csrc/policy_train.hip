@@ -336,6 +336,7 @@ __global__ __launch_bounds__(kStepRows * kWave) void train_plan_kernel(
     }
     prev = __builtin_amdgcn_readfirstlane(prev);
     if (prev != (unsigned)n - 1u) return;
+    handoff_acquire();
     // the micro-batch's last row: total in row order, scalars, tag, token_mean scales
     for (int j0 = 0; j0 < n; j0 += kWave) {
         const float v = j0 + lane < n ? __hip_atomic_load(rsum + r0 + j0 + lane, __ATOMIC_RELAXED,
@@ -688,8 +689,8 @@ constexpr int kSplitMaxP = 12;  // most pieces per row of any built shape (split
 // (s_memrealtime): partners are consecutive blocks, resident or next to be dispatched, and
 // publish within microseconds; past this bound (other streams' kernels holding the CUs, a grid
 // larger than what is resident) the piece computes the partner's state itself (no deadlock, no
-// error path, the same bits)
-constexpr unsigned kSplitWaitTicks = 5000u;  // 50 us (the variant field train_split_wait = ticks for tests)
+// error path, the same bits). The bound is knobs().train_split_wait (default 5000 ticks = 50 us;
+// tests shorten it through the variant).
 
 typedef __attribute__((address_space(1))) unsigned long long ptr_gu64;
 typedef __attribute__((address_space(1))) unsigned ptr_gu32;
@@ -1132,6 +1133,7 @@ __global__ __launch_bounds__(kStepRows * kWave) void train_fold_kernel(
     }
     prev = __builtin_amdgcn_readfirstlane(prev);
     if (prev != (unsigned)n - 1u) return;
+    handoff_acquire();
     RowRec tot{0.0, 0.0, 0.0, 0.0, 0.0};
     for (int j0 = 0; j0 < n; j0 += kWave) {
         double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1248,7 +1250,7 @@ constexpr SplitShape kSplitShapes[] = {
     {5, 256, 4},     // 4
     {6, 256, 5},     // 5
 };
-constexpr int kSplitShapeCount = sizeof(kSplitShapes) / sizeof(kSplitShapes[0]);
+static_assert(sizeof(kSplitShapes) / sizeof(kSplitShapes[0]) == 6, "variant.hip accepts train_split_shape 0..5");
 SplitKernel split_for(int nv, bool has_t, int shape, bool edge) {
     if (edge) {  // EDGE forms are built for the power-of-two shapes only
         switch (shape) {

@@ -514,7 +514,8 @@ struct TieSink {
 
 // Exact scores of the slots in `needm` of one vector (elements v0 + k, group hash h): the best
 // (score desc; ascending k, so a strict '>' keeps the lowest index, as the caller's ascending visit
-// order requires) starting from b. Out of line: one copy of the exact scoring per kernel.
+// order requires) starting from b. Inlined, with one copy of the scoring per site (a loop over
+// the needed slots): a call would drain the caller's loads in flight (noise.h).
 struct Slots8 {
     float v[8];
 };
@@ -624,11 +625,8 @@ __device__ __forceinline__ void sample_unit(
     // exact score of element v of the group with hash h and minimum E_g
     auto exact = [&](float xk, int v, uint32_t h, float Eg) -> float { return noise_score(xk, inv_t, v, h, Eg, key2); };
     // Every element of a candidate vector that can still reach the bar through the group bound
-    // (the additive form per element; a tie with the bar is evaluated). Unrolled over the slots:
-    // a slot's block runs only when some lane needs it (usually one or two per candidate vector).
-    // The exact scoring runs out of line (eval_slots, one copy): inlined at every visit site it
-    // made the T > 0 kernels 51-53 KB of code against greedy's 9 KB, and a split-mode workgroup
-    // lives ~9 us, so instruction fetch was part of the race's fixed cost.
+    // (the additive form per element; a tie with the bar is evaluated): eval_slots loops over the
+    // slots some bound could not rule out (usually one or two per candidate vector).
     auto eval_vec = [&](const float (&x)[VEC], const bool (&ok)[VEC], int v0, uint32_t h) {
         const float bits = (float)(int)__float_as_uint((float)(h >> 16));
         unsigned needm = 0u;
@@ -1021,6 +1019,7 @@ __device__ __forceinline__ void sample_unit(
         }
         __syncthreads();
         if (!s_last || threadIdx.x >= kWave) return;
+        handoff_acquire();
         Part q{-INFINITY, 0x7fffffff, -1e30f, 0.f, 0.f};  // identity for lanes past nsplit
         if (lane < nsplit) {
             const float* src = reinterpret_cast<const float*>(parts + (int64_t)row_i * nsplit + lane);
@@ -2861,6 +2860,7 @@ __global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(VPT > 6
         }
         __syncthreads();
         if (!s_last || threadIdx.x >= kWave) return;
+        handoff_acquire();
         Part q{-INFINITY, 0x7fffffff, -1e30f, 0.f, 0.f};
         if (lane < nsplit) {
             const float* src = reinterpret_cast<const float*>(parts + (int64_t)row_i * nsplit + lane);

@@ -4,7 +4,7 @@
 #include "common.h"
 
 #ifndef SKYRL_WIDE_ROWS_DEFAULT  // probe builds (scripts/probe/sampler_ab.py) A/B the routing
-#define SKYRL_WIDE_ROWS_DEFAULT 256
+#define SKYRL_WIDE_ROWS_DEFAULT 0  // the wide kernel is an A/B variant: slower
 #endif
 #ifndef SKYRL_WIDE_WGS_DEFAULT
 #define SKYRL_WIDE_WGS_DEFAULT 512
