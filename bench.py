@@ -59,14 +59,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 def SAMPLER_LABEL(nrows, rollout="live"):
     """The T = 1 sampler kernel(s) the library picks (csrc/sampler.hip launch_sample: at or above
-    256 rows one 512-thread workgroup per row, below it the wide split kernel)."""
+    256 rows one 512-thread workgroup per row, below it the split form of the same kernel)."""
     if rollout == "live":
         return ("skyrl_sample over the live decode batch (sample_kernel<bf16,3,512> one workgroup per row at >= 256 "
-                "live rows, sample_wide_kernel below: rows split over workgroups, every load in flight at once)")
+                "live rows, sample_kernel<bf16,3,256> below: rows split over workgroups, last arriver merges)")
     if nrows >= 256:
         return "skyrl_sample (sample_kernel<bf16,3,512>: T=1, one workgroup per row)"
-    return ("skyrl_sample (sample_wide_kernel<false,6>: T=1, each row over several workgroups with every load in "
-            "flight at once, last arriver merges)")
+    return ("skyrl_sample (sample_kernel<bf16,3,256>: T=1, each row over several 256-thread workgroups, last "
+            "arriver merges)")
 # reported beside frac, never instead of it: the guide's measured float4 copy (MI355X_MICROARCH.md,
 # "6.29 TB/s measured") for read+write kernels, and the read-only grid-stride stream our probe
 # measured on the box (7.0-7.1 TB/s, profiles/r03_rw_ceiling_probe2.log) for read-only kernels

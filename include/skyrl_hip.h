@@ -83,8 +83,6 @@ typedef struct skyrl_variant {
     int32_t sampler_split_gran;  /* multiple of 2048 in [2048, 65536]: split chunk granule (elements) */
     int32_t sampler_topk_fast;   /* {0, 1}: top_k <= 128 through the one-pass kernel */
     int32_t sampler_topp_fast;   /* {0, 1, 2}: top_p / min_p through the one-pass kernel (2: always) */
-    int32_t sampler_wide_rows;   /* [0, 1024]: unfiltered bf16 batches below this take the wide split kernel */
-    int32_t sampler_wide_wgs;    /* [1, 8192]: workgroups a wide launch aims at */
     int32_t topp_probe;          /* {0 .. 7, 11}: top_p timing probes (0 = product) */
     int32_t lmhead_pipe;         /* -1 default or 0..14: K pipeline of the lm_head MFMA GEMM */
     int32_t lmhead_group;        /* [0, 4096): M tiles per group of its tile order (0 = all) */

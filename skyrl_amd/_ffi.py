@@ -85,7 +85,7 @@ VARIANT_FIELDS = (
     "logprob_unroll", "logprob_nt", "train_resident", "train_resident_nt", "train_ntstore", "train_split",
     "train_split_shape", "train_split_wait", "grpo_slices", "loss_units", "loss_bwd_blocks", "grpo_loss_rpb",
     "finish_mode", "sampler_row", "sampler_split_rows", "sampler_split_wgs", "sampler_split_nt", "sampler_split_gran",
-    "sampler_topk_fast", "sampler_topp_fast", "sampler_wide_rows", "sampler_wide_wgs", "topp_probe", "lmhead_pipe",
+    "sampler_topk_fast", "sampler_topp_fast", "topp_probe", "lmhead_pipe",
     "lmhead_group", "attn_pf")
 VARIANT_DEFAULT = -(2 ** 31)  # SKYRL_VARIANT_DEFAULT
 

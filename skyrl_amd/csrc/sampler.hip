@@ -35,8 +35,7 @@ namespace skyrl {
 // this), sampler_split_wgs (workgroups a split launch aims at: 4 per CU at 256 threads),
 // sampler_split_nt (threads per split workgroup), sampler_split_gran (split chunks are multiples of
 // this many elements), sampler_topk_fast (0 = top_k on the pre-pass + MODE 2 kernels),
-// sampler_wide_rows / sampler_wide_wgs (unfiltered bf16 batches below this many rows take the wide
-// split kernel, aiming at this many workgroups; 0 rows: never), sampler_topp_fast (0 = top_p / min_p
+// sampler_topp_fast (0 = top_p / min_p
 // alone on the pre-pass + MODE 2 kernels; 1 = the one-pass kernel, except min_p without top_p below
 // the row-mode batch, where the pre-pass and the split MODE 2 sampler measured faster (32 / 64 / 128
 // rows: 26.2 / 33.0 / 43.2 vs 43.8 / 44.8 / 47.4 us; 256 rows: 68.1 vs 49.6; same tokens;
@@ -2645,243 +2644,6 @@ __global__ __launch_bounds__(kPNT) void sample_topp_pass2_kernel(
 
 constexpr int kMaxSplits = 64;
 
-// ---- wide split (r06): few rows, every load of a workgroup in flight at once ------------------
-// The per-rank decode batch of a DP job (64 rows at 8 GPUs) is 19 MB per step: the streaming
-// split kernel above runs it as a latency chain (first loads drained, a seeding round, then
-// two more load round trips, the fold, the hand-off; phase probe DESIGN §3). Here each
-// 512-thread workgroup owns a contiguous chunk of at most kWideVPT x 512 16-B vectors of one
-// row and issues ALL of its loads before the first wait: one memory round trip per workgroup.
-// Then, from registers: the raw max and sum-exp (logprob), per vector the group hash and the
-// additive bound, the exact score of the best-bounded vector's largest element as this lane's
-// seed, the workgroup's best seed as the bar (one LDS max, one barrier), the exact scores of
-// every element the bound cannot rule out, and the same wave / workgroup fold and last-arriver
-// merge as the split kernel. Decisions are the exact-score argmax (lowest index on ties) of
-// sample_kernel / oracle/sampler_ref.c; the filter only skips elements whose exact score is
-// provably below one already found. bf16, V % 8 == 0, 16-B aligned rows, no filters.
-constexpr int kWideNT = 512;
-constexpr int kWideVPT = 12;  // 16-B vectors per lane at most (48 VGPRs of packed logits; 20 spills)
-
-// a = this lane's bit of m set ? a : b, as one v_cndmask the compiler cannot fold: a chain of
-// `t == u ? d[t] : w` selects over a register array is otherwise turned back into a dynamically
-// indexed load, which puts the whole array in scratch
-__device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-    return r;
-}
-
-template <bool GREEDY, int VPT>
-__global__ __launch_bounds__(kWideNT) __attribute__((amdgpu_waves_per_eu(VPT > 6 ? 2 : 4))) void sample_wide_kernel(
-    const uint16_t* __restrict__ logits, int64_t ld, int V, int per_wg, float inv_t, uint64_t seed,
-    const int64_t* __restrict__ seq_ids, int64_t step, int32_t* __restrict__ tokens, float* __restrict__ logp_out,
-    Part* __restrict__ parts, unsigned* __restrict__ counters) {
-    constexpr int NW = kWideNT / kWave;
-    constexpr int VEC = 8;
-    __shared__ Part s_part[NW];
-    __shared__ float s_bar;
-    __shared__ int s_last;
-    const int row_i = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int nvec = V / VEC;
-    const int vb = split * per_wg;
-    const int ve = min(nvec, vb + per_wg);
-    const uint4* rv = reinterpret_cast<const uint4*>(logits + (int64_t)row_i * ld);
-    // every load first (clamped indices: unconditional, no per-load branch or wait)
-    uint4 d[VPT];
-#pragma unroll
-    for (int u = 0; u < VPT; ++u) d[u] = ld_stream(rv + min(vb + u * kWideNT + (int)threadIdx.x, ve - 1));
-    if (!GREEDY && threadIdx.x == 0) s_bar = -INFINITY;
-    const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
-    const uint32_t key2 = noise_key2(key);
-    const uint32_t keyb = noise_keyb(key);
-    const float temp = GREEDY ? 1.f : 1.0f / inv_t;
-    const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
-    auto unpack = [](const uint4& w, float (&x)[VEC]) {
-        uint16_t raw[VEC];
-        __builtin_memcpy(raw, &w, 16);
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) x[k] = bf16_to_f32(raw[k]);
-    };
-    bool ok[VPT];
-    float vmax[VPT];
-    float m = -1e30f;  // finite start: an all -inf lane never forms inf - inf
-#pragma unroll
-    for (int u = 0; u < VPT; ++u) {
-        ok[u] = vb + u * kWideNT + (int)threadIdx.x < ve;
-        float x[VEC];
-        unpack(d[u], x);
-        float vm = x[0];
-#pragma unroll
-        for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, x[k]);
-        vmax[u] = ok[u] ? vm : -INFINITY;
-        m = fmaxf(m, vmax[u]);
-    }
-    float s = 0.f;
-    float best_s = -INFINITY, best_x = 0.f;
-    int best_i = 0x7fffffff;
-#pragma unroll
-    for (int u = 0; u < VPT; ++u) {
-        float x[VEC];
-        unpack(d[u], x);
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) acc += fast_exp2((x[k] - m) * kLog2e);
-        s += ok[u] ? acc : 0.f;
-        if constexpr (GREEDY) {  // first maximum in ascending index order
-            const int v0 = (vb + u * kWideNT + (int)threadIdx.x) * VEC;
-            if (ok[u] && vmax[u] > best_s) {
-                int kk = VEC - 1;
-#pragma unroll
-                for (int k = VEC - 2; k >= 0; --k) kk = (x[k] == vmax[u]) ? k : kk;
-                best_s = vmax[u];
-                best_i = v0 + kk;
-                best_x = vmax[u];
-            }
-        }
-    }
-    if constexpr (!GREEDY) {
-        uint32_t h[VPT];
-        float bnd[VPT];  // the vector can beat `bar` only if !(bnd - (bar - C) T < 0)
-        int us = -1;
-        float bs = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < VPT; ++u) {
-            h[u] = ehash(key, keyb, (uint32_t)(vb + u * kWideNT + (int)threadIdx.x));  // group = vector index
-            bnd[u] = ok[u] ? fmaf(noise_bits(h[u]), -kT, vmax[u]) : -INFINITY;
-            if (bnd[u] > bs) {
-                bs = bnd[u];
-                us = u;
-            }
-        }
-        // One inlined site of the exact score (noise_score_inl) for the seed and every candidate: a
-        // call would save the VPT packed vectors to scratch around it. Work item j of a lane is a
-        // vector u (selected, not indexed: a dynamic index would put d[] in scratch) and its
-        // slots in `need`; item 0 is the seed (the largest element of the best-bounded vector).
-        auto pick = [&](int u, uint4& w, uint32_t& hu, int& v0) {
-            w = d[0];
-            hu = h[0];
-#pragma unroll
-            for (int t = 1; t < VPT; ++t) {
-                const uint64_t mk = __builtin_amdgcn_ballot_w64(t == u);
-                w.x = lane_sel(mk, d[t].x, w.x);
-                w.y = lane_sel(mk, d[t].y, w.y);
-                w.z = lane_sel(mk, d[t].z, w.z);
-                w.w = lane_sel(mk, d[t].w, w.w);
-                hu = lane_sel(mk, h[t], hu);
-            }
-            v0 = (vb + u * kWideNT + (int)threadIdx.x) * VEC;
-        };
-        auto slot = [](const uint4& w, int k) -> float {  // bf16 k of a packed vector, k dynamic
-            const uint32_t lo = (k & 2) ? ((k & 4) ? w.w : w.y) : ((k & 4) ? w.z : w.x);
-            return __uint_as_float((k & 1) ? (lo & 0xffff0000u) : (lo << 16));
-        };
-        auto eval = [&](const uint4& w, uint32_t hu, int v0, unsigned need) {
-            const float Eg = group_min_e(hu);
-            for (unsigned m = need; m; m &= m - 1) {
-                const int k = __builtin_ctz(m);
-                const float x = slot(w, k);
-                const float sc = noise_score_inl(x, inv_t, v0 + k, hu, Eg, key2);
-                if (better(sc, v0 + k, Best{best_s, best_i})) {
-                    best_s = sc;
-                    best_i = v0 + k;
-                    best_x = x;
-                }
-            }
-        };
-        if (us >= 0) {
-            uint4 w;
-            uint32_t hu;
-            int v0;
-            pick(us, w, hu, v0);
-            int kb = 0;
-            float xb = slot(w, 0);
-#pragma unroll
-            for (int k = 1; k < VEC; ++k) {
-                const float x = slot(w, k);
-                kb = x > xb ? k : kb;
-                xb = fmaxf(xb, x);
-            }
-            eval(w, hu, v0, 1u << kb);
-        }
-        // the workgroup's best seed is the bar every wave filters against
-        float bar = wave_max_uniform(best_s);
-        __syncthreads();  // s_bar initialised
-        if (lane == 0 && bar > -INFINITY) __hip_atomic_fetch_max(&s_bar, bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __syncthreads();
-        bar = fmaxf(bar, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_bar))));
-        float thr = (bar - kNoiseC) * temp;
-        auto cands = [&]() {  // vectors whose bound reaches thr (bnd = -inf for an empty slot: never)
-            unsigned c = 0u;
-#pragma unroll
-            for (int u = 0; u < VPT; ++u) c |= (!(bnd[u] - thr < 0.f) ? 1u : 0u) << u;
-            return c;
-        };
-        unsigned cm = cands();
-        while (__builtin_amdgcn_ballot_w64(cm != 0u) != 0) {
-            if (cm) {
-                const int u = __builtin_ctz(cm);
-                cm &= cm - 1;
-                uint4 w;
-                uint32_t hu;
-                int v0;
-                pick(u, w, hu, v0);
-                const float bits = noise_bits(hu);
-                unsigned need = 0u;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) need |= (!(fmaf(bits, -kT, slot(w, k)) - thr < 0.f) ? 1u : 0u) << k;
-                eval(w, hu, v0, need);
-            }
-            bar = fmaxf(bar, wave_max_uniform(best_s));  // the wave's own finds raise its filter
-            thr = (bar - kNoiseC) * temp;
-            cm &= cands();
-        }
-    }
-    // wave fold on DPP, then the workgroup's waves in order
-    const Part wp = wave_reduce_part(Part{best_s, best_i, m, s, best_x});
-    if (lane == 0) s_part[threadIdx.x / kWave] = wp;
-    __syncthreads();
-    Part p;
-    if (threadIdx.x == 0) {
-        p = s_part[0];
-#pragma unroll
-        for (int j = 1; j < NW; ++j) part_merge(p, s_part[j]);
-    }
-    if (nsplit > 1) {  // split-mode hand-off (sample_unit): sc1 record, ticket, sc1 loads by the last
-        if (threadIdx.x == 0) {
-            float* dst = reinterpret_cast<float*>(parts + (int64_t)row_i * nsplit + split);
-            st_wt(dst + 0, p.score);
-            st_wt(reinterpret_cast<int*>(dst) + 1, p.idx);
-            st_wt(dst + 2, p.m);
-            st_wt(dst + 3, p.s);
-            st_wt(dst + 4, p.xb);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned prev = __hip_atomic_fetch_add(counters + row_i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = prev == (unsigned)nsplit - 1u;
-        }
-        __syncthreads();
-        if (!s_last || threadIdx.x >= kWave) return;
-        handoff_acquire();
-        Part q{-INFINITY, 0x7fffffff, -1e30f, 0.f, 0.f};
-        if (lane < nsplit) {
-            const float* src = reinterpret_cast<const float*>(parts + (int64_t)row_i * nsplit + lane);
-            q.score = __hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            q.idx = __hip_atomic_load(reinterpret_cast<const int*>(src) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            q.m = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            q.s = __hip_atomic_load(src + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            q.xb = __hip_atomic_load(src + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        p = wave_reduce_part(q);
-    }
-    if (threadIdx.x == 0) {
-        tokens[row_i] = p.idx;
-        if (logp_out) {
-            const float lse = p.m + fast_log2(p.s) * kLn2;
-            logp_out[row_i] = (p.idx >= 0 && p.idx < V) ? p.xb - lse : __builtin_nanf("");
-        }
-        if (nsplit > 1) rearm(counters + row_i);
-    }
-}
-
 // Splits per row: below knobs().sampler_split_rows rows the row is cut into chunks of a multiple of
 // knobs().sampler_split_gran elements (default 8192 = one full streaming iteration of a 256-thread
 // split, so every split runs the pipelined main loop, not the ragged-tail path) for about
@@ -2986,36 +2748,6 @@ int launch_sample(const void* logits, int64_t ld, int nseq, int V, float tempera
             hipLaunchKernelGGL((sample_topp_pass2_kernel<T, true>), dim3(nseq, kP2Splits), dim3(kPNT), 0, stream, lg, ld,
                                V, inv_t, seed, seq_ids, step, tokens, logp, filt, pend, pend_nt, pties, pparts);
             return check_launch("sample_topp_pass2_kernel");
-        }
-    }
-    // few unfiltered bf16 rows: the wide split kernel (every load of a workgroup in flight at once)
-    if constexpr (sizeof(T) == 2) {
-        const int nvec = V / 8;
-        const int cap = kWideNT * kWideVPT;
-        if (!use_topk && !use_minp && !use_topp && nseq < knobs().sampler_wide_rows && nseq < kMaxSplitRows &&
-            V % 8 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && ((ld * (int64_t)sizeof(T)) & 15) == 0 &&
-            (nvec + cap - 1) / cap <= kMaxSplits) {
-            int ns = (knobs().sampler_wide_wgs + nseq - 1) / nseq;
-            ns = max(ns, (nvec + cap - 1) / cap);
-            ns = min(ns, min(kMaxSplits, (nvec + 2 * kWideNT - 1) / (2 * kWideNT)));  // >= 2 vectors per lane
-            const int per_wg = (nvec + ns - 1) / ns;
-            ns = (nvec + per_wg - 1) / per_wg;  // every split non-empty
-            const dim3 grid(nseq, ns);
-            const uint16_t* lg16 = reinterpret_cast<const uint16_t*>(logits);
-#define SKYRL_WIDE(G, VP)                                                                                        \
-    hipLaunchKernelGGL((sample_wide_kernel<G, VP>), grid, dim3(kWideNT), 0, stream, lg16, ld, V, per_wg, inv_t, seed, \
-                       seq_ids, step, tokens, logp, parts, counters)
-            if (per_wg <= 2 * kWideNT) {
-                if (greedy) SKYRL_WIDE(true, 2); else SKYRL_WIDE(false, 2);
-            } else if (per_wg <= 4 * kWideNT) {
-                if (greedy) SKYRL_WIDE(true, 4); else SKYRL_WIDE(false, 4);
-            } else if (per_wg <= 6 * kWideNT) {
-                if (greedy) SKYRL_WIDE(true, 6); else SKYRL_WIDE(false, 6);
-            } else {  // fewer, longer workgroups (sampler_wide_wgs < 512)
-                if (greedy) SKYRL_WIDE(true, kWideVPT); else SKYRL_WIDE(false, kWideVPT);
-            }
-#undef SKYRL_WIDE
-            return check_launch("sample_wide_kernel");
         }
     }
     if (use_topk || use_minp || use_topp) {

@@ -3,13 +3,6 @@
 #pragma once
 #include "common.h"
 
-#ifndef SKYRL_WIDE_ROWS_DEFAULT  // probe builds (scripts/probe/sampler_ab.py) A/B the routing
-#define SKYRL_WIDE_ROWS_DEFAULT 0  // the wide kernel is an A/B variant: slower
-#endif
-#ifndef SKYRL_WIDE_WGS_DEFAULT
-#define SKYRL_WIDE_WGS_DEFAULT 512
-#endif
-
 namespace skyrl {
 
 struct Knobs {
@@ -33,8 +26,6 @@ struct Knobs {
     int sampler_split_gran = 8192;
     int sampler_topk_fast = 1;
     int sampler_topp_fast = 1;
-    int sampler_wide_rows = SKYRL_WIDE_ROWS_DEFAULT;
-    int sampler_wide_wgs = SKYRL_WIDE_WGS_DEFAULT;
     int topp_probe = 0;
     int lmhead_pipe = 12;
     int lmhead_group = 8;

@@ -56,8 +56,6 @@ int VariantScope::enter(const skyrl_variant* v) {
     SKYRL_TAKE(sampler_split_gran, [](int x) { return x >= 2048 && x <= 65536 && x % 2048 == 0; });
     SKYRL_TAKE(sampler_topk_fast, in(0, 1));
     SKYRL_TAKE(sampler_topp_fast, in(0, 2));
-    SKYRL_TAKE(sampler_wide_rows, in(0, 1024));
-    SKYRL_TAKE(sampler_wide_wgs, in(1, 8192));
     SKYRL_TAKE(topp_probe, [](int x) { return (x >= 0 && x <= 7) || x == 11; });
     SKYRL_TAKE(lmhead_pipe, in(-1, 14));
     SKYRL_TAKE(lmhead_group, in(0, 4095));
