@@ -213,12 +213,14 @@ def run(args):
         raise ValueError(f"{N} rows per rank are not a multiple of the micro-batch {mb}")
     log(f"rank {rank}/{world}: rows [{row0}, {row0 + N}) of a {N_GLOBAL}-trajectory global batch "
         f"({args.scaling} scaling{f', emulating rank {args.emulate_rank} of {emulate}' if emulate > 1 else ''})")
-    # weight-sync order: "sync" (config 2, colocated synchronous): the optimizer step runs on the
-    # compute stream and only the weight all-gather overlaps the next rollout; "inflight" (configs
-    # 3/5, DP over xGMI with in-flight learner -> rollout sync, fully_async_trainer.py:415-419):
-    # reduce-scatter + clip/AdamW + all-gather run on the comm stream under the next step's
-    # rollout and ref pass, and the learner waits for the new weights before its old-policy pass
-    inflight = args.weight_sync == "inflight" or (args.weight_sync == "auto" and world > 1)
+    # weight-sync order: "sync" (the default at every world size): the optimizer step runs on the
+    # compute stream and the next rollout waits for the weight all-gather, as the reference pauses
+    # generation for the sync (fully_async_trainer.py:415-419); "inflight" (opt-in): reduce-scatter
+    # + clip/AdamW + all-gather on the comm stream under the next step's rollout and ref pass, the
+    # old-policy pass waiting for the new weights. The inflight overlap rewrites the rollout
+    # weights during generation, so it stands for an engine with double-buffered rollout weights;
+    # with synthetic logits nothing here reads them.
+    inflight = args.weight_sync == "inflight"
 
     # a12/a14 learner state: flat fp32 gradient of the policy (written by the transformer backward,
     # outside the path: synthetic here), FSDP2-style sharded AdamW, bf16 rollout weights
@@ -308,6 +310,8 @@ def run(args):
         nonlocal upd_done
         # ---- rollout: R decode steps over [N, V] logits (row stride R*V in the resident tensor)
         sampler.seed = step_idx
+        if opt is not None and not inflight:  # generation starts on the previous step's new weights
+            opt.wait_weights()
         sh = torch.cuda.current_stream(dev).cuda_stream
         for t in range(R):
             ptr, ld = (base_ptr + 2 * V * t, R * V) if full else (base_ptr + 2 * V * ((t * N) % (rows - N + 1)), V)
@@ -316,8 +320,6 @@ def run(args):
             sampler.step_ptr(ptr, ld, t, sh, nseq=live[t])
             if t % 64 == 63 or t == R - 1:
                 sample_timer.end(t % 64 + 1)
-        if opt is not None and not inflight:  # the previous step's all-gather overlapped the rollout
-            opt.wait_weights()
         # ---- pack ragged rollout output into the padded training tensors
         rtok = sampler.tokens[tok_t, tok_s]
         rlp_sampled = sampler.logprobs[tok_t, tok_s]
@@ -501,9 +503,10 @@ def run(args):
                            "(whole prompt groups; dispatch.py:122-141)" if args.scaling == "strong" else
                            "weak: every rank its own 512-trajectory batch"),
             "weight_sync": ("inflight: reduce-scatter + clip/AdamW + all-gather on the comm stream under the next "
-                            "step's rollout and ref pass; the old-policy pass waits for the new weights"
-                            if inflight else "sync: optimizer on the compute stream, the weight all-gather "
-                            "overlapping the next rollout"),
+                            "step's rollout and ref pass; the old-policy pass waits for the new weights (an engine "
+                            "would need double-buffered rollout weights for this overlap)"
+                            if inflight else "sync: optimizer on the compute stream; the next step's rollout "
+                            "waits for the weight all-gather (the reference pauses generation for the sync)"),
             "logits_resident_rows": rows, "logits_full_batch_resident": full,
             "final_loss_sum_last_step": round(mvals[0], 6),
             "policy_params": args.params, "grad_bucket_mb": args.bucket_mb,
@@ -1064,7 +1067,8 @@ def main():
                     help="(one process) run one rank's share of a W-rank strong-scaling job, collectives excluded")
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--weight-sync", choices=("auto", "sync", "inflight"), default="auto",
-                    help="auto: sync at 1 rank (config 2), inflight over DP ranks (configs 3/5)")
+                    help="auto = sync: the next rollout waits for the new weights; inflight: the update "
+                         "overlaps the next rollout (needs double-buffered engine weights)")
     ap.add_argument("--rollout", choices=("live", "all"), default="all",
                     help="live: each decode step samples the sequences still generating (continuous batching); "
                          "all (default, the r01-r05 workload): every sequence at every one of the R steps")
