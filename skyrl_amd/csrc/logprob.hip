@@ -37,82 +37,45 @@ __global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(
     const int64_t b = r / nt, t = r % nt;
     const T* row = logits + b * sb + t * st_;
 
+    SoftState st;
+    state_init(st);
     const bool vec_ok = (reinterpret_cast<uintptr_t>(row) % 16) == 0;
-    const int nvec = vec_ok ? V / VEC : 0;
-    const uint4* rv = reinterpret_cast<const uint4*>(row);
-    auto load_x = [&](int i, float (&x)[VEC]) {
-        E::unpack(kNT ? ld_stream(rv + i) : rv[i], x);
-        if (has_t) {
+    int done = 0;
+    if (vec_ok) {
+        const int nvec = V / VEC;
+        const uint4* rv = reinterpret_cast<const uint4*>(row);
+        int i = lane;
+        for (; i + (kUnroll - 1) * kWave < nvec; i += kUnroll * kWave) {
+            uint4 v[kUnroll];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) x[k] = E::apply_t(x[k], temp, true);
-        }
-    };
-    // the tails (and the robust re-run): state_add per vector / element
-    auto tails = [&](SoftState& st, int i) {
-        for (; i < nvec; i += kWave) {
-            float x[VEC];
-            load_x(i, x);
-            state_add<VEC>(st, x);
-        }
-        for (int j = nvec * VEC + lane; j < V; j += kWave) {
-            float x[1] = {E::apply_t(E::load(row + j), temp, has_t)};
-            state_add<1>(st, x);
-        }
-    };
-    // Main loop: kUnroll vectors per lane per iteration, lean accumulation (softmax.h lean_add)
-    // against a lane offset m seeded from the lane's first iteration and raised only when an
-    // iteration's sum reaches 2^64
-    float m = -3.402823466e38f;
-    f32x2_t S = {0.f, 0.f}, W = {0.f, 0.f};
-    bool bad = false;
-    int i = lane;
-    bool seeded = false;
-    for (; i + (kUnroll - 1) * kWave < nvec; i += kUnroll * kWave) {
-        float x[kUnroll][VEC];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) load_x(i + u * kWave, x[u]);
-        auto iter_max = [&](float mx) {
+            for (int u = 0; u < kUnroll; ++u) v[u] = kNT ? ld_stream(rv + i + u * kWave) : rv[i + u * kWave];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
+                float x[VEC];
+                E::unpack(v[u], x);
+                if (has_t) {
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) mx = fmaxf(mx, x[u][k]);
+                    for (int k = 0; k < VEC; ++k) x[k] = E::apply_t(x[k], temp, true);
+                }
+                state_add<VEC>(st, x);
             }
-            return mx;
-        };
-        if (!seeded) {  // the lane's first iteration sets the offset
-            seeded = true;
-            m = iter_max(m);  // (an all -inf iteration keeps the finite floor)
         }
-        float c = -m * kLog2e;
-        LeanAcc a{{0.f, 0.f}, {0.f, 0.f}};
+        for (; i < nvec; i += kWave) {
+            float x[VEC];
+            E::unpack(kNT ? ld_stream(rv + i) : rv[i], x);
+            if (has_t) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) lean_add<VEC>(x[u], c, a);
-        if (!(a.s.x + a.s.y < 0x1p64f)) {  // would overflow (or NaN / +inf): re-offset once
-            const float mx = iter_max(m);
-            const float dy = (m - mx) * kLog2e;
-            const float sc = fast_exp2(dy);
-            W = sc * (W + dy * S);
-            S = sc * S;
-            m = mx;
-            c = -m * kLog2e;
-            a = LeanAcc{{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) lean_add<VEC>(x[u], c, a);
-            bad = bad || !(a.s.x + a.s.y < 0x1p64f);
+                for (int k = 0; k < VEC; ++k) x[k] = E::apply_t(x[k], temp, true);
+            }
+            state_add<VEC>(st, x);
         }
-        S += a.s;
-        W += a.w;
+        done = nvec * VEC;
     }
-    SoftState st{m, S.x + S.y, W.x + W.y};
-    tails(st, i);
+    for (int i = done + lane; i < V; i += kWave) {
+        float x[1] = {E::apply_t(E::load(row + i), temp, has_t)};
+        state_add<1>(st, x);
+    }
     st = wave_merge(st);
-    // a -inf logit (0 * -inf in W), a NaN or +inf one, or an offset that could not absorb an
-    // iteration: the row again with the per-element clamped state (the reference's values)
-    if (__builtin_amdgcn_ballot_w64(bad) != 0 || !(fabsf(st.w) <= 3.402823466e38f) || !(st.s <= 3.402823466e38f)) {
-        state_init(st);
-        tails(st, lane);
-        st = wave_merge(st);
-    }
     if (lane == 0) {
         const float logs = fast_log2(st.s) * kLn2;
         const float lse = st.m + logs;

@@ -81,32 +81,6 @@ __device__ __forceinline__ void state_add(SoftState& st, const float (&x)[K]) {
     }
 }
 
-// Lean accumulation for the streaming main loops (r06): y = x log2(e) + c against a lane offset
-// c = -m log2(e) that moves only when an iteration would overflow, in packed fp32 pairs
-// (v_pk_fma / v_pk_add), with no running max and no clamp per element. Per 8 bf16: 4 pk_fma +
-// 8 exp + 4 pk_add + 4 pk_fma against state_add's per-element max, clamp, fma, add, fma and the
-// per-vector rescale. Under sustained HBM load the chip clocks down to ~1.4 GHz, and there
-// state_add's VALU work, not the bytes, set the logprob pass's time (profiles/r06_pmc_clock.json).
-// A -inf logit gives 0 * -inf = NaN in w: the caller re-runs such a row with state_add.
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-struct LeanAcc {
-    f32x2_t s, w;
-};
-template <int K>
-__device__ __forceinline__ void lean_add(const float (&x)[K], float c, LeanAcc& a) {
-    static_assert(K % 2 == 0, "pairs");
-    const f32x2_t l2 = {kLog2e, kLog2e};
-    const f32x2_t c2 = {c, c};
-#pragma unroll
-    for (int k = 0; k < K; k += 2) {
-        const f32x2_t x2 = {x[k], x[k + 1]};
-        const f32x2_t y = __builtin_elementwise_fma(x2, l2, c2);
-        const f32x2_t e = {fast_exp2(y.x), fast_exp2(y.y)};
-        a.s += e;
-        a.w = __builtin_elementwise_fma(e, y, a.w);
-    }
-}
-
 __device__ __forceinline__ void state_merge(SoftState& a, const SoftState& b) {
     const float mn = fmaxf(a.m, b.m);
     const float da = fmaxf((a.m - mn) * kLog2e, kDLow), db = fmaxf((b.m - mn) * kLog2e, kDLow);
