@@ -49,7 +49,8 @@ const char* skyrl_last_error(void);
  * skyrl_policy_train_plan / _micro_fwd / _fold; 9: per-parameter AdamW,
  * skyrl_adamw_seg_plan / _seg_update / _seg_tile, skyrl_debug_occupy, skyrl_policy_train_plan_grpo;
  * 10: skyrl_adv_norm_stats / _apply; 11: skyrl_tune and skyrl_debug_occupy removed, per-call
- * kernel variants through skyrl_variant and the *_ex entry points). */
+ * kernel variants through skyrl_variant and the *_ex entry points; 12: skyrl_variant.lmhead_persist,
+ * the persistent learner lm_head forward). */
 int skyrl_abi_version(void);
 /* ---- kernel variants, per call ---------------------------------------------------------------
  * Every entry point runs the tuned kernels. The *_ex forms (declared after each family) take a
@@ -87,6 +88,7 @@ typedef struct skyrl_variant {
     int32_t lmhead_pipe;         /* -1 default or 0..14: K pipeline of the lm_head MFMA GEMM */
     int32_t lmhead_group;        /* [0, 4096): M tiles per group of its tile order (0 = all) */
     int32_t attn_pf;             /* {0 default, 4, 6, 8}: K/V blocks in flight per D = 128 decode wave */
+    int32_t lmhead_persist;      /* [0, 4]: learner lm_head forward on the persistent tile kernel (0: off; 1..4 copy placement) */
 } skyrl_variant;
 /* Fills every field with SKYRL_VARIANT_DEFAULT (a pure function of its argument). */
 void skyrl_variant_init(skyrl_variant* v);

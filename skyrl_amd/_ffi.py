@@ -86,7 +86,7 @@ VARIANT_FIELDS = (
     "train_split_shape", "train_split_wait", "grpo_slices", "loss_units", "loss_bwd_blocks", "grpo_loss_rpb",
     "finish_mode", "sampler_row", "sampler_split_rows", "sampler_split_wgs", "sampler_split_nt", "sampler_split_gran",
     "sampler_topk_fast", "sampler_topp_fast", "topp_probe", "lmhead_pipe",
-    "lmhead_group", "attn_pf")
+    "lmhead_group", "attn_pf", "lmhead_persist")
 VARIANT_DEFAULT = -(2 ** 31)  # SKYRL_VARIANT_DEFAULT
 
 

@@ -24,4 +24,4 @@ int check_launch(const char* what) {
 
 extern "C" const char* skyrl_last_error(void) { return skyrl::g_last_error.c_str(); }
 
-extern "C" int skyrl_abi_version(void) { return 11; }
+extern "C" int skyrl_abi_version(void) { return 12; }

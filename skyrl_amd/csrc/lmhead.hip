@@ -30,15 +30,6 @@ struct __align__(16) ChunkState {
     float m, s, w, xl;
 };
 
-__device__ __forceinline__ void finalize_row(const SoftState& st, float xl, int64_t r, float* __restrict__ logp_out,
-                                             float* __restrict__ ent_out, float* __restrict__ lse_out) {
-    const float logs = fast_log2(st.s) * kLn2;
-    const float lse = st.m + logs;
-    logp_out[r] = xl - lse;  // NaN for a label outside [0, V), as logprob.hip
-    if (ent_out) ent_out[r] = logs - kLn2 * (st.w / st.s);
-    if (lse_out) lse_out[r] = lse;
-}
-
 __global__ __launch_bounds__(kThreads) void lmhead_fwd_kernel(
     const uint16_t* __restrict__ z, int64_t ldz, int T, int vc, int64_t v0, const int64_t* __restrict__ labels,
     int64_t lstride, float temp, bool has_t, ChunkState* __restrict__ state, int first, int last,

@@ -1001,6 +1001,388 @@ __global__ __launch_bounds__(64) void lmhead_sample_merge_kernel(const float4* _
     }
 }
 
+// LDS store / load of 16 B by inline asm: the compiler puts s_waitcnt vmcnt(0) in front of any LDS
+// access it can see while an LDS-DMA copy may be in flight, which would drain the next steps'
+// copies at the epilogue; these the caller orders itself (lgkmcnt waits + barriers)
+__device__ __forceinline__ void lds_st16(float4* p, f32x4 v) {
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)p;
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 lds_ld16(const float4* p) {
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)(const char*)p;
+    f32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+
+// ---- learner forward, persistent form (the default of skyrl_lmhead_logprob_fwd) ---------------
+// One 512-thread workgroup per CU walks the tiles q = i nwg + wg of the grouped order (wg in the
+// XCD-contiguous numbering, so in every round an XCD's 32 workgroups hold 8 M tiles x 4 N tiles of
+// one group) with ONE K pipeline across its tiles: global step g = i nk + t stages H in LDS stage
+// g & 1 and W in stage g % 3 (pipe 12's staging: H(g + 1) and W(g + 2) in flight while step g
+// computes), so the next tile's first copies are in flight through this tile's last steps and its
+// epilogue instead of after it.
+// The MFMAs take the operands swapped (A = the W fragment, B = the H fragment), so lane l of wave
+// (wm, wn) holds, for each of its 8 tokens m0 + 128 wm + 16 tb + (l & 15), the 16 columns
+// n0 + 64 wn + 16 vb + 4 (l >> 4) + r (vb, r < 4). The epilogue runs from registers (no LDS image):
+// the bf16 logits of a token's 16 columns fold into one (m, S, W) state per lane, two xor merges
+// join the lane groups, and the four column waves' states meet in the H stage the last step read (a
+// 16 KB scratch until step g + 1 restages it), merged in wn order by one thread per token into the
+// tile's state. The label logit is not taken here: lmhead_label_merge_kernel recomputes it with the
+// same MFMA chain, bit for bit.
+// CP (skyrl_variant lmhead_persist - 1): where a wave issues its 8 copies of a step: 0 all right
+// after the step's barrier; 1 the second wave of each SIMD (waves 4-7) after its first four MFMA
+// groups; 2 one copy per MFMA group; 3 role split: waves 0-3 copy all of H(g + 1) after the
+// barrier, waves 4-7 all of W(g + 2) after their first four MFMA groups.
+template <bool HAS_T, int CP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_logprob_pkernel(
+    const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
+    int mt, int nt, int gm, float temp, float4* __restrict__ parts) {
+    using G = Geo<256, 64, 2>;
+    constexpr int kT = 32768, kWBase = 2 * kT, kRow = 128;
+    __shared__ __attribute__((aligned(16))) char smem[163840];
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int ntiles = mt * nt;
+    const int my = wg < ntiles ? (ntiles - 1 - wg) / nwg + 1 : 0;
+    if (my == 0) return;
+    const int nk = K / 64;  // >= 2 (host)
+    const int nsteps = my * nk;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = w & 1, wn = w >> 1;
+    auto tile_mn = [&](int i, int& mtile, int& ntile) {
+        const int qq = min(i, my - 1) * nwg + wg;
+        if (gm <= 0 || gm >= mt) {
+            mtile = qq % mt;
+            ntile = qq / mt;
+        } else {
+            const int per = gm * nt, gi = qq / per, r = qq - gi * per, gsz = min(gm, mt - gi * gm);
+            mtile = gi * gm + r % gsz;
+            ntile = r / gsz;
+        }
+    };
+    // Staging: a step's copies are 16 pieces of 8 rows x 128 B per operand (lane -> row lane >> 3,
+    // 16-B chunk lane & 7 holding logical chunk (lane & 7) ^ swz(row)). CP 0-2: wave w copies H
+    // rows and W rows 32 w .. 32 w + 31 (4 pieces each); CP 3 (role split): waves 0-3 copy H only
+    // and waves 4-7 W only, rows 64 (w & 3) .. + 63 (8 pieces). Offsets are 32-bit element offsets
+    // of the current (oc) and the next (ox) tile (the host takes this path only when M ldh,
+    // N ldw < 2^31); CP 0-2 keep H in [0, 4) and W in [4, 8).
+    constexpr bool SPLIT = CP == 3;
+    const bool hrole = !SPLIT || __builtin_amdgcn_readfirstlane(w) < 4;  // SPLIT: this wave copies H
+    int srow[8], scol[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        srow[j] = SPLIT ? (w & 3) * 64 + j * 8 + (lane >> 3) : (w * 4 + (j & 3)) * 8 + (lane >> 3);
+        scol[j] = ((lane & 7) ^ G::swz(srow[j])) * 8;
+    }
+    uint32_t oc[8], ox[8];
+    auto offs = [&](int i, uint32_t (&o)[8]) {
+        int mtile, ntile;
+        tile_mn(i, mtile, ntile);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool isw = SPLIT ? !hrole : j >= 4;
+            o[j] = isw ? (uint32_t)min(ntile * 256 + srow[j], N - 1) * (uint32_t)ldw + (uint32_t)scol[j]
+                       : (uint32_t)min(mtile * BM + srow[j], M - 1) * (uint32_t)ldh + (uint32_t)scol[j];
+        }
+    };
+    // LDS byte offset of this wave's piece j inside a stage
+    auto pdst = [&](int j) { return SPLIT ? ((w & 3) * 8 + j) * 1024 : (w * 4 + (j & 3)) * 1024; };
+    // piece j: an H piece of step g + 1 or a W piece of step g + 2 (when those steps exist)
+    auto copy_piece = [&](auto j_tag, int g, int t, int hs, int ws) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_tag)::value;
+        const bool isw = SPLIT ? !hrole : j >= 4;
+        if (!isw) {
+            if (g + 1 >= nsteps) return;
+            const bool cur = t + 1 < nk;
+            __builtin_amdgcn_global_load_lds((gbl_void*)(H + (cur ? oc[j] : ox[j]) + (cur ? t + 1 : 0) * 64),
+                                             (lds_void*)(smem + (hs ^ 1) * kT + pdst(j)), 16, 0, 0);
+        } else {
+            if (g + 2 >= nsteps) return;
+            const bool cur = t + 2 < nk;
+            const int w2 = ws == 0 ? 2 : ws - 1;  // (g + 2) % 3
+            __builtin_amdgcn_global_load_lds((gbl_void*)(W + (cur ? oc[j] : ox[j]) + (cur ? t + 2 : t + 2 - nk) * 64),
+                                             (lds_void*)(smem + kWBase + w2 * kT + pdst(j)), 16, 0, 0);
+        }
+    };
+    // the prologue's copies: phase 0 H(0) and W(0), phase 1 W(1) (every W(1) piece after every
+    // W(0) piece, so the top of step 0 may leave exactly the W(1) pieces outstanding)
+    auto copy0 = [&](auto j_tag, int phase) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_tag)::value;
+        const bool isw = SPLIT ? !hrole : j >= 4;
+        if (!isw) {
+            if (phase == 0) __builtin_amdgcn_global_load_lds((gbl_void*)(H + oc[j]), (lds_void*)(smem + pdst(j)), 16, 0, 0);
+        } else if (phase == 0) {
+            __builtin_amdgcn_global_load_lds((gbl_void*)(W + oc[j]), (lds_void*)(smem + kWBase + pdst(j)), 16, 0, 0);
+        } else if (nsteps > 1) {
+            __builtin_amdgcn_global_load_lds((gbl_void*)(W + oc[j] + 64), (lds_void*)(smem + kWBase + kT + pdst(j)), 16, 0, 0);
+        }
+    };
+    auto copy_all = [&](int g, int t, int hs, int ws) __attribute__((always_inline)) {
+        copy_piece(std::integral_constant<int, 0>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 1>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 2>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 3>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 4>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 5>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 6>{}, g, t, hs, ws);
+        copy_piece(std::integral_constant<int, 7>{}, g, t, hs, ws);
+    };
+    // CP 1: the second wave of each SIMD copies mid-step; CP 3: the W waves do
+    const bool late = (CP == 1 && __builtin_amdgcn_readfirstlane(w) >= 4) || (SPLIT && !hrole);
+    int aoff[2], boff[2];
+    {
+        const int sw = G::swz(lane & 15);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c = (ks * 4 + (lane >> 4)) ^ sw;
+            aoff[ks] = (wm * 128 + (lane & 15)) * kRow + c * 16;
+            boff[ks] = kWBase + (wn * 64 + (lane & 15)) * kRow + c * 16;
+        }
+    }
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    offs(0, oc);
+    offs(1, ox);
+    int mtile, ntile;
+    tile_mn(0, mtile, ntile);
+#pragma unroll
+    for (int phase = 0; phase < 2; ++phase) {
+        copy0(std::integral_constant<int, 0>{}, phase);
+        copy0(std::integral_constant<int, 1>{}, phase);
+        copy0(std::integral_constant<int, 2>{}, phase);
+        copy0(std::integral_constant<int, 3>{}, phase);
+        copy0(std::integral_constant<int, 4>{}, phase);
+        copy0(std::integral_constant<int, 5>{}, phase);
+        copy0(std::integral_constant<int, 6>{}, phase);
+        copy0(std::integral_constant<int, 7>{}, phase);
+    }
+    int i = 0, t = 0, hs = 0, ws = 0;
+    bool stored = false;  // this wave issued the previous step's state store (one more vmcnt entry)
+    for (int g = 0; g < nsteps; ++g) {
+        // H(g) and W(g) have landed once only the younger W(g + 1) copies (if issued) and the
+        // previous epilogue's store (1) may be outstanding: 4 W pieces per wave (CP 0-2), 8 for a
+        // W wave and none for an H wave (CP 3, whose H(g) was issued after W(g + 1))
+        if (g + 1 < nsteps && !(SPLIT && hrole)) {
+            if constexpr (SPLIT) {
+                wait_vmcnt<8>();  // W waves never store
+            } else {
+                if (stored) wait_vmcnt<5>();
+                else wait_vmcnt<4>();
+            }
+        } else {
+            if (stored) wait_vmcnt<1>();
+            else wait_vmcnt<0>();
+        }
+        stored = false;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* sa = smem + hs * kT;
+        const char* sbw = smem + ws * kT;  // + boff's kWBase
+        // H(g + 1) and W(g + 2): this tile's next steps or the next tile's first ones
+        if (CP == 0 || ((CP == 1 || CP == 3) && !late)) copy_all(g, t, hs, ws);
+        // pipe 12's fragment pipeline (groups of 2 H x 4 W fragments), operands swapped
+        bf16x8 bq[2][4], aq[2][2];
+        auto ldA = [&](int ks, int mp, bf16x8 (&dst)[2]) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                dst[u] = *reinterpret_cast<const bf16x8*>(sa + aoff[ks] + (2 * mp + u) * 16 * kRow);
+        };
+        auto ldB = [&](int ks) {
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) bq[ks][nb] = *reinterpret_cast<const bf16x8*>(sbw + boff[ks] + nb * 16 * kRow);
+        };
+        ldB(0);
+        ldA(0, 0, aq[0]);
+#pragma unroll
+        for (int gg = 0; gg < 8; ++gg) {
+            const int ks = gg / 4, mp = gg % 4;
+            if constexpr (CP == 2) {
+                switch (gg) {
+                    case 0: copy_piece(std::integral_constant<int, 0>{}, g, t, hs, ws); break;
+                    case 1: copy_piece(std::integral_constant<int, 1>{}, g, t, hs, ws); break;
+                    case 2: copy_piece(std::integral_constant<int, 2>{}, g, t, hs, ws); break;
+                    case 3: copy_piece(std::integral_constant<int, 3>{}, g, t, hs, ws); break;
+                    case 4: copy_piece(std::integral_constant<int, 4>{}, g, t, hs, ws); break;
+                    case 5: copy_piece(std::integral_constant<int, 5>{}, g, t, hs, ws); break;
+                    case 6: copy_piece(std::integral_constant<int, 6>{}, g, t, hs, ws); break;
+                    default: copy_piece(std::integral_constant<int, 7>{}, g, t, hs, ws); break;
+                }
+            }
+            if ((CP == 1 || CP == 3) && late && gg == 4) copy_all(g, t, hs, ws);
+            if (gg + 1 < 8) {
+                if ((gg + 1) % 4 == 0) ldB((gg + 1) / 4);
+                ldA((gg + 1) / 4, (gg + 1) % 4, aq[(gg + 1) & 1]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    acc[2 * mp + u][nb] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks][nb], aq[gg & 1][u], acc[2 * mp + u][nb], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (t + 1 == nk) {
+            // ---- epilogue of tile i: every wave's reads of H stage hs are done, it is the scratch
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            float4* scr = reinterpret_cast<float4*>(smem + hs * kT);  // [256 tokens][4 column waves]
+            const int n0 = ntile * 256, m0 = mtile * BM;
+            const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
+            // a token's state over this wave's 64 columns: the max over the four lane groups
+            // first, then every exponential against it (no rescaling merges); sums joined by two
+            // xor adds. FULL: every column inside V (no masks, no clamps).
+            auto token_states = [&](auto full_tag) __attribute__((always_inline)) {
+                constexpr bool FULL = decltype(full_tag)::value;
+#pragma unroll
+                for (int tb = 0; tb < 8; ++tb) {
+                    float x[16];
+#pragma unroll
+                    for (int vb = 0; vb < 4; ++vb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = bf16_to_f32(f32_to_bf16(acc[tb][vb][r]));  // the logits the reference writes
+                            if constexpr (HAS_T) v = Elem<uint16_t>::apply_t(v, temp, true);
+                            if constexpr (!FULL) v = cbase + vb * 16 + r < N ? v : -INFINITY;
+                            x[vb * 4 + r] = v;
+                        }
+                    float mx = fmaxf(fmaxf(x[0], x[1]), x[2]);
+#pragma unroll
+                    for (int k = 3; k < 15; k += 2) mx = fmaxf(fmaxf(mx, x[k]), x[k + 1]);
+                    mx = fmaxf(mx, x[15]);
+                    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+                    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                    if constexpr (!FULL) mx = fmaxf(mx, -3.402823466e38f);  // columns all outside V: finite
+                    const float c = -mx * kLog2e;
+                    float sa = 0.f, sb = 0.f, wa = 0.f, wb = 0.f;  // two chains each
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        float y = fmaf(x[k], kLog2e, c);
+                        if constexpr (!FULL) y = fmaxf(y, kDLow);
+                        const float e = fast_exp2(y);
+                        if (k & 1) {
+                            sb += e;
+                            wb = fmaf(e, y, wb);
+                        } else {
+                            sa += e;
+                            wa = fmaf(e, y, wa);
+                        }
+                    }
+                    float ss = sa + sb, ww = wa + wb;
+                    ss += __shfl_xor(ss, 16, kWave);
+                    ww += __shfl_xor(ww, 16, kWave);
+                    ss += __shfl_xor(ss, 32, kWave);
+                    ww += __shfl_xor(ww, 32, kWave);
+                    if (lane < 16) lds_st16(scr + (wm * 128 + tb * 16 + lane) * 4 + wn, f32x4{mx, ss, ww, 0.f});
+                }
+            };
+            if (n0 + 256 <= N) token_states(std::true_type{});
+            else token_states(std::false_type{});
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (w < 4) {
+                const int tok = threadIdx.x;  // 0 .. 255
+                const f32x4 s0 = lds_ld16(scr + tok * 4 + 0), s1 = lds_ld16(scr + tok * 4 + 1);
+                const f32x4 s2 = lds_ld16(scr + tok * 4 + 2), s3 = lds_ld16(scr + tok * 4 + 3);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                SoftState st{s0[0], s0[1], s0[2]};
+                state_merge(st, SoftState{s1[0], s1[1], s1[2]});
+                state_merge(st, SoftState{s2[0], s2[1], s2[2]});
+                state_merge(st, SoftState{s3[0], s3[1], s3[2]});
+                // one store instruction per wave whenever any of its tokens is inside M
+                stored = m0 + w * 64 < M;
+                if (m0 + tok < M) parts[(int64_t)ntile * M + m0 + tok] = make_float4(st.m, st.s, st.w, __builtin_nanf(""));
+            }
+            // the next tile
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+            ++i;
+            t = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) oc[j] = ox[j];
+            offs(i + 1, ox);
+            tile_mn(i, mtile, ntile);
+        } else {
+            ++t;
+        }
+        hs ^= 1;
+        ws = ws == 2 ? 0 : ws + 1;
+    }
+}
+
+// The learner forward's finish, one wave per 16 tokens. The label logit by the tile kernel's own
+// MFMA chain: A = the 16 label rows of W, B = the 16 token rows of H, the k chunks of 32 in the
+// same order from a zero accumulator, so D[i][i] is the tile kernel's accumulator for (token i,
+// label i) bit for bit; rounded to bf16 and divided by T as there (NaN for a label outside [0, V),
+// as logprob.hip). Then the token's nt tile states: lane group q merges the tiles
+// [q nt / 4, (q + 1) nt / 4) in order, two xor merges join the groups, finalize.
+__global__ __launch_bounds__(64) void lmhead_label_merge_kernel(
+    const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int T, int V, int K,
+    const int64_t* __restrict__ labels, int64_t lstride, float temp, int has_t, const float4* __restrict__ parts, int nt,
+    float* __restrict__ logp_out, float* __restrict__ ent_out, float* __restrict__ lse_out) {
+    const int lane = threadIdx.x, i = lane & 15, grp = lane >> 4;
+    const int tok = min((int)blockIdx.x * 16 + i, T - 1);
+    const int64_t lab = labels[(int64_t)tok * lstride];
+    const bool valid = lab >= 0 && lab < V;
+    const uint16_t* wr = W + (valid ? lab : 0) * ldw + grp * 8;
+    const uint16_t* hr = H + (int64_t)tok * ldh + grp * 8;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int nkc = K / 32;
+    int kc = 0;
+    for (; kc + 4 <= nkc; kc += 4) {
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[u] = *reinterpret_cast<const bf16x8*>(wr + (kc + u) * 32);
+            b[u] = *reinterpret_cast<const bf16x8*>(hr + (kc + u) * 32);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
+    }
+    for (; kc < nkc; ++kc)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(wr + kc * 32),
+                                                      *reinterpret_cast<const bf16x8*>(hr + kc * 32), acc, 0, 0, 0);
+    // lane L holds D rows 4 (L >> 4) + r: row i's diagonal element is lane ((i >> 2) << 4) | i's r = i & 3
+    const int r3 = lane & 3;
+    const float dsel = r3 == 0 ? acc[0] : r3 == 1 ? acc[1] : r3 == 2 ? acc[2] : acc[3];
+    const float d = __shfl(dsel, ((i >> 2) << 4) | i, kWave);
+    float xl = bf16_to_f32(f32_to_bf16(d));
+    if (has_t) xl = Elem<uint16_t>::apply_t(xl, temp, true);
+    if (!valid) xl = __builtin_nanf("");
+    SoftState st;
+    state_init(st);
+    const int j1 = (grp + 1) * nt / 4;
+    int j = grp * nt / 4;
+    for (; j + 8 <= j1; j += 8) {
+        float4 c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = parts[(int64_t)(j + u) * T + tok];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) state_merge(st, SoftState{c[u].x, c[u].y, c[u].z});
+    }
+    for (; j < j1; ++j) {
+        const float4 c = parts[(int64_t)j * T + tok];
+        state_merge(st, SoftState{c.x, c.y, c.z});
+    }
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) {
+        SoftState o;
+        o.m = __shfl_xor(st.m, off, kWave);
+        o.s = __shfl_xor(st.s, off, kWave);
+        o.w = __shfl_xor(st.w, off, kWave);
+        state_merge(st, o);
+    }
+    if (lane < 16 && (int)blockIdx.x * 16 + lane < T) finalize_row(st, xl, tok, logp_out, ent_out, lse_out);
+}
+
 inline int tiles(int n, int b) { return (n + b - 1) / b; }
 
 using GemmKernel = void (*)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
@@ -1120,9 +1502,34 @@ extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, c
     SKYRL_REQUIRE(labels && logp_out && workspace, "lmhead_logprob_fwd: null pointer");
     SKYRL_REQUIRE(temperature > 0.f, "lmhead_logprob_fwd: temperature must be > 0");
     SKYRL_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "lmhead_logprob_fwd: workspace must be 16-B aligned");
+    float4* states = reinterpret_cast<float4*>(workspace);
+    if (knobs().lmhead_persist != 0 && K >= 128 && (int64_t)T * ld_hidden < (int64_t(1) << 31) &&
+        (int64_t)V * ld_weight < (int64_t(1) << 31)) {
+        // the persistent tile kernel (one workgroup per CU) + the label / merge launch
+        const int mt = tiles(T, BM), nt = tiles(V, 256);
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return fail(SKYRL_ERR_LAUNCH, "lmhead_logprob_fwd: device query failed");
+        const int grid = min(mt * nt, ncu);
+        const int cp = knobs().lmhead_persist - 1;
+        const bool ht = temperature != 1.0f;
+        auto pk = cp == 0   ? (ht ? lmhead_logprob_pkernel<true, 0> : lmhead_logprob_pkernel<false, 0>)
+                  : cp == 1 ? (ht ? lmhead_logprob_pkernel<true, 1> : lmhead_logprob_pkernel<false, 1>)
+                  : cp == 2 ? (ht ? lmhead_logprob_pkernel<true, 2> : lmhead_logprob_pkernel<false, 2>)
+                            : (ht ? lmhead_logprob_pkernel<true, 3> : lmhead_logprob_pkernel<false, 3>);
+        hipLaunchKernelGGL(pk, dim3(grid), dim3(512), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
+                           ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt, nt, group_for(mt),
+                           temperature, states);
+        rc = check_launch("lmhead_logprob_pkernel");
+        if (rc) return rc;
+        hipLaunchKernelGGL(lmhead_label_merge_kernel, dim3((unsigned)tiles(T, 16)), dim3(64), 0, as_stream(stream),
+                           reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
+                           ld_weight, T, V, K, labels, label_stride, temperature, temperature != 1.0f ? 1 : 0, states, nt,
+                           logp_out, entropy_out, lse_out);
+        return check_launch("lmhead_label_merge_kernel");
+    }
     const int pipe = pipe_for(T, ld_hidden, V, ld_weight);
     const int bn = tile_n(pipe), mt = tiles(T, BM), nt = tiles(V, bn);
-    float4* states = reinterpret_cast<float4*>(workspace);
     auto kern = pick_kernel<EPI_LOGPROB>(pipe);
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt | (group_for(mt) << 16), nullptr, 0ll,

@@ -102,6 +102,17 @@ __device__ __forceinline__ SoftState wave_merge(SoftState st) {
     return st;
 }
 
+// logp = x_label - lse, H = ln S - ln2 W / S and lse of a token's final state (lmhead.hip's chunk
+// path and lmhead_gemm.hip's tile path)
+__device__ __forceinline__ void finalize_row(const SoftState& st, float xl, int64_t r, float* __restrict__ logp_out,
+                                             float* __restrict__ ent_out, float* __restrict__ lse_out) {
+    const float logs = fast_log2(st.s) * kLn2;
+    const float lse = st.m + logs;
+    logp_out[r] = xl - lse;  // NaN for a label outside [0, V), as logprob.hip
+    if (ent_out) ent_out[r] = logs - kLn2 * (st.w / st.s);
+    if (lse_out) lse_out[r] = lse;
+}
+
 // Streaming 16-B load of data read once per pass (159 GB per pass >> L2/MALL): nontemporal.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_stream(const uint4* p) {

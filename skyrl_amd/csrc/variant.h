@@ -30,6 +30,7 @@ struct Knobs {
     int lmhead_pipe = 12;
     int lmhead_group = 8;
     int attn_pf = 0;
+    int lmhead_persist = 4;
 };
 inline constexpr Knobs kDefaultKnobs{};
 

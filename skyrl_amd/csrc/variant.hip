@@ -60,6 +60,7 @@ int VariantScope::enter(const skyrl_variant* v) {
     SKYRL_TAKE(lmhead_pipe, in(-1, 14));
     SKYRL_TAKE(lmhead_group, in(0, 4095));
     SKYRL_TAKE(attn_pf, one_of({0, 4, 6, 8}));
+    SKYRL_TAKE(lmhead_persist, in(0, 4));
 #undef SKYRL_TAKE
     if (rc) {
         active_ = false;  // nothing installed

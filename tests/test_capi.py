@@ -34,7 +34,7 @@ def test_ffi_signatures_cover_header():
 
 def test_abi_version_and_error_path():
     lib = _ffi.load()
-    assert lib.skyrl_abi_version() == 11
+    assert lib.skyrl_abi_version() == 12
     # argument validation happens on the host before any launch: no GPU needed
     with pytest.raises(_ffi.SkyrlHipError, match="temperature"):
         _ffi.call("skyrl_logprob_fwd", ctypes.c_void_p(16), _ffi.BF16, 8, 8, 1, 1, 8, ctypes.c_void_p(16), 1, 1,
