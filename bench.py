@@ -550,6 +550,7 @@ def run(args):
         result["rollout_attention"] = rollout_attention_leg(dev, NL)
     if legs and not args.no_lmhead_leg:
         result["rollout_lmhead_sample"] = lmhead_sample_leg(dev, NL)
+        result["learner_lmhead_fwd"] = learner_lmhead_fwd_leg(dev)
     if legs and not args.no_filtered_leg:
         result["sampler_filtered"] = sampler_filtered_leg(dev, NL, V)
     if legs and not args.no_vocab_legs:
@@ -827,6 +828,49 @@ def lmhead_sample_leg(dev, nseq, reps=30):
                        "peak": 2500.0, "unit": "TFLOP/s", "frac": round(tf / 2500.0, 4)}
     out["gemm_TFs"] = round(flops / (out["gemm_only_us"] * 1e-6) / 1e12, 1)
     out["logits_bytes_not_written"] = nseq * V * 2
+    return out
+
+
+def learner_lmhead_fwd_leg(dev, T=8192, reps=10):
+    """The learner's forward-only lm_head pass (old / ref log-probs + entropy) at
+    T = 8192 tokens of Qwen2.5-1.5B (hidden 1536 x lm_head [151,936, 1536] bf16):
+    fused   = skyrl_lmhead_logprob_fwd (persistent MFMA GEMM with the online softmax in its
+              epilogue + the label/merge launch): no logits leave the registers;
+    chunked = hipBLASLt GEMM into a reused [T, 16384] bf16 buffer + the HIP chunk merge.
+    Interleaved over 3 rounds, medians. The MFMA roofline is against the 2.5 PF/s dense bf16 peak."""
+    import statistics
+
+    from skyrl_amd import lmhead, ops
+
+    H, V = 1536, VOCAB
+    g = torch.Generator(device=dev).manual_seed(6)
+    w = (torch.randn(V, H, device=dev, generator=g) * (2.0 / H ** 0.5)).to(torch.bfloat16)
+    h = torch.randn(T, H, device=dev, generator=g).to(torch.bfloat16)
+    lab = torch.randint(0, V, (T,), device=dev, generator=g)
+    fns = {"fused": lambda: ops.lmhead_logprob_fwd(h, w, lab),
+           "chunked": lambda: lmhead.LMHeadLogprob.apply(h, w, lab, 1.0, True, None)}
+    times = {k: [] for k in fns}
+    with torch.no_grad():
+        for f in fns.values():
+            f()
+        torch.cuda.synchronize()
+        for _ in range(3):
+            for k, f in fns.items():
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(reps):
+                    f()
+                b.record()
+                b.synchronize()
+                times[k].append(a.elapsed_time(b) / reps)
+    out = {"tokens": T, "hidden": H, "vocab": V}
+    for k, v in times.items():
+        out[f"{k}_ms"] = round(statistics.median(v), 4)
+    flops = 2.0 * T * H * V
+    tf = flops / (out["fused_ms"] * 1e-3) / 1e12
+    out["roofline"] = {"kernel": "lmhead_logprob_pkernel + lmhead_label_merge_kernel", "bound": "mfma",
+                       "achieved": round(tf, 1), "peak": 2500.0, "unit": "TFLOP/s", "frac": round(tf / 2500.0, 4)}
+    out["logits_bytes_not_written"] = T * V * 2
     return out
 
 

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--check", type=int, default=1)
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3], help="skyrl_variant lmhead_persist values")
+    ap.add_argument("--groups", type=int, nargs="*", default=[], help="skyrl_variant lmhead_group values for the persistent default")
+    ap.add_argument("--no-chunked", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda")
     H, V = args.H, args.V
@@ -60,7 +62,17 @@ def main():
                 lmhead.lmhead_logprobs_and_entropy(h, W, lab, 1.0, True)
 
         fns = {f"persist{pv}": fused(pv) for pv in args.variants}
-        fns["chunked"] = chunked
+
+        def grouped(gp):
+            def f():
+                with _ffi.variant(lmhead_group=gp):
+                    ops.lmhead_logprob_fwd(h, W, lab)
+            return f
+
+        for gp in args.groups:
+            fns[f"group{gp}"] = grouped(gp)
+        if not args.no_chunked:
+            fns["chunked"] = chunked
         res = {k: [] for k in fns}
         for f in fns.values():
             f()

@@ -20,6 +20,10 @@ division and the dlogits are the HIP kernels, so the per-element numerics equal 
 ``ops.logprobs_and_entropy`` on the same bf16 logits. The trade is one extra GEMM in the
 backward (the recompute) against the bf16 logits and dlogits round trips through HBM, and
 O(T*chunk) instead of O(T*V) activation memory.
+
+Forward-only calls (the old / ref log-prob passes: no grad needed) take neither: they run
+``skyrl_lmhead_logprob_fwd``, our MFMA GEMM with the online softmax in its epilogue (the persistent
+tile kernel), so no logits, not even a chunk, leave the registers.
 """
 
 from __future__ import annotations
@@ -142,6 +146,16 @@ def _acc_mm(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
     acc.add_(torch.mm(a, b, out_dtype=torch.float32))
 
 
+def _epilogue_form_ok(h: torch.Tensor, weight: torch.Tensor) -> bool:
+    """The GEMM-epilogue kernel's operand rules (skyrl_lmhead_logprob_fwd): bf16, unit K stride,
+    K % 64 == 0, 16-B aligned rows."""
+    K = h.shape[-1]
+    return (h.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and h.dim() == 2 and weight.dim() == 2
+            and weight.shape[1] == K and K % 64 == 0 and h.stride(1) == 1 and weight.stride(1) == 1
+            and h.stride(0) % 8 == 0 and weight.stride(0) % 8 == 0
+            and h.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
+
+
 def lmhead_logprobs_and_entropy(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor,
                                 temperature: float = 1.0, compute_entropy: bool = True,
                                 chunk: Optional[int] = None):
@@ -149,8 +163,22 @@ def lmhead_logprobs_and_entropy(hidden: torch.Tensor, weight: torch.Tensor, labe
 
     hidden [..., H] bf16, weight [V, H] bf16 (the HF lm_head.weight layout), labels [...] int.
     Returns f32 tensors shaped like ``labels`` (entropy None when not requested); both are
-    differentiable w.r.t. hidden and weight.
+    differentiable w.r.t. hidden and weight. Without grad (no-grad mode or no operand that needs
+    one) and with ``chunk`` unset, the GEMM-epilogue kernel computes them.
     """
+    needs_grad = torch.is_grad_enabled() and (hidden.requires_grad or weight.requires_grad)
+    if not needs_grad and chunk is None and temperature > 0:
+        from . import ops
+        H = hidden.shape[-1]
+        h = hidden.reshape(-1, H)
+        if h.stride(-1) != 1:
+            h = h.contiguous()
+        if _epilogue_form_ok(h, weight) and h.is_cuda and weight.is_cuda:
+            lab, _ = _labels_flat(labels, h.shape[0], h.device)
+            lp, ent = ops.lmhead_logprob_fwd(h, weight, lab, temperature=float(temperature),
+                                             compute_entropy=bool(compute_entropy))
+            shape = labels.shape
+            return lp.view(shape), (ent.view(shape) if ent is not None else None)
     return LMHeadLogprob.apply(hidden, weight, labels, float(temperature), bool(compute_entropy), chunk)
 
 

@@ -205,10 +205,45 @@ def test_lmhead_logprob_fwd_matches_oracle_and_chunked(dev, V, K, temp):
     zt = (z.float() / temp).to(torch.bfloat16) if temp != 1.0 else z
     torch.testing.assert_close(lp.cpu(), cpu_ref.logprobs_from_logits(zt, lab), atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(ent.cpu(), cpu_ref.entropy_from_logits(zt), atol=1e-4, rtol=1e-5)
-    with torch.no_grad():
-        lc, ec = lmhead.lmhead_logprobs_and_entropy(hd, wd, lab.to(dev), temperature=temp)
+    with torch.no_grad():  # an explicit chunk keeps the chunked hipBLASLt path
+        lc, ec = lmhead.lmhead_logprobs_and_entropy(hd, wd, lab.to(dev), temperature=temp, chunk=lmhead.default_chunk(T, V))
+        # without grad and without a chunk the call is the GEMM-epilogue kernel itself
+        lr, er = lmhead.lmhead_logprobs_and_entropy(hd, wd, lab.to(dev), temperature=temp)
     torch.testing.assert_close(lp, lc, atol=2e-2, rtol=0)  # different GEMMs: bf16 logits may differ by an ulp
     torch.testing.assert_close(ent, ec, atol=2e-2, rtol=0)
+    assert torch.equal(lr, lp) and torch.equal(er, ent)
+
+
+@pytest.mark.parametrize("T,temp", [(1, 1.0), (255, 1.0), (257, 0.6), (2600, 1.0)])
+def test_lmhead_logprob_fwd_variants_and_edges(dev, T, temp):
+    """Every lmhead_persist variant (0: one tile per workgroup, LDS-image epilogue; 1-4: the
+    persistent kernel's copy placements) against the fp32 oracle on the kernel's own bf16 logits,
+    at token counts around the 256-row tile (ragged M), V not a multiple of 256 (ragged last N tile)
+    and labels at the vocabulary's ends; the persistent variants agree bit for bit."""
+    from oracle import cpu_ref
+    from skyrl_amd import _ffi
+
+    g = torch.Generator().manual_seed(T)
+    V, K = 3000 + 37, 256
+    h = torch.randn(T, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(V, K, generator=g) * (3.0 / K ** 0.5)).to(torch.bfloat16)
+    lab = torch.randint(0, V, (T,), generator=g)
+    lab[0] = V - 1
+    if T > 1:
+        lab[1] = 0
+    hd, wd = h.to(dev), w.to(dev)
+    z = ops.lmhead_gemm(hd, wd).cpu()
+    zt = (z.float() / temp).to(torch.bfloat16) if temp != 1.0 else z
+    e_lp, e_ent = cpu_ref.logprobs_from_logits(zt, lab), cpu_ref.entropy_from_logits(zt)
+    got = {}
+    for pv in range(5):
+        with _ffi.variant(lmhead_persist=pv):
+            lp, ent = ops.lmhead_logprob_fwd(hd, wd, lab.to(dev), temperature=temp)
+        torch.testing.assert_close(lp.cpu(), e_lp, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(ent.cpu(), e_ent, atol=1e-4, rtol=1e-5)
+        got[pv] = (lp, ent)
+    for pv in (2, 3, 4):
+        assert torch.equal(got[pv][0], got[1][0]) and torch.equal(got[pv][1], got[1][1])
 
 
 @pytest.mark.parametrize("group", [8, 4, 3, 0])
