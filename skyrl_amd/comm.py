@@ -673,20 +673,32 @@ class ParamSegments:
         self.touched = torch.ones(self.nparams, dtype=torch.int32, device=device)
         self.param_step = torch.zeros(self.nparams, dtype=torch.int32, device=device)
         self.coef = torch.zeros(2 * self.nparams, dtype=torch.float32, device=device)
-        # two pinned staging buffers for the host flags: a buffer is rewritten only after the
-        # copy that read it two steps ago has completed (its event)
-        self._host = [torch.ones(self.nparams, dtype=torch.int32).pin_memory() for _ in range(2)]
-        self._ev: List[Optional[torch.cuda.Event]] = [None, None]
-        self._k = 0
+        # pinned staging buffers for the host flags, each with the event of the copy that read
+        # it: upload() takes a buffer whose copy has completed (event.query(), never a wait) and
+        # pins a new one when none has, so the host never blocks on the device here
+        self._host: List[torch.Tensor] = []
+        self._ev: List[Optional[torch.cuda.Event]] = []
+
+    def _free_buffer(self) -> int:
+        for k, ev in enumerate(self._ev):
+            if ev is None or ev.query():
+                return k
+        self._host.append(torch.ones(self.nparams, dtype=torch.int32).pin_memory())
+        self._ev.append(None)
+        return len(self._host) - 1
 
     def upload(self, flags: Sequence[bool], group=None, collective: bool = False) -> None:
-        """Stage this rank's flags and (collective) MAX-reduce them over the group: no host sync."""
-        k = self._k
-        self._k ^= 1
-        if self._ev[k] is not None:
-            self._ev[k].synchronize()  # the copy of two steps ago
+        """Stage this rank's flags and (collective) MAX-reduce them over the group: no host sync
+        (the staging buffer is one whose previous copy has completed; the flags are written into
+        its numpy view, no per-step list -> tensor)."""
+        import numpy as np
+
+        k = self._free_buffer()
         h = self._host[k]
-        h[:-1] = torch.tensor([bool(f) for f in flags], dtype=torch.int32)
+        hv = h.numpy()
+        n = self.nparams - 1
+        hv[:n] = np.fromiter(flags, dtype=np.bool_, count=n)
+        hv[n] = 1  # the shard's padding pseudo-parameter is always updated
         self.touched.copy_(h, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.touched.device))
