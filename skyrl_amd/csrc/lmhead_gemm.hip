@@ -1034,10 +1034,15 @@ __device__ __forceinline__ f32x4 lds_ld16(const float4* p) {
 // after the step's barrier; 1 the second wave of each SIMD (waves 4-7) after its first four MFMA
 // groups; 2 one copy per MFMA group; 3 role split: waves 0-3 copy all of H(g + 1) after the
 // barrier, waves 4-7 all of W(g + 2) after their first four MFMA groups.
-template <bool HAS_T, int CP>
+// EPI: EPI_LOGPROB (the learner forward: per (tile, token) the softmax state (m, S, W) after the
+// reference's bf16 division by T, into parts[ntile][M]) or EPI_GREEDY (the decode side's greedy
+// step: per (token, tile) the first maximum and the raw (max, sum-exp), into parts[M][nt] and
+// part_x, lmhead_sample_merge_kernel's partials).
+template <int EPI, bool HAS_T, int CP>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void lmhead_logprob_pkernel(
     const uint16_t* __restrict__ H, int64_t ldh, const uint16_t* __restrict__ W, int64_t ldw, int M, int N, int K,
-    int mt, int nt, int gm, float temp, float4* __restrict__ parts) {
+    int mt, int nt, int gm, float temp, float4* __restrict__ parts, float* __restrict__ part_x) {
+    constexpr int NST = EPI == EPI_GREEDY ? 2 : 1;  // stores of a storing wave's epilogue
     using G = Geo<256, 64, 2>;
     constexpr int kT = 32768, kWBase = 2 * kT, kRow = 128;
     __shared__ __attribute__((aligned(16))) char smem[163840];
@@ -1171,11 +1176,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
             if constexpr (SPLIT) {
                 wait_vmcnt<8>();  // W waves never store
             } else {
-                if (stored) wait_vmcnt<5>();
+                if (stored) wait_vmcnt<4 + NST>();
                 else wait_vmcnt<4>();
             }
         } else {
-            if (stored) wait_vmcnt<1>();
+            if (stored) wait_vmcnt<NST>();
             else wait_vmcnt<0>();
         }
         stored = false;
@@ -1234,70 +1239,155 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
             float4* scr = reinterpret_cast<float4*>(smem + hs * kT);  // [256 tokens][4 column waves]
             const int n0 = ntile * 256, m0 = mtile * BM;
             const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
-            // a token's state over this wave's 64 columns: the max over the four lane groups
-            // first, then every exponential against it (no rescaling merges); sums joined by two
-            // xor adds. FULL: every column inside V (no masks, no clamps).
-            auto token_states = [&](auto full_tag) __attribute__((always_inline)) {
-                constexpr bool FULL = decltype(full_tag)::value;
-#pragma unroll
-                for (int tb = 0; tb < 8; ++tb) {
-                    float x[16];
-#pragma unroll
-                    for (int vb = 0; vb < 4; ++vb)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float v = bf16_to_f32(f32_to_bf16(acc[tb][vb][r]));  // the logits the reference writes
-                            if constexpr (HAS_T) v = Elem<uint16_t>::apply_t(v, temp, true);
-                            if constexpr (!FULL) v = cbase + vb * 16 + r < N ? v : -INFINITY;
-                            x[vb * 4 + r] = v;
+            if constexpr (EPI == EPI_LOGPROB) {
+                // a token's state over this wave's 64 columns: the max over the four lane groups
+                // first, then every exponential against it (no rescaling merges); sums joined by two
+                // xor adds. FULL: every column inside V (no masks, no clamps).
+                auto token_states = [&](auto full_tag) __attribute__((always_inline)) {
+                    constexpr bool FULL = decltype(full_tag)::value;
+    #pragma unroll
+                    for (int tb = 0; tb < 8; ++tb) {
+                        float x[16];
+    #pragma unroll
+                        for (int vb = 0; vb < 4; ++vb)
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                float v = bf16_to_f32(f32_to_bf16(acc[tb][vb][r]));  // the logits the reference writes
+                                if constexpr (HAS_T) v = Elem<uint16_t>::apply_t(v, temp, true);
+                                if constexpr (!FULL) v = cbase + vb * 16 + r < N ? v : -INFINITY;
+                                x[vb * 4 + r] = v;
+                            }
+                        float mx = fmaxf(fmaxf(x[0], x[1]), x[2]);
+    #pragma unroll
+                        for (int k = 3; k < 15; k += 2) mx = fmaxf(fmaxf(mx, x[k]), x[k + 1]);
+                        mx = fmaxf(mx, x[15]);
+                        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+                        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+                        if constexpr (!FULL) mx = fmaxf(mx, -3.402823466e38f);  // columns all outside V: finite
+                        const float c = -mx * kLog2e;
+                        float sa = 0.f, sb = 0.f, wa = 0.f, wb = 0.f;  // two chains each
+    #pragma unroll
+                        for (int k = 0; k < 16; ++k) {
+                            float y = fmaf(x[k], kLog2e, c);
+                            if constexpr (!FULL) y = fmaxf(y, kDLow);
+                            const float e = fast_exp2(y);
+                            if (k & 1) {
+                                sb += e;
+                                wb = fmaf(e, y, wb);
+                            } else {
+                                sa += e;
+                                wa = fmaf(e, y, wa);
+                            }
                         }
-                    float mx = fmaxf(fmaxf(x[0], x[1]), x[2]);
-#pragma unroll
-                    for (int k = 3; k < 15; k += 2) mx = fmaxf(fmaxf(mx, x[k]), x[k + 1]);
-                    mx = fmaxf(mx, x[15]);
-                    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-                    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-                    if constexpr (!FULL) mx = fmaxf(mx, -3.402823466e38f);  // columns all outside V: finite
-                    const float c = -mx * kLog2e;
-                    float sa = 0.f, sb = 0.f, wa = 0.f, wb = 0.f;  // two chains each
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        float y = fmaf(x[k], kLog2e, c);
-                        if constexpr (!FULL) y = fmaxf(y, kDLow);
-                        const float e = fast_exp2(y);
-                        if (k & 1) {
-                            sb += e;
-                            wb = fmaf(e, y, wb);
-                        } else {
-                            sa += e;
-                            wa = fmaf(e, y, wa);
-                        }
+                        float ss = sa + sb, ww = wa + wb;
+                        ss += __shfl_xor(ss, 16, kWave);
+                        ww += __shfl_xor(ww, 16, kWave);
+                        ss += __shfl_xor(ss, 32, kWave);
+                        ww += __shfl_xor(ww, 32, kWave);
+                        if (lane < 16) lds_st16(scr + (wm * 128 + tb * 16 + lane) * 4 + wn, f32x4{mx, ss, ww, 0.f});
                     }
-                    float ss = sa + sb, ww = wa + wb;
-                    ss += __shfl_xor(ss, 16, kWave);
-                    ww += __shfl_xor(ww, 16, kWave);
-                    ss += __shfl_xor(ss, 32, kWave);
-                    ww += __shfl_xor(ww, 32, kWave);
-                    if (lane < 16) lds_st16(scr + (wm * 128 + tb * 16 + lane) * 4 + wn, f32x4{mx, ss, ww, 0.f});
-                }
-            };
-            if (n0 + 256 <= N) token_states(std::true_type{});
-            else token_states(std::false_type{});
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            if (w < 4) {
-                const int tok = threadIdx.x;  // 0 .. 255
-                const f32x4 s0 = lds_ld16(scr + tok * 4 + 0), s1 = lds_ld16(scr + tok * 4 + 1);
-                const f32x4 s2 = lds_ld16(scr + tok * 4 + 2), s3 = lds_ld16(scr + tok * 4 + 3);
+                };
+                if (n0 + 256 <= N) token_states(std::true_type{});
+                else token_states(std::false_type{});
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                SoftState st{s0[0], s0[1], s0[2]};
-                state_merge(st, SoftState{s1[0], s1[1], s1[2]});
-                state_merge(st, SoftState{s2[0], s2[1], s2[2]});
-                state_merge(st, SoftState{s3[0], s3[1], s3[2]});
-                // one store instruction per wave whenever any of its tokens is inside M
-                stored = m0 + w * 64 < M;
-                if (m0 + tok < M) parts[(int64_t)ntile * M + m0 + tok] = make_float4(st.m, st.s, st.w, __builtin_nanf(""));
+                __builtin_amdgcn_s_barrier();
+                if (w < 4) {
+                    const int tok = threadIdx.x;  // 0 .. 255
+                    const f32x4 s0 = lds_ld16(scr + tok * 4 + 0), s1 = lds_ld16(scr + tok * 4 + 1);
+                    const f32x4 s2 = lds_ld16(scr + tok * 4 + 2), s3 = lds_ld16(scr + tok * 4 + 3);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    SoftState st{s0[0], s0[1], s0[2]};
+                    state_merge(st, SoftState{s1[0], s1[1], s1[2]});
+                    state_merge(st, SoftState{s2[0], s2[1], s2[2]});
+                    state_merge(st, SoftState{s3[0], s3[1], s3[2]});
+                    // one store instruction per wave whenever any of its tokens is inside M
+                    stored = m0 + w * 64 < M;
+                    if (m0 + tok < M) parts[(int64_t)ntile * M + m0 + tok] = make_float4(st.m, st.s, st.w, __builtin_nanf(""));
+                }
+            } else {
+                // greedy: the first maximum of the token's 64 columns (lane order is column order,
+                // then the lower index on equal values across lane groups) and the raw sum-exp
+                // against it
+                auto token_argmax = [&](auto full_tag) __attribute__((always_inline)) {
+                    constexpr bool FULL = decltype(full_tag)::value;
+#pragma unroll
+                    for (int tb = 0; tb < 8; ++tb) {
+                        float x[16];
+#pragma unroll
+                        for (int vb = 0; vb < 4; ++vb)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                float v = bf16_to_f32(f32_to_bf16(acc[tb][vb][r]));
+                                if constexpr (!FULL) v = cbase + vb * 16 + r < N ? v : -INFINITY;
+                                x[vb * 4 + r] = v;
+                            }
+                        float bx = x[0];
+                        int bk = 0;
+#pragma unroll
+                        for (int k = 1; k < 16; ++k) {
+                            if (x[k] > bx) {
+                                bx = x[k];
+                                bk = k;
+                            }
+                        }
+                        int bi = cbase + (bk >> 2) * 16 + (bk & 3);
+#pragma unroll
+                        for (int off = 16; off < 64; off <<= 1) {
+                            const float ox = __shfl_xor(bx, off, kWave);
+                            const int oi = __shfl_xor(bi, off, kWave);
+                            if (ox > bx || (ox == bx && oi < bi)) {
+                                bx = ox;
+                                bi = oi;
+                            }
+                        }
+                        // columns all outside V: a finite floor whose -mx log2e does not overflow
+                        // (-inf x then gives exp2(-inf) = 0, never inf - inf)
+                        const float mx = FULL ? bx : fmaxf(bx, -1e30f);
+                        const float c = -mx * kLog2e;
+                        float sa = 0.f, sb = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 16; k += 2) {
+                            sa += fast_exp2(fmaf(x[k], kLog2e, c));
+                            sb += fast_exp2(fmaf(x[k + 1], kLog2e, c));
+                        }
+                        float ss = sa + sb;
+                        ss += __shfl_xor(ss, 16, kWave);
+                        ss += __shfl_xor(ss, 32, kWave);
+                        if (lane < 16)
+                            lds_st16(scr + (wm * 128 + tb * 16 + lane) * 4 + wn, f32x4{bx, __int_as_float(bi), mx, ss});
+                    }
+                };
+                if (n0 + 256 <= N) token_argmax(std::true_type{});
+                else token_argmax(std::false_type{});
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (w < 4) {
+                    const int tok = threadIdx.x;  // 0 .. 255
+                    f32x4 r[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) r[j] = lds_ld16(scr + tok * 4 + j);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    float bx = r[0][0], m = r[0][2], sm = r[0][3];
+                    int bi = __float_as_int(r[0][1]);
+#pragma unroll
+                    for (int j = 1; j < 4; ++j) {
+                        if (r[j][0] > bx) {  // column waves in column order: strict '>' keeps the first
+                            bx = r[j][0];
+                            bi = __float_as_int(r[j][1]);
+                        }
+                        const float mn = fmaxf(m, r[j][2]);
+                        sm = sm * fast_exp2((m - mn) * kLog2e) + r[j][3] * fast_exp2((r[j][2] - mn) * kLog2e);
+                        m = mn;
+                    }
+                    stored = m0 + w * 64 < M;
+                    if (m0 + tok < M) {
+                        const int64_t pi = (int64_t)(m0 + tok) * nt + ntile;
+                        parts[pi] = make_float4(bx, __int_as_float(bi), m, sm);
+                        part_x[pi] = bx;
+                    }
+                }
             }
             // the next tile
 #pragma unroll
@@ -1477,6 +1567,31 @@ extern "C" int skyrl_lmhead_sample(const void* hidden, int64_t ld_hidden, const 
     const bool greedy = temperature == 0.f;
     const float inv_t = greedy ? 1.f : 1.0f / temperature;
     if (greedy) rowbar = nullptr;
+    if (greedy && knobs().lmhead_persist != 0 && K >= 128 && (int64_t)M * ld_hidden < (int64_t(1) << 31) &&
+        (int64_t)V * ld_weight < (int64_t(1) << 31)) {
+        // the persistent tile kernel when it has at least four rounds of tiles (decode batches of
+        // 512+ rows); below that one tile per workgroup balances better
+        const int pmt = tiles(M, BM), pnt = tiles(V, 256);
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return fail(SKYRL_ERR_LAUNCH, "lmhead_sample: device query failed");
+        if (pmt * pnt >= 4 * ncu) {
+            const int cp = knobs().lmhead_persist - 1;
+            auto pk = cp == 0   ? lmhead_logprob_pkernel<EPI_GREEDY, false, 0>
+                      : cp == 1 ? lmhead_logprob_pkernel<EPI_GREEDY, false, 1>
+                      : cp == 2 ? lmhead_logprob_pkernel<EPI_GREEDY, false, 2>
+                                : lmhead_logprob_pkernel<EPI_GREEDY, false, 3>;
+            float* px = reinterpret_cast<float*>(parts + (size_t)M * pnt);
+            hipLaunchKernelGGL(pk, dim3(min(pmt * pnt, ncu)), dim3(512), 0, as_stream(stream),
+                               reinterpret_cast<const uint16_t*>(hidden), ld_hidden, reinterpret_cast<const uint16_t*>(weight),
+                               ld_weight, M, V, K, pmt, pnt, group_for(pmt), 1.f, parts, px);
+            rc = check_launch("lmhead_logprob_pkernel<greedy>");
+            if (rc) return rc;
+            hipLaunchKernelGGL(lmhead_sample_merge_kernel, dim3(M), dim3(64), 0, as_stream(stream), parts, px, pnt,
+                               tokens_out, logp_out, nullptr);
+            return check_launch("lmhead_sample_merge_kernel");
+        }
+    }
     auto kern = greedy ? pick_kernel<EPI_GREEDY>(pipe) : pick_kernel<EPI_SAMPLE>(pipe);
     hipLaunchKernelGGL(kern, dim3(mt * nt), dim3(tile_threads(pipe)), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                        ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, M, V, K, mt | (group_for(mt) << 16), nullptr, 0ll, inv_t,
@@ -1513,13 +1628,13 @@ extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, c
         const int grid = min(mt * nt, ncu);
         const int cp = knobs().lmhead_persist - 1;
         const bool ht = temperature != 1.0f;
-        auto pk = cp == 0   ? (ht ? lmhead_logprob_pkernel<true, 0> : lmhead_logprob_pkernel<false, 0>)
-                  : cp == 1 ? (ht ? lmhead_logprob_pkernel<true, 1> : lmhead_logprob_pkernel<false, 1>)
-                  : cp == 2 ? (ht ? lmhead_logprob_pkernel<true, 2> : lmhead_logprob_pkernel<false, 2>)
-                            : (ht ? lmhead_logprob_pkernel<true, 3> : lmhead_logprob_pkernel<false, 3>);
+        auto pk = cp == 0   ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 0> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 0>)
+                  : cp == 1 ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 1> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 1>)
+                  : cp == 2 ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 2> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 2>)
+                            : (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 3> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 3>);
         hipLaunchKernelGGL(pk, dim3(grid), dim3(512), 0, as_stream(stream), reinterpret_cast<const uint16_t*>(hidden),
                            ld_hidden, reinterpret_cast<const uint16_t*>(weight), ld_weight, T, V, K, mt, nt, group_for(mt),
-                           temperature, states);
+                           temperature, states, nullptr);
         rc = check_launch("lmhead_logprob_pkernel");
         if (rc) return rc;
         hipLaunchKernelGGL(lmhead_label_merge_kernel, dim3((unsigned)tiles(T, 16)), dim3(64), 0, as_stream(stream),

@@ -184,6 +184,33 @@ def test_fused_sample_many_rows_steps_and_ties(dev, temp):
     assert torch.equal(tf.cpu(), tu.cpu())
 
 
+def test_fused_greedy_persistent_ties_and_variants(dev):
+    """Greedy decode batches of 512+ rows take the persistent tile kernel: on tie-heavy logits
+    (values in {-2..2} over V = 151,936, ragged last vocab tile) the first maximum wins as in the
+    unfused sampler, and the one-tile-per-workgroup kernel (lmhead_persist 0) gives the same
+    tokens and logprobs."""
+    from skyrl_amd import _ffi
+
+    g = torch.Generator().manual_seed(11)
+    M, V, K = 520, 151936, 128
+    hq = torch.zeros(M, K, dtype=torch.bfloat16)
+    hq[:, 0] = 1
+    hq[:, 1] = torch.randint(0, 2, (M,), generator=g).to(torch.bfloat16)
+    wq = torch.zeros(V, K, dtype=torch.bfloat16)
+    wq[:, 0] = torch.randint(-2, 2, (V,), generator=g).to(torch.bfloat16)
+    wq[:, 1] = torch.randint(0, 2, (V,), generator=g).to(torch.bfloat16)  # row-dependent maxima
+    hd, wd = hq.to(dev), wq.to(dev)
+    z = ops.lmhead_gemm(hd, wd)
+    tu, lu = ops.sample(z, temperature=0.0)
+    tf, lf = ops.lmhead_sample(hd, wd, temperature=0.0)
+    assert torch.equal(tf.cpu(), tu.cpu())
+    torch.testing.assert_close(lf.cpu(), lu.cpu(), atol=1e-4, rtol=1e-5)
+    with _ffi.variant(lmhead_persist=0):
+        t0, l0 = ops.lmhead_sample(hd, wd, temperature=0.0)
+    assert torch.equal(t0.cpu(), tf.cpu())
+    torch.testing.assert_close(l0.cpu(), lf.cpu(), atol=1e-5, rtol=1e-6)
+
+
 @pytest.mark.parametrize("V,K,temp", [(151936, 1536, 1.0), (50257, 768, 0.6), (4099, 128, 1.0)])
 def test_lmhead_logprob_fwd_matches_oracle_and_chunked(dev, V, K, temp):
     """Learner-side forward (old / ref log-probs): the GEMM's online-softmax epilogue equals the
