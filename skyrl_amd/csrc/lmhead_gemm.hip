@@ -88,6 +88,8 @@ __device__ __forceinline__ float bar_value(unsigned k) {
 }
 // hardware natural log (v_log_f32 is log2): within ~3e-6 of det_ln for the arguments here
 __device__ __forceinline__ float hw_ln(float x) { return __builtin_amdgcn_logf(x) * kLn2G; }
+// the group bound's slope in score units: ln2 2^-23 per unit of bits(float(h16)) (noise.h)
+constexpr float kBitsLn2 = 0.6931471805599453f * 1.1920928955078125e-7f;
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -785,16 +787,20 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
         float m = -1e30f, s = 0.f;   // raw online (max, sum-exp)
         float best_s = -INFINITY, best_x = -INFINITY;
         int best_i = 0x7fffffff;
-        float lng[NC], slack[NC];    // per group: -ln E_g and the non-min-slot bound slack
+        float ubc[NC], vmx[NC];      // per group: c_g >= -ln E_v + 0.01 for each of its slots; its max logit
+        uint32_t hg[NC];             // per group: its hash
+        float best_ub = -INFINITY;   // pass 1: the best group bound (its first maximum and its
+        int seed_g = -1, seed_k = 0; // minimum-E slot seed the bar)
         uint32_t key = 0u, key2 = 0u, keyb = 0u;
         if constexpr (!greedy) {
             key = row_key(seed, seq_ids ? seq_ids[grow] : (int64_t)grow, step);
             key2 = noise_key2(key);
             keyb = noise_keyb(key);
         }
-        // pass 1, every group: LSE; greedy: the first maximum; sampling: the exact score of the
-        // group's minimum-E slot p = h & 7 (its E is E_g itself, so the score needs no per-element
-        // hash) -- the best of those is the bar for everything else
+        // pass 1, every group: LSE; greedy: the first maximum; sampling: the group bound of the
+        // sampler kernels (one hash, no logarithm: E_v >= E_g > h16 2^-19, so -ln E_v <
+        // ln2 (146 - bits(float(h16)) 2^-23), plus 0.01) -- the first maximum of the group with
+        // the best bound gets one exact score below, the bar for everything else
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
             const int c = TPR * i + hh;
@@ -813,8 +819,9 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
             float vmax = x[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) vmax = fmaxf(vmax, x[k]);
-            lng[i] = 0.f;
-            slack[i] = 0.f;
+            ubc[i] = 0.f;
+            vmx[i] = -INFINITY;
+            hg[i] = 0u;
             if (cnt <= 0) continue;
             {
                 const float mn = fmaxf(m, vmax);
@@ -834,50 +841,59 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                     best_x = vmax;
                 }
             } else {
-                // Bounds only: L~ = -ln E_g by the hardware log of the exact E_g (absolute error
-                // < 1e-6 against -det_ln(E_g) for E_g >= 7e-9, the smallest E_g there is); the slack
-                // of a non-min slot (E = E_g + (-det_ln U) >= E_g - 1.2e-6, so its exact score is
-                // <= x inv_t + L + 1.4e-6 / E_g + 4e-6) is generous on both and infinite when E_g is
-                // too small for it. The group whose minimum slot has the best approximate score gets
-                // one exact score below: the tile's bar.
+                // bounds only (the decisions are exact scores below): every slot v of this group has
+                // exact score <= x_v inv_t + c_g
                 const uint32_t h = ehash(key, keyb, (uint32_t)v0 >> 3);
-                const int p = (int)(h & 7u);
-                const float eg = group_min_e(h);
-                const float L = -hw_ln(eg);
-                lng[i] = L;
-                slack[i] = eg < 1e-5f ? INFINITY : 2e-4f + 5e-6f / eg;
-                float xp = x[0];
+                const float cg = fmaf(noise_bits(h), -kBitsLn2, kNoiseC);
+                ubc[i] = cg;
+                vmx[i] = vmax;
+                hg[i] = h;
+                const float ub = vmax * inv_t + cg;
+                if (ub > best_ub) {  // which group seeds the bar: its first maximum
+                    int kk = 7;
 #pragma unroll
-                for (int k = 1; k < 8; ++k) xp = (k == p) ? x[k] : xp;
-                if (p < cnt) {
-                    const float ap = xp * inv_t + L;
-                    if (ap > best_s) {  // approximate: which minimum slot to score exactly
-                        best_s = ap;
-                        best_i = v0 + p;
-                    }
+                    for (int k = 6; k >= 0; --k) kk = (x[k] == vmax) ? k : kk;
+                    best_ub = ub;
+                    seed_g = i;
+                    seed_k = kk;
                 }
             }
         }
         if constexpr (!greedy) {
             GPHASE(3);
-            // the tile's bar: the exact score of the approximately best minimum slot of this thread
+            // the tile's bar: the exact score of the first maximum of this thread's best-bound group
             // (max over the row's threads), raised to the best exact score the row's finished tiles
             // published (rowbar); both are exact scores of elements some tile reports
+            // exact scores of the seed group's first maximum and of its minimum-E slot (p = h & 7:
+            // E_v = E_g there, the group's largest noise); lowest index on equal scores
             float bar = -INFINITY;
-            if (best_i != 0x7fffffff) {
-                const int c = (best_i - n0) >> 3, k = (best_i - n0) & 7;
-                const float xp = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + G::img_off(r, c) + k * 2));
-                const uint32_t h = ehash(key, keyb, (uint32_t)best_i >> 3);
-                bar = noise_score(xp, inv_t, best_i, h, group_min_e(h), key2);
-                best_s = bar;
-                best_x = xp;
-            } else {
-                best_s = -INFINITY;
+            best_s = -INFINITY;
+            if (seed_g >= 0) {
+                uint32_t hs = 0u;
+#pragma unroll
+                for (int i = 0; i < NC; ++i) hs = i == seed_g ? hg[i] : hs;  // (a select chain, no scratch)
+                const int c = TPR * seed_g + hh, vb = n0 + c * 8;
+                const int p = (int)(hs & 7u), cnt = min(8, N - vb);
+                const float eg = group_min_e(hs);
+                const int ks[2] = {min(p, seed_k), max(p, seed_k)};  // ascending index
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int k = ks[j];
+                    if (k >= cnt || (j == 1 && ks[1] == ks[0])) continue;
+                    const float xk = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + G::img_off(r, c) + k * 2));
+                    const float sc = noise_score(xk, inv_t, vb + k, hs, eg, key2);
+                    if (sc > best_s) {
+                        best_s = sc;
+                        best_i = vb + k;
+                        best_x = xk;
+                    }
+                }
+                bar = best_s;
             }
 #pragma unroll
             for (int o = 1; o < TPR; o <<= 1) bar = fmaxf(bar, __shfl_xor(bar, o, kWave));
             if (rowbar) bar = fmaxf(bar, bar_value(rowbar[grow]));
-            // pass 2: non-min slots whose bound reaches the bar, as a bit mask (bit 8 i + k)
+            // pass 2: the slots whose bound reaches the bar, as a bit mask (bit 8 i + k)
             uint32_t cm[NC / 4];
 #pragma unroll
             for (int j = 0; j < NC / 4; ++j) cm[j] = 0u;
@@ -886,9 +902,17 @@ __global__ __launch_bounds__(DB == 6 ? 256 : 2 * BN) __attribute__((amdgpu_waves
                 const int v0 = n0 + (TPR * i + hh) * 8;
                 const int cnt = min(8, N - v0);
                 const uint32_t wds[4] = {pk[i].x, pk[i].y, pk[i].z, pk[i].w};
-                // x inv_t >= lim can reach the bar (the rounding of x inv_t + L is inside 1e-6 |bar|)
-                const float lim = bar - lng[i] - slack[i] - 1e-6f * fabsf(bar);
+                // the cheap group test first (the bits bound: x inv_t + c_g, c_g's 0.01 margin covers
+                // det_ln's error, the rounding is inside 1e-6 |bar|); a group that passes gets the
+                // tight per-slot bound: L~ = -ln E_g by the hardware log of the exact E_g (within 1e-6
+                // of -det_ln(E_g) for E_g >= 7e-9, the smallest there is) and the slack of a non-min
+                // slot (E = E_g + (-det_ln U) >= E_g - 1.2e-6: exact score <= x inv_t + L + 1.4e-6 / E_g
+                // + 4e-6), infinite when E_g is too small for it
+                const float eps = 1e-6f * fabsf(bar);
                 uint32_t bm = 0u;
+                if (vmx[i] * inv_t + ubc[i] < bar - eps) continue;
+                const float eg = group_min_e(hg[i]);
+                const float lim = bar + hw_ln(eg) - (eg < 1e-5f ? INFINITY : 2e-4f + 5e-6f / eg) - eps;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const float xk = __uint_as_float((k & 1) ? (wds[k >> 1] & 0xffff0000u) : (wds[k >> 1] << 16));
