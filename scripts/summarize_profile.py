@@ -32,6 +32,8 @@ def main(tag, src=None):
         SRC = src
     os.makedirs(DST, exist_ok=True)
     stats = os.path.join(SRC, "trace", "run_kernel_stats.csv")
+    if not os.path.exists(stats):  # scripts/gpu_run.sh's prof step writes into the directory itself
+        stats = os.path.join(SRC, "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(DST, f"{tag}_kernel_stats.csv"))
         rows = list(csv.DictReader(open(stats)))
