@@ -71,6 +71,7 @@ def main():
 
         for gp in args.groups:
             fns[f"group{gp}"] = grouped(gp)
+        fns["persist_default_noentropy"] = lambda: ops.lmhead_logprob_fwd(h, W, lab, compute_entropy=False)
         if not args.no_chunked:
             fns["chunked"] = chunked
         res = {k: [] for k in fns}

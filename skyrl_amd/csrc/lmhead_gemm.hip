@@ -44,7 +44,7 @@ typedef __attribute__((address_space(1))) void gbl_void;
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2, EPI_LOGPROB = 3 };
+enum { EPI_STORE = 0, EPI_SAMPLE = 1, EPI_GREEDY = 2, EPI_LOGPROB = 3, EPI_LOGPROB_NOENT = 4 };
 
 // Tile geometry: BM (256) x BN output columns, NT = 2 BN threads as 2 (M) x BN/64 (N) waves of
 // 128 x 64 outputs; K in BKT-deep tiles through S LDS stages (S - 1 tiles in flight).
@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
             float4* scr = reinterpret_cast<float4*>(smem + hs * kT);  // [256 tokens][4 column waves]
             const int n0 = ntile * 256, m0 = mtile * BM;
             const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
-            if constexpr (EPI == EPI_LOGPROB) {
+            if constexpr (EPI == EPI_LOGPROB || EPI == EPI_LOGPROB_NOENT) {
                 // a token's state over this wave's 64 columns: the max over the four lane groups
                 // first, then every exponential against it (no rescaling merges); sums joined by two
                 // xor adds. FULL: every column inside V (no masks, no clamps).
@@ -1297,17 +1297,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
                             const float e = fast_exp2(y);
                             if (k & 1) {
                                 sb += e;
-                                wb = fmaf(e, y, wb);
+                                if constexpr (EPI == EPI_LOGPROB) wb = fmaf(e, y, wb);
                             } else {
                                 sa += e;
-                                wa = fmaf(e, y, wa);
+                                if constexpr (EPI == EPI_LOGPROB) wa = fmaf(e, y, wa);
                             }
                         }
-                        float ss = sa + sb, ww = wa + wb;
+                        float ss = sa + sb, ww = wa + wb;  // W only for the entropy (EPI_LOGPROB)
                         ss += __shfl_xor(ss, 16, kWave);
-                        ww += __shfl_xor(ww, 16, kWave);
                         ss += __shfl_xor(ss, 32, kWave);
-                        ww += __shfl_xor(ww, 32, kWave);
+                        if constexpr (EPI == EPI_LOGPROB) {
+                            ww += __shfl_xor(ww, 16, kWave);
+                            ww += __shfl_xor(ww, 32, kWave);
+                        }
                         if (lane < 16) lds_st16(scr + (wm * 128 + tb * 16 + lane) * 4 + wn, f32x4{mx, ss, ww, 0.f});
                     }
                 };
@@ -1652,7 +1654,8 @@ extern "C" int skyrl_lmhead_logprob_fwd(const void* hidden, int64_t ld_hidden, c
         const int grid = min(mt * nt, ncu);
         const int cp = knobs().lmhead_persist - 1;
         const bool ht = temperature != 1.0f;
-        auto pk = cp == 0   ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 0> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 0>)
+        auto pk = !entropy_out && cp == 3 ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB_NOENT, true, 3> : lmhead_logprob_pkernel<EPI_LOGPROB_NOENT, false, 3>)
+                  : cp == 0 ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 0> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 0>)
                   : cp == 1 ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 1> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 1>)
                   : cp == 2 ? (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 2> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 2>)
                             : (ht ? lmhead_logprob_pkernel<EPI_LOGPROB, true, 3> : lmhead_logprob_pkernel<EPI_LOGPROB, false, 3>);

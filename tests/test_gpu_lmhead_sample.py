@@ -271,6 +271,8 @@ def test_lmhead_logprob_fwd_variants_and_edges(dev, T, temp):
         got[pv] = (lp, ent)
     for pv in (2, 3, 4):
         assert torch.equal(got[pv][0], got[1][0]) and torch.equal(got[pv][1], got[1][1])
+    lp_ne, ent_ne = ops.lmhead_logprob_fwd(hd, wd, lab.to(dev), temperature=temp, compute_entropy=False)
+    assert ent_ne is None and torch.equal(lp_ne, got[4][0])  # the entropy-free epilogue: same log-probs
 
 
 @pytest.mark.parametrize("group", [8, 4, 3, 0])
