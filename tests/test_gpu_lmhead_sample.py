@@ -241,8 +241,8 @@ def test_lmhead_logprob_fwd_matches_oracle_and_chunked(dev, V, K, temp):
     assert torch.equal(lr, lp) and torch.equal(er, ent)
 
 
-@pytest.mark.parametrize("T,temp", [(1, 1.0), (255, 1.0), (257, 0.6), (2600, 1.0)])
-def test_lmhead_logprob_fwd_variants_and_edges(dev, T, temp):
+@pytest.mark.parametrize("T,temp,K", [(1, 1.0, 256), (255, 1.0, 256), (257, 0.6, 256), (2600, 1.0, 256), (700, 1.0, 128)])
+def test_lmhead_logprob_fwd_variants_and_edges(dev, T, temp, K):
     """Every lmhead_persist variant (0: one tile per workgroup, LDS-image epilogue; 1-4: the
     persistent kernel's copy placements) against the fp32 oracle on the kernel's own bf16 logits,
     at token counts around the 256-row tile (ragged M), V not a multiple of 256 (ragged last N tile)
@@ -251,7 +251,7 @@ def test_lmhead_logprob_fwd_variants_and_edges(dev, T, temp):
     from skyrl_amd import _ffi
 
     g = torch.Generator().manual_seed(T)
-    V, K = 3000 + 37, 256
+    V = 3000 + 37  # K = 128: two K steps per tile, so W(g + 2) is always the next tile's
     h = torch.randn(T, K, generator=g).to(torch.bfloat16)
     w = (torch.randn(V, K, generator=g) * (3.0 / K ** 0.5)).to(torch.bfloat16)
     lab = torch.randint(0, V, (T,), generator=g)
