@@ -503,6 +503,26 @@ __device__ uint64_t g_sphase[4096 * 8];
 #ifndef SKYRL_TP2_BAR_FORM
 #define SKYRL_TP2_BAR_FORM 1
 #endif
+// the top_p kernel's pass-1 bar (top_p only; min_p alone keeps the best record): R = 1 the best
+// exact score so far; R > 1 the R-th largest of the 8 waves' best scores, a lower bound on the
+// row's R-th best score, so pass 1 certifies a row unless its R best elements are all outside the
+// kept set (about (1 - top_p)^R of the rows). R = 3 (product): 0.05 rows of 512 left to pass 2
+// at top_p 0.95 against 27 with R = 1; pass 1 costs 49 -> 59 us (the lower bar lets ~2x the
+// candidate events through) and whole calls 77.7 / 70.3 / 80.0 -> 66.5 / 65.6 / 73.7 us at top_p
+// 0.95 T = 1 / 0.6 and top_p 0.9 (R = 2: 73.2 / 71.9 / 84.5, R = 4 slower than 3; tokens bit-exact;
+// profiles/r06v_topp_rbar_ab.json, scripts/probe/topp_rbar_ab.py)
+#ifndef SKYRL_TP_RBAR
+#define SKYRL_TP_RBAR 3
+#endif
+// pass 1 ranks the split cut key's records that beat e* by a scan of the row prefix (1, product:
+// with R = 3 these were most of the rows left, 9 of 11 over 20 steps) or leaves the row to pass 2 (0)
+#ifndef SKYRL_TP_TIERES
+#define SKYRL_TP_TIERES 1
+#endif
+#ifndef SKYRL_TP_RBAR_VEC  // R > 1: the waves' bests read by two 16-B LDS loads (1) or 8 atomic loads (0)
+#define SKYRL_TP_RBAR_VEC 1
+#endif
+static_assert(SKYRL_TP_BAR_FORM || SKYRL_TP_RBAR == 1, "the R-th-best bar is built on the publish-on-improvement form");
 struct TieSink {
     int32_t* idx;
     float* sc;
@@ -1567,6 +1587,7 @@ constexpr int kPE0 = 111;       // window: bf16 exponent fields 111..142, |x| in
 constexpr int kPHalf = 4096;    // keys per sign in the window
 constexpr int kPSlowCap = 512;  // elements below the window
 constexpr int kPTieCap = 1024;  // elements at a split cut key
+constexpr int kPTieRes = 64;    // pass 1 ranks at most this many cut-key records (else pass 2)
 constexpr int kPCandCap = 2048; // pass 1's exactly scored elements (seeds + bound survivors)
 constexpr int32_t kRowPending = -4;  // RowFilter.ik between the two top_p kernels: pass 2 to run
 constexpr int kP2Splits = 8;         // workgroups per left row in sample_topp_pass2_kernel
@@ -1603,8 +1624,16 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     __shared__ float s_cs[kPCandCap];     // pass 1's exactly scored elements: score, index, key
     __shared__ int32_t s_ci[kPCandCap];
     __shared__ uint16_t s_ck[kPCandCap];
-    __shared__ uint32_t s_nc, s_ntie;
+    __shared__ uint32_t s_nc, s_ntie, s_trn;
+#ifdef SKYRL_TP_COUNT
+    __shared__ uint32_t s_cnt[2];
+    if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0u;
+#endif
+    __shared__ int32_t s_tri[kPTieRes];  // pass 1's cut-key records that beat e* (SKYRL_TP_TIERES)
+    __shared__ float s_trs[kPTieRes];
     __shared__ float s_bar1;
+    __shared__ __attribute__((aligned(16))) float s_wbest[NW];  // R > 1: each wave's best exact score
+    constexpr int kRBar = TOPP ? SKYRL_TP_RBAR : 1;
     __shared__ float s_bs[NW];
     __shared__ int32_t s_bi[NW];
     __shared__ int s_icut;
@@ -1633,6 +1662,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         s_ntie = 0u;
         s_bar1 = -INFINITY;  // the workgroup's best exact score so far
     }
+    if (threadIdx.x < NW) s_wbest[threadIdx.x] = -INFINITY;
     for (int j = threadIdx.x; j < 2 * kPHalf + kWave; j += NT) s_hist[j] = 0u;
     __syncthreads();
 
@@ -1650,6 +1680,9 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     // it -- the certificate, which holds with probability about the kept mass (>= top_p); the other
     // rows take pass 2 (the re-read), with e* as its starting bar. (A margin below the bar, which
     // certifies more rows, made pass 1 slower than the re-reads it saved: DESIGN §3 "Filters".)
+    // top_p with SKYRL_TP_RBAR = R > 1: the bar is the R-th largest of the waves' best scores, so
+    // the certificate (e* >= that final bar) fails only when the row's R best elements are all cut
+    // (about (1 - top_p)^R), and recorded cut-key ties above e* are ranked in pass 1 (SKYRL_TP_TIERES).
     const uint32_t key = row_key(seed, seq_ids ? seq_ids[row_i] : (int64_t)row_i, step);
     const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
     const float temp = 1.0f / inv_t;
@@ -1668,12 +1701,49 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             s_ck[p] = (uint16_t)b;
         }
     };
+    // R > 1: the R-th largest of the waves' published bests (insertion into R sorted slots)
+    auto rbar = [&]() -> float {
+        float t[kRBar];
+#pragma unroll
+        for (int r = 0; r < kRBar; ++r) t[r] = -INFINITY;
+#if SKYRL_TP_RBAR_VEC  // two 16-B LDS reads (the other waves' stores seen at the next read: a
+                       // compiler barrier keeps the loads here)
+        asm volatile("" ::: "memory");
+        const float4 q0 = reinterpret_cast<const float4*>(s_wbest)[0], q1 = reinterpret_cast<const float4*>(s_wbest)[1];
+        const float wv[NW] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#endif
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+#if SKYRL_TP_RBAR_VEC
+            float v = wv[j];
+#else
+            float v = __hip_atomic_load(&s_wbest[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+#pragma unroll
+            for (int r = 0; r < kRBar; ++r) {
+                const float hi = fmaxf(t[r], v);
+                v = fminf(t[r], v);
+                t[r] = hi;
+            }
+        }
+        return uni(t[kRBar - 1]);
+    };
+    float wbest = -INFINITY;  // R > 1: this wave's best exact score (wave-uniform)
 #if SKYRL_TP_BAR_FORM
     // publish the wave's best new score and read the workgroup's when a lane beat the wave's bar,
     // else only read the workgroup's (as the unfiltered sampler's after_eval). s_bar1 stays the
     // best record: an unpublished score is <= bar1 <= s_bar1.
     float bar1 = -INFINITY;
     auto bar_merge = [&](float best_new) {
+        if constexpr (kRBar > 1) {  // every skipped element scores below the bar at its visit,
+                                    // which is at most the final R-th largest wave best
+            if (__builtin_amdgcn_ballot_w64(best_new > wbest) != 0) {
+                wbest = fmaxf(wbest, wave_max_uniform(best_new));
+                if (lane == 0) __hip_atomic_store(&s_wbest[w], wbest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            thr1 = (rbar() - kNoiseC) * temp;
+            return;
+        }
         if (__builtin_amdgcn_ballot_w64(best_new > bar1) != 0) {
             const float wb = wave_max_uniform(best_new);
             if (lane == 0 && wb > -INFINITY)
@@ -1698,6 +1768,15 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         const float bits = noise_bits(h);
         const bool cand = !(fmaf(bits, -kT, vm) - thr1 < 0.f);
         if (__builtin_amdgcn_ballot_w64(cand) == 0) return;
+#ifdef SKYRL_TP_COUNT  // (probe builds: candidate events per row, exact scores per row)
+        if (lane == 0) atomicAdd(&s_cnt[0], 1u);
+        {
+            uint32_t nsc = 0u;
+            for (int k = 0; k < VEC; ++k)
+                nsc += (cand && k < cnt && v0 + k != seed_v && !(fmaf(bits, -kT, x[k]) - thr1 < 0.f)) ? 1u : 0u;
+            if (nsc) atomicAdd(&s_cnt[1], nsc);
+        }
+#endif
         float bn = -INFINITY;
         if (cand) {
             const float Eg = group_min_e(h);
@@ -1782,6 +1861,11 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             record(sc, vb, bb);
             seed_v = vb;
             bar_merge(sc);
+            if constexpr (kRBar > 1) {  // every wave's seed published before the stream: an early
+                                        // visit against an unpublished (-inf) slot scores everything
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                thr1 = (rbar() - kNoiseC) * temp;
+            }
         }
         for (int base = 0; base < nfull; base += kStep) {
             const bool more = base + kStep < nfull;
@@ -1882,6 +1966,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     uint32_t kc = 0u;
     bool split = false;
     long long c = 0;
+    long long cut_cnt = 0;  // the cut key's element count (top_p)
     int ic = 0x7fffffff;
     if constexpr (TOPP) {
         if (!fb) {
@@ -1964,6 +2049,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 const int cb = cut_neg ? cj - kPHalf : kPHalf - 1 - cj;  // window offset of the cut value
                 kc = okey_bf16((uint16_t)((cut_neg ? 0x8000u : 0u) | (uint32_t)((kPE0 << 7) + cb)));
                 const long long cnt = (long long)s_hist[cut_neg ? kPHalf - 1 - cb : kPHalf + cb];
+                cut_cnt = cnt;
                 const unsigned long long qc = mass_q(from_key<T>(kc), mx, inv_t);
                 const unsigned long long A = s_cut_a;
                 // filter_row's rule: c = number of tie ranks j >= 0 with A + j qc < target (the first
@@ -1990,6 +2076,12 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     lse = uni(lse);
     if (!fb) {  // (the fallback's call site stays after the hot loops: the register allocation of
                 // the passes does not see it)
+#ifdef SKYRL_TP_COUNT
+    if (probe == 2 && threadIdx.x == 0) {
+        tokens[row_i] = (int)s_cnt[0];
+        if (logp_out) logp_out[row_i] = (float)s_cnt[1];
+    }
+#endif
     if (probe == 2) return;  // timing probe: pass 1 + the cut
     if (probe == 11) {  // timing probe: per row, the cut's and pass 1's times (10-ns ticks; tokens invalid)
         if (threadIdx.x == 0) {
@@ -2019,10 +2111,14 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         xlo = uni(from_key<T>(hi));
     }
-    // ---- pass 1's decision: the best admissible record e*, certified when it is the best record
-    //      (the final bar) and no unranked element of a split cut key beats it: an element the bound
-    //      skipped scored below the bar, so below e*; otherwise pass 2 decides, starting from e*
+    // ---- pass 1's decision: the best admissible record e*, certified when it reaches the final
+    //      bar (the best record; R > 1: the R-th largest wave best) and no unranked element of a split
+    //      cut key beats it: an element the bound skipped scored below the bar at its visit, so below
+    //      the final bar, so below e*; otherwise pass 2 decides, starting from e*
     Best e0{-INFINITY, 0x7fffffff};
+#ifdef SKYRL_TP_REASON
+    uint32_t why = 16u;
+#endif
     {
         const int nc = (int)min(s_nc, (uint32_t)kPCandCap);
         const bool complete = s_nc <= (uint32_t)kPCandCap;
@@ -2058,7 +2154,101 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
             for (int i = threadIdx.x; i < nc; i += NT) ntie += (better(s_cs[i], s_ci[i], es) && cls(i) == 2) ? 1u : 0u;
         if (ntie) atomicAdd(&s_ntie, ntie);
         __syncthreads();
-        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && s_ntie == 0u && es.score >= s_bar1;
+        const float bar_end = kRBar > 1 ? rbar() : s_bar1;  // (after the barriers above: final)
+        bool ties_ok = s_ntie == 0u;
+#ifdef SKYRL_TP_REASON
+        why |= (complete ? 0u : 1u) | (es.idx == 0x7fffffff ? 2u : 0u) | (s_ntie ? 4u : 0u) | (es.score < bar_end ? 8u : 0u);
+#endif
+#if SKYRL_TP_TIERES
+        // recorded elements of the split cut key that beat e*: kept iff fewer than c elements of that
+        // key precede them (filter_row's index order), so rank them here by a scan of the row prefix
+        // (cached: the row was just read) for the key's indices, instead of leaving the row to pass 2.
+        // The unrecorded ones scored below the bar, so below e*: the decision is the best of e* and the
+        // kept listed records.
+        if (TOPP && split && !ties_ok && s_ntie <= (uint32_t)kPTieRes && probe != 5 && complete &&
+            es.idx != 0x7fffffff && es.score >= bar_end) {
+            if (threadIdx.x == 0) s_trn = 0u;
+            __syncthreads();
+            for (int i = threadIdx.x; i < nc; i += NT)
+                if (cls(i) == 2 && better(s_cs[i], s_ci[i], es)) {
+                    const uint32_t p = atomicAdd(&s_trn, 1u);  // < kPTieRes (s_ntie counted the same set)
+                    s_tri[p] = s_ci[i];
+                    s_trs[p] = s_cs[i];
+                }
+            __syncthreads();
+            const int nr = (int)s_trn;
+            int imin = 0x7fffffff, imax = 0;
+            for (int j = 0; j < nr; ++j) {
+                imin = min(imin, s_tri[j]);
+                imax = max(imax, s_tri[j]);
+            }
+            // the shorter side: the key's indices below imax (rank = those below the record), or
+            // from imin on (rank = the key's count - those at or above the record)
+            const bool suffix = V - imin < imax;
+            const int e0 = suffix ? imin : 0, e1 = suffix ? V : imax;
+            const int vb = min((e0 + VEC - 1) / VEC, nvec), ve = max(vb, min(e1 / VEC, nvec));
+            auto tie_vec = [&](const uint4& pk, int i) {
+                uint16_t raw[VEC];
+                __builtin_memcpy(raw, &pk, 16);
+                uint32_t n = 0u;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) n += bf16_to_f32(raw[k]) == xc ? 1u : 0u;
+                if (n) {
+                    uint32_t p = atomicAdd(&s_nt, n);
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k)
+                        if (bf16_to_f32(raw[k]) == xc) s_tidx[p++] = i * VEC + k;  // (<= the key's count <= kPTieCap)
+                }
+            };
+            constexpr int kScanDepth = 8;  // loads in flight per lane (a lone workgroup: latency-bound)
+            for (int i0 = vb + (int)threadIdx.x; i0 < ve; i0 += kScanDepth * NT) {
+                uint4 pk[kScanDepth];
+#pragma unroll
+                for (int u = 0; u < kScanDepth; ++u) {
+                    const int i = i0 + u * NT;
+                    pk[u] = i < ve ? rv[i] : make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u);
+                }
+#pragma unroll
+                for (int u = 0; u < kScanDepth; ++u) tie_vec(pk[u], i0 + u * NT);
+            }
+            {  // the elements outside whole vectors: [e0, vb VEC) and [ve VEC, e1)
+                const int a1 = min(vb * VEC, e1), b0 = max(max(ve * VEC, a1), e0);
+                for (int i = e0 + (int)threadIdx.x; i < a1; i += NT)
+                    if (to_f<T>(row[i]) == xc) s_tidx[atomicAdd(&s_nt, 1u)] = i;
+                for (int i = b0 + (int)threadIdx.x; i < e1; i += NT)
+                    if (to_f<T>(row[i]) == xc) s_tidx[atomicAdd(&s_nt, 1u)] = i;
+            }
+            __syncthreads();
+            const int n = (int)s_nt;
+            Best tb{-INFINITY, 0x7fffffff};
+            if ((int)threadIdx.x < nr) {
+                const int ii = s_tri[threadIdx.x];
+                long long r = 0;
+                if (suffix) {
+                    for (int j = 0; j < n; ++j) r += s_tidx[j] >= ii ? 1 : 0;
+                    r = cut_cnt - r;
+                } else {
+                    for (int j = 0; j < n; ++j) r += s_tidx[j] < ii ? 1 : 0;
+                }
+                if (r < c) tb = Best{s_trs[threadIdx.x], ii};
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const float os = __shfl_xor(tb.score, off, kWave);
+                const int oi = __shfl_xor(tb.idx, off, kWave);
+                if (better(os, oi, tb)) tb = Best{os, oi};
+            }
+            if (lane == 0) {
+                s_bs[w] = tb.score;
+                s_bi[w] = tb.idx;
+            }
+            __syncthreads();
+            for (int j = 0; j < NW; ++j)
+                if (better(s_bs[j], s_bi[j], es)) es = Best{s_bs[j], s_bi[j]};
+            ties_ok = true;
+        }
+#endif
+        const bool certified = probe != 5 && complete && es.idx != 0x7fffffff && ties_ok && es.score >= bar_end;
         if (certified) {
             if (threadIdx.x == 0) {
                 tokens[row_i] = es.idx;
@@ -2080,7 +2270,11 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 pend[row_i] = ToppPending{xlo, xc, lse, mx, e0.score, e0.idx, split ? 1 : 0, kc, c};
                 pend_nt[2 * row_i] = 0u;      // the row's tie count and its pieces' arrival counter (the
                 pend_nt[2 * row_i + 1] = 0u;  // workspace layout moves with the batch size: not left re-armed)
+#ifdef SKYRL_TP_REASON  // (probe builds: why pass 1 left the row, kept through pass 2)
+                filt[row_i] = RowFilter{mx, why, kRowPending, kc, ic};
+#else
                 filt[row_i] = RowFilter{mx, 0u, kRowPending, kc, ic};
+#endif
             }
             return;
         }
@@ -2638,7 +2832,11 @@ __global__ __launch_bounds__(kPNT) void sample_topp_pass2_kernel(
     if (threadIdx.x == 0) {
         tokens[row_i] = b.idx;
         if (logp_out) logp_out[row_i] = (b.idx >= 0 && b.idx < V) ? to_f<T>(row[b.idx]) - st.lse : __builtin_nanf("");
+#ifdef SKYRL_TP_REASON
+        filt[row_i] = RowFilter{st.mx, filt[row_i].tk, kRowDone, st.kc, icut};
+#else
         filt[row_i] = RowFilter{st.mx, 0u, kRowDone, st.kc, icut};
+#endif
     }
 }
 

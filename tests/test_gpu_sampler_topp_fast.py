@@ -103,6 +103,27 @@ def test_topp_fast_matches_oracle_small_batches(dev):
         torch.testing.assert_close(lp, elp, atol=1e-4, rtol=1e-4)
 
 
+def test_topp_fast_ranks_cut_key_ties_in_pass1(dev):
+    """Rows on a coarse grid (values k/4): the top_p cut splits a tie group of tens to hundreds in
+    most rows, and with the R-th-best race bar (sampler.hip SKYRL_TP_RBAR) pass 1 often records
+    cut-key elements above e*, which it ranks by a scan of the row prefix (SKYRL_TP_TIERES) instead
+    of leaving the row to pass 2: tokens bit-exact and logprobs against oracle/sampler_ref.c over
+    three decode steps, and equal to the two-kernel path's."""
+    from oracle import sampler as osamp
+
+    V, n = 32000, 96
+    g = torch.Generator().manual_seed(17)
+    x = (torch.round(torch.randn(n, V, generator=g) * 12) / 4).to(torch.bfloat16)
+    ids = torch.arange(n, dtype=torch.int64) * 7 + 3
+    for step, (temp, p) in ((1, (1.0, 0.9)), (2, (1.0, 0.95)), (3, (0.6, 0.7))):
+        tok, lp, ff = _run(x.to(dev), True, temperature=temp, top_p=p, seed=9, seq_ids=ids.to(dev), step=step)
+        etok, elp = osamp.sample(x, temp, -1, p, 0.0, 9, ids, step)
+        assert torch.equal(tok, etok), (step, int((tok != etok).sum()))
+        torch.testing.assert_close(lp, elp, atol=1e-4, rtol=1e-4)
+        assert bool(((ff[:, 2] == _ROW_DONE) | (ff[:, 2] == _ROW_FALLBACK)).all())
+        _ab(x.to(dev), 0, temperature=temp, top_p=p, seed=9, seq_ids=ids.to(dev), step=step)
+
+
 def test_topp_fast_split_ties_and_fallback_rows(dev):
     """Rows built to take every branch: few distinct values (a tie group of ~25k at the cut: the
     fallback), rows -inf but for a handful of logits (taken: -inf weighs nothing), all-negative
