@@ -16,13 +16,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(ROOT, "skyrl_amd", "csrc")
-V, T, L = "-DSKYRL_TP_RBAR_VEC=1", "-DSKYRL_TP_TIERES=1", "-DSKYRL_TP_P2LIST=1"
-VARIANTS = {"r1": ["-DSKYRL_TP_RBAR=1"], "r1l": ["-DSKYRL_TP_RBAR=1", L]}
-VARIANTS.update({f"r{r}vt": [f"-DSKYRL_TP_RBAR={r}", V, T] for r in (3,)})
-VARIANTS.update({f"r{r}vtl": [f"-DSKYRL_TP_RBAR={r}", V, T, L] for r in (2, 3)})
-# pass 1 + the cut alone (topp_probe 2 as the build's default: no pass-2 launch, tokens invalid)
-P = "-DSKYRL_TP_PROBE0=2"
-VARIANTS.update({f"r{r}vtp2": [f"-DSKYRL_TP_RBAR={r}", V, T, P] for r in (3,)})
+H, P = "-DSKYRL_TP_HWPRE=1", "-DSKYRL_TP_PROBE0=2"
+# r1: the r05 product (best-record bar, ties left to pass 2) as the exactness reference; r3: the
+# product defaults (3rd largest wave best, vector reads, ties ranked in pass 1); h: the hardware-log
+# prefilter of the kept slots (SKYRL_TP_HWPRE, measured and removed from sampler.hip: no gain); p2: pass 1 + the cut alone (topp_probe 2, tokens invalid)
+VARIANTS = {"r1": ["-DSKYRL_TP_RBAR=1", "-DSKYRL_TP_TIERES=0"], "r3": [], "r3h": [H],
+            "r3h2": ["-DSKYRL_TP_HWPRE=2"], "r3p2": [P], "r3hp2": [H, P], "r3h2p2": ["-DSKYRL_TP_HWPRE=2", P],
+            "r1p2": ["-DSKYRL_TP_RBAR=1", P]}
 FILT = 1024 * 4  # the RowFilter array's offset (sampler.hip kCounterBytes); RowFilter = 5 x 4 B
 
 
