@@ -16,13 +16,12 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(ROOT, "skyrl_amd", "csrc")
-H, P = "-DSKYRL_TP_HWPRE=1", "-DSKYRL_TP_PROBE0=2"
-# r1: the r05 product (best-record bar, ties left to pass 2) as the exactness reference; r3: the
-# product defaults (3rd largest wave best, vector reads, ties ranked in pass 1); h: the hardware-log
-# prefilter of the kept slots (SKYRL_TP_HWPRE, measured and removed from sampler.hip: no gain); p2: pass 1 + the cut alone (topp_probe 2, tokens invalid)
-VARIANTS = {"r1": ["-DSKYRL_TP_RBAR=1", "-DSKYRL_TP_TIERES=0"], "r3": [], "r3h": [H],
-            "r3h2": ["-DSKYRL_TP_HWPRE=2"], "r3p2": [P], "r3hp2": [H, P], "r3h2p2": ["-DSKYRL_TP_HWPRE=2", P],
-            "r1p2": ["-DSKYRL_TP_RBAR=1", P]}
+P, ML = "-DSKYRL_TP_PROBE0=2", "-DSKYRL_MP_LIST=1"
+# r1: the product as built (the exactness reference); ml: min_p alone decided from pass 1's list of
+# the elements within T |ln min_p| of the running max (SKYRL_MP_LIST); p2: pass 1 + the cut alone
+VARIANTS = {"r1": [], "ml": [ML], "r1p2": [P], "mlp2": [ML, P]}
+CASES = {"minp0.05_T1": (1.0, 1.0, 0.05), "minp0.05_T0.6": (0.6, 1.0, 0.05), "minp0.1_T1": (1.0, 1.0, 0.1),
+         "p0.95_minp0.05_T1": (1.0, 0.95, 0.05)}
 FILT = 1024 * 4  # the RowFilter array's offset (sampler.hip kCounterBytes); RowFilter = 5 x 4 B
 
 
@@ -48,9 +47,8 @@ def run():
     ids = torch.arange(N, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev)
     libs = {k: ctypes.CDLL(os.path.join(HERE, f"libtprb_{k}.so")) for k in VARIANTS}
-    cases = {"p0.95_T1": (1.0, 0.95), "p0.95_T0.6": (0.6, 0.95), "p0.9_T1": (1.0, 0.9)}
     out = {}
-    for case, (temp, top_p) in cases.items():
+    for case, (temp, top_p, min_p) in CASES.items():
         ref = {}
         for rnd in range(3):
             for k, lib in libs.items():
@@ -61,7 +59,7 @@ def run():
 
                 def call(t):
                     rc = lib.skyrl_sample(ctypes.c_void_p(logits.data_ptr()), 1, ctypes.c_int64(V), N, V,
-                                          ctypes.c_float(temp), -1, ctypes.c_float(top_p), ctypes.c_float(0.0),
+                                          ctypes.c_float(temp), -1, ctypes.c_float(top_p), ctypes.c_float(min_p),
                                           ctypes.c_uint64(3), ctypes.c_void_p(ids.data_ptr()), ctypes.c_int64(t),
                                           ctypes.c_void_p(tok.data_ptr()), ctypes.c_void_p(lp.data_ptr()),
                                           ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(s.cuda_stream))

@@ -519,6 +519,15 @@ __device__ uint64_t g_sphase[4096 * 8];
 #ifndef SKYRL_TP_TIERES
 #define SKYRL_TP_TIERES 1
 #endif
+// min_p alone (sample_topp_kernel<T, false>): pass 1 lists every element with x/T >= (a lower
+// bound of the row max)/T + ln min_p -- a superset of the kept set -- instead of running the race,
+// and decides the row from the list once the max is known (1, product: every row decided in pass 1
+// against ~32 % with the race; min_p 0.05 at 512 x 151,936: 66.3 -> 50.7 us at T = 1, 60.7 -> 43.4
+// at T = 0.6, min_p 0.1 64.9 -> 45.8; tokens bit-exact; profiles/r06x_minp_list_ab.json); or the
+// race + certificate (0)
+#ifndef SKYRL_MP_LIST
+#define SKYRL_MP_LIST 1
+#endif
 #ifndef SKYRL_TP_RBAR_VEC  // R > 1: the waves' bests read by two 16-B LDS loads (1) or 8 atomic loads (0)
 #define SKYRL_TP_RBAR_VEC 1
 #endif
@@ -1631,7 +1640,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
 #endif
     __shared__ int32_t s_tri[kPTieRes];  // pass 1's cut-key records that beat e* (SKYRL_TP_TIERES)
     __shared__ float s_trs[kPTieRes];
-    __shared__ float s_bar1;
+    __shared__ float s_bar1, s_runmax;
     __shared__ __attribute__((aligned(16))) float s_wbest[NW];  // R > 1: each wave's best exact score
     constexpr int kRBar = TOPP ? SKYRL_TP_RBAR : 1;
     __shared__ float s_bs[NW];
@@ -1661,6 +1670,7 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
 
         s_ntie = 0u;
         s_bar1 = -INFINITY;  // the workgroup's best exact score so far
+        s_runmax = -INFINITY;  // list mode: the largest wave maximum published so far
     }
     if (threadIdx.x < NW) s_wbest[threadIdx.x] = -INFINITY;
     for (int j = threadIdx.x; j < 2 * kPHalf + kWave; j += NT) s_hist[j] = 0u;
@@ -1687,6 +1697,8 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
     const uint32_t key2 = noise_key2(key), keyb = noise_keyb(key);
     const float temp = 1.0f / inv_t;
     const float kT = 0.6931471805599453f * 1.1920928955078125e-7f * temp;
+    constexpr bool kList = !TOPP && SKYRL_MP_LIST;
+    float thr_run = -INFINITY;  // list mode: (a lower bound of the row max) / T + ln min_p, wave-uniform
     float thr1 = -INFINITY;  // (bar - C) T, wave-uniform
     int seed_v = -1;         // this lane's seed element (scored once: no duplicate record)
     auto record = [&](float sc, int v, uint32_t b) {
@@ -1791,6 +1803,27 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         bar_merge(bn);
     };
+    // list mode: the vector's elements that can be kept (x/T >= thr_run) into s_cs (values) / s_ci;
+    // after a vector that listed any, the wave publishes its running max and reads the workgroup's
+    auto collect = [&](const float (&x)[VEC], float vm, int v0, int cnt) {
+        const bool any = !(vm * inv_t < thr_run);
+        if (__builtin_amdgcn_ballot_w64(any) == 0) return;
+        if (any) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (k < cnt && !(x[k] * inv_t < thr_run)) {
+                    const uint32_t p = atomicAdd(&s_nc, 1u);
+                    if (p < (uint32_t)kPCandCap) {
+                        s_cs[p] = x[k];
+                        s_ci[p] = v0 + k;
+                    }
+                }
+            }
+        }
+        const float wm = wave_max_uniform(vmx);
+        if (lane == 0) __hip_atomic_fetch_max(&s_runmax, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        thr_run = fmaxf(wm, uni(s_runmax)) * inv_t + ln_min_p;
+    };
     auto rare_elem = [&](uint32_t b) {  // an element outside the window (top_p)
         const uint32_t a = b & 0x7fffu;
         if (a == 0u) {
@@ -1813,7 +1846,8 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         for (int k = 1; k < VEC; ++k) vm = fmaxf(vm, x[k]);
         vmx = fmaxf(vmx, vm);
 #ifndef SKYRL_TP_NORACE  // (probe builds only: timing attribution, tokens invalid)
-        gumbel(x, raw, vm, v0, VEC);
+        if constexpr (kList) collect(x, vm, v0, VEC);
+        else gumbel(x, raw, vm, v0, VEC);
 #endif
         {
             bool rare = false;
@@ -1840,6 +1874,20 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
     };
     if (nfull > 0) {
+        if constexpr (kList) {  // the first threshold: the maximum of every lane's first 4 vectors
+            float m0 = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                uint16_t raw[VEC];
+                __builtin_memcpy(raw, &cur[u], 16);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) m0 = fmaxf(m0, bf16_to_f32(raw[k]));
+            }
+            m0 = wave_max_uniform(m0);
+            if (lane == 0) __hip_atomic_fetch_max(&s_runmax, m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            thr_run = uni(s_runmax) * inv_t + ln_min_p;
+        } else
         // the wave's first bar: each lane's exact score of the largest element of its first vector
         {
             uint16_t raw[VEC];
@@ -1898,7 +1946,8 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         } else {  // an idle lane joins the ballots with nothing to score
             const uint16_t nb[VEC] = {0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u, 0xff80u};
             const float nx[VEC] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
-            gumbel(nx, nb, -INFINITY, 0, 0);
+            if constexpr (kList) collect(nx, -INFINITY, 0, 0);
+            else gumbel(nx, nb, -INFINITY, 0, 0);
         }
     }
     if (nvec * VEC < V) {  // the ragged tail: one partial group, lanes 0 .. cnt-1 one element each
@@ -1913,7 +1962,8 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         float tm = tx[0];
 #pragma unroll
         for (int k = 1; k < VEC; ++k) tm = fmaxf(tm, tx[k]);
-        gumbel(tx, tb, tm, t0, threadIdx.x == 0 ? cnt : 0);
+        if constexpr (kList) collect(tx, tm, t0, threadIdx.x == 0 ? cnt : 0);
+        else gumbel(tx, tb, tm, t0, threadIdx.x == 0 ? cnt : 0);
     }
     for (int i = nvec * VEC + threadIdx.x; i < V; i += NT) {  // ragged tail, one element per thread
         const uint16_t b = row[i];
@@ -2119,7 +2169,47 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
 #ifdef SKYRL_TP_REASON
     uint32_t why = 16u;
 #endif
-    {
+    if constexpr (kList) {
+        // list mode: every kept element (x >= xlo) is listed when the list did not overflow; their
+        // exact scores decide the row (the max is kept, so the list holds at least one). Overflow:
+        // the in-row pass 2 below, from no bar
+        if (probe != 5 && s_nc <= (uint32_t)kPCandCap) {
+            const int nc = (int)s_nc;
+            Best e{-INFINITY, 0x7fffffff};
+            for (int i = threadIdx.x; i < nc; i += NT) {
+                const float xv = s_cs[i];
+                if (xv >= xlo) {
+                    const int v = s_ci[i];
+                    const uint32_t h = ehash(key, keyb, (uint32_t)v >> 3);
+                    const float sc = noise_score(xv, inv_t, v, h, group_min_e(h), key2);
+                    if (better(sc, v, e)) e = Best{sc, v};
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const float os = __shfl_xor(e.score, off, kWave);
+                const int oi = __shfl_xor(e.idx, off, kWave);
+                if (better(os, oi, e)) e = Best{os, oi};
+            }
+            if (lane == 0) {
+                s_bs[w] = e.score;
+                s_bi[w] = e.idx;
+            }
+            __syncthreads();
+            Best es{s_bs[0], s_bi[0]};
+            for (int j = 1; j < NW; ++j)
+                if (better(s_bs[j], s_bi[j], es)) es = Best{s_bs[j], s_bi[j]};
+            if (es.idx != 0x7fffffff) {  // (block-uniform)
+                if (threadIdx.x == 0) {
+                    tokens[row_i] = es.idx;
+                    if (logp_out) logp_out[row_i] = to_f<T>(row[es.idx]) - lse;
+                    filt[row_i] = RowFilter{mx, 1u, kRowDone, kc, ic};
+                }
+                return;
+            }
+            __syncthreads();  // s_bs reused below
+        }
+    } else {
         const int nc = (int)min(s_nc, (uint32_t)kPCandCap);
         const bool complete = s_nc <= (uint32_t)kPCandCap;
         auto cls = [&](int i) -> int {  // 1 admissible, 0 inadmissible, 2 an element of the split cut key

@@ -124,6 +124,29 @@ def test_topp_fast_ranks_cut_key_ties_in_pass1(dev):
         _ab(x.to(dev), 0, temperature=temp, top_p=p, seed=9, seq_ids=ids.to(dev), step=step)
 
 
+def test_minp_list_mode_overflow_and_ordinary_rows(dev):
+    """min_p alone: pass 1 lists the elements within T |ln min_p| of the running max and decides
+    from the list (sampler.hip SKYRL_MP_LIST). Rows with thousands of elements at the max overflow
+    the list (2048) and take the in-row pass 2; rows whose max comes late in the row list many
+    elements early; ordinary rows: tokens bit-exact and logprobs against oracle/sampler_ref.c."""
+    from oracle import sampler as osamp
+
+    V, n = 32000, 48
+    g = torch.Generator().manual_seed(23)
+    flat = torch.randint(0, 3, (8, V), generator=g).float()                 # a third of the row at the max
+    late = torch.randn(8, V, generator=g) * 2
+    late[:, -64:] += 9.0                                                      # the max in the last vectors
+    ordinary = torch.randn(n - 16, V, generator=g) * 3
+    x = torch.cat([flat, late, ordinary]).to(torch.bfloat16)
+    ids = torch.arange(n, dtype=torch.int64) * 11 + 5
+    for step, (temp, mp) in ((1, (1.0, 0.05)), (2, (0.6, 0.1)), (3, (1.5, 0.3))):
+        tok, lp, ff = _run(x.to(dev), True, temperature=temp, min_p=mp, seed=13, seq_ids=ids.to(dev), step=step)
+        etok, elp = osamp.sample(x, temp, -1, 1.0, mp, 13, ids, step)
+        assert torch.equal(tok, etok), (step, int((tok != etok).sum()))
+        torch.testing.assert_close(lp, elp, atol=1e-4, rtol=1e-4)
+        assert bool((ff[:, 2] == _ROW_DONE).all())
+
+
 def test_topp_fast_split_ties_and_fallback_rows(dev):
     """Rows built to take every branch: few distinct values (a tie group of ~25k at the cut: the
     fallback), rows -inf but for a handful of logits (taken: -inf weighs nothing), all-negative
