@@ -1939,6 +1939,22 @@ __global__ __launch_bounds__(kPNT) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         __builtin_amdgcn_s_setprio(0);
     }
+    if constexpr (kList) {
+        if (nfull == 0) {  // a short row: the first threshold from every lane's first vector
+            float m0 = -INFINITY;
+            if ((int)threadIdx.x < nvec) {
+                const uint4 pk = rv[threadIdx.x];
+                uint16_t raw[VEC];
+                __builtin_memcpy(raw, &pk, 16);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) m0 = fmaxf(m0, bf16_to_f32(raw[k]));
+            }
+            m0 = wave_max_uniform(m0);
+            if (lane == 0) __hip_atomic_fetch_max(&s_runmax, m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            thr_run = uni(s_runmax) * inv_t + ln_min_p;
+        }
+    }
     for (int i0 = nfull; i0 < nvec; i0 += NT) {  // same trip count in every thread (wave ballots inside)
         const int i = i0 + (int)threadIdx.x;
         if (i < nvec) {
